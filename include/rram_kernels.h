@@ -1,0 +1,353 @@
+/*
+ * rram_kernels.h — C-ABI of the MI355X (gfx950) RRAM fault-simulation kernels.
+ *
+ * This is the drop-in device boundary below Caffe's Layer<Dtype>/Solver API
+ * (SURVEY.md §8b).  Every entry point:
+ *   - takes plain pointers (device memory unless stated), sizes and an opaque
+ *     stream handle (`rram_stream_t` == hipStream_t; NULL = default stream);
+ *   - returns an int status (RRAM_OK == 0) and never aborts; the message of
+ *     the last failure on the calling thread is in rram_last_error();
+ *   - is asynchronous on the given stream and allocates nothing (graph-capture
+ *     safe) unless the comment says otherwise.
+ * Each declaration cites the reference interface it replaces
+ * (paths relative to the reference repository fightingnoble/rram-caffe-simulation).
+ */
+#ifndef RRAM_KERNELS_H_
+#define RRAM_KERNELS_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* rram_stream_t; /* hipStream_t */
+
+enum {
+  RRAM_OK = 0,
+  RRAM_EINVAL = -1,      /* bad argument (null pointer, negative size, ...) */
+  RRAM_EHIP = -2,        /* HIP runtime error (launch / memcpy)             */
+  RRAM_ENOMEM = -3,      /* workspace too small / allocation failed          */
+  RRAM_EUNSUPPORTED = -4 /* shape or mode not supported by this build       */
+};
+
+const char* rram_kernels_version(void);
+const char* rram_last_error(void);
+/* hipDeviceSynchronize + error check (host-side convenience). */
+int rram_device_synchronize(void);
+
+/* ------------------------------------------------------------------------
+ * Fault model
+ * ---------------------------------------------------------------------- */
+
+/* Map uniforms in [0,1) to stuck values {-1,0,+1} in place:
+ *   u < split1 -> -1 ; u < split2 -> 0 ; else +1.
+ * Replaces FailureThresholdKernel / failure_threshold<Dtype>
+ * (src/caffe/failure_maker.cu:5-21). */
+int rram_fault_threshold(float* values, int64_t n, float split1, float split2,
+                         rram_stream_t stream);
+
+/* Draw a fresh fault state for one faultable blob with the build's
+ * counter-based RNG (Philox4x32-10, key = seed, counter = (pair index,
+ * map_id, layer_id, purpose)):
+ *   endurance[j] = mean + std * z_j            (fp32, z ~ N(0,1), Box-Muller)
+ *   values[j]    = -1 / 0 / +1 by the integer thresholds thr_neg, thr_zero
+ *                  applied to a 32-bit uniform word r (r < thr_neg -> -1,
+ *                  r < thr_zero -> 0, else +1; thresholds in [0, 2^32]).
+ * Replaces the GaussianFailureMaker constructor's draws
+ * (src/caffe/failure_maker.cpp:5-52: caffe_rng_gaussian + caffe_gpu_rng_uniform
+ * + failure_threshold). */
+int rram_fault_init(float* endurance, float* values, int64_t n, float mean,
+                    float std, uint64_t thr_neg, uint64_t thr_zero,
+                    uint64_t seed, uint32_t map_id, uint32_t layer_id,
+                    rram_stream_t stream);
+
+/* One Fail() step on one blob, reference FailKernel semantics, bit-exact:
+ *   if e <= 0: w = v
+ *   else if !(|dw| < eps): e -= decrement (fp32); if e <= 0: w = v
+ * (reference constants: decrement = 100, eps = 1e-20).
+ * broken_count (device, nullable): += number of cells with e <= 0 after the
+ * step (replaces the host D2H count loop of failure_maker.hpp:37-55).
+ * Replaces FailKernel / Fail_gpu / Fail_cpu (src/caffe/failure_maker.cu:23-58,
+ * src/caffe/failure_maker.cpp:55-81). */
+int rram_fail_apply(const float* dw, float* w, float* endurance,
+                    const float* values, int64_t n, float decrement, float eps,
+                    unsigned long long* broken_count, rram_stream_t stream);
+
+/* Several blobs in one launch (one segment per failure_learnable_params()[i]). */
+typedef struct {
+  const float* dw;
+  float* w;
+  float* endurance;
+  const float* values;
+  int64_t n;
+} rram_fail_seg;
+#define RRAM_MAX_SEGS 32
+int rram_fail_apply_batched(const rram_fail_seg* segs, int nsegs,
+                            float decrement, float eps,
+                            unsigned long long* broken_counts /* [nsegs] */,
+                            rram_stream_t stream);
+
+/* broken_count (device) += #{j : endurance[j] <= 0}. */
+int rram_broken_count(const float* endurance, int64_t n,
+                      unsigned long long* broken_count, rram_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Monte-Carlo fault-map injection (north_star kernel (1)).
+ * The reference expresses one fault map per process run as
+ * "endurance <= 0 at the first Fail()" (SURVEY.md §3.3); a map here is
+ * the same Bernoulli(p_fault) stuck-at draw made on the fly from
+ * (seed, map_id, layer_id, index), so w_out = inject(w_clean) reads 4 B and
+ * writes 4 B per weight.
+ * ---------------------------------------------------------------------- */
+enum {
+  RRAM_CELL_SINGLE = 0, /* one cell per weight; stuck value is a literal weight (reference) */
+  RRAM_CELL_DIFFPAIR = 1 /* w = G+ - G-, two cells per weight (extension)            */
+};
+
+typedef struct {
+  /* fault draw: broken iff r0 < thr_fault (thr in [0, 2^32]; p * 2^32 rounded up) */
+  uint64_t thr_fault;
+  /* single-cell stuck value from r1: -1 iff r1 < thr_neg, 0 iff r1 < thr_zero, else +1 */
+  uint64_t thr_neg;
+  uint64_t thr_zero;
+  /* differential pair: a broken cell sticks at G_max iff r1 < thr_sa1, else at 0 */
+  uint64_t thr_sa1;
+  float stuck_scale;    /* single cell: stuck weight = value * stuck_scale (1 = reference) */
+  float g_max;          /* conductance / weight range used by quantisation and diff-pair   */
+  int32_t quant_levels; /* 0/1 = off; L >= 2 uniform levels (extension)                      */
+  float var_sigma;      /* lognormal device variation sigma, 0 = off (extension)             */
+  int32_t cell_mode;    /* RRAM_CELL_SINGLE / RRAM_CELL_DIFFPAIR                              */
+  int32_t reserved;
+} rram_inject_cfg;
+
+/* w_out[j] = inject(w_clean[j]); counters (device, nullable) += #broken cells. */
+int rram_inject_rng(const float* w_clean, float* w_out, int64_t n,
+                    const rram_inject_cfg* cfg, uint64_t seed, uint32_t map_id,
+                    uint32_t layer_id, unsigned long long* counters,
+                    rram_stream_t stream);
+
+typedef struct {
+  const float* w_clean;
+  float* w_out;
+  int64_t n;
+  uint32_t layer_id;
+  uint32_t reserved;
+  rram_inject_cfg cfg;
+} rram_inject_seg;
+/* All faultable blobs of a net in one launch; counters[i] for segment i. */
+int rram_inject_rng_batched(const rram_inject_seg* segs, int nsegs,
+                            uint64_t seed, uint32_t map_id,
+                            unsigned long long* counters, rram_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Strategy / solver elementwise
+ * ---------------------------------------------------------------------- */
+
+/* dw[j] = 0 where |dw[j]| <= thr.  Replaces ThresholdFailureStrategy::Apply's
+ * inner loop (src/caffe/strategy.cpp:7-33); thr = threshold * lr * lr_mult.
+ * cleared (device, nullable) += #cleared. */
+int rram_threshold_strategy(float* dw, int64_t n, float thr,
+                            unsigned long long* cleared, rram_stream_t stream);
+
+/* g = h = momentum * h + local_rate * g.  Replaces SGDUpdate
+ * (src/caffe/solvers/sgd_solver.cu:6-20). */
+int rram_sgd_update(float* g, float* h, int64_t n, float momentum,
+                    float local_rate, rram_stream_t stream);
+
+/* Fused training tail for one blob: L2 decay, momentum
+ * update, threshold strategy, w -= dw, then Fail():
+ *   g += decay * w; g = h = mom*h + lr*g; if (|g| <= thr) g = 0; w -= g;
+ *   FailKernel(e, v, w, g).
+ * endurance/values may be NULL for a non-faultable blob (thr ignored then
+ * unless apply_thr != 0). */
+int rram_fused_update_fail(float* w, float* g, float* h, float* endurance,
+                           const float* values, int64_t n, float decay,
+                           float momentum, float local_rate, int apply_thr,
+                           float thr, float decrement, float eps,
+                           unsigned long long* broken_count,
+                           rram_stream_t stream);
+
+/* Level-1 helpers used by Blob::Update, Regularize, P2PSync-equivalent
+ * scaling (src/caffe/util/math_functions.cu:45-207). */
+int rram_axpy(int64_t n, float alpha, const float* x, float* y, rram_stream_t stream);
+int rram_axpby(int64_t n, float alpha, const float* x, float beta, float* y, rram_stream_t stream);
+int rram_scal(int64_t n, float alpha, float* x, rram_stream_t stream);
+int rram_set(int64_t n, float alpha, float* x, rram_stream_t stream);
+int rram_add(int64_t n, const float* a, const float* b, float* y, rram_stream_t stream);
+int rram_sign(int64_t n, const float* x, float* y, rram_stream_t stream);
+/* out[0] = sum(|x|) (device scalar). */
+int rram_asum(int64_t n, const float* x, float* out, rram_stream_t stream);
+/* out[0] = max(|x|) (device scalar). */
+int rram_absmax(int64_t n, const float* x, float* out, rram_stream_t stream);
+/* out[0] = sum(x*y) (device scalar). */
+int rram_dot(int64_t n, const float* x, const float* y, float* out, rram_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Dense GEMM on fp32 MFMA
+ * Caffe row-major semantics: C = alpha * op(A) * op(B) + beta * C with
+ * op(A) M x K, op(B) K x N, lda = TransA ? M : K, ldb = TransB ? K : N,
+ * ldc = N.  Replaces caffe_gpu_gemm (src/caffe/util/math_functions.cu:13-27).
+ * trans flags: 0 = CblasNoTrans, 1 = CblasTrans.
+ * ---------------------------------------------------------------------- */
+int rram_gemm_f32(int trans_a, int trans_b, int M, int N, int K, float alpha,
+                  const float* A, const float* B, float beta, float* C,
+                  rram_stream_t stream);
+
+enum { RRAM_BIAS_NONE = 0, RRAM_BIAS_ROW = 1, RRAM_BIAS_COL = 2 };
+/* Extended form: explicit leading dimensions, fused epilogue
+ *   C = act(alpha * op(A) op(B) + beta * C + bias)
+ * bias_mode ROW adds bias[m], COL adds bias[n]; relu != 0 clamps at 0.
+ * workspace (device, nullable) enables split-K for small-M x N grids; with
+ * workspace == NULL or too small the kernel runs without split-K. */
+int rram_gemm_f32_ex(int trans_a, int trans_b, int M, int N, int K,
+                     float alpha, const float* A, int lda, const float* B,
+                     int ldb, float beta, float* C, int ldc, const float* bias,
+                     int bias_mode, int relu, void* workspace,
+                     size_t workspace_bytes, rram_stream_t stream);
+
+/* y[M] = alpha * op(A) x + beta * y.  Replaces caffe_gpu_gemv
+ * (src/caffe/util/math_functions.cu:45-53). */
+int rram_gemv_f32(int trans_a, int M, int N, float alpha, const float* A,
+                  const float* x, float beta, float* y, rram_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Convolution
+ * NCHW fp32.  Forward is an implicit GEMM over the whole batch
+ * (M = Cout/g, N = num*Ho*Wo, K = Cin/g*kh*kw) on fp32 MFMA with im2col fused
+ * into the LDS fill, replacing the reference's per-image im2col +
+ * caffe_gpu_gemm loop (src/caffe/layers/conv_layer.cu:7-24,
+ * src/caffe/layers/base_conv_layer.cpp:325-350).
+ * ---------------------------------------------------------------------- */
+typedef struct {
+  int num, channels, height, width;  /* input  N, C, H, W            */
+  int num_output;                    /* Cout                          */
+  int kernel_h, kernel_w;
+  int pad_h, pad_w;
+  int stride_h, stride_w;
+  int dilation_h, dilation_w;
+  int group;
+  int out_h, out_w;                  /* filled by rram_conv_out_shape */
+} rram_conv_desc;
+
+/* Computes out_h/out_w with Caffe's rule (base_conv_layer.cpp:18-28 via
+ * conv_layer.cpp:9-19) and validates the descriptor. */
+int rram_conv_out_shape(rram_conv_desc* d);
+
+/* y = conv(x, w) + bias (bias nullable), optional fused ReLU. */
+int rram_conv2d_fwd(const rram_conv_desc* d, const float* x, const float* w,
+                    const float* bias, float* y, int relu, rram_stream_t stream);
+
+/* Bytes of device workspace the backward passes need for `images_per_chunk`
+ * images (explicit im2col/col2im buffer). */
+size_t rram_conv2d_bwd_workspace(const rram_conv_desc* d, int images_per_chunk);
+
+/* dw += conv weight gradient, db += bias gradient (db nullable);
+ * dx = data gradient (dx nullable).  Workspace from rram_conv2d_bwd_workspace.
+ * Replaces ConvolutionLayer::Backward_gpu (src/caffe/layers/conv_layer.cu:27-56). */
+int rram_conv2d_bwd(const rram_conv_desc* d, const float* x, const float* w,
+                    const float* dy, float* dw, float* db, float* dx,
+                    void* workspace, size_t workspace_bytes,
+                    rram_stream_t stream);
+
+/* Replaces im2col_gpu / col2im_gpu (src/caffe/util/im2col.cu:41-62,
+ * :300-320).  One image; col is [C*kh*kw][Ho*Wo]. col2im writes (not adds) im. */
+int rram_im2col(const float* im, int channels, int height, int width,
+                int kernel_h, int kernel_w, int pad_h, int pad_w, int stride_h,
+                int stride_w, int dilation_h, int dilation_w, float* col,
+                rram_stream_t stream);
+int rram_col2im(const float* col, int channels, int height, int width,
+                int kernel_h, int kernel_w, int pad_h, int pad_w, int stride_h,
+                int stride_w, int dilation_h, int dilation_w, float* im,
+                rram_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * InnerProduct
+ * top[M,N] = bottom[M,K] * W^T (+ bias), W is [N,K] (transpose=0) or [K,N]
+ * (transpose=1).  Replaces InnerProductLayer::Forward_gpu/Backward_gpu
+ * (src/caffe/layers/inner_product_layer.cu:9-75).
+ * ---------------------------------------------------------------------- */
+int rram_ip_fwd(const float* x, const float* w, const float* bias, float* y,
+                int M, int N, int K, int transpose, int relu, void* workspace,
+                size_t workspace_bytes, rram_stream_t stream);
+/* dw += ..., db += ... (nullable), dx = ... (nullable). */
+int rram_ip_bwd(const float* x, const float* w, const float* dy, float* dw,
+                float* db, float* dx, int M, int N, int K, int transpose,
+                rram_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Support layers needed to run the configs end to end (not fault path).
+ * ---------------------------------------------------------------------- */
+/* ReLU with Caffe's negative_slope (src/caffe/layers/relu_layer.cu). */
+int rram_relu_fwd(const float* x, float* y, int64_t n, float slope, rram_stream_t s);
+int rram_relu_bwd(const float* x, const float* dy, float* dx, int64_t n, float slope, rram_stream_t s);
+
+enum { RRAM_POOL_MAX = 0, RRAM_POOL_AVE = 1 };
+/* Pooling with Caffe's ceil output rule (pooling_layer.cpp:90-104);
+ * mask (int32, nullable) records argmax for MAX. */
+int rram_pool_fwd(const float* x, float* y, int* mask, int num, int channels,
+                  int height, int width, int pooled_h, int pooled_w,
+                  int kernel_h, int kernel_w, int stride_h, int stride_w,
+                  int pad_h, int pad_w, int method, rram_stream_t s);
+int rram_pool_bwd(const float* dy, const int* mask, float* dx, int num,
+                  int channels, int height, int width, int pooled_h,
+                  int pooled_w, int kernel_h, int kernel_w, int stride_h,
+                  int stride_w, int pad_h, int pad_w, int method, rram_stream_t s);
+
+/* LRN ACROSS_CHANNELS (lrn_layer.cu): scale = k + alpha/size * sum x^2,
+ * y = x * scale^-beta.  scale (nullable) keeps the scale for backward. */
+int rram_lrn_fwd(const float* x, float* y, float* scale, int num, int channels,
+                 int height, int width, int size, float alpha, float beta,
+                 float k, rram_stream_t s);
+int rram_lrn_bwd(const float* x, const float* y, const float* scale,
+                 const float* dy, float* dx, int num, int channels, int height,
+                 int width, int size, float alpha, float beta, rram_stream_t s);
+
+/* Softmax over `channels` for [outer][channels][inner]. */
+int rram_softmax_fwd(const float* x, float* y, int outer, int channels, int inner, rram_stream_t s);
+/* SoftmaxWithLoss forward: loss_out[0] = -sum log(max(p[label], FLT_MIN)) / normalizer
+ * where normalizer = #valid (ignore_label < 0 disables ignoring). */
+int rram_softmax_loss_fwd(const float* prob, const float* label, float* loss_out,
+                          int outer, int channels, int inner, int ignore_label,
+                          rram_stream_t s);
+int rram_softmax_loss_bwd(const float* prob, const float* label, float* dx,
+                          int outer, int channels, int inner, int ignore_label,
+                          float loss_weight, rram_stream_t s);
+/* Top-k accuracy (accuracy_layer.cpp:48-90): correct_out[0] = #correct,
+ * count_out[0] = #counted (device floats). */
+int rram_accuracy(const float* x, const float* label, float* correct_out,
+                  float* count_out, int outer, int channels, int inner,
+                  int top_k, int ignore_label, rram_stream_t s);
+/* Concat along axis 1 (copy one bottom into its slot). */
+int rram_concat_copy(const float* src, float* dst, int num, int src_channels_x_inner,
+                     int dst_channels_x_inner, int offset_x_inner, int backward,
+                     rram_stream_t s);
+/* Dropout train mode: mask from Philox(seed, layer, index); y = x*scale or 0. */
+int rram_dropout_fwd(const float* x, float* y, unsigned int* mask, int64_t n,
+                     float ratio, uint64_t seed, uint32_t layer_id, uint64_t iter,
+                     rram_stream_t s);
+int rram_dropout_bwd(const float* dy, const unsigned int* mask, float* dx,
+                     int64_t n, float ratio, rram_stream_t s);
+/* y[n][c][hw] += bias[c] */
+int rram_bias_add(float* y, const float* bias, int num, int channels, int inner, rram_stream_t s);
+/* db[c] += sum_{n,hw} dy[n][c][hw] */
+int rram_bias_bwd(const float* dy, float* db, int num, int channels, int inner, rram_stream_t s);
+
+/* ------------------------------------------------------------------------
+ * Fillers / synthetic data (Philox; seeded; statistically equivalent to the
+ * reference's boost/cuRAND fillers, not bit-identical).
+ * ---------------------------------------------------------------------- */
+int rram_fill_uniform(float* x, int64_t n, float lo, float hi, uint64_t seed,
+                      uint32_t stream_id, rram_stream_t s);
+int rram_fill_gaussian(float* x, int64_t n, float mean, float std,
+                       uint64_t seed, uint32_t stream_id, rram_stream_t s);
+/* x = floor(U[0, levels)) + offset (integer-valued synthetic images / labels). */
+int rram_fill_uniform_int(float* x, int64_t n, int levels, float offset,
+                          uint64_t seed, uint32_t stream_id, rram_stream_t s);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RRAM_KERNELS_H_ */

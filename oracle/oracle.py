@@ -1,0 +1,282 @@
+"""Python face of the CPU oracle — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module, and only as the checker / CPU baseline; the product
+(rram-caffe-simulation_amd/) never does.
+
+Two layers:
+  * ctypes binding of oracle.c (the fault arithmetic, Philox, GEMM, im2col,
+    conv — exact C restatements of the reference, see file header there);
+  * numpy restatements of the reference's CPU layer code for the support
+    layers and a Caffe-CPU-mode network forward (per-image im2col + sgemm via
+    numpy's OpenBLAS) used as the CPU baseline.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+SO = HERE / "_build" / "liboracle.so"
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not SO.exists():
+            build()
+        L = C.CDLL(str(SO))
+        P, I, I64, U32, U64, F = C.c_void_p, C.c_int, C.c_int64, C.c_uint32, C.c_uint64, C.c_float
+        L.oracle_philox.argtypes = [P, P, P]
+        L.oracle_fault_threshold.argtypes = [P, I64, F, F]
+        L.oracle_fault_init.argtypes = [P, P, I64, F, F, U64, U64, U64, U32, U32]
+        L.oracle_fail_apply.argtypes = [P, P, P, P, I64, F, F]
+        L.oracle_fail_apply.restype = I64
+        L.oracle_inject.argtypes = [P, P, I64, P, U64, U32, U32]
+        L.oracle_inject.restype = I64
+        L.oracle_threshold.argtypes = [P, I64, F]
+        L.oracle_threshold.restype = I64
+        L.oracle_sgd_update.argtypes = [P, P, I64, F, F]
+        L.oracle_fused_update_fail.argtypes = [P, P, P, P, P, I64, F, F, F, I, F, F, F]
+        L.oracle_fused_update_fail.restype = I64
+        L.oracle_gemm.argtypes = [I, I, I, I, I, F, P, P, F, P]
+        L.oracle_im2col.argtypes = [P] + [I] * 11 + [P]
+        L.oracle_col2im.argtypes = [P] + [I] * 11 + [P]
+        L.oracle_conv.argtypes = [P, I, I, I, I, P, P] + [I] * 10 + [P]
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray):
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def f32(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+class InjectCfg(C.Structure):  # == rram_inject_cfg
+    _fields_ = [
+        ("thr_fault", C.c_uint64), ("thr_neg", C.c_uint64), ("thr_zero", C.c_uint64),
+        ("thr_sa1", C.c_uint64), ("stuck_scale", C.c_float), ("g_max", C.c_float),
+        ("quant_levels", C.c_int32), ("var_sigma", C.c_float), ("cell_mode", C.c_int32),
+        ("reserved", C.c_int32),
+    ]
+
+
+# --------------------------------------------------------------- fault model
+def philox(ctr, key):
+    c = (C.c_uint32 * 4)(*ctr)
+    k = (C.c_uint32 * 2)(*key)
+    o = (C.c_uint32 * 4)()
+    lib().oracle_philox(c, k, o)
+    return list(o)
+
+
+def fault_threshold(u, split1, split2):
+    v = f32(u).copy()
+    lib().oracle_fault_threshold(_ptr(v), v.size, split1, split2)
+    return v
+
+
+def fault_init(n, mean, std, thr_neg, thr_zero, seed, map_id=0, layer_id=0):
+    e = np.empty(n, np.float32)
+    v = np.empty(n, np.float32)
+    lib().oracle_fault_init(_ptr(e), _ptr(v), n, mean, std, thr_neg, thr_zero, seed, map_id,
+                            layer_id)
+    return e, v
+
+
+def fail_apply(dw, w, e, v, decrement=100.0, eps=1e-20):
+    """Returns (w', e', broken_count); inputs are not modified."""
+    dw, v = f32(dw), f32(v)
+    w, e = f32(w).copy(), f32(e).copy()
+    nb = lib().oracle_fail_apply(_ptr(dw), _ptr(w), _ptr(e), _ptr(v), w.size, decrement, eps)
+    return w, e, nb
+
+
+def inject(src, cfg: InjectCfg, seed, map_id, layer_id):
+    src = f32(src)
+    dst = np.empty_like(src)
+    nb = lib().oracle_inject(_ptr(src), _ptr(dst), src.size, C.byref(cfg), seed, map_id, layer_id)
+    return dst, nb
+
+
+def threshold(dw, thr):
+    d = f32(dw).copy()
+    n = lib().oracle_threshold(_ptr(d), d.size, thr)
+    return d, n
+
+
+def sgd_update(g, h, momentum, lr):
+    g, h = f32(g).copy(), f32(h).copy()
+    lib().oracle_sgd_update(_ptr(g), _ptr(h), g.size, momentum, lr)
+    return g, h
+
+
+def fused_update_fail(w, g, h, e, v, decay, mom, lr, apply_thr, thr, dec=100.0, eps=1e-20):
+    w, g, h = f32(w).copy(), f32(g).copy(), f32(h).copy()
+    if e is not None:
+        e, v = f32(e).copy(), f32(v)
+        ep, vp = _ptr(e), _ptr(v)
+    else:
+        ep = vp = None
+    nb = lib().oracle_fused_update_fail(_ptr(w), _ptr(g), _ptr(h), ep, vp, w.size, decay, mom, lr,
+                                        int(apply_thr), thr, dec, eps)
+    return w, g, h, e, nb
+
+
+# ------------------------------------------------------------------ GEMM/conv
+def gemm(ta, tb, M, N, K, alpha, A, B, beta=0.0, Cm=None):
+    A, B = f32(A), f32(B)
+    out = np.zeros(M * N, np.float32) if Cm is None else f32(Cm).copy().reshape(-1)
+    lib().oracle_gemm(int(ta), int(tb), M, N, K, alpha, _ptr(A), _ptr(B), beta, _ptr(out))
+    return out.reshape(M, N)
+
+
+def out_size(h, k, p, s, d=1):
+    return (h + 2 * p - (d * (k - 1) + 1)) // s + 1
+
+
+def im2col(im, kh, kw, ph, pw, sh, sw, dh=1, dw=1):
+    im = f32(im)
+    Cc, H, W = im.shape
+    Ho, Wo = out_size(H, kh, ph, sh, dh), out_size(W, kw, pw, sw, dw)
+    col = np.empty((Cc * kh * kw, Ho * Wo), np.float32)
+    lib().oracle_im2col(_ptr(im), Cc, H, W, kh, kw, ph, pw, sh, sw, dh, dw, _ptr(col))
+    return col
+
+
+def col2im(col, Cc, H, W, kh, kw, ph, pw, sh, sw, dh=1, dw=1):
+    col = f32(col)
+    im = np.empty((Cc, H, W), np.float32)
+    lib().oracle_col2im(_ptr(col), Cc, H, W, kh, kw, ph, pw, sh, sw, dh, dw, _ptr(im))
+    return im
+
+
+def conv_naive(x, w, b, stride=1, pad=0, dilation=1, group=1):
+    """caffe_conv restatement (test_convolution_layer.cpp:21-139)."""
+    x, w = f32(x), f32(w)
+    N, Cc, H, W = x.shape
+    Cout, _, kh, kw = w.shape
+    Ho, Wo = out_size(H, kh, pad, stride, dilation), out_size(W, kw, pad, stride, dilation)
+    out = np.zeros((N, Cout, Ho, Wo), np.float32)
+    bp = _ptr(f32(b)) if b is not None else None
+    lib().oracle_conv(_ptr(x), N, Cc, H, W, _ptr(w), bp, Cout, kh, kw, pad, pad, stride, stride,
+                      dilation, dilation, group, _ptr(out))
+    return out
+
+
+# ------------------------------------------------- numpy layer restatements
+def conv_im2col(x, w, b, stride=1, pad=0, dilation=1, group=1):
+    """Caffe CPU-mode convolution: per image im2col_cpu + one sgemm per group
+    (base_conv_layer.cpp:256-290, conv_layer.cpp:7-24) on numpy/OpenBLAS."""
+    x, w = f32(x), f32(w)
+    N, Cc, H, W = x.shape
+    Cout, cg, kh, kw = w.shape
+    Ho, Wo = out_size(H, kh, pad, stride, dilation), out_size(W, kw, pad, stride, dilation)
+    out = np.empty((N, Cout, Ho * Wo), np.float32)
+    og = Cout // group
+    wm = w.reshape(group, og, cg * kh * kw)
+    for n in range(N):
+        col = im2col_np(x[n], kh, kw, pad, pad, stride, stride, dilation, dilation)
+        col = col.reshape(group, cg * kh * kw, Ho * Wo)
+        for g in range(group):
+            out[n, g * og:(g + 1) * og] = wm[g] @ col[g]
+    if b is not None:
+        out += f32(b)[None, :, None]
+    return out.reshape(N, Cout, Ho, Wo)
+
+
+def im2col_np(im, kh, kw, ph, pw, sh, sw, dh=1, dw=1):
+    """Vectorised numpy im2col with the same [C*kh*kw][Ho*Wo] layout (im2col.cpp:18-55)."""
+    Cc, H, W = im.shape
+    Ho, Wo = out_size(H, kh, ph, sh, dh), out_size(W, kw, pw, sw, dw)
+    p = np.zeros((Cc, H + 2 * ph, W + 2 * pw), np.float32)
+    p[:, ph:ph + H, pw:pw + W] = im
+    cols = np.empty((Cc, kh, kw, Ho, Wo), np.float32)
+    for a in range(kh):
+        for b in range(kw):
+            cols[:, a, b] = p[:, a * dh:a * dh + sh * (Ho - 1) + 1:sh,
+                              b * dw:b * dw + sw * (Wo - 1) + 1:sw]
+    return cols.reshape(Cc * kh * kw, Ho * Wo)
+
+
+def pool_out(h, k, p, s):
+    """pooling_layer.cpp:90-104 (ceil rule + clip when padded)."""
+    o = int(math.ceil((h + 2 * p - k) / s)) + 1
+    if p and (o - 1) * s >= h + p:
+        o -= 1
+    return o
+
+
+def pool(x, k, s, p=0, method="MAX"):
+    x = f32(x)
+    N, Cc, H, W = x.shape
+    PH, PW = pool_out(H, k, p, s), pool_out(W, k, p, s)
+    out = np.empty((N, Cc, PH, PW), np.float32)
+    for a in range(PH):
+        for b in range(PW):
+            hs, ws = a * s - p, b * s - p
+            if method == "MAX":
+                he, we = min(hs + k, H), min(ws + k, W)
+                hs, ws = max(hs, 0), max(ws, 0)
+                out[:, :, a, b] = x[:, :, hs:he, ws:we].max(axis=(2, 3))
+            else:
+                he, we = min(hs + k, H + p), min(ws + k, W + p)
+                size = (he - hs) * (we - ws)
+                hs, ws, he, we = max(hs, 0), max(ws, 0), min(he, H), min(we, W)
+                out[:, :, a, b] = x[:, :, hs:he, ws:we].sum(axis=(2, 3)) / size
+    return out
+
+
+def lrn(x, size, alpha, beta, k=1.0):
+    """lrn_layer.cpp CrossChannelForward_cpu: scale = k + alpha/size * sum x^2."""
+    x = f32(x)
+    N, Cc, H, W = x.shape
+    pre = (size - 1) // 2
+    sq = np.zeros((N, Cc + size - 1, H, W), np.float32)
+    sq[:, pre:pre + Cc] = x * x
+    scale = np.full(x.shape, k, np.float32)
+    for c in range(Cc):
+        scale[:, c] += (alpha / size) * sq[:, c:c + size].sum(axis=1)
+    return x * np.power(scale, -beta)
+
+
+def relu(x, slope=0.0):
+    x = f32(x)
+    return np.where(x > 0, x, x * slope).astype(np.float32)
+
+
+def softmax(x):
+    x = f32(x)
+    m = x.max(axis=1, keepdims=True)
+    e = np.exp(x - m)
+    return e / e.sum(axis=1, keepdims=True)
+
+
+def accuracy(x, label, top_k=1):
+    """accuracy_layer.cpp:48-90: (value, index) pairs, descending, top_k."""
+    x = f32(x).reshape(len(label), -1)
+    correct = 0
+    for i, lv in enumerate(np.asarray(label, dtype=np.int64)):
+        v = x[i, lv]
+        rank = int(np.sum((x[i] > v) | ((x[i] == v) & (np.arange(x.shape[1]) > lv))))
+        correct += rank < top_k
+    return correct
+
+
+def softmax_loss(prob, label):
+    p = prob[np.arange(len(label)), np.asarray(label, np.int64)]
+    return float(-np.log(np.maximum(p, np.finfo(np.float32).tiny)).sum() / len(label))

@@ -1,0 +1,244 @@
+// C-ABI entry points for GEMM / GEMV / convolution / InnerProduct.
+// The heavy lifting is in gemm.hip (MFMA core) — this file validates
+// arguments, computes Caffe's shape rules and sequences the backward passes.
+#include "rram_common.hpp"
+
+namespace rram {
+int gemm_core(int trans_a, int trans_b, int M, int N, int K, float alpha, const float* A, int lda,
+              const float* B, int ldb, float beta, float* C, int ldc, const float* bias,
+              int bias_mode, int relu, void* ws, size_t ws_bytes, hipStream_t s);
+int conv_fwd_core(const rram_conv_desc* d, const float* x, const float* w, const float* bias,
+                  float* y, int relu, hipStream_t s);
+int conv_bwd_weight_core(const rram_conv_desc* d, int nimg, const float* dy, const float* col,
+                         int64_t ldcol, float* dw, hipStream_t s);
+int conv_bwd_data_col_core(const rram_conv_desc* d, int nimg, const float* w, const float* dy,
+                           float* col, int64_t ldcol, hipStream_t s);
+int im2col_core(const float* im, int64_t im_img, int nimg, const rram_conv_desc* d, float* col,
+                int64_t ldcol, hipStream_t s);
+int col2im_core(const float* col, int64_t ldcol, int nimg, const rram_conv_desc* d, float* im,
+                int64_t im_img, int accumulate, hipStream_t s);
+int gemv_core(int trans, int M, int N, float alpha, const float* A, const float* x, float beta,
+              float* y, hipStream_t s);
+
+namespace {
+
+__global__ void __launch_bounds__(256) k_bias_add(float* __restrict__ y, const float* __restrict__ b,
+                                                  int num, int C, int inner) {
+  const int64_t total = (int64_t)num * C * inner;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = static_cast<int>((i / inner) % C);
+    y[i] += b[c];
+  }
+}
+
+// db[c] += sum over (n, inner) of dy; one block per channel, deterministic.
+__global__ void __launch_bounds__(256) k_bias_bwd(const float* __restrict__ dy, float* __restrict__ db,
+                                                  int num, int C, int inner) {
+  __shared__ float part[4];
+  const int c = blockIdx.x;
+  float s = 0.0f;
+  const int64_t per = (int64_t)num * inner;
+  for (int64_t j = threadIdx.x; j < per; j += blockDim.x) {
+    const int64_t n = j / inner, q = j - n * inner;
+    s += dy[(n * C + c) * inner + q];
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) db[c] += part[0] + part[1] + part[2] + part[3];
+}
+
+int check_desc(const rram_conv_desc* d) {
+  RRAM_REQUIRE(d != nullptr, "conv: desc is NULL");
+  RRAM_REQUIRE(d->num >= 0 && d->channels > 0 && d->height > 0 && d->width > 0 &&
+                   d->num_output > 0,
+               "conv: bad input/output sizes");
+  RRAM_REQUIRE(d->kernel_h > 0 && d->kernel_w > 0 && d->stride_h > 0 && d->stride_w > 0 &&
+                   d->dilation_h > 0 && d->dilation_w > 0 && d->pad_h >= 0 && d->pad_w >= 0,
+               "conv: bad kernel/stride/pad/dilation");
+  RRAM_REQUIRE(d->group > 0 && d->channels % d->group == 0 && d->num_output % d->group == 0,
+               "conv: channels and num_output must be divisible by group");
+  return RRAM_OK;
+}
+
+}  // namespace
+}  // namespace rram
+
+using namespace rram;
+
+extern "C" {
+
+int rram_gemm_f32_ex(int trans_a, int trans_b, int M, int N, int K, float alpha, const float* A,
+                     int lda, const float* B, int ldb, float beta, float* C, int ldc,
+                     const float* bias, int bias_mode, int relu, void* ws, size_t ws_bytes,
+                     rram_stream_t s) {
+  RRAM_REQUIRE(bias_mode >= RRAM_BIAS_NONE && bias_mode <= RRAM_BIAS_COL, "gemm: bad bias_mode");
+  return gemm_core(trans_a != 0, trans_b != 0, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, bias,
+                   bias_mode, relu, ws, ws_bytes, as_stream(s));
+}
+
+int rram_gemm_f32(int trans_a, int trans_b, int M, int N, int K, float alpha, const float* A,
+                  const float* B, float beta, float* C, rram_stream_t s) {
+  const int lda = trans_a ? M : K;
+  const int ldb = trans_b ? K : N;
+  return gemm_core(trans_a != 0, trans_b != 0, M, N, K, alpha, A, lda, B, ldb, beta, C, N, nullptr,
+                   RRAM_BIAS_NONE, 0, nullptr, 0, as_stream(s));
+}
+
+int rram_gemv_f32(int trans_a, int M, int N, float alpha, const float* A, const float* x,
+                  float beta, float* y, rram_stream_t s) {
+  return gemv_core(trans_a != 0, M, N, alpha, A, x, beta, y, as_stream(s));
+}
+
+int rram_conv_out_shape(rram_conv_desc* d) {
+  const int rc = check_desc(d);
+  if (rc) return rc;
+  const int ekh = d->dilation_h * (d->kernel_h - 1) + 1;
+  const int ekw = d->dilation_w * (d->kernel_w - 1) + 1;
+  RRAM_REQUIRE(d->height + 2 * d->pad_h >= ekh && d->width + 2 * d->pad_w >= ekw,
+               "conv: kernel larger than padded input");
+  d->out_h = (d->height + 2 * d->pad_h - ekh) / d->stride_h + 1;
+  d->out_w = (d->width + 2 * d->pad_w - ekw) / d->stride_w + 1;
+  return RRAM_OK;
+}
+
+int rram_conv2d_fwd(const rram_conv_desc* d_in, const float* x, const float* w, const float* bias,
+                    float* y, int relu, rram_stream_t s) {
+  rram_conv_desc d = *d_in;
+  int rc = rram_conv_out_shape(&d);
+  if (rc) return rc;
+  if (d.num == 0) return RRAM_OK;
+  RRAM_REQUIRE(x && w && y, "conv2d_fwd: NULL pointer");
+  RRAM_REQUIRE((int64_t)d.num * d.out_h * d.out_w < (1ll << 31), "conv2d_fwd: too many output positions");
+  return conv_fwd_core(&d, x, w, bias, y, relu, as_stream(s));
+}
+
+size_t rram_conv2d_bwd_workspace(const rram_conv_desc* d_in, int images_per_chunk) {
+  rram_conv_desc d = *d_in;
+  if (rram_conv_out_shape(&d) != RRAM_OK || images_per_chunk < 1) return 0;
+  return (size_t)d.channels * d.kernel_h * d.kernel_w * (size_t)images_per_chunk * d.out_h *
+         d.out_w * sizeof(float);
+}
+
+int rram_conv2d_bwd(const rram_conv_desc* d_in, const float* x, const float* w, const float* dy,
+                    float* dw, float* db, float* dx, void* ws, size_t ws_bytes, rram_stream_t st) {
+  rram_conv_desc d = *d_in;
+  int rc = rram_conv_out_shape(&d);
+  if (rc) return rc;
+  if (d.num == 0) return RRAM_OK;
+  RRAM_REQUIRE(dy != nullptr, "conv2d_bwd: dy is NULL");
+  hipStream_t s = as_stream(st);
+  const int HoWo = d.out_h * d.out_w;
+  if (db) {
+    hipLaunchKernelGGL(k_bias_bwd, dim3(d.num_output), dim3(256), 0, s, dy, db, d.num,
+                       d.num_output, HoWo);
+    rc = launch_status("conv bias bwd");
+    if (rc) return rc;
+  }
+  if (!dw && !dx) return RRAM_OK;
+  RRAM_REQUIRE(x && w, "conv2d_bwd: x/w NULL");
+  const size_t per_img = rram_conv2d_bwd_workspace(&d, 1);
+  RRAM_REQUIRE(ws != nullptr && ws_bytes >= per_img, "conv2d_bwd: workspace needs >= %zu bytes",
+               per_img);
+  int chunk = static_cast<int>(ws_bytes / per_img);
+  if (chunk > d.num) chunk = d.num;
+  float* col = static_cast<float*>(ws);
+  const int64_t chw = (int64_t)d.channels * d.height * d.width;
+  const int64_t ohw = (int64_t)d.num_output * HoWo;
+  for (int n0 = 0; n0 < d.num; n0 += chunk) {
+    const int nimg = (d.num - n0) < chunk ? (d.num - n0) : chunk;
+    const int64_t ldcol = (int64_t)nimg * HoWo;
+    if (dw) {
+      rc = im2col_core(x + n0 * chw, chw, nimg, &d, col, ldcol, s);
+      if (rc) return rc;
+      rc = conv_bwd_weight_core(&d, nimg, dy + n0 * ohw, col, ldcol, dw, s);
+      if (rc) return rc;
+    }
+    if (dx) {
+      rc = conv_bwd_data_col_core(&d, nimg, w, dy + n0 * ohw, col, ldcol, s);
+      if (rc) return rc;
+      rc = col2im_core(col, ldcol, nimg, &d, dx + n0 * chw, chw, 0, s);
+      if (rc) return rc;
+    }
+  }
+  return RRAM_OK;
+}
+
+int rram_im2col(const float* im, int C, int H, int W, int kh, int kw, int ph, int pw, int sh,
+                int sw, int dh, int dwl, float* col, rram_stream_t s) {
+  rram_conv_desc d{1, C, H, W, 1, kh, kw, ph, pw, sh, sw, dh, dwl, 1, 0, 0};
+  int rc = rram_conv_out_shape(&d);
+  if (rc) return rc;
+  RRAM_REQUIRE(im && col, "im2col: NULL");
+  return im2col_core(im, 0, 1, &d, col, (int64_t)d.out_h * d.out_w, as_stream(s));
+}
+
+int rram_col2im(const float* col, int C, int H, int W, int kh, int kw, int ph, int pw, int sh,
+                int sw, int dh, int dwl, float* im, rram_stream_t s) {
+  rram_conv_desc d{1, C, H, W, 1, kh, kw, ph, pw, sh, sw, dh, dwl, 1, 0, 0};
+  int rc = rram_conv_out_shape(&d);
+  if (rc) return rc;
+  RRAM_REQUIRE(im && col, "col2im: NULL");
+  return col2im_core(col, (int64_t)d.out_h * d.out_w, 1, &d, im, 0, 0, as_stream(s));
+}
+
+int rram_ip_fwd(const float* x, const float* w, const float* bias, float* y, int M, int N, int K,
+                int transpose, int relu, void* ws, size_t ws_bytes, rram_stream_t s) {
+  // top = bottom * W^T (W [N][K]) or bottom * W (W [K][N], transpose)
+  if (transpose)
+    return gemm_core(0, 0, M, N, K, 1.0f, x, K, w, N, 0.0f, y, N, bias, RRAM_BIAS_COL, relu, ws,
+                     ws_bytes, as_stream(s));
+  return gemm_core(0, 1, M, N, K, 1.0f, x, K, w, K, 0.0f, y, N, bias, RRAM_BIAS_COL, relu, ws,
+                   ws_bytes, as_stream(s));
+}
+
+int rram_ip_bwd(const float* x, const float* w, const float* dy, float* dw, float* db, float* dx,
+                int M, int N, int K, int transpose, rram_stream_t st) {
+  hipStream_t s = as_stream(st);
+  int rc;
+  if (dw) {
+    if (transpose)  // dW[K][N] += X^T dY
+      rc = gemm_core(1, 0, K, N, M, 1.0f, x, K, dy, N, 1.0f, dw, N, nullptr, 0, 0, nullptr, 0, s);
+    else  // dW[N][K] += dY^T X
+      rc = gemm_core(1, 0, N, K, M, 1.0f, dy, N, x, K, 1.0f, dw, K, nullptr, 0, 0, nullptr, 0, s);
+    if (rc) return rc;
+  }
+  if (db) {
+    // db[n] += sum_m dY[m][n]  (the reference's gemv against bias_multiplier_)
+    if (M > 0 && N > 0) {
+      hipLaunchKernelGGL(k_bias_bwd, dim3(N), dim3(256), 0, s, dy, db, M, N, 1);
+      rc = launch_status("ip bias bwd");
+      if (rc) return rc;
+    }
+  }
+  if (dx) {
+    if (transpose)  // dX[M][K] = dY W^T
+      rc = gemm_core(0, 1, M, K, N, 1.0f, dy, N, w, N, 0.0f, dx, K, nullptr, 0, 0, nullptr, 0, s);
+    else  // dX = dY W
+      rc = gemm_core(0, 0, M, K, N, 1.0f, dy, N, w, K, 0.0f, dx, K, nullptr, 0, 0, nullptr, 0, s);
+    if (rc) return rc;
+  }
+  return RRAM_OK;
+}
+
+int rram_bias_add(float* y, const float* b, int num, int C, int inner, rram_stream_t s) {
+  RRAM_REQUIRE(num >= 0 && C >= 0 && inner >= 0, "bias_add: negative size");
+  const int64_t total = (int64_t)num * C * inner;
+  if (total == 0) return RRAM_OK;
+  RRAM_REQUIRE(y && b, "bias_add: NULL");
+  hipLaunchKernelGGL(k_bias_add, dim3(stream_blocks(total)), dim3(256), 0, as_stream(s), y, b, num,
+                     C, inner);
+  return launch_status("bias_add");
+}
+
+int rram_bias_bwd(const float* dy, float* db, int num, int C, int inner, rram_stream_t s) {
+  RRAM_REQUIRE(num >= 0 && C >= 0 && inner >= 0, "bias_bwd: negative size");
+  if (C == 0) return RRAM_OK;
+  RRAM_REQUIRE(dy && db, "bias_bwd: NULL");
+  hipLaunchKernelGGL(k_bias_bwd, dim3(C), dim3(256), 0, as_stream(s), dy, db, num, C, inner);
+  return launch_status("bias_bwd");
+}
+
+}  // extern "C"

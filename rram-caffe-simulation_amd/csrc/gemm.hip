@@ -1,0 +1,684 @@
+// fp32 GEMM and implicit-GEMM convolution on gfx950 MFMA
+// (v_mfma_f32_32x32x2_f32: exact fp32, 64 FLOP/clk/SIMD).
+//
+// One templated kernel serves every contraction of the conv/IP path:
+//   C[m][n] = sum_k A(m,k) * B(n,k)
+// A and B are "operand views" (loader modes) so the same MFMA core runs
+//   - Caffe GEMM with any transpose combination  (KC / RC views),
+//   - implicit-im2col convolution forward         (CONV view: gather into LDS),
+//   - NCHW activations / gradients spanning images (NCHW / NCHWT views).
+// Block: 256 threads = 4 waves; each wave owns MI x NI tiles of 32x32.
+// LDS holds both operands k-contiguous ([row][BK+4]), double-buffered and
+// register-staged (global loads for tile t+1 are issued before the MFMAs of
+// tile t).  K is consumed in a permuted order inside a tile (lane half h at
+// step s uses k = h*BK/2 + s) so that each lane reads its fragments with
+// 16-byte LDS reads; the permutation is the same for A and B, so the
+// contraction is unchanged.
+#include "rram_common.hpp"
+
+namespace rram {
+namespace {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int BK = 16;
+constexpr int LDK = BK + 4;  // padded LDS row (floats); 80 B keeps 16-B alignment
+
+enum Mode : int { KC = 0, RC = 1, CONV = 2, NCHW = 3, NCHWT = 4 };
+enum OutMode : int { OUT_ROWMAJOR = 0, OUT_NCHW = 1 };
+
+// Fast unsigned division by a runtime constant (x < 2^31).
+struct FastDiv {
+  uint32_t d, m, s;
+};
+static FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f{d, 0, 0};
+  if (d <= 1) {
+    f.m = 0;
+    f.s = 0;
+    return f;
+  }
+  uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  f.s = s;
+  f.m = static_cast<uint32_t>(((1ull << 32) * ((1ull << s) - d)) / d + 1);
+  return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t x, const FastDiv& f) {
+  if (f.d <= 1) return x;
+  const uint32_t t = __umulhi(x, f.m);
+  return (t + x) >> f.s;
+}
+
+// Operand view: element (row, k).
+struct View {
+  const float* p;
+  int64_t ld;        // KC: row stride; RC: k stride; NCHW(T): channel stride (= HW)
+  int64_t img;       // NCHW/NCHWT/CONV: image stride
+  int rows, kdim;    // logical extent
+  FastDiv hw;        // NCHW/NCHWT: spatial size
+};
+
+struct ConvGeom {
+  int C, H, W, KH, KW, ph, pw, sh, sw, dh, dw, Ho, Wo;
+  FastDiv khkw, kw_div, howo, wo_div;
+  int64_t chw;  // image stride of the input (C*H*W)
+};
+
+struct Epi {
+  float* C;
+  int64_t ldc;       // ROWMAJOR: row stride; NCHW: channel stride (= HW)
+  int64_t cimg;      // NCHW: image stride (Cout*HW)
+  FastDiv hw;        // NCHW: spatial size
+  float alpha, beta;
+  const float* bias;
+  int bias_mode;
+  int relu;
+};
+
+struct Params {
+  View a, b;
+  ConvGeom cv;
+  Epi e;
+  int M, N, K;
+  int k_chunk;               // split-K chunk length (multiple of BK)
+  float* ws;                 // split-K partials [split][M][N] (nullptr: direct)
+  int64_t grp_a, grp_b, grp_c;  // per-group pointer offsets (blockIdx.z = group)
+  int64_t grp_bias;
+  int split;                 // number of K splits (blockIdx.z = split when > 1)
+};
+
+// Per-thread constant data of the B/A loader for the CONV view.
+struct ConvCol {
+  int64_t base;  // image offset of this thread's column (n*C*H*W)
+  int hb, wb;    // ho*sh - ph, wo*sw - pw
+  bool valid;
+};
+
+template <int ROWS>
+struct Loader {
+  static constexpr int EPT = ROWS * BK / 256;
+  float v[EPT];
+};
+
+__device__ __forceinline__ float ld_kc(const View& vw, int row, int k) {
+  return (row < vw.rows && k < vw.kdim) ? vw.p[(int64_t)row * vw.ld + k] : 0.0f;
+}
+__device__ __forceinline__ float ld_rc(const View& vw, int row, int k) {
+  return (row < vw.rows && k < vw.kdim) ? vw.p[(int64_t)k * vw.ld + row] : 0.0f;
+}
+// NCHW: row = channel, k = flattened (image, spatial)
+__device__ __forceinline__ float ld_nchw(const View& vw, int row, int k) {
+  if (row >= vw.rows || k >= vw.kdim) return 0.0f;
+  const uint32_t im = fdiv(static_cast<uint32_t>(k), vw.hw);
+  const uint32_t s = static_cast<uint32_t>(k) - im * vw.hw.d;
+  return vw.p[(int64_t)im * vw.img + (int64_t)row * vw.ld + s];
+}
+// NCHWT: row = flattened (image, spatial), k = channel
+__device__ __forceinline__ float ld_nchwt(const View& vw, int row, int k) {
+  if (row >= vw.rows || k >= vw.kdim) return 0.0f;
+  const uint32_t im = fdiv(static_cast<uint32_t>(row), vw.hw);
+  const uint32_t s = static_cast<uint32_t>(row) - im * vw.hw.d;
+  return vw.p[(int64_t)im * vw.img + (int64_t)k * vw.ld + s];
+}
+
+// Element e of a ROWS x BK tile -> (row, k) for a view mode.  KC / NCHW are
+// k-fastest (memory is contiguous along k); the others are row-fastest.
+template <int MODE, int ROWS>
+__device__ __forceinline__ void tile_coord(int e, int& row, int& k) {
+  if (MODE == KC || MODE == NCHW) {
+    row = e / BK;
+    k = e % BK;
+  } else {
+    row = e % ROWS;
+    k = e / ROWS;
+  }
+}
+
+template <int MODE, int ROWS>
+__device__ __forceinline__ void load_tile(Loader<ROWS>& L, const View& vw, const ConvGeom& cv,
+                                          const ConvCol& col, int row0, int k0, int kend) {
+  constexpr int EPT = Loader<ROWS>::EPT;
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) {
+    const int e = threadIdx.x + i * 256;
+    int r, kk;
+    tile_coord<MODE, ROWS>(e, r, kk);
+    const int row = row0 + r;
+    const int k = k0 + kk;
+    float x = 0.0f;
+    if (MODE == KC) {
+      if (k < kend) x = ld_kc(vw, row, k);
+    } else if (MODE == RC) {
+      if (k < kend) x = ld_rc(vw, row, k);
+    } else if (MODE == NCHW) {
+      if (k < kend) x = ld_nchw(vw, row, k);
+    } else if (MODE == NCHWT) {
+      if (k < kend) x = ld_nchwt(vw, row, k);
+    } else {  // CONV gather: k is wave-uniform for ROWS >= 64
+      const int ku = __builtin_amdgcn_readfirstlane(k);
+      const uint32_t c = fdiv(static_cast<uint32_t>(ku), cv.khkw);
+      const uint32_t rem = static_cast<uint32_t>(ku) - c * cv.khkw.d;
+      const uint32_t kh = fdiv(rem, cv.kw_div);
+      const uint32_t kw = rem - kh * cv.kw_div.d;
+      const int iy = col.hb + static_cast<int>(kh) * cv.dh;
+      const int ix = col.wb + static_cast<int>(kw) * cv.dw;
+      if (col.valid && ku < kend && static_cast<unsigned>(iy) < static_cast<unsigned>(cv.H) &&
+          static_cast<unsigned>(ix) < static_cast<unsigned>(cv.W))
+        x = vw.p[col.base + (int64_t)c * cv.H * cv.W + (int64_t)iy * cv.W + ix];
+    }
+    L.v[i] = x;
+  }
+}
+
+template <int MODE, int ROWS>
+__device__ __forceinline__ void store_tile(const Loader<ROWS>& L, float* lds) {
+  constexpr int EPT = Loader<ROWS>::EPT;
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) {
+    const int e = threadIdx.x + i * 256;
+    int r, kk;
+    tile_coord<MODE, ROWS>(e, r, kk);
+    lds[r * LDK + kk] = L.v[i];
+  }
+}
+
+template <int WM, int WN, int MI, int NI, int AM, int BMODE, int OM>
+__global__ void __launch_bounds__(256) k_gemm(Params P) {
+  constexpr int BMr = WM * MI * 32;
+  constexpr int BNr = WN * NI * 32;
+  static_assert(WM * WN == 4, "4 waves per block");
+  static_assert(BMr * BK % 256 == 0 && BNr * BK % 256 == 0, "tile/threads");
+  __shared__ __attribute__((aligned(16))) float As[2][BMr * LDK];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BNr * LDK];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wm = wave / WN;
+  const int wn = wave % WN;
+
+  // blockIdx.x -> N tiles (fastest, so consecutive blocks share the A panel)
+  const int n0 = blockIdx.x * BNr;
+  const int m0 = blockIdx.y * BMr;
+  int z = blockIdx.z;
+
+  View va = P.a, vb = P.b;
+  Epi ep = P.e;
+  int kbeg = 0, kend = P.K;
+  float* part = nullptr;
+  if (P.split > 1) {
+    kbeg = z * P.k_chunk;
+    kend = min(P.K, kbeg + P.k_chunk);
+    part = P.ws + (int64_t)z * P.M * P.N;
+  } else if (z > 0) {  // conv group
+    va.p += z * P.grp_a;
+    vb.p += z * P.grp_b;
+    ep.C += z * P.grp_c;
+    if (ep.bias) ep.bias += z * P.grp_bias;
+  }
+
+  // CONV column precompute (B operand rows = output positions)
+  ConvCol col{0, 0, 0, false};
+  if (BMODE == CONV) {
+    int r, kk;
+    tile_coord<CONV, BNr>(threadIdx.x, r, kk);
+    const int p = n0 + r;
+    if (p < P.N) {
+      const uint32_t im = fdiv(static_cast<uint32_t>(p), P.cv.howo);
+      const uint32_t s = static_cast<uint32_t>(p) - im * P.cv.howo.d;
+      const uint32_t ho = fdiv(s, P.cv.wo_div);
+      const uint32_t wo = s - ho * P.cv.wo_div.d;
+      col.base = (int64_t)im * P.cv.chw;
+      col.hb = static_cast<int>(ho) * P.cv.sh - P.cv.ph;
+      col.wb = static_cast<int>(wo) * P.cv.sw - P.cv.pw;
+      col.valid = true;
+    }
+  }
+
+  floatx16 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+  Loader<BMr> la;
+  Loader<BNr> lb;
+  const int ntiles = (kend - kbeg + BK - 1) / BK;
+  if (ntiles > 0) {
+    load_tile<AM, BMr>(la, va, P.cv, col, m0, kbeg, kend);
+    load_tile<BMODE, BNr>(lb, vb, P.cv, col, n0, kbeg, kend);
+    store_tile<AM, BMr>(la, As[0]);
+    store_tile<BMODE, BNr>(lb, Bs[0]);
+  }
+  __syncthreads();
+
+  const int lr = lane & 31;
+  const int lh = lane >> 5;
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    const bool more = (t + 1) < ntiles;
+    if (more) {
+      const int kn = kbeg + (t + 1) * BK;
+      load_tile<AM, BMr>(la, va, P.cv, col, m0, kn, kend);
+      load_tile<BMODE, BNr>(lb, vb, P.cv, col, n0, kn, kend);
+    }
+    float4 af[MI][2], bf[NI][2];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const float* pa = &As[cur][(wm * MI * 32 + i * 32 + lr) * LDK + lh * (BK / 2)];
+      af[i][0] = *reinterpret_cast<const float4*>(pa);
+      af[i][1] = *reinterpret_cast<const float4*>(pa + 4);
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const float* pb = &Bs[cur][(wn * NI * 32 + j * 32 + lr) * LDK + lh * (BK / 2)];
+      bf[j][0] = *reinterpret_cast<const float4*>(pb);
+      bf[j][1] = *reinterpret_cast<const float4*>(pb + 4);
+    }
+#pragma unroll
+    for (int s = 0; s < BK / 2; ++s) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const float4 q = af[i][s >> 2];
+        const float a = (s & 3) == 0 ? q.x : (s & 3) == 1 ? q.y : (s & 3) == 2 ? q.z : q.w;
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const float4 u = bf[j][s >> 2];
+          const float b = (s & 3) == 0 ? u.x : (s & 3) == 1 ? u.y : (s & 3) == 2 ? u.z : u.w;
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+    if (more) {
+      store_tile<AM, BMr>(la, As[cur ^ 1]);
+      store_tile<BMODE, BNr>(lb, Bs[cur ^ 1]);
+    }
+    __syncthreads();
+  }
+
+  // epilogue: acc[i][j][r] -> row = (r&3) + 8*(r>>2) + 4*lh, col = lr
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int n = n0 + wn * NI * 32 + j * 32 + lr;
+    if (n >= P.N) continue;
+    int64_t cbase = 0;
+    if (OM == OUT_NCHW && part == nullptr) {
+      const uint32_t im = fdiv(static_cast<uint32_t>(n), ep.hw);
+      const uint32_t s = static_cast<uint32_t>(n) - im * ep.hw.d;
+      cbase = (int64_t)im * ep.cimg + s;
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * MI * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m >= P.M) continue;
+        const float v = acc[i][j][r];
+        if (part != nullptr) {
+          part[(int64_t)m * P.N + n] = v;
+          continue;
+        }
+        float* dst = (OM == OUT_NCHW) ? (ep.C + cbase + (int64_t)m * ep.ldc)
+                                      : (ep.C + (int64_t)m * ep.ldc + n);
+        float o = ep.alpha * v;
+        if (ep.beta != 0.0f) o += ep.beta * *dst;
+        if (ep.bias_mode == RRAM_BIAS_ROW) o += ep.bias[m];
+        else if (ep.bias_mode == RRAM_BIAS_COL) o += ep.bias[n];
+        if (ep.relu) o = fmaxf(o, 0.0f);
+        *dst = o;
+      }
+    }
+  }
+}
+
+// split-K reduction + epilogue (row-major C only)
+__global__ void __launch_bounds__(256) k_splitk_reduce(const float* __restrict__ ws, int split, int M,
+                                                       int N, Epi ep) {
+  const int64_t total = (int64_t)M * N;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.0f;
+    for (int z = 0; z < split; ++z) s += ws[(int64_t)z * total + idx];
+    const int m = static_cast<int>(idx / N);
+    const int n = static_cast<int>(idx - (int64_t)m * N);
+    float* dst = ep.C + (int64_t)m * ep.ldc + n;
+    float o = ep.alpha * s;
+    if (ep.beta != 0.0f) o += ep.beta * *dst;
+    if (ep.bias_mode == RRAM_BIAS_ROW) o += ep.bias[m];
+    else if (ep.bias_mode == RRAM_BIAS_COL) o += ep.bias[n];
+    if (ep.relu) o = fmaxf(o, 0.0f);
+    *dst = o;
+  }
+}
+
+// y = alpha * op(A) x + beta * y, one wave per output element row
+__global__ void __launch_bounds__(256) k_gemv(int trans, int M, int N, float alpha,
+                                              const float* __restrict__ A,
+                                              const float* __restrict__ x, float beta,
+                                              float* __restrict__ y) {
+  // non-trans: y[M] = A[M][N] x[N];  trans: y[N] = A[M][N]^T x[M]
+  const int outs = trans ? N : M;
+  const int red = trans ? M : N;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  const int nw = (gridDim.x * blockDim.x) >> 6;
+  for (int o = wave; o < outs; o += nw) {
+    float s = 0.0f;
+    for (int r = lane; r < red; r += 64) {
+      const float a = trans ? A[(int64_t)r * N + o] : A[(int64_t)o * N + r];
+      s += a * x[r];
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if (lane == 0) y[o] = alpha * s + (beta != 0.0f ? beta * y[o] : 0.0f);
+  }
+}
+
+// im2col / col2im for `nimg` images written into a [K][ldcol] matrix at
+// column offset img*HoWo (ldcol >= nimg*HoWo).
+__global__ void __launch_bounds__(256)
+    k_im2col(const float* __restrict__ im, int64_t im_img, int nimg, int C, int H, int W, int KH,
+             int KW, int ph, int pw, int sh, int sw, int dh, int dw, int Ho, int Wo,
+             float* __restrict__ col, int64_t ldcol) {
+  const int64_t total = (int64_t)nimg * C * KH * KW * Ho * Wo;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    int64_t t = idx;
+    const int wo = t % Wo; t /= Wo;
+    const int ho = t % Ho; t /= Ho;
+    const int kw = t % KW; t /= KW;
+    const int kh = t % KH; t /= KH;
+    const int c = t % C; t /= C;
+    const int n = static_cast<int>(t);
+    const int iy = ho * sh - ph + kh * dh;
+    const int ix = wo * sw - pw + kw * dw;
+    float v = 0.0f;
+    if (static_cast<unsigned>(iy) < static_cast<unsigned>(H) &&
+        static_cast<unsigned>(ix) < static_cast<unsigned>(W))
+      v = im[n * im_img + ((int64_t)c * H + iy) * W + ix];
+    const int64_t krow = ((int64_t)c * KH + kh) * KW + kw;
+    col[krow * ldcol + (int64_t)n * Ho * Wo + (int64_t)ho * Wo + wo] = v;
+  }
+}
+
+// col2im: one thread per image pixel, gathers all column entries that map to it
+__global__ void __launch_bounds__(256)
+    k_col2im(const float* __restrict__ col, int64_t ldcol, int nimg, int C, int H, int W, int KH,
+             int KW, int ph, int pw, int sh, int sw, int dh, int dw, int Ho, int Wo,
+             float* __restrict__ im, int64_t im_img, int accumulate) {
+  const int64_t total = (int64_t)nimg * C * H * W;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    int64_t t = idx;
+    const int x = t % W; t /= W;
+    const int y = t % H; t /= H;
+    const int c = t % C; t /= C;
+    const int n = static_cast<int>(t);
+    float s = 0.0f;
+    for (int kh = 0; kh < KH; ++kh) {
+      const int yy = y + ph - kh * dh;
+      if (yy < 0 || yy % sh) continue;
+      const int ho = yy / sh;
+      if (ho >= Ho) continue;
+      for (int kw = 0; kw < KW; ++kw) {
+        const int xx = x + pw - kw * dw;
+        if (xx < 0 || xx % sw) continue;
+        const int wo = xx / sw;
+        if (wo >= Wo) continue;
+        const int64_t krow = ((int64_t)c * KH + kh) * KW + kw;
+        s += col[krow * ldcol + (int64_t)n * Ho * Wo + (int64_t)ho * Wo + wo];
+      }
+    }
+    float* dst = im + n * im_img + ((int64_t)c * H + y) * W + x;
+    *dst = accumulate ? *dst + s : s;
+  }
+}
+
+template <int WM, int WN, int MI, int NI, int AM, int BMODE, int OM>
+int launch_cfg(const Params& P, int gz, hipStream_t s) {
+  constexpr int BMr = WM * MI * 32, BNr = WN * NI * 32;
+  dim3 grid((P.N + BNr - 1) / BNr, (P.M + BMr - 1) / BMr, gz);
+  hipLaunchKernelGGL((k_gemm<WM, WN, MI, NI, AM, BMODE, OM>), grid, dim3(256), 0, s, P);
+  return launch_status("gemm");
+}
+
+// Tile choice: 128x128 when the grid still fills the chip, else 64x64.
+template <int AM, int BMODE, int OM>
+int launch(const Params& P, int gz, hipStream_t s) {
+  const int64_t big = (int64_t)((P.N + 127) / 128) * ((P.M + 127) / 128) * gz;
+  if (P.M > 64 && big >= 512) return launch_cfg<2, 2, 2, 2, AM, BMODE, OM>(P, gz, s);
+  if (P.M <= 64) return launch_cfg<1, 4, 2, 1, AM, BMODE, OM>(P, gz, s);  // 64 x 128
+  return launch_cfg<2, 2, 1, 1, AM, BMODE, OM>(P, gz, s);                 // 64 x 64
+}
+
+int dispatch(int am, int bm, int om, const Params& P, int gz, hipStream_t s) {
+#define RRAM_D(A_, B_, O_) \
+  if (am == A_ && bm == B_ && om == O_) return launch<A_, B_, O_>(P, gz, s);
+  RRAM_D(KC, KC, OUT_ROWMAJOR)
+  RRAM_D(KC, RC, OUT_ROWMAJOR)
+  RRAM_D(RC, KC, OUT_ROWMAJOR)
+  RRAM_D(RC, RC, OUT_ROWMAJOR)
+  RRAM_D(KC, CONV, OUT_NCHW)
+  RRAM_D(NCHW, KC, OUT_ROWMAJOR)
+  RRAM_D(RC, NCHWT, OUT_ROWMAJOR)
+#undef RRAM_D
+  set_error("gemm: unsupported operand combination %d/%d/%d", am, bm, om);
+  return RRAM_EUNSUPPORTED;
+}
+
+Epi make_epi(float* C, int64_t ldc, float alpha, float beta, const float* bias, int bias_mode,
+             int relu) {
+  Epi e{};
+  e.C = C;
+  e.ldc = ldc;
+  e.cimg = 0;
+  e.hw = make_fastdiv(1);
+  e.alpha = alpha;
+  e.beta = beta;
+  e.bias = bias;
+  e.bias_mode = bias ? bias_mode : RRAM_BIAS_NONE;
+  e.relu = relu;
+  return e;
+}
+
+View make_view(const float* p, int64_t ld, int rows, int kdim) {
+  View v{};
+  v.p = p;
+  v.ld = ld;
+  v.img = 0;
+  v.rows = rows;
+  v.kdim = kdim;
+  v.hw = make_fastdiv(1);
+  return v;
+}
+
+}  // namespace
+
+// Shared by conv.cpp-style entry points below.
+int gemm_core(int trans_a, int trans_b, int M, int N, int K, float alpha, const float* A, int lda,
+              const float* B, int ldb, float beta, float* C, int ldc, const float* bias,
+              int bias_mode, int relu, void* ws, size_t ws_bytes, hipStream_t s) {
+  RRAM_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gemm: negative size");
+  if (M == 0 || N == 0) return RRAM_OK;
+  RRAM_REQUIRE(C != nullptr, "gemm: C is NULL");
+  RRAM_REQUIRE(K == 0 || (A && B), "gemm: A/B NULL");
+  RRAM_REQUIRE(ldc >= N, "gemm: ldc < N");
+  Params P{};
+  // A view: rows = M, contraction = K
+  P.a = trans_a ? make_view(A, lda, M, K) : make_view(A, lda, M, K);
+  P.b = make_view(B, ldb, N, K);
+  P.e = make_epi(C, ldc, alpha, beta, bias, bias_mode, relu);
+  P.M = M;
+  P.N = N;
+  P.K = K;
+  P.split = 1;
+  P.k_chunk = K;
+  // op(A)(m,k) = trans_a ? A[k*lda+m] : A[m*lda+k]; op(B)(k,n) = trans_b ? B[n*ldb+k] : B[k*ldb+n]
+  const int am = trans_a ? RC : KC;
+  const int bm = trans_b ? KC : RC;
+  RRAM_REQUIRE(trans_a ? lda >= M : lda >= K || K == 0, "gemm: lda too small");
+  RRAM_REQUIRE(trans_b ? ldb >= K || K == 0 : ldb >= N, "gemm: ldb too small");
+  // split-K when the 128x128 grid is far below the CU count and K is long
+  const int64_t tiles = (int64_t)((N + 127) / 128) * ((M + 127) / 128);
+  int split = 1;
+  if (ws != nullptr && tiles < 256 && K >= 1024) {
+    split = static_cast<int>(256 / (tiles > 0 ? tiles : 1));
+    if (split > 16) split = 16;
+    while (split > 1 && (K / split) < 256) --split;
+    while (split > 1 && (size_t)split * M * N * sizeof(float) > ws_bytes) --split;
+  }
+  if (split > 1) {
+    int chunk = (K + split - 1) / split;
+    chunk = (chunk + BK - 1) / BK * BK;
+    split = (K + chunk - 1) / chunk;
+    P.split = split;
+    P.k_chunk = chunk;
+    P.ws = static_cast<float*>(ws);
+    // big tiles for the split grid
+    dim3 grid((N + 127) / 128, (M + 127) / 128, split);
+    if (am == KC && bm == KC)
+      hipLaunchKernelGGL((k_gemm<2, 2, 2, 2, KC, KC, OUT_ROWMAJOR>), grid, dim3(256), 0, s, P);
+    else if (am == KC && bm == RC)
+      hipLaunchKernelGGL((k_gemm<2, 2, 2, 2, KC, RC, OUT_ROWMAJOR>), grid, dim3(256), 0, s, P);
+    else if (am == RC && bm == KC)
+      hipLaunchKernelGGL((k_gemm<2, 2, 2, 2, RC, KC, OUT_ROWMAJOR>), grid, dim3(256), 0, s, P);
+    else
+      hipLaunchKernelGGL((k_gemm<2, 2, 2, 2, RC, RC, OUT_ROWMAJOR>), grid, dim3(256), 0, s, P);
+    int rc = launch_status("gemm splitk");
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_splitk_reduce, dim3(stream_blocks((int64_t)M * N)), dim3(256), 0, s,
+                       P.ws, split, M, N, P.e);
+    return launch_status("gemm splitk reduce");
+  }
+  return dispatch(am, bm, OUT_ROWMAJOR, P, 1, s);
+}
+
+int conv_fwd_core(const rram_conv_desc* d, const float* x, const float* w, const float* bias,
+                  float* y, int relu, hipStream_t s) {
+  const int g = d->group;
+  const int cin_g = d->channels / g, cout_g = d->num_output / g;
+  const int K = cin_g * d->kernel_h * d->kernel_w;
+  const int HoWo = d->out_h * d->out_w;
+  Params P{};
+  P.M = cout_g;
+  P.N = d->num * HoWo;
+  P.K = K;
+  P.split = 1;
+  P.k_chunk = K;
+  P.a = make_view(w, K, cout_g, K);
+  P.b = make_view(x, 0, P.N, K);
+  ConvGeom& cv = P.cv;
+  cv.C = cin_g;
+  cv.H = d->height;
+  cv.W = d->width;
+  cv.KH = d->kernel_h;
+  cv.KW = d->kernel_w;
+  cv.ph = d->pad_h;
+  cv.pw = d->pad_w;
+  cv.sh = d->stride_h;
+  cv.sw = d->stride_w;
+  cv.dh = d->dilation_h;
+  cv.dw = d->dilation_w;
+  cv.Ho = d->out_h;
+  cv.Wo = d->out_w;
+  cv.khkw = make_fastdiv(d->kernel_h * d->kernel_w);
+  cv.kw_div = make_fastdiv(d->kernel_w);
+  cv.howo = make_fastdiv(HoWo);
+  cv.wo_div = make_fastdiv(d->out_w);
+  cv.chw = (int64_t)d->channels * d->height * d->width;
+  P.e = make_epi(y, HoWo, 1.0f, 0.0f, bias, RRAM_BIAS_ROW, relu);
+  P.e.cimg = (int64_t)d->num_output * HoWo;
+  P.e.hw = make_fastdiv(HoWo);
+  P.grp_a = (int64_t)cout_g * K;
+  P.grp_b = (int64_t)cin_g * d->height * d->width;
+  P.grp_c = (int64_t)cout_g * HoWo;
+  P.grp_bias = cout_g;
+  return dispatch(KC, CONV, OUT_NCHW, P, g, s);
+}
+
+// dW_g[co][k] += sum_p dY_g[co][p] col_g[k][p]   (col: [Cin*kh*kw][ldcol])
+int conv_bwd_weight_core(const rram_conv_desc* d, int nimg, const float* dy, const float* col,
+                         int64_t ldcol, float* dw, hipStream_t s) {
+  const int g = d->group;
+  const int cin_g = d->channels / g, cout_g = d->num_output / g;
+  const int K = cin_g * d->kernel_h * d->kernel_w;
+  const int HoWo = d->out_h * d->out_w;
+  for (int gi = 0; gi < g; ++gi) {
+    Params P{};
+    P.M = cout_g;
+    P.N = K;
+    P.K = nimg * HoWo;
+    P.split = 1;
+    P.k_chunk = P.K;
+    P.a = make_view(dy + (int64_t)gi * cout_g * HoWo, HoWo, cout_g, P.K);
+    P.a.img = (int64_t)d->num_output * HoWo;
+    P.a.hw = make_fastdiv(HoWo);
+    P.b = make_view(col + (int64_t)gi * K * ldcol, ldcol, K, P.K);
+    P.e = make_epi(dw + (int64_t)gi * cout_g * K, K, 1.0f, 1.0f, nullptr, 0, 0);
+    const int rc = dispatch(NCHW, KC, OUT_ROWMAJOR, P, 1, s);
+    if (rc) return rc;
+  }
+  return RRAM_OK;
+}
+
+// dcol_g[k][p] = sum_co W_g[co][k] dY_g[co][p]
+int conv_bwd_data_col_core(const rram_conv_desc* d, int nimg, const float* w, const float* dy,
+                           float* col, int64_t ldcol, hipStream_t s) {
+  const int g = d->group;
+  const int cin_g = d->channels / g, cout_g = d->num_output / g;
+  const int K = cin_g * d->kernel_h * d->kernel_w;
+  const int HoWo = d->out_h * d->out_w;
+  for (int gi = 0; gi < g; ++gi) {
+    Params P{};
+    P.M = K;
+    P.N = nimg * HoWo;
+    P.K = cout_g;
+    P.split = 1;
+    P.k_chunk = P.K;
+    P.a = make_view(w + (int64_t)gi * cout_g * K, K, K, cout_g);  // RC: A(k_row, co) = W[co*K + k]
+    P.b = make_view(dy + (int64_t)gi * cout_g * HoWo, HoWo, P.N, cout_g);
+    P.b.img = (int64_t)d->num_output * HoWo;
+    P.b.hw = make_fastdiv(HoWo);
+    P.e = make_epi(col + (int64_t)gi * K * ldcol, ldcol, 1.0f, 0.0f, nullptr, 0, 0);
+    const int rc = dispatch(RC, NCHWT, OUT_ROWMAJOR, P, 1, s);
+    if (rc) return rc;
+  }
+  return RRAM_OK;
+}
+
+int im2col_core(const float* im, int64_t im_img, int nimg, const rram_conv_desc* d, float* col,
+                int64_t ldcol, hipStream_t s) {
+  const int64_t total = (int64_t)nimg * d->channels * d->kernel_h * d->kernel_w * d->out_h * d->out_w;
+  if (total == 0) return RRAM_OK;
+  hipLaunchKernelGGL(k_im2col, dim3(stream_blocks(total)), dim3(256), 0, s, im, im_img, nimg,
+                     d->channels, d->height, d->width, d->kernel_h, d->kernel_w, d->pad_h,
+                     d->pad_w, d->stride_h, d->stride_w, d->dilation_h, d->dilation_w, d->out_h,
+                     d->out_w, col, ldcol);
+  return launch_status("im2col");
+}
+
+int col2im_core(const float* col, int64_t ldcol, int nimg, const rram_conv_desc* d, float* im,
+                int64_t im_img, int accumulate, hipStream_t s) {
+  const int64_t total = (int64_t)nimg * d->channels * d->height * d->width;
+  if (total == 0) return RRAM_OK;
+  hipLaunchKernelGGL(k_col2im, dim3(stream_blocks(total)), dim3(256), 0, s, col, ldcol, nimg,
+                     d->channels, d->height, d->width, d->kernel_h, d->kernel_w, d->pad_h,
+                     d->pad_w, d->stride_h, d->stride_w, d->dilation_h, d->dilation_w, d->out_h,
+                     d->out_w, im, im_img, accumulate);
+  return launch_status("col2im");
+}
+
+int gemv_core(int trans, int M, int N, float alpha, const float* A, const float* x, float beta,
+              float* y, hipStream_t s) {
+  RRAM_REQUIRE(M >= 0 && N >= 0, "gemv: negative size");
+  const int outs = trans ? N : M;
+  if (outs == 0) return RRAM_OK;
+  RRAM_REQUIRE(A && x && y, "gemv: NULL");
+  const int blocks = (outs + 3) / 4 < 2048 ? (outs + 3) / 4 : 2048;
+  hipLaunchKernelGGL(k_gemv, dim3(blocks), dim3(256), 0, s, trans, M, N, alpha, A, x, beta, y);
+  return launch_status("gemv");
+}
+
+}  // namespace rram

@@ -1,0 +1,439 @@
+// Support layers needed to run LeNet / CIFAR / AlexNet / GoogLeNet end to end
+// (SURVEY.md §2.1 "minimal correct support kernels").  Semantics follow the
+// reference layers (file:line cited per kernel); none of these is on the
+// fault path, so they are plain coalesced elementwise / per-column kernels.
+#include <float.h>
+#include <math.h>
+
+#include "rram_common.hpp"
+
+namespace rram {
+namespace {
+
+#define GRID_LOOP(i, n)                                                            \
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < (n); \
+       i += (int64_t)gridDim.x * blockDim.x)
+
+// relu_layer.cu:9-15 / :35-44
+__global__ void k_relu_fwd(const float* __restrict__ x, float* __restrict__ y, int64_t n, float slope) {
+  GRID_LOOP(i, n) {
+    const float v = x[i];
+    y[i] = v > 0.0f ? v : v * slope;
+  }
+}
+__global__ void k_relu_bwd(const float* __restrict__ x, const float* __restrict__ dy,
+                           float* __restrict__ dx, int64_t n, float slope) {
+  GRID_LOOP(i, n) dx[i] = dy[i] * ((x[i] > 0.0f) + (x[i] <= 0.0f) * slope);
+}
+
+// pooling_layer.cu MaxPoolForward / AvePoolForward
+__global__ void k_pool_fwd(const float* __restrict__ x, float* __restrict__ y, int* __restrict__ mask,
+                           int num, int C, int H, int W, int PH, int PW, int kh, int kw, int sh,
+                           int sw, int ph, int pw, int method) {
+  const int64_t total = (int64_t)num * C * PH * PW;
+  GRID_LOOP(idx, total) {
+    const int pwi = idx % PW;
+    const int phi = (idx / PW) % PH;
+    const int64_t nc = idx / PW / PH;
+    const float* xs = x + nc * H * W;
+    int hs = phi * sh - ph, ws = pwi * sw - pw;
+    if (method == RRAM_POOL_MAX) {
+      const int he = min(hs + kh, H), we = min(ws + kw, W);
+      hs = max(hs, 0);
+      ws = max(ws, 0);
+      float mv = -FLT_MAX;
+      int mi = -1;
+      for (int h = hs; h < he; ++h)
+        for (int w = ws; w < we; ++w)
+          if (xs[h * W + w] > mv) {
+            mi = h * W + w;
+            mv = xs[mi];
+          }
+      y[idx] = mv;
+      if (mask) mask[idx] = mi;
+    } else {
+      int he = min(hs + kh, H + ph), we = min(ws + kw, W + pw);
+      const int psize = (he - hs) * (we - ws);
+      hs = max(hs, 0);
+      ws = max(ws, 0);
+      he = min(he, H);
+      we = min(we, W);
+      float s = 0.0f;
+      for (int h = hs; h < he; ++h)
+        for (int w = ws; w < we; ++w) s += xs[h * W + w];
+      y[idx] = s / psize;
+    }
+  }
+}
+
+// pooling_layer.cu MaxPoolBackward / AvePoolBackward
+__global__ void k_pool_bwd(const float* __restrict__ dy, const int* __restrict__ mask,
+                           float* __restrict__ dx, int num, int C, int H, int W, int PH, int PW,
+                           int kh, int kw, int sh, int sw, int ph, int pw, int method) {
+  const int64_t total = (int64_t)num * C * H * W;
+  GRID_LOOP(idx, total) {
+    const int w = idx % W;
+    const int h = (idx / W) % H;
+    const int64_t nc = idx / W / H;
+    const float* d = dy + nc * PH * PW;
+    float g = 0.0f;
+    if (method == RRAM_POOL_MAX) {
+      const int* m = mask + nc * PH * PW;
+      const int phs = (h + ph < kh) ? 0 : (h + ph - kh) / sh + 1;
+      const int phe = min((h + ph) / sh + 1, PH);
+      const int pws = (w + pw < kw) ? 0 : (w + pw - kw) / sw + 1;
+      const int pwe = min((w + pw) / sw + 1, PW);
+      for (int a = phs; a < phe; ++a)
+        for (int b = pws; b < pwe; ++b)
+          if (m[a * PW + b] == h * W + w) g += d[a * PW + b];
+    } else {
+      const int hh = h + ph, ww = w + pw;
+      const int phs = (hh < kh) ? 0 : (hh - kh) / sh + 1;
+      const int phe = min(hh / sh + 1, PH);
+      const int pws = (ww < kw) ? 0 : (ww - kw) / sw + 1;
+      const int pwe = min(ww / sw + 1, PW);
+      for (int a = phs; a < phe; ++a)
+        for (int b = pws; b < pwe; ++b) {
+          const int hs = a * sh - ph, ws = b * sw - pw;
+          const int he = min(hs + kh, H + ph), we = min(ws + kw, W + pw);
+          g += d[a * PW + b] / ((he - hs) * (we - ws));
+        }
+    }
+    dx[idx] = g;
+  }
+}
+
+// lrn_layer.cu LRNFillScale + LRNComputeOutput (window sum evaluated directly)
+__global__ void k_lrn_fwd(const float* __restrict__ x, float* __restrict__ y, float* __restrict__ scale,
+                          int num, int C, int HW, int size, float alpha_over_size, float beta,
+                          float k) {
+  const int64_t total = (int64_t)num * C * HW;
+  const int pre = (size - 1) / 2;
+  GRID_LOOP(idx, total) {
+    const int s = idx % HW;
+    const int c = (idx / HW) % C;
+    const int64_t n = idx / HW / C;
+    const float* xc = x + n * C * HW + s;
+    float acc = 0.0f;
+    const int c0 = max(c - pre, 0), c1 = min(c - pre + size, C);
+    for (int j = c0; j < c1; ++j) {
+      const float v = xc[(int64_t)j * HW];
+      acc += v * v;
+    }
+    const float sc = k + acc * alpha_over_size;
+    if (scale) scale[idx] = sc;
+    y[idx] = x[idx] * powf(sc, -beta);
+  }
+}
+
+// lrn_layer.cu LRNComputeDiff
+__global__ void k_lrn_bwd(const float* __restrict__ x, const float* __restrict__ y,
+                          const float* __restrict__ scale, const float* __restrict__ dy,
+                          float* __restrict__ dx, int num, int C, int HW, int size,
+                          float cache_ratio, float beta) {
+  const int64_t total = (int64_t)num * C * HW;
+  const int pre = (size - 1) / 2;
+  const int post = size - pre - 1;
+  GRID_LOOP(idx, total) {
+    const int s = idx % HW;
+    const int c = (idx / HW) % C;
+    const int64_t base = (idx / HW / C) * C * HW + s;
+    // channels j whose window contains c: j in [c - post, c + pre]
+    float ratio = 0.0f;
+    const int j0 = max(c - post, 0), j1 = min(c + pre + 1, C);
+    for (int j = j0; j < j1; ++j) {
+      const int64_t o = base + (int64_t)j * HW;
+      ratio += dy[o] * y[o] / scale[o];
+    }
+    dx[idx] = dy[idx] * powf(scale[idx], -beta) - cache_ratio * x[idx] * ratio;
+  }
+}
+
+// softmax_layer.cu: one wave per (outer, inner) column
+__global__ void __launch_bounds__(256) k_softmax(const float* __restrict__ x, float* __restrict__ y,
+                                                 int outer, int C, int inner) {
+  const int lane = threadIdx.x & 63;
+  const int64_t cols = (int64_t)outer * inner;
+  for (int64_t col = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; col < cols;
+       col += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+    const int64_t o = col / inner, q = col - o * inner;
+    const float* xs = x + o * C * inner + q;
+    float* ys = y + o * C * inner + q;
+    float m = -FLT_MAX;
+    for (int c = lane; c < C; c += 64) m = fmaxf(m, xs[(int64_t)c * inner]);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+    float s = 0.0f;
+    for (int c = lane; c < C; c += 64) {
+      const float e = expf(xs[(int64_t)c * inner] - m);
+      ys[(int64_t)c * inner] = e;
+      s += e;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    for (int c = lane; c < C; c += 64) ys[(int64_t)c * inner] /= s;
+  }
+}
+
+// softmax_loss_layer.cpp:95-112 (single block, deterministic)
+__global__ void __launch_bounds__(1024) k_softmax_loss_fwd(const float* __restrict__ prob,
+                                                           const float* __restrict__ label,
+                                                           float* out, int outer, int C, int inner,
+                                                           int ignore) {
+  __shared__ float sl[16], sc[16];
+  float loss = 0.0f, cnt = 0.0f;
+  const int64_t cols = (int64_t)outer * inner;
+  for (int64_t col = threadIdx.x; col < cols; col += blockDim.x) {
+    const int64_t o = col / inner, q = col - o * inner;
+    const int lv = static_cast<int>(label[col]);
+    if (ignore >= 0 && lv == ignore) continue;
+    loss -= logf(fmaxf(prob[(o * C + lv) * inner + q], FLT_MIN));
+    cnt += 1.0f;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    loss += __shfl_xor(loss, off, 64);
+    cnt += __shfl_xor(cnt, off, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    sl[threadIdx.x >> 6] = loss;
+    sc[threadIdx.x >> 6] = cnt;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float L = 0.0f, N = 0.0f;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
+      L += sl[i];
+      N += sc[i];
+    }
+    out[0] = L / fmaxf(N, 1.0f);
+  }
+}
+
+__global__ void k_softmax_loss_bwd(const float* __restrict__ prob, const float* __restrict__ label,
+                                   float* __restrict__ dx, int outer, int C, int inner, int ignore,
+                                   float scale_valid) {
+  const int64_t total = (int64_t)outer * C * inner;
+  GRID_LOOP(idx, total) {
+    const int64_t q = idx % inner;
+    const int c = static_cast<int>((idx / inner) % C);
+    const int64_t o = idx / inner / C;
+    const int lv = static_cast<int>(label[o * inner + q]);
+    if (ignore >= 0 && lv == ignore) {
+      dx[idx] = 0.0f;
+    } else {
+      dx[idx] = (prob[idx] - (c == lv ? 1.0f : 0.0f)) * scale_valid;
+    }
+  }
+}
+
+__global__ void k_count_valid(const float* __restrict__ label, int64_t n, int ignore, float* out) {
+  __shared__ float part[16];
+  float c = 0.0f;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x)
+    c += (ignore >= 0 && static_cast<int>(label[i]) == ignore) ? 0.0f : 1.0f;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.0f;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) s += part[i];
+    out[0] = s;
+  }
+}
+
+// accuracy_layer.cpp:48-90: label counted correct when its (value, index)
+// pair is within the top_k of the descending pair order.
+__global__ void __launch_bounds__(1024) k_accuracy(const float* __restrict__ x,
+                                                   const float* __restrict__ label, float* correct,
+                                                   float* count, int outer, int C, int inner,
+                                                   int top_k, int ignore) {
+  __shared__ float sa[16], sc[16];
+  float acc = 0.0f, cnt = 0.0f;
+  const int64_t cols = (int64_t)outer * inner;
+  for (int64_t col = threadIdx.x; col < cols; col += blockDim.x) {
+    const int64_t o = col / inner, q = col - o * inner;
+    const int lv = static_cast<int>(label[col]);
+    if (ignore >= 0 && lv == ignore) continue;
+    const float* xs = x + o * C * inner + q;
+    const float v = xs[(int64_t)lv * inner];
+    int rank = 0;
+    for (int c = 0; c < C; ++c) {
+      const float u = xs[(int64_t)c * inner];
+      rank += (u > v) || (u == v && c > lv);
+    }
+    acc += rank < top_k ? 1.0f : 0.0f;
+    cnt += 1.0f;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    acc += __shfl_xor(acc, off, 64);
+    cnt += __shfl_xor(cnt, off, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    sa[threadIdx.x >> 6] = acc;
+    sc[threadIdx.x >> 6] = cnt;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float A = 0.0f, N = 0.0f;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
+      A += sa[i];
+      N += sc[i];
+    }
+    correct[0] = A;
+    count[0] = N;
+  }
+}
+
+// concat_layer.cu Concat kernel (axis 1)
+__global__ void k_concat(const float* __restrict__ src, float* __restrict__ dst, int num, int sci,
+                         int dci, int off, int backward) {
+  const int64_t total = (int64_t)num * sci;
+  GRID_LOOP(idx, total) {
+    const int64_t n = idx / sci, j = idx - n * sci;
+    const int64_t d = n * dci + off + j;
+    if (backward) const_cast<float*>(src)[idx] = dst[d];
+    else dst[d] = src[idx];
+  }
+}
+
+}  // namespace
+}  // namespace rram
+
+using namespace rram;
+
+extern "C" {
+
+int rram_relu_fwd(const float* x, float* y, int64_t n, float slope, rram_stream_t s) {
+  RRAM_REQUIRE(n >= 0, "relu: n < 0");
+  if (n == 0) return RRAM_OK;
+  RRAM_REQUIRE(x && y, "relu: NULL");
+  hipLaunchKernelGGL(k_relu_fwd, dim3(stream_blocks(n)), dim3(kThreads), 0, as_stream(s), x, y, n, slope);
+  return launch_status("relu_fwd");
+}
+int rram_relu_bwd(const float* x, const float* dy, float* dx, int64_t n, float slope, rram_stream_t s) {
+  RRAM_REQUIRE(n >= 0, "relu: n < 0");
+  if (n == 0) return RRAM_OK;
+  RRAM_REQUIRE(x && dy && dx, "relu: NULL");
+  hipLaunchKernelGGL(k_relu_bwd, dim3(stream_blocks(n)), dim3(kThreads), 0, as_stream(s), x, dy, dx, n, slope);
+  return launch_status("relu_bwd");
+}
+
+int rram_pool_fwd(const float* x, float* y, int* mask, int num, int C, int H, int W, int PH, int PW,
+                  int kh, int kw, int sh, int sw, int ph, int pw, int method, rram_stream_t s) {
+  RRAM_REQUIRE(num >= 0 && C > 0 && H > 0 && W > 0 && PH > 0 && PW > 0 && kh > 0 && kw > 0 &&
+                   sh > 0 && sw > 0 && ph >= 0 && pw >= 0,
+               "pool_fwd: bad geometry");
+  RRAM_REQUIRE(method == RRAM_POOL_MAX || method == RRAM_POOL_AVE, "pool_fwd: bad method");
+  const int64_t total = (int64_t)num * C * PH * PW;
+  if (total == 0) return RRAM_OK;
+  RRAM_REQUIRE(x && y, "pool_fwd: NULL");
+  hipLaunchKernelGGL(k_pool_fwd, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), x, y,
+                     mask, num, C, H, W, PH, PW, kh, kw, sh, sw, ph, pw, method);
+  return launch_status("pool_fwd");
+}
+int rram_pool_bwd(const float* dy, const int* mask, float* dx, int num, int C, int H, int W, int PH,
+                  int PW, int kh, int kw, int sh, int sw, int ph, int pw, int method, rram_stream_t s) {
+  RRAM_REQUIRE(num >= 0 && C > 0 && H > 0 && W > 0 && PH > 0 && PW > 0 && sh > 0 && sw > 0,
+               "pool_bwd: bad geometry");
+  RRAM_REQUIRE(method != RRAM_POOL_MAX || mask != nullptr, "pool_bwd: MAX needs mask");
+  const int64_t total = (int64_t)num * C * H * W;
+  if (total == 0) return RRAM_OK;
+  RRAM_REQUIRE(dy && dx, "pool_bwd: NULL");
+  hipLaunchKernelGGL(k_pool_bwd, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), dy,
+                     mask, dx, num, C, H, W, PH, PW, kh, kw, sh, sw, ph, pw, method);
+  return launch_status("pool_bwd");
+}
+
+int rram_lrn_fwd(const float* x, float* y, float* scale, int num, int C, int H, int W, int size,
+                 float alpha, float beta, float k, rram_stream_t s) {
+  RRAM_REQUIRE(num >= 0 && C > 0 && H > 0 && W > 0 && size > 0 && (size & 1),
+               "lrn_fwd: bad geometry (local_size must be odd)");
+  const int64_t total = (int64_t)num * C * H * W;
+  if (total == 0) return RRAM_OK;
+  RRAM_REQUIRE(x && y, "lrn_fwd: NULL");
+  hipLaunchKernelGGL(k_lrn_fwd, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), x, y,
+                     scale, num, C, H * W, size, alpha / size, beta, k);
+  return launch_status("lrn_fwd");
+}
+int rram_lrn_bwd(const float* x, const float* y, const float* scale, const float* dy, float* dx,
+                 int num, int C, int H, int W, int size, float alpha, float beta, rram_stream_t s) {
+  RRAM_REQUIRE(num >= 0 && C > 0 && H > 0 && W > 0 && size > 0 && (size & 1),
+               "lrn_bwd: bad geometry");
+  const int64_t total = (int64_t)num * C * H * W;
+  if (total == 0) return RRAM_OK;
+  RRAM_REQUIRE(x && y && scale && dy && dx, "lrn_bwd: NULL");
+  hipLaunchKernelGGL(k_lrn_bwd, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), x, y,
+                     scale, dy, dx, num, C, H * W, size, 2.0f * alpha * beta / size, beta);
+  return launch_status("lrn_bwd");
+}
+
+int rram_softmax_fwd(const float* x, float* y, int outer, int C, int inner, rram_stream_t s) {
+  RRAM_REQUIRE(outer >= 0 && C > 0 && inner > 0, "softmax: bad shape");
+  const int64_t cols = (int64_t)outer * inner;
+  if (cols == 0) return RRAM_OK;
+  RRAM_REQUIRE(x && y, "softmax: NULL");
+  int blocks = static_cast<int>((cols + 3) / 4);
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(k_softmax, dim3(blocks), dim3(256), 0, as_stream(s), x, y, outer, C, inner);
+  return launch_status("softmax");
+}
+
+int rram_softmax_loss_fwd(const float* prob, const float* label, float* out, int outer, int C,
+                          int inner, int ignore, rram_stream_t s) {
+  RRAM_REQUIRE(outer >= 0 && C > 0 && inner > 0 && out, "softmax_loss_fwd: bad args");
+  RRAM_REQUIRE(outer == 0 || (prob && label), "softmax_loss_fwd: NULL");
+  hipLaunchKernelGGL(k_softmax_loss_fwd, dim3(1), dim3(1024), 0, as_stream(s), prob, label, out,
+                     outer, C, inner, ignore);
+  return launch_status("softmax_loss_fwd");
+}
+
+int rram_softmax_loss_bwd(const float* prob, const float* label, float* dx, int outer, int C,
+                          int inner, int ignore, float loss_weight, rram_stream_t s) {
+  RRAM_REQUIRE(outer >= 0 && C > 0 && inner > 0, "softmax_loss_bwd: bad shape");
+  const int64_t total = (int64_t)outer * C * inner;
+  if (total == 0) return RRAM_OK;
+  RRAM_REQUIRE(prob && label && dx, "softmax_loss_bwd: NULL");
+  // normalizer = #valid labels; computed on host for the common no-ignore case
+  float scale = loss_weight / static_cast<float>((int64_t)outer * inner);
+  if (ignore >= 0) {
+    float* dcount = nullptr;
+    RRAM_HIP_RET(hipMallocAsync(reinterpret_cast<void**>(&dcount), sizeof(float), as_stream(s)));
+    hipLaunchKernelGGL(k_count_valid, dim3(1), dim3(1024), 0, as_stream(s), label,
+                       (int64_t)outer * inner, ignore, dcount);
+    float hc = 0.f;
+    RRAM_HIP_RET(hipMemcpyAsync(&hc, dcount, sizeof(float), hipMemcpyDeviceToHost, as_stream(s)));
+    RRAM_HIP_RET(hipStreamSynchronize(as_stream(s)));
+    RRAM_HIP_RET(hipFreeAsync(dcount, as_stream(s)));
+    scale = loss_weight / fmaxf(hc, 1.0f);
+  }
+  hipLaunchKernelGGL(k_softmax_loss_bwd, dim3(stream_blocks(total)), dim3(kThreads), 0,
+                     as_stream(s), prob, label, dx, outer, C, inner, ignore, scale);
+  return launch_status("softmax_loss_bwd");
+}
+
+int rram_accuracy(const float* x, const float* label, float* correct, float* count, int outer,
+                  int C, int inner, int top_k, int ignore, rram_stream_t s) {
+  RRAM_REQUIRE(outer >= 0 && C > 0 && inner > 0 && top_k >= 1 && correct && count,
+               "accuracy: bad args");
+  RRAM_REQUIRE(outer == 0 || (x && label), "accuracy: NULL");
+  hipLaunchKernelGGL(k_accuracy, dim3(1), dim3(1024), 0, as_stream(s), x, label, correct, count,
+                     outer, C, inner, top_k, ignore);
+  return launch_status("accuracy");
+}
+
+int rram_concat_copy(const float* src, float* dst, int num, int sci, int dci, int off, int backward,
+                     rram_stream_t s) {
+  RRAM_REQUIRE(num >= 0 && sci >= 0 && dci >= sci && off >= 0 && off + sci <= dci,
+               "concat: bad geometry");
+  const int64_t total = (int64_t)num * sci;
+  if (total == 0) return RRAM_OK;
+  RRAM_REQUIRE(src && dst, "concat: NULL");
+  hipLaunchKernelGGL(k_concat, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), src, dst,
+                     num, sci, dci, off, backward);
+  return launch_status("concat");
+}
+
+}  // extern "C"

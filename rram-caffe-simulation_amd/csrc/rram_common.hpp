@@ -1,0 +1,103 @@
+// Shared helpers for the gfx950 kernels: status plumbing, launch geometry and
+// the counter-based RNG (Philox4x32-10) used by every random draw.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+
+#include "rram_kernels.h"
+
+namespace rram {
+
+// ---------------------------------------------------------------------------
+// Status plumbing: every C-ABI entry returns an int and records a message.
+// ---------------------------------------------------------------------------
+void set_error(const char* fmt, ...);
+void clear_error();
+
+#define RRAM_REQUIRE(cond, ...)                 \
+  do {                                          \
+    if (!(cond)) {                              \
+      ::rram::set_error(__VA_ARGS__);           \
+      return RRAM_EINVAL;                       \
+    }                                           \
+  } while (0)
+
+#define RRAM_HIP_RET(expr)                                                   \
+  do {                                                                       \
+    hipError_t e_ = (expr);                                                  \
+    if (e_ != hipSuccess) {                                                  \
+      ::rram::set_error("%s: %s", #expr, hipGetErrorString(e_));             \
+      return RRAM_EHIP;                                                      \
+    }                                                                        \
+  } while (0)
+
+// Check the launch just issued (hipGetLastError) and return its status.
+int launch_status(const char* what);
+
+inline hipStream_t as_stream(rram_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Streaming-kernel geometry: 256 threads, at most 8 blocks per CU x 256 CUs,
+// grid-stride beyond that (cdna_hip_programming.md Guideline 11).
+constexpr int kThreads = 256;
+constexpr int kMaxStreamBlocks = 2048;
+inline int stream_blocks(int64_t work_items) {
+  int64_t b = (work_items + kThreads - 1) / kThreads;
+  if (b < 1) b = 1;
+  if (b > kMaxStreamBlocks) b = kMaxStreamBlocks;
+  return static_cast<int>(b);
+}
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al., SC'11), host + device.  Counter layout used by
+// the fault draws: {index_lo, index_hi, map_id, (layer_id << 4) | purpose},
+// key = {seed_lo, seed_hi}.
+// ---------------------------------------------------------------------------
+struct U32x4 {
+  uint32_t x, y, z, w;
+};
+
+__host__ __device__ __forceinline__ U32x4 philox4x32_10(U32x4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = static_cast<uint64_t>(0xD2511F53u) * c.x;
+    const uint64_t p1 = static_cast<uint64_t>(0xCD9E8D57u) * c.z;
+    const uint32_t hi0 = static_cast<uint32_t>(p0 >> 32), lo0 = static_cast<uint32_t>(p0);
+    const uint32_t hi1 = static_cast<uint32_t>(p1 >> 32), lo1 = static_cast<uint32_t>(p1);
+    c = U32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+enum Purpose : uint32_t {
+  kPurposeFault = 0,     // broken / stuck-value words
+  kPurposeVariation = 1, // Box-Muller words for lognormal variation
+  kPurposePairFault = 2, // differential-pair cell faults
+  kPurposePairVar = 3,   // differential-pair variation
+  kPurposeEndurance = 4, // endurance normal draw (fault_init)
+  kPurposeFill = 5,      // fillers
+  kPurposeDropout = 6,
+};
+
+__host__ __device__ __forceinline__ U32x4 draw(uint64_t seed, uint64_t index, uint32_t map_id,
+                                               uint32_t layer_id, uint32_t purpose) {
+  U32x4 c{static_cast<uint32_t>(index), static_cast<uint32_t>(index >> 32), map_id,
+          (layer_id << 4) | (purpose & 15u)};
+  return philox4x32_10(c, static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32));
+}
+
+// 32-bit word -> uniform in (0, 1] (never 0: safe for log) and [0, 1).
+__host__ __device__ __forceinline__ float u01_open0(uint32_t r) {
+  return (static_cast<float>(r >> 8) + 1.0f) * (1.0f / 16777216.0f);
+}
+__host__ __device__ __forceinline__ float u01(uint32_t r) {
+  return static_cast<float>(r >> 8) * (1.0f / 16777216.0f);
+}
+
+}  // namespace rram

@@ -1,0 +1,197 @@
+"""Thin torch-tensor wrappers over the C-ABI (device memory via torch, calls
+via ctypes).  Every op launches on torch's current HIP stream and raises
+RramError on a non-zero status.  No CPU fallback: tensors must live on the GPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _kernels as K
+
+
+def _lib():
+    return K.load()
+
+
+def _stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _p(t):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise K.RramError("rramsim ops take device tensors (no CPU fallback)")
+    if t.dtype not in (torch.float32, torch.int32, torch.int64, torch.uint64):
+        raise K.RramError(f"unsupported dtype {t.dtype}")
+    return C.c_void_p(t.data_ptr())
+
+
+def _f32(t, name):
+    if t is not None and (t.dtype != torch.float32 or not t.is_contiguous()):
+        raise K.RramError(f"{name} must be a contiguous float32 tensor")
+
+
+def counters(n: int, device="cuda") -> torch.Tensor:
+    return torch.zeros(n, dtype=torch.int64, device=device)
+
+
+def fault_threshold(values, split1, split2):
+    _f32(values, "values")
+    K.check(_lib().rram_fault_threshold(_p(values), values.numel(), split1, split2, _stream()),
+            "fault_threshold")
+
+
+def fault_init(endurance, values, mean, std, thr_neg, thr_zero, seed, map_id=0, layer_id=0):
+    _f32(endurance, "endurance")
+    _f32(values, "values")
+    K.check(_lib().rram_fault_init(_p(endurance), _p(values), endurance.numel(), mean, std,
+                                   thr_neg, thr_zero, seed, map_id, layer_id, _stream()),
+            "fault_init")
+
+
+def fail_apply(dw, w, endurance, values, decrement=100.0, eps=1e-20, counter=None):
+    for t, nm in ((dw, "dw"), (w, "w"), (endurance, "endurance"), (values, "values")):
+        _f32(t, nm)
+    K.check(_lib().rram_fail_apply(_p(dw), _p(w), _p(endurance), _p(values), w.numel(),
+                                   decrement, eps, _p(counter), _stream()), "fail_apply")
+
+
+def fail_apply_batched(segs, decrement=100.0, eps=1e-20, counters_t=None):
+    arr = (K.FailSeg * len(segs))()
+    for i, (dw, w, e, v) in enumerate(segs):
+        arr[i] = K.FailSeg(dw.data_ptr(), w.data_ptr(), e.data_ptr(), v.data_ptr(), w.numel())
+    K.check(_lib().rram_fail_apply_batched(arr, len(segs), decrement, eps, _p(counters_t),
+                                           _stream()), "fail_apply_batched")
+
+
+def inject(w_clean, w_out, cfg, seed, map_id, layer_id, counter=None):
+    _f32(w_clean, "w_clean")
+    _f32(w_out, "w_out")
+    K.check(_lib().rram_inject_rng(_p(w_clean), _p(w_out), w_clean.numel(), C.byref(cfg), seed,
+                                   map_id, layer_id, _p(counter), _stream()), "inject_rng")
+
+
+def inject_batched(segs, seed, map_id, counters_t=None):
+    """segs: list of (w_clean, w_out, layer_id, cfg)."""
+    arr = (K.InjectSeg * len(segs))()
+    for i, (src, dst, lid, cfg) in enumerate(segs):
+        arr[i] = K.InjectSeg(src.data_ptr(), dst.data_ptr(), src.numel(), lid, 0, cfg)
+    K.check(_lib().rram_inject_rng_batched(arr, len(segs), seed, map_id, _p(counters_t),
+                                           _stream()), "inject_rng_batched")
+
+
+def threshold_strategy(dw, thr, counter=None):
+    _f32(dw, "dw")
+    K.check(_lib().rram_threshold_strategy(_p(dw), dw.numel(), thr, _p(counter), _stream()),
+            "threshold_strategy")
+
+
+def sgd_update(g, h, momentum, local_rate):
+    K.check(_lib().rram_sgd_update(_p(g), _p(h), g.numel(), momentum, local_rate, _stream()),
+            "sgd_update")
+
+
+def fused_update_fail(w, g, h, e, v, decay, momentum, lr, apply_thr, thr, decrement=100.0,
+                      eps=1e-20, counter=None):
+    K.check(_lib().rram_fused_update_fail(_p(w), _p(g), _p(h), _p(e), _p(v), w.numel(), decay,
+                                          momentum, lr, int(apply_thr), thr, decrement, eps,
+                                          _p(counter), _stream()), "fused_update_fail")
+
+
+def gemm(trans_a, trans_b, M, N, K_, alpha, A, B, beta, Cm):
+    K.check(_lib().rram_gemm_f32(int(trans_a), int(trans_b), M, N, K_, alpha, _p(A), _p(B), beta,
+                                 _p(Cm), _stream()), "gemm")
+
+
+def gemm_ex(trans_a, trans_b, M, N, K_, alpha, A, lda, B, ldb, beta, Cm, ldc, bias=None,
+            bias_mode=0, relu=False, workspace=None):
+    ws = _p(workspace)
+    wsb = workspace.numel() * workspace.element_size() if workspace is not None else 0
+    K.check(_lib().rram_gemm_f32_ex(int(trans_a), int(trans_b), M, N, K_, alpha, _p(A), lda,
+                                    _p(B), ldb, beta, _p(Cm), ldc, _p(bias), bias_mode, int(relu),
+                                    ws, wsb, _stream()), "gemm_ex")
+
+
+def conv_desc(x_shape, num_output, kernel, stride=1, pad=0, dilation=1, group=1):
+    kh, kw = (kernel, kernel) if isinstance(kernel, int) else kernel
+    sh, sw = (stride, stride) if isinstance(stride, int) else stride
+    ph, pw = (pad, pad) if isinstance(pad, int) else pad
+    dh, dw = (dilation, dilation) if isinstance(dilation, int) else dilation
+    n, c, h, w = x_shape
+    d = K.ConvDesc(n, c, h, w, num_output, kh, kw, ph, pw, sh, sw, dh, dw, group, 0, 0)
+    K.check(_lib().rram_conv_out_shape(C.byref(d)), "conv_out_shape")
+    return d
+
+
+def conv2d_fwd(d, x, w, bias, y, relu=False):
+    K.check(_lib().rram_conv2d_fwd(C.byref(d), _p(x), _p(w), _p(bias), _p(y), int(relu),
+                                   _stream()), "conv2d_fwd")
+
+
+def conv2d_bwd(d, x, w, dy, dw=None, db=None, dx=None, workspace=None):
+    wsb = workspace.numel() * workspace.element_size() if workspace is not None else 0
+    K.check(_lib().rram_conv2d_bwd(C.byref(d), _p(x), _p(w), _p(dy), _p(dw), _p(db), _p(dx),
+                                   _p(workspace), wsb, _stream()), "conv2d_bwd")
+
+
+def conv2d_bwd_workspace(d, images):
+    return _lib().rram_conv2d_bwd_workspace(C.byref(d), images)
+
+
+def im2col(im, C_, H, W, kh, kw, ph, pw, sh, sw, dh, dw, col):
+    K.check(_lib().rram_im2col(_p(im), C_, H, W, kh, kw, ph, pw, sh, sw, dh, dw, _p(col),
+                               _stream()), "im2col")
+
+
+def col2im(col, C_, H, W, kh, kw, ph, pw, sh, sw, dh, dw, im):
+    K.check(_lib().rram_col2im(_p(col), C_, H, W, kh, kw, ph, pw, sh, sw, dh, dw, _p(im),
+                               _stream()), "col2im")
+
+
+def ip_fwd(x, w, bias, y, M, N, K_, transpose=False, relu=False, workspace=None):
+    wsb = workspace.numel() * workspace.element_size() if workspace is not None else 0
+    K.check(_lib().rram_ip_fwd(_p(x), _p(w), _p(bias), _p(y), M, N, K_, int(transpose), int(relu),
+                               _p(workspace), wsb, _stream()), "ip_fwd")
+
+
+def ip_bwd(x, w, dy, dw, db, dx, M, N, K_, transpose=False):
+    K.check(_lib().rram_ip_bwd(_p(x), _p(w), _p(dy), _p(dw), _p(db), _p(dx), M, N, K_,
+                               int(transpose), _stream()), "ip_bwd")
+
+
+def pool_fwd(x, y, mask, geom, method):
+    K.check(_lib().rram_pool_fwd(_p(x), _p(y), _p(mask), *geom, method, _stream()), "pool_fwd")
+
+
+def pool_bwd(dy, mask, dx, geom, method):
+    K.check(_lib().rram_pool_bwd(_p(dy), _p(mask), _p(dx), *geom, method, _stream()), "pool_bwd")
+
+
+def lrn_fwd(x, y, scale, n, c, h, w, size, alpha, beta, k):
+    K.check(_lib().rram_lrn_fwd(_p(x), _p(y), _p(scale), n, c, h, w, size, alpha, beta, k,
+                                _stream()), "lrn_fwd")
+
+
+def lrn_bwd(x, y, scale, dy, dx, n, c, h, w, size, alpha, beta):
+    K.check(_lib().rram_lrn_bwd(_p(x), _p(y), _p(scale), _p(dy), _p(dx), n, c, h, w, size, alpha,
+                                beta, _stream()), "lrn_bwd")
+
+
+def softmax_fwd(x, y, outer, channels, inner):
+    K.check(_lib().rram_softmax_fwd(_p(x), _p(y), outer, channels, inner, _stream()), "softmax")
+
+
+def accuracy(x, label, correct, count, outer, channels, inner, top_k=1, ignore=-1):
+    K.check(_lib().rram_accuracy(_p(x), _p(label), _p(correct), _p(count), outer, channels, inner,
+                                 top_k, ignore, _stream()), "accuracy")
+
+
+def fill_uniform(x, lo, hi, seed, sid=0):
+    K.check(_lib().rram_fill_uniform(_p(x), x.numel(), lo, hi, seed, sid, _stream()), "fill")
+
+
+def fill_gaussian(x, mean, std, seed, sid=0):
+    K.check(_lib().rram_fill_gaussian(_p(x), x.numel(), mean, std, seed, sid, _stream()), "fill")

@@ -1,0 +1,67 @@
+"""CPU tests of the drop-in boundary: the C-ABI libraries load and export every
+symbol their headers declare (no compute calls — there is no GPU here)."""
+import ctypes
+import re
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def declared(header: Path):
+    text = header.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rram_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_kernel_header_symbols_exported():
+    from rramsim import _kernels as K
+    lib = K.load()
+    names = declared(ROOT / "include" / "rram_kernels.h")
+    assert len(names) > 40
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    # every declared symbol has a ctypes signature (the Python view is complete)
+    assert sorted(set(names) - set(K.SIGNATURES)) == []
+
+
+def test_kernel_structs_match_header():
+    from rramsim import _kernels as K
+    assert ctypes.sizeof(K.InjectCfg) == 56
+    assert ctypes.sizeof(K.InjectSeg) == 8 + 8 + 8 + 4 + 4 + 56
+    assert ctypes.sizeof(K.FailSeg) == 40
+    assert ctypes.sizeof(K.ConvDesc) == 16 * 4
+
+
+def test_version_and_error_string_callable():
+    from rramsim import _kernels as K
+    lib = K.load()
+    assert lib.rram_kernels_version().startswith(b"rram_kernels")
+    assert isinstance(lib.rram_last_error(), bytes)
+
+
+def test_invalid_args_return_status_not_abort():
+    """Argument validation runs on the host before any launch (no GPU needed)."""
+    from rramsim import _kernels as K
+    lib = K.load()
+    assert lib.rram_fail_apply(None, None, None, None, -1, 100.0, 1e-20, None, None) == K.RRAM_EINVAL
+    assert b"n < 0" in lib.rram_last_error()
+    assert lib.rram_inject_rng(None, None, 10, None, 0, 0, 0, None, None) == K.RRAM_EINVAL
+    d = K.ConvDesc(1, 3, 8, 8, 4, 3, 3, 0, 0, 1, 1, 1, 1, 2, 0, 0)   # 3 % 2 != 0
+    assert lib.rram_conv_out_shape(ctypes.byref(d)) == K.RRAM_EINVAL
+    d = K.ConvDesc(2, 3, 227, 227, 96, 11, 11, 0, 0, 4, 4, 1, 1, 1, 0, 0)
+    assert lib.rram_conv_out_shape(ctypes.byref(d)) == K.RRAM_OK and d.out_h == 55 == d.out_w
+    # zero-size work is a successful no-op that never touches the device
+    assert lib.rram_fail_apply(None, None, None, None, 0, 100.0, 1e-20, None, None) == K.RRAM_OK
+
+
+def test_caffe_header_symbols_exported():
+    hdr = ROOT / "include" / "rram_caffe.h"
+    if not hdr.exists():
+        pytest.skip("host runtime header not present yet")
+    from rramsim import _kernels as K
+    K.load()
+    lib = ctypes.CDLL(str(K.CAFFE_SO))
+    missing = [n for n in declared(hdr) if not hasattr(lib, n)]
+    assert not missing, missing

@@ -1,0 +1,429 @@
+"""GPU parity tests: the HIP kernels through the C-ABI vs the CPU oracle.
+
+Bit-exact for mask application, endurance arithmetic, quantisation and the
+integer RNG decisions; fp32 tolerance (stated per test) for floating-point
+contractions and transcendental-based draws.
+"""
+import json
+import math
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+GOLD = Path(__file__).resolve().parent / "golden"
+
+
+def from_bits(b):
+    return np.array(b, np.uint32).view(np.float32)
+
+
+def T(a, dev):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dev)
+
+
+def N(t):
+    import torch
+    torch.cuda.synchronize()
+    return t.detach().cpu().numpy()
+
+
+def bits_equal(a, b):
+    return np.array_equal(np.asarray(a, np.float32).view(np.uint32),
+                          np.asarray(b, np.float32).view(np.uint32))
+
+
+# ------------------------------------------------------------- fail_apply
+def test_fail_apply_golden_bit_exact(device):
+    from rramsim import ops
+    d = json.loads((GOLD / "fail_apply_kat.json").read_text())
+    for c in d["cases"]:
+        w, e, v = T(from_bits(c["w0_bits"]), device), T(from_bits(c["e0_bits"]), device), \
+            T(from_bits(c["v_bits"]), device)
+        cnt = ops.counters(1, device)
+        for st in c["steps"]:
+            cnt.zero_()
+            ops.fail_apply(T(from_bits(st["dw_bits"]), device), w, e, v, d["decrement"], d["eps"], cnt)
+        assert bits_equal(N(w), from_bits(c["w_bits"]))
+        assert bits_equal(N(e), from_bits(c["e_bits"]))
+        assert int(N(cnt)[0]) == c["broken"]
+
+
+@pytest.mark.parametrize("n", [1, 3, 4097, 1 << 20, 3_000_001])
+def test_fail_apply_random_vs_oracle(device, oracle_mod, n):
+    from rramsim import ops
+    rng = np.random.default_rng(n)
+    e = rng.normal(300, 200, n).astype(np.float32)
+    v = rng.integers(-1, 2, n).astype(np.float32)
+    w = rng.standard_normal(n).astype(np.float32)
+    dw = np.where(rng.random(n) < 0.3, 0.0, rng.standard_normal(n) * 1e-3).astype(np.float32)
+    tw, te = T(w, device), T(e, device)
+    cnt = ops.counters(1, device)
+    for _ in range(3):
+        cnt.zero_()
+        ops.fail_apply(T(dw, device), tw, te, T(v, device), counter=cnt)
+        w, e, nb = oracle_mod.fail_apply(dw, w, e, v)
+    assert bits_equal(N(tw), w) and bits_equal(N(te), e) and int(N(cnt)[0]) == nb
+
+
+def test_fail_apply_batched_unaligned_segments(device, oracle_mod):
+    """Segments at odd float offsets of one flat buffer (the P2PSync-style
+    aliasing of params, parallel.cpp:25-67) take the scalar path."""
+    import torch
+    from rramsim import ops
+    rng = np.random.default_rng(9)
+    sizes = [4096 * 9, 4096, 1001, 1000, 37, 1]
+    tot = sum(sizes) + 1
+    e = rng.normal(150, 100, tot).astype(np.float32)
+    v = rng.integers(-1, 2, tot).astype(np.float32)
+    w = rng.standard_normal(tot).astype(np.float32)
+    dw = rng.standard_normal(tot).astype(np.float32)
+    te, tv, tw, tdw = (T(a, device) for a in (e, v, w, dw))
+    segs, off = [], 1
+    for s in sizes:
+        segs.append((tdw[off:off + s], tw[off:off + s], te[off:off + s], tv[off:off + s]))
+        off += s
+    cnt = ops.counters(len(sizes), device)
+    ops.fail_apply_batched(segs, counters_t=cnt)
+    off = 1
+    for i, s in enumerate(sizes):
+        sl = slice(off, off + s)
+        w2, e2, nb = oracle_mod.fail_apply(dw[sl], w[sl], e[sl], v[sl])
+        w[sl], e[sl] = w2, e2
+        assert int(N(cnt)[i]) == nb
+        off += s
+    assert bits_equal(N(tw), w) and bits_equal(N(te), e)
+
+
+def test_fault_threshold_bit_exact(device, oracle_mod):
+    from rramsim import ops
+    u = np.random.default_rng(2).random(100_003).astype(np.float32)
+    t = T(u, device)
+    ops.fault_threshold(t, 0.25, 0.75)
+    assert bits_equal(N(t), oracle_mod.fault_threshold(u, 0.25, 0.75))
+
+
+def test_fault_init_vs_oracle(device, oracle_mod):
+    import torch
+    from rramsim import ops, split_thresholds
+    n = 200_001
+    tn, tz = split_thresholds(10, 20, 10)
+    e = torch.empty(n, device=device)
+    v = torch.empty(n, device=device)
+    ops.fault_init(e, v, 5e6, 1e6, tn, tz, seed=1701, map_id=0, layer_id=2)
+    e_ref, v_ref = oracle_mod.fault_init(n, 5e6, 1e6, tn, tz, 1701, 0, 2)
+    assert bits_equal(N(v), v_ref)                    # integer RNG decisions: exact
+    np.testing.assert_allclose(N(e), e_ref, rtol=2e-6, atol=2.0)  # logf/sincosf ulps
+
+
+# -------------------------------------------------------------- injection
+def _cfg_pair(p, **kw):
+    from rramsim import make_inject_cfg
+    c = make_inject_cfg(p, **kw)
+    import oracle
+    oc = oracle.InjectCfg(c.thr_fault, c.thr_neg, c.thr_zero, c.thr_sa1, c.stuck_scale, c.g_max,
+                          c.quant_levels, c.var_sigma, c.cell_mode, 0)
+    return c, oc
+
+
+@pytest.mark.parametrize("n", [1, 2, 7, 4096, 100_003, 4096 * 1000 + 3])
+@pytest.mark.parametrize("mode", ["stuck", "quant", "stuck_scaled"])
+def test_inject_bit_exact_vs_oracle(device, oracle_mod, n, mode):
+    import torch
+    from rramsim import ops
+    kw = {"stuck": {}, "quant": dict(quant_levels=32, g_max=0.08),
+          "stuck_scaled": dict(stuck_scale=0.05)}[mode]
+    c, oc = _cfg_pair(0.05, neg=5, zero=90, pos=5, **kw)
+    src = (np.random.default_rng(n).standard_normal(n) * 0.02).astype(np.float32)
+    ts = T(src, device)
+    out = torch.empty_like(ts)
+    cnt = ops.counters(1, device)
+    ops.inject(ts, out, c, seed=1701, map_id=3, layer_id=5, counter=cnt)
+    ref, nb = oracle_mod.inject(src, oc, 1701, 3, 5)
+    assert bits_equal(N(out), ref)
+    assert int(N(cnt)[0]) == nb
+
+
+@pytest.mark.parametrize("mode", ["var", "quant_var", "pair", "pair_quant_var"])
+def test_inject_extensions_vs_oracle(device, oracle_mod, mode):
+    import torch
+    from rramsim import ops
+    kw = {"var": dict(var_sigma=0.1), "quant_var": dict(quant_levels=16, g_max=0.1, var_sigma=0.05),
+          "pair": dict(cell_mode=1, g_max=0.1, p_sa1=0.3),
+          "pair_quant_var": dict(cell_mode=1, g_max=0.1, quant_levels=8, var_sigma=0.1)}[mode]
+    c, oc = _cfg_pair(0.02, **kw)
+    n = 65_537
+    src = (np.random.default_rng(11).standard_normal(n) * 0.03).astype(np.float32)
+    ts = T(src, device)
+    out = torch.empty_like(ts)
+    cnt = ops.counters(1, device)
+    ops.inject(ts, out, c, seed=99, map_id=1, layer_id=0, counter=cnt)
+    ref, nb = oracle_mod.inject(src, oc, 99, 1, 0)
+    assert int(N(cnt)[0]) == nb                         # decisions are integer-exact
+    np.testing.assert_allclose(N(out), ref, rtol=1e-5, atol=1e-7)  # expf/logf ulps
+
+
+def test_inject_batched_alexnet_sizes_binomial(device):
+    """Full AlexNet IP sizes (fc6/fc7/fc8 + biases, 58,631,144 weights): the
+    broken fraction of each blob inside the 3.8-sigma binomial CI
+    (test_random_number_generator.cpp:17-19 pattern), untouched weights
+    unchanged, stuck values in {-1, 0, +1}."""
+    import torch
+    from rramsim import ops, make_inject_cfg
+    shapes = [(4096, 9216), (4096,), (4096, 4096), (4096,), (1000, 4096), (1000,)]
+    p = 0.01
+    c = make_inject_cfg(p, 10, 20, 10)
+    segs, srcs, outs = [], [], []
+    g = torch.Generator(device=device).manual_seed(0)
+    for i, sh in enumerate(shapes):
+        s = torch.rand(sh, device=device, generator=g) * 0.5 + 2.0   # never in {-1,0,1}
+        o = torch.empty_like(s)
+        srcs.append(s)
+        outs.append(o)
+        segs.append((s, o, i, c))
+    cnt = ops.counters(len(shapes), device)
+    ops.inject_batched(segs, seed=1701, map_id=42, counters_t=cnt)
+    torch.cuda.synchronize()
+    counts = cnt.cpu().numpy()
+    for i, (s, o) in enumerate(zip(srcs, outs)):
+        changed = (o != s)
+        nb = int(changed.sum())
+        assert nb == counts[i]
+        n = s.numel()
+        assert abs(nb / n - p) <= 3.8 * math.sqrt(p * (1 - p) / n) + 1.0 / n
+        vals = o[changed]
+        assert bool(((vals == -1) | (vals == 0) | (vals == 1)).all())
+    # -1/0/+1 split over all broken cells: 1/4, 1/2, 1/4
+    allv = torch.cat([o[o != s] for s, o in zip(srcs, outs)])
+    for val, q in ((-1, 0.25), (0, 0.5), (1, 0.25)):
+        frac = float((allv == val).float().mean())
+        assert abs(frac - q) <= 3.8 * math.sqrt(q * (1 - q) / allv.numel())
+
+
+def test_inject_maps_independent_and_deterministic(device):
+    import torch
+    from rramsim import ops, make_inject_cfg
+    c = make_inject_cfg(0.1)
+    s = torch.full((1 << 20,), 5.0, device=device)
+    a, b, a2 = torch.empty_like(s), torch.empty_like(s), torch.empty_like(s)
+    ops.inject(s, a, c, 1, 0, 0)
+    ops.inject(s, b, c, 1, 1, 0)
+    ops.inject(s, a2, c, 1, 0, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(a, a2)
+    ma, mb = (a != 5), (b != 5)
+    both = float((ma & mb).float().mean())
+    assert abs(both - 0.01) < 0.002      # independent maps: P(both) = p^2
+
+
+# -------------------------------------------------- threshold / SGD / fused
+def test_threshold_strategy_bit_exact(device, oracle_mod):
+    from rramsim import ops
+    dw = (np.random.default_rng(4).standard_normal(300_001) * 1e-3).astype(np.float32)
+    t = T(dw, device)
+    cnt = ops.counters(1, device)
+    ops.threshold_strategy(t, 5e-4, cnt)
+    ref, n = oracle_mod.threshold(dw, 5e-4)
+    assert bits_equal(N(t), ref) and int(N(cnt)[0]) == n
+
+
+def test_sgd_update_and_fused_tail(device, oracle_mod):
+    from rramsim import ops
+    rng = np.random.default_rng(8)
+    n = 100_000
+    w, g, h = (rng.standard_normal(n).astype(np.float32) for _ in range(3))
+    e = rng.normal(150, 100, n).astype(np.float32)
+    v = rng.integers(-1, 2, n).astype(np.float32)
+    tg, th = T(g, device), T(h, device)
+    ops.sgd_update(tg, th, 0.9, 0.01)
+    g2, h2 = oracle_mod.sgd_update(g, h, 0.9, 0.01)
+    np.testing.assert_allclose(N(tg), g2, rtol=1e-6, atol=1e-7)   # fma contraction allowed
+    tw, tg, th, te = T(w, device), T(g, device), T(h, device), T(e, device)
+    cnt = ops.counters(1, device)
+    ops.fused_update_fail(tw, tg, th, te, T(v, device), 0.004, 0.9, 0.01, True, 1e-3, counter=cnt)
+    w3, g3, h3, e3, nb = oracle_mod.fused_update_fail(w, g, h, e, v, 0.004, 0.9, 0.01, True, 1e-3)
+    np.testing.assert_allclose(N(tw), w3, rtol=1e-5, atol=1e-6)
+    # endurance decisions may flip only where |g| sits within rounding of thr / eps
+    assert abs(int(N(cnt)[0]) - nb) <= 2
+
+
+# ------------------------------------------------------------------ GEMM
+def test_gemm_kat_exact(device):
+    import torch
+    from rramsim import ops
+    d = json.loads((GOLD / "gemm_kat.json").read_text())
+    A, B, AT, BT = (T(np.array(d[k], np.float32), device) for k in ("A", "B", "A_T", "B_T"))
+    ref = np.array(d["C"], np.float32).reshape(2, 4)
+    for ta, tb, a, b in ((0, 0, A, B), (1, 0, AT, B), (1, 1, AT, BT), (0, 1, A, BT)):
+        C = torch.full((2, 4), 7.0, device=device)
+        ops.gemm(ta, tb, 2, 4, 3, 1.0, a, b, 0.0, C)
+        assert np.array_equal(N(C), ref), (ta, tb)
+
+
+def _gemm_ref(ta, tb, A, B):
+    a = A.T if ta else A
+    b = B.T if tb else B
+    return a.astype(np.float64) @ b.astype(np.float64), np.abs(a).astype(np.float64) @ np.abs(b)
+
+
+@pytest.mark.parametrize("shape", [(1, 1, 1), (31, 33, 17), (128, 128, 16), (200, 300, 1000),
+                                   (256, 1000, 4096), (96, 3025, 363), (7, 5000, 3)])
+@pytest.mark.parametrize("tt", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_gemm_random_vs_fp64(device, shape, tt):
+    import torch
+    from rramsim import ops
+    M, Nn, K = shape
+    ta, tb = tt
+    rng = np.random.default_rng(M * 7 + Nn + K)
+    A = rng.standard_normal((K, M) if ta else (M, K)).astype(np.float32)
+    B = rng.standard_normal((Nn, K) if tb else (K, Nn)).astype(np.float32)
+    C0 = rng.standard_normal((M, Nn)).astype(np.float32)
+    tc = T(C0, device)
+    ops.gemm(ta, tb, M, Nn, K, 0.5, T(A, device), T(B, device), 1.5, tc)
+    ref, scale = _gemm_ref(ta, tb, A, B)
+    ref = 0.5 * ref + 1.5 * C0
+    err = np.abs(N(tc) - ref)
+    assert np.all(err <= 1e-5 * (0.5 * scale + 1.5 * np.abs(C0)) + 1e-6)   # fp32, 1e-5 of sum|a*b|
+
+
+def test_gemm_epilogue_and_splitk(device):
+    import torch
+    from rramsim import ops
+    rng = np.random.default_rng(17)
+    M, Nn, K = 256, 1000, 4096          # AlexNet fc8 shape: split-K path
+    X = rng.standard_normal((M, K)).astype(np.float32)
+    W = rng.standard_normal((Nn, K)).astype(np.float32) * 0.01
+    b = rng.standard_normal(Nn).astype(np.float32)
+    ws = torch.empty(64 << 20, dtype=torch.uint8, device=device)
+    out = torch.empty(M, Nn, device=device)
+    ops.gemm_ex(0, 1, M, Nn, K, 1.0, T(X, device), K, T(W, device), K, 0.0, out, Nn,
+                T(b, device), 2, True, ws)
+    ref = np.maximum(X.astype(np.float64) @ W.T.astype(np.float64) + b, 0)
+    scale = np.abs(X) @ np.abs(W.T) + np.abs(b)
+    assert np.all(np.abs(N(out) - ref) <= 1e-5 * scale + 1e-6)
+    out2 = torch.empty(M, Nn, device=device)
+    ops.ip_fwd(T(X, device), T(W, device), T(b, device), out2, M, Nn, K, relu=True)
+    assert np.all(np.abs(N(out2) - ref) <= 1e-5 * scale + 1e-6)
+
+
+# ------------------------------------------------------------------ conv
+CONV_CASES = [
+    dict(x=(2, 3, 6, 4), cout=4, k=3, s=2, p=0, d=1, g=1),
+    dict(x=(2, 3, 6, 4), cout=3, k=3, s=2, p=0, d=1, g=3),
+    dict(x=(2, 3, 6, 4), cout=4, k=1, s=1, p=0, d=1, g=1),
+    dict(x=(2, 3, 8, 7), cout=4, k=3, s=1, p=0, d=2, g=1),
+    dict(x=(2, 3, 227, 227), cout=96, k=11, s=4, p=0, d=1, g=1),   # AlexNet conv1, 2 images
+    dict(x=(2, 96, 27, 27), cout=256, k=5, s=1, p=2, d=1, g=2),    # conv2
+    dict(x=(2, 256, 13, 13), cout=384, k=3, s=1, p=1, d=1, g=1),   # conv3
+    dict(x=(3, 384, 13, 13), cout=384, k=3, s=1, p=1, d=1, g=2),   # conv4
+    dict(x=(4, 32, 16, 16), cout=32, k=5, s=1, p=2, d=1, g=1),     # CIFAR conv2
+    dict(x=(5, 480, 14, 14), cout=64, k=1, s=1, p=0, d=1, g=1),    # GoogLeNet 1x1
+]
+
+
+@pytest.mark.parametrize("cs", CONV_CASES)
+def test_conv_fwd_vs_oracle(device, oracle_mod, cs):
+    import torch
+    from rramsim import ops
+    rng = np.random.default_rng(1701)
+    x = rng.standard_normal(cs["x"]).astype(np.float32)
+    w = (rng.standard_normal((cs["cout"], cs["x"][1] // cs["g"], cs["k"], cs["k"])) * 0.1).astype(np.float32)
+    b = rng.standard_normal(cs["cout"]).astype(np.float32)
+    d = ops.conv_desc(cs["x"], cs["cout"], cs["k"], cs["s"], cs["p"], cs["d"], cs["g"])
+    y = torch.empty((cs["x"][0], cs["cout"], d.out_h, d.out_w), device=device)
+    ops.conv2d_fwd(d, T(x, device), T(w, device), T(b, device), y)
+    if np.prod(cs["x"]) * cs["cout"] * cs["k"] ** 2 < 5e7:
+        ref = oracle_mod.conv_naive(x, w, b, cs["s"], cs["p"], cs["d"], cs["g"])
+    else:
+        ref = oracle_mod.conv_im2col(x, w, b, cs["s"], cs["p"], cs["d"], cs["g"])
+    np.testing.assert_allclose(N(y), ref, atol=1e-4, rtol=1e-4)   # test_convolution_layer.cpp:256
+    # fused ReLU epilogue
+    ops.conv2d_fwd(d, T(x, device), T(w, device), T(b, device), y, relu=True)
+    np.testing.assert_allclose(N(y), np.maximum(ref, 0), atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("cs", CONV_CASES[:4] + [CONV_CASES[8]])
+def test_conv_bwd_vs_torch(device, cs):
+    import torch
+    from rramsim import ops
+    torch.manual_seed(0)
+    x = torch.randn(cs["x"], dtype=torch.float32)
+    w = torch.randn(cs["cout"], cs["x"][1] // cs["g"], cs["k"], cs["k"]) * 0.1
+    b = torch.randn(cs["cout"])
+    xr, wr, br = (t.clone().requires_grad_(True) for t in (x, w, b))
+    yr = torch.nn.functional.conv2d(xr, wr, br, cs["s"], cs["p"], cs["d"], cs["g"])
+    dy = torch.randn_like(yr)
+    yr.backward(dy)
+    d = ops.conv_desc(cs["x"], cs["cout"], cs["k"], cs["s"], cs["p"], cs["d"], cs["g"])
+    dw = torch.zeros_like(w, device=device)
+    db = torch.zeros_like(b, device=device)
+    dx = torch.empty_like(x, device=device)
+    ws = torch.empty(ops.conv2d_bwd_workspace(d, 2) // 4 + 1, device=device)   # forces chunking
+    ops.conv2d_bwd(d, x.to(device), w.to(device), dy.to(device), dw, db, dx, ws)
+    torch.cuda.synchronize()
+    for got, ref in ((dw, wr.grad), (db, br.grad), (dx, xr.grad)):
+        np.testing.assert_allclose(got.cpu().numpy(), ref.numpy(), atol=1e-3, rtol=1e-4)
+
+
+def test_ip_bwd_vs_torch(device):
+    import torch
+    from rramsim import ops
+    torch.manual_seed(1)
+    M, Nn, K = 64, 500, 800                  # LeNet ip1
+    x, w, b = torch.randn(M, K), torch.randn(Nn, K) * 0.05, torch.randn(Nn)
+    xr, wr, br = (t.clone().requires_grad_(True) for t in (x, w, b))
+    y = xr @ wr.T + br
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    dw = torch.zeros(Nn, K, device=device)
+    db = torch.zeros(Nn, device=device)
+    dx = torch.empty(M, K, device=device)
+    ops.ip_bwd(x.to(device), w.to(device), dy.to(device), dw, db, dx, M, Nn, K)
+    torch.cuda.synchronize()
+    for got, ref in ((dw, wr.grad), (db, br.grad), (dx, xr.grad)):
+        np.testing.assert_allclose(got.cpu().numpy(), ref.numpy(), atol=1e-3, rtol=1e-4)
+
+
+def test_im2col_col2im_vs_oracle(device, oracle_mod):
+    import torch
+    from rramsim import ops
+    im = np.random.default_rng(3).standard_normal((5, 15, 15)).astype(np.float32)
+    ref = oracle_mod.im2col(im, 3, 3, 0, 0, 2, 2, 3, 3)           # test_im2col_kernel.cu:36-62
+    col = torch.empty(ref.shape, device=device)
+    ops.im2col(T(im, device), 5, 15, 15, 3, 3, 0, 0, 2, 2, 3, 3, col)
+    assert bits_equal(N(col), ref)
+    back = torch.empty((5, 15, 15), device=device)
+    ops.col2im(col, 5, 15, 15, 3, 3, 0, 0, 2, 2, 3, 3, back)
+    np.testing.assert_allclose(N(back), oracle_mod.col2im(ref, 5, 15, 15, 3, 3, 0, 0, 2, 2, 3, 3),
+                               rtol=1e-6, atol=1e-6)
+
+
+# ---------------------------------------------------------- support layers
+def test_pool_lrn_softmax_accuracy_vs_oracle(device, oracle_mod):
+    import torch
+    from rramsim import ops
+    rng = np.random.default_rng(6)
+    x = rng.standard_normal((3, 8, 13, 13)).astype(np.float32)
+    for method, k, s, p in (("MAX", 3, 2, 0), ("AVE", 3, 2, 1), ("MAX", 2, 2, 0), ("AVE", 5, 3, 0)):
+        ref = oracle_mod.pool(x, k, s, p, method)
+        y = torch.empty(ref.shape, device=device)
+        mask = torch.empty(ref.shape, dtype=torch.int32, device=device)
+        geom = (3, 8, 13, 13, ref.shape[2], ref.shape[3], k, k, s, s, p, p)
+        ops.pool_fwd(T(x, device), y, mask, geom, 0 if method == "MAX" else 1)
+        np.testing.assert_allclose(N(y), ref, rtol=1e-6, atol=1e-6)
+    ref = oracle_mod.lrn(x, 5, 1e-4, 0.75, 1.0)
+    y = torch.empty_like(T(x, device))
+    ops.lrn_fwd(T(x, device), y, None, 3, 8, 13, 13, 5, 1e-4, 0.75, 1.0)
+    np.testing.assert_allclose(N(y), ref, rtol=1e-5, atol=1e-6)
+    logits = rng.standard_normal((256, 1000)).astype(np.float32)
+    pr = torch.empty(256, 1000, device=device)
+    ops.softmax_fwd(T(logits, device), pr, 256, 1000, 1)
+    np.testing.assert_allclose(N(pr), oracle_mod.softmax(logits), rtol=1e-5, atol=1e-7)
+    label = rng.integers(0, 1000, 256).astype(np.float32)
+    logits[:, 5] = logits[:, 7]                       # ties exercise the pair ordering
+    cor, cnt = torch.zeros(1, device=device), torch.zeros(1, device=device)
+    for k in (1, 5):
+        ops.accuracy(T(logits, device), T(label, device), cor, cnt, 256, 1000, 1, top_k=k)
+        assert int(N(cor)[0]) == oracle_mod.accuracy(logits, label, k) and int(N(cnt)[0]) == 256
