@@ -315,10 +315,11 @@ int rram_softmax_loss_bwd(const float* prob, const float* label, float* dx,
                           int outer, int channels, int inner, int ignore_label,
                           float loss_weight, rram_stream_t s);
 /* Top-k accuracy (accuracy_layer.cpp:48-90): correct_out[0] = #correct,
- * count_out[0] = #counted (device floats). */
+ * count_out[0] = #counted, ratio_out[0] (nullable) = #correct / #counted
+ * (device floats; the layer's top). */
 int rram_accuracy(const float* x, const float* label, float* correct_out,
-                  float* count_out, int outer, int channels, int inner,
-                  int top_k, int ignore_label, rram_stream_t s);
+                  float* count_out, float* ratio_out, int outer, int channels,
+                  int inner, int top_k, int ignore_label, rram_stream_t s);
 /* Concat along axis 1 (copy one bottom into its slot). */
 int rram_concat_copy(const float* src, float* dst, int num, int src_channels_x_inner,
                      int dst_channels_x_inner, int offset_x_inner, int backward,

@@ -247,8 +247,8 @@ __global__ void k_count_valid(const float* __restrict__ label, int64_t n, int ig
 // pair is within the top_k of the descending pair order.
 __global__ void __launch_bounds__(1024) k_accuracy(const float* __restrict__ x,
                                                    const float* __restrict__ label, float* correct,
-                                                   float* count, int outer, int C, int inner,
-                                                   int top_k, int ignore) {
+                                                   float* count, float* ratio, int outer, int C,
+                                                   int inner, int top_k, int ignore) {
   __shared__ float sa[16], sc[16];
   float acc = 0.0f, cnt = 0.0f;
   const int64_t cols = (int64_t)outer * inner;
@@ -284,6 +284,7 @@ __global__ void __launch_bounds__(1024) k_accuracy(const float* __restrict__ x,
     }
     correct[0] = A;
     count[0] = N;
+    if (ratio) ratio[0] = A / fmaxf(N, 1.0f);
   }
 }
 
@@ -414,13 +415,13 @@ int rram_softmax_loss_bwd(const float* prob, const float* label, float* dx, int 
   return launch_status("softmax_loss_bwd");
 }
 
-int rram_accuracy(const float* x, const float* label, float* correct, float* count, int outer,
-                  int C, int inner, int top_k, int ignore, rram_stream_t s) {
+int rram_accuracy(const float* x, const float* label, float* correct, float* count, float* ratio,
+                  int outer, int C, int inner, int top_k, int ignore, rram_stream_t s) {
   RRAM_REQUIRE(outer >= 0 && C > 0 && inner > 0 && top_k >= 1 && correct && count,
                "accuracy: bad args");
   RRAM_REQUIRE(outer == 0 || (x && label), "accuracy: NULL");
   hipLaunchKernelGGL(k_accuracy, dim3(1), dim3(1024), 0, as_stream(s), x, label, correct, count,
-                     outer, C, inner, top_k, ignore);
+                     ratio, outer, C, inner, top_k, ignore);
   return launch_status("accuracy");
 }
 

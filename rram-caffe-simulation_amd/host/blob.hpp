@@ -1,0 +1,83 @@
+// SyncedMemory + Blob: the reference's lazy host/device mirror
+// (include/caffe/syncedmem.hpp:45-83, src/caffe/syncedmem.cpp:25-153;
+// include/caffe/blob.hpp:209-274).  Device-resident by default: a host mirror
+// is only materialised when cpu_data() is asked for, so the fault path never
+// ping-pongs.  set_gpu_data() borrows external memory,
+// which is how parameters are aliased into one flat buffer for data-parallel
+// gradient all-reduce (parallel.cpp:25-115).
+#pragma once
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+
+namespace caffe {
+
+class SyncedMemory {
+ public:
+  enum SyncedHead { UNINITIALIZED, HEAD_AT_CPU, HEAD_AT_GPU, SYNCED };
+  explicit SyncedMemory(size_t size = 0) : size_(size) {}
+  ~SyncedMemory();
+  SyncedMemory(const SyncedMemory&) = delete;
+  SyncedMemory& operator=(const SyncedMemory&) = delete;
+
+  const void* cpu_data();
+  const void* gpu_data();
+  void* mutable_cpu_data();
+  void* mutable_gpu_data();
+  void set_cpu_data(void* data);   // borrow host memory
+  void set_gpu_data(void* data);   // borrow device memory
+  SyncedHead head() const { return head_; }
+  size_t size() const { return size_; }
+
+ private:
+  void to_cpu();
+  void to_gpu();
+  void* cpu_ptr_ = nullptr;
+  void* gpu_ptr_ = nullptr;
+  size_t size_;
+  SyncedHead head_ = UNINITIALIZED;
+  bool own_cpu_ = false, own_gpu_ = false;
+};
+
+template <typename Dtype>
+class Blob {
+ public:
+  Blob() = default;
+  explicit Blob(const std::vector<int>& shape) { Reshape(shape); }
+  void Reshape(const std::vector<int>& shape);
+  void ReshapeLike(const Blob& o) { Reshape(o.shape()); }
+  const std::vector<int>& shape() const { return shape_; }
+  int shape(int i) const { return shape_[i < 0 ? i + (int)shape_.size() : i]; }
+  int num_axes() const { return static_cast<int>(shape_.size()); }
+  int64_t count() const { return count_; }
+  int64_t count(int start, int end = -1) const;
+  std::string shape_string() const;
+
+  const Dtype* cpu_data() const { return static_cast<const Dtype*>(data_->cpu_data()); }
+  const Dtype* gpu_data() const { return static_cast<const Dtype*>(data_->gpu_data()); }
+  const Dtype* cpu_diff() const { return static_cast<const Dtype*>(diff_->cpu_data()); }
+  const Dtype* gpu_diff() const { return static_cast<const Dtype*>(diff_->gpu_data()); }
+  Dtype* mutable_cpu_data() { return static_cast<Dtype*>(data_->mutable_cpu_data()); }
+  Dtype* mutable_gpu_data() { return static_cast<Dtype*>(data_->mutable_gpu_data()); }
+  Dtype* mutable_cpu_diff() { return static_cast<Dtype*>(diff_->mutable_cpu_data()); }
+  Dtype* mutable_gpu_diff() { return static_cast<Dtype*>(diff_->mutable_gpu_data()); }
+  void set_gpu_data(Dtype* p) { data_->set_gpu_data(p); }
+  void set_gpu_diff(Dtype* p) { diff_->set_gpu_data(p); }
+
+  // data -= diff (blob.cpp:156-179, caffe_gpu_axpy(-1))
+  void Update();
+  void ShareData(const Blob& o) { data_ = o.data_; }
+  void ShareDiff(const Blob& o) { diff_ = o.diff_; }
+  const std::shared_ptr<SyncedMemory>& data() const { return data_; }
+  const std::shared_ptr<SyncedMemory>& diff() const { return diff_; }
+
+ private:
+  std::vector<int> shape_;
+  int64_t count_ = 0, capacity_ = 0;
+  std::shared_ptr<SyncedMemory> data_, diff_;
+};
+
+}  // namespace caffe

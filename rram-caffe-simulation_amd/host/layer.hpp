@@ -1,0 +1,124 @@
+// Layer<Dtype> plugin API (include/caffe/layer.hpp:33-445) and the layer
+// registry (layer_factory.hpp:127-135).  Public non-virtual SetUp / Forward /
+// Backward; protected virtual LayerSetUp / Reshape / Forward_gpu /
+// Backward_gpu.  This build is device-only: Forward_cpu/Backward_cpu are not
+// part of the product (the CPU restatement lives in oracle/ as a checker).
+#pragma once
+
+#include <functional>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "blob.hpp"
+#include "proto.hpp"
+
+namespace caffe {
+
+template <typename Dtype>
+class Net;
+
+template <typename Dtype>
+class Layer {
+ public:
+  explicit Layer(const Msg& param) : layer_param_(param) {
+    phase_ = param.str("phase", "TRAIN") == "TEST" ? TEST : TRAIN;
+  }
+  virtual ~Layer() = default;
+
+  void SetUp(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) {
+    CheckBlobCounts(bottom, top);
+    LayerSetUp(bottom, top);
+    Reshape(bottom, top);
+    SetLossWeights(top);
+  }
+  virtual void LayerSetUp(const std::vector<Blob<Dtype>*>&, const std::vector<Blob<Dtype>*>&) {}
+  virtual void Reshape(const std::vector<Blob<Dtype>*>& bottom,
+                       const std::vector<Blob<Dtype>*>& top) = 0;
+
+  // layer.hpp:451-487: Reshape -> Forward_gpu -> loss = sum(top * loss_weight)
+  Dtype Forward(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top);
+  void Backward(const std::vector<Blob<Dtype>*>& top, const std::vector<bool>& propagate_down,
+                const std::vector<Blob<Dtype>*>& bottom) {
+    Backward_gpu(top, propagate_down, bottom);
+  }
+
+  std::vector<std::shared_ptr<Blob<Dtype>>>& blobs() { return blobs_; }
+  const Msg& layer_param() const { return layer_param_; }
+  std::string name() const { return layer_param_.str("name"); }
+  virtual const char* type() const = 0;
+  virtual int ExactNumBottomBlobs() const { return -1; }
+  virtual int MinBottomBlobs() const { return -1; }
+  virtual int ExactNumTopBlobs() const { return -1; }
+  virtual int MinTopBlobs() const { return -1; }
+  virtual bool EqualNumBottomTopBlobs() const { return false; }
+  virtual bool AllowForceBackward(int) const { return true; }
+  virtual bool IsLoss() const { return false; }
+
+  Dtype loss(int top_index) const {
+    return top_index < (int)loss_.size() ? loss_[top_index] : Dtype(0);
+  }
+  void set_loss(int top_index, Dtype v) {
+    if ((int)loss_.size() <= top_index) loss_.resize(top_index + 1, Dtype(0));
+    loss_[top_index] = v;
+  }
+  bool param_propagate_down(int i) const {
+    return i < (int)param_propagate_down_.size() ? param_propagate_down_[i] : false;
+  }
+  void set_param_propagate_down(int i, bool v) {
+    if ((int)param_propagate_down_.size() <= i) param_propagate_down_.resize(i + 1, true);
+    param_propagate_down_[i] = v;
+  }
+  Phase phase() const { return phase_; }
+  void set_phase(Phase p) { phase_ = p; }
+  // per-layer id used to decorrelate RNG streams (dropout, fillers)
+  uint32_t layer_id = 0;
+  uint64_t iter = 0;
+
+ protected:
+  virtual void Forward_gpu(const std::vector<Blob<Dtype>*>& bottom,
+                           const std::vector<Blob<Dtype>*>& top) = 0;
+  virtual void Backward_gpu(const std::vector<Blob<Dtype>*>& top,
+                            const std::vector<bool>& propagate_down,
+                            const std::vector<Blob<Dtype>*>& bottom) = 0;
+  void CheckBlobCounts(const std::vector<Blob<Dtype>*>& bottom,
+                       const std::vector<Blob<Dtype>*>& top);
+  void SetLossWeights(const std::vector<Blob<Dtype>*>& top);
+
+  Msg layer_param_;
+  Phase phase_;
+  std::vector<std::shared_ptr<Blob<Dtype>>> blobs_;
+  std::vector<bool> param_propagate_down_;
+  std::vector<Dtype> loss_;
+};
+
+// ------------------------------------------------------------ registry
+template <typename Dtype>
+class LayerRegistry {
+ public:
+  using Creator = std::function<std::shared_ptr<Layer<Dtype>>(const Msg&)>;
+  static std::map<std::string, Creator>& Registry();
+  static void AddCreator(const std::string& type, Creator c) { Registry()[type] = std::move(c); }
+  static std::shared_ptr<Layer<Dtype>> CreateLayer(const Msg& param);
+  static std::vector<std::string> LayerTypeList();
+};
+
+template <typename Dtype>
+struct LayerRegisterer {
+  LayerRegisterer(const std::string& type, typename LayerRegistry<Dtype>::Creator c) {
+    LayerRegistry<Dtype>::AddCreator(type, std::move(c));
+  }
+};
+
+#define REGISTER_LAYER_CLASS(type)                                                  \
+  static ::caffe::LayerRegisterer<float> g_creator_f_##type(                        \
+      #type, [](const ::caffe::Msg& p) -> std::shared_ptr<::caffe::Layer<float>> {  \
+        return std::make_shared<type##Layer<float>>(p);                             \
+      })
+
+// Fill a parameter blob from a FillerParameter message (filler.hpp):
+// constant / gaussian / uniform / xavier / msra, seeded counter RNG.
+void FillBlob(Blob<float>* blob, const Msg& filler, uint64_t seed, uint32_t stream_id);
+
+}  // namespace caffe

@@ -24,7 +24,7 @@ def _p(t):
         return None
     if not t.is_cuda:
         raise K.RramError("rramsim ops take device tensors (no CPU fallback)")
-    if t.dtype not in (torch.float32, torch.int32, torch.int64, torch.uint64):
+    if t.dtype not in (torch.float32, torch.int32, torch.int64, torch.uint64, torch.uint8):
         raise K.RramError(f"unsupported dtype {t.dtype}")
     return C.c_void_p(t.data_ptr())
 
@@ -184,9 +184,9 @@ def softmax_fwd(x, y, outer, channels, inner):
     K.check(_lib().rram_softmax_fwd(_p(x), _p(y), outer, channels, inner, _stream()), "softmax")
 
 
-def accuracy(x, label, correct, count, outer, channels, inner, top_k=1, ignore=-1):
-    K.check(_lib().rram_accuracy(_p(x), _p(label), _p(correct), _p(count), outer, channels, inner,
-                                 top_k, ignore, _stream()), "accuracy")
+def accuracy(x, label, correct, count, outer, channels, inner, top_k=1, ignore=-1, ratio=None):
+    K.check(_lib().rram_accuracy(_p(x), _p(label), _p(correct), _p(count), _p(ratio), outer,
+                                 channels, inner, top_k, ignore, _stream()), "accuracy")
 
 
 def fill_uniform(x, lo, hi, seed, sid=0):
