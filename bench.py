@@ -1,0 +1,239 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Monte-Carlo fault-map inference, AlexNet b256.
+
+One step = one fault map on every rank: inject a fresh stuck-at fault map into
+the clean InnerProduct weights (counter-based RNG, HBM-bound kernel), then run
+the full AlexNet forward over the 256-image eval batch (implicit-GEMM conv and
+IP GEMMs on fp32 MFMA, LRN/pool/softmax/accuracy), accumulating accuracy and
+loss on the device.  Maps are sharded across ranks (map m on rank m mod N; no
+data-path collective); one RCCL all-reduce of the statistics closes the job.
+
+Prints ONE JSON line (rank 0):
+  value = images classified under faults per second, summed over ranks
+  roofline = the conv/IP GEMMs (dominant kernels) vs the fp32 MFMA peak
+  roofline_inject = the injection kernel vs HBM peak
+  cpu_baseline = Caffe CPU mode restated (per-image im2col + OpenBLAS sgemm,
+                 oracle fault injection) on a bounded sample, rank 0 at N=1.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]
+        torchrun --nproc-per-node N bench.py --gpus N ...  (one rank per GPU, RCCL)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "rram-caffe-simulation_amd" / "python"))
+
+MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 MFMA = fp32 vector peak (dense)
+HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
+
+
+def conv_ip_flops(layers_desc, batch):
+    """Algorithmic FLOPs (2*M*N*K summed over conv incl. groups + IP) per batch."""
+    return sum(d["flops"] for d in layers_desc) * 1.0
+
+
+def alexnet_gemm_table(batch):
+    """(layer, FLOPs per batch) for AlexNet at 227x227."""
+    convs = [("conv1", 96, 3, 11, 55, 1), ("conv2", 256, 96, 5, 27, 2), ("conv3", 384, 256, 3, 13, 1),
+             ("conv4", 384, 384, 3, 13, 2), ("conv5", 256, 384, 3, 13, 2)]
+    t = {}
+    for name, co, ci, k, o, g in convs:
+        t[name] = 2.0 * batch * co * o * o * (ci // g) * k * k
+    for name, n, k in (("fc6", 4096, 9216), ("fc7", 4096, 4096), ("fc8", 1000, 4096)):
+        t[name] = 2.0 * batch * n * k
+    return t
+
+
+def cpu_baseline(batch, p_fault, seed, budget_s=12.0):
+    """Caffe CPU mode (restated in oracle/): per-image im2col + sgemm on
+    numpy's OpenBLAS, scalar C fault injection.  Bounded sample: one fault map
+    injected into all 58.6M IP weights, then as many single-image forwards as
+    fit in ~budget_s; images/s extrapolated to a 256-image map."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import numpy as np
+    import oracle
+    from rramsim import make_inject_cfg
+
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("internal_api") == "openblas"]
+                      or [1])
+    except Exception:  # pragma: no cover
+        threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    rng = np.random.default_rng(seed)
+    W = {"conv1": (96, 3, 11), "conv2": (256, 48, 5), "conv3": (384, 256, 3), "conv4": (384, 192, 3),
+         "conv5": (256, 192, 3)}
+    w = {k: (rng.standard_normal((co, ci, kk, kk)) * 0.01).astype(np.float32) for k, (co, ci, kk) in W.items()}
+    b = {k: np.zeros(W[k][0], np.float32) for k in W}
+    fc = {"fc6": (4096, 9216), "fc7": (4096, 4096), "fc8": (1000, 4096)}
+    fw = {k: (rng.standard_normal(s) * 0.005).astype(np.float32) for k, s in fc.items()}
+    fb = {k: np.full(s[0], 0.1, np.float32) for k, s in fc.items()}
+    c = make_inject_cfg(p_fault)
+    oc = oracle.InjectCfg(c.thr_fault, c.thr_neg, c.thr_zero, c.thr_sa1, 1.0, 0.0, 0, 0.0, 0, 0)
+    t0 = time.perf_counter()
+    lid = 0
+    for k in fc:
+        fw[k], _ = oracle.inject(fw[k], oc, seed, 0, lid)
+        fb[k], _ = oracle.inject(fb[k], oc, seed, 0, lid + 1)
+        lid += 2
+    t_inject = time.perf_counter() - t0
+    x_all = (rng.integers(0, 256, (batch, 3, 227, 227)) - 128).astype(np.float32)
+
+    def fwd(x):
+        y = oracle.relu(oracle.conv_im2col(x, w["conv1"], b["conv1"], 4, 0))
+        y = oracle.pool(oracle.lrn(y, 5, 1e-4, 0.75), 3, 2)
+        y = oracle.relu(oracle.conv_im2col(y, w["conv2"], b["conv2"], 1, 2, 1, 2))
+        y = oracle.pool(oracle.lrn(y, 5, 1e-4, 0.75), 3, 2)
+        y = oracle.relu(oracle.conv_im2col(y, w["conv3"], b["conv3"], 1, 1))
+        y = oracle.relu(oracle.conv_im2col(y, w["conv4"], b["conv4"], 1, 1, 1, 2))
+        y = oracle.relu(oracle.conv_im2col(y, w["conv5"], b["conv5"], 1, 1, 1, 2))
+        y = oracle.pool(y, 3, 2).reshape(x.shape[0], -1)
+        for k in ("fc6", "fc7", "fc8"):
+            y = y @ fw[k].T + fb[k]
+            if k != "fc8":
+                y = np.maximum(y, 0)
+        return oracle.softmax(y)
+
+    n, t1 = 0, time.perf_counter()
+    while n < 2 or (time.perf_counter() - t1 < budget_s and n < batch):
+        fwd(x_all[n:n + 1])
+        n += 1
+    t_img = (time.perf_counter() - t1) / n
+    per_map = t_inject + batch * t_img
+    return {"value": round(batch / per_map, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"1 fault map (C oracle inject of 58,631,144 IP weights: {t_inject:.2f} s) + {n} "
+                      f"single-image AlexNet forwards (im2col + OpenBLAS sgemm: {t_img * 1e3:.0f} ms/img), "
+                      f"extrapolated to one {batch}-image map"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--p-fault", type=float, default=0.01)
+    ap.add_argument("--seed", type=int, default=1701)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--profile-layers", action="store_true", help="print the per-layer table to stderr")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from rramsim import caffe, make_inject_cfg, models
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    caffe.set_stream_from_torch()
+    caffe.set_random_seed(args.seed)
+
+    net = caffe.Net(models.alexnet(test_batch=args.batch), "test", models.net_options("alexnet"))
+    cfg = make_inject_cfg(args.p_fault)             # reference stuck-at semantics, neg/zero/pos 10/20/10
+    mc = caffe.MonteCarlo(net, cfg, seed=args.seed, max_maps=args.steps + args.warmup + 8)
+
+    def step(i):
+        mc.run(rank + world * i, 1)                 # map m on rank m mod N
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    mc.reset()
+    net.layer_times(reset=True)
+    mc.inject_times(reset=True)
+    net.set_timing(True)
+    mc.set_timing(True)
+
+    stats = torch.zeros(8, dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    net.set_timing(False)
+    mc.set_timing(False)
+    st = mc.stats()
+    vals = st["sums"] + [float(sum(st["broken"])), float(st["maps"])]
+    stats[:len(vals)] = torch.tensor(vals, dtype=torch.float64)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(stats)                     # RCCL: accuracy / loss / broken-cell sums
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = float(t.item())
+
+    # ---- roofline from the live hipEvent layer timings of the timed region
+    lt = net.layer_times()
+    flops = alexnet_gemm_table(args.batch)
+    gemm_ms = sum(ms for (name, typ, ms, cnt) in lt if name in flops) / args.steps
+    gemm_flops = sum(flops.values())
+    achieved_tf = gemm_flops / (gemm_ms * 1e-3) / 1e12
+    inj_ms, inj_n, inj_w = mc.inject_times()
+    inj_ms_per = inj_ms / max(inj_n, 1)
+    inj_gbps = 8.0 * inj_w / (inj_ms_per * 1e-3) / 1e9
+    if args.profile_layers and rank == 0:
+        for name, typ, ms, cnt in lt:
+            print(f"{name:>12s} {typ:>16s} {ms / max(cnt, 1):9.3f} ms", file=sys.stderr)
+
+    n_images = world * args.steps * args.batch
+    value = n_images / elapsed
+    out_names = [k for k in net.outputs().keys()]
+    mean_out = {nm: float(stats[k].item()) / max(1.0, float(stats[len(st["sums"]) + 1].item()))
+                for k, nm in enumerate(out_names[:len(st["sums"])])}
+    res = {
+        "metric": "Monte Carlo fault-map inferences/sec, AlexNet b256",
+        "value": round(value, 2),
+        "unit": "images/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (U{0..255}-128 images 3x227x227, random labels; seeded Caffe-filler weights)",
+        "config": {"workload": "alexnet_b256_mc_faultmap_inference", "model": "AlexNet (bvlc_alexnet train_val, TEST)",
+                   "global_batch": args.batch * world, "batch_per_map": args.batch, "maps_per_step": world,
+                   "p_fault": args.p_fault, "stuck_split_neg_zero_pos": [10, 20, 10],
+                   "fault_layers": "InnerProduct (58,631,144 weights)", "parallelism": f"mc-maps x{world} (RCCL stats all-reduce)"},
+        "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 2), "peak": MFMA_F32_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(achieved_tf / MFMA_F32_PEAK_TFLOPS, 4), "traffic": None,
+                     "kernel": "conv1-5 implicit-GEMM + fc6-8 GEMM (fp32 MFMA 32x32x2), per step",
+                     "algorithmic_flops_per_step": gemm_flops, "avg_ms_per_step": round(gemm_ms, 4)},
+        "roofline_inject": {"bound": "hbm", "achieved": round(inj_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                            "frac": round(inj_gbps / HBM_PEAK_GBPS, 4), "traffic": None,
+                            "algorithmic_bytes_per_launch": 8 * inj_w, "avg_us_per_launch": round(inj_ms_per * 1e3, 2)},
+        "mc_stats": {"maps": int(stats[len(st["sums"]) + 1].item()), "mean_outputs": mean_out,
+                     "broken_cells": int(stats[len(st["sums"])].item())},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(args.batch, args.p_fault, args.seed, args.cpu_budget)
+    elif rank == 0:
+        res["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    mc.close()
+    net.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,146 @@
+/*
+ * rram_caffe.h — C-ABI of the C++ Caffe-shaped host runtime (librram_caffe.so).
+ *
+ * The host keeps the reference's C++ API (caffe::Net / Layer / Solver /
+ * FailureMaker, host/ headers) and exposes it through opaque handles so that
+ * non-C++ callers (Python ctypes, the bench, a cgo/JNI binding) can drive the
+ * drop-in path.  Every call returns RRAM_OK (0) or a negative status and never
+ * aborts; rram_caffe_last_error() holds the message (the reference's glog
+ * CHECK failures become RRAM_EINVAL here).
+ *
+ * Device pointers handed out (blob / param / fault-state accessors) stay valid
+ * until the owning handle is destroyed or the blob is reshaped.
+ */
+#ifndef RRAM_CAFFE_H_
+#define RRAM_CAFFE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "rram_kernels.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct rram_net_s* rram_net_t;
+typedef struct rram_solver_s* rram_solver_t;
+typedef struct rram_mc_s* rram_mc_t;
+
+enum { RRAM_PHASE_TRAIN = 0, RRAM_PHASE_TEST = 1 };
+
+const char* rram_caffe_last_error(void);
+/* All host work of the calling thread is issued on this stream (Caffe::Get()
+ * is per-thread, common.cpp:13-20).  NULL = default stream. */
+int rram_caffe_set_stream(rram_stream_t stream);
+/* Caffe::set_random_seed (common.cpp:131-147): seeds fillers, synthetic data,
+ * fault draws. */
+int rram_caffe_set_random_seed(uint64_t seed);
+int rram_caffe_synchronize(void);
+
+/* ---------------------------------------------------------------- Net
+ * net_prototxt: NetParameter text (caffe.proto); options: text-format
+ * key/values, e.g. 'data_shape: "3,227,227" num_classes: 1000
+ * fault_layers: "InnerProduct" fuse_relu: true'.  Replaces Net<Dtype>(param)
+ * (net.cpp:42-300). */
+int rram_net_create(const char* net_prototxt, int phase, const char* options, rram_net_t* out);
+int rram_net_destroy(rram_net_t net);
+/* Net::Forward (net.cpp:558-569); loss_out (nullable) gets the weighted loss
+ * when compute_loss != 0 (one small D2H). */
+int rram_net_forward(rram_net_t net, int compute_loss, float* loss_out);
+int rram_net_backward(rram_net_t net);
+int rram_net_update(rram_net_t net);
+int rram_net_clear_param_diffs(rram_net_t net);
+int rram_net_num_layers(rram_net_t net, int* n);
+/* name/type copied into caller buffers of `cap` bytes */
+int rram_net_layer_info(rram_net_t net, int i, char* name, char* type, int cap, int* num_params);
+int rram_net_num_blobs(rram_net_t net, int* n);
+int rram_net_blob_name(rram_net_t net, int i, char* name, int cap);
+/* device pointers and shape (up to 8 axes) of a named blob */
+int rram_net_blob(rram_net_t net, const char* name, float** data, float** diff, int* shape, int* num_axes);
+int rram_net_num_params(rram_net_t net, int* n);
+int rram_net_param(rram_net_t net, int i, float** data, float** diff, int64_t* count, float* lr_mult,
+                   float* decay_mult);
+/* Net::failure_learnable_params() (net.hpp:181-183): InnerProduct weights and
+ * biases; layer_id = owning layer index. */
+int rram_net_num_failure_params(rram_net_t net, int* n);
+int rram_net_failure_param(rram_net_t net, int i, float** data, float** diff, int64_t* count, int* layer_id);
+int rram_net_num_outputs(rram_net_t net, int* n);
+int rram_net_output(rram_net_t net, int i, char* name, int cap, float** data, int64_t* count);
+/* Net::ShareTrainedLayersWith (net.cpp:697-720) */
+int rram_net_share_trained(rram_net_t dst, rram_net_t src);
+/* P2PSync GPUParams equivalent (parallel.cpp:25-115): alias every learnable
+ * param into caller-owned flat device buffers of rram_net_flat_param_count
+ * floats (data copied in, diff zeroed). */
+int rram_net_flat_param_count(rram_net_t net, int64_t* n);
+int rram_net_alias_flat_params(rram_net_t net, float* data, float* diff);
+/* Per-layer forward timing (`caffe time`, tools/caffe.cpp:334-421): hipEvents
+ * around every layer on the working stream.  layer_times synchronises and
+ * returns total ms and launch count per layer since the last reset. */
+int rram_net_set_timing(rram_net_t net, int enable);
+int rram_net_layer_times(rram_net_t net, double* ms, long* counts, int cap, int* n, int reset);
+/* Host-only structural view (no device): phase filter + split insertion;
+ * writes "name\ttype\tbottoms\ttops\n" lines into out (cap bytes);
+ * *needed = bytes required including the terminator. */
+int rram_net_describe(const char* net_prototxt, int phase, char* out, size_t cap, size_t* needed);
+
+/* ------------------------------------------------------------- Solver
+ * SGDSolver with the fork's fault hooks (solver.cpp:14-40, :237-325).
+ * net_prototxt (nullable) overrides the solver's net: / net_param.
+ * options: the net options above plus fused_update: true|false. */
+int rram_solver_create(const char* solver_prototxt, const char* net_prototxt, const char* options,
+                       rram_solver_t* out);
+int rram_solver_destroy(rram_solver_t s);
+int rram_solver_step(rram_solver_t s, int iters);
+int rram_solver_solve(rram_solver_t s);
+int rram_solver_iter(rram_solver_t s, int* iter);
+int rram_solver_smoothed_loss(rram_solver_t s, float* loss);
+int rram_solver_learning_rate(rram_solver_t s, float* lr);
+/* train net handle (owned by the solver; do not destroy) */
+int rram_solver_net(rram_solver_t s, rram_net_t* net);
+int rram_solver_num_test_nets(rram_solver_t s, int* n);
+int rram_solver_test_net(rram_solver_t s, int i, rram_net_t* net);
+/* Solver::Test (solver.cpp:385-458): mean of every output element over test_iter */
+int rram_solver_test(rram_solver_t s, int test_net, float* scores, int cap, int* n);
+/* on_gradients_ready callback (solver.hpp:80-91, parallel.cpp:324-380):
+ * called once per iteration after backward, before the update. */
+typedef void (*rram_callback_t)(void* user);
+int rram_solver_set_gradient_callback(rram_solver_t s, rram_callback_t cb, void* user);
+/* log lines in the reference's format ("Iteration N, loss = ...",
+ * "    Test net output #k: name = v"), delivered to cb (NULL = silent). */
+typedef void (*rram_log_callback_t)(const char* line, void* user);
+int rram_solver_set_log_callback(rram_solver_t s, rram_log_callback_t cb, void* user);
+/* Fault state (GaussianFailureMaker::fail_iterations(), failure_maker.hpp:82-84):
+ * endurance = blob data, stuck values = blob diff, reference layout.
+ * n = 0 when the solver has no failure_pattern. */
+int rram_solver_num_fail_blobs(rram_solver_t s, int* n);
+int rram_solver_fail_state(rram_solver_t s, int i, float** endurance, float** values, int64_t* count);
+/* broken cells per faultable blob after the last Fail() (device count, one D2H) */
+int rram_solver_broken_counts(rram_solver_t s, unsigned long long* out, int cap, int* n);
+
+/* --------------------------------------------------------- Monte-Carlo
+ * Fault-map inference on a TEST-phase net: for maps m in [begin, begin+count):
+ * inject(clean weights) -> forward -> accumulate scalar outputs.  cfgs: one
+ * config for every faultable blob, or ncfg == 1 for all.  The net's
+ * faultable weights are restored when the handle is destroyed. */
+int rram_mc_create(rram_net_t net, const rram_inject_cfg* cfgs, int ncfg, uint64_t seed, int max_maps,
+                   rram_mc_t* out);
+int rram_mc_destroy(rram_mc_t mc);
+/* asynchronous on the caller's stream */
+int rram_mc_run(rram_mc_t mc, uint32_t map_begin, uint32_t map_count);
+int rram_mc_reset(rram_mc_t mc);
+int rram_mc_restore_clean(rram_mc_t mc);
+/* synchronises; sums[n_outputs] over maps, broken[n_fault_blobs] summed over
+ * maps, per_map[min(maps, max_maps) * n_outputs] (nullable buffers skip). */
+int rram_mc_stats(rram_mc_t mc, double* sums, int sums_cap, int* n_outputs, unsigned long long* broken,
+                  int broken_cap, int* n_blobs, float* per_map, int per_map_cap, int* maps_run);
+/* hipEvent timing of the injection launches; inject_times synchronises and
+ * returns total ms / launches since the last reset, and the faultable weight count. */
+int rram_mc_set_timing(rram_mc_t mc, int enable);
+int rram_mc_inject_times(rram_mc_t mc, double* ms, long* launches, int64_t* weights, int reset);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RRAM_CAFFE_H_ */

@@ -304,6 +304,15 @@ int rram_lrn_bwd(const float* x, const float* y, const float* scale,
                  const float* dy, float* dx, int num, int channels, int height,
                  int width, int size, float alpha, float beta, rram_stream_t s);
 
+/* LRN WITHIN_CHANNEL (lrn_layer.cpp: square -> AVE pool (local_size, pad
+ * (size-1)/2, stride 1) -> (1 + alpha * avg)^-beta -> product); scale keeps
+ * 1 + alpha * avg for backward (nullable in forward-only use). */
+int rram_lrn_within_fwd(const float* x, float* y, float* scale, int num, int channels, int height,
+                        int width, int size, float alpha, float beta, rram_stream_t s);
+int rram_lrn_within_bwd(const float* x, const float* scale, const float* dy, float* dx, int num,
+                        int channels, int height, int width, int size, float alpha, float beta,
+                        rram_stream_t s);
+
 /* Softmax over `channels` for [outer][channels][inner]. */
 int rram_softmax_fwd(const float* x, float* y, int outer, int channels, int inner, rram_stream_t s);
 /* SoftmaxWithLoss forward: loss_out[0] = -sum log(max(p[label], FLT_MIN)) / normalizer

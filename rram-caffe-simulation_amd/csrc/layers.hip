@@ -149,6 +149,58 @@ __global__ void k_lrn_bwd(const float* __restrict__ x, const float* __restrict__
   }
 }
 
+// LRN WITHIN_CHANNEL (lrn_layer.cpp WithinChannelForward: square -> AVE pool
+// (k = size, pad = (size-1)/2, stride 1, Caffe's pool_size rule) -> (1 + alpha*.)^-beta -> product)
+__device__ __forceinline__ int within_psize(int p, int pre, int size, int L) {
+  const int s = p - pre;
+  const int e = min(s + size, L + pre);
+  return e - s;
+}
+__global__ void k_lrn_within_fwd(const float* __restrict__ x, float* __restrict__ y, float* __restrict__ scale,
+                                 int64_t planes, int H, int W, int size, float alpha, float beta) {
+  const int64_t total = planes * H * W;
+  const int pre = (size - 1) / 2;
+  GRID_LOOP(idx, total) {
+    const int w = idx % W;
+    const int h = (idx / W) % H;
+    const float* xp = x + (idx / W / H) * H * W;
+    const int hs = max(h - pre, 0), he = min(h - pre + size, H);
+    const int ws = max(w - pre, 0), we = min(w - pre + size, W);
+    float s = 0.0f;
+    for (int a = hs; a < he; ++a)
+      for (int b = ws; b < we; ++b) {
+        const float v = xp[a * W + b];
+        s += v * v;
+      }
+    const float n = static_cast<float>(within_psize(h, pre, size, H) * within_psize(w, pre, size, W));
+    const float sc = 1.0f + alpha * (s / n);
+    if (scale) scale[idx] = sc;
+    y[idx] = x[idx] * powf(sc, -beta);
+  }
+}
+__global__ void k_lrn_within_bwd(const float* __restrict__ x, const float* __restrict__ scale,
+                                 const float* __restrict__ dy, float* __restrict__ dx, int64_t planes, int H,
+                                 int W, int size, float alpha, float beta) {
+  const int64_t total = planes * H * W;
+  const int pre = (size - 1) / 2;
+  GRID_LOOP(idx, total) {
+    const int w = idx % W;
+    const int h = (idx / W) % H;
+    const int64_t base = (idx / W / H) * H * W;
+    // windows p containing r: p - pre <= r <= p - pre + size - 1
+    const int ps = max(h + pre - size + 1, 0), pe = min(h + pre, H - 1);
+    const int qs = max(w + pre - size + 1, 0), qe = min(w + pre, W - 1);
+    float acc = 0.0f;
+    for (int a = ps; a <= pe; ++a)
+      for (int b = qs; b <= qe; ++b) {
+        const int64_t o = base + a * W + b;
+        const float n = static_cast<float>(within_psize(a, pre, size, H) * within_psize(b, pre, size, W));
+        acc += dy[o] * x[o] * powf(scale[o], -beta - 1.0f) / n;
+      }
+    dx[idx] = dy[idx] * powf(scale[idx], -beta) - 2.0f * alpha * beta * x[idx] * acc;
+  }
+}
+
 // softmax_layer.cu: one wave per (outer, inner) column
 __global__ void __launch_bounds__(256) k_softmax(const float* __restrict__ x, float* __restrict__ y,
                                                  int outer, int C, int inner) {
@@ -369,6 +421,27 @@ int rram_lrn_bwd(const float* x, const float* y, const float* scale, const float
   hipLaunchKernelGGL(k_lrn_bwd, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), x, y,
                      scale, dy, dx, num, C, H * W, size, 2.0f * alpha * beta / size, beta);
   return launch_status("lrn_bwd");
+}
+
+int rram_lrn_within_fwd(const float* x, float* y, float* scale, int num, int C, int H, int W, int size,
+                        float alpha, float beta, rram_stream_t s) {
+  RRAM_REQUIRE(num >= 0 && C > 0 && H > 0 && W > 0 && size > 0 && (size & 1), "lrn_within_fwd: bad geometry");
+  const int64_t total = (int64_t)num * C * H * W;
+  if (total == 0) return RRAM_OK;
+  RRAM_REQUIRE(x && y, "lrn_within_fwd: NULL");
+  hipLaunchKernelGGL(k_lrn_within_fwd, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), x, y,
+                     scale, (int64_t)num * C, H, W, size, alpha, beta);
+  return launch_status("lrn_within_fwd");
+}
+int rram_lrn_within_bwd(const float* x, const float* scale, const float* dy, float* dx, int num, int C, int H,
+                        int W, int size, float alpha, float beta, rram_stream_t s) {
+  RRAM_REQUIRE(num >= 0 && C > 0 && H > 0 && W > 0 && size > 0 && (size & 1), "lrn_within_bwd: bad geometry");
+  const int64_t total = (int64_t)num * C * H * W;
+  if (total == 0) return RRAM_OK;
+  RRAM_REQUIRE(x && scale && dy && dx, "lrn_within_bwd: NULL");
+  hipLaunchKernelGGL(k_lrn_within_bwd, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), x, scale,
+                     dy, dx, (int64_t)num * C, H, W, size, alpha, beta);
+  return launch_status("lrn_within_bwd");
 }
 
 int rram_softmax_fwd(const float* x, float* y, int outer, int C, int inner, rram_stream_t s) {

@@ -1,0 +1,479 @@
+// extern "C" face of the host runtime (include/rram_caffe.h).  Exceptions
+// (the reference's fatal CHECKs) become status codes + a thread-local message.
+#include <cstring>
+#include <string>
+
+#include "rram_caffe.h"
+#include "solver.hpp"
+
+using namespace caffe;
+
+struct rram_net_s {
+  std::shared_ptr<Net<float>> net;
+};
+struct rram_solver_s {
+  std::unique_ptr<Solver<float>> solver;
+  rram_net_s train;
+  std::vector<rram_net_s> tests;
+  rram_callback_t grad_cb = nullptr;
+  void* grad_user = nullptr;
+  rram_log_callback_t log_cb = nullptr;
+  void* log_user = nullptr;
+};
+struct rram_mc_s {
+  std::unique_ptr<MonteCarlo<float>> mc;
+};
+
+static thread_local std::string g_caffe_err;
+
+template <typename F>
+static int guarded(F&& f) {
+  try {
+    f();
+    return RRAM_OK;
+  } catch (const std::exception& e) {
+    g_caffe_err = e.what();
+    return RRAM_EINVAL;
+  } catch (...) {
+    g_caffe_err = "unknown C++ exception";
+    return RRAM_EINVAL;
+  }
+}
+
+#define NEED(p)                                               \
+  do {                                                        \
+    if (!(p)) throw Error(std::string("NULL argument: ") + #p); \
+  } while (0)
+
+static void copy_str(const std::string& s, char* dst, int cap) {
+  if (!dst || cap <= 0) return;
+  const size_t n = std::min<size_t>(s.size(), (size_t)cap - 1);
+  std::memcpy(dst, s.data(), n);
+  dst[n] = '\0';
+}
+
+static Msg parse_opts(const char* options) { return options ? parse_prototxt(options) : Msg(); }
+
+extern "C" {
+
+const char* rram_caffe_last_error(void) { return g_caffe_err.c_str(); }
+int rram_caffe_set_stream(rram_stream_t s) {
+  return guarded([&] { Caffe::set_stream(s); });
+}
+int rram_caffe_set_random_seed(uint64_t seed) {
+  return guarded([&] { Caffe::set_random_seed(seed); });
+}
+int rram_caffe_synchronize(void) {
+  return guarded([&] { Caffe::synchronize(); });
+}
+
+// ------------------------------------------------------------------- Net
+int rram_net_create(const char* txt, int phase, const char* options, rram_net_t* out) {
+  return guarded([&] {
+    NEED(txt);
+    NEED(out);
+    auto* h = new rram_net_s;
+    try {
+      h->net = std::make_shared<Net<float>>(parse_prototxt(txt), phase == RRAM_PHASE_TEST ? TEST : TRAIN,
+                                            parse_opts(options));
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+int rram_net_destroy(rram_net_t n) {
+  return guarded([&] { delete n; });
+}
+int rram_net_forward(rram_net_t n, int compute_loss, float* loss) {
+  return guarded([&] {
+    NEED(n);
+    float l = n->net->Forward(compute_loss != 0);
+    if (loss) *loss = l;
+  });
+}
+int rram_net_backward(rram_net_t n) {
+  return guarded([&] {
+    NEED(n);
+    n->net->Backward();
+  });
+}
+int rram_net_update(rram_net_t n) {
+  return guarded([&] {
+    NEED(n);
+    n->net->Update();
+  });
+}
+int rram_net_clear_param_diffs(rram_net_t n) {
+  return guarded([&] {
+    NEED(n);
+    n->net->ClearParamDiffs();
+  });
+}
+int rram_net_num_layers(rram_net_t n, int* k) {
+  return guarded([&] {
+    NEED(n);
+    NEED(k);
+    *k = (int)n->net->layers().size();
+  });
+}
+int rram_net_layer_info(rram_net_t n, int i, char* name, char* type, int cap, int* np) {
+  return guarded([&] {
+    NEED(n);
+    const auto& L = n->net->layers();
+    if (i < 0 || i >= (int)L.size()) throw Error("layer index out of range");
+    copy_str(n->net->layer_names()[i], name, cap);
+    copy_str(L[i]->type(), type, cap);
+    if (np) *np = (int)L[i]->blobs().size();
+  });
+}
+int rram_net_num_blobs(rram_net_t n, int* k) {
+  return guarded([&] {
+    NEED(n);
+    NEED(k);
+    *k = (int)n->net->blobs().size();
+  });
+}
+int rram_net_blob_name(rram_net_t n, int i, char* name, int cap) {
+  return guarded([&] {
+    NEED(n);
+    if (i < 0 || i >= (int)n->net->blob_names().size()) throw Error("blob index out of range");
+    copy_str(n->net->blob_names()[i], name, cap);
+  });
+}
+int rram_net_blob(rram_net_t n, const char* name, float** data, float** diff, int* shape, int* naxes) {
+  return guarded([&] {
+    NEED(n);
+    NEED(name);
+    auto b = n->net->blob_by_name(name);
+    if (!b) throw Error(std::string("Unknown blob name ") + name);
+    if (data) *data = b->mutable_gpu_data();
+    if (diff) *diff = b->mutable_gpu_diff();
+    if (naxes) *naxes = b->num_axes();
+    if (shape)
+      for (int a = 0; a < b->num_axes() && a < 8; ++a) shape[a] = b->shape(a);
+  });
+}
+int rram_net_num_params(rram_net_t n, int* k) {
+  return guarded([&] {
+    NEED(n);
+    NEED(k);
+    *k = (int)n->net->learnable_params().size();
+  });
+}
+int rram_net_param(rram_net_t n, int i, float** data, float** diff, int64_t* count, float* lr, float* dm) {
+  return guarded([&] {
+    NEED(n);
+    const auto& P = n->net->learnable_params();
+    if (i < 0 || i >= (int)P.size()) throw Error("param index out of range");
+    if (data) *data = P[i]->mutable_gpu_data();
+    if (diff) *diff = P[i]->mutable_gpu_diff();
+    if (count) *count = P[i]->count();
+    if (lr) *lr = n->net->params_lr()[i];
+    if (dm) *dm = n->net->params_weight_decay()[i];
+  });
+}
+int rram_net_num_failure_params(rram_net_t n, int* k) {
+  return guarded([&] {
+    NEED(n);
+    NEED(k);
+    *k = (int)n->net->failure_learnable_params().size();
+  });
+}
+int rram_net_failure_param(rram_net_t n, int i, float** data, float** diff, int64_t* count, int* layer_id) {
+  return guarded([&] {
+    NEED(n);
+    const auto& P = n->net->failure_learnable_params();
+    if (i < 0 || i >= (int)P.size()) throw Error("failure param index out of range");
+    if (data) *data = P[i]->mutable_gpu_data();
+    if (diff) *diff = P[i]->mutable_gpu_diff();
+    if (count) *count = P[i]->count();
+    if (layer_id) *layer_id = n->net->failure_learnable_layer_ids()[i];
+  });
+}
+int rram_net_num_outputs(rram_net_t n, int* k) {
+  return guarded([&] {
+    NEED(n);
+    NEED(k);
+    *k = (int)n->net->output_blobs().size();
+  });
+}
+int rram_net_output(rram_net_t n, int i, char* name, int cap, float** data, int64_t* count) {
+  return guarded([&] {
+    NEED(n);
+    const auto& O = n->net->output_blobs();
+    if (i < 0 || i >= (int)O.size()) throw Error("output index out of range");
+    copy_str(n->net->blob_names()[n->net->output_blob_indices()[i]], name, cap);
+    if (data) *data = O[i]->mutable_gpu_data();
+    if (count) *count = O[i]->count();
+  });
+}
+int rram_net_share_trained(rram_net_t dst, rram_net_t src) {
+  return guarded([&] {
+    NEED(dst);
+    NEED(src);
+    dst->net->ShareTrainedLayersWith(src->net.get());
+  });
+}
+int rram_net_flat_param_count(rram_net_t n, int64_t* k) {
+  return guarded([&] {
+    NEED(n);
+    NEED(k);
+    *k = n->net->flat_param_count();
+  });
+}
+int rram_net_alias_flat_params(rram_net_t n, float* data, float* diff) {
+  return guarded([&] {
+    NEED(n);
+    NEED(data);
+    NEED(diff);
+    n->net->alias_flat_params(data, diff);
+  });
+}
+
+int rram_net_set_timing(rram_net_t n, int enable) {
+  return guarded([&] {
+    NEED(n);
+    n->net->set_timing(enable != 0);
+  });
+}
+int rram_net_layer_times(rram_net_t n, double* ms, long* counts, int cap, int* k, int reset) {
+  return guarded([&] {
+    NEED(n);
+    auto& t = n->net->timer();
+    t.collect();
+    const int L = (int)n->net->layers().size();
+    if (k) *k = L;
+    for (int i = 0; i < L && i < cap; ++i) {
+      auto it = t.totals().find(i);
+      auto ic = t.counts().find(i);
+      if (ms) ms[i] = it == t.totals().end() ? 0.0 : it->second;
+      if (counts) counts[i] = ic == t.counts().end() ? 0 : ic->second;
+    }
+    if (reset) t.clear();
+  });
+}
+int rram_net_describe(const char* txt, int phase, char* out, size_t cap, size_t* needed) {
+  return guarded([&] {
+    NEED(txt);
+    std::string d = DescribeNet(parse_prototxt(txt), phase == RRAM_PHASE_TEST ? TEST : TRAIN);
+    if (needed) *needed = d.size() + 1;
+    if (out && cap > 0) {
+      const size_t n = std::min(d.size(), cap - 1);
+      std::memcpy(out, d.data(), n);
+      out[n] = '\0';
+    }
+  });
+}
+
+// ---------------------------------------------------------------- Solver
+int rram_solver_create(const char* sp, const char* np, const char* options, rram_solver_t* out) {
+  return guarded([&] {
+    NEED(sp);
+    NEED(out);
+    Msg netp;
+    if (np) netp = parse_prototxt(np);
+    auto* h = new rram_solver_s;
+    try {
+      h->solver = std::make_unique<Solver<float>>(parse_prototxt(sp), np ? &netp : nullptr, parse_opts(options));
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    h->train.net = h->solver->net();
+    for (auto& t : h->solver->test_nets()) h->tests.push_back(rram_net_s{t});
+    *out = h;
+  });
+}
+int rram_solver_destroy(rram_solver_t s) {
+  return guarded([&] { delete s; });
+}
+int rram_solver_step(rram_solver_t s, int iters) {
+  return guarded([&] {
+    NEED(s);
+    s->solver->Step(iters);
+  });
+}
+int rram_solver_solve(rram_solver_t s) {
+  return guarded([&] {
+    NEED(s);
+    s->solver->Solve();
+  });
+}
+int rram_solver_iter(rram_solver_t s, int* it) {
+  return guarded([&] {
+    NEED(s);
+    NEED(it);
+    *it = s->solver->iter();
+  });
+}
+int rram_solver_smoothed_loss(rram_solver_t s, float* l) {
+  return guarded([&] {
+    NEED(s);
+    NEED(l);
+    *l = s->solver->smoothed_loss();
+  });
+}
+int rram_solver_learning_rate(rram_solver_t s, float* lr) {
+  return guarded([&] {
+    NEED(s);
+    NEED(lr);
+    *lr = s->solver->GetLearningRate();
+  });
+}
+int rram_solver_net(rram_solver_t s, rram_net_t* n) {
+  return guarded([&] {
+    NEED(s);
+    NEED(n);
+    *n = &s->train;
+  });
+}
+int rram_solver_num_test_nets(rram_solver_t s, int* n) {
+  return guarded([&] {
+    NEED(s);
+    NEED(n);
+    *n = (int)s->tests.size();
+  });
+}
+int rram_solver_test_net(rram_solver_t s, int i, rram_net_t* n) {
+  return guarded([&] {
+    NEED(s);
+    NEED(n);
+    if (i < 0 || i >= (int)s->tests.size()) throw Error("test net index out of range");
+    *n = &s->tests[i];
+  });
+}
+int rram_solver_test(rram_solver_t s, int t, float* scores, int cap, int* n) {
+  return guarded([&] {
+    NEED(s);
+    auto r = s->solver->Test(t);
+    if (n) *n = (int)r.size();
+    for (int i = 0; i < (int)r.size() && i < cap && scores; ++i) scores[i] = r[i];
+  });
+}
+int rram_solver_set_gradient_callback(rram_solver_t s, rram_callback_t cb, void* user) {
+  return guarded([&] {
+    NEED(s);
+    s->grad_cb = cb;
+    s->grad_user = user;
+    if (cb) s->solver->on_gradients_ready = [s] { s->grad_cb(s->grad_user); };
+    else s->solver->on_gradients_ready = nullptr;
+  });
+}
+int rram_solver_set_log_callback(rram_solver_t s, rram_log_callback_t cb, void* user) {
+  return guarded([&] {
+    NEED(s);
+    s->log_cb = cb;
+    s->log_user = user;
+    if (cb) s->solver->log = [s](const std::string& l) { s->log_cb(l.c_str(), s->log_user); };
+    else s->solver->log = nullptr;
+  });
+}
+int rram_solver_num_fail_blobs(rram_solver_t s, int* n) {
+  return guarded([&] {
+    NEED(s);
+    NEED(n);
+    auto fm = s->solver->failure_maker();
+    *n = fm ? (int)fm->fail_iterations().size() : 0;
+  });
+}
+int rram_solver_fail_state(rram_solver_t s, int i, float** e, float** v, int64_t* count) {
+  return guarded([&] {
+    NEED(s);
+    auto fm = s->solver->failure_maker();
+    if (!fm) throw Error("solver has no failure_pattern");
+    auto fi = fm->fail_iterations();
+    if (i < 0 || i >= (int)fi.size()) throw Error("fail blob index out of range");
+    if (e) *e = fi[i]->mutable_gpu_data();
+    if (v) *v = fi[i]->mutable_gpu_diff();
+    if (count) *count = fi[i]->count();
+  });
+}
+int rram_solver_broken_counts(rram_solver_t s, unsigned long long* out, int cap, int* n) {
+  return guarded([&] {
+    NEED(s);
+    auto fm = s->solver->failure_maker();
+    std::vector<unsigned long long> c = fm ? fm->broken_counts() : std::vector<unsigned long long>();
+    if (n) *n = (int)c.size();
+    for (int i = 0; i < (int)c.size() && i < cap && out; ++i) out[i] = c[i];
+  });
+}
+
+// ----------------------------------------------------------- Monte-Carlo
+int rram_mc_create(rram_net_t net, const rram_inject_cfg* cfgs, int ncfg, uint64_t seed, int max_maps,
+                   rram_mc_t* out) {
+  return guarded([&] {
+    NEED(net);
+    NEED(cfgs);
+    NEED(out);
+    if (ncfg < 1) throw Error("rram_mc_create: ncfg must be >= 1");
+    std::vector<rram_inject_cfg> v(cfgs, cfgs + ncfg);
+    auto* h = new rram_mc_s;
+    try {
+      h->mc = std::make_unique<MonteCarlo<float>>(net->net, v, seed, max_maps);
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+int rram_mc_destroy(rram_mc_t m) {
+  return guarded([&] { delete m; });
+}
+int rram_mc_run(rram_mc_t m, uint32_t begin, uint32_t count) {
+  return guarded([&] {
+    NEED(m);
+    m->mc->Run(begin, count);
+  });
+}
+int rram_mc_reset(rram_mc_t m) {
+  return guarded([&] {
+    NEED(m);
+    m->mc->Reset();
+  });
+}
+int rram_mc_restore_clean(rram_mc_t m) {
+  return guarded([&] {
+    NEED(m);
+    m->mc->RestoreClean();
+  });
+}
+int rram_mc_set_timing(rram_mc_t m, int enable) {
+  return guarded([&] {
+    NEED(m);
+    m->mc->set_timing(enable != 0);
+  });
+}
+int rram_mc_inject_times(rram_mc_t m, double* ms, long* launches, int64_t* weights, int reset) {
+  return guarded([&] {
+    NEED(m);
+    auto& t = m->mc->timer();
+    t.collect();
+    auto it = t.totals().find(0);
+    auto ic = t.counts().find(0);
+    if (ms) *ms = it == t.totals().end() ? 0.0 : it->second;
+    if (launches) *launches = ic == t.counts().end() ? 0 : ic->second;
+    if (weights) *weights = m->mc->fault_weights();
+    if (reset) t.clear();
+  });
+}
+int rram_mc_stats(rram_mc_t m, double* sums, int sums_cap, int* n_out, unsigned long long* broken, int bcap,
+                  int* n_blobs, float* per_map, int pcap, int* maps_run) {
+  return guarded([&] {
+    NEED(m);
+    std::vector<double> o;
+    std::vector<unsigned long long> b;
+    std::vector<float> pm;
+    m->mc->Stats(o, b, pm);
+    if (n_out) *n_out = (int)o.size();
+    if (n_blobs) *n_blobs = (int)b.size();
+    if (maps_run) *maps_run = m->mc->maps_run();
+    for (int i = 0; sums && i < (int)o.size() && i < sums_cap; ++i) sums[i] = o[i];
+    for (int i = 0; broken && i < (int)b.size() && i < bcap; ++i) broken[i] = b[i];
+    for (int i = 0; per_map && i < (int)pm.size() && i < pcap; ++i) per_map[i] = pm[i];
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,750 @@
+// Layer implementations (device-only) + registry + fillers.
+#include "layers.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+namespace caffe {
+
+// ---------------------------------------------------------------- base
+template <typename Dtype>
+Dtype Layer<Dtype>::Forward(const std::vector<Blob<Dtype>*>& bottom,
+                            const std::vector<Blob<Dtype>*>& top) {
+  Reshape(bottom, top);
+  Forward_gpu(bottom, top);
+  return Dtype(0);  // loss is read from the loss tops by Net (no per-layer sync)
+}
+
+template <typename Dtype>
+void Layer<Dtype>::CheckBlobCounts(const std::vector<Blob<Dtype>*>& bottom,
+                                   const std::vector<Blob<Dtype>*>& top) {
+  const std::string nm = name() + " (" + type() + ")";
+  if (ExactNumBottomBlobs() >= 0)
+    CAFFE_CHECK((int)bottom.size() == ExactNumBottomBlobs(), nm << " takes " << ExactNumBottomBlobs() << " bottom blob(s)");
+  if (MinBottomBlobs() >= 0)
+    CAFFE_CHECK((int)bottom.size() >= MinBottomBlobs(), nm << " takes at least " << MinBottomBlobs() << " bottom blob(s)");
+  if (ExactNumTopBlobs() >= 0)
+    CAFFE_CHECK((int)top.size() == ExactNumTopBlobs(), nm << " produces " << ExactNumTopBlobs() << " top blob(s)");
+  if (MinTopBlobs() >= 0)
+    CAFFE_CHECK((int)top.size() >= MinTopBlobs(), nm << " produces at least " << MinTopBlobs() << " top blob(s)");
+  if (EqualNumBottomTopBlobs())
+    CAFFE_CHECK(bottom.size() == top.size(), nm << " needs equal bottom and top counts");
+}
+
+template <typename Dtype>
+void Layer<Dtype>::SetLossWeights(const std::vector<Blob<Dtype>*>& top) {
+  auto lw = layer_param_.nums("loss_weight");
+  loss_.assign(top.size(), Dtype(0));
+  if (!lw.empty()) {
+    CAFFE_CHECK(lw.size() == top.size(), name() << ": loss_weight must be given for every top");
+    for (size_t i = 0; i < top.size(); ++i) loss_[i] = static_cast<Dtype>(lw[i]);
+  } else if (IsLoss() && !top.empty()) {
+    loss_[0] = Dtype(1);
+  }
+}
+
+template <typename Dtype>
+std::map<std::string, typename LayerRegistry<Dtype>::Creator>& LayerRegistry<Dtype>::Registry() {
+  static std::map<std::string, Creator> r;
+  return r;
+}
+template <typename Dtype>
+std::shared_ptr<Layer<Dtype>> LayerRegistry<Dtype>::CreateLayer(const Msg& param) {
+  const std::string t = param.str("type");
+  auto& r = Registry();
+  auto it = r.find(t);
+  CAFFE_CHECK(it != r.end(), "Unknown layer type: " << t << " (layer " << param.str("name") << ")");
+  return it->second(param);
+}
+template <typename Dtype>
+std::vector<std::string> LayerRegistry<Dtype>::LayerTypeList() {
+  std::vector<std::string> v;
+  for (auto& kv : Registry()) v.push_back(kv.first);
+  return v;
+}
+
+template class Layer<float>;
+template class LayerRegistry<float>;
+
+// --------------------------------------------------------------- fillers
+static uint32_t hash32(const std::string& s) {
+  uint32_t h = 2166136261u;
+  for (unsigned char c : s) h = (h ^ c) * 16777619u;
+  return h;
+}
+
+void FillBlob(Blob<float>* blob, const Msg& f, uint64_t seed, uint32_t sid) {
+  const std::string type = f.str("type", "constant");
+  const int64_t n = blob->count();
+  float* d = blob->mutable_gpu_data();
+  const rram_stream_t s = Caffe::stream();
+  auto fan = [&](bool in) -> double {
+    if (blob->num_axes() < 2) return (double)n;
+    return in ? (double)n / blob->shape(0) : (double)n / blob->shape(1);
+  };
+  auto norm_n = [&]() -> double {
+    const std::string vn = f.str("variance_norm", "FAN_IN");
+    if (vn == "FAN_OUT") return fan(false);
+    if (vn == "AVERAGE") return (fan(true) + fan(false)) / 2.0;
+    return fan(true);
+  };
+  if (type == "constant") {
+    RRAM_CALL(rram_set(n, static_cast<float>(f.num("value", 0.0)), d, s));
+  } else if (type == "gaussian") {
+    RRAM_CALL(rram_fill_gaussian(d, n, static_cast<float>(f.num("mean", 0.0)),
+                                 static_cast<float>(f.num("std", 1.0)), seed, sid, s));
+    CAFFE_CHECK(f.integer("sparse", -1) < 0, "gaussian filler: sparse is not supported");
+  } else if (type == "uniform") {
+    RRAM_CALL(rram_fill_uniform(d, n, static_cast<float>(f.num("min", 0.0)),
+                                static_cast<float>(f.num("max", 1.0)), seed, sid, s));
+  } else if (type == "xavier") {  // filler.hpp XavierFiller: U(-sqrt(3/n), sqrt(3/n))
+    const float sc = static_cast<float>(std::sqrt(3.0 / norm_n()));
+    RRAM_CALL(rram_fill_uniform(d, n, -sc, sc, seed, sid, s));
+  } else if (type == "msra") {  // MSRAFiller: N(0, sqrt(2/n))
+    RRAM_CALL(rram_fill_gaussian(d, n, 0.0f, static_cast<float>(std::sqrt(2.0 / norm_n())), seed, sid, s));
+  } else {
+    throw Error("Unknown filler type: " + type);
+  }
+}
+
+static std::vector<int> ints_of(const Msg& m, const std::string& k) {
+  std::vector<int> r;
+  for (double v : m.nums(k)) r.push_back(static_cast<int>(v));
+  return r;
+}
+
+// Caffe's kernel/stride/pad parsing (base_conv_layer.cpp:19-110, 2-D case)
+static void hw_param(const Msg& p, const std::string& base, int def, int& h, int& w) {
+  if (p.has(base + "_h") || p.has(base + "_w")) {
+    h = static_cast<int>(p.integer(base + "_h", def));
+    w = static_cast<int>(p.integer(base + "_w", def));
+    return;
+  }
+  const std::string key = base == "kernel" ? "kernel_size" : base;
+  auto v = ints_of(p, key);
+  if (v.empty()) {
+    h = w = def;
+  } else if (v.size() == 1) {
+    h = w = v[0];
+  } else {
+    h = v[0];
+    w = v[1];
+  }
+}
+
+// ★ ------------------------------------------------------- Convolution
+template <typename Dtype>
+void ConvolutionLayer<Dtype>::LayerSetUp(const std::vector<Blob<Dtype>*>& bottom,
+                                         const std::vector<Blob<Dtype>*>& top) {
+  const Msg& cp = this->layer_param_.sub_or_empty("convolution_param");
+  CAFFE_CHECK(bottom[0]->num_axes() == 4, "Convolution: only 2-D (4-axis) inputs are supported");
+  int kh, kw, sh, sw, ph, pw, dh, dw;
+  hw_param(cp, "kernel", 0, kh, kw);
+  hw_param(cp, "stride", 1, sh, sw);
+  hw_param(cp, "pad", 0, ph, pw);
+  hw_param(cp, "dilation", 1, dh, dw);
+  CAFFE_CHECK(kh > 0 && kw > 0, "Convolution: kernel size must be given and > 0");
+  desc_ = rram_conv_desc{0, bottom[0]->shape(1), 0, 0, (int)cp.integer("num_output", 0), kh, kw, ph, pw,
+                         sh, sw, dh, dw, (int)cp.integer("group", 1), 0, 0};
+  CAFFE_CHECK(desc_.num_output > 0, "Convolution: num_output must be > 0");
+  CAFFE_CHECK(desc_.channels % desc_.group == 0 && desc_.num_output % desc_.group == 0,
+              "Convolution: channels/num_output must be divisible by group");
+  bias_term_ = cp.boolean("bias_term", true);
+  this->blobs_.clear();
+  this->blobs_.push_back(std::make_shared<Blob<Dtype>>(
+      std::vector<int>{desc_.num_output, desc_.channels / desc_.group, kh, kw}));
+  const uint64_t seed = Caffe::seed() ^ (uint64_t)hash32(this->name()) << 20;
+  FillBlob(this->blobs_[0].get(), cp.sub_or_empty("weight_filler"), seed, 0);
+  if (bias_term_) {
+    this->blobs_.push_back(std::make_shared<Blob<Dtype>>(std::vector<int>{desc_.num_output}));
+    FillBlob(this->blobs_[1].get(), cp.sub_or_empty("bias_filler"), seed, 1);
+  }
+  this->param_propagate_down_.assign(this->blobs_.size(), true);
+}
+
+template <typename Dtype>
+void ConvolutionLayer<Dtype>::Reshape(const std::vector<Blob<Dtype>*>& bottom,
+                                      const std::vector<Blob<Dtype>*>& top) {
+  CAFFE_CHECK(bottom[0]->shape(1) == desc_.channels, this->name() << ": input channels changed");
+  desc_.num = bottom[0]->shape(0);
+  desc_.height = bottom[0]->shape(2);
+  desc_.width = bottom[0]->shape(3);
+  RRAM_CALL(rram_conv_out_shape(&desc_));
+  top[0]->Reshape({desc_.num, desc_.num_output, desc_.out_h, desc_.out_w});
+}
+
+template <typename Dtype>
+void ConvolutionLayer<Dtype>::Forward_gpu(const std::vector<Blob<Dtype>*>& bottom,
+                                          const std::vector<Blob<Dtype>*>& top) {
+  CAFFE_CHECK(bottom[0] != top[0], this->name() << ": in-place convolution is not allowed");
+  RRAM_CALL(rram_conv2d_fwd(&desc_, bottom[0]->gpu_data(), this->blobs_[0]->gpu_data(),
+                            bias_term_ ? this->blobs_[1]->gpu_data() : nullptr,
+                            top[0]->mutable_gpu_data(), fused_relu ? 1 : 0, Caffe::stream()));
+}
+
+template <typename Dtype>
+void ConvolutionLayer<Dtype>::Backward_gpu(const std::vector<Blob<Dtype>*>& top,
+                                           const std::vector<bool>& pd,
+                                           const std::vector<Blob<Dtype>*>& bottom) {
+  const bool dw = this->param_propagate_down(0);
+  const bool db = bias_term_ && this->param_propagate_down(1);
+  const bool dx = pd.size() > 0 && pd[0];
+  if (!dw && !db && !dx) return;
+  size_t need = rram_conv2d_bwd_workspace(&desc_, 1);
+  // chunk up to 64 images per col buffer (bounded at 1 GiB)
+  int imgs = std::max(1, std::min(desc_.num, (int)std::min<size_t>(64, (1ull << 30) / std::max<size_t>(need, 1))));
+  void* ws = Caffe::workspace(need * imgs);
+  RRAM_CALL(rram_conv2d_bwd(&desc_, bottom[0]->gpu_data(), this->blobs_[0]->gpu_data(),
+                            top[0]->gpu_diff(), dw ? this->blobs_[0]->mutable_gpu_diff() : nullptr,
+                            db ? this->blobs_[1]->mutable_gpu_diff() : nullptr,
+                            dx ? bottom[0]->mutable_gpu_diff() : nullptr, ws, Caffe::workspace_size(),
+                            Caffe::stream()));
+}
+
+// ★ ------------------------------------------------------ InnerProduct
+template <typename Dtype>
+void InnerProductLayer<Dtype>::LayerSetUp(const std::vector<Blob<Dtype>*>& bottom,
+                                          const std::vector<Blob<Dtype>*>& top) {
+  const Msg& ip = this->layer_param_.sub_or_empty("inner_product_param");
+  N_ = static_cast<int>(ip.integer("num_output", 0));
+  CAFFE_CHECK(N_ > 0, this->name() << ": num_output must be > 0");
+  bias_term_ = ip.boolean("bias_term", true);
+  transpose_ = ip.boolean("transpose", false);
+  axis_ = static_cast<int>(ip.integer("axis", 1));
+  if (axis_ < 0) axis_ += bottom[0]->num_axes();
+  K_ = static_cast<int>(bottom[0]->count(axis_));
+  this->blobs_.clear();
+  this->blobs_.push_back(std::make_shared<Blob<Dtype>>(
+      transpose_ ? std::vector<int>{K_, N_} : std::vector<int>{N_, K_}));
+  const uint64_t seed = Caffe::seed() ^ (uint64_t)hash32(this->name()) << 20;
+  FillBlob(this->blobs_[0].get(), ip.sub_or_empty("weight_filler"), seed, 0);
+  if (bias_term_) {
+    this->blobs_.push_back(std::make_shared<Blob<Dtype>>(std::vector<int>{N_}));
+    FillBlob(this->blobs_[1].get(), ip.sub_or_empty("bias_filler"), seed, 1);
+  }
+  this->param_propagate_down_.assign(this->blobs_.size(), true);
+}
+
+template <typename Dtype>
+void InnerProductLayer<Dtype>::Reshape(const std::vector<Blob<Dtype>*>& bottom,
+                                       const std::vector<Blob<Dtype>*>& top) {
+  CAFFE_CHECK(bottom[0]->count(axis_) == K_, this->name() << ": input size incompatible with weights");
+  M_ = static_cast<int>(bottom[0]->count(0, axis_));
+  std::vector<int> s(bottom[0]->shape().begin(), bottom[0]->shape().begin() + axis_);
+  s.push_back(N_);
+  top[0]->Reshape(s);
+}
+
+template <typename Dtype>
+void InnerProductLayer<Dtype>::Forward_gpu(const std::vector<Blob<Dtype>*>& bottom,
+                                           const std::vector<Blob<Dtype>*>& top) {
+  // split-K partials need up to 16 x M x N floats
+  const size_t ws_need = (size_t)16 * M_ * N_ * sizeof(float);
+  void* ws = Caffe::workspace(std::min<size_t>(ws_need, 256ull << 20));
+  RRAM_CALL(rram_ip_fwd(bottom[0]->gpu_data(), this->blobs_[0]->gpu_data(),
+                        bias_term_ ? this->blobs_[1]->gpu_data() : nullptr,
+                        top[0]->mutable_gpu_data(), M_, N_, K_, transpose_ ? 1 : 0,
+                        fused_relu ? 1 : 0, ws, Caffe::workspace_size(), Caffe::stream()));
+}
+
+template <typename Dtype>
+void InnerProductLayer<Dtype>::Backward_gpu(const std::vector<Blob<Dtype>*>& top,
+                                            const std::vector<bool>& pd,
+                                            const std::vector<Blob<Dtype>*>& bottom) {
+  RRAM_CALL(rram_ip_bwd(bottom[0]->gpu_data(), this->blobs_[0]->gpu_data(), top[0]->gpu_diff(),
+                        this->param_propagate_down(0) ? this->blobs_[0]->mutable_gpu_diff() : nullptr,
+                        (bias_term_ && this->param_propagate_down(1)) ? this->blobs_[1]->mutable_gpu_diff() : nullptr,
+                        (pd.size() && pd[0]) ? bottom[0]->mutable_gpu_diff() : nullptr, M_, N_, K_,
+                        transpose_ ? 1 : 0, Caffe::stream()));
+}
+
+// ------------------------------------------------------------------ ReLU
+template <typename Dtype>
+void ReLULayer<Dtype>::Forward_gpu(const std::vector<Blob<Dtype>*>& bottom,
+                                   const std::vector<Blob<Dtype>*>& top) {
+  if (folded) return;  // applied in the producer's GEMM epilogue
+  RRAM_CALL(rram_relu_fwd(bottom[0]->gpu_data(), top[0]->mutable_gpu_data(), bottom[0]->count(),
+                          negative_slope(), Caffe::stream()));
+}
+template <typename Dtype>
+void ReLULayer<Dtype>::Backward_gpu(const std::vector<Blob<Dtype>*>& top, const std::vector<bool>& pd,
+                                    const std::vector<Blob<Dtype>*>& bottom) {
+  if (!pd.size() || !pd[0]) return;
+  // in-place: bottom data is the ReLU output; x > 0 <=> y > 0 for slope 0 (relu_layer.cu:35-44)
+  RRAM_CALL(rram_relu_bwd(bottom[0]->gpu_data(), top[0]->gpu_diff(), bottom[0]->mutable_gpu_diff(),
+                          bottom[0]->count(), negative_slope(), Caffe::stream()));
+}
+
+// ----------------------------------------------------------------- Split
+template <typename Dtype>
+void SplitLayer<Dtype>::Reshape(const std::vector<Blob<Dtype>*>& bottom,
+                                const std::vector<Blob<Dtype>*>& top) {
+  for (auto* t : top) {
+    t->ReshapeLike(*bottom[0]);
+    t->ShareData(*bottom[0]);
+  }
+}
+template <typename Dtype>
+void SplitLayer<Dtype>::Backward_gpu(const std::vector<Blob<Dtype>*>& top, const std::vector<bool>& pd,
+                                     const std::vector<Blob<Dtype>*>& bottom) {
+  if (!pd.size() || !pd[0]) return;
+  const int64_t n = bottom[0]->count();
+  if (top.size() == 1) {
+    HIP_CALL(hipMemcpyAsync(bottom[0]->mutable_gpu_diff(), top[0]->gpu_diff(), n * sizeof(Dtype),
+                            hipMemcpyDeviceToDevice, Caffe::hip_stream()));
+    return;
+  }
+  RRAM_CALL(rram_add(n, top[0]->gpu_diff(), top[1]->gpu_diff(), bottom[0]->mutable_gpu_diff(), Caffe::stream()));
+  for (size_t i = 2; i < top.size(); ++i)
+    RRAM_CALL(rram_axpy(n, 1.0f, top[i]->gpu_diff(), bottom[0]->mutable_gpu_diff(), Caffe::stream()));
+}
+
+// --------------------------------------------------------------- Pooling
+template <typename Dtype>
+class PoolingLayer : public Layer<Dtype> {
+ public:
+  explicit PoolingLayer(const Msg& p) : Layer<Dtype>(p) {}
+  const char* type() const override { return "Pooling"; }
+  int ExactNumBottomBlobs() const override { return 1; }
+  int ExactNumTopBlobs() const override { return 1; }
+  void LayerSetUp(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>&) override {
+    const Msg& pp = this->layer_param_.sub_or_empty("pooling_param");
+    const std::string pool = pp.str("pool", "MAX");
+    CAFFE_CHECK(pool == "MAX" || pool == "AVE", this->name() << ": pool " << pool << " not supported");
+    method_ = pool == "MAX" ? RRAM_POOL_MAX : RRAM_POOL_AVE;
+    global_ = pp.boolean("global_pooling", false);
+    hw_param(pp, "kernel", 0, kh_, kw_);
+    hw_param(pp, "stride", 1, sh_, sw_);
+    hw_param(pp, "pad", 0, ph_, pw_);
+    if (!global_) CAFFE_CHECK(kh_ > 0 && kw_ > 0, this->name() << ": kernel size required");
+    (void)bottom;
+  }
+  void Reshape(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
+    C_ = bottom[0]->shape(1);
+    H_ = bottom[0]->shape(2);
+    W_ = bottom[0]->shape(3);
+    if (global_) {
+      kh_ = H_;
+      kw_ = W_;
+    }
+    // pooling_layer.cpp:90-104
+    PH_ = (int)std::ceil((float)(H_ + 2 * ph_ - kh_) / sh_) + 1;
+    PW_ = (int)std::ceil((float)(W_ + 2 * pw_ - kw_) / sw_) + 1;
+    if (ph_ || pw_) {
+      if ((PH_ - 1) * sh_ >= H_ + ph_) --PH_;
+      if ((PW_ - 1) * sw_ >= W_ + pw_) --PW_;
+    }
+    top[0]->Reshape({bottom[0]->shape(0), C_, PH_, PW_});
+    if (method_ == RRAM_POOL_MAX) mask_.Reshape(top[0]->shape());
+  }
+
+ protected:
+  void Forward_gpu(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
+    int* mask = (method_ == RRAM_POOL_MAX && this->phase_ == TRAIN)
+                    ? reinterpret_cast<int*>(mask_.mutable_gpu_data()) : nullptr;
+    RRAM_CALL(rram_pool_fwd(bottom[0]->gpu_data(), top[0]->mutable_gpu_data(), mask, bottom[0]->shape(0),
+                            C_, H_, W_, PH_, PW_, kh_, kw_, sh_, sw_, ph_, pw_, method_, Caffe::stream()));
+  }
+  void Backward_gpu(const std::vector<Blob<Dtype>*>& top, const std::vector<bool>& pd,
+                    const std::vector<Blob<Dtype>*>& bottom) override {
+    if (!pd.size() || !pd[0]) return;
+    CAFFE_CHECK(method_ != RRAM_POOL_MAX || this->phase_ == TRAIN, "MAX pool backward needs TRAIN phase");
+    RRAM_CALL(rram_pool_bwd(top[0]->gpu_diff(),
+                            method_ == RRAM_POOL_MAX ? reinterpret_cast<const int*>(mask_.gpu_data()) : nullptr,
+                            bottom[0]->mutable_gpu_diff(), bottom[0]->shape(0), C_, H_, W_, PH_, PW_, kh_,
+                            kw_, sh_, sw_, ph_, pw_, method_, Caffe::stream()));
+  }
+  int method_ = RRAM_POOL_MAX, kh_ = 0, kw_ = 0, sh_ = 1, sw_ = 1, ph_ = 0, pw_ = 0;
+  int C_ = 0, H_ = 0, W_ = 0, PH_ = 0, PW_ = 0;
+  bool global_ = false;
+  Blob<Dtype> mask_;
+};
+
+// -------------------------------------------------------------------- LRN
+template <typename Dtype>
+class LRNLayer : public Layer<Dtype> {
+ public:
+  explicit LRNLayer(const Msg& p) : Layer<Dtype>(p) {}
+  const char* type() const override { return "LRN"; }
+  int ExactNumBottomBlobs() const override { return 1; }
+  int ExactNumTopBlobs() const override { return 1; }
+  void LayerSetUp(const std::vector<Blob<Dtype>*>&, const std::vector<Blob<Dtype>*>&) override {
+    const Msg& lp = this->layer_param_.sub_or_empty("lrn_param");
+    size_ = (int)lp.integer("local_size", 5);
+    alpha_ = (float)lp.num("alpha", 1.0);
+    beta_ = (float)lp.num("beta", 0.75);
+    k_ = (float)lp.num("k", 1.0);
+    const std::string region = lp.str("norm_region", "ACROSS_CHANNELS");
+    CAFFE_CHECK(region == "ACROSS_CHANNELS" || region == "WITHIN_CHANNEL",
+                this->name() << ": unknown norm_region " << region);
+    within_ = region == "WITHIN_CHANNEL";
+    CAFFE_CHECK(size_ % 2 == 1, "LRN only supports odd values for local_size");
+  }
+  void Reshape(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
+    top[0]->ReshapeLike(*bottom[0]);
+    if (this->phase_ == TRAIN) scale_.ReshapeLike(*bottom[0]);
+  }
+
+ protected:
+  void Forward_gpu(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
+    CAFFE_CHECK(bottom[0] != top[0], "LRN cannot run in place");
+    auto& b = *bottom[0];
+    float* sc = this->phase_ == TRAIN ? scale_.mutable_gpu_data() : nullptr;
+    if (within_)
+      RRAM_CALL(rram_lrn_within_fwd(b.gpu_data(), top[0]->mutable_gpu_data(), sc, b.shape(0), b.shape(1),
+                                    b.shape(2), b.shape(3), size_, alpha_, beta_, Caffe::stream()));
+    else
+      RRAM_CALL(rram_lrn_fwd(b.gpu_data(), top[0]->mutable_gpu_data(), sc, b.shape(0), b.shape(1), b.shape(2),
+                             b.shape(3), size_, alpha_, beta_, k_, Caffe::stream()));
+  }
+  void Backward_gpu(const std::vector<Blob<Dtype>*>& top, const std::vector<bool>& pd,
+                    const std::vector<Blob<Dtype>*>& bottom) override {
+    if (!pd.size() || !pd[0]) return;
+    auto& b = *bottom[0];
+    if (within_)
+      RRAM_CALL(rram_lrn_within_bwd(b.gpu_data(), scale_.gpu_data(), top[0]->gpu_diff(), b.mutable_gpu_diff(),
+                                    b.shape(0), b.shape(1), b.shape(2), b.shape(3), size_, alpha_, beta_,
+                                    Caffe::stream()));
+    else
+      RRAM_CALL(rram_lrn_bwd(b.gpu_data(), top[0]->gpu_data(), scale_.gpu_data(), top[0]->gpu_diff(),
+                             b.mutable_gpu_diff(), b.shape(0), b.shape(1), b.shape(2), b.shape(3), size_,
+                             alpha_, beta_, Caffe::stream()));
+  }
+  int size_ = 5;
+  float alpha_ = 1, beta_ = 0.75f, k_ = 1;
+  bool within_ = false;
+  Blob<Dtype> scale_;
+};
+
+// ---------------------------------------------------------------- Dropout
+template <typename Dtype>
+class DropoutLayer : public Layer<Dtype> {
+ public:
+  explicit DropoutLayer(const Msg& p) : Layer<Dtype>(p) {}
+  const char* type() const override { return "Dropout"; }
+  int ExactNumBottomBlobs() const override { return 1; }
+  int ExactNumTopBlobs() const override { return 1; }
+  void Reshape(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
+    ratio_ = (float)this->layer_param_.sub_or_empty("dropout_param").num("dropout_ratio", 0.5);
+    top[0]->ReshapeLike(*bottom[0]);
+    if (this->phase_ == TRAIN) mask_.ReshapeLike(*bottom[0]);
+  }
+
+ protected:
+  void Forward_gpu(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
+    const int64_t n = bottom[0]->count();
+    if (this->phase_ == TRAIN) {
+      RRAM_CALL(rram_dropout_fwd(bottom[0]->gpu_data(), top[0]->mutable_gpu_data(),
+                                 reinterpret_cast<unsigned*>(mask_.mutable_gpu_data()), n, ratio_,
+                                 Caffe::seed(), this->layer_id, this->iter, Caffe::stream()));
+    } else if (bottom[0] != top[0]) {
+      HIP_CALL(hipMemcpyAsync(top[0]->mutable_gpu_data(), bottom[0]->gpu_data(), n * sizeof(Dtype),
+                              hipMemcpyDeviceToDevice, Caffe::hip_stream()));
+    }
+  }
+  void Backward_gpu(const std::vector<Blob<Dtype>*>& top, const std::vector<bool>& pd,
+                    const std::vector<Blob<Dtype>*>& bottom) override {
+    if (!pd.size() || !pd[0]) return;
+    const int64_t n = bottom[0]->count();
+    if (this->phase_ == TRAIN) {
+      RRAM_CALL(rram_dropout_bwd(top[0]->gpu_diff(), reinterpret_cast<const unsigned*>(mask_.gpu_data()),
+                                 bottom[0]->mutable_gpu_diff(), n, ratio_, Caffe::stream()));
+    } else if (bottom[0] != top[0]) {
+      HIP_CALL(hipMemcpyAsync(bottom[0]->mutable_gpu_diff(), top[0]->gpu_diff(), n * sizeof(Dtype),
+                              hipMemcpyDeviceToDevice, Caffe::hip_stream()));
+    }
+  }
+  float ratio_ = 0.5f;
+  Blob<Dtype> mask_;
+};
+
+static void softmax_dims(const Blob<float>& b, int axis, int& outer, int& C, int& inner) {
+  if (axis < 0) axis += b.num_axes();
+  outer = (int)b.count(0, axis);
+  C = b.shape(axis);
+  inner = (int)b.count(axis + 1);
+}
+
+// ---------------------------------------------------------------- Softmax
+template <typename Dtype>
+class SoftmaxLayer : public Layer<Dtype> {
+ public:
+  explicit SoftmaxLayer(const Msg& p) : Layer<Dtype>(p) {}
+  const char* type() const override { return "Softmax"; }
+  int ExactNumBottomBlobs() const override { return 1; }
+  int ExactNumTopBlobs() const override { return 1; }
+  void Reshape(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
+    top[0]->ReshapeLike(*bottom[0]);
+  }
+
+ protected:
+  void Forward_gpu(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
+    int o, c, i;
+    softmax_dims(*bottom[0], (int)this->layer_param_.sub_or_empty("softmax_param").integer("axis", 1), o, c, i);
+    RRAM_CALL(rram_softmax_fwd(bottom[0]->gpu_data(), top[0]->mutable_gpu_data(), o, c, i, Caffe::stream()));
+  }
+  void Backward_gpu(const std::vector<Blob<Dtype>*>&, const std::vector<bool>& pd,
+                    const std::vector<Blob<Dtype>*>&) override {
+    CAFFE_CHECK(!pd.size() || !pd[0], "Softmax backward is not part of this build (use SoftmaxWithLoss)");
+  }
+};
+
+// -------------------------------------------------------- SoftmaxWithLoss
+template <typename Dtype>
+class SoftmaxWithLossLayer : public Layer<Dtype> {
+ public:
+  explicit SoftmaxWithLossLayer(const Msg& p) : Layer<Dtype>(p) {}
+  const char* type() const override { return "SoftmaxWithLoss"; }
+  int ExactNumBottomBlobs() const override { return 2; }
+  int MinTopBlobs() const override { return 1; }
+  bool IsLoss() const override { return true; }
+  void LayerSetUp(const std::vector<Blob<Dtype>*>&, const std::vector<Blob<Dtype>*>&) override {
+    const Msg& lp = this->layer_param_.sub_or_empty("loss_param");
+    ignore_ = lp.has("ignore_label") ? (int)lp.integer("ignore_label") : -1;
+    const std::string norm = lp.str("normalization", lp.has("normalize") ? (lp.boolean("normalize") ? "VALID" : "BATCH_SIZE") : "VALID");
+    CAFFE_CHECK(norm == "VALID" || (norm == "BATCH_SIZE" && ignore_ < 0) || (norm == "FULL" && ignore_ < 0),
+                this->name() << ": loss normalization " << norm << " not supported");
+    axis_ = (int)this->layer_param_.sub_or_empty("softmax_param").integer("axis", 1);
+  }
+  void Reshape(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
+    prob_.ReshapeLike(*bottom[0]);
+    top[0]->Reshape({});
+    if (top.size() > 1) top[1]->ReshapeLike(*bottom[0]);
+  }
+
+ protected:
+  void Forward_gpu(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
+    int o, c, i;
+    softmax_dims(*bottom[0], axis_, o, c, i);
+    RRAM_CALL(rram_softmax_fwd(bottom[0]->gpu_data(), prob_.mutable_gpu_data(), o, c, i, Caffe::stream()));
+    RRAM_CALL(rram_softmax_loss_fwd(prob_.gpu_data(), bottom[1]->gpu_data(), top[0]->mutable_gpu_data(), o,
+                                    c, i, ignore_, Caffe::stream()));
+    if (top.size() > 1)
+      HIP_CALL(hipMemcpyAsync(top[1]->mutable_gpu_data(), prob_.gpu_data(), prob_.count() * sizeof(Dtype),
+                              hipMemcpyDeviceToDevice, Caffe::hip_stream()));
+  }
+  void Backward_gpu(const std::vector<Blob<Dtype>*>&, const std::vector<bool>& pd,
+                    const std::vector<Blob<Dtype>*>& bottom) override {
+    CAFFE_CHECK(pd.size() < 2 || !pd[1], this->name() << " cannot backpropagate to label inputs");
+    if (!pd.size() || !pd[0]) return;
+    int o, c, i;
+    softmax_dims(*bottom[0], axis_, o, c, i);
+    RRAM_CALL(rram_softmax_loss_bwd(prob_.gpu_data(), bottom[1]->gpu_data(), bottom[0]->mutable_gpu_diff(),
+                                    o, c, i, ignore_, this->loss(0), Caffe::stream()));
+  }
+  Blob<Dtype> prob_;
+  int ignore_ = -1, axis_ = 1;
+};
+
+// --------------------------------------------------------------- Accuracy
+template <typename Dtype>
+class AccuracyLayer : public Layer<Dtype> {
+ public:
+  explicit AccuracyLayer(const Msg& p) : Layer<Dtype>(p) {}
+  const char* type() const override { return "Accuracy"; }
+  int ExactNumBottomBlobs() const override { return 2; }
+  int ExactNumTopBlobs() const override { return 1; }
+  void LayerSetUp(const std::vector<Blob<Dtype>*>&, const std::vector<Blob<Dtype>*>&) override {
+    const Msg& ap = this->layer_param_.sub_or_empty("accuracy_param");
+    top_k_ = (int)ap.integer("top_k", 1);
+    axis_ = (int)ap.integer("axis", 1);
+    ignore_ = ap.has("ignore_label") ? (int)ap.integer("ignore_label") : -1;
+  }
+  void Reshape(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
+    int o, c, i;
+    softmax_dims(*bottom[0], axis_, o, c, i);
+    CAFFE_CHECK(top_k_ <= c, "top_k must be less than or equal to the number of classes");
+    CAFFE_CHECK((int64_t)o * i == bottom[1]->count(), "number of labels must match number of predictions");
+    top[0]->Reshape({});
+    counts_.Reshape({2});
+  }
+  bool AllowForceBackward(int) const override { return false; }
+
+ protected:
+  void Forward_gpu(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
+    int o, c, i;
+    softmax_dims(*bottom[0], axis_, o, c, i);
+    float* cnt = counts_.mutable_gpu_data();
+    RRAM_CALL(rram_accuracy(bottom[0]->gpu_data(), bottom[1]->gpu_data(), cnt, cnt + 1,
+                            top[0]->mutable_gpu_data(), o, c, i, top_k_, ignore_, Caffe::stream()));
+  }
+  void Backward_gpu(const std::vector<Blob<Dtype>*>&, const std::vector<bool>&,
+                    const std::vector<Blob<Dtype>*>&) override {}
+  int top_k_ = 1, axis_ = 1, ignore_ = -1;
+  Blob<Dtype> counts_;
+};
+
+// ----------------------------------------------------------------- Concat
+template <typename Dtype>
+class ConcatLayer : public Layer<Dtype> {
+ public:
+  explicit ConcatLayer(const Msg& p) : Layer<Dtype>(p) {}
+  const char* type() const override { return "Concat"; }
+  int MinBottomBlobs() const override { return 1; }
+  int ExactNumTopBlobs() const override { return 1; }
+  void Reshape(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
+    const Msg& cp = this->layer_param_.sub_or_empty("concat_param");
+    int axis = (int)cp.integer("axis", cp.integer("concat_dim", 1));
+    CAFFE_CHECK(axis == 1, this->name() << ": only channel concatenation is supported");
+    std::vector<int> s = bottom[0]->shape();
+    int ch = 0;
+    for (auto* b : bottom) {
+      CAFFE_CHECK(b->num_axes() == (int)s.size() && b->shape(0) == s[0] && b->count(2) == bottom[0]->count(2),
+                  this->name() << ": bottom shapes must match except along the concat axis");
+      ch += b->shape(1);
+    }
+    s[1] = ch;
+    top[0]->Reshape(s);
+  }
+
+ protected:
+  void Forward_gpu(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
+    const int inner = (int)top[0]->count(2), dci = top[0]->shape(1) * inner, num = top[0]->shape(0);
+    int off = 0;
+    for (auto* b : bottom) {
+      const int sci = b->shape(1) * inner;
+      RRAM_CALL(rram_concat_copy(b->gpu_data(), top[0]->mutable_gpu_data(), num, sci, dci, off, 0, Caffe::stream()));
+      off += sci;
+    }
+  }
+  void Backward_gpu(const std::vector<Blob<Dtype>*>& top, const std::vector<bool>& pd,
+                    const std::vector<Blob<Dtype>*>& bottom) override {
+    const int inner = (int)top[0]->count(2), dci = top[0]->shape(1) * inner, num = top[0]->shape(0);
+    int off = 0;
+    for (size_t i = 0; i < bottom.size(); ++i) {
+      const int sci = bottom[i]->shape(1) * inner;
+      if (i < pd.size() && pd[i])
+        RRAM_CALL(rram_concat_copy(bottom[i]->mutable_gpu_diff(), const_cast<float*>(top[0]->gpu_diff()), num,
+                                   sci, dci, off, 1, Caffe::stream()));
+      off += sci;
+    }
+  }
+};
+
+// ----------------------------------------------------- data-like layers
+static std::vector<int> shape_of(const Msg& s) { return ints_of(s, "dim"); }
+
+template <typename Dtype>
+class InputLayer : public Layer<Dtype> {
+ public:
+  explicit InputLayer(const Msg& p) : Layer<Dtype>(p) {}
+  const char* type() const override { return "Input"; }
+  int ExactNumBottomBlobs() const override { return 0; }
+  void LayerSetUp(const std::vector<Blob<Dtype>*>&, const std::vector<Blob<Dtype>*>& top) override {
+    auto shapes = this->layer_param_.sub_or_empty("input_param").subs("shape");
+    CAFFE_CHECK(shapes.size() == 1 || shapes.size() == top.size(),
+                this->name() << ": give one input shape or one per top");
+    for (size_t i = 0; i < top.size(); ++i) top[i]->Reshape(shape_of(*shapes[shapes.size() == 1 ? 0 : i]));
+  }
+  void Reshape(const std::vector<Blob<Dtype>*>&, const std::vector<Blob<Dtype>*>&) override {}
+
+ protected:
+  void Forward_gpu(const std::vector<Blob<Dtype>*>&, const std::vector<Blob<Dtype>*>&) override {}
+  void Backward_gpu(const std::vector<Blob<Dtype>*>&, const std::vector<bool>&,
+                    const std::vector<Blob<Dtype>*>&) override {}
+};
+
+template <typename Dtype>
+class DummyDataLayer : public Layer<Dtype> {
+ public:
+  explicit DummyDataLayer(const Msg& p) : Layer<Dtype>(p) {}
+  const char* type() const override { return "DummyData"; }
+  int ExactNumBottomBlobs() const override { return 0; }
+  void LayerSetUp(const std::vector<Blob<Dtype>*>&, const std::vector<Blob<Dtype>*>& top) override {
+    const Msg& dp = this->layer_param_.sub_or_empty("dummy_data_param");
+    auto shapes = dp.subs("shape");
+    auto fillers = dp.subs("data_filler");
+    for (size_t i = 0; i < top.size(); ++i) {
+      if (!shapes.empty()) {
+        top[i]->Reshape(shape_of(*shapes[shapes.size() == 1 ? 0 : i]));
+      } else {
+        auto g = [&](const char* k) { auto v = dp.nums(k); return v.empty() ? 1 : (int)v[v.size() == 1 ? 0 : i]; };
+        top[i]->Reshape({g("num"), g("channels"), g("height"), g("width")});
+      }
+      static const Msg zero;
+      const Msg& f = fillers.empty() ? zero : *fillers[fillers.size() == 1 ? 0 : i];
+      FillBlob(top[i], f, Caffe::seed() ^ 0xD0D0ull, (uint32_t)(this->layer_id * 16 + i));
+    }
+  }
+  void Reshape(const std::vector<Blob<Dtype>*>&, const std::vector<Blob<Dtype>*>&) override {}
+
+ protected:
+  void Forward_gpu(const std::vector<Blob<Dtype>*>&, const std::vector<Blob<Dtype>*>&) override {}
+  void Backward_gpu(const std::vector<Blob<Dtype>*>&, const std::vector<bool>&,
+                    const std::vector<Blob<Dtype>*>&) override {}
+};
+
+// Data / ImageData / HDF5Data / MemoryData / WindowData: the configs' LMDB /
+// LevelDB / image sources are out of scope, so these tops are
+// synthetic tensors of the shape the source would produce:
+// integer pixels U{0..255}, minus 128 when the layer subtracts a mean, times
+// transform_param.scale; labels U{0..num_classes-1}.  The per-image shape
+// comes from the net option `data_shape` (set via rram_net_create).
+template <typename Dtype>
+class SyntheticDataLayer : public Layer<Dtype> {
+ public:
+  explicit SyntheticDataLayer(const Msg& p) : Layer<Dtype>(p) {}
+  const char* type() const override { return "Data"; }
+  int ExactNumBottomBlobs() const override { return 0; }
+  void LayerSetUp(const std::vector<Blob<Dtype>*>&, const std::vector<Blob<Dtype>*>& top) override {
+    const Msg& p = this->layer_param_;
+    const Msg* dp = nullptr;
+    for (const char* k : {"data_param", "image_data_param", "hdf5_data_param", "memory_data_param", "window_data_param"})
+      if (p.sub(k)) dp = p.sub(k);
+    const int batch = dp ? (int)dp->integer("batch_size", 1) : 1;
+    const Msg& tp = p.sub_or_empty("transform_param");
+    std::vector<int> img = ints_of(p, "rram_data_shape");
+    CAFFE_CHECK(img.size() == 3, this->name() << ": synthetic data needs a C,H,W data_shape option");
+    if (tp.has("crop_size")) img[1] = img[2] = (int)tp.integer("crop_size");
+    std::vector<int> s{batch};
+    s.insert(s.end(), img.begin(), img.end());
+    top[0]->Reshape(s);
+    const float scale = (float)tp.num("scale", 1.0);
+    const bool mean = tp.has("mean_file") || tp.has("mean_value");
+    const uint64_t seed = Caffe::seed() ^ 0xDA7Aull;
+    RRAM_CALL(rram_fill_uniform_int(top[0]->mutable_gpu_data(), top[0]->count(), 256, mean ? -128.0f : 0.0f,
+                                    seed, this->layer_id * 16, Caffe::stream()));
+    if (scale != 1.0f) RRAM_CALL(rram_scal(top[0]->count(), scale, top[0]->mutable_gpu_data(), Caffe::stream()));
+    if (top.size() > 1) {
+      top[1]->Reshape({batch});
+      const int classes = (int)p.integer("rram_num_classes", 10);
+      RRAM_CALL(rram_fill_uniform_int(top[1]->mutable_gpu_data(), batch, classes, 0.0f, seed,
+                                      this->layer_id * 16 + 1, Caffe::stream()));
+    }
+  }
+  void Reshape(const std::vector<Blob<Dtype>*>&, const std::vector<Blob<Dtype>*>&) override {}
+
+ protected:
+  void Forward_gpu(const std::vector<Blob<Dtype>*>&, const std::vector<Blob<Dtype>*>&) override {}
+  void Backward_gpu(const std::vector<Blob<Dtype>*>&, const std::vector<bool>&,
+                    const std::vector<Blob<Dtype>*>&) override {}
+};
+
+REGISTER_LAYER_CLASS(Convolution);
+REGISTER_LAYER_CLASS(InnerProduct);
+REGISTER_LAYER_CLASS(ReLU);
+REGISTER_LAYER_CLASS(Split);
+REGISTER_LAYER_CLASS(Pooling);
+REGISTER_LAYER_CLASS(LRN);
+REGISTER_LAYER_CLASS(Dropout);
+REGISTER_LAYER_CLASS(Softmax);
+REGISTER_LAYER_CLASS(SoftmaxWithLoss);
+REGISTER_LAYER_CLASS(Accuracy);
+REGISTER_LAYER_CLASS(Concat);
+REGISTER_LAYER_CLASS(Input);
+REGISTER_LAYER_CLASS(DummyData);
+static ::caffe::LayerRegisterer<float> g_data_aliases[] = {
+    {"Data", [](const Msg& p) -> std::shared_ptr<Layer<float>> { return std::make_shared<SyntheticDataLayer<float>>(p); }},
+    {"ImageData", [](const Msg& p) -> std::shared_ptr<Layer<float>> { return std::make_shared<SyntheticDataLayer<float>>(p); }},
+    {"HDF5Data", [](const Msg& p) -> std::shared_ptr<Layer<float>> { return std::make_shared<SyntheticDataLayer<float>>(p); }},
+    {"MemoryData", [](const Msg& p) -> std::shared_ptr<Layer<float>> { return std::make_shared<SyntheticDataLayer<float>>(p); }},
+    {"WindowData", [](const Msg& p) -> std::shared_ptr<Layer<float>> { return std::make_shared<SyntheticDataLayer<float>>(p); }},
+};
+
+template class ConvolutionLayer<float>;
+template class InnerProductLayer<float>;
+template class ReLULayer<float>;
+template class SplitLayer<float>;
+
+}  // namespace caffe

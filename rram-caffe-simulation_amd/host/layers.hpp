@@ -1,0 +1,90 @@
+// Concrete layers.  ★ = on the fault-simulation hot path:
+// Convolution (a5/a6), InnerProduct (a7).  The rest are the minimal support
+// layers the configs need, each a thin call into
+// librram_kernels.so.
+#pragma once
+
+#include "layer.hpp"
+
+namespace caffe {
+
+// ★ Convolution (conv_layer.cpp:7-73, base_conv_layer.cpp:11-254): implicit
+// GEMM forward on fp32 MFMA over the whole batch; optional fused ReLU when
+// the net folds a following in-place ReLU into this layer.
+template <typename Dtype>
+class ConvolutionLayer : public Layer<Dtype> {
+ public:
+  explicit ConvolutionLayer(const Msg& p) : Layer<Dtype>(p) {}
+  void LayerSetUp(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override;
+  void Reshape(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override;
+  const char* type() const override { return "Convolution"; }
+  int ExactNumBottomBlobs() const override { return 1; }
+  int ExactNumTopBlobs() const override { return 1; }
+  bool fused_relu = false;
+  const rram_conv_desc& desc() const { return desc_; }
+
+ protected:
+  void Forward_gpu(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override;
+  void Backward_gpu(const std::vector<Blob<Dtype>*>& top, const std::vector<bool>& pd,
+                    const std::vector<Blob<Dtype>*>& bottom) override;
+  rram_conv_desc desc_{};
+  bool bias_term_ = true;
+};
+
+// ★ InnerProduct (inner_product_layer.cpp:9-141, .cu:9-75).
+template <typename Dtype>
+class InnerProductLayer : public Layer<Dtype> {
+ public:
+  explicit InnerProductLayer(const Msg& p) : Layer<Dtype>(p) {}
+  void LayerSetUp(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override;
+  void Reshape(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override;
+  const char* type() const override { return "InnerProduct"; }
+  int ExactNumBottomBlobs() const override { return 1; }
+  int ExactNumTopBlobs() const override { return 1; }
+  bool fused_relu = false;
+  int M() const { return M_; }
+  int N() const { return N_; }
+  int K() const { return K_; }
+
+ protected:
+  void Forward_gpu(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override;
+  void Backward_gpu(const std::vector<Blob<Dtype>*>& top, const std::vector<bool>& pd,
+                    const std::vector<Blob<Dtype>*>& bottom) override;
+  int M_ = 0, N_ = 0, K_ = 0, axis_ = 1;
+  bool bias_term_ = true, transpose_ = false;
+};
+
+template <typename Dtype>
+class ReLULayer : public Layer<Dtype> {
+ public:
+  explicit ReLULayer(const Msg& p) : Layer<Dtype>(p) {}
+  void Reshape(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
+    top[0]->ReshapeLike(*bottom[0]);
+  }
+  const char* type() const override { return "ReLU"; }
+  float negative_slope() const {
+    return static_cast<float>(this->layer_param_.sub_or_empty("relu_param").num("negative_slope", 0.0));
+  }
+  // set by Net when the producing Conv/IP layer applies the ReLU in its epilogue
+  bool folded = false;
+
+ protected:
+  void Forward_gpu(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override;
+  void Backward_gpu(const std::vector<Blob<Dtype>*>& top, const std::vector<bool>& pd,
+                    const std::vector<Blob<Dtype>*>& bottom) override;
+};
+
+template <typename Dtype>
+class SplitLayer : public Layer<Dtype> {
+ public:
+  explicit SplitLayer(const Msg& p) : Layer<Dtype>(p) {}
+  void Reshape(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override;
+  const char* type() const override { return "Split"; }
+
+ protected:
+  void Forward_gpu(const std::vector<Blob<Dtype>*>&, const std::vector<Blob<Dtype>*>&) override {}
+  void Backward_gpu(const std::vector<Blob<Dtype>*>& top, const std::vector<bool>& pd,
+                    const std::vector<Blob<Dtype>*>& bottom) override;
+};
+
+}  // namespace caffe

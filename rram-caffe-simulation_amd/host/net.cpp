@@ -1,0 +1,392 @@
+#include "net.hpp"
+
+#include <algorithm>
+#include <set>
+#include <sstream>
+
+namespace caffe {
+
+static bool rule_matches(const Msg& rule, Phase phase) {
+  if (rule.has("phase")) {
+    const std::string p = rule.str("phase");
+    if ((p == "TRAIN") != (phase == TRAIN)) return false;
+  }
+  // stage / level rules: the configs do not use them; a rule that names a
+  // stage never matches the default (stage-less) net state
+  if (rule.has("stage") || rule.has("min_level") || rule.has("max_level")) return false;
+  return true;
+}
+
+Msg FilterNet(const Msg& param, Phase phase) {
+  CAFFE_CHECK(!param.has("layers"), "V1 'layers' nets are not supported; upgrade to 'layer' (upgrade_net_proto_text)");
+  Msg out;
+  for (auto& f : param.fields) {
+    if (f.first != "layer") {
+      out.fields.push_back(f);
+      continue;
+    }
+    const Msg& l = *f.second.msg;
+    auto inc = l.subs("include");
+    auto exc = l.subs("exclude");
+    CAFFE_CHECK(inc.empty() || exc.empty(), "layer " << l.str("name") << " has both include and exclude rules");
+    bool keep = inc.empty();
+    for (auto* r : exc)
+      if (rule_matches(*r, phase)) keep = false;
+    for (auto* r : inc)
+      if (rule_matches(*r, phase)) keep = true;
+    if (keep) out.fields.push_back(f);
+  }
+  return out;
+}
+
+static std::string split_name(const std::string& blob, const std::string& layer, int top, int k) {
+  std::ostringstream o;
+  o << blob << "_" << layer << "_" << top << "_split_" << k;
+  return o.str();
+}
+
+Msg InsertSplits(const Msg& param) {
+  // collect layers
+  std::vector<std::shared_ptr<Msg>> layers;
+  for (auto& f : param.fields)
+    if (f.first == "layer") layers.push_back(f.second.msg);
+  std::map<std::string, std::pair<int, int>> last_top;
+  std::map<std::pair<int, int>, int> consumers;
+  std::vector<std::vector<std::pair<int, int>>> src(layers.size());
+  for (size_t i = 0; i < layers.size(); ++i) {
+    for (auto& b : layers[i]->strs("bottom")) {
+      auto it = last_top.find(b);
+      CAFFE_CHECK(it != last_top.end(), "Unknown bottom blob '" << b << "' (layer " << layers[i]->str("name") << ")");
+      src[i].push_back(it->second);
+      consumers[it->second]++;
+    }
+    auto tops = layers[i]->strs("top");
+    for (size_t j = 0; j < tops.size(); ++j) last_top[tops[j]] = {(int)i, (int)j};
+  }
+  Msg out;
+  for (auto& f : param.fields)
+    if (f.first != "layer") out.fields.push_back(f);
+  std::map<std::pair<int, int>, int> used;
+  for (size_t i = 0; i < layers.size(); ++i) {
+    Msg l = *layers[i];
+    // rename bottoms that read a split source
+    int bj = 0;
+    for (auto& fld : l.fields) {
+      if (fld.first != "bottom") continue;
+      auto s = src[i][bj++];
+      if (consumers[s] > 1) {
+        const Msg& pl = *layers[s.first];
+        fld.second.scalar = split_name(pl.strs("top")[s.second], pl.str("name"), s.second, used[s]++);
+      }
+    }
+    Value v;
+    v.is_msg = true;
+    v.msg = std::make_shared<Msg>(l);
+    out.fields.emplace_back("layer", v);
+    auto tops = layers[i]->strs("top");
+    for (size_t j = 0; j < tops.size(); ++j) {
+      const int c = consumers[{(int)i, (int)j}];
+      if (c <= 1) continue;
+      Msg& sp = out.add_sub("layer");
+      const std::string lname = layers[i]->str("name");
+      sp.set("name", tops[j] + "_" + lname + "_" + std::to_string(j) + "_split", true);
+      sp.set("type", "Split", true);
+      Value bv;
+      bv.quoted = true;
+      bv.scalar = tops[j];
+      sp.fields.emplace_back("bottom", bv);
+      for (int k = 0; k < c; ++k) {
+        Value tv;
+        tv.quoted = true;
+        tv.scalar = split_name(tops[j], lname, (int)j, k);
+        sp.fields.emplace_back("top", tv);
+      }
+    }
+  }
+  return out;
+}
+
+// Deploy-style top-level inputs (`input:` + `input_shape` / `input_dim`)
+static Msg InputsToLayer(const Msg& param) {
+  auto inputs = param.strs("input");
+  if (inputs.empty()) return param;
+  Msg out;
+  Msg& il = out.add_sub("layer");
+  il.set("name", "input", true);
+  il.set("type", "Input", true);
+  Msg& ip = il.add_sub("input_param");
+  auto shapes = param.subs("input_shape");
+  auto dims = param.nums("input_dim");
+  for (size_t i = 0; i < inputs.size(); ++i) {
+    il.add("top", inputs[i], true);
+    Msg& sh = ip.add_sub("shape");
+    if (!shapes.empty()) {
+      for (double d : shapes[i]->nums("dim")) sh.add("dim", std::to_string((long long)d));
+    } else {
+      CAFFE_CHECK(dims.size() >= 4 * (i + 1), "input_dim must give 4 dims per input");
+      for (int k = 0; k < 4; ++k) sh.add("dim", std::to_string((long long)dims[4 * i + k]));
+    }
+  }
+  for (auto& f : param.fields)
+    if (f.first != "input" && f.first != "input_shape" && f.first != "input_dim") out.fields.push_back(f);
+  return out;
+}
+
+template <typename Dtype>
+Net<Dtype>::Net(const Msg& in_param, Phase phase, const Msg& options) : phase_(phase) {
+  Msg param = InsertSplits(FilterNet(InputsToLayer(in_param), phase));
+  name_ = param.str("name", "net");
+  {
+    std::string fl = options.str("fault_layers", "InnerProduct");
+    std::stringstream ss(fl);
+    std::string t;
+    while (std::getline(ss, t, ',')) fault_layer_types_.push_back(t);
+  }
+  const bool fuse_relu = options.boolean("fuse_relu", true);
+  std::vector<int> data_shape;
+  {
+    std::string ds = options.str("data_shape", "");
+    std::stringstream ss(ds);
+    std::string t;
+    while (std::getline(ss, t, ',')) data_shape.push_back(std::stoi(t));
+  }
+  std::set<std::string> available;  // produced, not yet consumed
+  int lid = 0;
+  for (auto* lp_const : param.subs("layer")) {
+    Msg lp = *lp_const;
+    lp.set("phase", phase == TRAIN ? "TRAIN" : "TEST");
+    const std::string type = lp.str("type");
+    if (type == "Data" || type == "ImageData" || type == "HDF5Data" || type == "MemoryData" || type == "WindowData") {
+      for (int d : data_shape) lp.add("rram_data_shape", std::to_string(d));
+      lp.set("rram_num_classes", options.str("num_classes", "10"));
+    }
+    auto layer = LayerRegistry<Dtype>::CreateLayer(lp);
+    layer->layer_id = static_cast<uint32_t>(lid);
+    const std::string lname = lp.str("name");
+    CAFFE_CHECK(!layer_names_index_.count(lname), "duplicate layer name " << lname);
+    layer_names_index_[lname] = lid;
+    layer_names_.push_back(lname);
+    layers_.push_back(layer);
+    bottom_vecs_.emplace_back();
+    top_vecs_.emplace_back();
+    bottom_id_vecs_.emplace_back();
+    top_id_vecs_.emplace_back();
+    bottom_need_backward_.emplace_back();
+    // bottoms
+    auto propagate = lp.nums("propagate_down");
+    auto bottoms = lp.strs("bottom");
+    bool need_bw = false;
+    for (size_t j = 0; j < bottoms.size(); ++j) {
+      auto it = blob_names_index_.find(bottoms[j]);
+      CAFFE_CHECK(it != blob_names_index_.end(), "Unknown bottom blob '" << bottoms[j] << "' (layer " << lname << ")");
+      bottom_vecs_[lid].push_back(blobs_[it->second].get());
+      bottom_id_vecs_[lid].push_back(it->second);
+      available.erase(bottoms[j]);
+      bool nb = blob_need_backward_flag(it->second);
+      if (!propagate.empty()) nb = nb && propagate[j] != 0;
+      bottom_need_backward_[lid].push_back(nb);
+      need_bw = need_bw || nb;
+    }
+    // tops (in place when a top reuses a bottom name)
+    auto tops = lp.strs("top");
+    for (size_t j = 0; j < tops.size(); ++j) {
+      int id;
+      if (j < bottoms.size() && bottoms[j] == tops[j]) {
+        id = blob_names_index_[tops[j]];
+      } else {
+        CAFFE_CHECK(!blob_names_index_.count(tops[j]), "top blob '" << tops[j] << "' produced twice (layer " << lname << ")");
+        id = static_cast<int>(blobs_.size());
+        blobs_.push_back(std::make_shared<Blob<Dtype>>());
+        blob_names_.push_back(tops[j]);
+        blob_names_index_[tops[j]] = id;
+        blob_need_backward_.push_back(false);
+      }
+      top_vecs_[lid].push_back(blobs_[id].get());
+      top_id_vecs_[lid].push_back(id);
+      available.insert(tops[j]);
+    }
+    layer->SetUp(bottom_vecs_[lid], top_vecs_[lid]);
+    for (size_t j = 0; j < tops.size(); ++j) {
+      const float lw = static_cast<float>(layer->loss(static_cast<int>(j)));
+      if ((int)blob_loss_weights_.size() <= top_id_vecs_[lid][j]) blob_loss_weights_.resize(top_id_vecs_[lid][j] + 1, 0.f);
+      blob_loss_weights_[top_id_vecs_[lid][j]] = lw;
+    }
+    // params
+    auto pspecs = lp.subs("param");
+    for (size_t p = 0; p < layer->blobs().size(); ++p) {
+      AppendParam(lid, static_cast<int>(p), lp);
+      const float lr = p < pspecs.size() ? static_cast<float>(pspecs[p]->num("lr_mult", 1.0)) : 1.0f;
+      layer->set_param_propagate_down(static_cast<int>(p), lr != 0.0f);
+      need_bw = need_bw || lr != 0.0f;
+    }
+    layer_need_backward_.push_back(need_bw);
+    for (int id : top_id_vecs_[lid]) blob_need_backward_[id] = blob_need_backward_[id] || need_bw;
+    // fold an in-place ReLU (slope 0) into the producing Conv / IP epilogue
+    if (fuse_relu && type == "ReLU" && lid > 0 && bottoms.size() == 1 && tops.size() == 1 && bottoms[0] == tops[0]) {
+      auto* relu = dynamic_cast<ReLULayer<Dtype>*>(layer.get());
+      auto& prev = layers_[lid - 1];
+      const bool prev_makes_it = top_id_vecs_[lid - 1].size() == 1 && top_id_vecs_[lid - 1][0] == bottom_id_vecs_[lid][0];
+      if (relu && relu->negative_slope() == 0.0f && prev_makes_it) {
+        if (auto* c = dynamic_cast<ConvolutionLayer<Dtype>*>(prev.get())) {
+          c->fused_relu = true;
+          relu->folded = true;
+        } else if (auto* ip = dynamic_cast<InnerProductLayer<Dtype>*>(prev.get())) {
+          ip->fused_relu = true;
+          relu->folded = true;
+        }
+      }
+    }
+    ++lid;
+  }
+  for (auto& n : available) {
+    const int id = blob_names_index_[n];
+    net_output_blobs_.push_back(blobs_[id].get());
+    net_output_blob_indices_.push_back(id);
+  }
+  blob_loss_weights_.resize(blobs_.size(), 0.f);
+}
+
+template <typename Dtype>
+void Net<Dtype>::AppendParam(int layer_id, int param_id, const Msg& lp) {
+  auto pspecs = lp.subs("param");
+  const Msg* spec = param_id < (int)pspecs.size() ? pspecs[param_id] : nullptr;
+  const std::string pname = spec ? spec->str("name", "") : "";
+  const int net_param_id = static_cast<int>(params_.size());
+  params_.push_back(layers_[layer_id]->blobs()[param_id]);
+  if (!pname.empty() && param_names_index_.count(pname)) {
+    // shared parameter: alias the owner's storage (net.cpp:497-540)
+    const int owner = param_names_index_[pname];
+    param_owners_.push_back(owner);
+    CAFFE_CHECK(params_[owner]->count() == params_[net_param_id]->count(), "shared param '" << pname << "' size mismatch");
+    params_[net_param_id]->ShareData(*params_[owner]);
+    params_[net_param_id]->ShareDiff(*params_[owner]);
+    return;
+  }
+  param_owners_.push_back(-1);
+  if (!pname.empty()) param_names_index_[pname] = net_param_id;
+  const int learnable_id = static_cast<int>(learnable_params_.size());
+  learnable_params_.push_back(params_[net_param_id].get());
+  params_lr_.push_back(spec ? static_cast<float>(spec->num("lr_mult", 1.0)) : 1.0f);
+  params_weight_decay_.push_back(spec ? static_cast<float>(spec->num("decay_mult", 1.0)) : 1.0f);
+  // reference fault registry (net.cpp:482-493): InnerProduct weights + biases
+  const std::string type = layers_[layer_id]->type();
+  if (std::find(fault_layer_types_.begin(), fault_layer_types_.end(), type) != fault_layer_types_.end()) {
+    failure_learnable_params_.push_back(params_[net_param_id].get());
+    failure_learnable_layer_ids_.push_back(layer_id);
+    failure_learnable_param_ids_.push_back(learnable_id);
+    if (type == "InnerProduct" && params_[net_param_id]->num_axes() == 2)
+      fc_params_ids_.push_back(static_cast<int>(failure_learnable_params_.size()) - 1);
+  }
+}
+
+std::string DescribeNet(const Msg& in_param, Phase phase) {
+  Msg param = InsertSplits(FilterNet(InputsToLayer(in_param), phase));
+  std::ostringstream o;
+  auto join = [](const std::vector<std::string>& v) {
+    std::string s;
+    for (size_t i = 0; i < v.size(); ++i) s += (i ? "," : "") + v[i];
+    return s;
+  };
+  for (auto* l : param.subs("layer"))
+    o << l->str("name") << "\t" << l->str("type") << "\t" << join(l->strs("bottom")) << "\t" << join(l->strs("top"))
+      << "\n";
+  return o.str();
+}
+
+template <typename Dtype>
+Dtype Net<Dtype>::ForwardFromTo(int start, int end, bool compute_loss) {
+  for (int i = start; i <= end; ++i) {
+    if (timing_) timer_.start(i);
+    layers_[i]->Forward(bottom_vecs_[i], top_vecs_[i]);
+    if (timing_) timer_.stop(i);
+  }
+  if (!compute_loss) return Dtype(0);
+  // loss = sum over loss tops of weight * value (layer.hpp:451-487); one D2H per loss top
+  Dtype loss = 0;
+  for (int i = start; i <= end; ++i)
+    for (size_t j = 0; j < top_vecs_[i].size(); ++j) {
+      const Dtype w = layers_[i]->loss(static_cast<int>(j));
+      if (w == Dtype(0)) continue;
+      const Blob<Dtype>* t = top_vecs_[i][j];
+      std::vector<Dtype> h(t->count());
+      HIP_CALL(hipMemcpyAsync(h.data(), t->gpu_data(), t->count() * sizeof(Dtype), hipMemcpyDeviceToHost,
+                              Caffe::hip_stream()));
+      HIP_CALL(hipStreamSynchronize(Caffe::hip_stream()));
+      for (Dtype v : h) loss += w * v;
+    }
+  return loss;
+}
+
+template <typename Dtype>
+Dtype Net<Dtype>::Forward(bool compute_loss) {
+  return ForwardFromTo(0, static_cast<int>(layers_.size()) - 1, compute_loss);
+}
+
+template <typename Dtype>
+void Net<Dtype>::Backward() {
+  for (int i = static_cast<int>(layers_.size()) - 1; i >= 0; --i)
+    if (layer_need_backward_[i]) layers_[i]->Backward(top_vecs_[i], bottom_need_backward_[i], bottom_vecs_[i]);
+}
+
+template <typename Dtype>
+void Net<Dtype>::Update() {
+  for (auto* p : learnable_params_) p->Update();
+}
+
+template <typename Dtype>
+void Net<Dtype>::ClearParamDiffs() {
+  for (auto* p : learnable_params_)
+    HIP_CALL(hipMemsetAsync(p->mutable_gpu_diff(), 0, p->count() * sizeof(Dtype), Caffe::hip_stream()));
+}
+
+template <typename Dtype>
+void Net<Dtype>::ShareTrainedLayersWith(const Net* other) {
+  for (size_t i = 0; i < other->layers_.size(); ++i) {
+    auto it = layer_names_index_.find(other->layer_names_[i]);
+    if (it == layer_names_index_.end()) continue;
+    auto& mine = layers_[it->second]->blobs();
+    auto& src = other->layers_[i]->blobs();
+    CAFFE_CHECK(mine.size() == src.size(), "Incompatible number of blobs for layer " << other->layer_names_[i]);
+    for (size_t j = 0; j < mine.size(); ++j) {
+      CAFFE_CHECK(mine[j]->shape() == src[j]->shape(), "Cannot share param " << j << " of layer "
+                  << other->layer_names_[i] << ": shape mismatch " << mine[j]->shape_string() << " vs " << src[j]->shape_string());
+      mine[j]->ShareData(*src[j]);
+    }
+  }
+}
+
+template <typename Dtype>
+std::shared_ptr<Blob<Dtype>> Net<Dtype>::blob_by_name(const std::string& n) const {
+  auto it = blob_names_index_.find(n);
+  return it == blob_names_index_.end() ? nullptr : blobs_[it->second];
+}
+template <typename Dtype>
+std::shared_ptr<Layer<Dtype>> Net<Dtype>::layer_by_name(const std::string& n) const {
+  auto it = layer_names_index_.find(n);
+  return it == layer_names_index_.end() ? nullptr : layers_[it->second];
+}
+
+template <typename Dtype>
+int64_t Net<Dtype>::flat_param_count() const {
+  int64_t n = 0;
+  for (auto* p : learnable_params_) n += p->count();
+  return n;
+}
+
+template <typename Dtype>
+void Net<Dtype>::alias_flat_params(Dtype* data, Dtype* diff) {
+  int64_t off = 0;
+  for (auto* p : learnable_params_) {
+    const int64_t n = p->count();
+    HIP_CALL(hipMemcpyAsync(data + off, p->gpu_data(), n * sizeof(Dtype), hipMemcpyDeviceToDevice, Caffe::hip_stream()));
+    HIP_CALL(hipMemsetAsync(diff + off, 0, n * sizeof(Dtype), Caffe::hip_stream()));
+    p->set_gpu_data(data + off);
+    p->set_gpu_diff(diff + off);
+    off += n;
+  }
+  HIP_CALL(hipStreamSynchronize(Caffe::hip_stream()));
+}
+
+template class Net<float>;
+
+}  // namespace caffe

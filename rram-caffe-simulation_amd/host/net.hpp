@@ -1,0 +1,113 @@
+// Net<Dtype>: the layer DAG (src/caffe/net.cpp, include/caffe/net.hpp).
+// Keeps the reference's fault-parameter registry: failure_learnable_params()
+// holds the weights and biases of every InnerProduct layer and fc_params_ids_
+// the 2-D ones (net.cpp:482-493, net.hpp:181-186).
+#pragma once
+
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "layers.hpp"
+#include "timer.hpp"
+
+namespace caffe {
+
+template <typename Dtype>
+class Net {
+ public:
+  // options: data_shape ("C,H,W" for synthetic Data layers), num_classes,
+  // fault_layers ("InnerProduct" = reference; "InnerProduct,Convolution" = extension),
+  // fuse_relu (true).
+  Net(const Msg& param, Phase phase, const Msg& options = Msg());
+
+  Dtype Forward(bool compute_loss = true);
+  Dtype ForwardFromTo(int start, int end, bool compute_loss = true);
+  void Backward();
+  Dtype ForwardBackward() {
+    Dtype l = Forward(true);
+    Backward();
+    return l;
+  }
+  void Update();
+  void ClearParamDiffs();
+  void ShareTrainedLayersWith(const Net* other);
+
+  const std::string& name() const { return name_; }
+  Phase phase() const { return phase_; }
+  const std::vector<std::shared_ptr<Layer<Dtype>>>& layers() const { return layers_; }
+  const std::vector<std::string>& layer_names() const { return layer_names_; }
+  const std::vector<std::shared_ptr<Blob<Dtype>>>& blobs() const { return blobs_; }
+  const std::vector<std::string>& blob_names() const { return blob_names_; }
+  const std::vector<Blob<Dtype>*>& learnable_params() const { return learnable_params_; }
+  const std::vector<float>& params_lr() const { return params_lr_; }
+  const std::vector<float>& params_weight_decay() const { return params_weight_decay_; }
+  const std::vector<Blob<Dtype>*>& failure_learnable_params() const { return failure_learnable_params_; }
+  const std::vector<int>& failure_learnable_layer_ids() const { return failure_learnable_layer_ids_; }
+  // index into learnable_params() of each failure param (fixes Appendix A Q6)
+  const std::vector<int>& failure_learnable_param_ids() const { return failure_learnable_param_ids_; }
+  std::vector<int> fc_params_ids_;
+  const std::vector<Blob<Dtype>*>& output_blobs() const { return net_output_blobs_; }
+  const std::vector<int>& output_blob_indices() const { return net_output_blob_indices_; }
+  const std::vector<float>& blob_loss_weights() const { return blob_loss_weights_; }
+  std::shared_ptr<Blob<Dtype>> blob_by_name(const std::string& n) const;
+  std::shared_ptr<Layer<Dtype>> layer_by_name(const std::string& n) const;
+  bool has_blob(const std::string& n) const { return blob_names_index_.count(n) > 0; }
+
+  // Flat learnable-parameter buffers (parallel.cpp:25-115 GPUParams): copies
+  // the current values into `data` / zeroes `diff` and aliases every learnable
+  // param into them, so one all-reduce covers all gradients.
+  int64_t flat_param_count() const;
+  void alias_flat_params(Dtype* data, Dtype* diff);
+
+  void set_iter(uint64_t it) {
+    for (auto& l : layers_) l->iter = it;
+  }
+
+  // per-layer forward timing with hipEvents (`caffe time`, tools/caffe.cpp:334-421)
+  void set_timing(bool on) { timing_ = on; }
+  EventTimer& timer() { return timer_; }
+
+ private:
+  bool timing_ = false;
+  EventTimer timer_;
+  void AppendParam(int layer_id, int param_id, const Msg& layer_param);
+
+  std::string name_;
+  Phase phase_;
+  std::vector<std::shared_ptr<Layer<Dtype>>> layers_;
+  std::vector<std::string> layer_names_;
+  std::map<std::string, int> layer_names_index_;
+  std::vector<std::shared_ptr<Blob<Dtype>>> blobs_;
+  std::vector<std::string> blob_names_;
+  std::map<std::string, int> blob_names_index_;
+  std::vector<std::vector<Blob<Dtype>*>> bottom_vecs_, top_vecs_;
+  std::vector<std::vector<int>> bottom_id_vecs_, top_id_vecs_;
+  std::vector<std::vector<bool>> bottom_need_backward_;
+  std::vector<bool> layer_need_backward_;
+  std::vector<bool> blob_need_backward_;
+  bool blob_need_backward_flag(int id) const { return blob_need_backward_[id]; }
+  std::vector<std::shared_ptr<Blob<Dtype>>> params_;
+  std::vector<Blob<Dtype>*> learnable_params_;
+  std::vector<float> params_lr_, params_weight_decay_;
+  std::vector<int> param_owners_;
+  std::map<std::string, int> param_names_index_;
+  std::vector<Blob<Dtype>*> failure_learnable_params_;
+  std::vector<int> failure_learnable_layer_ids_, failure_learnable_param_ids_;
+  std::vector<Blob<Dtype>*> net_output_blobs_;
+  std::vector<int> net_output_blob_indices_;
+  std::vector<float> blob_loss_weights_;
+  std::vector<std::string> fault_layer_types_;
+};
+
+// Phase/rule filtering (net.cpp FilterNet + StateMeetsRule, phase only) and
+// split insertion for blobs consumed more than once (insert_splits.cpp).
+Msg FilterNet(const Msg& param, Phase phase);
+Msg InsertSplits(const Msg& param);
+// Structural description after input conversion, phase filtering and split
+// insertion: one line per layer "name\ttype\tbottoms\ttops" (comma-joined).
+// Pure host logic (no device), used by the CPU tests.
+std::string DescribeNet(const Msg& param, Phase phase);
+
+}  // namespace caffe

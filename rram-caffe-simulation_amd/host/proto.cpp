@@ -243,6 +243,12 @@ void Msg::set(const std::string& k, const std::string& v, bool quoted) {
   val.quoted = quoted;
   fields.emplace_back(k, val);
 }
+void Msg::add(const std::string& k, const std::string& v, bool quoted) {
+  Value val;
+  val.scalar = v;
+  val.quoted = quoted;
+  fields.emplace_back(k, val);
+}
 Msg& Msg::add_sub(const std::string& k) {
   Value v;
   v.is_msg = true;

@@ -48,6 +48,7 @@ class Msg {
 
   // mutation helpers (used for programmatic nets / overrides)
   void set(const std::string& k, const std::string& v, bool quoted = false);
+  void add(const std::string& k, const std::string& v, bool quoted = false);  // repeated
   Msg& add_sub(const std::string& k);
 
   std::string debug_string(int indent = 0) const;

@@ -1,0 +1,519 @@
+#include "solver.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <sstream>
+
+namespace caffe {
+
+// ============================================================ FailureMaker
+template <typename Dtype>
+FailureMaker<Dtype>::~FailureMaker() {
+  if (d_counts_) (void)hipFree(d_counts_);
+}
+
+template <typename Dtype>
+std::shared_ptr<FailureMaker<Dtype>> FailureMaker<Dtype>::CreateMaker(const Msg& param,
+                                                                      std::shared_ptr<Net<Dtype>> net) {
+  const std::string type = param.str("type", "gaussian");
+  if (type == "gaussian") return std::make_shared<GaussianFailureMaker<Dtype>>(param, net);
+  CAFFE_CHECK(type != "uniform", "failure_pattern type 'uniform' is declared in caffe.proto but not implemented "
+                                 "by the reference either (Appendix A Q13)");
+  return nullptr;
+}
+
+template <typename Dtype>
+std::vector<Blob<Dtype>*> FailureMaker<Dtype>::fail_iterations() {
+  std::vector<Blob<Dtype>*> v;
+  for (auto& b : fail_iterations_) v.push_back(b.get());
+  return v;
+}
+
+template <typename Dtype>
+std::vector<unsigned long long> FailureMaker<Dtype>::broken_counts() {
+  std::vector<unsigned long long> h(fail_iterations_.size(), 0);
+  if (d_counts_ && !h.empty()) {
+    HIP_CALL(hipMemcpyAsync(h.data(), d_counts_, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                            Caffe::hip_stream()));
+    HIP_CALL(hipStreamSynchronize(Caffe::hip_stream()));
+  }
+  return h;
+}
+
+// failure_maker.cpp:5-52
+template <typename Dtype>
+GaussianFailureMaker<Dtype>::GaussianFailureMaker(const Msg& param, std::shared_ptr<Net<Dtype>> net)
+    : FailureMaker<Dtype>(param) {
+  this->net_ = net;
+  long long neg = 10, zero = 20, pos = 10;  // defaults (failure_maker.cpp:17-21)
+  if (const Msg* fp = param.sub("failure_prob")) {
+    neg = fp->integer("neg", 10);
+    zero = fp->integer("zero", 20);
+    pos = fp->integer("pos", 10);
+    CAFFE_CHECK(neg >= 0, "Probability for failure to -1 must be greater or equal than 0");
+    CAFFE_CHECK(zero >= 0, "Probability for failure to 0 must be greater or equal than 0");
+    CAFFE_CHECK(pos >= 0, "Probability for failure to 1 must be greater or equal than 0");
+  }
+  const long long sum = neg + zero + pos;
+  CAFFE_CHECK(sum > 0, "failure_prob entries sum to 0");
+  const uint64_t thr_neg = ((uint64_t)neg * (1ull << 32) + sum - 1) / sum;
+  const uint64_t thr_zero = ((uint64_t)(neg + zero) * (1ull << 32) + sum - 1) / sum;
+  const float mean = static_cast<float>(param.num("mean", 10000));  // caffe.proto:255 defaults
+  const float std = static_cast<float>(param.num("std", 100));
+  decrement = static_cast<float>(param.num("rram_decrement", 100.0));
+  const auto& fps = net->failure_learnable_params();
+  for (size_t i = 0; i < fps.size(); ++i) {
+    auto b = std::make_unique<Blob<Dtype>>(fps[i]->shape());
+    RRAM_CALL(rram_fault_init(b->mutable_gpu_data(), b->mutable_gpu_diff(), b->count(), mean, std, thr_neg,
+                              thr_zero, Caffe::seed(), 0u, static_cast<uint32_t>(i), Caffe::stream()));
+    this->fail_iterations_.push_back(std::move(b));
+  }
+  if (!fps.empty()) {
+    HIP_CALL(hipMalloc(&this->d_counts_, fps.size() * sizeof(unsigned long long)));
+    HIP_CALL(hipMemsetAsync(this->d_counts_, 0, fps.size() * sizeof(unsigned long long), Caffe::hip_stream()));
+  }
+}
+
+// failure_maker.cu:44-58 — all blobs in batched launches of <= RRAM_MAX_SEGS
+template <typename Dtype>
+void GaussianFailureMaker<Dtype>::Fail_gpu(int /*iter*/) {
+  const auto& fps = this->net_->failure_learnable_params();
+  const size_t n = fps.size();
+  if (!n) return;
+  HIP_CALL(hipMemsetAsync(this->d_counts_, 0, n * sizeof(unsigned long long), Caffe::hip_stream()));
+  std::vector<rram_fail_seg> segs(n);
+  for (size_t i = 0; i < n; ++i) {
+    auto& fi = this->fail_iterations_[i];
+    segs[i] = rram_fail_seg{fps[i]->gpu_diff(), fps[i]->mutable_gpu_data(), fi->mutable_gpu_data(), fi->gpu_diff(),
+                            fps[i]->count()};
+  }
+  for (size_t s = 0; s < n; s += RRAM_MAX_SEGS) {
+    const int k = static_cast<int>(std::min<size_t>(RRAM_MAX_SEGS, n - s));
+    RRAM_CALL(rram_fail_apply_batched(segs.data() + s, k, decrement, epsilon, this->d_counts_ + s, Caffe::stream()));
+  }
+}
+
+// ============================================================ strategies
+template <typename Dtype>
+std::shared_ptr<FailureStrategy<Dtype>> FailureStrategy<Dtype>::CreateStrategy(
+    const Msg& param, std::shared_ptr<FailureMaker<Dtype>> fm, std::shared_ptr<Net<Dtype>> net,
+    const Solver<Dtype>* s) {
+  const std::string type = param.str("type");
+  if (type == "threshold") {
+    auto p = std::make_shared<ThresholdFailureStrategy<Dtype>>(param, fm, net, s);
+    p->reference_lr_index = param.boolean("rram_reference_lr_index", false);
+    return p;
+  }
+  if (type == "remapping" || type == "genetic")
+    throw Error("failure_strategy '" + type + "' (periodic FC-neuron remapping) is not part of this build yet "
+                "(SURVEY.md §8f-4)");
+  throw Error("No strategy named `" + type + "` exists.");
+}
+
+template <typename Dtype>
+float ThresholdFailureStrategy<Dtype>::threshold_for(int i) const {
+  const auto& lr = this->net_->params_lr();
+  const int idx = reference_lr_index ? i : this->net_->failure_learnable_param_ids()[i];
+  CAFFE_CHECK(idx < (int)lr.size(), "params_lr index out of range");
+  return threshold() * static_cast<float>(lr[idx]) * static_cast<float>(this->solver_->GetLearningRate());
+}
+
+// strategy.cpp:7-33, on the device (no D2H/H2D round trip)
+template <typename Dtype>
+void ThresholdFailureStrategy<Dtype>::Apply() {
+  const auto& fps = this->net_->failure_learnable_params();
+  for (size_t i = 0; i < fps.size(); ++i)
+    RRAM_CALL(rram_threshold_strategy(fps[i]->mutable_gpu_diff(), fps[i]->count(), threshold_for((int)i), nullptr,
+                                      Caffe::stream()));
+}
+
+// ================================================================ Solver
+static Msg load_net_param(const Msg& sp, const Msg* net_param) {
+  if (net_param) return *net_param;
+  if (const Msg* np = sp.sub("net_param")) return *np;
+  if (const Msg* np = sp.sub("train_net_param")) return *np;
+  std::string f = sp.str("net", sp.str("train_net", ""));
+  CAFFE_CHECK(!f.empty(), "solver: no net given (net / net_param / train_net)");
+  return parse_prototxt_file(f);
+}
+
+template <typename Dtype>
+Solver<Dtype>::Solver(const Msg& sp, const Msg* net_param, const Msg& options) : param_(sp) {
+  if (sp.has("random_seed") && sp.integer("random_seed") >= 0)
+    Caffe::set_random_seed(static_cast<uint64_t>(sp.integer("random_seed")));
+  fused_update_ = options.boolean("fused_update", false);
+  const Msg np = load_net_param(sp, net_param);
+  net_ = std::make_shared<Net<Dtype>>(np, TRAIN, options);
+  // solver.cpp:132-148: fault maker and strategies on the root solver
+  if (const Msg* fp = sp.sub("failure_pattern")) InitFailurePattern(*fp);
+  for (auto* st : sp.subs("failure_strategy")) {
+    auto p = FailureStrategy<Dtype>::CreateStrategy(*st, fmaker_, net_, this);
+    strategys_.push_back(p);
+  }
+  // test nets (solver.cpp:155-230): test_net_param / test_net, else the train net in TEST phase
+  std::vector<Msg> tnp;
+  for (auto* t : sp.subs("test_net_param")) tnp.push_back(*t);
+  for (auto& f : sp.strs("test_net")) tnp.push_back(parse_prototxt_file(f));
+  if (tnp.empty() && sp.count("test_iter") > 0) tnp.push_back(np);
+  for (auto& t : tnp) {
+    test_nets_.push_back(std::make_shared<Net<Dtype>>(t, TEST, options));
+    test_nets_.back()->ShareTrainedLayersWith(net_.get());
+  }
+  for (auto* p : net_->learnable_params()) {
+    history_.push_back(std::make_unique<Blob<Dtype>>(p->shape()));
+    HIP_CALL(hipMemsetAsync(history_.back()->mutable_gpu_data(), 0, p->count() * sizeof(Dtype), Caffe::hip_stream()));
+    temp_.push_back(std::make_unique<Blob<Dtype>>(p->shape()));
+  }
+  CAFFE_CHECK(param_.str("type", "SGD") == "SGD" && param_.str("solver_type", "SGD") == "SGD",
+              "only the SGD solver is part of this build (SURVEY.md §2.1)");
+}
+
+// solver.cpp:14-23
+template <typename Dtype>
+void Solver<Dtype>::InitFailurePattern(const Msg& fp) {
+  if (fp.str("type", "gaussian") == "none") return;
+  fmaker_ = FailureMaker<Dtype>::CreateMaker(fp, net_);
+}
+
+// sgd_solver.cpp GetLearningRate
+template <typename Dtype>
+Dtype Solver<Dtype>::GetLearningRate() const {
+  const std::string policy = param_.str("lr_policy", "fixed");
+  const double base = param_.num("base_lr", 0.01), gamma = param_.num("gamma", 0.0), power = param_.num("power", 0.0);
+  const double it = iter_;
+  if (policy == "fixed") return (Dtype)base;
+  if (policy == "step") return (Dtype)(base * std::pow(gamma, std::floor(it / (double)param_.integer("stepsize", 1))));
+  if (policy == "exp") return (Dtype)(base * std::pow(gamma, it));
+  if (policy == "inv") return (Dtype)(base * std::pow(1.0 + gamma * it, -power));
+  if (policy == "multistep") {
+    auto sv = param_.nums("stepvalue");
+    int step = 0;
+    while (step < (int)sv.size() && it >= sv[step]) ++step;
+    return (Dtype)(base * std::pow(gamma, step));
+  }
+  if (policy == "poly") return (Dtype)(base * std::pow(1.0 - it / (double)param_.integer("max_iter", 1), power));
+  if (policy == "sigmoid")
+    return (Dtype)(base * (1.0 / (1.0 + std::exp(-gamma * (it - (double)param_.integer("stepsize", 1))))));
+  throw Error("Unknown learning rate policy: " + policy);
+}
+
+template <typename Dtype>
+void Solver<Dtype>::ClipGradients() {
+  const double clip = param_.num("clip_gradients", -1.0);
+  if (clip < 0) return;
+  const auto& ps = net_->learnable_params();
+  double sumsq = 0;
+  Dtype* dtmp = nullptr;
+  HIP_CALL(hipMallocAsync(reinterpret_cast<void**>(&dtmp), sizeof(Dtype), Caffe::hip_stream()));
+  for (auto* p : ps) {
+    Dtype h = 0;
+    RRAM_CALL(rram_dot(p->count(), p->gpu_diff(), p->gpu_diff(), dtmp, Caffe::stream()));
+    HIP_CALL(hipMemcpyAsync(&h, dtmp, sizeof(Dtype), hipMemcpyDeviceToHost, Caffe::hip_stream()));
+    HIP_CALL(hipStreamSynchronize(Caffe::hip_stream()));
+    sumsq += h;
+  }
+  HIP_CALL(hipFreeAsync(dtmp, Caffe::hip_stream()));
+  const double l2 = std::sqrt(sumsq);
+  if (l2 > clip)
+    for (auto* p : ps) RRAM_CALL(rram_scal(p->count(), (Dtype)(clip / l2), p->mutable_gpu_diff(), Caffe::stream()));
+}
+
+// sgd_solver.cpp:148-214
+template <typename Dtype>
+void Solver<Dtype>::Regularize(int id) {
+  auto* p = net_->learnable_params()[id];
+  const Dtype decay = (Dtype)param_.num("weight_decay", 0.0) * net_->params_weight_decay()[id];
+  if (decay == Dtype(0)) return;
+  const std::string rt = param_.str("regularization_type", "L2");
+  if (rt == "L2") {
+    RRAM_CALL(rram_axpy(p->count(), decay, p->gpu_data(), p->mutable_gpu_diff(), Caffe::stream()));
+  } else if (rt == "L1") {
+    RRAM_CALL(rram_sign(p->count(), p->gpu_data(), temp_[id]->mutable_gpu_data(), Caffe::stream()));
+    RRAM_CALL(rram_axpy(p->count(), decay, temp_[id]->gpu_data(), p->mutable_gpu_diff(), Caffe::stream()));
+  } else {
+    throw Error("Unknown regularization type: " + rt);
+  }
+}
+
+// sgd_solver.cpp:216-247 (GPU branch: SGDUpdate kernel)
+template <typename Dtype>
+void Solver<Dtype>::ComputeUpdateValue(int id, Dtype rate) {
+  auto* p = net_->learnable_params()[id];
+  const Dtype local = rate * net_->params_lr()[id];
+  RRAM_CALL(rram_sgd_update(p->mutable_gpu_diff(), history_[id]->mutable_gpu_data(), p->count(),
+                            (Dtype)param_.num("momentum", 0.0), local, Caffe::stream()));
+}
+
+// sgd_solver.cpp:101-116 (Normalize for iter_size > 1 folded into a scale)
+template <typename Dtype>
+void Solver<Dtype>::ComputeUpdate() {
+  const Dtype rate = GetLearningRate();
+  ClipGradients();
+  const int iter_size = (int)param_.integer("iter_size", 1);
+  const auto& ps = net_->learnable_params();
+  for (int i = 0; i < (int)ps.size(); ++i) {
+    if (iter_size > 1) RRAM_CALL(rram_scal(ps[i]->count(), Dtype(1) / iter_size, ps[i]->mutable_gpu_diff(), Caffe::stream()));
+    Regularize(i);
+    ComputeUpdateValue(i, rate);
+  }
+}
+
+// solver.cpp:25-33
+template <typename Dtype>
+void Solver<Dtype>::ApplyStrategy() {
+  if (!fmaker_) return;
+  for (auto& s : strategys_) s->Apply();
+}
+
+template <typename Dtype>
+void Solver<Dtype>::ApplyUpdate() {
+  net_->Update();
+}
+
+// Regularize(L2) + SGDUpdate + threshold + Update + Fail in
+// one HBM pass per blob.  Same arithmetic sequence as the separate kernels.
+template <typename Dtype>
+void Solver<Dtype>::FusedTail() {
+  const Dtype rate = GetLearningRate();
+  const auto& ps = net_->learnable_params();
+  const auto& fids = net_->failure_learnable_param_ids();
+  const Dtype mom = (Dtype)param_.num("momentum", 0.0);
+  const Dtype wd = (Dtype)param_.num("weight_decay", 0.0);
+  ThresholdFailureStrategy<Dtype>* thr = nullptr;
+  for (auto& s : strategys_) thr = dynamic_cast<ThresholdFailureStrategy<Dtype>*>(s.get());
+  auto* gm = dynamic_cast<GaussianFailureMaker<Dtype>*>(fmaker_.get());
+  std::vector<Blob<Dtype>*> fi = fmaker_ ? fmaker_->fail_iterations() : std::vector<Blob<Dtype>*>();
+  unsigned long long* counts = fmaker_ ? fmaker_->device_counts() : nullptr;
+  if (counts)
+    HIP_CALL(hipMemsetAsync(counts, 0, fi.size() * sizeof(unsigned long long), Caffe::hip_stream()));
+  for (int i = 0; i < (int)ps.size(); ++i) {
+    int f = -1;
+    for (int k = 0; k < (int)fids.size(); ++k)
+      if (fids[k] == i) f = k;
+    const bool faulty = gm && f >= 0;
+    RRAM_CALL(rram_fused_update_fail(
+        ps[i]->mutable_gpu_data(), ps[i]->mutable_gpu_diff(), history_[i]->mutable_gpu_data(),
+        faulty ? fi[f]->mutable_gpu_data() : nullptr, faulty ? fi[f]->gpu_diff() : nullptr, ps[i]->count(),
+        wd * net_->params_weight_decay()[i], mom, rate * net_->params_lr()[i], (faulty && thr) ? 1 : 0,
+        (faulty && thr) ? thr->threshold_for(f) : 0.0f, gm ? gm->decrement : 100.0f, gm ? gm->epsilon : 1e-20f,
+        (faulty && counts) ? counts + f : nullptr, Caffe::stream()));
+  }
+}
+
+// solver.cpp:237-325 (fork order: ComputeUpdate -> ApplyStrategy -> ApplyUpdate -> Fail)
+template <typename Dtype>
+void Solver<Dtype>::Step(int iters) {
+  const int stop = iter_ + iters;
+  const int display = (int)param_.integer("display", 0);
+  const int test_interval = (int)param_.integer("test_interval", 0);
+  const int average_loss = (int)param_.integer("average_loss", 1);
+  const int iter_size = (int)param_.integer("iter_size", 1);
+  const bool can_fuse = fused_update_ && param_.num("clip_gradients", -1.0) < 0 && iter_size == 1 &&
+                        param_.str("regularization_type", "L2") == "L2";
+  while (iter_ < stop) {
+    net_->ClearParamDiffs();
+    if (test_interval && iter_ % test_interval == 0 && (iter_ > 0 || param_.boolean("test_initialization", true)))
+      TestAll();
+    const bool disp = display && iter_ % display == 0;
+    net_->set_iter((uint64_t)iter_);
+    Dtype loss = 0;
+    for (int i = 0; i < iter_size; ++i) {
+      loss += net_->Forward(disp || average_loss > 1);
+      net_->Backward();
+    }
+    loss /= iter_size;
+    if (disp || average_loss > 1) {
+      if ((int)losses_.size() < average_loss) {
+        losses_.push_back(loss);
+        smoothed_loss_ = (smoothed_loss_ * (losses_.size() - 1) + loss) / losses_.size();
+      } else {
+        const int idx = iter_ % average_loss;
+        smoothed_loss_ += (loss - losses_[idx]) / average_loss;
+        losses_[idx] = loss;
+      }
+    }
+    if (disp) {
+      std::ostringstream o;
+      o << "Iteration " << iter_ << ", loss = " << smoothed_loss_;
+      emit(o.str());
+    }
+    if (on_gradients_ready) on_gradients_ready();
+    if (can_fuse) {
+      FusedTail();
+    } else {
+      ComputeUpdate();
+      ApplyStrategy();
+      ApplyUpdate();
+      Fail(iter_);
+    }
+    ++iter_;
+  }
+}
+
+template <typename Dtype>
+void Solver<Dtype>::Solve() {
+  const int max_iter = (int)param_.integer("max_iter", 0);
+  Step(max_iter - iter_);
+  if (param_.integer("display", 0) && max_iter % std::max<long long>(1, param_.integer("display", 1)) == 0) {
+    std::ostringstream o;
+    o << "Iteration " << iter_ << ", loss = " << smoothed_loss_;
+    emit(o.str());
+  }
+  const int ti = (int)param_.integer("test_interval", 0);
+  if (ti && iter_ % ti == 0) TestAll();
+  emit("Optimization Done.");
+}
+
+template <typename Dtype>
+std::vector<std::vector<Dtype>> Solver<Dtype>::TestAll() {
+  std::vector<std::vector<Dtype>> r;
+  for (int i = 0; i < (int)test_nets_.size(); ++i) r.push_back(Test(i));
+  return r;
+}
+
+// solver.cpp:385-458: mean over test_iter of every output element
+template <typename Dtype>
+std::vector<Dtype> Solver<Dtype>::Test(int id) {
+  CAFFE_CHECK(id >= 0 && id < (int)test_nets_.size(), "test net index out of range");
+  auto tn = test_nets_[id];
+  auto ti = param_.nums("test_iter");
+  const int iters = ti.empty() ? 1 : (int)ti[std::min<size_t>(id, ti.size() - 1)];
+  std::vector<Dtype> score;
+  Dtype loss = 0;
+  for (int it = 0; it < iters; ++it) {
+    loss += tn->Forward(true);
+    int k = 0;
+    for (auto* b : tn->output_blobs()) {
+      std::vector<Dtype> h(b->count());
+      HIP_CALL(hipMemcpyAsync(h.data(), b->gpu_data(), b->count() * sizeof(Dtype), hipMemcpyDeviceToHost,
+                              Caffe::hip_stream()));
+      HIP_CALL(hipStreamSynchronize(Caffe::hip_stream()));
+      for (Dtype v : h) {
+        if (it == 0) score.push_back(v);
+        else score[k] += v;
+        ++k;
+      }
+    }
+  }
+  for (auto& s : score) s /= iters;
+  std::ostringstream o;
+  o << "Iteration " << iter_ << ", Testing net (#" << id << ")";
+  emit(o.str());
+  int k = 0;
+  for (size_t j = 0; j < tn->output_blobs().size(); ++j) {
+    const int bid = tn->output_blob_indices()[j];
+    const float lw = tn->blob_loss_weights()[bid];
+    for (int64_t e = 0; e < tn->output_blobs()[j]->count(); ++e, ++k) {
+      std::ostringstream l;
+      l << "    Test net output #" << k << ": " << tn->blob_names()[bid] << " = " << score[k];
+      if (lw) l << " (* " << lw << " = " << lw * score[k] << " loss)";
+      emit(l.str());
+    }
+  }
+  return score;
+}
+
+// ============================================================ MonteCarlo
+template <typename Dtype>
+MonteCarlo<Dtype>::MonteCarlo(std::shared_ptr<Net<Dtype>> net, const std::vector<rram_inject_cfg>& cfgs,
+                              uint64_t seed, int max_maps)
+    : net_(net), seed_(seed), max_maps_(max_maps) {
+  params_ = net_->failure_learnable_params();
+  CAFFE_CHECK(!params_.empty(), "MonteCarlo: the net has no faultable (InnerProduct) parameters");
+  CAFFE_CHECK(cfgs.size() == 1 || cfgs.size() == params_.size(),
+              "MonteCarlo: give one inject config or one per faultable blob (" << params_.size() << ")");
+  cfgs_ = cfgs;
+  if (cfgs_.size() == 1) cfgs_.resize(params_.size(), cfgs[0]);
+  for (auto* p : params_) {
+    Dtype* c = nullptr;
+    HIP_CALL(hipMalloc(reinterpret_cast<void**>(&c), p->count() * sizeof(Dtype)));
+    HIP_CALL(hipMemcpyAsync(c, p->gpu_data(), p->count() * sizeof(Dtype), hipMemcpyDeviceToDevice, Caffe::hip_stream()));
+    clean_.push_back(c);
+  }
+  for (auto* b : net_->output_blobs())
+    if (b->count() == 1) outs_.push_back(b);
+  const size_t no = std::max<size_t>(outs_.size(), 1);
+  HIP_CALL(hipMalloc(reinterpret_cast<void**>(&d_sums_), no * sizeof(Dtype)));
+  HIP_CALL(hipMalloc(reinterpret_cast<void**>(&d_per_map_), std::max(1, max_maps_) * no * sizeof(Dtype)));
+  HIP_CALL(hipMalloc(reinterpret_cast<void**>(&d_broken_), params_.size() * sizeof(unsigned long long)));
+  Reset();
+}
+
+template <typename Dtype>
+MonteCarlo<Dtype>::~MonteCarlo() {
+  try {
+    RestoreClean();
+    Caffe::synchronize();
+  } catch (...) {
+  }
+  for (auto* c : clean_) (void)hipFree(c);
+  (void)hipFree(d_sums_);
+  (void)hipFree(d_per_map_);
+  (void)hipFree(d_broken_);
+}
+
+template <typename Dtype>
+void MonteCarlo<Dtype>::Reset() {
+  maps_run_ = 0;
+  HIP_CALL(hipMemsetAsync(d_sums_, 0, std::max<size_t>(outs_.size(), 1) * sizeof(Dtype), Caffe::hip_stream()));
+  HIP_CALL(hipMemsetAsync(d_broken_, 0, params_.size() * sizeof(unsigned long long), Caffe::hip_stream()));
+}
+
+template <typename Dtype>
+void MonteCarlo<Dtype>::RestoreClean() {
+  for (size_t i = 0; i < params_.size(); ++i)
+    HIP_CALL(hipMemcpyAsync(params_[i]->mutable_gpu_data(), clean_[i], params_[i]->count() * sizeof(Dtype),
+                            hipMemcpyDeviceToDevice, Caffe::hip_stream()));
+}
+
+template <typename Dtype>
+void MonteCarlo<Dtype>::Run(uint32_t map_begin, uint32_t map_count) {
+  std::vector<rram_inject_seg> segs(params_.size());
+  for (size_t i = 0; i < params_.size(); ++i)
+    segs[i] = rram_inject_seg{clean_[i], params_[i]->mutable_gpu_data(), params_[i]->count(), (uint32_t)i, 0, cfgs_[i]};
+  const size_t no = outs_.size();
+  for (uint32_t m = map_begin; m < map_begin + map_count; ++m) {
+    if (timing_) timer_.start(0);
+    for (size_t s = 0; s < segs.size(); s += RRAM_MAX_SEGS) {
+      const int k = static_cast<int>(std::min<size_t>(RRAM_MAX_SEGS, segs.size() - s));
+      RRAM_CALL(rram_inject_rng_batched(segs.data() + s, k, seed_, m, d_broken_ + s, Caffe::stream()));
+    }
+    if (timing_) timer_.stop(0);
+    net_->Forward(false);
+    for (size_t k = 0; k < no; ++k) {
+      RRAM_CALL(rram_axpy(1, Dtype(1), outs_[k]->gpu_data(), d_sums_ + k, Caffe::stream()));
+      if (maps_run_ < max_maps_)
+        HIP_CALL(hipMemcpyAsync(d_per_map_ + (size_t)maps_run_ * no + k, outs_[k]->gpu_data(), sizeof(Dtype),
+                                hipMemcpyDeviceToDevice, Caffe::hip_stream()));
+    }
+    ++maps_run_;
+  }
+}
+
+template <typename Dtype>
+void MonteCarlo<Dtype>::Stats(std::vector<double>& outputs, std::vector<unsigned long long>& broken,
+                              std::vector<float>& per_map) const {
+  const size_t no = outs_.size();
+  std::vector<Dtype> s(no);
+  broken.assign(params_.size(), 0);
+  const int pm = std::min(maps_run_, max_maps_);
+  per_map.assign((size_t)pm * no, 0.f);
+  if (no) HIP_CALL(hipMemcpyAsync(s.data(), d_sums_, no * sizeof(Dtype), hipMemcpyDeviceToHost, Caffe::hip_stream()));
+  HIP_CALL(hipMemcpyAsync(broken.data(), d_broken_, broken.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                          Caffe::hip_stream()));
+  if (pm && no)
+    HIP_CALL(hipMemcpyAsync(per_map.data(), d_per_map_, per_map.size() * sizeof(float), hipMemcpyDeviceToHost,
+                            Caffe::hip_stream()));
+  HIP_CALL(hipStreamSynchronize(Caffe::hip_stream()));
+  outputs.assign(s.begin(), s.end());
+}
+
+template class FailureMaker<float>;
+template class GaussianFailureMaker<float>;
+template class FailureStrategy<float>;
+template class ThresholdFailureStrategy<float>;
+template class Solver<float>;
+template class MonteCarlo<float>;
+
+}  // namespace caffe

@@ -1,0 +1,193 @@
+// Fault model, fault-tolerance strategies, SGD solver and the Monte-Carlo
+// fault-map driver.
+//
+//   FailureMaker / GaussianFailureMaker  — include/caffe/failure_maker.hpp:11-96,
+//       src/caffe/failure_maker.cpp, failure_maker.cu
+//   FailureStrategy / ThresholdFailureStrategy — include/caffe/strategy.hpp:34-82,
+//       src/caffe/strategy.cpp:7-33 (a3)
+//   Solver / SGDSolver — src/caffe/solver.cpp (fork hooks :14-40, :132-148,
+//       Step order :237-325, Test :385-458), src/caffe/solvers/sgd_solver.cpp (a4, a11)
+//   MonteCarlo — the reference's one-map-per-run fault-injected Test
+//        generalised to many maps per launch sequence.
+#pragma once
+
+#include <functional>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "net.hpp"
+
+namespace caffe {
+
+template <typename Dtype>
+class Solver;
+
+template <typename Dtype>
+class FailureMaker {
+ public:
+  explicit FailureMaker(const Msg& param) : param_(param) {}
+  virtual ~FailureMaker();
+  // failure_maker.hpp:23-30: nullptr unless type == "gaussian"
+  static std::shared_ptr<FailureMaker<Dtype>> CreateMaker(const Msg& param, std::shared_ptr<Net<Dtype>> net);
+  // failure_maker.hpp:32-58 without the per-iteration D2H count (Appendix A Q5):
+  // the broken count accumulates on the device, read it with broken_counts().
+  void Fail(int iter) { Fail_gpu(iter); }
+  virtual void Fail_gpu(int iter) = 0;
+  std::vector<Blob<Dtype>*> fail_iterations();
+  std::vector<unsigned long long> broken_counts();  // per failure param, after the last Fail()
+  unsigned long long* device_counts() { return d_counts_; }
+  const Msg& param() const { return param_; }
+
+ protected:
+  Msg param_;
+  std::shared_ptr<Net<Dtype>> net_;
+  // endurance in data, stuck value in diff (reference layout, failure_maker.cpp:30-36)
+  std::vector<std::unique_ptr<Blob<Dtype>>> fail_iterations_;
+  unsigned long long* d_counts_ = nullptr;
+};
+
+template <typename Dtype>
+class GaussianFailureMaker : public FailureMaker<Dtype> {
+ public:
+  GaussianFailureMaker(const Msg& param, std::shared_ptr<Net<Dtype>> net);
+  void Fail_gpu(int iter) override;
+  float decrement = 100.0f;  // "batch size FIXME" constant (failure_maker.cpp:73)
+  float epsilon = 1e-20f;    // failure_maker.cpp:56
+};
+
+template <typename Dtype>
+class FailureStrategy {
+ public:
+  FailureStrategy(const Msg& param, std::shared_ptr<FailureMaker<Dtype>> fm, std::shared_ptr<Net<Dtype>> net,
+                  const Solver<Dtype>* solver)
+      : param_(param), fmaker_(fm), net_(net), solver_(solver) {}
+  virtual ~FailureStrategy() = default;
+  // strategy.hpp:34-50; unknown type -> Error (Appendix A Q10: fail cleanly)
+  static std::shared_ptr<FailureStrategy<Dtype>> CreateStrategy(const Msg& param, std::shared_ptr<FailureMaker<Dtype>> fm,
+                                                                std::shared_ptr<Net<Dtype>> net, const Solver<Dtype>* s);
+  virtual void Apply() = 0;
+  virtual const char* type() const = 0;
+
+ protected:
+  Msg param_;
+  std::shared_ptr<FailureMaker<Dtype>> fmaker_;
+  std::shared_ptr<Net<Dtype>> net_;
+  const Solver<Dtype>* solver_;
+};
+
+template <typename Dtype>
+class ThresholdFailureStrategy : public FailureStrategy<Dtype> {
+ public:
+  using FailureStrategy<Dtype>::FailureStrategy;
+  void Apply() override;
+  const char* type() const override { return "threshold"; }
+  float threshold() const { return static_cast<float>(this->param_.num("threshold", 0.001)); }
+  // per failure param: threshold * lr * lr_mult (strategy.cpp:12-14)
+  float threshold_for(int failure_param_index) const;
+  // Appendix A Q6: the reference indexes params_lr() with the failure-param
+  // index; true reproduces that quirk, false (default) uses the param's own lr_mult.
+  bool reference_lr_index = false;
+};
+
+template <typename Dtype>
+class Solver {
+ public:
+  // solver_param: SolverParameter text; net_param (optional) overrides `net:`;
+  // options: net options (data_shape, num_classes, fault_layers, fuse_relu)
+  // plus `fused_update` (true: one fused HBM pass per blob for the training tail).
+  Solver(const Msg& solver_param, const Msg* net_param, const Msg& options);
+  virtual ~Solver() = default;
+
+  void Step(int iters);
+  void Solve();
+  // returns the mean of every output element of test net `id` over test_iter
+  std::vector<Dtype> Test(int id = 0);
+  std::vector<std::vector<Dtype>> TestAll();
+
+  std::shared_ptr<Net<Dtype>> net() { return net_; }
+  const std::vector<std::shared_ptr<Net<Dtype>>>& test_nets() const { return test_nets_; }
+  int iter() const { return iter_; }
+  const Msg& param() const { return param_; }
+  Dtype GetLearningRate() const;
+  std::shared_ptr<FailureMaker<Dtype>> failure_maker() { return fmaker_; }
+  const std::vector<std::shared_ptr<FailureStrategy<Dtype>>>& strategies() const { return strategys_; }
+  Dtype smoothed_loss() const { return smoothed_loss_; }
+  // Solver::Callback::on_gradients_ready (solver.hpp:80-91): the data-parallel
+  // hook (RCCL all-reduce of the flat gradient buffer).
+  std::function<void()> on_gradients_ready;
+  std::function<void(const std::string&)> log;
+
+ protected:
+  void InitFailurePattern(const Msg& failure_param);
+  void ComputeUpdate();
+  void ApplyStrategy();
+  void ApplyUpdate();
+  void FusedTail();
+  void Fail(int iter) {
+    if (fmaker_) fmaker_->Fail(iter);
+  }
+  void ClipGradients();
+  void Regularize(int param_id);
+  void ComputeUpdateValue(int param_id, Dtype rate);
+  void emit(const std::string& s) {
+    if (log) log(s);
+  }
+
+  Msg param_;
+  std::shared_ptr<Net<Dtype>> net_;
+  std::vector<std::shared_ptr<Net<Dtype>>> test_nets_;
+  std::vector<std::unique_ptr<Blob<Dtype>>> history_, temp_;
+  std::shared_ptr<FailureMaker<Dtype>> fmaker_;
+  std::vector<std::shared_ptr<FailureStrategy<Dtype>>> strategys_;
+  int iter_ = 0, current_step_ = 0;
+  Dtype smoothed_loss_ = 0;
+  std::vector<Dtype> losses_;
+  bool fused_update_ = false;
+};
+
+// Monte-Carlo fault-map inference (north_star).
+// For every map m: inject(clean IP weights -> net weights) with the counter
+// RNG keyed by (seed, m, blob), forward the TEST net, accumulate its outputs
+// (accuracy, loss) and the per-blob broken-cell counts on the device.
+template <typename Dtype>
+class MonteCarlo {
+ public:
+  MonteCarlo(std::shared_ptr<Net<Dtype>> net, const std::vector<rram_inject_cfg>& cfgs, uint64_t seed,
+             int max_maps);
+  ~MonteCarlo();
+  void Run(uint32_t map_begin, uint32_t map_count);
+  void Reset();
+  // sums over the maps run so far: outputs[n_outputs] (each output's mean over
+  // its elements), broken[n_fault_blobs], per_map[maps_run][n_outputs]
+  void Stats(std::vector<double>& outputs, std::vector<unsigned long long>& broken,
+             std::vector<float>& per_map) const;
+  int maps_run() const { return maps_run_; }
+  int num_outputs() const { return static_cast<int>(outs_.size()); }
+  void RestoreClean();
+  // hipEvent timing of the injection launches (key 0)
+  void set_timing(bool on) { timing_ = on; }
+  EventTimer& timer() { return timer_; }
+  int64_t fault_weights() const {
+    int64_t n = 0;
+    for (auto* p : params_) n += p->count();
+    return n;
+  }
+
+ private:
+  bool timing_ = false;
+  EventTimer timer_;
+  std::shared_ptr<Net<Dtype>> net_;
+  std::vector<rram_inject_cfg> cfgs_;
+  uint64_t seed_;
+  int max_maps_;
+  int maps_run_ = 0;
+  std::vector<Blob<Dtype>*> params_;
+  std::vector<Dtype*> clean_;
+  std::vector<Blob<Dtype>*> outs_;
+  Dtype* d_sums_ = nullptr;       // [n_outputs]
+  Dtype* d_per_map_ = nullptr;    // [max_maps][n_outputs]
+  unsigned long long* d_broken_ = nullptr;
+};
+
+}  // namespace caffe

@@ -1,0 +1,65 @@
+// hipEvent timers on the working stream (benchmark.cpp:30-95 Timer, used by
+// `caffe time`, tools/caffe.cpp:334-421).  Events are recorded around each
+// timed region without synchronising; collect() waits once and sums.
+#pragma once
+
+#include <map>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "common.hpp"
+
+namespace caffe {
+
+class EventTimer {
+ public:
+  ~EventTimer() { clear(); }
+  void start(int key) {
+    hipEvent_t a, b;
+    HIP_CALL(hipEventCreate(&a));
+    HIP_CALL(hipEventCreate(&b));
+    HIP_CALL(hipEventRecord(a, Caffe::hip_stream()));
+    open_[key] = pending_.size();
+    pending_.push_back({key, {a, b}});
+  }
+  void stop(int key) {
+    auto it = open_.find(key);
+    CAFFE_CHECK(it != open_.end(), "EventTimer::stop without start");
+    HIP_CALL(hipEventRecord(pending_[it->second].second.second, Caffe::hip_stream()));
+    open_.erase(it);
+  }
+  // waits for all recorded intervals; adds them to totals() / counts()
+  void collect() {
+    for (auto& p : pending_) {
+      HIP_CALL(hipEventSynchronize(p.second.second));
+      float ms = 0.f;
+      HIP_CALL(hipEventElapsedTime(&ms, p.second.first, p.second.second));
+      totals_[p.first] += ms;
+      counts_[p.first] += 1;
+      (void)hipEventDestroy(p.second.first);
+      (void)hipEventDestroy(p.second.second);
+    }
+    pending_.clear();
+  }
+  void clear() {
+    for (auto& p : pending_) {
+      (void)hipEventDestroy(p.second.first);
+      (void)hipEventDestroy(p.second.second);
+    }
+    pending_.clear();
+    open_.clear();
+    totals_.clear();
+    counts_.clear();
+  }
+  const std::map<int, double>& totals() const { return totals_; }
+  const std::map<int, long>& counts() const { return counts_; }
+
+ private:
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending_;
+  std::map<int, size_t> open_;
+  std::map<int, double> totals_;
+  std::map<int, long> counts_;
+};
+
+}  // namespace caffe

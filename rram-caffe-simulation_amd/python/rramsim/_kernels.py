@@ -97,6 +97,8 @@ SIGNATURES = {
     "rram_pool_bwd": (I, [P, P, P] + [I] * 13 + [P]),
     "rram_lrn_fwd": (I, [P, P, P, I, I, I, I, I, F, F, F, P]),
     "rram_lrn_bwd": (I, [P, P, P, P, P, I, I, I, I, I, F, F, P]),
+    "rram_lrn_within_fwd": (I, [P, P, P, I, I, I, I, I, F, F, P]),
+    "rram_lrn_within_bwd": (I, [P, P, P, P, I, I, I, I, I, F, F, P]),
     "rram_softmax_fwd": (I, [P, P, I, I, I, P]),
     "rram_softmax_loss_fwd": (I, [P, P, P, I, I, I, I, P]),
     "rram_softmax_loss_bwd": (I, [P, P, P, I, I, I, I, F, P]),

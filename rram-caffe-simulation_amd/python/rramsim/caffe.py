@@ -1,0 +1,430 @@
+"""ctypes view of the C++ host runtime (include/rram_caffe.h): Net, Solver,
+MonteCarlo.  Mirrors pycaffe's shape of API (Net.forward/backward, blobs,
+params; Solver.step/test) so tests read like the reference's own; every call
+goes through librram_caffe.so -> librram_kernels.so.  No CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, List, Optional
+
+from . import _kernels as K
+
+P, I, I64, U32, U64, F = C.c_void_p, C.c_int, C.c_int64, C.c_uint32, C.c_uint64, C.c_float
+PP = C.POINTER(C.c_void_p)
+PI = C.POINTER(C.c_int)
+PI64 = C.POINTER(C.c_int64)
+PF = C.POINTER(C.c_float)
+CB = C.CFUNCTYPE(None, C.c_void_p)
+LOGCB = C.CFUNCTYPE(None, C.c_char_p, C.c_void_p)
+
+SIGNATURES = {
+    "rram_caffe_last_error": (C.c_char_p, []),
+    "rram_caffe_set_stream": (I, [P]),
+    "rram_caffe_set_random_seed": (I, [U64]),
+    "rram_caffe_synchronize": (I, []),
+    "rram_net_create": (I, [C.c_char_p, I, C.c_char_p, PP]),
+    "rram_net_destroy": (I, [P]),
+    "rram_net_forward": (I, [P, I, PF]),
+    "rram_net_backward": (I, [P]),
+    "rram_net_update": (I, [P]),
+    "rram_net_clear_param_diffs": (I, [P]),
+    "rram_net_num_layers": (I, [P, PI]),
+    "rram_net_layer_info": (I, [P, I, C.c_char_p, C.c_char_p, I, PI]),
+    "rram_net_num_blobs": (I, [P, PI]),
+    "rram_net_blob_name": (I, [P, I, C.c_char_p, I]),
+    "rram_net_blob": (I, [P, C.c_char_p, PP, PP, PI, PI]),
+    "rram_net_num_params": (I, [P, PI]),
+    "rram_net_param": (I, [P, I, PP, PP, PI64, PF, PF]),
+    "rram_net_num_failure_params": (I, [P, PI]),
+    "rram_net_failure_param": (I, [P, I, PP, PP, PI64, PI]),
+    "rram_net_num_outputs": (I, [P, PI]),
+    "rram_net_output": (I, [P, I, C.c_char_p, I, PP, PI64]),
+    "rram_net_share_trained": (I, [P, P]),
+    "rram_net_flat_param_count": (I, [P, PI64]),
+    "rram_net_alias_flat_params": (I, [P, P, P]),
+    "rram_net_set_timing": (I, [P, I]),
+    "rram_net_layer_times": (I, [P, C.POINTER(C.c_double), C.POINTER(C.c_long), I, PI, I]),
+    "rram_net_describe": (I, [C.c_char_p, I, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "rram_mc_set_timing": (I, [P, I]),
+    "rram_mc_inject_times": (I, [P, C.POINTER(C.c_double), C.POINTER(C.c_long), PI64, I]),
+    "rram_solver_create": (I, [C.c_char_p, C.c_char_p, C.c_char_p, PP]),
+    "rram_solver_destroy": (I, [P]),
+    "rram_solver_step": (I, [P, I]),
+    "rram_solver_solve": (I, [P]),
+    "rram_solver_iter": (I, [P, PI]),
+    "rram_solver_smoothed_loss": (I, [P, PF]),
+    "rram_solver_learning_rate": (I, [P, PF]),
+    "rram_solver_net": (I, [P, PP]),
+    "rram_solver_num_test_nets": (I, [P, PI]),
+    "rram_solver_test_net": (I, [P, I, PP]),
+    "rram_solver_test": (I, [P, I, PF, I, PI]),
+    "rram_solver_set_gradient_callback": (I, [P, CB, P]),
+    "rram_solver_set_log_callback": (I, [P, LOGCB, P]),
+    "rram_solver_num_fail_blobs": (I, [P, PI]),
+    "rram_solver_fail_state": (I, [P, I, PP, PP, PI64]),
+    "rram_solver_broken_counts": (I, [P, C.POINTER(C.c_ulonglong), I, PI]),
+    "rram_mc_create": (I, [P, P, I, U64, I, PP]),
+    "rram_mc_destroy": (I, [P]),
+    "rram_mc_run": (I, [P, U32, U32]),
+    "rram_mc_reset": (I, [P]),
+    "rram_mc_restore_clean": (I, [P]),
+    "rram_mc_stats": (I, [P, C.POINTER(C.c_double), I, PI, C.POINTER(C.c_ulonglong), I, PI, PF, I, PI]),
+}
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        K.load()  # kernels first (RTLD_GLOBAL)
+        if not K.CAFFE_SO.exists():
+            raise K.RramError(f"{K.CAFFE_SO} not built; there is no CPU fallback")
+        lib = C.CDLL(str(K.CAFFE_SO))
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def check(rc, what=""):
+    if rc != 0:
+        raise K.RramError(f"{what} failed ({rc}): {load().rram_caffe_last_error().decode(errors='replace')}")
+
+
+def set_stream_from_torch():
+    import torch
+    check(load().rram_caffe_set_stream(C.c_void_p(torch.cuda.current_stream().cuda_stream)), "set_stream")
+
+
+def set_random_seed(seed: int):
+    check(load().rram_caffe_set_random_seed(seed), "set_random_seed")
+
+
+def synchronize():
+    check(load().rram_caffe_synchronize(), "synchronize")
+
+
+def options_text(opts: Optional[Dict]) -> Optional[bytes]:
+    if not opts:
+        return None
+    parts = []
+    for k, v in opts.items():
+        if isinstance(v, bool):
+            parts.append(f"{k}: {'true' if v else 'false'}")
+        elif isinstance(v, (int, float)):
+            parts.append(f"{k}: {v}")
+        elif isinstance(v, (tuple, list)):
+            parts.append(f'{k}: "{",".join(str(x) for x in v)}"')
+        else:
+            parts.append(f'{k}: "{v}"')
+    return " ".join(parts).encode()
+
+
+def describe(prototxt: str, phase: str = "test") -> List[tuple]:
+    """Host-only structural view of a net (phase filter + split insertion):
+    [(name, type, [bottoms], [tops])].  Needs no GPU."""
+    lib = load()
+    need = C.c_size_t()
+    ph = 0 if phase == "train" else 1
+    check(lib.rram_net_describe(prototxt.encode(), ph, None, 0, C.byref(need)), "net_describe")
+    buf = C.create_string_buffer(need.value)
+    check(lib.rram_net_describe(prototxt.encode(), ph, buf, need.value, None), "net_describe")
+    out = []
+    for line in buf.value.decode().splitlines():
+        name, typ, bots, tops = line.split("\t")
+        out.append((name, typ, [b for b in bots.split(",") if b], [t for t in tops.split(",") if t]))
+    return out
+
+
+def _wrap_device(ptr: int, shape):
+    """Zero-copy float32 torch view of a device pointer (via __cuda_array_interface__)."""
+    import torch
+
+    class _Iface:
+        def __init__(self, p, s):
+            self.__cuda_array_interface__ = {"shape": tuple(s), "typestr": "<f4", "data": (p, False),
+                                             "version": 2, "strides": None}
+    if len(shape) == 0:
+        shape = (1,)
+    return torch.as_tensor(_Iface(ptr, shape), device="cuda")
+
+
+class Net:
+    """caffe::Net<float> (net.cpp).  phase: 'train' | 'test'."""
+
+    def __init__(self, prototxt: str, phase: str = "test", options: Optional[Dict] = None,
+                 _handle=None, _owned=True):
+        self._lib = load()
+        if _handle is not None:
+            self.h = _handle
+        else:
+            h = C.c_void_p()
+            check(self._lib.rram_net_create(prototxt.encode(), 0 if phase == "train" else 1,
+                                            options_text(options), C.byref(h)), "net_create")
+            self.h = h
+        self._owned = _owned and _handle is None
+
+    def close(self):
+        if getattr(self, "_owned", False) and self.h:
+            self._lib.rram_net_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def forward(self, compute_loss=True) -> float:
+        loss = C.c_float(0)
+        check(self._lib.rram_net_forward(self.h, int(compute_loss), C.byref(loss)), "forward")
+        return loss.value
+
+    def backward(self):
+        check(self._lib.rram_net_backward(self.h), "backward")
+
+    def update(self):
+        check(self._lib.rram_net_update(self.h), "update")
+
+    def clear_param_diffs(self):
+        check(self._lib.rram_net_clear_param_diffs(self.h), "clear_param_diffs")
+
+    def layers(self) -> List[tuple]:
+        n = C.c_int()
+        check(self._lib.rram_net_num_layers(self.h, C.byref(n)), "num_layers")
+        out = []
+        for i in range(n.value):
+            name, typ, np_ = C.create_string_buffer(256), C.create_string_buffer(256), C.c_int()
+            check(self._lib.rram_net_layer_info(self.h, i, name, typ, 256, C.byref(np_)), "layer_info")
+            out.append((name.value.decode(), typ.value.decode(), np_.value))
+        return out
+
+    def blob_names(self) -> List[str]:
+        n = C.c_int()
+        check(self._lib.rram_net_num_blobs(self.h, C.byref(n)), "num_blobs")
+        names = []
+        for i in range(n.value):
+            b = C.create_string_buffer(512)
+            check(self._lib.rram_net_blob_name(self.h, i, b, 512), "blob_name")
+            names.append(b.value.decode())
+        return names
+
+    def blob(self, name: str, diff=False):
+        d, g = C.c_void_p(), C.c_void_p()
+        shape = (C.c_int * 8)()
+        na = C.c_int()
+        check(self._lib.rram_net_blob(self.h, name.encode(), C.byref(d), C.byref(g), shape, C.byref(na)),
+              f"blob {name}")
+        return _wrap_device((g if diff else d).value, [shape[i] for i in range(na.value)])
+
+    def params(self):
+        n = C.c_int()
+        check(self._lib.rram_net_num_params(self.h, C.byref(n)), "num_params")
+        out = []
+        for i in range(n.value):
+            d, g, cnt, lr, dm = C.c_void_p(), C.c_void_p(), C.c_int64(), C.c_float(), C.c_float()
+            check(self._lib.rram_net_param(self.h, i, C.byref(d), C.byref(g), C.byref(cnt), C.byref(lr),
+                                           C.byref(dm)), "param")
+            out.append(dict(data=_wrap_device(d.value, (cnt.value,)), diff=_wrap_device(g.value, (cnt.value,)),
+                            lr_mult=lr.value, decay_mult=dm.value))
+        return out
+
+    def failure_params(self):
+        n = C.c_int()
+        check(self._lib.rram_net_num_failure_params(self.h, C.byref(n)), "num_failure_params")
+        out = []
+        for i in range(n.value):
+            d, g, cnt, lid = C.c_void_p(), C.c_void_p(), C.c_int64(), C.c_int()
+            check(self._lib.rram_net_failure_param(self.h, i, C.byref(d), C.byref(g), C.byref(cnt),
+                                                   C.byref(lid)), "failure_param")
+            out.append(dict(data=_wrap_device(d.value, (cnt.value,)), diff=_wrap_device(g.value, (cnt.value,)),
+                            count=cnt.value, layer_id=lid.value))
+        return out
+
+    def outputs(self) -> Dict[str, object]:
+        n = C.c_int()
+        check(self._lib.rram_net_num_outputs(self.h, C.byref(n)), "num_outputs")
+        out = {}
+        for i in range(n.value):
+            name, d, cnt = C.create_string_buffer(256), C.c_void_p(), C.c_int64()
+            check(self._lib.rram_net_output(self.h, i, name, 256, C.byref(d), C.byref(cnt)), "output")
+            out[name.value.decode()] = _wrap_device(d.value, (cnt.value,))
+        return out
+
+    def set_timing(self, on: bool):
+        check(self._lib.rram_net_set_timing(self.h, int(on)), "set_timing")
+
+    def layer_times(self, reset=False):
+        """[(layer name, type, total ms, launches)] since the last reset."""
+        L = self.layers()
+        ms = (C.c_double * len(L))()
+        cnt = (C.c_long * len(L))()
+        n = C.c_int()
+        check(self._lib.rram_net_layer_times(self.h, ms, cnt, len(L), C.byref(n), int(reset)), "layer_times")
+        return [(L[i][0], L[i][1], ms[i], cnt[i]) for i in range(len(L))]
+
+    def share_trained_with(self, other: "Net"):
+        check(self._lib.rram_net_share_trained(self.h, other.h), "share_trained")
+
+    def flat_param_count(self) -> int:
+        n = C.c_int64()
+        check(self._lib.rram_net_flat_param_count(self.h, C.byref(n)), "flat_param_count")
+        return n.value
+
+    def alias_flat_params(self, data_t, diff_t):
+        check(self._lib.rram_net_alias_flat_params(self.h, C.c_void_p(data_t.data_ptr()),
+                                                   C.c_void_p(diff_t.data_ptr())), "alias_flat_params")
+
+
+class Solver:
+    """caffe::SGDSolver with the fork's fault hooks."""
+
+    def __init__(self, solver_prototxt: str, net_prototxt: Optional[str] = None,
+                 options: Optional[Dict] = None, log=None):
+        self._lib = load()
+        h = C.c_void_p()
+        check(self._lib.rram_solver_create(solver_prototxt.encode(),
+                                           net_prototxt.encode() if net_prototxt else None,
+                                           options_text(options), C.byref(h)), "solver_create")
+        self.h = h
+        self._cb = None
+        self._logcb = None
+        self.log_lines: List[str] = []
+
+        def _log(line, _user):
+            s = line.decode()
+            self.log_lines.append(s)
+            if log:
+                log(s)
+        self._logcb = LOGCB(_log)
+        check(self._lib.rram_solver_set_log_callback(self.h, self._logcb, None), "set_log_callback")
+
+    def close(self):
+        if self.h:
+            self._lib.rram_solver_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def net(self) -> Net:
+        n = C.c_void_p()
+        check(self._lib.rram_solver_net(self.h, C.byref(n)), "solver_net")
+        return Net("", _handle=n, _owned=False)
+
+    def test_net(self, i=0) -> Net:
+        n = C.c_void_p()
+        check(self._lib.rram_solver_test_net(self.h, i, C.byref(n)), "solver_test_net")
+        return Net("", _handle=n, _owned=False)
+
+    @property
+    def iter(self) -> int:
+        v = C.c_int()
+        check(self._lib.rram_solver_iter(self.h, C.byref(v)), "iter")
+        return v.value
+
+    def learning_rate(self) -> float:
+        v = C.c_float()
+        check(self._lib.rram_solver_learning_rate(self.h, C.byref(v)), "learning_rate")
+        return v.value
+
+    def smoothed_loss(self) -> float:
+        v = C.c_float()
+        check(self._lib.rram_solver_smoothed_loss(self.h, C.byref(v)), "smoothed_loss")
+        return v.value
+
+    def step(self, iters: int):
+        check(self._lib.rram_solver_step(self.h, iters), "step")
+
+    def solve(self):
+        check(self._lib.rram_solver_solve(self.h), "solve")
+
+    def test(self, i=0) -> List[float]:
+        buf = (C.c_float * 1024)()
+        n = C.c_int()
+        check(self._lib.rram_solver_test(self.h, i, buf, 1024, C.byref(n)), "test")
+        return [buf[k] for k in range(n.value)]
+
+    def set_gradient_callback(self, fn):
+        self._cb = CB(lambda _u: fn())
+        check(self._lib.rram_solver_set_gradient_callback(self.h, self._cb, None), "set_gradient_callback")
+
+    def fail_state(self):
+        n = C.c_int()
+        check(self._lib.rram_solver_num_fail_blobs(self.h, C.byref(n)), "num_fail_blobs")
+        out = []
+        for i in range(n.value):
+            e, v, cnt = C.c_void_p(), C.c_void_p(), C.c_int64()
+            check(self._lib.rram_solver_fail_state(self.h, i, C.byref(e), C.byref(v), C.byref(cnt)), "fail_state")
+            out.append((_wrap_device(e.value, (cnt.value,)), _wrap_device(v.value, (cnt.value,))))
+        return out
+
+    def broken_counts(self) -> List[int]:
+        buf = (C.c_ulonglong * 256)()
+        n = C.c_int()
+        check(self._lib.rram_solver_broken_counts(self.h, buf, 256, C.byref(n)), "broken_counts")
+        return [buf[i] for i in range(n.value)]
+
+
+class MonteCarlo:
+    """Fault-map Monte-Carlo inference driver (rram_mc_*)."""
+
+    def __init__(self, net: Net, cfgs, seed: int, max_maps: int = 4096):
+        self._lib = load()
+        if not isinstance(cfgs, (list, tuple)):
+            cfgs = [cfgs]
+        arr = (K.InjectCfg * len(cfgs))(*cfgs)
+        h = C.c_void_p()
+        check(self._lib.rram_mc_create(net.h, C.cast(arr, C.c_void_p), len(cfgs), seed, max_maps, C.byref(h)),
+              "mc_create")
+        self.h, self.net, self.max_maps = h, net, max_maps
+
+    def run(self, begin: int, count: int):
+        check(self._lib.rram_mc_run(self.h, begin, count), "mc_run")
+
+    def reset(self):
+        check(self._lib.rram_mc_reset(self.h), "mc_reset")
+
+    def restore_clean(self):
+        check(self._lib.rram_mc_restore_clean(self.h), "mc_restore_clean")
+
+    def set_timing(self, on: bool):
+        check(self._lib.rram_mc_set_timing(self.h, int(on)), "mc_set_timing")
+
+    def inject_times(self, reset=False):
+        """(total ms, launches, faultable weights) of the injection launches."""
+        ms, n, w = C.c_double(), C.c_long(), C.c_int64()
+        check(self._lib.rram_mc_inject_times(self.h, C.byref(ms), C.byref(n), C.byref(w), int(reset)),
+              "mc_inject_times")
+        return ms.value, n.value, w.value
+
+    def stats(self):
+        sums = (C.c_double * 64)()
+        broken = (C.c_ulonglong * 256)()
+        per_map = (C.c_float * (self.max_maps * 8))()
+        no, nb, mr = C.c_int(), C.c_int(), C.c_int()
+        check(self._lib.rram_mc_stats(self.h, sums, 64, C.byref(no), broken, 256, C.byref(nb), per_map,
+                                      self.max_maps * 8, C.byref(mr)), "mc_stats")
+        n_out = no.value
+        pm = [[per_map[m * n_out + k] for k in range(n_out)] for m in range(min(mr.value, self.max_maps))]
+        return dict(sums=[sums[i] for i in range(n_out)], broken=[broken[i] for i in range(nb.value)],
+                    per_map=pm, maps=mr.value)
+
+    def close(self):
+        if self.h:
+            self._lib.rram_mc_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
