@@ -22,14 +22,26 @@ __device__ __forceinline__ void wave_count_add(bool pred, unsigned long long* co
     atomicAdd(counter, static_cast<unsigned long long>(__popcll(m)));
   }
 }
-__device__ __forceinline__ void wave_count_add_n(unsigned cnt, unsigned long long* counter) {
-  // sum of small per-lane counts over the wave
+// Block-level sum of per-lane counts, ONE atomic per block.  Many waves
+// adding to one address serialise at the memory side (MI355X_MICROARCH.md
+// "Global float atomics", contention row), so counters are flushed per block,
+// and per block only when its segment changes or its loop ends.
+// Must be reached by every thread of the block (contains __syncthreads).
+__device__ __forceinline__ void block_count_flush(unsigned cnt, unsigned long long* counter) {
+  __shared__ unsigned part[4];
   unsigned v = cnt;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  if (counter != nullptr && (threadIdx.x & 63) == 0 && v != 0u) {
-    atomicAdd(counter, static_cast<unsigned long long>(v));
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0 && counter != nullptr) {
+    const unsigned t = part[0] + part[1] + part[2] + part[3];
+    if (t) atomicAdd(counter, static_cast<unsigned long long>(t));
   }
+}
+__device__ __forceinline__ void wave_count_add_n(unsigned cnt, unsigned long long* counter) {
+  block_count_flush(cnt, counter);
 }
 
 // ---------------------------------------------------------------------------
@@ -109,10 +121,9 @@ struct FailSegs {
 
 constexpr int kFailChunk = 256 * 4 * 4;  // elements per block-chunk
 
-__device__ __forceinline__ void fail_range(const float* __restrict__ dw, float* __restrict__ w,
-                                           float* __restrict__ e, const float* __restrict__ v,
-                                           int64_t begin, int64_t end, float dec, float eps,
-                                           unsigned long long* counter) {
+__device__ __forceinline__ unsigned fail_range(const float* __restrict__ dw, float* __restrict__ w,
+                                               float* __restrict__ e, const float* __restrict__ v,
+                                               int64_t begin, int64_t end, float dec, float eps) {
   const bool vec = aligned16(dw + begin) && aligned16(w + begin) && aligned16(e + begin) &&
                    aligned16(v + begin);
   unsigned cnt = 0;
@@ -153,21 +164,28 @@ __device__ __forceinline__ void fail_range(const float* __restrict__ dw, float* 
       if (wr) w[i] = ww;
     }
   }
-  wave_count_add_n(cnt, counter);
+  return cnt;
 }
 
 __global__ void __launch_bounds__(256)
     k_fail_apply_batched(FailSegs segs, float dec, float eps, unsigned long long* counters) {
   const int64_t total = segs.chunk_start[segs.nsegs];
+  int cur = -1;  // block-uniform: flush the count once per segment visited
+  unsigned cnt = 0;
   for (int64_t c = blockIdx.x; c < total; c += gridDim.x) {
     int s = 0;
     while (c >= segs.chunk_start[s + 1]) ++s;
+    if (s != cur) {
+      if (cur >= 0) block_count_flush(cnt, counters ? counters + cur : nullptr);
+      cnt = 0;
+      cur = s;
+    }
     const rram_fail_seg& sg = segs.s[s];
     const int64_t begin = (c - segs.chunk_start[s]) * kFailChunk;
     const int64_t end = min(begin + (int64_t)kFailChunk, sg.n);
-    fail_range(sg.dw, sg.w, sg.endurance, sg.values, begin, end, dec, eps,
-               counters ? counters + s : nullptr);
+    cnt += fail_range(sg.dw, sg.w, sg.endurance, sg.values, begin, end, dec, eps);
   }
+  if (cur >= 0) block_count_flush(cnt, counters ? counters + cur : nullptr);
 }
 
 __global__ void __launch_bounds__(256)
@@ -323,13 +341,19 @@ __device__ __forceinline__ float inject1(float w, int64_t i, uint64_t seed, uint
 __global__ void __launch_bounds__(256)
     k_inject_batched(InjectSegs segs, uint64_t seed, uint32_t map_id, unsigned long long* counters) {
   const int64_t total = segs.chunk_start[segs.nsegs];
+  int cur = -1;  // block-uniform: flush the count once per segment visited
+  unsigned nb = 0;
   for (int64_t c = blockIdx.x; c < total; c += gridDim.x) {
     int s = 0;
     while (c >= segs.chunk_start[s + 1]) ++s;
+    if (s != cur) {
+      if (cur >= 0) block_count_flush(nb, counters ? counters + cur : nullptr);
+      nb = 0;
+      cur = s;
+    }
     const InjectSeg& g = segs.s[s];
     const int64_t begin = (c - segs.chunk_start[s]) * kInjChunk;
     const int64_t end = min(begin + (int64_t)kInjChunk, g.n);
-    unsigned nb = 0;
     // vector path: begin is a multiple of 4 (chunk size), pointers 16-B aligned
     if (aligned16(g.src) && aligned16(g.dst)) {
       const int64_t nv = (end - begin) >> 2;
@@ -353,8 +377,8 @@ __global__ void __launch_bounds__(256)
       for (int64_t i = begin + threadIdx.x; i < end; i += 256)
         g.dst[i] = inject1(g.src[i], i, seed, map_id, g, nb);
     }
-    wave_count_add_n(nb, counters ? counters + s : nullptr);
   }
+  if (cur >= 0) block_count_flush(nb, counters ? counters + cur : nullptr);
 }
 
 // ---------------------------------------------------------------------------

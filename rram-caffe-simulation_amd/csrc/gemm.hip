@@ -4,16 +4,18 @@
 // One templated kernel serves every contraction of the conv/IP path:
 //   C[m][n] = sum_k A(m,k) * B(n,k)
 // A and B are "operand views" (loader modes) so the same MFMA core runs
-//   - Caffe GEMM with any transpose combination  (KC / RC views),
+//   - Caffe GEMM with any transpose combination  (KC / KCV / RC views),
 //   - implicit-im2col convolution forward         (CONV view: gather into LDS),
 //   - NCHW activations / gradients spanning images (NCHW / NCHWT views).
 // Block: 256 threads = 4 waves; each wave owns MI x NI tiles of 32x32.
 // LDS holds both operands k-contiguous ([row][BK+4]), double-buffered and
-// register-staged (global loads for tile t+1 are issued before the MFMAs of
-// tile t).  K is consumed in a permuted order inside a tile (lane half h at
-// step s uses k = h*BK/2 + s) so that each lane reads its fragments with
-// 16-byte LDS reads; the permutation is the same for A and B, so the
-// contraction is unchanged.
+// register-staged: the global loads of K-tile t+1 are issued before the MFMAs
+// of tile t and written to the other LDS buffer after them (one barrier per
+// K-tile).  Inside a tile K is consumed in a permuted order (lane half h at
+// step s of sub-block q uses k = 16q + 8h + s) so each lane reads its
+// fragments with 16-byte LDS reads; A and B use the same permutation, so the
+// contraction is unchanged.  Blocks are remapped so that each XCD (own L2)
+// receives a contiguous run of tiles that share operand panels.
 #include "rram_common.hpp"
 
 namespace rram {
@@ -21,10 +23,11 @@ namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-constexpr int BK = 16;
-constexpr int LDK = BK + 4;  // padded LDS row (floats); 80 B keeps 16-B alignment
+constexpr int BK = 32;
+constexpr int LDK = BK + 4;  // padded LDS row (floats): 144 B, 16-B aligned, conflict-free b128 reads
 
-enum Mode : int { KC = 0, RC = 1, CONV = 2, NCHW = 3, NCHWT = 4 };
+// KCV = KC with 16-byte global loads (row stride, base and K all multiples of 4 floats)
+enum Mode : int { KC = 0, RC = 1, CONV = 2, NCHW = 3, NCHWT = 4, KCV = 5 };
 enum OutMode : int { OUT_ROWMAJOR = 0, OUT_NCHW = 1 };
 
 // Fast unsigned division by a runtime constant (x < 2^31).
@@ -44,8 +47,8 @@ static FastDiv make_fastdiv(uint32_t d) {
   f.m = static_cast<uint32_t>(((1ull << 32) * ((1ull << s) - d)) / d + 1);
   return f;
 }
+// d == 1 is encoded as m = 0, s = 0, so no branch is needed
 __device__ __forceinline__ uint32_t fdiv(uint32_t x, const FastDiv& f) {
-  if (f.d <= 1) return x;
   const uint32_t t = __umulhi(x, f.m);
   return (t + x) >> f.s;
 }
@@ -83,12 +86,13 @@ struct Params {
   int M, N, K;
   int k_chunk;               // split-K chunk length (multiple of BK)
   float* ws;                 // split-K partials [split][M][N] (nullptr: direct)
-  int64_t grp_a, grp_b, grp_c;  // per-group pointer offsets (blockIdx.z = group)
+  int64_t grp_a, grp_b, grp_c;  // per-group pointer offsets (z = group)
   int64_t grp_bias;
-  int split;                 // number of K splits (blockIdx.z = split when > 1)
+  int split;                 // number of K splits (z = split when > 1)
+  int tiles_m, tiles_n, tiles_z;
 };
 
-// Per-thread constant data of the B/A loader for the CONV view.
+// Per-thread constant data of the B loader for the CONV view.
 struct ConvCol {
   int64_t base;  // image offset of this thread's column (n*C*H*W)
   int hb, wb;    // ho*sh - ph, wo*sw - pw
@@ -101,29 +105,41 @@ struct Loader {
   float v[EPT];
 };
 
-__device__ __forceinline__ float ld_kc(const View& vw, int row, int k) {
-  return (row < vw.rows && k < vw.kdim) ? vw.p[(int64_t)row * vw.ld + k] : 0.0f;
+// Branch-free guarded loads: an out-of-range element loads from the view's
+// base (always valid) and is replaced by 0, so the load stream has no
+// exec-mask branches.
+// The guard selects the ADDRESS (a 16-byte zero block for out-of-range
+// elements), never the loaded value: a select on the value would force an
+// s_waitcnt right after the load and serialise the prefetch behind it.
+__device__ __attribute__((aligned(16))) float g_zero4[4] = {0.f, 0.f, 0.f, 0.f};
+__device__ __forceinline__ float ld_guard(const float* p, int64_t off, bool ok) {
+  return *(ok ? p + off : g_zero4);
 }
-__device__ __forceinline__ float ld_rc(const View& vw, int row, int k) {
-  return (row < vw.rows && k < vw.kdim) ? vw.p[(int64_t)k * vw.ld + row] : 0.0f;
+__device__ __forceinline__ float ld_kc(const View& vw, int row, int k, bool kok) {
+  const bool ok = kok && row < vw.rows;
+  return ld_guard(vw.p, (int64_t)row * vw.ld + k, ok);
+}
+__device__ __forceinline__ float ld_rc(const View& vw, int row, int k, bool kok) {
+  const bool ok = kok && row < vw.rows;
+  return ld_guard(vw.p, (int64_t)k * vw.ld + row, ok);
 }
 // NCHW: row = channel, k = flattened (image, spatial)
-__device__ __forceinline__ float ld_nchw(const View& vw, int row, int k) {
-  if (row >= vw.rows || k >= vw.kdim) return 0.0f;
+__device__ __forceinline__ float ld_nchw(const View& vw, int row, int k, bool kok) {
+  const bool ok = kok && row < vw.rows;
   const uint32_t im = fdiv(static_cast<uint32_t>(k), vw.hw);
   const uint32_t s = static_cast<uint32_t>(k) - im * vw.hw.d;
-  return vw.p[(int64_t)im * vw.img + (int64_t)row * vw.ld + s];
+  return ld_guard(vw.p, (int64_t)im * vw.img + (int64_t)row * vw.ld + s, ok);
 }
 // NCHWT: row = flattened (image, spatial), k = channel
-__device__ __forceinline__ float ld_nchwt(const View& vw, int row, int k) {
-  if (row >= vw.rows || k >= vw.kdim) return 0.0f;
+__device__ __forceinline__ float ld_nchwt(const View& vw, int row, int k, bool kok) {
+  const bool ok = kok && row < vw.rows;
   const uint32_t im = fdiv(static_cast<uint32_t>(row), vw.hw);
   const uint32_t s = static_cast<uint32_t>(row) - im * vw.hw.d;
-  return vw.p[(int64_t)im * vw.img + (int64_t)k * vw.ld + s];
+  return ld_guard(vw.p, (int64_t)im * vw.img + (int64_t)k * vw.ld + s, ok);
 }
 
-// Element e of a ROWS x BK tile -> (row, k) for a view mode.  KC / NCHW are
-// k-fastest (memory is contiguous along k); the others are row-fastest.
+// Element e of a ROWS x BK tile -> (row, k) for a scalar view mode.  KC / NCHW
+// are k-fastest (memory is contiguous along k); the others are row-fastest.
 template <int MODE, int ROWS>
 __device__ __forceinline__ void tile_coord(int e, int& row, int& k) {
   if (MODE == KC || MODE == NCHW) {
@@ -139,6 +155,23 @@ template <int MODE, int ROWS>
 __device__ __forceinline__ void load_tile(Loader<ROWS>& L, const View& vw, const ConvGeom& cv,
                                           const ConvCol& col, int row0, int k0, int kend) {
   constexpr int EPT = Loader<ROWS>::EPT;
+  if (MODE == KCV) {
+    // 16-byte loads: float4 q -> (row = q / (BK/4), k4 = q % (BK/4)); K-range
+    // ends are multiples of 4 so a float4 is entirely in or out of range
+#pragma unroll
+    for (int i = 0; i < EPT / 4; ++i) {
+      const int q = threadIdx.x + i * 256;
+      const int r = q / (BK / 4);
+      const int k = k0 + 4 * (q % (BK / 4));
+      const bool ok = row0 + r < vw.rows && k < kend;
+      const float4 x = *reinterpret_cast<const float4*>(ok ? vw.p + (int64_t)(row0 + r) * vw.ld + k : g_zero4);
+      L.v[4 * i] = x.x;
+      L.v[4 * i + 1] = x.y;
+      L.v[4 * i + 2] = x.z;
+      L.v[4 * i + 3] = x.w;
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < EPT; ++i) {
     const int e = threadIdx.x + i * 256;
@@ -146,16 +179,16 @@ __device__ __forceinline__ void load_tile(Loader<ROWS>& L, const View& vw, const
     tile_coord<MODE, ROWS>(e, r, kk);
     const int row = row0 + r;
     const int k = k0 + kk;
-    float x = 0.0f;
+    float x;
     if (MODE == KC) {
-      if (k < kend) x = ld_kc(vw, row, k);
+      x = ld_kc(vw, row, k, k < kend);
     } else if (MODE == RC) {
-      if (k < kend) x = ld_rc(vw, row, k);
+      x = ld_rc(vw, row, k, k < kend);
     } else if (MODE == NCHW) {
-      if (k < kend) x = ld_nchw(vw, row, k);
+      x = ld_nchw(vw, row, k, k < kend);
     } else if (MODE == NCHWT) {
-      if (k < kend) x = ld_nchwt(vw, row, k);
-    } else {  // CONV gather: k is wave-uniform for ROWS >= 64
+      x = ld_nchwt(vw, row, k, k < kend);
+    } else {  // CONV gather: k is wave-uniform (ROWS >= 64), decomposed on the scalar unit
       const int ku = __builtin_amdgcn_readfirstlane(k);
       const uint32_t c = fdiv(static_cast<uint32_t>(ku), cv.khkw);
       const uint32_t rem = static_cast<uint32_t>(ku) - c * cv.khkw.d;
@@ -163,9 +196,11 @@ __device__ __forceinline__ void load_tile(Loader<ROWS>& L, const View& vw, const
       const uint32_t kw = rem - kh * cv.kw_div.d;
       const int iy = col.hb + static_cast<int>(kh) * cv.dh;
       const int ix = col.wb + static_cast<int>(kw) * cv.dw;
-      if (col.valid && ku < kend && static_cast<unsigned>(iy) < static_cast<unsigned>(cv.H) &&
-          static_cast<unsigned>(ix) < static_cast<unsigned>(cv.W))
-        x = vw.p[col.base + (int64_t)c * cv.H * cv.W + (int64_t)iy * cv.W + ix];
+      const bool ok = col.valid && ku < kend && static_cast<unsigned>(iy) < static_cast<unsigned>(cv.H) &&
+                      static_cast<unsigned>(ix) < static_cast<unsigned>(cv.W);
+      // 32-bit offset inside the image (C*H*W < 2^31 is checked on the host)
+      const int off = static_cast<int>(c) * (cv.H * cv.W) + iy * cv.W + ix;
+      x = ld_guard(vw.p + col.base, off, ok);
     }
     L.v[i] = x;
   }
@@ -174,6 +209,15 @@ __device__ __forceinline__ void load_tile(Loader<ROWS>& L, const View& vw, const
 template <int MODE, int ROWS>
 __device__ __forceinline__ void store_tile(const Loader<ROWS>& L, float* lds) {
   constexpr int EPT = Loader<ROWS>::EPT;
+  if (MODE == KCV) {
+#pragma unroll
+    for (int i = 0; i < EPT / 4; ++i) {
+      const int q = threadIdx.x + i * 256;
+      *reinterpret_cast<float4*>(lds + (q / (BK / 4)) * LDK + 4 * (q % (BK / 4))) =
+          make_float4(L.v[4 * i], L.v[4 * i + 1], L.v[4 * i + 2], L.v[4 * i + 3]);
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < EPT; ++i) {
     const int e = threadIdx.x + i * 256;
@@ -183,12 +227,16 @@ __device__ __forceinline__ void store_tile(const Loader<ROWS>& L, float* lds) {
   }
 }
 
+__device__ __forceinline__ float pick(const float4& q, int s) {
+  return (s & 3) == 0 ? q.x : (s & 3) == 1 ? q.y : (s & 3) == 2 ? q.z : q.w;
+}
+
 template <int WM, int WN, int MI, int NI, int AM, int BMODE, int OM>
 __global__ void __launch_bounds__(256) k_gemm(Params P) {
   constexpr int BMr = WM * MI * 32;
   constexpr int BNr = WN * NI * 32;
   static_assert(WM * WN == 4, "4 waves per block");
-  static_assert(BMr * BK % 256 == 0 && BNr * BK % 256 == 0, "tile/threads");
+  static_assert(BMr * BK % 1024 == 0 && BNr * BK % 1024 == 0, "tile/threads");
   __shared__ __attribute__((aligned(16))) float As[2][BMr * LDK];
   __shared__ __attribute__((aligned(16))) float Bs[2][BNr * LDK];
 
@@ -197,10 +245,20 @@ __global__ void __launch_bounds__(256) k_gemm(Params P) {
   const int wm = wave / WN;
   const int wn = wave % WN;
 
-  // blockIdx.x -> N tiles (fastest, so consecutive blocks share the A panel)
-  const int n0 = blockIdx.x * BNr;
-  const int m0 = blockIdx.y * BMr;
-  int z = blockIdx.z;
+  // XCD-aware tile order (cdna_hip_programming.md §5.5 T1, bijective form):
+  // dispatch deals blocks round-robin over 8 XCDs, so give every XCD a
+  // contiguous range of tiles; within it the m-tiles of one n-tile are
+  // adjacent (they share the B panel) and consecutive n-tiles follow.
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, loc = bid >> 3;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int tid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const int tm = tid % P.tiles_m;
+  const int tn = (tid / P.tiles_m) % P.tiles_n;
+  const int z = tid / (P.tiles_m * P.tiles_n);
+  const int n0 = tn * BNr;
+  const int m0 = tm * BMr;
 
   View va = P.a, vb = P.b;
   Epi ep = P.e;
@@ -217,7 +275,7 @@ __global__ void __launch_bounds__(256) k_gemm(Params P) {
     if (ep.bias) ep.bias += z * P.grp_bias;
   }
 
-  // CONV column precompute (B operand rows = output positions)
+  // CONV column precompute (B operand rows = output positions; fixed per thread)
   ConvCol col{0, 0, 0, false};
   if (BMODE == CONV) {
     int r, kk;
@@ -264,33 +322,35 @@ __global__ void __launch_bounds__(256) k_gemm(Params P) {
       load_tile<AM, BMr>(la, va, P.cv, col, m0, kn, kend);
       load_tile<BMODE, BNr>(lb, vb, P.cv, col, n0, kn, kend);
     }
-    float4 af[MI][2], bf[NI][2];
+    // keep the prefetch loads ahead of the MFMAs and the LDS writes behind them
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      const float* pa = &As[cur][(wm * MI * 32 + i * 32 + lr) * LDK + lh * (BK / 2)];
-      af[i][0] = *reinterpret_cast<const float4*>(pa);
-      af[i][1] = *reinterpret_cast<const float4*>(pa + 4);
-    }
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const float* pb = &Bs[cur][(wn * NI * 32 + j * 32 + lr) * LDK + lh * (BK / 2)];
-      bf[j][0] = *reinterpret_cast<const float4*>(pb);
-      bf[j][1] = *reinterpret_cast<const float4*>(pb + 4);
-    }
-#pragma unroll
-    for (int s = 0; s < BK / 2; ++s) {
+    for (int q = 0; q < BK / 16; ++q) {
+      float4 af[MI][2], bf[NI][2];
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
-        const float4 q = af[i][s >> 2];
-        const float a = (s & 3) == 0 ? q.x : (s & 3) == 1 ? q.y : (s & 3) == 2 ? q.z : q.w;
+        const float* pa = &As[cur][(wm * MI * 32 + i * 32 + lr) * LDK + q * 16 + lh * 8];
+        af[i][0] = *reinterpret_cast<const float4*>(pa);
+        af[i][1] = *reinterpret_cast<const float4*>(pa + 4);
+      }
 #pragma unroll
-        for (int j = 0; j < NI; ++j) {
-          const float4 u = bf[j][s >> 2];
-          const float b = (s & 3) == 0 ? u.x : (s & 3) == 1 ? u.y : (s & 3) == 2 ? u.z : u.w;
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[i][j], 0, 0, 0);
+      for (int j = 0; j < NI; ++j) {
+        const float* pb = &Bs[cur][(wn * NI * 32 + j * 32 + lr) * LDK + q * 16 + lh * 8];
+        bf[j][0] = *reinterpret_cast<const float4*>(pb);
+        bf[j][1] = *reinterpret_cast<const float4*>(pb + 4);
+      }
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const float a = pick(af[i][s >> 2], s);
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, pick(bf[j][s >> 2], s), acc[i][j], 0, 0, 0);
         }
       }
     }
+    __builtin_amdgcn_sched_barrier(0);
     if (more) {
       store_tile<AM, BMr>(la, As[cur ^ 1]);
       store_tile<BMODE, BNr>(lb, Bs[cur ^ 1]);
@@ -436,36 +496,54 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+
 template <int WM, int WN, int MI, int NI, int AM, int BMODE, int OM>
-int launch_cfg(const Params& P, int gz, hipStream_t s) {
+int launch_cfg(Params P, int gz, hipStream_t s) {
   constexpr int BMr = WM * MI * 32, BNr = WN * NI * 32;
-  dim3 grid((P.N + BNr - 1) / BNr, (P.M + BMr - 1) / BMr, gz);
-  hipLaunchKernelGGL((k_gemm<WM, WN, MI, NI, AM, BMODE, OM>), grid, dim3(256), 0, s, P);
+  P.tiles_m = (P.M + BMr - 1) / BMr;
+  P.tiles_n = (P.N + BNr - 1) / BNr;
+  P.tiles_z = gz;
+  const int64_t nwg = (int64_t)P.tiles_m * P.tiles_n * gz;
+  RRAM_REQUIRE(nwg < (1ll << 31), "gemm: grid too large");
+  hipLaunchKernelGGL((k_gemm<WM, WN, MI, NI, AM, BMODE, OM>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, P);
   return launch_status("gemm");
 }
 
-// Tile choice: 128x128 when the grid still fills the chip, else 64x64.
+// Tile choice: 128x128 when that grid still fills the chip (>= 2 waves of
+// 256 CUs), 64x128 for M <= 64, else 64x64.  force_big: split-K grids.
 template <int AM, int BMODE, int OM>
-int launch(const Params& P, int gz, hipStream_t s) {
+int launch(const Params& P, int gz, hipStream_t s, bool force_big) {
   const int64_t big = (int64_t)((P.N + 127) / 128) * ((P.M + 127) / 128) * gz;
-  if (P.M > 64 && big >= 512) return launch_cfg<2, 2, 2, 2, AM, BMODE, OM>(P, gz, s);
+  if (force_big || (P.M > 64 && big >= 512)) return launch_cfg<2, 2, 2, 2, AM, BMODE, OM>(P, gz, s);
   if (P.M <= 64) return launch_cfg<1, 4, 2, 1, AM, BMODE, OM>(P, gz, s);  // 64 x 128
   return launch_cfg<2, 2, 1, 1, AM, BMODE, OM>(P, gz, s);                 // 64 x 64
 }
 
-int dispatch(int am, int bm, int om, const Params& P, int gz, hipStream_t s) {
+int dispatch(int am, int bm, int om, const Params& P, int gz, hipStream_t s, bool force_big = false) {
 #define RRAM_D(A_, B_, O_) \
-  if (am == A_ && bm == B_ && om == O_) return launch<A_, B_, O_>(P, gz, s);
+  if (am == A_ && bm == B_ && om == O_) return launch<A_, B_, O_>(P, gz, s, force_big);
   RRAM_D(KC, KC, OUT_ROWMAJOR)
+  RRAM_D(KCV, KC, OUT_ROWMAJOR)
+  RRAM_D(KC, KCV, OUT_ROWMAJOR)
+  RRAM_D(KCV, KCV, OUT_ROWMAJOR)
   RRAM_D(KC, RC, OUT_ROWMAJOR)
+  RRAM_D(KCV, RC, OUT_ROWMAJOR)
   RRAM_D(RC, KC, OUT_ROWMAJOR)
+  RRAM_D(RC, KCV, OUT_ROWMAJOR)
   RRAM_D(RC, RC, OUT_ROWMAJOR)
   RRAM_D(KC, CONV, OUT_NCHW)
+  RRAM_D(KCV, CONV, OUT_NCHW)
   RRAM_D(NCHW, KC, OUT_ROWMAJOR)
+  RRAM_D(NCHW, KCV, OUT_ROWMAJOR)
   RRAM_D(RC, NCHWT, OUT_ROWMAJOR)
 #undef RRAM_D
   set_error("gemm: unsupported operand combination %d/%d/%d", am, bm, om);
   return RRAM_EUNSUPPORTED;
+}
+
+// KC view eligible for 16-byte loads (also for every group offset)
+bool vec_ok(const float* p, int64_t ld, int K, int64_t grp = 0) {
+  return (reinterpret_cast<uintptr_t>(p) & 15u) == 0 && (ld & 3) == 0 && (K & 3) == 0 && (grp & 3) == 0;
 }
 
 Epi make_epi(float* C, int64_t ldc, float alpha, float beta, const float* bias, int bias_mode,
@@ -496,7 +574,7 @@ View make_view(const float* p, int64_t ld, int rows, int kdim) {
 
 }  // namespace
 
-// Shared by conv.cpp-style entry points below.
+// Shared by the C-ABI entry points in conv_api.hip.
 int gemm_core(int trans_a, int trans_b, int M, int N, int K, float alpha, const float* A, int lda,
               const float* B, int ldb, float beta, float* C, int ldc, const float* bias,
               int bias_mode, int relu, void* ws, size_t ws_bytes, hipStream_t s) {
@@ -505,9 +583,10 @@ int gemm_core(int trans_a, int trans_b, int M, int N, int K, float alpha, const 
   RRAM_REQUIRE(C != nullptr, "gemm: C is NULL");
   RRAM_REQUIRE(K == 0 || (A && B), "gemm: A/B NULL");
   RRAM_REQUIRE(ldc >= N, "gemm: ldc < N");
+  RRAM_REQUIRE(trans_a ? lda >= M : lda >= K || K == 0, "gemm: lda too small");
+  RRAM_REQUIRE(trans_b ? ldb >= K || K == 0 : ldb >= N, "gemm: ldb too small");
   Params P{};
-  // A view: rows = M, contraction = K
-  P.a = trans_a ? make_view(A, lda, M, K) : make_view(A, lda, M, K);
+  P.a = make_view(A, lda, M, K);
   P.b = make_view(B, ldb, N, K);
   P.e = make_epi(C, ldc, alpha, beta, bias, bias_mode, relu);
   P.M = M;
@@ -516,10 +595,10 @@ int gemm_core(int trans_a, int trans_b, int M, int N, int K, float alpha, const 
   P.split = 1;
   P.k_chunk = K;
   // op(A)(m,k) = trans_a ? A[k*lda+m] : A[m*lda+k]; op(B)(k,n) = trans_b ? B[n*ldb+k] : B[k*ldb+n]
-  const int am = trans_a ? RC : KC;
-  const int bm = trans_b ? KC : RC;
-  RRAM_REQUIRE(trans_a ? lda >= M : lda >= K || K == 0, "gemm: lda too small");
-  RRAM_REQUIRE(trans_b ? ldb >= K || K == 0 : ldb >= N, "gemm: ldb too small");
+  int am = trans_a ? RC : KC;
+  int bm = trans_b ? KC : RC;
+  if (am == KC && vec_ok(A, lda, K)) am = KCV;
+  if (bm == KC && vec_ok(B, ldb, K)) bm = KCV;
   // split-K when the 128x128 grid is far below the CU count and K is long
   const int64_t tiles = (int64_t)((N + 127) / 128) * ((M + 127) / 128);
   int split = 1;
@@ -536,17 +615,7 @@ int gemm_core(int trans_a, int trans_b, int M, int N, int K, float alpha, const 
     P.split = split;
     P.k_chunk = chunk;
     P.ws = static_cast<float*>(ws);
-    // big tiles for the split grid
-    dim3 grid((N + 127) / 128, (M + 127) / 128, split);
-    if (am == KC && bm == KC)
-      hipLaunchKernelGGL((k_gemm<2, 2, 2, 2, KC, KC, OUT_ROWMAJOR>), grid, dim3(256), 0, s, P);
-    else if (am == KC && bm == RC)
-      hipLaunchKernelGGL((k_gemm<2, 2, 2, 2, KC, RC, OUT_ROWMAJOR>), grid, dim3(256), 0, s, P);
-    else if (am == RC && bm == KC)
-      hipLaunchKernelGGL((k_gemm<2, 2, 2, 2, RC, KC, OUT_ROWMAJOR>), grid, dim3(256), 0, s, P);
-    else
-      hipLaunchKernelGGL((k_gemm<2, 2, 2, 2, RC, RC, OUT_ROWMAJOR>), grid, dim3(256), 0, s, P);
-    int rc = launch_status("gemm splitk");
+    int rc = dispatch(am, bm, OUT_ROWMAJOR, P, split, s, true);
     if (rc) return rc;
     hipLaunchKernelGGL(k_splitk_reduce, dim3(stream_blocks((int64_t)M * N)), dim3(256), 0, s,
                        P.ws, split, M, N, P.e);
@@ -554,6 +623,7 @@ int gemm_core(int trans_a, int trans_b, int M, int N, int K, float alpha, const 
   }
   return dispatch(am, bm, OUT_ROWMAJOR, P, 1, s);
 }
+
 
 int conv_fwd_core(const rram_conv_desc* d, const float* x, const float* w, const float* bias,
                   float* y, int relu, hipStream_t s) {
@@ -588,6 +658,7 @@ int conv_fwd_core(const rram_conv_desc* d, const float* x, const float* w, const
   cv.howo = make_fastdiv(HoWo);
   cv.wo_div = make_fastdiv(d->out_w);
   cv.chw = (int64_t)d->channels * d->height * d->width;
+  RRAM_REQUIRE(cv.chw < (1ll << 31), "conv2d_fwd: one image must have < 2^31 elements");
   P.e = make_epi(y, HoWo, 1.0f, 0.0f, bias, RRAM_BIAS_ROW, relu);
   P.e.cimg = (int64_t)d->num_output * HoWo;
   P.e.hw = make_fastdiv(HoWo);
@@ -595,7 +666,7 @@ int conv_fwd_core(const rram_conv_desc* d, const float* x, const float* w, const
   P.grp_b = (int64_t)cin_g * d->height * d->width;
   P.grp_c = (int64_t)cout_g * HoWo;
   P.grp_bias = cout_g;
-  return dispatch(KC, CONV, OUT_NCHW, P, g, s);
+  return dispatch(vec_ok(w, K, K, P.grp_a) ? KCV : KC, CONV, OUT_NCHW, P, g, s);
 }
 
 // dW_g[co][k] += sum_p dY_g[co][p] col_g[k][p]   (col: [Cin*kh*kw][ldcol])
@@ -617,7 +688,7 @@ int conv_bwd_weight_core(const rram_conv_desc* d, int nimg, const float* dy, con
     P.a.hw = make_fastdiv(HoWo);
     P.b = make_view(col + (int64_t)gi * K * ldcol, ldcol, K, P.K);
     P.e = make_epi(dw + (int64_t)gi * cout_g * K, K, 1.0f, 1.0f, nullptr, 0, 0);
-    const int rc = dispatch(NCHW, KC, OUT_ROWMAJOR, P, 1, s);
+    const int rc = dispatch(NCHW, vec_ok(P.b.p, ldcol, P.K) ? KCV : KC, OUT_ROWMAJOR, P, 1, s);
     if (rc) return rc;
   }
   return RRAM_OK;

@@ -10,9 +10,17 @@
 namespace rram {
 namespace {
 
-#define GRID_LOOP(i, n)                                                            \
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < (n); \
-       i += (int64_t)gridDim.x * blockDim.x)
+// a^b for a > 0 via the native v_log_f32 / v_exp_f32 (powf's special-case
+// handling is not needed for LRN scales, which are >= k > 0)
+__device__ __forceinline__ float pow_pos(float a, float b) { return exp2f(b * log2f(a)); }
+
+// 32-bit index arithmetic (64-bit division is a long software sequence on
+// the VALU); every host wrapper checks that its element count is < 2^31.
+#define GRID_LOOP(i, n)                                                                    \
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < static_cast<int>(n); \
+       i += gridDim.x * blockDim.x)
+#define RRAM_REQUIRE_I32(total, what) \
+  RRAM_REQUIRE((int64_t)(total) < 2147483647ll, what ": more than 2^31 elements is not supported")
 
 // relu_layer.cu:9-15 / :35-44
 __global__ void k_relu_fwd(const float* __restrict__ x, float* __restrict__ y, int64_t n, float slope) {
@@ -122,7 +130,7 @@ __global__ void k_lrn_fwd(const float* __restrict__ x, float* __restrict__ y, fl
     }
     const float sc = k + acc * alpha_over_size;
     if (scale) scale[idx] = sc;
-    y[idx] = x[idx] * powf(sc, -beta);
+    y[idx] = x[idx] * pow_pos(sc, -beta);
   }
 }
 
@@ -145,7 +153,7 @@ __global__ void k_lrn_bwd(const float* __restrict__ x, const float* __restrict__
       const int64_t o = base + (int64_t)j * HW;
       ratio += dy[o] * y[o] / scale[o];
     }
-    dx[idx] = dy[idx] * powf(scale[idx], -beta) - cache_ratio * x[idx] * ratio;
+    dx[idx] = dy[idx] * pow_pos(scale[idx], -beta) - cache_ratio * x[idx] * ratio;
   }
 }
 
@@ -175,7 +183,7 @@ __global__ void k_lrn_within_fwd(const float* __restrict__ x, float* __restrict_
     const float n = static_cast<float>(within_psize(h, pre, size, H) * within_psize(w, pre, size, W));
     const float sc = 1.0f + alpha * (s / n);
     if (scale) scale[idx] = sc;
-    y[idx] = x[idx] * powf(sc, -beta);
+    y[idx] = x[idx] * pow_pos(sc, -beta);
   }
 }
 __global__ void k_lrn_within_bwd(const float* __restrict__ x, const float* __restrict__ scale,
@@ -195,9 +203,9 @@ __global__ void k_lrn_within_bwd(const float* __restrict__ x, const float* __res
       for (int b = qs; b <= qe; ++b) {
         const int64_t o = base + a * W + b;
         const float n = static_cast<float>(within_psize(a, pre, size, H) * within_psize(b, pre, size, W));
-        acc += dy[o] * x[o] * powf(scale[o], -beta - 1.0f) / n;
+        acc += dy[o] * x[o] * pow_pos(scale[o], -beta - 1.0f) / n;
       }
-    dx[idx] = dy[idx] * powf(scale[idx], -beta) - 2.0f * alpha * beta * x[idx] * acc;
+    dx[idx] = dy[idx] * pow_pos(scale[idx], -beta) - 2.0f * alpha * beta * x[idx] * acc;
   }
 }
 
@@ -296,41 +304,42 @@ __global__ void k_count_valid(const float* __restrict__ label, int64_t n, int ig
 }
 
 // accuracy_layer.cpp:48-90: label counted correct when its (value, index)
-// pair is within the top_k of the descending pair order.
+// pair is within the top_k of the descending pair order.  One wave per
+// sample (lanes over classes); single block, deterministic integer sums.
 __global__ void __launch_bounds__(1024) k_accuracy(const float* __restrict__ x,
                                                    const float* __restrict__ label, float* correct,
                                                    float* count, float* ratio, int outer, int C,
                                                    int inner, int top_k, int ignore) {
   __shared__ float sa[16], sc[16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   float acc = 0.0f, cnt = 0.0f;
   const int64_t cols = (int64_t)outer * inner;
-  for (int64_t col = threadIdx.x; col < cols; col += blockDim.x) {
+  for (int64_t col = wave; col < cols; col += nw) {
     const int64_t o = col / inner, q = col - o * inner;
     const int lv = static_cast<int>(label[col]);
     if (ignore >= 0 && lv == ignore) continue;
     const float* xs = x + o * C * inner + q;
     const float v = xs[(int64_t)lv * inner];
     int rank = 0;
-    for (int c = 0; c < C; ++c) {
+    for (int c = lane; c < C; c += 64) {
       const float u = xs[(int64_t)c * inner];
       rank += (u > v) || (u == v && c > lv);
     }
-    acc += rank < top_k ? 1.0f : 0.0f;
-    cnt += 1.0f;
-  }
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    acc += __shfl_xor(acc, off, 64);
-    cnt += __shfl_xor(cnt, off, 64);
+    for (int off = 32; off > 0; off >>= 1) rank += __shfl_xor(rank, off, 64);
+    if (lane == 0) {
+      acc += rank < top_k ? 1.0f : 0.0f;
+      cnt += 1.0f;
+    }
   }
-  if ((threadIdx.x & 63) == 0) {
-    sa[threadIdx.x >> 6] = acc;
-    sc[threadIdx.x >> 6] = cnt;
+  if (lane == 0) {
+    sa[wave] = acc;
+    sc[wave] = cnt;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     float A = 0.0f, N = 0.0f;
-    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
+    for (int i = 0; i < nw; ++i) {
       A += sa[i];
       N += sc[i];
     }
@@ -361,6 +370,7 @@ extern "C" {
 
 int rram_relu_fwd(const float* x, float* y, int64_t n, float slope, rram_stream_t s) {
   RRAM_REQUIRE(n >= 0, "relu: n < 0");
+  RRAM_REQUIRE_I32(n, "relu");
   if (n == 0) return RRAM_OK;
   RRAM_REQUIRE(x && y, "relu: NULL");
   hipLaunchKernelGGL(k_relu_fwd, dim3(stream_blocks(n)), dim3(kThreads), 0, as_stream(s), x, y, n, slope);
@@ -368,6 +378,7 @@ int rram_relu_fwd(const float* x, float* y, int64_t n, float slope, rram_stream_
 }
 int rram_relu_bwd(const float* x, const float* dy, float* dx, int64_t n, float slope, rram_stream_t s) {
   RRAM_REQUIRE(n >= 0, "relu: n < 0");
+  RRAM_REQUIRE_I32(n, "relu");
   if (n == 0) return RRAM_OK;
   RRAM_REQUIRE(x && dy && dx, "relu: NULL");
   hipLaunchKernelGGL(k_relu_bwd, dim3(stream_blocks(n)), dim3(kThreads), 0, as_stream(s), x, dy, dx, n, slope);
@@ -381,6 +392,7 @@ int rram_pool_fwd(const float* x, float* y, int* mask, int num, int C, int H, in
                "pool_fwd: bad geometry");
   RRAM_REQUIRE(method == RRAM_POOL_MAX || method == RRAM_POOL_AVE, "pool_fwd: bad method");
   const int64_t total = (int64_t)num * C * PH * PW;
+  RRAM_REQUIRE_I32(total, "layer kernel");
   if (total == 0) return RRAM_OK;
   RRAM_REQUIRE(x && y, "pool_fwd: NULL");
   hipLaunchKernelGGL(k_pool_fwd, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), x, y,
@@ -393,6 +405,7 @@ int rram_pool_bwd(const float* dy, const int* mask, float* dx, int num, int C, i
                "pool_bwd: bad geometry");
   RRAM_REQUIRE(method != RRAM_POOL_MAX || mask != nullptr, "pool_bwd: MAX needs mask");
   const int64_t total = (int64_t)num * C * H * W;
+  RRAM_REQUIRE_I32(total, "layer kernel");
   if (total == 0) return RRAM_OK;
   RRAM_REQUIRE(dy && dx, "pool_bwd: NULL");
   hipLaunchKernelGGL(k_pool_bwd, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), dy,
@@ -405,6 +418,7 @@ int rram_lrn_fwd(const float* x, float* y, float* scale, int num, int C, int H, 
   RRAM_REQUIRE(num >= 0 && C > 0 && H > 0 && W > 0 && size > 0 && (size & 1),
                "lrn_fwd: bad geometry (local_size must be odd)");
   const int64_t total = (int64_t)num * C * H * W;
+  RRAM_REQUIRE_I32(total, "layer kernel");
   if (total == 0) return RRAM_OK;
   RRAM_REQUIRE(x && y, "lrn_fwd: NULL");
   hipLaunchKernelGGL(k_lrn_fwd, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), x, y,
@@ -416,6 +430,7 @@ int rram_lrn_bwd(const float* x, const float* y, const float* scale, const float
   RRAM_REQUIRE(num >= 0 && C > 0 && H > 0 && W > 0 && size > 0 && (size & 1),
                "lrn_bwd: bad geometry");
   const int64_t total = (int64_t)num * C * H * W;
+  RRAM_REQUIRE_I32(total, "layer kernel");
   if (total == 0) return RRAM_OK;
   RRAM_REQUIRE(x && y && scale && dy && dx, "lrn_bwd: NULL");
   hipLaunchKernelGGL(k_lrn_bwd, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), x, y,
@@ -427,6 +442,7 @@ int rram_lrn_within_fwd(const float* x, float* y, float* scale, int num, int C, 
                         float alpha, float beta, rram_stream_t s) {
   RRAM_REQUIRE(num >= 0 && C > 0 && H > 0 && W > 0 && size > 0 && (size & 1), "lrn_within_fwd: bad geometry");
   const int64_t total = (int64_t)num * C * H * W;
+  RRAM_REQUIRE_I32(total, "layer kernel");
   if (total == 0) return RRAM_OK;
   RRAM_REQUIRE(x && y, "lrn_within_fwd: NULL");
   hipLaunchKernelGGL(k_lrn_within_fwd, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), x, y,
@@ -437,6 +453,7 @@ int rram_lrn_within_bwd(const float* x, const float* scale, const float* dy, flo
                         int W, int size, float alpha, float beta, rram_stream_t s) {
   RRAM_REQUIRE(num >= 0 && C > 0 && H > 0 && W > 0 && size > 0 && (size & 1), "lrn_within_bwd: bad geometry");
   const int64_t total = (int64_t)num * C * H * W;
+  RRAM_REQUIRE_I32(total, "layer kernel");
   if (total == 0) return RRAM_OK;
   RRAM_REQUIRE(x && scale && dy && dx, "lrn_within_bwd: NULL");
   hipLaunchKernelGGL(k_lrn_within_bwd, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), x, scale,
@@ -468,6 +485,7 @@ int rram_softmax_loss_bwd(const float* prob, const float* label, float* dx, int 
                           int inner, int ignore, float loss_weight, rram_stream_t s) {
   RRAM_REQUIRE(outer >= 0 && C > 0 && inner > 0, "softmax_loss_bwd: bad shape");
   const int64_t total = (int64_t)outer * C * inner;
+  RRAM_REQUIRE_I32(total, "layer kernel");
   if (total == 0) return RRAM_OK;
   RRAM_REQUIRE(prob && label && dx, "softmax_loss_bwd: NULL");
   // normalizer = #valid labels; computed on host for the common no-ignore case
@@ -503,6 +521,7 @@ int rram_concat_copy(const float* src, float* dst, int num, int sci, int dci, in
   RRAM_REQUIRE(num >= 0 && sci >= 0 && dci >= sci && off >= 0 && off + sci <= dci,
                "concat: bad geometry");
   const int64_t total = (int64_t)num * sci;
+  RRAM_REQUIRE_I32(total, "layer kernel");
   if (total == 0) return RRAM_OK;
   RRAM_REQUIRE(src && dst, "concat: NULL");
   hipLaunchKernelGGL(k_concat, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), src, dst,

@@ -702,7 +702,7 @@ class SyntheticDataLayer : public Layer<Dtype> {
     top[0]->Reshape(s);
     const float scale = (float)tp.num("scale", 1.0);
     const bool mean = tp.has("mean_file") || tp.has("mean_value");
-    const uint64_t seed = Caffe::seed() ^ 0xDA7Aull;
+    const uint64_t seed = Caffe::seed() ^ 0xDA7Aull ^ ((uint64_t)p.integer("rram_data_seed", 0) * 0x9E3779B97F4A7C15ull);
     RRAM_CALL(rram_fill_uniform_int(top[0]->mutable_gpu_data(), top[0]->count(), 256, mean ? -128.0f : 0.0f,
                                     seed, this->layer_id * 16, Caffe::stream()));
     if (scale != 1.0f) RRAM_CALL(rram_scal(top[0]->count(), scale, top[0]->mutable_gpu_data(), Caffe::stream()));

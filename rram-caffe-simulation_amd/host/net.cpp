@@ -159,6 +159,7 @@ Net<Dtype>::Net(const Msg& in_param, Phase phase, const Msg& options) : phase_(p
     if (type == "Data" || type == "ImageData" || type == "HDF5Data" || type == "MemoryData" || type == "WindowData") {
       for (int d : data_shape) lp.add("rram_data_shape", std::to_string(d));
       lp.set("rram_num_classes", options.str("num_classes", "10"));
+      lp.set("rram_data_seed", options.str("data_seed", "0"));
     }
     auto layer = LayerRegistry<Dtype>::CreateLayer(lp);
     layer->layer_id = static_cast<uint32_t>(lid);
