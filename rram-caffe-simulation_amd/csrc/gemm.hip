@@ -66,6 +66,7 @@ struct ConvGeom {
   int C, H, W, KH, KW, ph, pw, sh, sw, dh, dw, Ho, Wo;
   FastDiv khkw, kw_div, howo, wo_div;
   int64_t chw;  // image stride of the input (C*H*W)
+  int in_bytes; // bytes addressable from the group's input base (buffer range)
 };
 
 struct Epi {
@@ -97,6 +98,8 @@ struct ConvCol {
   int64_t base;  // image offset of this thread's column (n*C*H*W)
   int hb, wb;    // ho*sh - ph, wo*sw - pw
   bool valid;
+  int pbase;     // n*C*H*W + hb*W + wb (element offset inside the group's input)
+  __amdgpu_buffer_rsrc_t rsrc;  // raw buffer over the group's input (OOB loads return 0)
 };
 
 template <int ROWS>
@@ -172,6 +175,41 @@ __device__ __forceinline__ void load_tile(Loader<ROWS>& L, const View& vw, const
     }
     return;
   }
+  if (MODE == CONV) {
+    // implicit im2col: thread = one output position (row) x EPT consecutive k.
+    // The k segment start is wave-uniform (ROWS >= 64), so (c, kh, kw) is
+    // decomposed once per tile on the scalar unit and stepped incrementally;
+    // per element the VALU does two bounds compares and one offset add, and
+    // the load is a raw buffer load whose out-of-range offset returns 0.
+    const int seg = threadIdx.x / ROWS;
+    const int ks = __builtin_amdgcn_readfirstlane(k0 + seg * EPT);
+    uint32_t c = fdiv(static_cast<uint32_t>(ks), cv.khkw);
+    const uint32_t rem = static_cast<uint32_t>(ks) - c * cv.khkw.d;
+    uint32_t kh = fdiv(rem, cv.kw_div);
+    uint32_t kw = rem - kh * cv.kw_div.d;
+    const int HW = cv.H * cv.W;
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int khd = static_cast<int>(kh) * cv.dh, kwd = static_cast<int>(kw) * cv.dw;
+      const bool ok = col.valid && (ks + i) < kend &&
+                      static_cast<unsigned>(col.hb + khd) < static_cast<unsigned>(cv.H) &&
+                      static_cast<unsigned>(col.wb + kwd) < static_cast<unsigned>(cv.W);
+      const int soff = static_cast<int>(c) * HW + khd * cv.W + kwd;  // wave-uniform
+      const uint32_t boff = ok ? static_cast<uint32_t>(col.pbase + soff) * 4u : 0xFFFFFFFFu;
+      L.v[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(col.rsrc, boff, 0, 0));
+      // step (c, kh, kw) by one k
+      ++kw;
+      if (kw == cv.kw_div.d) {
+        kw = 0;
+        ++kh;
+        if (kh * cv.kw_div.d == cv.khkw.d) {
+          kh = 0;
+          ++c;
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < EPT; ++i) {
     const int e = threadIdx.x + i * 256;
@@ -186,21 +224,8 @@ __device__ __forceinline__ void load_tile(Loader<ROWS>& L, const View& vw, const
       x = ld_rc(vw, row, k, k < kend);
     } else if (MODE == NCHW) {
       x = ld_nchw(vw, row, k, k < kend);
-    } else if (MODE == NCHWT) {
+    } else {
       x = ld_nchwt(vw, row, k, k < kend);
-    } else {  // CONV gather: k is wave-uniform (ROWS >= 64), decomposed on the scalar unit
-      const int ku = __builtin_amdgcn_readfirstlane(k);
-      const uint32_t c = fdiv(static_cast<uint32_t>(ku), cv.khkw);
-      const uint32_t rem = static_cast<uint32_t>(ku) - c * cv.khkw.d;
-      const uint32_t kh = fdiv(rem, cv.kw_div);
-      const uint32_t kw = rem - kh * cv.kw_div.d;
-      const int iy = col.hb + static_cast<int>(kh) * cv.dh;
-      const int ix = col.wb + static_cast<int>(kw) * cv.dw;
-      const bool ok = col.valid && ku < kend && static_cast<unsigned>(iy) < static_cast<unsigned>(cv.H) &&
-                      static_cast<unsigned>(ix) < static_cast<unsigned>(cv.W);
-      // 32-bit offset inside the image (C*H*W < 2^31 is checked on the host)
-      const int off = static_cast<int>(c) * (cv.H * cv.W) + iy * cv.W + ix;
-      x = ld_guard(vw.p + col.base, off, ok);
     }
     L.v[i] = x;
   }
@@ -209,6 +234,15 @@ __device__ __forceinline__ void load_tile(Loader<ROWS>& L, const View& vw, const
 template <int MODE, int ROWS>
 __device__ __forceinline__ void store_tile(const Loader<ROWS>& L, float* lds) {
   constexpr int EPT = Loader<ROWS>::EPT;
+  if (MODE == CONV) {
+    // EPT consecutive k of one row: 16-byte LDS writes (row stride 36 dwords
+    // puts the 8 lanes of a ds_write_b128 group on distinct bank quads)
+    float* dst = lds + (threadIdx.x % ROWS) * LDK + (threadIdx.x / ROWS) * EPT;
+#pragma unroll
+    for (int i = 0; i < EPT / 4; ++i)
+      *reinterpret_cast<float4*>(dst + 4 * i) = make_float4(L.v[4 * i], L.v[4 * i + 1], L.v[4 * i + 2], L.v[4 * i + 3]);
+    return;
+  }
   if (MODE == KCV) {
 #pragma unroll
     for (int i = 0; i < EPT / 4; ++i) {
@@ -290,7 +324,10 @@ __global__ void __launch_bounds__(256) k_gemm(Params P) {
       col.hb = static_cast<int>(ho) * P.cv.sh - P.cv.ph;
       col.wb = static_cast<int>(wo) * P.cv.sw - P.cv.pw;
       col.valid = true;
+      col.pbase = static_cast<int>(col.base) + col.hb * P.cv.W + col.wb;
     }
+    // group base pointer, range = the whole remaining input (host checks < 2^32 bytes)
+    col.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(vb.p), 0, P.cv.in_bytes, 0x00020000);
   }
 
   floatx16 acc[MI][NI];
@@ -509,14 +546,34 @@ int launch_cfg(Params P, int gz, hipStream_t s) {
   return launch_status("gemm");
 }
 
-// Tile choice: 128x128 when that grid still fills the chip (>= 2 waves of
-// 256 CUs), 64x128 for M <= 64, else 64x64.  force_big: split-K grids.
+// Tile choice.  BN = 128 with BM in {192, 128, 96, 64} picked to minimise the
+// padded rows of M (AlexNet: conv1 M = 96, conv4 M = 192 per group) as long as
+// the grid keeps >= 2 blocks per CU; 64x64 when even that grid is too small.
+// force_big: split-K grids (128x128).
 template <int AM, int BMODE, int OM>
 int launch(const Params& P, int gz, hipStream_t s, bool force_big) {
-  const int64_t big = (int64_t)((P.N + 127) / 128) * ((P.M + 127) / 128) * gz;
-  if (force_big || (P.M > 64 && big >= 512)) return launch_cfg<2, 2, 2, 2, AM, BMODE, OM>(P, gz, s);
-  if (P.M <= 64) return launch_cfg<1, 4, 2, 1, AM, BMODE, OM>(P, gz, s);  // 64 x 128
-  return launch_cfg<2, 2, 1, 1, AM, BMODE, OM>(P, gz, s);                 // 64 x 64
+  if (force_big) return launch_cfg<2, 2, 2, 2, AM, BMODE, OM>(P, gz, s);
+  const int64_t ntn = (P.N + 127) / 128;
+  const int cands[4] = {128, 192, 96, 64};  // ties keep 128 (2 blocks per CU)
+  int best = 0;
+  int64_t best_pad = -1;
+  for (int c : cands) {
+    const int64_t tiles_m = (P.M + c - 1) / c;
+    if (tiles_m * ntn * gz < 512 && c != 64) continue;
+    const int64_t pad = tiles_m * c - P.M;
+    if (best_pad < 0 || pad < best_pad) {
+      best = c;
+      best_pad = pad;
+    }
+  }
+  if (best == 64 && ntn * ((P.M + 63) / 64) * gz < 256)
+    return launch_cfg<2, 2, 1, 1, AM, BMODE, OM>(P, gz, s);  // 64 x 64: twice the blocks
+  switch (best) {
+    case 192: return launch_cfg<2, 2, 3, 2, AM, BMODE, OM>(P, gz, s);  // 192 x 128
+    case 128: return launch_cfg<2, 2, 2, 2, AM, BMODE, OM>(P, gz, s);  // 128 x 128
+    case 96: return launch_cfg<1, 4, 3, 1, AM, BMODE, OM>(P, gz, s);   //  96 x 128
+    default: return launch_cfg<1, 4, 2, 1, AM, BMODE, OM>(P, gz, s);   //  64 x 128
+  }
 }
 
 int dispatch(int am, int bm, int om, const Params& P, int gz, hipStream_t s, bool force_big = false) {
@@ -658,7 +715,8 @@ int conv_fwd_core(const rram_conv_desc* d, const float* x, const float* w, const
   cv.howo = make_fastdiv(HoWo);
   cv.wo_div = make_fastdiv(d->out_w);
   cv.chw = (int64_t)d->channels * d->height * d->width;
-  RRAM_REQUIRE(cv.chw < (1ll << 31), "conv2d_fwd: one image must have < 2^31 elements");
+  RRAM_REQUIRE((int64_t)d->num * cv.chw * 4 < (1ll << 31), "conv2d_fwd: input must be < 2 GiB (32-bit buffer offsets)");
+  cv.in_bytes = static_cast<int>((int64_t)d->num * cv.chw * 4);
   P.e = make_epi(y, HoWo, 1.0f, 0.0f, bias, RRAM_BIAS_ROW, relu);
   P.e.cimg = (int64_t)d->num_output * HoWo;
   P.e.hw = make_fastdiv(HoWo);

@@ -134,6 +134,43 @@ __global__ void k_lrn_fwd(const float* __restrict__ x, float* __restrict__ y, fl
   }
 }
 
+// lrn_layer.cu LRNFillScale's sliding window (same add-then-subtract order):
+// one thread per (n, h, w) column walks the channels with the window in
+// registers, so x is read once and y written once.
+template <int SIZE>
+__global__ void __launch_bounds__(256) k_lrn_fwd_slide(const float* __restrict__ x, float* __restrict__ y,
+                                                       float* __restrict__ scale, int num, int C, int HW,
+                                                       float alpha_over_size, float beta, float k) {
+  constexpr int PRE = (SIZE - 1) / 2, POST = SIZE - PRE - 1;
+  GRID_LOOP(idx, num * HW) {
+    const int s = idx % HW;
+    const int64_t base = (int64_t)(idx / HW) * C * HW + s;
+    const float* xc = x + base;
+    float* yc = y + base;
+    float win[SIZE];
+#pragma unroll
+    for (int j = 0; j < SIZE; ++j) {
+      const int cc = j - PRE;
+      win[j] = (cc >= 0 && cc < C) ? xc[(int64_t)cc * HW] : 0.0f;
+    }
+    float acc = 0.0f;
+#pragma unroll
+    for (int j = PRE; j < SIZE; ++j) acc += win[j] * win[j];
+    for (int c = 0; c < C; ++c) {
+      const float sc = k + acc * alpha_over_size;
+      if (scale) scale[base + (int64_t)c * HW] = sc;
+      yc[(int64_t)c * HW] = win[PRE] * pow_pos(sc, -beta);
+      const float out = win[0];
+#pragma unroll
+      for (int j = 0; j < SIZE - 1; ++j) win[j] = win[j + 1];
+      const int cn = c + POST + 1;
+      win[SIZE - 1] = cn < C ? xc[(int64_t)cn * HW] : 0.0f;
+      acc += win[SIZE - 1] * win[SIZE - 1];
+      acc -= out * out;
+    }
+  }
+}
+
 // lrn_layer.cu LRNComputeDiff
 __global__ void k_lrn_bwd(const float* __restrict__ x, const float* __restrict__ y,
                           const float* __restrict__ scale, const float* __restrict__ dy,
@@ -421,8 +458,16 @@ int rram_lrn_fwd(const float* x, float* y, float* scale, int num, int C, int H, 
   RRAM_REQUIRE_I32(total, "layer kernel");
   if (total == 0) return RRAM_OK;
   RRAM_REQUIRE(x && y, "lrn_fwd: NULL");
-  hipLaunchKernelGGL(k_lrn_fwd, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), x, y,
-                     scale, num, C, H * W, size, alpha / size, beta, k);
+  const int cols = num * H * W;
+  if (size == 5)
+    hipLaunchKernelGGL(k_lrn_fwd_slide<5>, dim3(stream_blocks(cols)), dim3(kThreads), 0, as_stream(s), x, y,
+                       scale, num, C, H * W, alpha / size, beta, k);
+  else if (size == 3)
+    hipLaunchKernelGGL(k_lrn_fwd_slide<3>, dim3(stream_blocks(cols)), dim3(kThreads), 0, as_stream(s), x, y,
+                       scale, num, C, H * W, alpha / size, beta, k);
+  else
+    hipLaunchKernelGGL(k_lrn_fwd, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), x, y,
+                       scale, num, C, H * W, size, alpha / size, beta, k);
   return launch_status("lrn_fwd");
 }
 int rram_lrn_bwd(const float* x, const float* y, const float* scale, const float* dy, float* dx,
