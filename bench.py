@@ -34,11 +34,6 @@ MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 MFMA = fp32 vector pe
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 
 
-def conv_ip_flops(layers_desc, batch):
-    """Algorithmic FLOPs (2*M*N*K summed over conv incl. groups + IP) per batch."""
-    return sum(d["flops"] for d in layers_desc) * 1.0
-
-
 def alexnet_gemm_table(batch):
     """(layer, FLOPs per batch) for AlexNet at 227x227."""
     convs = [("conv1", 96, 3, 11, 55, 1), ("conv2", 256, 96, 5, 27, 2), ("conv3", 384, 256, 3, 13, 1),
@@ -124,6 +119,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--profile-layers", action="store_true", help="print the per-layer table to stderr")
+    ap.add_argument("--workload", default="alexnet_mc",
+                    choices=["alexnet_mc", "cifar10_quick_mc", "cifar10_full_train", "googlenet_sweep", "lenet_train"],
+                    help="alexnet_mc is the headline (BASELINE.json metric); the others are the remaining configs")
     args = ap.parse_args()
 
     import torch
@@ -139,6 +137,15 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
     caffe.set_stream_from_torch()
     caffe.set_random_seed(args.seed)
+    if args.workload != "alexnet_mc":
+        sys.path.insert(0, str(ROOT / "scripts"))
+        from bench_workloads import run_workload
+        res = run_workload(args, world, rank, dev)
+        if rank == 0:
+            print(json.dumps(res), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     net = caffe.Net(models.alexnet(test_batch=args.batch), "test", models.net_options("alexnet"))
     cfg = make_inject_cfg(args.p_fault)             # reference stuck-at semantics, neg/zero/pos 10/20/10

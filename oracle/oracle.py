@@ -254,6 +254,16 @@ def lrn(x, size, alpha, beta, k=1.0):
     return x * np.power(scale, -beta)
 
 
+def lrn_within(x, size, alpha, beta):
+    """lrn_layer.cpp WithinChannelForward (lines 155-163 + the LayerSetUp sub-net
+    at 17-62): square -> AVE pool(size, pad (size-1)/2, stride 1) -> power
+    (1 + alpha * avg)^-beta -> eltwise product with x."""
+    x = f32(x)
+    pre = (size - 1) // 2
+    avg = pool(x * x, size, 1, pre, "AVE")
+    return (x * np.power(np.float32(1.0) + np.float32(alpha) * avg, np.float32(-beta))).astype(np.float32)
+
+
 def relu(x, slope=0.0):
     x = f32(x)
     return np.where(x > 0, x, x * slope).astype(np.float32)

@@ -15,13 +15,6 @@ __device__ __forceinline__ bool aligned16(const void* p) {
   return (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
 }
 
-// Count `pred` over the wave and add it with one atomic from lane 0.
-__device__ __forceinline__ void wave_count_add(bool pred, unsigned long long* counter) {
-  const unsigned long long m = __ballot(pred);
-  if (counter != nullptr && (threadIdx.x & 63) == 0 && m != 0ull) {
-    atomicAdd(counter, static_cast<unsigned long long>(__popcll(m)));
-  }
-}
 // Block-level sum of per-lane counts, ONE atomic per block.  Many waves
 // adding to one address serialise at the memory side (MI355X_MICROARCH.md
 // "Global float atomics", contention row), so counters are flushed per block,
@@ -271,10 +264,11 @@ __device__ __forceinline__ float inject_pair(float w, uint64_t idx, uint64_t see
 }
 
 // Four consecutive elements starting at an even index i (two RNG pairs).
+template <bool FAST>
 __device__ __forceinline__ float4 inject4(float4 w, int64_t i, uint64_t seed, uint32_t map_id,
                                           const InjectSeg& g, unsigned& nb) {
   float o[4] = {w.x, w.y, w.z, w.w};
-  if (g.mode == 0) {
+  if (FAST || g.mode == 0) {
     // plain stuck-at fast path: one Philox call per pair of weights
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -310,9 +304,10 @@ __device__ __forceinline__ float4 inject4(float4 w, int64_t i, uint64_t seed, ui
   return make_float4(o[0], o[1], o[2], o[3]);
 }
 
+template <bool FAST>
 __device__ __forceinline__ float inject1(float w, int64_t i, uint64_t seed, uint32_t map_id,
                                          const InjectSeg& g, unsigned& nb) {
-  if (g.mode == 2) return inject_pair(w, (uint64_t)i, seed, map_id, g, nb);
+  if (!FAST && g.mode == 2) return inject_pair(w, (uint64_t)i, seed, map_id, g, nb);
   const uint64_t pr = (uint64_t)(i >> 1);
   const bool odd = (i & 1) != 0;
   const U32x4 r = draw(seed, pr, map_id, g.layer_id, kPurposeFault);
@@ -320,7 +315,7 @@ __device__ __forceinline__ float inject1(float w, int64_t i, uint64_t seed, uint
   const uint32_t rv = odd ? r.w : r.y;
   bool b;
   float out;
-  if (g.mode == 0) {
+  if (FAST || g.mode == 0) {
     b = static_cast<uint64_t>(rf) < g.thr_fault;
     out = b ? stuck_value(rv, g.thr_neg, g.thr_zero) * g.stuck_scale : w;
   } else {
@@ -338,6 +333,10 @@ __device__ __forceinline__ float inject1(float w, int64_t i, uint64_t seed, uint
   return out;
 }
 
+// FAST: every segment is plain stuck-at (mode 0), so the quantisation /
+// variation / pair paths are compiled out and the kernel's register budget is
+// that of the Philox + stuck-value path alone (higher occupancy).
+template <bool FAST>
 __global__ void __launch_bounds__(256)
     k_inject_batched(InjectSegs segs, uint64_t seed, uint32_t map_id, unsigned long long* counters) {
   const int64_t total = segs.chunk_start[segs.nsegs];
@@ -369,13 +368,13 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int64_t q = threadIdx.x + u * 256;
-        if (q < nv) d4[q] = inject4(buf[u], begin + 4 * q, seed, map_id, g, nb);
+        if (q < nv) d4[q] = inject4<FAST>(buf[u], begin + 4 * q, seed, map_id, g, nb);
       }
       for (int64_t i = begin + 4 * nv + threadIdx.x; i < end; i += 256)
-        g.dst[i] = inject1(g.src[i], i, seed, map_id, g, nb);
+        g.dst[i] = inject1<FAST>(g.src[i], i, seed, map_id, g, nb);
     } else {
       for (int64_t i = begin + threadIdx.x; i < end; i += 256)
-        g.dst[i] = inject1(g.src[i], i, seed, map_id, g, nb);
+        g.dst[i] = inject1<FAST>(g.src[i], i, seed, map_id, g, nb);
     }
   }
   if (cur >= 0) block_count_flush(nb, counters ? counters + cur : nullptr);
@@ -715,8 +714,14 @@ int rram_inject_rng_batched(const rram_inject_seg* segs, int nsegs, uint64_t see
   const int64_t total = is.chunk_start[nsegs];
   if (total == 0) return RRAM_OK;
   const int grid = static_cast<int>(total < kMaxStreamBlocks ? total : kMaxStreamBlocks);
-  hipLaunchKernelGGL(k_inject_batched, dim3(grid), dim3(kThreads), 0, as_stream(s), is, seed,
-                     map_id, counters);
+  bool fast = true;
+  for (int i = 0; i < nsegs; ++i) fast = fast && is.s[i].mode == 0;
+  if (fast)
+    hipLaunchKernelGGL(k_inject_batched<true>, dim3(grid), dim3(kThreads), 0, as_stream(s), is, seed,
+                       map_id, counters);
+  else
+    hipLaunchKernelGGL(k_inject_batched<false>, dim3(grid), dim3(kThreads), 0, as_stream(s), is, seed,
+                       map_id, counters);
   return launch_status("inject_rng");
 }
 

@@ -188,6 +188,7 @@ __device__ __forceinline__ void load_tile(Loader<ROWS>& L, const View& vw, const
     uint32_t kh = fdiv(rem, cv.kw_div);
     uint32_t kw = rem - kh * cv.kw_div.d;
     const int HW = cv.H * cv.W;
+    const uint32_t KW = cv.kw_div.d, KH = cv.khkw.d / (KW ? KW : 1u);
 #pragma unroll
     for (int i = 0; i < EPT; ++i) {
       const int khd = static_cast<int>(kh) * cv.dh, kwd = static_cast<int>(kw) * cv.dw;
@@ -195,18 +196,19 @@ __device__ __forceinline__ void load_tile(Loader<ROWS>& L, const View& vw, const
                       static_cast<unsigned>(col.hb + khd) < static_cast<unsigned>(cv.H) &&
                       static_cast<unsigned>(col.wb + kwd) < static_cast<unsigned>(cv.W);
       const int soff = static_cast<int>(c) * HW + khd * cv.W + kwd;  // wave-uniform
-      const uint32_t boff = ok ? static_cast<uint32_t>(col.pbase + soff) * 4u : 0xFFFFFFFFu;
+      // offset computed unconditionally and OR-ed with an all-ones mask when
+      // out of range: a select, never an exec-mask branch, so the loads stay
+      // in one basic block with the MFMAs they are interleaved with
+      const uint32_t boff = (static_cast<uint32_t>(col.pbase + soff) * 4u) | (ok ? 0u : 0xFFFFFFFFu);
       L.v[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(col.rsrc, boff, 0, 0));
-      // step (c, kh, kw) by one k
-      ++kw;
-      if (kw == cv.kw_div.d) {
-        kw = 0;
-        ++kh;
-        if (kh * cv.kw_div.d == cv.khkw.d) {
-          kh = 0;
-          ++c;
-        }
-      }
+      // step (c, kh, kw) by one k, branch-free (scalar selects)
+      kw += 1u;
+      const uint32_t cw = kw == KW;
+      kw = cw ? 0u : kw;
+      kh += cw;
+      const uint32_t ch = kh == KH;
+      kh = ch ? 0u : kh;
+      c += ch;
     }
     return;
   }
@@ -229,6 +231,12 @@ __device__ __forceinline__ void load_tile(Loader<ROWS>& L, const View& vw, const
     }
     L.v[i] = x;
   }
+}
+
+// global load instructions one thread issues per K-tile
+template <int MODE, int ROWS>
+constexpr int vmem_per_tile() {
+  return MODE == KCV ? Loader<ROWS>::EPT / 4 : Loader<ROWS>::EPT;
 }
 
 template <int MODE, int ROWS>
@@ -354,13 +362,13 @@ __global__ void __launch_bounds__(256) k_gemm(Params P) {
   for (int t = 0; t < ntiles; ++t) {
     const int cur = t & 1;
     const bool more = (t + 1) < ntiles;
-    if (more) {
+    {
+      // unconditional (no basic-block split): past the last tile every
+      // element is out of range and the guarded loads return zeros
       const int kn = kbeg + (t + 1) * BK;
       load_tile<AM, BMr>(la, va, P.cv, col, m0, kn, kend);
       load_tile<BMODE, BNr>(lb, vb, P.cv, col, n0, kn, kend);
     }
-    // keep the prefetch loads ahead of the MFMAs and the LDS writes behind them
-    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int q = 0; q < BK / 16; ++q) {
       float4 af[MI][2], bf[NI][2];
@@ -387,6 +395,19 @@ __global__ void __launch_bounds__(256) k_gemm(Params P) {
         }
       }
     }
+    // Interleave the next tile's global loads with the first MFMAs (a wave
+    // issues VALU / VMEM while its MFMAs run): one load, then NMF MFMAs.
+    {
+      constexpr int NVM = vmem_per_tile<AM, BMr>() + vmem_per_tile<BMODE, BNr>();
+      constexpr int NMF_TOT = MI * NI * BK / 2;
+      constexpr int NMF = NMF_TOT / (2 * NVM) > 0 ? NMF_TOT / (2 * NVM) : 1;
+#pragma unroll
+      for (int v = 0; v < NVM; ++v) {
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);    // VMEM read
+        __builtin_amdgcn_sched_group_barrier(0x008, NMF, 0);  // MFMA
+      }
+    }
+    // the LDS writes of the staged tile stay behind every MFMA
     __builtin_amdgcn_sched_barrier(0);
     if (more) {
       store_tile<AM, BMr>(la, As[cur ^ 1]);

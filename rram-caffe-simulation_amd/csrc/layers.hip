@@ -74,6 +74,46 @@ __global__ void k_pool_fwd(const float* __restrict__ x, float* __restrict__ y, i
   }
 }
 
+// MAX pooling with a compile-time window (AlexNet/CaffeNet/GoogLeNet 3x3, LeNet
+// 2x2): all K*K guarded loads are issued before the compares, same strict-">"
+// first-argmax rule and -FLT_MAX start as MaxPoolForward (pooling_layer.cu).
+template <int K>
+__global__ void __launch_bounds__(256) k_pool_max_fixed(const float* __restrict__ x, float* __restrict__ y,
+                                                        int* __restrict__ mask, int num, int C, int H, int W,
+                                                        int PH, int PW, int sh, int sw, int ph, int pw) {
+  const int total = num * C * PH * PW;
+  GRID_LOOP(idx, total) {
+    const int pwi = idx % PW;
+    const int phi = (idx / PW) % PH;
+    const int nc = idx / PW / PH;
+    const float* xs = x + (int64_t)nc * H * W;
+    const int hs = phi * sh - ph, ws = pwi * sw - pw;
+    float v[K * K];
+    bool ok[K * K];
+#pragma unroll
+    for (int a = 0; a < K; ++a)
+#pragma unroll
+      for (int b = 0; b < K; ++b) {
+        const int h = hs + a, w = ws + b;
+        ok[a * K + b] = static_cast<unsigned>(h) < static_cast<unsigned>(H) &&
+                        static_cast<unsigned>(w) < static_cast<unsigned>(W);
+        v[a * K + b] = ok[a * K + b] ? xs[h * W + w] : 0.0f;
+      }
+    float mv = -FLT_MAX;
+    int mi = -1;
+#pragma unroll
+    for (int a = 0; a < K; ++a)
+#pragma unroll
+      for (int b = 0; b < K; ++b)
+        if (ok[a * K + b] && v[a * K + b] > mv) {
+          mv = v[a * K + b];
+          mi = (hs + a) * W + (ws + b);
+        }
+    y[idx] = mv;
+    if (mask) mask[idx] = mi;
+  }
+}
+
 // pooling_layer.cu MaxPoolBackward / AvePoolBackward
 __global__ void k_pool_bwd(const float* __restrict__ dy, const int* __restrict__ mask,
                            float* __restrict__ dx, int num, int C, int H, int W, int PH, int PW,
@@ -142,32 +182,43 @@ __global__ void __launch_bounds__(256) k_lrn_fwd_slide(const float* __restrict__
                                                        float* __restrict__ scale, int num, int C, int HW,
                                                        float alpha_over_size, float beta, float k) {
   constexpr int PRE = (SIZE - 1) / 2, POST = SIZE - PRE - 1;
-  GRID_LOOP(idx, num * HW) {
-    const int s = idx % HW;
-    const int64_t base = (int64_t)(idx / HW) * C * HW + s;
-    const float* xc = x + base;
-    float* yc = y + base;
-    float win[SIZE];
+  constexpr int D = 8;  // channels prefetched per step: D independent loads in flight per thread
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // one (image, pixel) column per thread
+  if (idx >= num * HW) return;
+  const int s = idx % HW;
+  const int64_t base = (int64_t)(idx / HW) * C * HW + s;
+  const float* xc = x + base;
+  float* yc = y + base;
+  // ring of the SIZE channels centred on c, plus D channels read ahead
+  float win[SIZE + D];
 #pragma unroll
-    for (int j = 0; j < SIZE; ++j) {
-      const int cc = j - PRE;
-      win[j] = (cc >= 0 && cc < C) ? xc[(int64_t)cc * HW] : 0.0f;
+  for (int j = 0; j < SIZE; ++j) {
+    const int cc = j - PRE;
+    win[j] = (cc >= 0 && cc < C) ? xc[(int64_t)cc * HW] : 0.0f;
+  }
+  float acc = 0.0f;
+#pragma unroll
+  for (int j = PRE; j < SIZE; ++j) acc += win[j] * win[j];
+  for (int c0 = 0; c0 < C; c0 += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int cn = c0 + d + POST + 1;
+      win[SIZE + d] = cn < C ? xc[(int64_t)cn * HW] : 0.0f;
     }
-    float acc = 0.0f;
 #pragma unroll
-    for (int j = PRE; j < SIZE; ++j) acc += win[j] * win[j];
-    for (int c = 0; c < C; ++c) {
-      const float sc = k + acc * alpha_over_size;
-      if (scale) scale[base + (int64_t)c * HW] = sc;
-      yc[(int64_t)c * HW] = win[PRE] * pow_pos(sc, -beta);
-      const float out = win[0];
-#pragma unroll
-      for (int j = 0; j < SIZE - 1; ++j) win[j] = win[j + 1];
-      const int cn = c + POST + 1;
-      win[SIZE - 1] = cn < C ? xc[(int64_t)cn * HW] : 0.0f;
-      acc += win[SIZE - 1] * win[SIZE - 1];
-      acc -= out * out;
+    for (int d = 0; d < D; ++d) {
+      const int c = c0 + d;
+      if (c < C) {
+        // same add-then-subtract order as LRNFillScale (lrn_layer.cu:26-43)
+        const float sc = k + acc * alpha_over_size;
+        if (scale) scale[base + (int64_t)c * HW] = sc;
+        yc[(int64_t)c * HW] = win[d + PRE] * pow_pos(sc, -beta);
+        acc += win[d + SIZE] * win[d + SIZE];
+        acc -= win[d] * win[d];
+      }
     }
+#pragma unroll
+    for (int j = 0; j < SIZE; ++j) win[j] = win[j + D];
   }
 }
 
@@ -432,8 +483,15 @@ int rram_pool_fwd(const float* x, float* y, int* mask, int num, int C, int H, in
   RRAM_REQUIRE_I32(total, "layer kernel");
   if (total == 0) return RRAM_OK;
   RRAM_REQUIRE(x && y, "pool_fwd: NULL");
-  hipLaunchKernelGGL(k_pool_fwd, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), x, y,
-                     mask, num, C, H, W, PH, PW, kh, kw, sh, sw, ph, pw, method);
+  if (method == RRAM_POOL_MAX && kh == kw && kh == 3)
+    hipLaunchKernelGGL(k_pool_max_fixed<3>, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), x, y,
+                       mask, num, C, H, W, PH, PW, sh, sw, ph, pw);
+  else if (method == RRAM_POOL_MAX && kh == kw && kh == 2)
+    hipLaunchKernelGGL(k_pool_max_fixed<2>, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), x, y,
+                       mask, num, C, H, W, PH, PW, sh, sw, ph, pw);
+  else
+    hipLaunchKernelGGL(k_pool_fwd, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), x, y,
+                       mask, num, C, H, W, PH, PW, kh, kw, sh, sw, ph, pw, method);
   return launch_status("pool_fwd");
 }
 int rram_pool_bwd(const float* dy, const int* mask, float* dx, int num, int C, int H, int W, int PH,
@@ -460,10 +518,10 @@ int rram_lrn_fwd(const float* x, float* y, float* scale, int num, int C, int H, 
   RRAM_REQUIRE(x && y, "lrn_fwd: NULL");
   const int cols = num * H * W;
   if (size == 5)
-    hipLaunchKernelGGL(k_lrn_fwd_slide<5>, dim3(stream_blocks(cols)), dim3(kThreads), 0, as_stream(s), x, y,
+    hipLaunchKernelGGL(k_lrn_fwd_slide<5>, dim3((cols + kThreads - 1) / kThreads), dim3(kThreads), 0, as_stream(s), x, y,
                        scale, num, C, H * W, alpha / size, beta, k);
   else if (size == 3)
-    hipLaunchKernelGGL(k_lrn_fwd_slide<3>, dim3(stream_blocks(cols)), dim3(kThreads), 0, as_stream(s), x, y,
+    hipLaunchKernelGGL(k_lrn_fwd_slide<3>, dim3((cols + kThreads - 1) / kThreads), dim3(kThreads), 0, as_stream(s), x, y,
                        scale, num, C, H * W, alpha / size, beta, k);
   else
     hipLaunchKernelGGL(k_lrn_fwd, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), x, y,

@@ -61,6 +61,15 @@ struct U32x4 {
   uint32_t x, y, z, w;
 };
 
+// a ^ b ^ c; one v_bitop3_b32 (gfx950) on the device
+__host__ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+  return a ^ b ^ c;
+#endif
+}
+
 __host__ __device__ __forceinline__ U32x4 philox4x32_10(U32x4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
@@ -68,7 +77,7 @@ __host__ __device__ __forceinline__ U32x4 philox4x32_10(U32x4 c, uint32_t k0, ui
     const uint64_t p1 = static_cast<uint64_t>(0xCD9E8D57u) * c.z;
     const uint32_t hi0 = static_cast<uint32_t>(p0 >> 32), lo0 = static_cast<uint32_t>(p0);
     const uint32_t hi1 = static_cast<uint32_t>(p1 >> 32), lo1 = static_cast<uint32_t>(p1);
-    c = U32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    c = U32x4{xor3(hi1, c.y, k0), lo1, xor3(hi0, c.w, k1), lo0};
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
   }

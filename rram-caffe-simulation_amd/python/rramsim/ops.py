@@ -180,6 +180,48 @@ def lrn_bwd(x, y, scale, dy, dx, n, c, h, w, size, alpha, beta):
                                 beta, _stream()), "lrn_bwd")
 
 
+def lrn_within_fwd(x, y, scale, n, c, h, w, size, alpha, beta):
+    K.check(_lib().rram_lrn_within_fwd(_p(x), _p(y), _p(scale), n, c, h, w, size, alpha, beta,
+                                       _stream()), "lrn_within_fwd")
+
+
+def lrn_within_bwd(x, scale, dy, dx, n, c, h, w, size, alpha, beta):
+    K.check(_lib().rram_lrn_within_bwd(_p(x), _p(scale), _p(dy), _p(dx), n, c, h, w, size, alpha,
+                                       beta, _stream()), "lrn_within_bwd")
+
+
+def relu_fwd(x, y, slope=0.0):
+    K.check(_lib().rram_relu_fwd(_p(x), _p(y), x.numel(), slope, _stream()), "relu_fwd")
+
+
+def relu_bwd(x, dy, dx, slope=0.0):
+    K.check(_lib().rram_relu_bwd(_p(x), _p(dy), _p(dx), x.numel(), slope, _stream()), "relu_bwd")
+
+
+def softmax_loss_fwd(prob, label, loss, outer, channels, inner, ignore=-1):
+    K.check(_lib().rram_softmax_loss_fwd(_p(prob), _p(label), _p(loss), outer, channels, inner, ignore,
+                                         _stream()), "softmax_loss_fwd")
+
+
+def softmax_loss_bwd(prob, label, dx, outer, channels, inner, ignore=-1, loss_weight=1.0):
+    K.check(_lib().rram_softmax_loss_bwd(_p(prob), _p(label), _p(dx), outer, channels, inner, ignore,
+                                         loss_weight, _stream()), "softmax_loss_bwd")
+
+
+def concat_copy(src, dst, num, src_cxi, dst_cxi, off_xi, backward=False):
+    K.check(_lib().rram_concat_copy(_p(src), _p(dst), num, src_cxi, dst_cxi, off_xi, int(backward),
+                                    _stream()), "concat")
+
+
+def dropout_fwd(x, y, mask, ratio, seed, layer_id=0, it=0):
+    K.check(_lib().rram_dropout_fwd(_p(x), _p(y), _p(mask), x.numel(), ratio, seed, layer_id, it,
+                                    _stream()), "dropout_fwd")
+
+
+def dropout_bwd(dy, mask, dx, ratio):
+    K.check(_lib().rram_dropout_bwd(_p(dy), _p(mask), _p(dx), dy.numel(), ratio, _stream()), "dropout_bwd")
+
+
 def softmax_fwd(x, y, outer, channels, inner):
     K.check(_lib().rram_softmax_fwd(_p(x), _p(y), outer, channels, inner, _stream()), "softmax")
 

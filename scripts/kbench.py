@@ -25,6 +25,39 @@ def timeit(fn, iters=20, warm=3):
     return s.elapsed_time(e) / iters * 1e-3
 
 
+def micro(dev):
+    """Practical ceilings: pure fp32-MFMA chains, a 16-B copy of the injection's
+    bytes, and Philox4x32-10 calls/s without memory traffic (scripts/microbench.hip)."""
+    import ctypes as C
+    import subprocess
+    so = ROOT / "scripts" / "_build" / "libmicro.so"
+    src = ROOT / "scripts" / "microbench.hip"
+    if not so.exists() or so.stat().st_mtime < src.stat().st_mtime:
+        so.parent.mkdir(exist_ok=True)
+        subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-shared", "-fPIC",
+                               "-o", str(so), str(src)])
+    lib = C.CDLL(str(so))
+    st = lambda: C.c_void_p(torch.cuda.current_stream().cuda_stream)  # noqa: E731
+    out = {}
+    o = torch.zeros(16, device=dev)
+    blocks, iters = 256 * 8, 2000
+    t = timeit(lambda: lib.micro_mfma_f32(C.c_void_p(o.data_ptr()), blocks, iters, st()), iters=5, warm=2)
+    out["mfma_f32_peak_TFs"] = blocks * 4 * iters * 16 * 32 * 32 * 2 * 2 / t / 1e12
+    n = 58_631_144 // 4 * 4
+    x = torch.randn(n, device=dev)
+    y = torch.empty_like(x)
+    for nb in (2048, 8192, 32768):
+        t = timeit(lambda: lib.micro_copy_f32(C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()),
+                                              C.c_int64(n), nb, st()))
+        out[f"copy16B_{nb}blk_GBps"] = 8 * n / t / 1e9
+    u = torch.empty(256 * 8192, dtype=torch.int32, device=dev)
+    cpt = 64
+    t = timeit(lambda: lib.micro_philox(C.c_void_p(u.data_ptr()), 8192, C.c_int64(cpt), st()))
+    out["philox_Gcalls_per_s"] = 256 * 8192 * cpt / t / 1e9
+    out["philox_us_per_alexnet_map"] = 58_631_144 / 2 / (out["philox_Gcalls_per_s"] * 1e9) * 1e6
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="")
@@ -95,6 +128,8 @@ def main():
         Cm = torch.empty(M, N, device=dev)
         t = timeit(lambda: ops.gemm(0, 0, M, N, K, 1.0, A, Bm, 0.0, Cm), iters=5)
         res["sq4096_TFs"] = 2.0 * M * N * K / t / 1e12
+    if a.only in ("", "micro"):
+        res.update(micro(dev))
     for k, v in res.items():
         print(f"{k:>20s} {v:10.3f}")
 

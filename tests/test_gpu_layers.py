@@ -1,0 +1,201 @@
+"""Support-layer forward/backward kernels against plain PyTorch fp32 references
+(autograd for the backward passes).  These are the layers the config nets run
+around the conv/IP GEMMs: ReLU, pooling, LRN (both regions), softmax loss,
+dropout, concat.  Caffe-specific rules (ceil pooling output, AVE-pool divisor
+over the padded window, max-pool first-argmax) are in the references below."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(a, device):
+    import torch
+    return torch.as_tensor(np.ascontiguousarray(a, np.float32)).to(device)
+
+
+def test_relu_fwd_bwd(device):
+    import torch
+    from rramsim import ops
+    x = torch.randn(4097, device=device)
+    dy = torch.randn_like(x)
+    for slope in (0.0, 0.1):
+        y, dx = torch.empty_like(x), torch.empty_like(x)
+        ops.relu_fwd(x, y, slope)
+        ops.relu_bwd(x, dy, dx, slope)
+        assert torch.equal(y, torch.where(x > 0, x, x * slope))
+        assert torch.equal(dx, torch.where(x > 0, dy, dy * slope))
+
+
+def _caffe_pool_ref(x, k, s, p, method):
+    """pooling_layer.cpp:90-104 ceil rule; AVE divides by the window clipped to
+    [-pad, H+pad) (pooling_layer.cpp:196-222), MAX ignores the padding."""
+    import torch
+    import torch.nn.functional as F
+    N, C, H, W = x.shape
+    PH = -(-(H + 2 * p - k) // s) + 1
+    PW = -(-(W + 2 * p - k) // s) + 1
+    if p and (PH - 1) * s >= H + p:
+        PH -= 1
+    if p and (PW - 1) * s >= W + p:
+        PW -= 1
+    if method == "MAX":
+        xp = F.pad(x, (p, p + k, p, p + k), value=-float("inf"))
+    else:
+        xp = F.pad(x, (p, p + k, p, p + k), value=0.0)
+    rows = []
+    for a in range(PH):
+        cols = []
+        for b in range(PW):
+            win = xp[:, :, a * s:a * s + k, b * s:b * s + k]
+            if method == "MAX":
+                cols.append(win.amax(dim=(2, 3)))
+            else:
+                he, we = min(a * s - p + k, H + p), min(b * s - p + k, W + p)
+                size = (he - (a * s - p)) * (we - (b * s - p))
+                cols.append(win.sum(dim=(2, 3)) / size)
+        rows.append(torch.stack(cols, -1))
+    return torch.stack(rows, -2)
+
+
+@pytest.mark.parametrize("method,k,s,p", [("MAX", 3, 2, 0), ("MAX", 2, 2, 0), ("MAX", 3, 2, 1),
+                                          ("AVE", 3, 2, 1), ("AVE", 5, 3, 0), ("AVE", 3, 1, 1)])
+def test_pool_fwd_bwd_vs_autograd(device, method, k, s, p):
+    import torch
+    from rramsim import ops
+    torch.manual_seed(3)
+    x = torch.randn(2, 5, 13, 11, device=device).requires_grad_(True)
+    ref = _caffe_pool_ref(x, k, s, p, method)
+    dy = torch.randn_like(ref)
+    ref.backward(dy)
+    N, C, H, W = x.shape
+    geom = (N, C, H, W, ref.shape[2], ref.shape[3], k, k, s, s, p, p)
+    y = torch.empty_like(ref)
+    mask = torch.empty(ref.shape, dtype=torch.int32, device=device)
+    dx = torch.empty_like(x)
+    m = 0 if method == "MAX" else 1
+    ops.pool_fwd(x.detach(), y, mask, geom, m)
+    ops.pool_bwd(dy, mask, dx, geom, m)
+    torch.testing.assert_close(y, ref.detach(), rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(dx, x.grad, rtol=1e-5, atol=1e-6)
+
+
+def _lrn_across_ref(x, size, alpha, beta, k):
+    import torch.nn.functional as F
+    pre = (size - 1) // 2
+    sq = F.pad((x * x).unsqueeze(1), (0, 0, 0, 0, pre, size - 1 - pre)).squeeze(1)
+    s = sum(sq[:, i:i + x.shape[1]] for i in range(size))
+    return x * (k + alpha / size * s) ** (-beta)
+
+
+def _lrn_within_ref(x, size, alpha, beta):
+    import torch.nn.functional as F
+    pre = (size - 1) // 2
+    avg = F.avg_pool2d(x * x, size, 1, pre, count_include_pad=True)
+    return x * (1.0 + alpha * avg) ** (-beta)
+
+
+@pytest.mark.parametrize("size", [3, 5])
+def test_lrn_across_fwd_bwd_vs_autograd(device, size):
+    import torch
+    from rramsim import ops
+    torch.manual_seed(4)
+    x = (3 * torch.randn(3, 11, 7, 9, device=device)).requires_grad_(True)
+    alpha, beta, k = 1e-2, 0.75, 2.0
+    ref = _lrn_across_ref(x, size, alpha, beta, k)
+    dy = torch.randn_like(ref)
+    ref.backward(dy)
+    N, C, H, W = x.shape
+    y, sc, dx = torch.empty_like(ref), torch.empty_like(ref), torch.empty_like(ref)
+    ops.lrn_fwd(x.detach(), y, sc, N, C, H, W, size, alpha, beta, k)
+    ops.lrn_bwd(x.detach(), y, sc, dy, dx, N, C, H, W, size, alpha, beta)
+    torch.testing.assert_close(y, ref.detach(), rtol=2e-5, atol=1e-6)
+    torch.testing.assert_close(dx, x.grad, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("size", [3, 5])
+def test_lrn_within_fwd_bwd_vs_autograd(device, size):
+    """cifar10_full's norm1/norm2 (lrn_layer.cpp WithinChannelForward/Backward)."""
+    import torch
+    from rramsim import ops
+    torch.manual_seed(5)
+    x = (3 * torch.randn(2, 4, 9, 8, device=device)).requires_grad_(True)
+    alpha, beta = 5e-2, 0.75
+    ref = _lrn_within_ref(x, size, alpha, beta)
+    dy = torch.randn_like(ref)
+    ref.backward(dy)
+    N, C, H, W = x.shape
+    y, sc, dx = torch.empty_like(ref), torch.empty_like(ref), torch.empty_like(ref)
+    ops.lrn_within_fwd(x.detach(), y, sc, N, C, H, W, size, alpha, beta)
+    ops.lrn_within_bwd(x.detach(), sc, dy, dx, N, C, H, W, size, alpha, beta)
+    torch.testing.assert_close(y, ref.detach(), rtol=2e-5, atol=1e-6)
+    torch.testing.assert_close(dx, x.grad, rtol=1e-4, atol=1e-5)
+
+
+def test_lrn_within_matches_numpy_oracle(device, oracle_mod):
+    import torch
+    from rramsim import ops
+    rng = np.random.default_rng(9)
+    x = rng.standard_normal((2, 3, 8, 8)).astype(np.float32) * 2
+    ref = oracle_mod.lrn_within(x, 3, 5e-5 * 9, 0.75)
+    y = torch.empty(x.shape, device=device)
+    ops.lrn_within_fwd(_t(x, device), y, None, 2, 3, 8, 8, 3, 5e-5 * 9, 0.75)
+    np.testing.assert_allclose(y.cpu().numpy(), ref, rtol=2e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("inner", [1, 6])
+def test_softmax_loss_fwd_bwd_vs_autograd(device, inner):
+    import torch
+    import torch.nn.functional as F
+    from rramsim import ops
+    torch.manual_seed(6)
+    outer, C = 17, 10
+    logits = torch.randn(outer, C, inner, device=device).requires_grad_(True)
+    label = torch.randint(0, C, (outer, inner), device=device)
+    loss = F.cross_entropy(logits, label)
+    loss.backward()
+    prob = torch.empty(outer, C, inner, device=device)
+    ops.softmax_fwd(logits.detach(), prob, outer, C, inner)
+    out = torch.zeros(1, device=device)
+    dx = torch.empty_like(prob)
+    lf = label.float()
+    ops.softmax_loss_fwd(prob, lf, out, outer, C, inner)
+    ops.softmax_loss_bwd(prob, lf, dx, outer, C, inner)
+    torch.testing.assert_close(out[0], loss.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(dx, logits.grad, rtol=1e-5, atol=1e-7)
+
+
+def test_dropout_fwd_bwd(device):
+    import torch
+    from rramsim import ops
+    x = torch.randn(1 << 16, device=device)
+    dy = torch.randn_like(x)
+    y, dx = torch.empty_like(x), torch.empty_like(x)
+    mask = torch.empty(x.shape, dtype=torch.int32, device=device)
+    ops.dropout_fwd(x, y, mask, 0.5, seed=11, layer_id=3, it=2)
+    ops.dropout_bwd(dy, mask, dx, 0.5)
+    keep = mask.bool()
+    assert abs(keep.float().mean().item() - 0.5) < 0.01        # 64k draws, sd 0.002
+    assert torch.equal(y, torch.where(keep, x * 2.0, torch.zeros_like(x)))
+    assert torch.equal(dx, torch.where(keep, dy * 2.0, torch.zeros_like(x)))
+    y2 = torch.empty_like(x)
+    mask2 = torch.empty_like(mask)
+    ops.dropout_fwd(x, y2, mask2, 0.5, seed=11, layer_id=3, it=2)
+    assert torch.equal(mask, mask2)                             # counter-based: deterministic
+    ops.dropout_fwd(x, y2, mask2, 0.5, seed=11, layer_id=3, it=3)
+    assert not torch.equal(mask, mask2)                         # fresh mask per iteration
+
+
+def test_concat_fwd_bwd(device):
+    import torch
+    from rramsim import ops
+    a = torch.randn(3, 4, 5, device=device)
+    b = torch.randn(3, 6, 5, device=device)
+    dst = torch.empty(3, 10, 5, device=device)
+    ops.concat_copy(a, dst, 3, 4 * 5, 10 * 5, 0)
+    ops.concat_copy(b, dst, 3, 6 * 5, 10 * 5, 4 * 5)
+    assert torch.equal(dst, torch.cat([a, b], 1))
+    da, db = torch.empty_like(a), torch.empty_like(b)
+    ops.concat_copy(da, dst, 3, 4 * 5, 10 * 5, 0, backward=True)
+    ops.concat_copy(db, dst, 3, 6 * 5, 10 * 5, 4 * 5, backward=True)
+    assert torch.equal(da, a) and torch.equal(db, b)
