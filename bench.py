@@ -160,7 +160,7 @@ def main():
     mc.reset()
     net.layer_times(reset=True)
     mc.inject_times(reset=True)
-    net.set_timing(True)
+    net.set_timing(1 if args.profile_layers else 2)   # events only around conv / IP unless profiling
     mc.set_timing(True)
 
     stats = torch.zeros(8, dtype=torch.float64, device=dev)

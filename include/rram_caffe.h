@@ -75,8 +75,10 @@ int rram_net_share_trained(rram_net_t dst, rram_net_t src);
 int rram_net_flat_param_count(rram_net_t net, int64_t* n);
 int rram_net_alias_flat_params(rram_net_t net, float* data, float* diff);
 /* Per-layer forward timing (`caffe time`, tools/caffe.cpp:334-421): hipEvents
- * around every layer on the working stream.  layer_times synchronises and
- * returns total ms and launch count per layer since the last reset. */
+ * around every layer (enable = 1) or only around layers that own parameters,
+ * i.e. Convolution / InnerProduct (enable = 2), on the working stream.
+ * layer_times synchronises and returns total ms and launch count per layer
+ * since the last reset. */
 int rram_net_set_timing(rram_net_t net, int enable);
 int rram_net_layer_times(rram_net_t net, double* ms, long* counts, int cap, int* n, int reset);
 /* Host-only structural view (no device): phase filter + split insertion;

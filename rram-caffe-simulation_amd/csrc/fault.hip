@@ -4,6 +4,7 @@
 // 16-byte (float4) loads and stores per lane where the pointers allow it,
 // 256-thread blocks, grid-stride, wave-level ballot reductions for counters.
 #include <math.h>
+#include <stdlib.h>
 
 #include "rram_common.hpp"
 
@@ -713,7 +714,14 @@ int rram_inject_rng_batched(const rram_inject_seg* segs, int nsegs, uint64_t see
   }
   const int64_t total = is.chunk_start[nsegs];
   if (total == 0) return RRAM_OK;
-  const int grid = static_cast<int>(total < kMaxStreamBlocks ? total : kMaxStreamBlocks);
+  // blocks striding over 4096-weight chunks; RRAM_INJECT_GRID (tuning knob)
+  // overrides the default cap
+  static const int64_t grid_cap = [] {
+    const char* e = getenv("RRAM_INJECT_GRID");
+    const long v = e ? atol(e) : 0;
+    return v > 0 ? static_cast<int64_t>(v) : static_cast<int64_t>(kMaxStreamBlocks);
+  }();
+  const int grid = static_cast<int>(total < grid_cap ? total : grid_cap);
   bool fast = true;
   for (int i = 0; i < nsegs; ++i) fast = fast && is.s[i].mode == 0;
   if (fast)

@@ -393,48 +393,46 @@ __global__ void k_count_valid(const float* __restrict__ label, int64_t n, int ig
 
 // accuracy_layer.cpp:48-90: label counted correct when its (value, index)
 // pair is within the top_k of the descending pair order.  One wave per
-// sample (lanes over classes); single block, deterministic integer sums.
-__global__ void __launch_bounds__(1024) k_accuracy(const float* __restrict__ x,
-                                                   const float* __restrict__ label, float* correct,
-                                                   float* count, float* ratio, int outer, int C,
-                                                   int inner, int top_k, int ignore) {
-  __shared__ float sa[16], sc[16];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  float acc = 0.0f, cnt = 0.0f;
+// (outer, inner) column (lanes over classes), many blocks; the per-block
+// counts are integers, so float atomics on them are exact and order-independent.
+__global__ void __launch_bounds__(256) k_accuracy(const float* __restrict__ x, const float* __restrict__ label,
+                                                  float* correct, float* count, int outer, int C, int inner,
+                                                  int top_k, int ignore) {
+  __shared__ int sa[4], sc[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t cols = (int64_t)outer * inner;
-  for (int64_t col = wave; col < cols; col += nw) {
+  const int64_t col = (int64_t)blockIdx.x * 4 + wave;
+  int hit = 0, cnt = 0;
+  if (col < cols) {
     const int64_t o = col / inner, q = col - o * inner;
     const int lv = static_cast<int>(label[col]);
-    if (ignore >= 0 && lv == ignore) continue;
-    const float* xs = x + o * C * inner + q;
-    const float v = xs[(int64_t)lv * inner];
-    int rank = 0;
-    for (int c = lane; c < C; c += 64) {
-      const float u = xs[(int64_t)c * inner];
-      rank += (u > v) || (u == v && c > lv);
-    }
+    if (!(ignore >= 0 && lv == ignore)) {
+      const float* xs = x + o * C * inner + q;
+      const float v = xs[(int64_t)lv * inner];
+      int rank = 0;  // #classes ahead of the label in Caffe's (value, index) descending order
+      for (int c = lane; c < C; c += 64) {
+        const float u = xs[(int64_t)c * inner];
+        rank += (u > v) || (u == v && c > lv);
+      }
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) rank += __shfl_xor(rank, off, 64);
-    if (lane == 0) {
-      acc += rank < top_k ? 1.0f : 0.0f;
-      cnt += 1.0f;
+      for (int off = 32; off > 0; off >>= 1) rank += __shfl_xor(rank, off, 64);
+      hit = rank < top_k;
+      cnt = 1;
     }
   }
   if (lane == 0) {
-    sa[wave] = acc;
+    sa[wave] = hit;
     sc[wave] = cnt;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    float A = 0.0f, N = 0.0f;
-    for (int i = 0; i < nw; ++i) {
-      A += sa[i];
-      N += sc[i];
-    }
-    correct[0] = A;
-    count[0] = N;
-    if (ratio) ratio[0] = A / fmaxf(N, 1.0f);
+    const int A = sa[0] + sa[1] + sa[2] + sa[3], N = sc[0] + sc[1] + sc[2] + sc[3];
+    if (A) atomicAdd(correct, static_cast<float>(A));
+    if (N) atomicAdd(count, static_cast<float>(N));
   }
+}
+__global__ void k_accuracy_ratio(const float* correct, const float* count, float* ratio) {
+  ratio[0] = correct[0] / fmaxf(count[0], 1.0f);
 }
 
 // concat_layer.cu Concat kernel (axis 1)
@@ -614,8 +612,14 @@ int rram_accuracy(const float* x, const float* label, float* correct, float* cou
   RRAM_REQUIRE(outer >= 0 && C > 0 && inner > 0 && top_k >= 1 && correct && count,
                "accuracy: bad args");
   RRAM_REQUIRE(outer == 0 || (x && label), "accuracy: NULL");
-  hipLaunchKernelGGL(k_accuracy, dim3(1), dim3(1024), 0, as_stream(s), x, label, correct, count,
-                     ratio, outer, C, inner, top_k, ignore);
+  const int64_t cols = (int64_t)outer * inner;
+  RRAM_REQUIRE(cols < (1ll << 24), "accuracy: more than 2^24 samples (float counts would round)");
+  RRAM_HIP_RET(hipMemsetAsync(correct, 0, sizeof(float), as_stream(s)));
+  RRAM_HIP_RET(hipMemsetAsync(count, 0, sizeof(float), as_stream(s)));
+  if (cols > 0)
+    hipLaunchKernelGGL(k_accuracy, dim3(static_cast<unsigned>((cols + 3) / 4)), dim3(256), 0, as_stream(s), x,
+                       label, correct, count, outer, C, inner, top_k, ignore);
+  if (ratio) hipLaunchKernelGGL(k_accuracy_ratio, dim3(1), dim3(1), 0, as_stream(s), correct, count, ratio);
   return launch_status("accuracy");
 }
 

@@ -235,7 +235,7 @@ int rram_net_alias_flat_params(rram_net_t n, float* data, float* diff) {
 int rram_net_set_timing(rram_net_t n, int enable) {
   return guarded([&] {
     NEED(n);
-    n->net->set_timing(enable != 0);
+    n->net->set_timing(enable == 2 ? 2 : (enable != 0 ? 1 : 0));
   });
 }
 int rram_net_layer_times(rram_net_t n, double* ms, long* counts, int cap, int* k, int reset) {

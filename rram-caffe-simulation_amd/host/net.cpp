@@ -297,9 +297,10 @@ std::string DescribeNet(const Msg& in_param, Phase phase) {
 template <typename Dtype>
 Dtype Net<Dtype>::ForwardFromTo(int start, int end, bool compute_loss) {
   for (int i = start; i <= end; ++i) {
-    if (timing_) timer_.start(i);
+    const bool timed = timing_ == 1 || (timing_ == 2 && !layers_[i]->blobs().empty());
+    if (timed) timer_.start(i);
     layers_[i]->Forward(bottom_vecs_[i], top_vecs_[i]);
-    if (timing_) timer_.stop(i);
+    if (timed) timer_.stop(i);
   }
   if (!compute_loss) return Dtype(0);
   // loss = sum over loss tops of weight * value (layer.hpp:451-487); one D2H per loss top

@@ -65,12 +65,13 @@ class Net {
     for (auto& l : layers_) l->iter = it;
   }
 
-  // per-layer forward timing with hipEvents (`caffe time`, tools/caffe.cpp:334-421)
-  void set_timing(bool on) { timing_ = on; }
+  // per-layer forward timing with hipEvents (`caffe time`, tools/caffe.cpp:334-421):
+  // 0 off, 1 every layer, 2 only layers that own parameters (conv / IP)
+  void set_timing(int mode) { timing_ = mode; }
   EventTimer& timer() { return timer_; }
 
  private:
-  bool timing_ = false;
+  int timing_ = 0;
   EventTimer timer_;
   void AppendParam(int layer_id, int param_id, const Msg& layer_param);
 

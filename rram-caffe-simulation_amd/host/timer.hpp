@@ -16,9 +16,7 @@ class EventTimer {
  public:
   ~EventTimer() { clear(); }
   void start(int key) {
-    hipEvent_t a, b;
-    HIP_CALL(hipEventCreate(&a));
-    HIP_CALL(hipEventCreate(&b));
+    hipEvent_t a = take(), b = take();
     HIP_CALL(hipEventRecord(a, Caffe::hip_stream()));
     open_[key] = pending_.size();
     pending_.push_back({key, {a, b}});
@@ -37,16 +35,18 @@ class EventTimer {
       HIP_CALL(hipEventElapsedTime(&ms, p.second.first, p.second.second));
       totals_[p.first] += ms;
       counts_[p.first] += 1;
-      (void)hipEventDestroy(p.second.first);
-      (void)hipEventDestroy(p.second.second);
+      free_.push_back(p.second.first);
+      free_.push_back(p.second.second);
     }
     pending_.clear();
   }
   void clear() {
     for (auto& p : pending_) {
-      (void)hipEventDestroy(p.second.first);
-      (void)hipEventDestroy(p.second.second);
+      free_.push_back(p.second.first);
+      free_.push_back(p.second.second);
     }
+    for (hipEvent_t e : free_) (void)hipEventDestroy(e);
+    free_.clear();
     pending_.clear();
     open_.clear();
     totals_.clear();
@@ -56,6 +56,19 @@ class EventTimer {
   const std::map<int, long>& counts() const { return counts_; }
 
  private:
+  // events are pooled (no create/destroy per interval) and skip the
+  // system-scope release fence: they only order work on this device
+  hipEvent_t take() {
+    if (!free_.empty()) {
+      hipEvent_t e = free_.back();
+      free_.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    HIP_CALL(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+    return e;
+  }
+  std::vector<hipEvent_t> free_;
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending_;
   std::map<int, size_t> open_;
   std::map<int, double> totals_;

@@ -255,8 +255,9 @@ class Net:
             out[name.value.decode()] = _wrap_device(d.value, (cnt.value,))
         return out
 
-    def set_timing(self, on: bool):
-        check(self._lib.rram_net_set_timing(self.h, int(on)), "set_timing")
+    def set_timing(self, mode):
+        """False/0 off, True/1 every layer, 2 only parameter layers (conv / IP)."""
+        check(self._lib.rram_net_set_timing(self.h, int(mode)), "set_timing")
 
     def layer_times(self, reset=False):
         """[(layer name, type, total ms, launches)] since the last reset."""
