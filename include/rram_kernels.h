@@ -313,6 +313,18 @@ int rram_lrn_within_bwd(const float* x, const float* scale, const float* dy, flo
                         int channels, int height, int width, int size, float alpha, float beta,
                         rram_stream_t s);
 
+/* Inference fusion (TEST phase) of LRN ACROSS_CHANNELS followed by MAX
+ * pooling whose bottom is the LRN top and nothing else reads it:
+ * y = maxpool(lrn(x)) without materialising lrn(x).  Every LRN value is
+ * rram_lrn_fwd's bit for bit; window rule as rram_pool_fwd.  kernel in {2,3}
+ * (square), size in {3,5}, pad < kernel.  Replaces LRNLayer::Forward_gpu +
+ * PoolingLayer::Forward_gpu (src/caffe/layers/lrn_layer.cu:9-99,
+ * src/caffe/layers/pooling_layer.cu:11-47,158-178) for that layer pair. */
+int rram_lrn_maxpool_fwd(const float* x, float* y, int num, int channels, int height, int width,
+                         int pooled_h, int pooled_w, int kernel, int stride_h, int stride_w,
+                         int pad_h, int pad_w, int size, float alpha, float beta, float k,
+                         rram_stream_t s);
+
 /* Softmax over `channels` for [outer][channels][inner]. */
 int rram_softmax_fwd(const float* x, float* y, int outer, int channels, int inner, rram_stream_t s);
 /* SoftmaxWithLoss forward: loss_out[0] = -sum log(max(p[label], FLT_MIN)) / normalizer

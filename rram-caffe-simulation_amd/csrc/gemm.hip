@@ -16,6 +16,8 @@
 // fragments with 16-byte LDS reads; A and B use the same permutation, so the
 // contraction is unchanged.  Blocks are remapped so that each XCD (own L2)
 // receives a contiguous run of tiles that share operand panels.
+#include <stdlib.h>
+
 #include "rram_common.hpp"
 
 namespace rram {
@@ -23,8 +25,12 @@ namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
+// K-tile depth is a template parameter KB (16 or 32); LDS rows are padded to
+// KB + 4 floats (80 / 144 B: 16-B aligned, conflict-free ds_read_b128 for 16
+// consecutive rows).  BK is the split-K chunk granularity (multiple of both).
 constexpr int BK = 32;
-constexpr int LDK = BK + 4;  // padded LDS row (floats): 144 B, 16-B aligned, conflict-free b128 reads
+template <int KB>
+constexpr int ldk_of() { return KB + 4; }
 
 // KCV = KC with 16-byte global loads (row stride, base and K all multiples of 4 floats)
 enum Mode : int { KC = 0, RC = 1, CONV = 2, NCHW = 3, NCHWT = 4, KCV = 5 };
@@ -102,9 +108,9 @@ struct ConvCol {
   __amdgpu_buffer_rsrc_t rsrc;  // raw buffer over the group's input (OOB loads return 0)
 };
 
-template <int ROWS>
+template <int ROWS, int KB>
 struct Loader {
-  static constexpr int EPT = ROWS * BK / 256;
+  static constexpr int EPT = ROWS * KB / 256;
   float v[EPT];
 };
 
@@ -143,29 +149,29 @@ __device__ __forceinline__ float ld_nchwt(const View& vw, int row, int k, bool k
 
 // Element e of a ROWS x BK tile -> (row, k) for a scalar view mode.  KC / NCHW
 // are k-fastest (memory is contiguous along k); the others are row-fastest.
-template <int MODE, int ROWS>
+template <int MODE, int ROWS, int KB>
 __device__ __forceinline__ void tile_coord(int e, int& row, int& k) {
   if (MODE == KC || MODE == NCHW) {
-    row = e / BK;
-    k = e % BK;
+    row = e / KB;
+    k = e % KB;
   } else {
     row = e % ROWS;
     k = e / ROWS;
   }
 }
 
-template <int MODE, int ROWS>
-__device__ __forceinline__ void load_tile(Loader<ROWS>& L, const View& vw, const ConvGeom& cv,
+template <int MODE, int ROWS, int KB>
+__device__ __forceinline__ void load_tile(Loader<ROWS, KB>& L, const View& vw, const ConvGeom& cv,
                                           const ConvCol& col, int row0, int k0, int kend) {
-  constexpr int EPT = Loader<ROWS>::EPT;
+  constexpr int EPT = Loader<ROWS, KB>::EPT;
   if (MODE == KCV) {
-    // 16-byte loads: float4 q -> (row = q / (BK/4), k4 = q % (BK/4)); K-range
+    // 16-byte loads: float4 q -> (row = q / (KB/4), k4 = q % (KB/4)); K-range
     // ends are multiples of 4 so a float4 is entirely in or out of range
 #pragma unroll
     for (int i = 0; i < EPT / 4; ++i) {
       const int q = threadIdx.x + i * 256;
-      const int r = q / (BK / 4);
-      const int k = k0 + 4 * (q % (BK / 4));
+      const int r = q / (KB / 4);
+      const int k = k0 + 4 * (q % (KB / 4));
       const bool ok = row0 + r < vw.rows && k < kend;
       const float4 x = *reinterpret_cast<const float4*>(ok ? vw.p + (int64_t)(row0 + r) * vw.ld + k : g_zero4);
       L.v[4 * i] = x.x;
@@ -216,7 +222,7 @@ __device__ __forceinline__ void load_tile(Loader<ROWS>& L, const View& vw, const
   for (int i = 0; i < EPT; ++i) {
     const int e = threadIdx.x + i * 256;
     int r, kk;
-    tile_coord<MODE, ROWS>(e, r, kk);
+    tile_coord<MODE, ROWS, KB>(e, r, kk);
     const int row = row0 + r;
     const int k = k0 + kk;
     float x;
@@ -234,14 +240,15 @@ __device__ __forceinline__ void load_tile(Loader<ROWS>& L, const View& vw, const
 }
 
 // global load instructions one thread issues per K-tile
-template <int MODE, int ROWS>
+template <int MODE, int ROWS, int KB>
 constexpr int vmem_per_tile() {
-  return MODE == KCV ? Loader<ROWS>::EPT / 4 : Loader<ROWS>::EPT;
+  return MODE == KCV ? Loader<ROWS, KB>::EPT / 4 : Loader<ROWS, KB>::EPT;
 }
 
-template <int MODE, int ROWS>
-__device__ __forceinline__ void store_tile(const Loader<ROWS>& L, float* lds) {
-  constexpr int EPT = Loader<ROWS>::EPT;
+template <int MODE, int ROWS, int KB>
+__device__ __forceinline__ void store_tile(const Loader<ROWS, KB>& L, float* lds) {
+  constexpr int EPT = Loader<ROWS, KB>::EPT;
+  constexpr int LDK = ldk_of<KB>();
   if (MODE == CONV) {
     // EPT consecutive k of one row: 16-byte LDS writes (row stride 36 dwords
     // puts the 8 lanes of a ds_write_b128 group on distinct bank quads)
@@ -255,7 +262,7 @@ __device__ __forceinline__ void store_tile(const Loader<ROWS>& L, float* lds) {
 #pragma unroll
     for (int i = 0; i < EPT / 4; ++i) {
       const int q = threadIdx.x + i * 256;
-      *reinterpret_cast<float4*>(lds + (q / (BK / 4)) * LDK + 4 * (q % (BK / 4))) =
+      *reinterpret_cast<float4*>(lds + (q / (KB / 4)) * LDK + 4 * (q % (KB / 4))) =
           make_float4(L.v[4 * i], L.v[4 * i + 1], L.v[4 * i + 2], L.v[4 * i + 3]);
     }
     return;
@@ -264,7 +271,7 @@ __device__ __forceinline__ void store_tile(const Loader<ROWS>& L, float* lds) {
   for (int i = 0; i < EPT; ++i) {
     const int e = threadIdx.x + i * 256;
     int r, kk;
-    tile_coord<MODE, ROWS>(e, r, kk);
+    tile_coord<MODE, ROWS, KB>(e, r, kk);
     lds[r * LDK + kk] = L.v[i];
   }
 }
@@ -273,12 +280,14 @@ __device__ __forceinline__ float pick(const float4& q, int s) {
   return (s & 3) == 0 ? q.x : (s & 3) == 1 ? q.y : (s & 3) == 2 ? q.z : q.w;
 }
 
-template <int WM, int WN, int MI, int NI, int AM, int BMODE, int OM>
+template <int WM, int WN, int MI, int NI, int AM, int BMODE, int OM, int KB>
 __global__ void __launch_bounds__(256) k_gemm(Params P) {
   constexpr int BMr = WM * MI * 32;
   constexpr int BNr = WN * NI * 32;
+  constexpr int LDK = ldk_of<KB>();
   static_assert(WM * WN == 4, "4 waves per block");
-  static_assert(BMr * BK % 1024 == 0 && BNr * BK % 1024 == 0, "tile/threads");
+  static_assert(KB == 16 || KB == 32, "K-tile depth");
+  static_assert(BMr * KB % 1024 == 0 && BNr * KB % 1024 == 0, "tile/threads");
   __shared__ __attribute__((aligned(16))) float As[2][BMr * LDK];
   __shared__ __attribute__((aligned(16))) float Bs[2][BNr * LDK];
 
@@ -321,7 +330,7 @@ __global__ void __launch_bounds__(256) k_gemm(Params P) {
   ConvCol col{0, 0, 0, false};
   if (BMODE == CONV) {
     int r, kk;
-    tile_coord<CONV, BNr>(threadIdx.x, r, kk);
+    tile_coord<CONV, BNr, KB>(threadIdx.x, r, kk);
     const int p = n0 + r;
     if (p < P.N) {
       const uint32_t im = fdiv(static_cast<uint32_t>(p), P.cv.howo);
@@ -346,14 +355,14 @@ __global__ void __launch_bounds__(256) k_gemm(Params P) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
-  Loader<BMr> la;
-  Loader<BNr> lb;
-  const int ntiles = (kend - kbeg + BK - 1) / BK;
+  Loader<BMr, KB> la;
+  Loader<BNr, KB> lb;
+  const int ntiles = (kend - kbeg + KB - 1) / KB;
   if (ntiles > 0) {
-    load_tile<AM, BMr>(la, va, P.cv, col, m0, kbeg, kend);
-    load_tile<BMODE, BNr>(lb, vb, P.cv, col, n0, kbeg, kend);
-    store_tile<AM, BMr>(la, As[0]);
-    store_tile<BMODE, BNr>(lb, Bs[0]);
+    load_tile<AM, BMr, KB>(la, va, P.cv, col, m0, kbeg, kend);
+    load_tile<BMODE, BNr, KB>(lb, vb, P.cv, col, n0, kbeg, kend);
+    store_tile<AM, BMr, KB>(la, As[0]);
+    store_tile<BMODE, BNr, KB>(lb, Bs[0]);
   }
   __syncthreads();
 
@@ -365,12 +374,12 @@ __global__ void __launch_bounds__(256) k_gemm(Params P) {
     {
       // unconditional (no basic-block split): past the last tile every
       // element is out of range and the guarded loads return zeros
-      const int kn = kbeg + (t + 1) * BK;
-      load_tile<AM, BMr>(la, va, P.cv, col, m0, kn, kend);
-      load_tile<BMODE, BNr>(lb, vb, P.cv, col, n0, kn, kend);
+      const int kn = kbeg + (t + 1) * KB;
+      load_tile<AM, BMr, KB>(la, va, P.cv, col, m0, kn, kend);
+      load_tile<BMODE, BNr, KB>(lb, vb, P.cv, col, n0, kn, kend);
     }
 #pragma unroll
-    for (int q = 0; q < BK / 16; ++q) {
+    for (int q = 0; q < KB / 16; ++q) {
       float4 af[MI][2], bf[NI][2];
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
@@ -398,8 +407,8 @@ __global__ void __launch_bounds__(256) k_gemm(Params P) {
     // Interleave the next tile's global loads with the first MFMAs (a wave
     // issues VALU / VMEM while its MFMAs run): one load, then NMF MFMAs.
     {
-      constexpr int NVM = vmem_per_tile<AM, BMr>() + vmem_per_tile<BMODE, BNr>();
-      constexpr int NMF_TOT = MI * NI * BK / 2;
+      constexpr int NVM = vmem_per_tile<AM, BMr, KB>() + vmem_per_tile<BMODE, BNr, KB>();
+      constexpr int NMF_TOT = MI * NI * KB / 2;
       constexpr int NMF = NMF_TOT / (2 * NVM) > 0 ? NMF_TOT / (2 * NVM) : 1;
 #pragma unroll
       for (int v = 0; v < NVM; ++v) {
@@ -410,8 +419,8 @@ __global__ void __launch_bounds__(256) k_gemm(Params P) {
     // the LDS writes of the staged tile stay behind every MFMA
     __builtin_amdgcn_sched_barrier(0);
     if (more) {
-      store_tile<AM, BMr>(la, As[cur ^ 1]);
-      store_tile<BMODE, BNr>(lb, Bs[cur ^ 1]);
+      store_tile<AM, BMr, KB>(la, As[cur ^ 1]);
+      store_tile<BMODE, BNr, KB>(lb, Bs[cur ^ 1]);
     }
     __syncthreads();
   }
@@ -555,7 +564,7 @@ __global__ void __launch_bounds__(256)
 }
 
 
-template <int WM, int WN, int MI, int NI, int AM, int BMODE, int OM>
+template <int WM, int WN, int MI, int NI, int AM, int BMODE, int OM, int KB>
 int launch_cfg(Params P, int gz, hipStream_t s) {
   constexpr int BMr = WM * MI * 32, BNr = WN * NI * 32;
   P.tiles_m = (P.M + BMr - 1) / BMr;
@@ -563,7 +572,7 @@ int launch_cfg(Params P, int gz, hipStream_t s) {
   P.tiles_z = gz;
   const int64_t nwg = (int64_t)P.tiles_m * P.tiles_n * gz;
   RRAM_REQUIRE(nwg < (1ll << 31), "gemm: grid too large");
-  hipLaunchKernelGGL((k_gemm<WM, WN, MI, NI, AM, BMODE, OM>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, P);
+  hipLaunchKernelGGL((k_gemm<WM, WN, MI, NI, AM, BMODE, OM, KB>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, P);
   return launch_status("gemm");
 }
 
@@ -571,9 +580,9 @@ int launch_cfg(Params P, int gz, hipStream_t s) {
 // padded rows of M (AlexNet: conv1 M = 96, conv4 M = 192 per group) as long as
 // the grid keeps >= 2 blocks per CU; 64x64 when even that grid is too small.
 // force_big: split-K grids (128x128).
-template <int AM, int BMODE, int OM>
+template <int AM, int BMODE, int OM, int KB>
 int launch(const Params& P, int gz, hipStream_t s, bool force_big) {
-  if (force_big) return launch_cfg<2, 2, 2, 2, AM, BMODE, OM>(P, gz, s);
+  if (force_big) return launch_cfg<2, 2, 2, 2, AM, BMODE, OM, KB>(P, gz, s);
   const int64_t ntn = (P.N + 127) / 128;
   const int cands[4] = {128, 192, 96, 64};  // ties keep 128 (2 blocks per CU)
   int best = 0;
@@ -588,18 +597,33 @@ int launch(const Params& P, int gz, hipStream_t s, bool force_big) {
     }
   }
   if (best == 64 && ntn * ((P.M + 63) / 64) * gz < 256)
-    return launch_cfg<2, 2, 1, 1, AM, BMODE, OM>(P, gz, s);  // 64 x 64: twice the blocks
+    return launch_cfg<2, 2, 1, 1, AM, BMODE, OM, KB>(P, gz, s);  // 64 x 64: twice the blocks
   switch (best) {
-    case 192: return launch_cfg<2, 2, 3, 2, AM, BMODE, OM>(P, gz, s);  // 192 x 128
-    case 128: return launch_cfg<2, 2, 2, 2, AM, BMODE, OM>(P, gz, s);  // 128 x 128
-    case 96: return launch_cfg<1, 4, 3, 1, AM, BMODE, OM>(P, gz, s);   //  96 x 128
-    default: return launch_cfg<1, 4, 2, 1, AM, BMODE, OM>(P, gz, s);   //  64 x 128
+    case 192: return launch_cfg<2, 2, 3, 2, AM, BMODE, OM, KB>(P, gz, s);  // 192 x 128
+    case 128: return launch_cfg<2, 2, 2, 2, AM, BMODE, OM, KB>(P, gz, s);  // 128 x 128
+    case 96:
+      if constexpr (KB == 16) return launch_cfg<2, 2, 2, 2, AM, BMODE, OM, KB>(P, gz, s);  // 96 x 16 splits float4s
+      else return launch_cfg<1, 4, 3, 1, AM, BMODE, OM, KB>(P, gz, s);   //  96 x 128
+    default: return launch_cfg<1, 4, 2, 1, AM, BMODE, OM, KB>(P, gz, s);   //  64 x 128
   }
 }
 
+// K-tile depth of the implicit-GEMM convolution (tuning knob RRAM_GEMM_KB = 16 | 32)
+int conv_kb() {
+  static const int kb = [] {
+    const char* e = getenv("RRAM_GEMM_KB");
+    return (e && atoi(e) == 16) ? 16 : 32;
+  }();
+  return kb;
+}
+
 int dispatch(int am, int bm, int om, const Params& P, int gz, hipStream_t s, bool force_big = false) {
+  if (bm == CONV && om == OUT_NCHW && conv_kb() == 16) {
+    if (am == KC) return launch<KC, CONV, OUT_NCHW, 16>(P, gz, s, force_big);
+    if (am == KCV) return launch<KCV, CONV, OUT_NCHW, 16>(P, gz, s, force_big);
+  }
 #define RRAM_D(A_, B_, O_) \
-  if (am == A_ && bm == B_ && om == O_) return launch<A_, B_, O_>(P, gz, s, force_big);
+  if (am == A_ && bm == B_ && om == O_) return launch<A_, B_, O_, 32>(P, gz, s, force_big);
   RRAM_D(KC, KC, OUT_ROWMAJOR)
   RRAM_D(KCV, KC, OUT_ROWMAJOR)
   RRAM_D(KC, KCV, OUT_ROWMAJOR)

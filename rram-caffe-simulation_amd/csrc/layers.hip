@@ -198,7 +198,7 @@ __global__ void __launch_bounds__(256) k_lrn_fwd_slide(const float* __restrict__
   }
   float acc = 0.0f;
 #pragma unroll
-  for (int j = PRE; j < SIZE; ++j) acc += win[j] * win[j];
+  for (int j = PRE; j < SIZE; ++j) acc = lrn_sq_add(acc, win[j]);
   for (int c0 = 0; c0 < C; c0 += D) {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
@@ -210,11 +210,10 @@ __global__ void __launch_bounds__(256) k_lrn_fwd_slide(const float* __restrict__
       const int c = c0 + d;
       if (c < C) {
         // same add-then-subtract order as LRNFillScale (lrn_layer.cu:26-43)
-        const float sc = k + acc * alpha_over_size;
+        const float sc = lrn_scale(acc, alpha_over_size, k);
         if (scale) scale[base + (int64_t)c * HW] = sc;
-        yc[(int64_t)c * HW] = win[d + PRE] * pow_pos(sc, -beta);
-        acc += win[d + SIZE] * win[d + SIZE];
-        acc -= win[d] * win[d];
+        yc[(int64_t)c * HW] = lrn_out(win[d + PRE], sc, beta);
+        acc = lrn_slide(acc, win[d + SIZE], win[d]);
       }
     }
 #pragma unroll

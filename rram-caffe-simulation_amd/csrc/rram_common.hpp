@@ -101,6 +101,21 @@ __host__ __device__ __forceinline__ U32x4 draw(uint64_t seed, uint64_t index, ui
   return philox4x32_10(c, static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32));
 }
 
+// LRN ACROSS_CHANNELS arithmetic (lrn_layer.cu:9-78), shared by the unfused
+// kernel (layers.hip) and the LRN+pool fusion (fused.hip) so both produce the
+// same bits: explicit fmaf leaves nothing to the compiler's contraction choice.
+__device__ __forceinline__ float lrn_sq_add(float acc, float v) { return fmaf(v, v, acc); }
+__device__ __forceinline__ float lrn_slide(float acc, float add, float sub) {
+  return fmaf(-sub, sub, fmaf(add, add, acc));  // add the entering channel, then drop the leaving one
+}
+__device__ __forceinline__ float lrn_scale(float acc, float alpha_over_size, float k) {
+  return fmaf(acc, alpha_over_size, k);
+}
+// x * scale^-beta via v_log_f32 / v_exp_f32 (scale >= k > 0)
+__device__ __forceinline__ float lrn_out(float x, float scale, float beta) {
+  return x * exp2f(-beta * log2f(scale));
+}
+
 // 32-bit word -> uniform in (0, 1] (never 0: safe for log) and [0, 1).
 __host__ __device__ __forceinline__ float u01_open0(uint32_t r) {
   return (static_cast<float>(r >> 8) + 1.0f) * (1.0f / 16777216.0f);

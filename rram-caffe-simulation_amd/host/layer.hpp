@@ -76,6 +76,19 @@ class Layer {
   uint32_t layer_id = 0;
   uint64_t iter = 0;
 
+  // TEST-phase fusion (Net::Net): an ACROSS_CHANNELS LRN whose top only feeds
+  // a MAX pool hands its work to the pool (rram_lrn_maxpool_fwd); the LRN's
+  // Forward then only reshapes.  lrn_params() reports an LRN's parameters,
+  // fuse_lrn_before() asks the consumer to take them over.
+  virtual bool lrn_params(int& /*size*/, float& /*alpha*/, float& /*beta*/, float& /*k*/) const {
+    return false;
+  }
+  virtual bool fuse_lrn_before(Blob<Dtype>* /*lrn_bottom*/, int /*size*/, float /*alpha*/,
+                               float /*beta*/, float /*k*/) {
+    return false;
+  }
+  bool folded_into_next = false;
+
  protected:
   virtual void Forward_gpu(const std::vector<Blob<Dtype>*>& bottom,
                            const std::vector<Blob<Dtype>*>& top) = 0;

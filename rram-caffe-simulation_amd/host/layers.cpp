@@ -339,8 +339,26 @@ class PoolingLayer : public Layer<Dtype> {
     if (method_ == RRAM_POOL_MAX) mask_.Reshape(top[0]->shape());
   }
 
+  bool fuse_lrn_before(Blob<Dtype>* lrn_bottom, int size, float alpha, float beta, float k) override {
+    if (this->phase_ != TEST || method_ != RRAM_POOL_MAX || global_ || kh_ != kw_ || (kh_ != 2 && kh_ != 3) ||
+        ph_ >= kh_ || pw_ >= kw_ || (size != 3 && size != 5))
+      return false;
+    lrn_src_ = lrn_bottom;
+    lrn_size_ = size;
+    lrn_alpha_ = alpha;
+    lrn_beta_ = beta;
+    lrn_k_ = k;
+    return true;
+  }
+
  protected:
   void Forward_gpu(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
+    if (lrn_src_ != nullptr) {  // LRN folded into this pool (Net::Net, TEST phase)
+      RRAM_CALL(rram_lrn_maxpool_fwd(lrn_src_->gpu_data(), top[0]->mutable_gpu_data(), bottom[0]->shape(0), C_, H_,
+                                     W_, PH_, PW_, kh_, sh_, sw_, ph_, pw_, lrn_size_, lrn_alpha_, lrn_beta_, lrn_k_,
+                                     Caffe::stream()));
+      return;
+    }
     int* mask = (method_ == RRAM_POOL_MAX && this->phase_ == TRAIN)
                     ? reinterpret_cast<int*>(mask_.mutable_gpu_data()) : nullptr;
     RRAM_CALL(rram_pool_fwd(bottom[0]->gpu_data(), top[0]->mutable_gpu_data(), mask, bottom[0]->shape(0),
@@ -359,6 +377,9 @@ class PoolingLayer : public Layer<Dtype> {
   int C_ = 0, H_ = 0, W_ = 0, PH_ = 0, PW_ = 0;
   bool global_ = false;
   Blob<Dtype> mask_;
+  Blob<Dtype>* lrn_src_ = nullptr;  // bottom of a folded LRN (nullptr: unfused)
+  int lrn_size_ = 5;
+  float lrn_alpha_ = 1, lrn_beta_ = 0.75f, lrn_k_ = 1;
 };
 
 // -------------------------------------------------------------------- LRN
@@ -385,10 +406,19 @@ class LRNLayer : public Layer<Dtype> {
     top[0]->ReshapeLike(*bottom[0]);
     if (this->phase_ == TRAIN) scale_.ReshapeLike(*bottom[0]);
   }
+  bool lrn_params(int& size, float& alpha, float& beta, float& k) const override {
+    if (within_) return false;
+    size = size_;
+    alpha = alpha_;
+    beta = beta_;
+    k = k_;
+    return true;
+  }
 
  protected:
   void Forward_gpu(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
     CAFFE_CHECK(bottom[0] != top[0], "LRN cannot run in place");
+    if (this->folded_into_next) return;  // computed by the following MAX pool
     auto& b = *bottom[0];
     float* sc = this->phase_ == TRAIN ? scale_.mutable_gpu_data() : nullptr;
     if (within_)

@@ -143,6 +143,7 @@ Net<Dtype>::Net(const Msg& in_param, Phase phase, const Msg& options) : phase_(p
     while (std::getline(ss, t, ',')) fault_layer_types_.push_back(t);
   }
   const bool fuse_relu = options.boolean("fuse_relu", true);
+  const bool fuse_lrn_pool = options.boolean("fuse_lrn_pool", true);
   std::vector<int> data_shape;
   {
     std::string ds = options.str("data_shape", "");
@@ -236,6 +237,20 @@ Net<Dtype>::Net(const Msg& in_param, Phase phase, const Msg& options) : phase_(p
           relu->folded = true;
         }
       }
+    }
+    // TEST phase: fold an ACROSS_CHANNELS LRN into the MAX pool that is the only
+    // reader of its top (a second reader would sit behind a Split layer); the
+    // LRN top is then never materialised (rram_lrn_maxpool_fwd)
+    if (fuse_lrn_pool && phase == TEST && type == "Pooling" && lid > 0 && bottoms.size() == 1) {
+      auto& prev = layers_[lid - 1];
+      int sz = 0;
+      float a = 0.f, b = 0.f, kk = 0.f;
+      const bool prev_makes_it = bottom_vecs_[lid - 1].size() == 1 && top_id_vecs_[lid - 1].size() == 1 &&
+                                 top_id_vecs_[lid - 1][0] == bottom_id_vecs_[lid][0] &&
+                                 bottom_id_vecs_[lid - 1][0] != top_id_vecs_[lid - 1][0];
+      if (prev_makes_it && prev->lrn_params(sz, a, b, kk) &&
+          layer->fuse_lrn_before(bottom_vecs_[lid - 1][0], sz, a, b, kk))
+        prev->folded_into_next = true;
     }
     ++lid;
   }

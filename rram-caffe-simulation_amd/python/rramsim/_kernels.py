@@ -99,6 +99,7 @@ SIGNATURES = {
     "rram_lrn_bwd": (I, [P, P, P, P, P, I, I, I, I, I, F, F, P]),
     "rram_lrn_within_fwd": (I, [P, P, P, I, I, I, I, I, F, F, P]),
     "rram_lrn_within_bwd": (I, [P, P, P, P, I, I, I, I, I, F, F, P]),
+    "rram_lrn_maxpool_fwd": (I, [P, P, I, I, I, I, I, I, I, I, I, I, I, I, F, F, F, P]),
     "rram_softmax_fwd": (I, [P, P, I, I, I, P]),
     "rram_softmax_loss_fwd": (I, [P, P, P, I, I, I, I, P]),
     "rram_softmax_loss_bwd": (I, [P, P, P, I, I, I, I, F, P]),

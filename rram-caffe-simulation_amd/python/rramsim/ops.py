@@ -180,6 +180,11 @@ def lrn_bwd(x, y, scale, dy, dx, n, c, h, w, size, alpha, beta):
                                 beta, _stream()), "lrn_bwd")
 
 
+def lrn_maxpool_fwd(x, y, n, c, h, w, ph, pw, kernel, stride, pad, size, alpha, beta, k=1.0):
+    K.check(_lib().rram_lrn_maxpool_fwd(_p(x), _p(y), n, c, h, w, ph, pw, kernel, stride, stride, pad, pad,
+                                        size, alpha, beta, k, _stream()), "lrn_maxpool_fwd")
+
+
 def lrn_within_fwd(x, y, scale, n, c, h, w, size, alpha, beta):
     K.check(_lib().rram_lrn_within_fwd(_p(x), _p(y), _p(scale), n, c, h, w, size, alpha, beta,
                                        _stream()), "lrn_within_fwd")

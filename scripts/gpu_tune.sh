@@ -5,7 +5,7 @@ set -o pipefail
 O=gpurun_out
 mkdir -p $O
 timeout -k 10 600 python -m pytest ${TESTS:-tests/test_gpu_kernels.py tests/test_gpu_layers.py tests/test_gpu_host.py} -m gpu -q -x > $O/pytest_tune.log 2>&1 || exit $?
-for g in 2048 4096 8192 16384; do
+for g in 2048 8192 1073741824; do
   RRAM_INJECT_GRID=$g timeout -k 10 120 python scripts/kbench.py --only inject > $O/kb_inject_$g.log 2>&1 || exit $?
 done
 timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench_t2.json 2> $O/bench_t2.err || exit $?

@@ -113,6 +113,50 @@ def test_lrn_across_fwd_bwd_vs_autograd(device, size):
     torch.testing.assert_close(dx, x.grad, rtol=1e-4, atol=1e-5)
 
 
+@pytest.mark.parametrize("size,k,s,p,C,H", [(5, 3, 2, 0, 13, 15), (5, 3, 2, 0, 96, 55), (3, 3, 2, 1, 7, 12),
+                                             (5, 2, 2, 0, 9, 10), (3, 3, 1, 0, 6, 8)])
+def test_lrn_maxpool_fused_equals_unfused(device, size, k, s, p, C, H):
+    """rram_lrn_maxpool_fwd == rram_lrn_fwd then rram_pool_fwd, bit for bit
+    (same LRN arithmetic; window edges of the ceil rule), and the torch fp32
+    reference within the LRN tolerance."""
+    import torch
+    from rramsim import ops
+    torch.manual_seed(9)
+    N, W = 3, H - 1
+    x = 4 * torch.randn(N, C, H, W, device=device)
+    alpha, beta, kk = 1e-2, 0.75, 1.5
+    lrn = torch.empty_like(x)
+    ops.lrn_fwd(x, lrn, None, N, C, H, W, size, alpha, beta, kk)
+    ref = _caffe_pool_ref(lrn, k, s, p, "MAX")
+    PH, PW = ref.shape[2], ref.shape[3]
+    unfused = torch.empty_like(ref)
+    ops.pool_fwd(lrn, unfused, None, (N, C, H, W, PH, PW, k, k, s, s, p, p), 0)
+    fused = torch.full_like(ref, float("nan"))
+    ops.lrn_maxpool_fwd(x, fused, N, C, H, W, PH, PW, k, s, p, size, alpha, beta, kk)
+    torch.cuda.synchronize()
+    assert torch.equal(fused, unfused)
+    torch.testing.assert_close(fused, _caffe_pool_ref(_lrn_across_ref(x, size, alpha, beta, kk), k, s, p, "MAX"),
+                               rtol=2e-5, atol=1e-6)
+
+
+def test_lrn_maxpool_fusion_in_alexnet_test_net(device):
+    """Net folds norm1/norm2 into pool1/pool2 in the TEST phase; the net outputs
+    are bit-identical to the unfused net."""
+    import torch
+    from rramsim import caffe, models
+    caffe.set_stream_from_torch()
+    outs = []
+    for fuse in (False, True):
+        caffe.set_random_seed(1701)
+        net = caffe.Net(models.alexnet(test_batch=4), "test", models.net_options("alexnet", fuse_lrn_pool=fuse))
+        net.forward()
+        torch.cuda.synchronize()
+        outs.append({b: net.blob(b).detach().cpu().clone() for b in ("pool1", "pool2", "fc8")})
+        net.close()
+    for b in ("pool1", "pool2", "fc8"):
+        assert torch.equal(outs[0][b], outs[1][b]), b
+
+
 @pytest.mark.parametrize("size", [3, 5])
 def test_lrn_within_fwd_bwd_vs_autograd(device, size):
     """cifar10_full's norm1/norm2 (lrn_layer.cpp WithinChannelForward/Backward)."""
