@@ -108,6 +108,17 @@ def cpu_baseline(batch, p_fault, seed, budget_s=12.0):
                       f"extrapolated to one {batch}-image map"}
 
 
+def load_traffic():
+    """HBM bytes from the committed rocprofv3 PMC passes of this same command
+    (scripts/pmc.sh + scripts/pmc_traffic.py -> profiles/pmc_traffic.json):
+    PMC counters cannot be read from inside the timed process itself."""
+    p = ROOT / "profiles" / "pmc_traffic.json"
+    try:
+        return json.loads(p.read_text())
+    except (OSError, ValueError):
+        return {}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -198,6 +209,7 @@ def main():
         for name, typ, ms, cnt in lt:
             print(f"{name:>12s} {typ:>16s} {ms / max(cnt, 1):9.3f} ms", file=sys.stderr)
 
+    traffic = load_traffic()
     n_images = world * args.steps * args.batch
     value = n_images / elapsed
     out_names = [k for k in net.outputs().keys()]
@@ -221,12 +233,15 @@ def main():
                    "p_fault": args.p_fault, "stuck_split_neg_zero_pos": [10, 20, 10],
                    "fault_layers": "InnerProduct (58,631,144 weights)", "parallelism": f"mc-maps x{world} (RCCL stats all-reduce)"},
         "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 2), "peak": MFMA_F32_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(achieved_tf / MFMA_F32_PEAK_TFLOPS, 4), "traffic": None,
+                     "unit": "TFLOP/s", "frac": round(achieved_tf / MFMA_F32_PEAK_TFLOPS, 4),
+                     "traffic": traffic.get("gemm", {}).get("bytes_per_step"),
                      "kernel": "conv1-5 implicit-GEMM + fc6-8 GEMM (fp32 MFMA 32x32x2), per step",
                      "algorithmic_flops_per_step": gemm_flops, "avg_ms_per_step": round(gemm_ms, 4)},
         "roofline_inject": {"bound": "hbm", "achieved": round(inj_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                            "frac": round(inj_gbps / HBM_PEAK_GBPS, 4), "traffic": None,
+                            "frac": round(inj_gbps / HBM_PEAK_GBPS, 4),
+                            "traffic": traffic.get("inject", {}).get("bytes_per_launch"),
                             "algorithmic_bytes_per_launch": 8 * inj_w, "avg_us_per_launch": round(inj_ms_per * 1e3, 2)},
+        "traffic_source": traffic.get("source"),
         "mc_stats": {"maps": int(stats[len(st["sums"]) + 1].item()), "mean_outputs": mean_out,
                      "broken_cells": int(stats[len(st["sums"])].item())},
     }

@@ -120,6 +120,39 @@ int rram_solver_fail_state(rram_solver_t s, int i, float** endurance, float** va
 /* broken cells per faultable blob after the last Fail() (device count, one D2H) */
 int rram_solver_broken_counts(rram_solver_t s, unsigned long long* out, int cap, int* n);
 
+/* Solver::ApplyStrategy (solver.cpp:25-33): run every failure_strategy's
+ * Apply() once, outside Step (threshold / remapping / genetic). */
+int rram_solver_apply_strategies(rram_solver_t s);
+/* Strategy i's type and counters: genetic -> (dist before, dist after,
+ * accepted swaps) of its last Apply(); others -> zeros. */
+int rram_solver_strategy_info(rram_solver_t s, int i, char* type, int cap, int* a, int* b, int* c);
+/* Solver::Snapshot (solver.cpp:461-518, BINARYPROTO): writes
+ * <snapshot_prefix>_iter_N.{caffemodel,solverstate,faultstate}; the
+ * .solverstate path is copied into path_out (cap bytes, nullable). */
+int rram_solver_snapshot(rram_solver_t s, char* path_out, int cap);
+/* Solver::Restore (sgd_solver.cpp:309-326) from a .solverstate; the fault
+ * maps are restored when the matching .faultstate exists. */
+int rram_solver_restore(rram_solver_t s, const char* state_file);
+/* Solver::Solve(resume_file) (solver.cpp:328-370); resume_file nullable. */
+int rram_solver_solve_from(rram_solver_t s, const char* resume_file);
+
+/* ------------------------------------------------------ weight files
+ * Net::CopyTrainedLayersFrom (net.cpp:765-818) for a binary .caffemodel
+ * (NetParameter `layer` or V1 `layers`), and Net::ToProto + write
+ * (net.cpp:871-880): name/type/bottom/top/blobs of every layer. */
+int rram_net_copy_trained_layers_from(rram_net_t net, const char* caffemodel);
+int rram_net_save_weights(rram_net_t net, const char* caffemodel, int write_diff);
+/* Host-only (no device): one line per blob of a .caffemodel,
+ * "layer\ttype\tindex\tshape\tcount\tdata_sum\tdiff_count"; *needed = bytes
+ * including the terminator. */
+int rram_caffemodel_describe(const char* caffemodel, char* out, size_t cap, size_t* needed);
+/* Host-only: parse a binary proto file and serialise it again
+ * (kind 0 NetParameter, 1 SolverState, 2 BlobProtoVector). */
+int rram_proto_rewrite(const char* in_path, const char* out_path, int kind);
+/* Host-only: n outputs of glibc's rand() after srand(seed) (the genetic
+ * strategy's generator, strategy.cpp:170-175). */
+int rram_glibc_rand(uint32_t seed, int n, int* out);
+
 /* --------------------------------------------------------- Monte-Carlo
  * Fault-map inference on a TEST-phase net: for maps m in [begin, begin+count):
  * inject(clean weights) -> forward -> accumulate scalar outputs.  cfgs: one

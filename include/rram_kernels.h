@@ -151,6 +151,27 @@ int rram_inject_rng_batched(const rram_inject_seg* segs, int nsegs,
 int rram_threshold_strategy(float* dw, int64_t n, float thr,
                             unsigned long long* cleared, rram_stream_t stream);
 
+/* Remapping statistics (RemappingFailureStrategy::GetFailFlagMat + the two
+ * asum loops of SortFCNeurons, src/caffe/strategy.cpp:36-77): for a
+ * [rows x cols] fault state, flag = (endurance < 0 && value == 0);
+ * row_counts[r] = #flags in row r (written), col_counts[c] += #flags in
+ * column c (accumulated; zero it first).  Either output may be NULL. */
+int rram_stuck_zero_counts(const float* endurance, const float* values, int rows, int cols,
+                           unsigned* row_counts, unsigned* col_counts, rram_stream_t stream);
+
+/* Neuron moves of the remapping / genetic strategies (strategy.cpp:109-135,
+ * 237-283) as gathers with device index vectors (src != dst):
+ *   rows:  dst[to[j]*row_len + c] = src[from[j]*row_len + c]
+ *   cols:  dst[k*cols + to[j]]    = src[k*cols + from[j]]   (k < rows)
+ *   elems: dst[to[j]]             = src[from[j]]
+ * Rows / elements not named in `to` are left untouched. */
+int rram_permute_rows(const float* src, float* dst, int64_t row_len, const int* to, const int* from,
+                      int n, rram_stream_t stream);
+int rram_permute_cols(const float* src, float* dst, int rows, int cols, const int* to, const int* from,
+                      int n, rram_stream_t stream);
+int rram_permute_elems(const float* src, float* dst, const int* to, const int* from, int n,
+                       rram_stream_t stream);
+
 /* g = h = momentum * h + local_rate * g.  Replaces SGDUpdate
  * (src/caffe/solvers/sgd_solver.cu:6-20). */
 int rram_sgd_update(float* g, float* h, int64_t n, float momentum,

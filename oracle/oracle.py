@@ -290,3 +290,100 @@ def accuracy(x, label, top_k=1):
 def softmax_loss(prob, label):
     p = prob[np.arange(len(label)), np.asarray(label, np.int64)]
     return float(-np.log(np.maximum(p, np.finfo(np.float32).tiny)).sum() / len(label))
+
+
+# ----------------------------------------------------------------------------
+# Fault-tolerance strategies (src/caffe/strategy.cpp) — numpy / pure-Python
+# restatements for small nets.  The reference sorts with std::sort (unstable);
+# callers give inputs whose sort keys are distinct, so argsort is the same order.
+# ----------------------------------------------------------------------------
+def remap_orders(e_list, v_list):
+    """SortFCNeurons (strategy.cpp:48-86): e_list / v_list are the fault states
+    of the FC weight blobs (2-D, in fc_params_ids_ order)."""
+    flags = [((e < 0) & (v == 0)).astype(np.int64) for e, v in zip(e_list, v_list)]  # GetFailFlagMat :36-45
+    orders = []
+    for i in range(1, len(flags)):
+        zero_nums = flags[i - 1].sum(axis=1) + flags[i].sum(axis=0)   # asum row + strided asum column
+        assert len(np.unique(zero_nums)) == len(zero_nums), "oracle needs distinct sort keys"
+        orders.append(np.argsort(zero_nums, kind="stable"))
+    return orders
+
+
+def remap_apply(fc_w, fc_wd, fc_b, fc_bd, e_list, v_list, prune_orders, compat=False):
+    """RemappingFailureStrategy::Apply (strategy.cpp:88-137) on copies.
+    fc_w/fc_wd: FC weight data/diff (2-D), fc_b/fc_bd: their biases."""
+    W = [w.copy() for w in fc_w]
+    Wd = [w.copy() for w in fc_wd]
+    B = [b.copy() for b in fc_b]
+    Bd = [b.copy() for b in fc_bd]
+    orders = remap_orders(e_list, v_list)
+    for i in range(1, len(W)):
+        order, prune = orders[i - 1], np.asarray(prune_orders[i - 1])
+        rw, rwd, rb, rbd = W[i - 1].copy(), Wd[i - 1].copy(), B[i - 1].copy(), Bd[i - 1].copy()
+        for j in range(len(order)):
+            W[i - 1][order[j]] = rw[prune[j]]
+            Wd[i - 1][order[j]] = rwd[prune[j]]
+            if compat:   # strategy.cpp:118-119 reads the weight array (Appendix A Q8)
+                B[i - 1][order[j]] = rw.reshape(-1)[prune[j]]
+                Bd[i - 1][order[j]] = rwd.reshape(-1)[prune[j]]
+            else:
+                B[i - 1][order[j]] = rb[prune[j]]
+                Bd[i - 1][order[j]] = rbd[prune[j]]
+        ow, owd = W[i].copy(), Wd[i].copy()
+        for j in range(len(order)):
+            W[i][:, order[j]] = ow[:, prune[j]]
+            Wd[i][:, order[j]] = owd[:, prune[j]]
+    return W, Wd, B, Bd, orders
+
+
+def genetic_apply(fc_ids, fail_e, prune, weights, rand, switch_time, compat=False):
+    """GeneticFailureStrategy::Apply (strategy.cpp:158-288) on copies.
+    fail_e / prune / weights: per failure param (flat arrays; weights as
+    (data, diff, shape)); fc_ids: indices of the FC weight params; rand: the
+    rand() stream.  Returns (weights', prune', dist_before, dist_after, accepted)."""
+    eps = np.float32(1e-20)
+    P = [p.astype(np.float32).copy() for p in prune]
+    Wt = [(d.copy(), g.copy(), s) for d, g, s in weights]
+
+    def overall():
+        return sum(int(((p < eps) & (e < 0)).sum()) for p, e in zip(P, fail_e))
+    before = overall()
+    size = len(fc_ids)
+    accepted = 0
+    i = 0
+    while i < switch_time:
+        li = rand() % (size - 1) + 1
+        a, b = fc_ids[li - 1], fc_ids[li]
+        layer_dim, in_dim = Wt[a][2]
+        n1 = rand() % layer_dim
+        n2 = rand() % layer_dim
+        if n1 == n2:
+            continue
+        i += 1
+        out_dim = Wt[b][2][0]
+        fin = fail_e[a].reshape(layer_dim, in_dim)
+        fout = fail_e[b].reshape(out_dim, layer_dim)
+        pin = P[a].reshape(layer_dim, in_dim)
+        pout = P[b].reshape(out_dim, layer_dim)
+        db = int(((pin[n1] < eps) & (fin[n1] < 0)).sum() + ((pin[n2] < eps) & (fin[n2] < 0)).sum()
+                 + ((pout[:, n1] < eps) & (fout[:, n1] < 0)).sum() + ((pout[:, n2] < eps) & (fout[:, n2] < 0)).sum())
+        da = int(((pin[n2] < eps) & (fin[n1] < 0)).sum() + ((pin[n1] < eps) & (fin[n2] < 0)).sum()
+                 + ((pout[:, n2] < eps) & (fout[:, n1] < 0)).sum() + ((pout[:, n1] < eps) & (fout[:, n2] < 0)).sum())
+        if da < db:
+            accepted += 1
+            for arr in (Wt[a][0], Wt[a][1]):
+                m = arr.reshape(layer_dim, in_dim)
+                m[[n1, n2]] = m[[n2, n1]]
+            for arr in (Wt[a + 1][0], Wt[a + 1][1]):   # bias (strategy.cpp:250-255)
+                arr[[n1, n2]] = arr[[n2, n1]]
+            pin[[n1, n2]] = pin[[n2, n1]]
+            if compat:                                   # Appendix A Q9 (strategy.cpp:265-267)
+                flat = P[a]
+                flat[n1], flat[n2] = flat[n2], flat[n1]
+            elif a + 1 < len(P) and P[a + 1].size == layer_dim:
+                P[a + 1][[n1, n2]] = P[a + 1][[n2, n1]]
+            for arr in (Wt[b][0], Wt[b][1]):
+                m = arr.reshape(out_dim, layer_dim)
+                m[:, [n1, n2]] = m[:, [n2, n1]]
+            pout[:, [n1, n2]] = pout[:, [n2, n1]]
+    return Wt, P, before, overall(), accepted

@@ -400,6 +400,96 @@ int rram_solver_broken_counts(rram_solver_t s, unsigned long long* out, int cap,
   });
 }
 
+int rram_solver_apply_strategies(rram_solver_t s) {
+  return guarded([&] {
+    NEED(s);
+    for (auto& st : s->solver->strategies()) st->Apply();
+  });
+}
+int rram_solver_strategy_info(rram_solver_t s, int i, char* type, int cap, int* a, int* b, int* c) {
+  return guarded([&] {
+    NEED(s);
+    const auto& v = s->solver->strategies();
+    if (i < 0 || i >= (int)v.size()) throw Error("strategy index out of range");
+    copy_str(v[i]->type(), type, cap);
+    int x = 0, y = 0, z = 0;
+    if (auto* g = dynamic_cast<GeneticFailureStrategy<float>*>(v[i].get())) {
+      x = g->last_before();
+      y = g->last_after();
+      z = g->last_accepted();
+    }
+    if (a) *a = x;
+    if (b) *b = y;
+    if (c) *c = z;
+  });
+}
+int rram_solver_snapshot(rram_solver_t s, char* path_out, int cap) {
+  return guarded([&] {
+    NEED(s);
+    copy_str(s->solver->Snapshot(), path_out, cap);
+  });
+}
+int rram_solver_restore(rram_solver_t s, const char* state_file) {
+  return guarded([&] {
+    NEED(s);
+    NEED(state_file);
+    s->solver->Restore(state_file);
+  });
+}
+int rram_solver_solve_from(rram_solver_t s, const char* resume_file) {
+  return guarded([&] {
+    NEED(s);
+    s->solver->Solve(resume_file);
+  });
+}
+
+// ------------------------------------------------------------ weight files
+int rram_net_copy_trained_layers_from(rram_net_t n, const char* path) {
+  return guarded([&] {
+    NEED(n);
+    NEED(path);
+    n->net->CopyTrainedLayersFrom(std::string(path));
+  });
+}
+int rram_net_save_weights(rram_net_t n, const char* path, int write_diff) {
+  return guarded([&] {
+    NEED(n);
+    NEED(path);
+    WriteFileBytes(path, SerializeNetParameter(n->net->ToProto(write_diff != 0)));
+  });
+}
+int rram_caffemodel_describe(const char* path, char* out, size_t cap, size_t* needed) {
+  return guarded([&] {
+    NEED(path);
+    const std::string d = DescribeNetProto(ParseNetParameter(ReadFileBytes(path)));
+    if (needed) *needed = d.size() + 1;
+    if (out && cap > 0) {
+      const size_t k = std::min(d.size(), cap - 1);
+      std::memcpy(out, d.data(), k);
+      out[k] = '\0';
+    }
+  });
+}
+int rram_proto_rewrite(const char* in, const char* out, int kind) {
+  return guarded([&] {
+    NEED(in);
+    NEED(out);
+    const std::string b = ReadFileBytes(in);
+    if (kind == 0) WriteFileBytes(out, SerializeNetParameter(ParseNetParameter(b)));
+    else if (kind == 1) WriteFileBytes(out, SerializeSolverState(ParseSolverState(b)));
+    else if (kind == 2) WriteFileBytes(out, SerializeBlobProtoVector(ParseBlobProtoVector(b)));
+    else throw Error("rram_proto_rewrite: kind must be 0, 1 or 2");
+  });
+}
+int rram_glibc_rand(uint32_t seed, int n, int* out) {
+  return guarded([&] {
+    if (n < 0) throw Error("n < 0");
+    if (n > 0) NEED(out);
+    GlibcRand r(seed);
+    for (int i = 0; i < n; ++i) out[i] = r();
+  });
+}
+
 // ----------------------------------------------------------- Monte-Carlo
 int rram_mc_create(rram_net_t net, const rram_inject_cfg* cfgs, int ncfg, uint64_t seed, int max_maps,
                    rram_mc_t* out) {

@@ -372,6 +372,87 @@ void Net<Dtype>::ShareTrainedLayersWith(const Net* other) {
   }
 }
 
+// Blob::FromProto(proto, reshape = false) (blob.cpp:448-496): H2D of data, and
+// of diff when the proto carries one.
+template <typename Dtype>
+void BlobFromProto(Blob<Dtype>* b, const BlobProtoData& p) {
+  CAFFE_CHECK((int64_t)p.data.size() == b->count(), "blob data count " << p.data.size() << " != " << b->count());
+  HIP_CALL(hipMemcpyAsync(b->mutable_gpu_data(), p.data.data(), p.data.size() * sizeof(Dtype), hipMemcpyHostToDevice,
+                          Caffe::hip_stream()));
+  if (!p.diff.empty()) {
+    CAFFE_CHECK((int64_t)p.diff.size() == b->count(), "blob diff count " << p.diff.size() << " != " << b->count());
+    HIP_CALL(hipMemcpyAsync(b->mutable_gpu_diff(), p.diff.data(), p.diff.size() * sizeof(Dtype),
+                            hipMemcpyHostToDevice, Caffe::hip_stream()));
+  }
+  HIP_CALL(hipStreamSynchronize(Caffe::hip_stream()));  // the host vectors die with the caller
+}
+
+// Blob::ToProto (blob.cpp:518-535)
+template <typename Dtype>
+BlobProtoData BlobToProto(Blob<Dtype>* b, bool write_diff) {
+  BlobProtoData p;
+  p.shape.assign(b->shape().begin(), b->shape().end());
+  p.data.resize(b->count());
+  HIP_CALL(hipMemcpyAsync(p.data.data(), b->gpu_data(), p.data.size() * sizeof(Dtype), hipMemcpyDeviceToHost,
+                          Caffe::hip_stream()));
+  if (write_diff) {
+    p.diff.resize(b->count());
+    HIP_CALL(hipMemcpyAsync(p.diff.data(), b->gpu_diff(), p.diff.size() * sizeof(Dtype), hipMemcpyDeviceToHost,
+                            Caffe::hip_stream()));
+  }
+  HIP_CALL(hipStreamSynchronize(Caffe::hip_stream()));
+  return p;
+}
+template void BlobFromProto<float>(Blob<float>*, const BlobProtoData&);
+template BlobProtoData BlobToProto<float>(Blob<float>*, bool);
+
+// net.cpp:765-800: match source layers by name, same blob count, ShapeEquals
+template <typename Dtype>
+void Net<Dtype>::CopyTrainedLayersFrom(const NetProtoData& param) {
+  for (const auto& src : param.layers) {
+    auto it = layer_names_index_.find(src.name);
+    if (it == layer_names_index_.end()) continue;  // "Ignoring source layer"
+    auto& target = layers_[it->second]->blobs();
+    CAFFE_CHECK(target.size() == src.blobs.size(), "Incompatible number of blobs for layer " << src.name);
+    for (size_t j = 0; j < target.size(); ++j) {
+      if (!ShapeEquals(target[j]->shape(), src.blobs[j])) {
+        std::ostringstream s;
+        for (size_t a = 0; a < src.blobs[j].shape.size(); ++a) s << (a ? " " : "") << src.blobs[j].shape[a];
+        throw Error("Cannot copy param " + std::to_string(j) + " weights from layer '" + src.name +
+                    "'; shape mismatch.  Source param shape is " + s.str() + "; target param shape is " +
+                    target[j]->shape_string());
+      }
+      BlobFromProto(target[j].get(), src.blobs[j]);
+    }
+  }
+}
+
+// net.cpp:803-818 (binary proto; HDF5 weights are out of scope)
+template <typename Dtype>
+void Net<Dtype>::CopyTrainedLayersFrom(const std::string& path) {
+  CAFFE_CHECK(path.size() < 3 || path.compare(path.size() - 3, 3, ".h5") != 0,
+              "HDF5 weight files are not supported by this build: " << path);
+  CopyTrainedLayersFrom(ParseNetParameter(ReadFileBytes(path)));
+}
+
+// net.cpp:871-880 / layer.hpp ToProto: name, type, bottoms, tops and blobs of
+// every layer (the other LayerParameter fields live in the prototxt)
+template <typename Dtype>
+NetProtoData Net<Dtype>::ToProto(bool write_diff) const {
+  NetProtoData n;
+  n.name = name_;
+  for (size_t i = 0; i < layers_.size(); ++i) {
+    LayerProtoData L;
+    L.name = layer_names_[i];
+    L.type = layers_[i]->type();
+    L.bottom = layers_[i]->layer_param().strs("bottom");
+    L.top = layers_[i]->layer_param().strs("top");
+    for (auto& b : layers_[i]->blobs()) L.blobs.push_back(BlobToProto(b.get(), write_diff));
+    n.layers.push_back(std::move(L));
+  }
+  return n;
+}
+
 template <typename Dtype>
 std::shared_ptr<Blob<Dtype>> Net<Dtype>::blob_by_name(const std::string& n) const {
   auto it = blob_names_index_.find(n);

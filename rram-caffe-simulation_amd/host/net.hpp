@@ -9,10 +9,22 @@
 #include <string>
 #include <vector>
 
+#include "io.hpp"
+#include "io.hpp"
 #include "layers.hpp"
 #include "timer.hpp"
 
 namespace caffe {
+
+template <typename Dtype>
+void BlobFromProto(Blob<Dtype>* b, const BlobProtoData& p);  // shape-checked by the caller
+template <typename Dtype>
+BlobProtoData BlobToProto(Blob<Dtype>* b, bool write_diff);
+
+template <typename Dtype>
+void BlobFromProto(Blob<Dtype>* b, const BlobProtoData& p);  // shape-checked by the caller
+template <typename Dtype>
+BlobProtoData BlobToProto(Blob<Dtype>* b, bool write_diff);
 
 template <typename Dtype>
 class Net {
@@ -33,6 +45,10 @@ class Net {
   void Update();
   void ClearParamDiffs();
   void ShareTrainedLayersWith(const Net* other);
+  // .caffemodel weights (net.cpp:765-880, binary proto only; io.hpp)
+  void CopyTrainedLayersFrom(const NetProtoData& param);
+  void CopyTrainedLayersFrom(const std::string& path);
+  NetProtoData ToProto(bool write_diff = false) const;
 
   const std::string& name() const { return name_; }
   Phase phase() const { return phase_; }

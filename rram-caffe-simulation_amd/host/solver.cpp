@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <fstream>
 #include <sstream>
 
 namespace caffe {
@@ -105,9 +106,16 @@ std::shared_ptr<FailureStrategy<Dtype>> FailureStrategy<Dtype>::CreateStrategy(
     p->reference_lr_index = param.boolean("rram_reference_lr_index", false);
     return p;
   }
-  if (type == "remapping" || type == "genetic")
-    throw Error("failure_strategy '" + type + "' (periodic FC-neuron remapping) is not part of this build yet "
-                "(SURVEY.md §8f-4)");
+  if (type == "remapping") {
+    auto p = std::make_shared<RemappingFailureStrategy<Dtype>>(param, fm, net, s);
+    p->reference_compat = param.boolean("rram_reference_compat", false);
+    return p;
+  }
+  if (type == "genetic") {
+    auto p = std::make_shared<GeneticFailureStrategy<Dtype>>(param, fm, net, s);
+    p->reference_compat = param.boolean("rram_reference_compat", false);
+    return p;
+  }
   throw Error("No strategy named `" + type + "` exists.");
 }
 
@@ -139,7 +147,7 @@ static Msg load_net_param(const Msg& sp, const Msg* net_param) {
 }
 
 template <typename Dtype>
-Solver<Dtype>::Solver(const Msg& sp, const Msg* net_param, const Msg& options) : param_(sp) {
+Solver<Dtype>::Solver(const Msg& sp, const Msg* net_param, const Msg& options) : param_(sp), options_(options) {
   if (sp.has("random_seed") && sp.integer("random_seed") >= 0)
     Caffe::set_random_seed(static_cast<uint64_t>(sp.integer("random_seed")));
   fused_update_ = options.boolean("fused_update", false);
@@ -348,13 +356,24 @@ void Solver<Dtype>::Step(int iters) {
       Fail(iter_);
     }
     ++iter_;
+    const long long snap = param_.integer("snapshot", 0);  // solver.cpp:312-318
+    if (snap && iter_ % snap == 0) Snapshot();
   }
 }
 
 template <typename Dtype>
-void Solver<Dtype>::Solve() {
+void Solver<Dtype>::Solve(const char* resume_file) {
+  if (resume_file) {
+    emit(std::string("Restoring previous solver status from ") + resume_file);
+    Restore(resume_file);
+  }
   const int max_iter = (int)param_.integer("max_iter", 0);
   Step(max_iter - iter_);
+  // solver.cpp:345-350 (only with a snapshot_prefix: the reference would write
+  // "_iter_N.caffemodel" into the working directory without one)
+  const long long snap = param_.integer("snapshot", 0);
+  if (param_.has("snapshot_prefix") && param_.boolean("snapshot_after_train", true) && (!snap || iter_ % snap != 0))
+    Snapshot();
   if (param_.integer("display", 0) && max_iter % std::max<long long>(1, param_.integer("display", 1)) == 0) {
     std::ostringstream o;
     o << "Iteration " << iter_ << ", loss = " << smoothed_loss_;
@@ -363,6 +382,60 @@ void Solver<Dtype>::Solve() {
   const int ti = (int)param_.integer("test_interval", 0);
   if (ti && iter_ % ti == 0) TestAll();
   emit("Optimization Done.");
+}
+
+template <typename Dtype>
+std::string Solver<Dtype>::Snapshot() {
+  CAFFE_CHECK(param_.str("snapshot_format", "BINARYPROTO") == "BINARYPROTO",
+              "only snapshot_format: BINARYPROTO is supported by this build (HDF5: DESIGN.md §6)");
+  const std::string model = SnapshotFilename(".caffemodel");
+  emit("Snapshotting to binary proto file " + model);
+  WriteFileBytes(model, SerializeNetParameter(net_->ToProto(param_.boolean("snapshot_diff", false))));
+  SolverStateData st;
+  st.iter = iter_;
+  st.learned_net = model;
+  st.current_step = current_step_;
+  for (auto& h : history_) st.history.push_back(BlobToProto(h.get(), false));
+  const std::string state = SnapshotFilename(".solverstate");
+  emit("Snapshotting solver state to binary proto file " + state);
+  WriteFileBytes(state, SerializeSolverState(st));
+  if (fmaker_) {
+    std::vector<BlobProtoData> fs;
+    for (auto* b : fmaker_->fail_iterations()) fs.push_back(BlobToProto(b, true));  // data = e, diff = v
+    WriteFileBytes(SnapshotFilename(".faultstate"), SerializeBlobProtoVector(fs));
+  }
+  return state;
+}
+
+template <typename Dtype>
+void Solver<Dtype>::Restore(const std::string& state_file) {
+  CAFFE_CHECK(state_file.size() < 3 || state_file.compare(state_file.size() - 3, 3, ".h5") != 0,
+              "HDF5 solver states are not supported by this build: " << state_file);
+  const SolverStateData st = ParseSolverState(ReadFileBytes(state_file));
+  iter_ = st.iter;
+  if (!st.learned_net.empty()) net_->CopyTrainedLayersFrom(st.learned_net);
+  current_step_ = st.current_step;
+  CAFFE_CHECK(st.history.size() == history_.size(), "Incorrect length of history blobs.");
+  for (size_t i = 0; i < history_.size(); ++i) {
+    CAFFE_CHECK(ShapeEquals(history_[i]->shape(), st.history[i]), "history blob " << i << ": shape mismatch");
+    BlobFromProto(history_[i].get(), st.history[i]);
+  }
+  const std::string suffix = ".solverstate";
+  if (fmaker_ && state_file.size() > suffix.size() &&
+      state_file.compare(state_file.size() - suffix.size(), suffix.size(), suffix) == 0) {
+    const std::string fpath = state_file.substr(0, state_file.size() - suffix.size()) + ".faultstate";
+    std::ifstream probe(fpath, std::ios::binary);
+    if (probe.good()) {
+      const auto fs = ParseBlobProtoVector(ReadFileBytes(fpath));
+      auto fi = fmaker_->fail_iterations();
+      CAFFE_CHECK(fs.size() == fi.size(), "fault state: " << fs.size() << " blobs, net has " << fi.size());
+      for (size_t i = 0; i < fi.size(); ++i) {
+        CAFFE_CHECK(ShapeEquals(fi[i]->shape(), fs[i]) && !fs[i].diff.empty(), "fault state blob " << i << ": mismatch");
+        BlobFromProto(fi[i], fs[i]);
+      }
+      emit("Restored fault state from " + fpath);
+    }
+  }
 }
 
 template <typename Dtype>

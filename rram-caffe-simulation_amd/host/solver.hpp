@@ -90,6 +90,73 @@ class ThresholdFailureStrategy : public FailureStrategy<Dtype> {
   bool reference_lr_index = false;
 };
 
+// glibc rand()/random() (TYPE_3 additive feedback generator of srandom_r /
+// random_r): the reference's genetic strategy draws with unseeded rand()
+// (strategy.cpp:170-175, Appendix A Q9), i.e. this generator at seed 1.
+class GlibcRand {
+ public:
+  explicit GlibcRand(uint32_t seed = 1);
+  int operator()();  // in [0, RAND_MAX = 2^31 - 1]
+
+ private:
+  uint32_t r_[34];
+  int i_ = 0;  // ring position of r[k - 34]
+};
+
+// strategy.hpp:84-142 / strategy.cpp:35-137.  Every `period` iterations after
+// `start`, the FC neurons are re-ordered so that the neurons the pretrained
+// prune order ranks most prunable land on the physical neurons with the most
+// stuck-at-zero cells.  Counts on the device, sort on the host (std::sort with
+// the reference comparator, so ties resolve identically), moves as gathers.
+// rram_reference_compat: true reproduces Appendix A Q8 (bias rows copied from
+// the weight array, strategy.cpp:118-119).
+template <typename Dtype>
+class RemappingFailureStrategy : public FailureStrategy<Dtype> {
+ public:
+  RemappingFailureStrategy(const Msg& param, std::shared_ptr<FailureMaker<Dtype>> fm, std::shared_ptr<Net<Dtype>> net,
+                           const Solver<Dtype>* solver);
+  void Apply() override;
+  const char* type() const override { return "remapping"; }
+  // orders[i-1] for FC pair (i-1, i): neuron indices of FC layer i-1 sorted
+  // by (#flagged cells in its input row + #flagged cells in its output column)
+  std::vector<std::vector<int>> SortFCNeurons();
+  const std::vector<std::vector<int>>& prune_orders() const { return prune_orders_; }
+  bool reference_compat = false;
+
+ private:
+  int period_ = 100, start_ = 0, times_ = 0;
+  std::vector<std::vector<int>> prune_orders_;
+};
+
+// strategy.hpp:144-183 / strategy.cpp:139-288.  Random pairwise neuron swaps
+// accepted when they move failed cells onto weights the prune net marks as
+// prunable.  The decisions only read the fault state and the prune masks, so
+// they run on host copies; the accepted swaps compose into one permutation
+// per FC blob, applied on the device in one gather per array.
+// rram_reference_compat: true reproduces Q9's flat prune_input[n1]/[n2] swap
+// (strategy.cpp:265-267); rram_rand_seed (default 1 = glibc's unseeded rand).
+template <typename Dtype>
+class GeneticFailureStrategy : public FailureStrategy<Dtype> {
+ public:
+  GeneticFailureStrategy(const Msg& param, std::shared_ptr<FailureMaker<Dtype>> fm, std::shared_ptr<Net<Dtype>> net,
+                         const Solver<Dtype>* solver);
+  void Apply() override;
+  const char* type() const override { return "genetic"; }
+  int CalculateOverallDist();
+  int last_before() const { return before_; }
+  int last_after() const { return after_; }
+  int last_accepted() const { return accepted_; }
+  bool reference_compat = false;
+
+ private:
+  void FetchEndurance();
+  int switch_time_ = 100, period_ = 100, start_ = 0, times_ = 0;
+  int before_ = 0, after_ = 0, accepted_ = 0;
+  GlibcRand rand_;
+  std::vector<std::vector<float>> prune_;  // prune net failure params (host, mutated by swaps)
+  std::vector<std::vector<float>> endur_;     // endurance of every failure param (host copy per Apply)
+};
+
 template <typename Dtype>
 class Solver {
  public:
@@ -100,7 +167,20 @@ class Solver {
   virtual ~Solver() = default;
 
   void Step(int iters);
-  void Solve();
+  // solver.cpp:328-370; resume_file: a .solverstate to Restore() first
+  void Solve(const char* resume_file = nullptr);
+  // solver.cpp:461-518 (BINARYPROTO): <prefix>_iter_N.caffemodel and
+  // .solverstate, plus <prefix>_iter_N.faultstate with the fault maps
+  // (Appendix A Q11: the reference redraws them on resume).  Returns the
+  // .solverstate path.
+  std::string Snapshot();
+  // sgd_solver.cpp:309-326; the fault maps come back too when the matching
+  // .faultstate file exists
+  void Restore(const std::string& state_file);
+  const Msg& net_options() const { return options_; }
+  void emit_log(const std::string& s) const {
+    if (log) log(s);
+  }
   // returns the mean of every output element of test net `id` over test_iter
   std::vector<Dtype> Test(int id = 0);
   std::vector<std::vector<Dtype>> TestAll();
@@ -134,7 +214,12 @@ class Solver {
     if (log) log(s);
   }
 
+  std::string SnapshotFilename(const std::string& ext) const {
+    return param_.str("snapshot_prefix") + "_iter_" + std::to_string(iter_) + ext;
+  }
+
   Msg param_;
+  Msg options_;
   std::shared_ptr<Net<Dtype>> net_;
   std::vector<std::shared_ptr<Net<Dtype>>> test_nets_;
   std::vector<std::unique_ptr<Blob<Dtype>>> history_, temp_;

@@ -69,6 +69,10 @@ SIGNATURES = {
     "rram_inject_rng": (I, [P, P, I64, P, U64, U32, U32, P, P]),
     "rram_inject_rng_batched": (I, [P, I, U64, U32, P, P]),
     "rram_threshold_strategy": (I, [P, I64, F, P, P]),
+    "rram_stuck_zero_counts": (I, [P, P, I, I, P, P, P]),
+    "rram_permute_rows": (I, [P, P, I64, P, P, I, P]),
+    "rram_permute_cols": (I, [P, P, I, I, P, P, I, P]),
+    "rram_permute_elems": (I, [P, P, P, P, I, P]),
     "rram_sgd_update": (I, [P, P, I64, F, F, P]),
     "rram_fused_update_fail": (I, [P, P, P, P, P, I64, F, F, F, I, F, F, F, P, P]),
     "rram_axpy": (I, [I64, F, P, P, P]),

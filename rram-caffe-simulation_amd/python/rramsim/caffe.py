@@ -64,6 +64,16 @@ SIGNATURES = {
     "rram_solver_num_fail_blobs": (I, [P, PI]),
     "rram_solver_fail_state": (I, [P, I, PP, PP, PI64]),
     "rram_solver_broken_counts": (I, [P, C.POINTER(C.c_ulonglong), I, PI]),
+    "rram_solver_apply_strategies": (I, [P]),
+    "rram_solver_strategy_info": (I, [P, I, C.c_char_p, I, PI, PI, PI]),
+    "rram_solver_snapshot": (I, [P, C.c_char_p, I]),
+    "rram_solver_restore": (I, [P, C.c_char_p]),
+    "rram_solver_solve_from": (I, [P, C.c_char_p]),
+    "rram_net_copy_trained_layers_from": (I, [P, C.c_char_p]),
+    "rram_net_save_weights": (I, [P, C.c_char_p, I]),
+    "rram_caffemodel_describe": (I, [C.c_char_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "rram_proto_rewrite": (I, [C.c_char_p, C.c_char_p, I]),
+    "rram_glibc_rand": (I, [U32, I, PI]),
     "rram_mc_create": (I, [P, P, I, U64, I, PP]),
     "rram_mc_destroy": (I, [P]),
     "rram_mc_run": (I, [P, U32, U32]),
@@ -138,6 +148,35 @@ def describe(prototxt: str, phase: str = "test") -> List[tuple]:
         name, typ, bots, tops = line.split("\t")
         out.append((name, typ, [b for b in bots.split(",") if b], [t for t in tops.split(",") if t]))
     return out
+
+
+def caffemodel_describe(path: str) -> List[tuple]:
+    """Host-only: [(layer, type, blob_index, shape, count, data_sum, diff_count)]
+    of a binary .caffemodel (NetParameter `layer` or V1 `layers`)."""
+    lib = load()
+    need = C.c_size_t()
+    check(lib.rram_caffemodel_describe(str(path).encode(), None, 0, C.byref(need)), "caffemodel_describe")
+    buf = C.create_string_buffer(need.value)
+    check(lib.rram_caffemodel_describe(str(path).encode(), buf, need.value, None), "caffemodel_describe")
+    out = []
+    for line in buf.value.decode().splitlines():
+        name, typ, idx, shape, n, dsum, ndiff = line.split("\t")
+        out.append((name, typ, -1 if idx == "-" else int(idx), tuple(int(x) for x in shape.split(",") if x),
+                    int(n), float(dsum), int(ndiff)))
+    return out
+
+
+def proto_rewrite(src: str, dst: str, kind: str = "net"):
+    """Host-only: parse a binary proto and serialise it again (net | solverstate | blobs)."""
+    k = {"net": 0, "solverstate": 1, "blobs": 2}[kind]
+    check(load().rram_proto_rewrite(str(src).encode(), str(dst).encode(), k), "proto_rewrite")
+
+
+def glibc_rand(seed: int, n: int) -> List[int]:
+    """Host-only: n draws of the genetic strategy's glibc rand() after srand(seed)."""
+    buf = (C.c_int * max(n, 1))()
+    check(load().rram_glibc_rand(seed, n, buf), "glibc_rand")
+    return [buf[i] for i in range(n)]
 
 
 def _wrap_device(ptr: int, shape):
@@ -271,6 +310,14 @@ class Net:
     def share_trained_with(self, other: "Net"):
         check(self._lib.rram_net_share_trained(self.h, other.h), "share_trained")
 
+    def copy_from(self, caffemodel: str):
+        """Net::CopyTrainedLayersFrom (binary .caffemodel)."""
+        check(self._lib.rram_net_copy_trained_layers_from(self.h, str(caffemodel).encode()), "copy_trained_layers_from")
+
+    def save(self, caffemodel: str, write_diff: bool = False):
+        """Net::ToProto + WriteProtoToBinaryFile."""
+        check(self._lib.rram_net_save_weights(self.h, str(caffemodel).encode(), int(write_diff)), "save_weights")
+
     def flat_param_count(self) -> int:
         n = C.c_int64()
         check(self._lib.rram_net_flat_param_count(self.h, C.byref(n)), "flat_param_count")
@@ -345,8 +392,29 @@ class Solver:
     def step(self, iters: int):
         check(self._lib.rram_solver_step(self.h, iters), "step")
 
-    def solve(self):
-        check(self._lib.rram_solver_solve(self.h), "solve")
+    def solve(self, resume_file: Optional[str] = None):
+        if resume_file is None:
+            check(self._lib.rram_solver_solve(self.h), "solve")
+        else:
+            check(self._lib.rram_solver_solve_from(self.h, str(resume_file).encode()), "solve")
+
+    def snapshot(self) -> str:
+        buf = C.create_string_buffer(4096)
+        check(self._lib.rram_solver_snapshot(self.h, buf, 4096), "snapshot")
+        return buf.value.decode()
+
+    def restore(self, state_file: str):
+        check(self._lib.rram_solver_restore(self.h, str(state_file).encode()), "restore")
+
+    def apply_strategies(self):
+        check(self._lib.rram_solver_apply_strategies(self.h), "apply_strategies")
+
+    def strategy_info(self, i=0):
+        t = C.create_string_buffer(64)
+        a, b, c = C.c_int(), C.c_int(), C.c_int()
+        check(self._lib.rram_solver_strategy_info(self.h, i, t, 64, C.byref(a), C.byref(b), C.byref(c)),
+              "strategy_info")
+        return t.value.decode(), a.value, b.value, c.value
 
     def test(self, i=0) -> List[float]:
         buf = (C.c_float * 1024)()

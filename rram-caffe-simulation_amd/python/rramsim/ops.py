@@ -83,6 +83,28 @@ def inject_batched(segs, seed, map_id, counters_t=None):
                                            _stream()), "inject_rng_batched")
 
 
+def stuck_zero_counts(e, v, rows, cols, row_counts, col_counts):
+    """row_counts[r] = #(e<0 & v==0) in row r; col_counts[c] += same per column (int32 tensors)."""
+    _f32(e, "endurance")
+    _f32(v, "values")
+    K.check(_lib().rram_stuck_zero_counts(_p(e), _p(v), rows, cols, _p(row_counts), _p(col_counts), _stream()),
+            "stuck_zero_counts")
+
+
+def permute_rows(src, dst, row_len, to, frm):
+    K.check(_lib().rram_permute_rows(_p(src), _p(dst), row_len, _p(to), _p(frm), to.numel(), _stream()),
+            "permute_rows")
+
+
+def permute_cols(src, dst, rows, cols, to, frm):
+    K.check(_lib().rram_permute_cols(_p(src), _p(dst), rows, cols, _p(to), _p(frm), to.numel(), _stream()),
+            "permute_cols")
+
+
+def permute_elems(src, dst, to, frm):
+    K.check(_lib().rram_permute_elems(_p(src), _p(dst), _p(to), _p(frm), to.numel(), _stream()), "permute_elems")
+
+
 def threshold_strategy(dw, thr, counter=None):
     _f32(dw, "dw")
     K.check(_lib().rram_threshold_strategy(_p(dw), dw.numel(), thr, _p(counter), _stream()),
