@@ -18,6 +18,11 @@
 // receives a contiguous run of tiles that share operand panels.
 #include <stdlib.h>
 
+#include <array>
+#include <map>
+#include <mutex>
+#include <vector>
+
 #include "rram_common.hpp"
 
 namespace rram {
@@ -33,7 +38,9 @@ template <int KB>
 constexpr int ldk_of() { return KB + 4; }
 
 // KCV = KC with 16-byte global loads (row stride, base and K all multiples of 4 floats)
-enum Mode : int { KC = 0, RC = 1, CONV = 2, NCHW = 3, NCHWT = 4, KCV = 5 };
+// CONVT = CONV with a per-k offset/tap table (conv_table below) read by scalar
+// loads: no (c, kh, kw) stepping and no multiplies in the gather.
+enum Mode : int { KC = 0, RC = 1, CONV = 2, NCHW = 3, NCHWT = 4, KCV = 5, CONVT = 6 };
 enum OutMode : int { OUT_ROWMAJOR = 0, OUT_NCHW = 1 };
 
 // Fast unsigned division by a runtime constant (x < 2^31).
@@ -73,6 +80,8 @@ struct ConvGeom {
   FastDiv khkw, kw_div, howo, wo_div;
   int64_t chw;  // image stride of the input (C*H*W)
   int in_bytes; // bytes addressable from the group's input base (buffer range)
+  const int2* tbl;  // CONVT: per k {4*(c*H*W + kh*dh*W + kw*dw), tap}; tap 31 = never valid
+  int taps;         // CONVT: kh*kw taps tracked in the per-column validity mask (0: pad-free)
 };
 
 struct Epi {
@@ -106,6 +115,7 @@ struct ConvCol {
   bool valid;
   int pbase;     // n*C*H*W + hb*W + wb (element offset inside the group's input)
   __amdgpu_buffer_rsrc_t rsrc;  // raw buffer over the group's input (OOB loads return 0)
+  uint32_t bad;  // CONVT: bit t set = tap t of this column reads padding (bit 31 always set)
 };
 
 template <int ROWS, int KB>
@@ -181,6 +191,27 @@ __device__ __forceinline__ void load_tile(Loader<ROWS, KB>& L, const View& vw, c
     }
     return;
   }
+  if (MODE == CONVT) {
+    // implicit im2col from the table: thread = one output position x EPT
+    // consecutive k; the k segment is wave-uniform, so each table entry is a
+    // scalar load, and per element the VALU does one add, one bit extract
+    // (0 or -1: this column's tap reads padding / k past K) and one or that
+    // turns the offset into an out-of-range one (the buffer load returns 0).
+    const int seg = threadIdx.x / ROWS;
+    const int ks = __builtin_amdgcn_readfirstlane(k0 + seg * EPT);
+    const int2* te = cv.tbl + ks;
+    // descriptor rebuilt here from uniform values so it provably lives in SGPRs
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(vw.p), 0, cv.in_bytes, 0x00020000);
+    const uint32_t pb4 = static_cast<uint32_t>(col.pbase) * 4u;
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int2 t = te[i];
+      const uint32_t bad = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(col.bad), t.y, 1));
+      L.v[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, (pb4 + static_cast<uint32_t>(t.x)) | bad, 0, 0));
+    }
+    return;
+  }
   if (MODE == CONV) {
     // implicit im2col: thread = one output position (row) x EPT consecutive k.
     // The k segment start is wave-uniform (ROWS >= 64), so (c, kh, kw) is
@@ -249,7 +280,7 @@ template <int MODE, int ROWS, int KB>
 __device__ __forceinline__ void store_tile(const Loader<ROWS, KB>& L, float* lds) {
   constexpr int EPT = Loader<ROWS, KB>::EPT;
   constexpr int LDK = ldk_of<KB>();
-  if (MODE == CONV) {
+  if (MODE == CONV || MODE == CONVT) {
     // EPT consecutive k of one row: 16-byte LDS writes (row stride 36 dwords
     // puts the 8 lanes of a ds_write_b128 group on distinct bank quads)
     float* dst = lds + (threadIdx.x % ROWS) * LDK + (threadIdx.x / ROWS) * EPT;
@@ -305,9 +336,12 @@ __global__ void __launch_bounds__(256) k_gemm(Params P) {
   const int xcd = bid & 7, loc = bid >> 3;
   const int q8 = nwg >> 3, r8 = nwg & 7;
   const int tid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
-  const int tm = tid % P.tiles_m;
-  const int tn = (tid / P.tiles_m) % P.tiles_n;
-  const int z = tid / (P.tiles_m * P.tiles_n);
+  // integer division by a runtime divisor is expanded on the VALU; pin the
+  // (block-uniform) results to SGPRs so the operand pointers and the buffer
+  // descriptor derived from them stay scalar
+  const int tm = __builtin_amdgcn_readfirstlane(tid % P.tiles_m);
+  const int tn = __builtin_amdgcn_readfirstlane((tid / P.tiles_m) % P.tiles_n);
+  const int z = __builtin_amdgcn_readfirstlane(tid / (P.tiles_m * P.tiles_n));
   const int n0 = tn * BNr;
   const int m0 = tm * BMr;
 
@@ -328,7 +362,7 @@ __global__ void __launch_bounds__(256) k_gemm(Params P) {
 
   // CONV column precompute (B operand rows = output positions; fixed per thread)
   ConvCol col{0, 0, 0, false};
-  if (BMODE == CONV) {
+  if (BMODE == CONV || BMODE == CONVT) {
     int r, kk;
     tile_coord<CONV, BNr, KB>(threadIdx.x, r, kk);
     const int p = n0 + r;
@@ -342,6 +376,21 @@ __global__ void __launch_bounds__(256) k_gemm(Params P) {
       col.wb = static_cast<int>(wo) * P.cv.sw - P.cv.pw;
       col.valid = true;
       col.pbase = static_cast<int>(col.base) + col.hb * P.cv.W + col.wb;
+    }
+    if (BMODE == CONVT) {
+      // validity of every kernel tap for this column, once per block
+      uint32_t good = 0;
+      if (P.cv.taps == 0) {
+        good = col.valid ? 1u : 0u;  // pad-free: every tap is inside the image
+      } else if (col.valid) {
+        for (int t = 0; t < P.cv.taps; ++t) {
+          const int kh = t / P.cv.KW, kw = t - kh * P.cv.KW;
+          good |= static_cast<uint32_t>(static_cast<unsigned>(col.hb + kh * P.cv.dh) < static_cast<unsigned>(P.cv.H) &&
+                                        static_cast<unsigned>(col.wb + kw * P.cv.dw) < static_cast<unsigned>(P.cv.W))
+                  << t;
+        }
+      }
+      col.bad = ~good | 0x80000000u;
     }
     // group base pointer, range = the whole remaining input (host checks < 2^32 bytes)
     col.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(vb.p), 0, P.cv.in_bytes, 0x00020000);
@@ -622,6 +671,10 @@ int dispatch(int am, int bm, int om, const Params& P, int gz, hipStream_t s, boo
     if (am == KC) return launch<KC, CONV, OUT_NCHW, 16>(P, gz, s, force_big);
     if (am == KCV) return launch<KCV, CONV, OUT_NCHW, 16>(P, gz, s, force_big);
   }
+  if (bm == CONVT && om == OUT_NCHW && conv_kb() == 16) {
+    if (am == KC) return launch<KC, CONVT, OUT_NCHW, 16>(P, gz, s, force_big);
+    if (am == KCV) return launch<KCV, CONVT, OUT_NCHW, 16>(P, gz, s, force_big);
+  }
 #define RRAM_D(A_, B_, O_) \
   if (am == A_ && bm == B_ && om == O_) return launch<A_, B_, O_, 32>(P, gz, s, force_big);
   RRAM_D(KC, KC, OUT_ROWMAJOR)
@@ -635,6 +688,8 @@ int dispatch(int am, int bm, int om, const Params& P, int gz, hipStream_t s, boo
   RRAM_D(RC, RC, OUT_ROWMAJOR)
   RRAM_D(KC, CONV, OUT_NCHW)
   RRAM_D(KCV, CONV, OUT_NCHW)
+  RRAM_D(KC, CONVT, OUT_NCHW)
+  RRAM_D(KCV, CONVT, OUT_NCHW)
   RRAM_D(NCHW, KC, OUT_ROWMAJOR)
   RRAM_D(NCHW, KCV, OUT_ROWMAJOR)
   RRAM_D(RC, NCHWT, OUT_ROWMAJOR)
@@ -672,6 +727,38 @@ View make_view(const float* p, int64_t ld, int rows, int kdim) {
   v.kdim = kdim;
   v.hw = make_fastdiv(1);
   return v;
+}
+
+// Per-geometry gather table of the CONVT loader, built once per process and
+// cached (a few KB per conv geometry; never freed).  Entry k < K holds the
+// input offset of reduction index k = (c, kh, kw) in bytes and its tap
+// kh*KW + kw (0 for pad-free convolutions, whose taps are always inside the
+// image); entries past K (the last tile's tail and the one-tile prefetch
+// overrun) hold tap 31, which no column marks valid.
+const int2* conv_table(const ConvGeom& cv, int K, bool padded, hipStream_t s) {
+  static std::mutex mu;
+  static std::map<std::array<int, 9>, int2*> cache;
+  const std::array<int, 9> key{cv.C, cv.H, cv.W, cv.KH, cv.KW, cv.dh, cv.dw, padded ? 1 : 0, K};
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  const int len = (K + BK - 1) / BK * BK + 2 * BK;
+  std::vector<int2> h(len, int2{0, 31});
+  for (int k = 0; k < K; ++k) {
+    const int c = k / (cv.KH * cv.KW), r = k % (cv.KH * cv.KW);
+    const int kh = r / cv.KW, kw = r % cv.KW;
+    h[k].x = 4 * (c * cv.H * cv.W + kh * cv.dh * cv.W + kw * cv.dw);
+    h[k].y = padded ? r : 0;
+  }
+  int2* d = nullptr;
+  if (hipMalloc(&d, len * sizeof(int2)) != hipSuccess) return nullptr;
+  if (hipMemcpyAsync(d, h.data(), len * sizeof(int2), hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess) {
+    (void)hipFree(d);
+    return nullptr;
+  }
+  cache[key] = d;
+  return d;
 }
 
 }  // namespace
@@ -769,7 +856,16 @@ int conv_fwd_core(const rram_conv_desc* d, const float* x, const float* w, const
   P.grp_b = (int64_t)cin_g * d->height * d->width;
   P.grp_c = (int64_t)cout_g * HoWo;
   P.grp_bias = cout_g;
-  return dispatch(vec_ok(w, K, K, P.grp_a) ? KCV : KC, CONV, OUT_NCHW, P, g, s);
+  // table-driven gather when the taps fit the 31-bit validity mask (or no padding)
+  const bool padded = d->pad_h > 0 || d->pad_w > 0;
+  int bmode = CONV;
+  if (getenv("RRAM_CONV_NO_TABLE") == nullptr && (!padded || d->kernel_h * d->kernel_w <= 31) &&
+      (int64_t)cin_g * d->height * d->width * 4 < (1ll << 31)) {
+    cv.tbl = conv_table(cv, K, padded, s);
+    cv.taps = padded ? d->kernel_h * d->kernel_w : 0;
+    if (cv.tbl) bmode = CONVT;
+  }
+  return dispatch(vec_ok(w, K, K, P.grp_a) ? KCV : KC, bmode, OUT_NCHW, P, g, s);
 }
 
 // dW_g[co][k] += sum_p dY_g[co][p] col_g[k][p]   (col: [Cin*kh*kw][ldcol])
