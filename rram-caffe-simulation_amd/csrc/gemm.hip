@@ -632,6 +632,12 @@ int launch_cfg(Params P, int gz, hipStream_t s) {
 template <int AM, int BMODE, int OM, int KB>
 int launch(const Params& P, int gz, hipStream_t s, bool force_big) {
   if (force_big) return launch_cfg<2, 2, 2, 2, AM, BMODE, OM, KB>(P, gz, s);
+  // tuning knob: RRAM_GEMM_TILE = 64 | 96 | 128 | 192 forces BM (BN = 128), 6464 the 64x64 tile
+  static const int forced = [] {
+    const char* e = getenv("RRAM_GEMM_TILE");
+    return e ? atoi(e) : 0;
+  }();
+  if (forced == 6464) return launch_cfg<2, 2, 1, 1, AM, BMODE, OM, KB>(P, gz, s);
   const int64_t ntn = (P.N + 127) / 128;
   const int cands[4] = {128, 192, 96, 64};  // ties keep 128 (2 blocks per CU)
   int best = 0;
@@ -645,7 +651,10 @@ int launch(const Params& P, int gz, hipStream_t s, bool force_big) {
       best_pad = pad;
     }
   }
-  if (best == 64 && ntn * ((P.M + 63) / 64) * gz < 256)
+  if (KB == 16 && !forced && P.M % 128 != 0 && P.M % 64 == 0 && ntn * (P.M / 64) * gz >= 512)
+    best = 64;  // e.g. M = 192: three unpadded 64-row tiles beat one 192-row tile at KB = 16
+  if (forced == 64 || forced == 96 || forced == 128 || forced == 192) best = forced;
+  else if (best == 64 && ntn * ((P.M + 63) / 64) * gz < 256)
     return launch_cfg<2, 2, 1, 1, AM, BMODE, OM, KB>(P, gz, s);  // 64 x 64: twice the blocks
   switch (best) {
     case 192: return launch_cfg<2, 2, 3, 2, AM, BMODE, OM, KB>(P, gz, s);  // 192 x 128
@@ -658,20 +667,24 @@ int launch(const Params& P, int gz, hipStream_t s, bool force_big) {
 }
 
 // K-tile depth of the implicit-GEMM convolution (tuning knob RRAM_GEMM_KB = 16 | 32)
-int conv_kb() {
-  static const int kb = [] {
+// Measured on MI355X (scripts/gpu_sweep.sh, AlexNet b256): K >= 1024 runs
+// faster with 16-deep K-tiles (half the LDS and loader registers: 3 waves per
+// SIMD instead of 2), short K (conv1, K = 363) with 32.
+int conv_kb(int K) {
+  static const int forced = [] {
     const char* e = getenv("RRAM_GEMM_KB");
-    return (e && atoi(e) == 16) ? 16 : 32;
+    return e ? atoi(e) : 0;
   }();
-  return kb;
+  if (forced == 16 || forced == 32) return forced;
+  return K >= 1024 ? 16 : 32;
 }
 
 int dispatch(int am, int bm, int om, const Params& P, int gz, hipStream_t s, bool force_big = false) {
-  if (bm == CONV && om == OUT_NCHW && conv_kb() == 16) {
+  if (bm == CONV && om == OUT_NCHW && conv_kb(P.K) == 16) {
     if (am == KC) return launch<KC, CONV, OUT_NCHW, 16>(P, gz, s, force_big);
     if (am == KCV) return launch<KCV, CONV, OUT_NCHW, 16>(P, gz, s, force_big);
   }
-  if (bm == CONVT && om == OUT_NCHW && conv_kb() == 16) {
+  if (bm == CONVT && om == OUT_NCHW && conv_kb(P.K) == 16) {
     if (am == KC) return launch<KC, CONVT, OUT_NCHW, 16>(P, gz, s, force_big);
     if (am == KCV) return launch<KCV, CONVT, OUT_NCHW, 16>(P, gz, s, force_big);
   }
