@@ -11,85 +11,132 @@ namespace {
 
 // LRN ACROSS_CHANNELS followed by MAX pooling with a K x K window.
 //
-// One thread per pooled (n, ph, pw) walks the channels.  For each of the K*K
-// input positions of its window it keeps the SIZE-channel ring of x and the
-// running sum of squares, updated exactly as k_lrn_fwd_slide / LRNFillScale
+// Block = one image x a band of RB pooled rows; it walks all channels once.
+// Per channel, every thread produces the LRN value of up to PPT input pixels of
+// the band (the band's input rows are contiguous in memory, so the loads are
+// coalesced), keeping for each pixel the SIZE-channel ring of x and the running
+// sum of squares, updated exactly as k_lrn_fwd_slide / LRNFillScale
 // (lrn_layer.cu:9-51: add the channel entering the window, then subtract the
 // one leaving it), so each LRN value x * (k + alpha/size * sum)^-beta
-// (lrn_layer.cu:72-78) is the unfused kernel's bit for bit.  The max over the
-// window follows MaxPoolForward (pooling_layer.cu:11-47): window clipped to
-// the image, -FLT_MAX start, strict ">" in row-major order.
-// HBM traffic: x read once (neighbouring windows overlap in L2), y written once;
-// the LRN output (the pool's bottom) is never materialised.
-template <int K, int SIZE>
+// (lrn_layer.cu:72-78) is the unfused kernel's bit for bit.  The values go to
+// an LDS plane (double-buffered: one barrier per channel) from which the
+// band's pooled outputs take the max over their window exactly as
+// MaxPoolForward (pooling_layer.cu:11-47): window clipped to the image,
+// -FLT_MAX start, strict ">" in row-major order.
+// HBM traffic: x read once (plus the one shared input row between adjacent
+// bands), y written once; the LRN output never leaves the CU.
+constexpr int kBandPix = 512;  // input pixels per band (PPT = 2 per thread)
+
+// G channels per barrier; the loads run one group ahead.  Measured on MI355X
+// (AlexNet b256): G = 2 for norm1 (55 x 55 planes), G = 4 for norm2 (27 x 27).
+template <int K, int SIZE, int G>
 __global__ void __launch_bounds__(256)
-    k_lrn_maxpool(const float* __restrict__ x, float* __restrict__ y, int num, int C, int H, int W,
-                  int PH, int PW, int sh, int sw, int ph, int pw, float alpha_over_size, float beta,
-                  float k) {
+    k_lrn_maxpool_band(const float* __restrict__ x, float* __restrict__ y, int C, int H, int W, int PH, int PW,
+                       int sh, int sw, int ph, int pw, int RB, float alpha_over_size, float beta, float k) {
   constexpr int PRE = (SIZE - 1) / 2, POST = SIZE - PRE - 1;
-  constexpr int P = K * K;
-  constexpr int D = 4;  // channels loaded ahead per step (D * P loads in flight)
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= num * PH * PW) return;
-  const int pwi = idx % PW;
-  const int phi = (idx / PW) % PH;
-  const int n = idx / (PW * PH);
-  const int hs = phi * sh - ph, ws = pwi * sw - pw;
+  constexpr int D = G;
+  constexpr int R = SIZE + 2 * D;  // ring: the SIZE-window, this group's D new channels, the next group's
+  constexpr int PPT = kBandPix / 256;
+  __shared__ float ybuf[2][D][kBandPix];
+  const int n = blockIdx.y;
+  const int pr0 = blockIdx.x * RB;
+  const int pr1 = min(PH, pr0 + RB);
+  const int h0 = max(0, pr0 * sh - ph);
+  const int h1 = min(H, (pr1 - 1) * sh - ph + K);  // exclusive
+  const int NP = (h1 - h0) * W;
   const int HW = H * W;
-  const float* xn = x + (int64_t)n * C * HW;
-  float* yn = y + (int64_t)n * C * PH * PW + phi * PW + pwi;
-  int off[P];
-  bool ok[P];
+  const float* xb = x + (int64_t)n * C * HW + (int64_t)h0 * W;
+  int pix[PPT];
+  bool own[PPT];
 #pragma unroll
-  for (int a = 0; a < K; ++a)
-#pragma unroll
-    for (int b = 0; b < K; ++b) {
-      const int h = hs + a, w = ws + b;
-      ok[a * K + b] = static_cast<unsigned>(h) < static_cast<unsigned>(H) &&
-                      static_cast<unsigned>(w) < static_cast<unsigned>(W);
-      off[a * K + b] = ok[a * K + b] ? h * W + w : 0;
-    }
-  // win[p][j] = x at channel (c - PRE + j), zero outside [0, C)
-  float win[P][SIZE + D];
-  float acc[P];
-#pragma unroll
-  for (int p = 0; p < P; ++p) {
-#pragma unroll
-    for (int j = 0; j < SIZE; ++j) {
-      const int cc = j - PRE;
-      win[p][j] = (cc >= 0 && cc < C && ok[p]) ? xn[(int64_t)cc * HW + off[p]] : 0.0f;
-    }
-    acc[p] = 0.0f;
-#pragma unroll
-    for (int j = PRE; j < SIZE; ++j) acc[p] = lrn_sq_add(acc[p], win[p][j]);
+  for (int q = 0; q < PPT; ++q) {
+    pix[q] = threadIdx.x + q * 256;
+    own[q] = pix[q] < NP;
   }
-  for (int c0 = 0; c0 < C; c0 += D) {
+  auto ld = [&](int q, int cc) { return (cc >= 0 && cc < C && own[q]) ? xb[(int64_t)cc * HW + pix[q]] : 0.0f; };
+  // win[q][j] = x at channel (c0 - PRE + j) of pixel q, zero outside [0, C)
+  float win[PPT][R];
+  float acc[PPT];
+#pragma unroll
+  for (int q = 0; q < PPT; ++q) {
+#pragma unroll
+    for (int j = 0; j < SIZE + D; ++j) win[q][j] = ld(q, j - PRE);
+    acc[q] = 0.0f;
+#pragma unroll
+    for (int j = PRE; j < SIZE; ++j) acc[q] = lrn_sq_add(acc[q], win[q][j]);
+  }
+  const int NO = (pr1 - pr0) * PW;  // pooled outputs of the band per channel
+  const int64_t PHW = (int64_t)PH * PW;
+  float* yn = y + (int64_t)n * C * PHW;
+  // pooling items of a group: (channel d, output o), consecutive outputs of
+  // one channel on consecutive lanes (coalesced stores); each thread's items
+  // and their windows are fixed for the whole channel walk, so they are
+  // decoded once here: LDS base of the window, tap validity (the window
+  // clipped to the image), output offset
+  constexpr int MAXI = D;  // D * NO <= D * 256 items
+  int it_d[MAXI], it_l[MAXI], it_out[MAXI];
+  uint32_t it_ok[MAXI];
+#pragma unroll
+  for (int i = 0; i < MAXI; ++i) {
+    const int it = threadIdx.x + i * 256;
+    const int d = it / max(NO, 1), o = it - d * NO;
+    const int prl = o / PW, pwi = o - prl * PW;
+    const int hr = (pr0 + prl) * sh - ph, wr = pwi * sw - pw;
+    uint32_t ok = 0;
+#pragma unroll
+    for (int a = 0; a < K; ++a)
+#pragma unroll
+      for (int b = 0; b < K; ++b)
+        ok |= static_cast<uint32_t>(static_cast<unsigned>(hr + a) < static_cast<unsigned>(H) &&
+                                    static_cast<unsigned>(wr + b) < static_cast<unsigned>(W))
+              << (a * K + b);
+    it_d[i] = it < D * NO ? d : D;  // D = no item
+    it_l[i] = (hr - h0) * W + wr;
+    it_out[i] = (pr0 + prl) * PW + pwi;
+    it_ok[i] = ok;
+  }
+  for (int c0 = 0, g = 0; c0 < C; c0 += D, ++g) {
+    // next group's entering channels, in flight during this group's work
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+      for (int q = 0; q < PPT; ++q) win[q][SIZE + D + d] = ld(q, c0 + D + POST + 1 + d);
+    float(*yb)[kBandPix] = ybuf[g & 1];
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      const int cn = c0 + d + POST + 1;
 #pragma unroll
-      for (int p = 0; p < P; ++p)
-        win[p][SIZE + d] = (cn < C && ok[p]) ? xn[(int64_t)cn * HW + off[p]] : 0.0f;
+      for (int q = 0; q < PPT; ++q) {
+        // the helpers k_lrn_fwd_slide uses, in the same order
+        const float v = lrn_out(win[q][d + PRE], lrn_scale(acc[q], alpha_over_size, k), beta);
+        if (own[q]) yb[d][pix[q]] = v;
+        acc[q] = lrn_slide(acc[q], win[q][d + SIZE], win[q][d]);
+      }
     }
+    __syncthreads();
+    // pool the group's D channels (MaxPoolForward: -FLT_MAX start, strict ">"
+    // in row-major window order over the taps inside the image)
+    const int nd = min(D, C - c0);
 #pragma unroll
-    for (int d = 0; d < D; ++d) {
-      const int c = c0 + d;
-      if (c < C) {
+    for (int i = 0; i < MAXI; ++i) {
+      const int d = it_d[i];
+      if (d < nd) {
+        const float* yl = yb[d] + it_l[i];
         float mv = -FLT_MAX;
 #pragma unroll
-        for (int p = 0; p < P; ++p) {
-          // the helpers k_lrn_fwd_slide uses, in the same order
-          const float v = lrn_out(win[p][d + PRE], lrn_scale(acc[p], alpha_over_size, k), beta);
-          if (ok[p] && v > mv) mv = v;
-          acc[p] = lrn_slide(acc[p], win[p][d + SIZE], win[p][d]);
-        }
-        yn[(int64_t)c * PH * PW] = mv;
+        for (int a = 0; a < K; ++a)
+#pragma unroll
+          for (int b = 0; b < K; ++b) {
+            const bool ok = (it_ok[i] >> (a * K + b)) & 1u;
+            const float v = yl[ok ? a * W + b : -it_l[i]];  // masked taps read element 0
+            if (ok && v > mv) mv = v;
+          }
+        yn[(int64_t)(c0 + d) * PHW + it_out[i]] = mv;
       }
     }
 #pragma unroll
-    for (int p = 0; p < P; ++p)
+    for (int q = 0; q < PPT; ++q)
 #pragma unroll
-      for (int j = 0; j < SIZE; ++j) win[p][j] = win[p][j + D];
+      for (int j = 0; j < SIZE + D; ++j) win[q][j] = win[q][j + D];
   }
 }
 
@@ -109,17 +156,32 @@ int rram_lrn_maxpool_fwd(const float* x, float* y, int num, int C, int H, int W,
   RRAM_REQUIRE((kernel == 2 || kernel == 3) && (size == 3 || size == 5),
                "lrn_maxpool_fwd: supports kernel 2/3 and local_size 3/5 (got %d, %d)", kernel, size);
   RRAM_REQUIRE(ph < kernel && pw < kernel, "lrn_maxpool_fwd: pad must be < kernel");
-  const int64_t cols = (int64_t)num * PH * PW;
-  RRAM_REQUIRE((int64_t)num * C * H * W < 2147483647ll && cols * C < 2147483647ll,
+  RRAM_REQUIRE((int64_t)num * C * H * W < 2147483647ll && (int64_t)num * C * PH * PW < 2147483647ll,
                "lrn_maxpool_fwd: more than 2^31 elements is not supported");
-  if (cols == 0) return RRAM_OK;
+  if (num == 0) return RRAM_OK;
   RRAM_REQUIRE(x && y, "lrn_maxpool_fwd: NULL");
-  const dim3 grid(static_cast<unsigned>((cols + kThreads - 1) / kThreads));
+  // band height: input rows of RB pooled rows must fit the block's pixel
+  // budget and RB * PW outputs its threads; prefer >= 1024 blocks
+  auto fits = [&](int rb) {
+    const int rows = min(H, (rb - 1) * sh + kernel);
+    return rb * PW <= kThreads && rows * W <= kBandPix;
+  };
+  RRAM_REQUIRE(fits(1), "lrn_maxpool_fwd: a pooled row needs more than %d input pixels", kBandPix);
+  int rb = 1;
+  while (rb < PH && fits(rb + 1)) ++rb;
+  while (rb > 1 && (int64_t)num * ((PH + rb - 1) / rb) < 1024 && fits(rb - 1) && (rb - 1) * sh >= kernel) --rb;
+  const dim3 grid(static_cast<unsigned>((PH + rb - 1) / rb), static_cast<unsigned>(num));
   const float aos = alpha / size;
-#define RRAM_LP(K_, S_)                                                                                   \
-  if (kernel == K_ && size == S_)                                                                         \
-    hipLaunchKernelGGL((k_lrn_maxpool<K_, S_>), grid, dim3(kThreads), 0, as_stream(s), x, y, num, C, H, W, \
-                       PH, PW, sh, sw, ph, pw, aos, beta, k);
+  const bool big = H * W >= 1024;
+#define RRAM_LP(K_, S_)                                                                                     \
+  if (kernel == K_ && size == S_) {                                                                         \
+    if (big)                                                                                                \
+      hipLaunchKernelGGL((k_lrn_maxpool_band<K_, S_, 2>), grid, dim3(kThreads), 0, as_stream(s), x, y, C, H, \
+                         W, PH, PW, sh, sw, ph, pw, rb, aos, beta, k);                                      \
+    else                                                                                                    \
+      hipLaunchKernelGGL((k_lrn_maxpool_band<K_, S_, 4>), grid, dim3(kThreads), 0, as_stream(s), x, y, C, H, \
+                         W, PH, PW, sh, sw, ph, pw, rb, aos, beta, k);                                      \
+  }
   RRAM_LP(3, 5)
   else RRAM_LP(3, 3) else RRAM_LP(2, 5) else RRAM_LP(2, 3)
 #undef RRAM_LP

@@ -114,7 +114,8 @@ def test_lrn_across_fwd_bwd_vs_autograd(device, size):
 
 
 @pytest.mark.parametrize("size,k,s,p,C,H", [(5, 3, 2, 0, 13, 15), (5, 3, 2, 0, 96, 55), (3, 3, 2, 1, 7, 12),
-                                             (5, 2, 2, 0, 9, 10), (3, 3, 1, 0, 6, 8)])
+                                             (5, 2, 2, 0, 9, 10), (3, 3, 1, 0, 6, 8), (5, 3, 2, 0, 256, 27),
+                                             (5, 2, 1, 1, 5, 21), (3, 3, 3, 2, 4, 30)])
 def test_lrn_maxpool_fused_equals_unfused(device, size, k, s, p, C, H):
     """rram_lrn_maxpool_fwd == rram_lrn_fwd then rram_pool_fwd, bit for bit
     (same LRN arithmetic; window edges of the ceil rule), and the torch fp32
