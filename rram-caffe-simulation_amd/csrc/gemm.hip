@@ -420,6 +420,9 @@ __global__ void __launch_bounds__(256) k_gemm(Params P) {
   for (int t = 0; t < ntiles; ++t) {
     const int cur = t & 1;
     const bool more = (t + 1) < ntiles;
+#ifdef RRAM_V_PRIO
+    __builtin_amdgcn_s_setprio(1);
+#endif
     {
       // unconditional (no basic-block split): past the last tile every
       // element is out of range and the guarded loads return zeros
@@ -455,18 +458,27 @@ __global__ void __launch_bounds__(256) k_gemm(Params P) {
     }
     // Interleave the next tile's global loads with the first MFMAs (a wave
     // issues VALU / VMEM while its MFMAs run): one load, then NMF MFMAs.
+#ifndef RRAM_V_NOSCHED
     {
       constexpr int NVM = vmem_per_tile<AM, BMr, KB>() + vmem_per_tile<BMODE, BNr, KB>();
       constexpr int NMF_TOT = MI * NI * KB / 2;
+#ifdef RRAM_V_SPREAD
+      constexpr int NMF = NMF_TOT / NVM > 0 ? NMF_TOT / NVM : 1;
+#else
       constexpr int NMF = NMF_TOT / (2 * NVM) > 0 ? NMF_TOT / (2 * NVM) : 1;
+#endif
 #pragma unroll
       for (int v = 0; v < NVM; ++v) {
         __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);    // VMEM read
         __builtin_amdgcn_sched_group_barrier(0x008, NMF, 0);  // MFMA
       }
     }
+#endif
     // the LDS writes of the staged tile stay behind every MFMA
     __builtin_amdgcn_sched_barrier(0);
+#ifdef RRAM_V_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
     if (more) {
       store_tile<AM, BMr, KB>(la, As[cur ^ 1]);
       store_tile<BMODE, BNr, KB>(lb, Bs[cur ^ 1]);

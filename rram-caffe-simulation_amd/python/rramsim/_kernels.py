@@ -14,7 +14,9 @@ import os
 from pathlib import Path
 
 _PKG_ROOT = Path(__file__).resolve().parents[2]          # rram-caffe-simulation_amd/
-LIB_DIR = _PKG_ROOT / "lib"
+# RRAM_LIB_DIR: developer override to A/B kernel variants built into another
+# in-tree directory (scripts/gpu_variants.sh); the product loads lib/.
+LIB_DIR = Path(os.environ["RRAM_LIB_DIR"]) if os.environ.get("RRAM_LIB_DIR") else _PKG_ROOT / "lib"
 KERNELS_SO = LIB_DIR / "librram_kernels.so"
 CAFFE_SO = LIB_DIR / "librram_caffe.so"
 
