@@ -270,6 +270,14 @@ class MonteCarlo {
   std::vector<Blob<Dtype>*> params_;
   std::vector<Dtype*> clean_;
   std::vector<Blob<Dtype>*> outs_;
+  // injection overlap: map m's injection runs on side_ while the layers
+  // before the first faultable one run on the working stream; the faultable
+  // layers wait for it (ev_injected_), the next injection waits for the
+  // previous map's forward (ev_free_)
+  bool overlap_ = true;
+  int first_fault_layer_ = 0;
+  hipStream_t side_ = nullptr;
+  hipEvent_t ev_free_ = nullptr, ev_injected_ = nullptr;
   Dtype* d_sums_ = nullptr;       // [n_outputs]
   Dtype* d_per_map_ = nullptr;    // [max_maps][n_outputs]
   unsigned long long* d_broken_ = nullptr;

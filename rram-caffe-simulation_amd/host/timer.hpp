@@ -15,16 +15,17 @@ namespace caffe {
 class EventTimer {
  public:
   ~EventTimer() { clear(); }
-  void start(int key) {
+  // stream: where the timed work runs (nullptr = the working stream)
+  void start(int key, hipStream_t stream = nullptr) {
     hipEvent_t a = take(), b = take();
-    HIP_CALL(hipEventRecord(a, Caffe::hip_stream()));
+    HIP_CALL(hipEventRecord(a, stream ? stream : Caffe::hip_stream()));
     open_[key] = pending_.size();
     pending_.push_back({key, {a, b}});
   }
-  void stop(int key) {
+  void stop(int key, hipStream_t stream = nullptr) {
     auto it = open_.find(key);
     CAFFE_CHECK(it != open_.end(), "EventTimer::stop without start");
-    HIP_CALL(hipEventRecord(pending_[it->second].second.second, Caffe::hip_stream()));
+    HIP_CALL(hipEventRecord(pending_[it->second].second.second, stream ? stream : Caffe::hip_stream()));
     open_.erase(it);
   }
   // waits for all recorded intervals; adds them to totals() / counts()
