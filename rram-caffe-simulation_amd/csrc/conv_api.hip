@@ -10,7 +10,8 @@ int gemm_core(int trans_a, int trans_b, int M, int N, int K, float alpha, const 
 int conv_fwd_core(const rram_conv_desc* d, const float* x, const float* w, const float* bias,
                   float* y, int relu, hipStream_t s);
 int conv_bwd_weight_core(const rram_conv_desc* d, int nimg, const float* dy, const float* col,
-                         int64_t ldcol, float* dw, hipStream_t s);
+                         int64_t ldcol, float* dw, void* part, size_t part_bytes, hipStream_t s);
+int bwd_weight_split(int M, int N, int64_t K);
 int conv_bwd_data_col_core(const rram_conv_desc* d, int nimg, const float* w, const float* dy,
                            float* col, int64_t ldcol, hipStream_t s);
 int im2col_core(const float* im, int64_t im_img, int nimg, const rram_conv_desc* d, float* col,
@@ -32,16 +33,16 @@ __global__ void __launch_bounds__(256) k_bias_add(float* __restrict__ y, const f
   }
 }
 
-// db[c] += sum over (n, inner) of dy; one block per channel, deterministic.
+// db[c] += sum over (n, inner) of dy; one block per channel, deterministic
+// (fixed per-thread order, fixed tree); image-major walk, no divisions.
 __global__ void __launch_bounds__(256) k_bias_bwd(const float* __restrict__ dy, float* __restrict__ db,
                                                   int num, int C, int inner) {
   __shared__ float part[4];
   const int c = blockIdx.x;
   float s = 0.0f;
-  const int64_t per = (int64_t)num * inner;
-  for (int64_t j = threadIdx.x; j < per; j += blockDim.x) {
-    const int64_t n = j / inner, q = j - n * inner;
-    s += dy[(n * C + c) * inner + q];
+  for (int n = 0; n < num; ++n) {
+    const float* row = dy + ((int64_t)n * C + c) * inner;
+    for (int q = threadIdx.x; q < inner; q += blockDim.x) s += row[q];
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
@@ -115,11 +116,24 @@ int rram_conv2d_fwd(const rram_conv_desc* d_in, const float* x, const float* w, 
   return conv_fwd_core(&d, x, w, bias, y, relu, as_stream(s));
 }
 
+namespace {
+// split-K partial buffer of the weight gradient (conv_bwd_weight_core) for
+// chunks of `imgs` images
+size_t bwd_part_bytes(const rram_conv_desc& d, int imgs) {
+  const int M = d.num_output / d.group;
+  const int N = d.channels / d.group * d.kernel_h * d.kernel_w;
+  const int sp = bwd_weight_split(M, N, (int64_t)imgs * d.out_h * d.out_w);
+  return sp > 1 ? (size_t)sp * M * N * sizeof(float) : 0;
+}
+size_t col_bytes(const rram_conv_desc& d, int imgs) {
+  return (size_t)d.channels * d.kernel_h * d.kernel_w * (size_t)imgs * d.out_h * d.out_w * sizeof(float);
+}
+}  // namespace
+
 size_t rram_conv2d_bwd_workspace(const rram_conv_desc* d_in, int images_per_chunk) {
   rram_conv_desc d = *d_in;
   if (rram_conv_out_shape(&d) != RRAM_OK || images_per_chunk < 1) return 0;
-  return (size_t)d.channels * d.kernel_h * d.kernel_w * (size_t)images_per_chunk * d.out_h *
-         d.out_w * sizeof(float);
+  return col_bytes(d, images_per_chunk) + bwd_part_bytes(d, images_per_chunk);
 }
 
 int rram_conv2d_bwd(const rram_conv_desc* d_in, const float* x, const float* w, const float* dy,
@@ -139,12 +153,21 @@ int rram_conv2d_bwd(const rram_conv_desc* d_in, const float* x, const float* w, 
   }
   if (!dw && !dx) return RRAM_OK;
   RRAM_REQUIRE(x && w, "conv2d_bwd: x/w NULL");
-  const size_t per_img = rram_conv2d_bwd_workspace(&d, 1);
+  const size_t per_img = col_bytes(d, 1);
   RRAM_REQUIRE(ws != nullptr && ws_bytes >= per_img, "conv2d_bwd: workspace needs >= %zu bytes",
                per_img);
+  // the largest image chunk whose col buffer + weight-gradient partials fit
   int chunk = static_cast<int>(ws_bytes / per_img);
   if (chunk > d.num) chunk = d.num;
+  size_t part_bytes = dw ? bwd_part_bytes(d, chunk) : 0;
+  while (chunk > 1 && col_bytes(d, chunk) + part_bytes > ws_bytes) {
+    --chunk;
+    part_bytes = bwd_part_bytes(d, chunk);
+  }
+  if (col_bytes(d, chunk) + part_bytes > ws_bytes) part_bytes = 0;  // no split-K
   float* col = static_cast<float*>(ws);
+  void* part = part_bytes ? static_cast<char*>(ws) + (col_bytes(d, chunk) + 255) / 256 * 256 : nullptr;
+  if (part && (col_bytes(d, chunk) + 255) / 256 * 256 + part_bytes > ws_bytes) part = nullptr;
   const int64_t chw = (int64_t)d.channels * d.height * d.width;
   const int64_t ohw = (int64_t)d.num_output * HoWo;
   for (int n0 = 0; n0 < d.num; n0 += chunk) {
@@ -153,7 +176,7 @@ int rram_conv2d_bwd(const rram_conv_desc* d_in, const float* x, const float* w, 
     if (dw) {
       rc = im2col_core(x + n0 * chw, chw, nimg, &d, col, ldcol, s);
       if (rc) return rc;
-      rc = conv_bwd_weight_core(&d, nimg, dy + n0 * ohw, col, ldcol, dw, s);
+      rc = conv_bwd_weight_core(&d, nimg, dy + n0 * ohw, col, ldcol, dw, part, part ? part_bytes : 0, s);
       if (rc) return rc;
     }
     if (dx) {

@@ -643,7 +643,11 @@ int launch_cfg(Params P, int gz, hipStream_t s) {
 // force_big: split-K grids (128x128).
 template <int AM, int BMODE, int OM, int KB>
 int launch(const Params& P, int gz, hipStream_t s, bool force_big) {
-  if (force_big) return launch_cfg<2, 2, 2, 2, AM, BMODE, OM, KB>(P, gz, s);
+  if (force_big) {
+    // split-K grids: 64 x 64 tiles when an operand is that thin (conv weight gradients)
+    if (P.M <= 64 || P.N <= 64) return launch_cfg<2, 2, 1, 1, AM, BMODE, OM, KB>(P, gz, s);
+    return launch_cfg<2, 2, 2, 2, AM, BMODE, OM, KB>(P, gz, s);
+  }
   // tuning knob: RRAM_GEMM_TILE = 64 | 96 | 128 | 192 forces BM (BN = 128), 6464 the 64x64 tile
   static const int forced = [] {
     const char* e = getenv("RRAM_GEMM_TILE");
@@ -893,9 +897,25 @@ int conv_fwd_core(const rram_conv_desc* d, const float* x, const float* w, const
   return dispatch(vec_ok(w, K, K, P.grp_a) ? KCV : KC, bmode, OUT_NCHW, P, g, s);
 }
 
-// dW_g[co][k] += sum_p dY_g[co][p] col_g[k][p]   (col: [Cin*kh*kw][ldcol])
+// Split-K factor of the weight-gradient GEMM: M = Cout/g and N = Cin/g*kh*kw
+// are small while K = images*Ho*Wo is long (CIFAR conv1: 32 x 75 x 102400),
+// so without a split the grid is a couple of blocks.  Aim for ~1024 blocks of
+// 64 x 64 (or 128 x 128) tiles with >= 512 K per split, <= 64 splits and
+// <= 256 MB of partials.
+int bwd_weight_split(int M, int N, int64_t K) {
+  const int64_t t = (M <= 64 || N <= 64) ? (int64_t)((M + 63) / 64) * ((N + 63) / 64)
+                                         : (int64_t)((M + 127) / 128) * ((N + 127) / 128);
+  int64_t sp = 1024 / (t > 0 ? t : 1);
+  if (sp > 64) sp = 64;
+  while (sp > 1 && K / sp < 512) --sp;
+  while (sp > 1 && sp * M * N * 4 > (256ll << 20)) --sp;
+  return static_cast<int>(sp < 1 ? 1 : sp);
+}
+
+// dW_g[co][k] += sum_p dY_g[co][p] col_g[k][p]   (col: [Cin*kh*kw][ldcol]);
+// part (nullable): part_bytes of split-K partials (see bwd_weight_split)
 int conv_bwd_weight_core(const rram_conv_desc* d, int nimg, const float* dy, const float* col,
-                         int64_t ldcol, float* dw, hipStream_t s) {
+                         int64_t ldcol, float* dw, void* part, size_t part_bytes, hipStream_t s) {
   const int g = d->group;
   const int cin_g = d->channels / g, cout_g = d->num_output / g;
   const int K = cin_g * d->kernel_h * d->kernel_w;
@@ -912,7 +932,26 @@ int conv_bwd_weight_core(const rram_conv_desc* d, int nimg, const float* dy, con
     P.a.hw = make_fastdiv(HoWo);
     P.b = make_view(col + (int64_t)gi * K * ldcol, ldcol, K, P.K);
     P.e = make_epi(dw + (int64_t)gi * cout_g * K, K, 1.0f, 1.0f, nullptr, 0, 0);
-    const int rc = dispatch(NCHW, vec_ok(P.b.p, ldcol, P.K) ? KCV : KC, OUT_ROWMAJOR, P, 1, s);
+    const int bm = vec_ok(P.b.p, ldcol, P.K) ? KCV : KC;
+    int split = part ? bwd_weight_split(P.M, P.N, P.K) : 1;
+    while (split > 1 && (size_t)split * P.M * P.N * sizeof(float) > part_bytes) --split;
+    if (split > 1) {
+      int chunk = (P.K + split - 1) / split;
+      chunk = (chunk + BK - 1) / BK * BK;
+      split = (P.K + chunk - 1) / chunk;
+      P.split = split;
+      P.k_chunk = chunk;
+      P.ws = static_cast<float*>(part);
+      int rc = dispatch(NCHW, bm, OUT_ROWMAJOR, P, split, s, true);
+      if (rc) return rc;
+      // dw += sum of the partials (beta = 1), fixed summation order
+      hipLaunchKernelGGL(k_splitk_reduce, dim3(stream_blocks((int64_t)P.M * P.N)), dim3(256), 0, s, P.ws, split,
+                         P.M, P.N, P.e);
+      rc = launch_status("conv bwd weight split-K reduce");
+      if (rc) return rc;
+      continue;
+    }
+    const int rc = dispatch(NCHW, bm, OUT_ROWMAJOR, P, 1, s);
     if (rc) return rc;
   }
   return RRAM_OK;
