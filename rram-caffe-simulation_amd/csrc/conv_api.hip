@@ -51,6 +51,34 @@ __global__ void __launch_bounds__(256) k_bias_bwd(const float* __restrict__ dy, 
   if (threadIdx.x == 0) db[c] += part[0] + part[1] + part[2] + part[3];
 }
 
+// Two-stage deterministic bias gradient when a workspace is at hand: block
+// (c, j) sums images [j*per, (j+1)*per) of channel c into part[c][j]; then
+// db[c] += part[c][0] + ... + part[c][S-1] in order.
+__global__ void __launch_bounds__(256) k_bias_bwd_part(const float* __restrict__ dy, float* __restrict__ part,
+                                                       int num, int C, int inner, int per) {
+  __shared__ float red[4];
+  const int c = blockIdx.x, j = blockIdx.y;
+  const int n1 = min(num, (j + 1) * per);
+  float s = 0.0f;
+  for (int n = j * per; n < n1; ++n) {
+    const float* row = dy + ((int64_t)n * C + c) * inner;
+    for (int q = threadIdx.x; q < inner; q += blockDim.x) s += row[q];
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[(int64_t)c * gridDim.y + j] = red[0] + red[1] + red[2] + red[3];
+}
+__global__ void __launch_bounds__(256) k_bias_bwd_reduce(const float* __restrict__ part, float* __restrict__ db,
+                                                         int C, int S) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.0f;
+  for (int j = 0; j < S; ++j) s += part[(int64_t)c * S + j];
+  db[c] += s;
+}
+
 int check_desc(const rram_conv_desc* d) {
   RRAM_REQUIRE(d != nullptr, "conv: desc is NULL");
   RRAM_REQUIRE(d->num >= 0 && d->channels > 0 && d->height > 0 && d->width > 0 &&
@@ -146,8 +174,20 @@ int rram_conv2d_bwd(const rram_conv_desc* d_in, const float* x, const float* w, 
   hipStream_t s = as_stream(st);
   const int HoWo = d.out_h * d.out_w;
   if (db) {
-    hipLaunchKernelGGL(k_bias_bwd, dim3(d.num_output), dim3(256), 0, s, dy, db, d.num,
-                       d.num_output, HoWo);
+    const int S = d.num < 64 ? d.num : 64;
+    if (ws && S > 1 && ws_bytes >= (size_t)d.num_output * S * sizeof(float)) {
+      // the workspace head holds the partials; the passes below reuse it after
+      // this reduction (same stream)
+      float* part = static_cast<float*>(ws);
+      const int per = (d.num + S - 1) / S;
+      const int Sx = (d.num + per - 1) / per;
+      hipLaunchKernelGGL(k_bias_bwd_part, dim3(d.num_output, Sx), dim3(256), 0, s, dy, part, d.num, d.num_output,
+                         HoWo, per);
+      hipLaunchKernelGGL(k_bias_bwd_reduce, dim3((d.num_output + 255) / 256), dim3(256), 0, s, part, db,
+                         d.num_output, Sx);
+    } else {
+      hipLaunchKernelGGL(k_bias_bwd, dim3(d.num_output), dim3(256), 0, s, dy, db, d.num, d.num_output, HoWo);
+    }
     rc = launch_status("conv bias bwd");
     if (rc) return rc;
   }

@@ -18,6 +18,7 @@
 // receives a contiguous run of tiles that share operand panels.
 #include <stdlib.h>
 
+#include <algorithm>
 #include <array>
 #include <map>
 #include <mutex>
@@ -564,30 +565,32 @@ __global__ void __launch_bounds__(256) k_gemv(int trans, int M, int N, float alp
   }
 }
 
-// im2col / col2im for `nimg` images written into a [K][ldcol] matrix at
-// column offset img*HoWo (ldcol >= nimg*HoWo).
+// im2col for `nimg` images written into a [K][ldcol] matrix at column offset
+// img*HoWo (ldcol >= nimg*HoWo).  Grid: y = column-matrix row (c, kh, kw),
+// block-uniform, so its decomposition is scalar; x strides over the output
+// positions (n, ho, wo) with 32-bit magic-number divisions; stores are
+// coalesced along the row.
 __global__ void __launch_bounds__(256)
     k_im2col(const float* __restrict__ im, int64_t im_img, int nimg, int C, int H, int W, int KH,
              int KW, int ph, int pw, int sh, int sw, int dh, int dw, int Ho, int Wo,
-             float* __restrict__ col, int64_t ldcol) {
-  const int64_t total = (int64_t)nimg * C * KH * KW * Ho * Wo;
-  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    int64_t t = idx;
-    const int wo = t % Wo; t /= Wo;
-    const int ho = t % Ho; t /= Ho;
-    const int kw = t % KW; t /= KW;
-    const int kh = t % KH; t /= KH;
-    const int c = t % C; t /= C;
-    const int n = static_cast<int>(t);
-    const int iy = ho * sh - ph + kh * dh;
-    const int ix = wo * sw - pw + kw * dw;
+             float* __restrict__ col, int64_t ldcol, FastDiv howo, FastDiv wo_div) {
+  const int krow = blockIdx.y;
+  const int kw = krow % KW, kh = (krow / KW) % KH, c = krow / (KW * KH);
+  const int HoWo = Ho * Wo;
+  const int P = nimg * HoWo;
+  float* dst = col + (int64_t)krow * ldcol;
+  const float* src = im + (int64_t)c * H * W;
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
+    const uint32_t n = fdiv(static_cast<uint32_t>(p), howo);
+    const uint32_t r = static_cast<uint32_t>(p) - n * howo.d;
+    const uint32_t ho = fdiv(r, wo_div);
+    const uint32_t wo = r - ho * wo_div.d;
+    const int iy = static_cast<int>(ho) * sh - ph + kh * dh;
+    const int ix = static_cast<int>(wo) * sw - pw + kw * dw;
     float v = 0.0f;
-    if (static_cast<unsigned>(iy) < static_cast<unsigned>(H) &&
-        static_cast<unsigned>(ix) < static_cast<unsigned>(W))
-      v = im[n * im_img + ((int64_t)c * H + iy) * W + ix];
-    const int64_t krow = ((int64_t)c * KH + kh) * KW + kw;
-    col[krow * ldcol + (int64_t)n * Ho * Wo + (int64_t)ho * Wo + wo] = v;
+    if (static_cast<unsigned>(iy) < static_cast<unsigned>(H) && static_cast<unsigned>(ix) < static_cast<unsigned>(W))
+      v = src[n * im_img + iy * W + ix];
+    dst[p] = v;
   }
 }
 
@@ -986,10 +989,15 @@ int im2col_core(const float* im, int64_t im_img, int nimg, const rram_conv_desc*
                 int64_t ldcol, hipStream_t s) {
   const int64_t total = (int64_t)nimg * d->channels * d->kernel_h * d->kernel_w * d->out_h * d->out_w;
   if (total == 0) return RRAM_OK;
-  hipLaunchKernelGGL(k_im2col, dim3(stream_blocks(total)), dim3(256), 0, s, im, im_img, nimg,
+  const int rows = d->channels * d->kernel_h * d->kernel_w;
+  const int64_t P = (int64_t)nimg * d->out_h * d->out_w;
+  RRAM_REQUIRE(P < (1ll << 31) && (int64_t)nimg * im_img < (1ll << 31) && rows < 65536,
+               "im2col: more than 2^31 positions / input elements or 65535 rows is not supported");
+  const int gx = static_cast<int>(std::min<int64_t>((P + 255) / 256, 64));
+  hipLaunchKernelGGL(k_im2col, dim3(gx, rows), dim3(256), 0, s, im, im_img, nimg,
                      d->channels, d->height, d->width, d->kernel_h, d->kernel_w, d->pad_h,
                      d->pad_w, d->stride_h, d->stride_w, d->dilation_h, d->dilation_w, d->out_h,
-                     d->out_w, col, ldcol);
+                     d->out_w, col, ldcol, make_fastdiv(d->out_h * d->out_w), make_fastdiv(d->out_w));
   return launch_status("im2col");
 }
 

@@ -352,6 +352,10 @@ void Net<Dtype>::Update() {
 
 template <typename Dtype>
 void Net<Dtype>::ClearParamDiffs() {
+  if (flat_diff_) {  // every learnable diff lives in one buffer: one memset
+    HIP_CALL(hipMemsetAsync(flat_diff_, 0, flat_param_count() * sizeof(Dtype), Caffe::hip_stream()));
+    return;
+  }
   for (auto* p : learnable_params_)
     HIP_CALL(hipMemsetAsync(p->mutable_gpu_diff(), 0, p->count() * sizeof(Dtype), Caffe::hip_stream()));
 }
@@ -482,6 +486,7 @@ void Net<Dtype>::alias_flat_params(Dtype* data, Dtype* diff) {
     p->set_gpu_diff(diff + off);
     off += n;
   }
+  flat_diff_ = diff;
   HIP_CALL(hipStreamSynchronize(Caffe::hip_stream()));
 }
 

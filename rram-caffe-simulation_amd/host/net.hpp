@@ -10,16 +10,10 @@
 #include <vector>
 
 #include "io.hpp"
-#include "io.hpp"
 #include "layers.hpp"
 #include "timer.hpp"
 
 namespace caffe {
-
-template <typename Dtype>
-void BlobFromProto(Blob<Dtype>* b, const BlobProtoData& p);  // shape-checked by the caller
-template <typename Dtype>
-BlobProtoData BlobToProto(Blob<Dtype>* b, bool write_diff);
 
 template <typename Dtype>
 void BlobFromProto(Blob<Dtype>* b, const BlobProtoData& p);  // shape-checked by the caller
@@ -89,6 +83,7 @@ class Net {
  private:
   int timing_ = 0;
   EventTimer timer_;
+  Dtype* flat_diff_ = nullptr;  // set by alias_flat_params
   void AppendParam(int layer_id, int param_id, const Msg& layer_param);
 
   std::string name_;

@@ -176,6 +176,19 @@ Solver<Dtype>::Solver(const Msg& sp, const Msg* net_param, const Msg& options) :
   }
   CAFFE_CHECK(param_.str("type", "SGD") == "SGD" && param_.str("solver_type", "SGD") == "SGD",
               "only the SGD solver is part of this build (SURVEY.md §2.1)");
+  const int64_t nflat = net_->flat_param_count();
+  if (nflat > 0 && options.boolean("flat_params", true)) {
+    HIP_CALL(hipMalloc(&flat_, 2 * nflat * sizeof(Dtype)));
+    net_->alias_flat_params(static_cast<Dtype*>(flat_), static_cast<Dtype*>(flat_) + nflat);
+  }
+}
+
+template <typename Dtype>
+Solver<Dtype>::~Solver() {
+  if (flat_) {
+    (void)hipStreamSynchronize(Caffe::hip_stream());
+    (void)hipFree(flat_);
+  }
 }
 
 // solver.cpp:14-23

@@ -164,7 +164,7 @@ class Solver {
   // options: net options (data_shape, num_classes, fault_layers, fuse_relu)
   // plus `fused_update` (true: one fused HBM pass per blob for the training tail).
   Solver(const Msg& solver_param, const Msg* net_param, const Msg& options);
-  virtual ~Solver() = default;
+  virtual ~Solver();
 
   void Step(int iters);
   // solver.cpp:328-370; resume_file: a .solverstate to Restore() first
@@ -220,6 +220,9 @@ class Solver {
 
   Msg param_;
   Msg options_;
+  // flat learnable data / diff buffers the params are aliased into
+  // (ClearParamDiffs becomes one memset; the data-parallel all-reduce re-aliases)
+  void* flat_ = nullptr;
   std::shared_ptr<Net<Dtype>> net_;
   std::vector<std::shared_ptr<Net<Dtype>>> test_nets_;
   std::vector<std::unique_ptr<Blob<Dtype>>> history_, temp_;
