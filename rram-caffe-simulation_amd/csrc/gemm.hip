@@ -41,7 +41,8 @@ constexpr int ldk_of() { return KB + 4; }
 // KCV = KC with 16-byte global loads (row stride, base and K all multiples of 4 floats)
 // CONVT = CONV with a per-k offset/tap table (conv_table below) read by scalar
 // loads: no (c, kh, kw) stepping and no multiplies in the gather.
-enum Mode : int { KC = 0, RC = 1, CONV = 2, NCHW = 3, NCHWT = 4, KCV = 5, CONVT = 6 };
+// CONVT64: the same with a 64-bit tap mask (kh*kw <= 63, e.g. 7 x 7 with padding)
+enum Mode : int { KC = 0, RC = 1, CONV = 2, NCHW = 3, NCHWT = 4, KCV = 5, CONVT = 6, CONVT64 = 7 };
 enum OutMode : int { OUT_ROWMAJOR = 0, OUT_NCHW = 1 };
 
 // Fast unsigned division by a runtime constant (x < 2^31).
@@ -116,7 +117,8 @@ struct ConvCol {
   bool valid;
   int pbase;     // n*C*H*W + hb*W + wb (element offset inside the group's input)
   __amdgpu_buffer_rsrc_t rsrc;  // raw buffer over the group's input (OOB loads return 0)
-  uint32_t bad;  // CONVT: bit t set = tap t of this column reads padding (bit 31 always set)
+  uint32_t bad;     // CONVT: bit t set = tap t of this column reads padding (bit 31 always set)
+  uint32_t bad_hi;  // CONVT64: taps 32..63 (bit 63 always set)
 };
 
 template <int ROWS, int KB>
@@ -192,7 +194,7 @@ __device__ __forceinline__ void load_tile(Loader<ROWS, KB>& L, const View& vw, c
     }
     return;
   }
-  if (MODE == CONVT) {
+  if (MODE == CONVT || MODE == CONVT64) {
     // implicit im2col from the table: thread = one output position x EPT
     // consecutive k; the k segment is wave-uniform, so each table entry is a
     // scalar load, and per element the VALU does one add, one bit extract
@@ -208,7 +210,8 @@ __device__ __forceinline__ void load_tile(Loader<ROWS, KB>& L, const View& vw, c
 #pragma unroll
     for (int i = 0; i < EPT; ++i) {
       const int2 t = te[i];
-      const uint32_t bad = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(col.bad), t.y, 1));
+      const uint32_t word = (MODE == CONVT64 && t.y >= 32) ? col.bad_hi : col.bad;
+      const uint32_t bad = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(word), t.y & 31, 1));
       L.v[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, (pb4 + static_cast<uint32_t>(t.x)) | bad, 0, 0));
     }
     return;
@@ -281,7 +284,7 @@ template <int MODE, int ROWS, int KB>
 __device__ __forceinline__ void store_tile(const Loader<ROWS, KB>& L, float* lds) {
   constexpr int EPT = Loader<ROWS, KB>::EPT;
   constexpr int LDK = ldk_of<KB>();
-  if (MODE == CONV || MODE == CONVT) {
+  if (MODE == CONV || MODE == CONVT || MODE == CONVT64) {
     // EPT consecutive k of one row: 16-byte LDS writes (row stride 36 dwords
     // puts the 8 lanes of a ds_write_b128 group on distinct bank quads)
     float* dst = lds + (threadIdx.x % ROWS) * LDK + (threadIdx.x / ROWS) * EPT;
@@ -363,7 +366,7 @@ __global__ void __launch_bounds__(256) k_gemm(Params P) {
 
   // CONV column precompute (B operand rows = output positions; fixed per thread)
   ConvCol col{0, 0, 0, false};
-  if (BMODE == CONV || BMODE == CONVT) {
+  if (BMODE == CONV || BMODE == CONVT || BMODE == CONVT64) {
     int r, kk;
     tile_coord<CONV, BNr, KB>(threadIdx.x, r, kk);
     const int p = n0 + r;
@@ -378,20 +381,25 @@ __global__ void __launch_bounds__(256) k_gemm(Params P) {
       col.valid = true;
       col.pbase = static_cast<int>(col.base) + col.hb * P.cv.W + col.wb;
     }
-    if (BMODE == CONVT) {
+    if (BMODE == CONVT || BMODE == CONVT64) {
       // validity of every kernel tap for this column, once per block
-      uint32_t good = 0;
+      uint64_t good = 0;
       if (P.cv.taps == 0) {
         good = col.valid ? 1u : 0u;  // pad-free: every tap is inside the image
       } else if (col.valid) {
         for (int t = 0; t < P.cv.taps; ++t) {
           const int kh = t / P.cv.KW, kw = t - kh * P.cv.KW;
-          good |= static_cast<uint32_t>(static_cast<unsigned>(col.hb + kh * P.cv.dh) < static_cast<unsigned>(P.cv.H) &&
+          good |= static_cast<uint64_t>(static_cast<unsigned>(col.hb + kh * P.cv.dh) < static_cast<unsigned>(P.cv.H) &&
                                         static_cast<unsigned>(col.wb + kw * P.cv.dw) < static_cast<unsigned>(P.cv.W))
                   << t;
         }
       }
-      col.bad = ~good | 0x80000000u;
+      if (BMODE == CONVT) {
+        col.bad = ~static_cast<uint32_t>(good) | 0x80000000u;
+      } else {
+        col.bad = ~static_cast<uint32_t>(good);
+        col.bad_hi = ~static_cast<uint32_t>(good >> 32) | 0x80000000u;
+      }
     }
     // group base pointer, range = the whole remaining input (host checks < 2^32 bytes)
     col.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(vb.p), 0, P.cv.in_bytes, 0x00020000);
@@ -707,6 +715,10 @@ int dispatch(int am, int bm, int om, const Params& P, int gz, hipStream_t s, boo
     if (am == KC) return launch<KC, CONVT, OUT_NCHW, 16>(P, gz, s, force_big);
     if (am == KCV) return launch<KCV, CONVT, OUT_NCHW, 16>(P, gz, s, force_big);
   }
+  if (bm == CONVT64 && om == OUT_NCHW && conv_kb(P.K) == 16) {
+    if (am == KC) return launch<KC, CONVT64, OUT_NCHW, 16>(P, gz, s, force_big);
+    if (am == KCV) return launch<KCV, CONVT64, OUT_NCHW, 16>(P, gz, s, force_big);
+  }
 #define RRAM_D(A_, B_, O_) \
   if (am == A_ && bm == B_ && om == O_) return launch<A_, B_, O_, 32>(P, gz, s, force_big);
   RRAM_D(KC, KC, OUT_ROWMAJOR)
@@ -722,6 +734,8 @@ int dispatch(int am, int bm, int om, const Params& P, int gz, hipStream_t s, boo
   RRAM_D(KCV, CONV, OUT_NCHW)
   RRAM_D(KC, CONVT, OUT_NCHW)
   RRAM_D(KCV, CONVT, OUT_NCHW)
+  RRAM_D(KC, CONVT64, OUT_NCHW)
+  RRAM_D(KCV, CONVT64, OUT_NCHW)
   RRAM_D(NCHW, KC, OUT_ROWMAJOR)
   RRAM_D(NCHW, KCV, OUT_ROWMAJOR)
   RRAM_D(RC, NCHWT, OUT_ROWMAJOR)
@@ -767,15 +781,15 @@ View make_view(const float* p, int64_t ld, int rows, int kdim) {
 // kh*KW + kw (0 for pad-free convolutions, whose taps are always inside the
 // image); entries past K (the last tile's tail and the one-tile prefetch
 // overrun) hold tap 31, which no column marks valid.
-const int2* conv_table(const ConvGeom& cv, int K, bool padded, hipStream_t s) {
+const int2* conv_table(const ConvGeom& cv, int K, bool padded, bool wide, hipStream_t s) {
   static std::mutex mu;
-  static std::map<std::array<int, 9>, int2*> cache;
-  const std::array<int, 9> key{cv.C, cv.H, cv.W, cv.KH, cv.KW, cv.dh, cv.dw, padded ? 1 : 0, K};
+  static std::map<std::array<int, 10>, int2*> cache;
+  const std::array<int, 10> key{cv.C, cv.H, cv.W, cv.KH, cv.KW, cv.dh, cv.dw, padded ? 1 : 0, K, wide ? 1 : 0};
   std::lock_guard<std::mutex> g(mu);
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
   const int len = (K + BK - 1) / BK * BK + 2 * BK;
-  std::vector<int2> h(len, int2{0, 31});
+  std::vector<int2> h(len, int2{0, wide ? 63 : 31});  // the never-valid tap
   for (int k = 0; k < K; ++k) {
     const int c = k / (cv.KH * cv.KW), r = k % (cv.KH * cv.KW);
     const int kh = r / cv.KW, kw = r % cv.KW;
@@ -888,14 +902,16 @@ int conv_fwd_core(const rram_conv_desc* d, const float* x, const float* w, const
   P.grp_b = (int64_t)cin_g * d->height * d->width;
   P.grp_c = (int64_t)cout_g * HoWo;
   P.grp_bias = cout_g;
-  // table-driven gather when the taps fit the 31-bit validity mask (or no padding)
+  // table-driven gather when the taps fit the 31-bit (or 63-bit) validity mask (or no padding)
   const bool padded = d->pad_h > 0 || d->pad_w > 0;
+  const int taps = d->kernel_h * d->kernel_w;
+  const bool wide = padded && taps > 31;
   int bmode = CONV;
-  if (getenv("RRAM_CONV_NO_TABLE") == nullptr && (!padded || d->kernel_h * d->kernel_w <= 31) &&
+  if (getenv("RRAM_CONV_NO_TABLE") == nullptr && (!padded || taps <= 63) &&
       (int64_t)cin_g * d->height * d->width * 4 < (1ll << 31)) {
-    cv.tbl = conv_table(cv, K, padded, s);
-    cv.taps = padded ? d->kernel_h * d->kernel_w : 0;
-    if (cv.tbl) bmode = CONVT;
+    cv.tbl = conv_table(cv, K, padded, wide, s);
+    cv.taps = padded ? taps : 0;
+    if (cv.tbl) bmode = wide ? CONVT64 : CONVT;
   }
   return dispatch(vec_ok(w, K, K, P.grp_a) ? KCV : KC, bmode, OUT_NCHW, P, g, s);
 }

@@ -320,6 +320,9 @@ CONV_CASES = [
     dict(x=(3, 384, 13, 13), cout=384, k=3, s=1, p=1, d=1, g=2),   # conv4
     dict(x=(4, 32, 16, 16), cout=32, k=5, s=1, p=2, d=1, g=1),     # CIFAR conv2
     dict(x=(5, 480, 14, 14), cout=64, k=1, s=1, p=0, d=1, g=1),    # GoogLeNet 1x1
+    dict(x=(2, 3, 40, 37), cout=64, k=7, s=2, p=3, d=1, g=1),      # GoogLeNet conv1 (64-bit tap mask)
+    dict(x=(2, 5, 19, 23), cout=8, k=9, s=1, p=4, d=1, g=1),       # 81 taps, padded: the stepped gather
+    dict(x=(2, 4, 21, 21), cout=6, k=5, s=2, p=3, d=2, g=2),       # dilation + groups + padding
 ]
 
 
