@@ -5,6 +5,8 @@
 #include <float.h>
 #include <math.h>
 
+#include <stdlib.h>
+
 #include "rram_common.hpp"
 
 namespace rram {
@@ -111,6 +113,58 @@ __global__ void __launch_bounds__(256) k_pool_max_fixed(const float* __restrict_
         }
     y[idx] = mv;
     if (mask) mask[idx] = mi;
+  }
+}
+
+// The same max pool for small planes (H*W <= kPlaneTile): a block stages
+// whole (n, c) planes - contiguous in NCHW - in LDS with coalesced 16-byte
+// loads, then computes every output of those planes from LDS, so each input
+// is read from HBM once and the K*K window re-reads stay on-chip.  Outputs
+// are written contiguously.  Same window, order and tie rule as above.
+constexpr int kPlaneTile = 4096;  // floats of LDS per block
+template <int K>
+__global__ void __launch_bounds__(256) k_pool_max_planes(const float* __restrict__ x, float* __restrict__ y,
+                                                         int* __restrict__ mask, int planes, int H, int W, int PH,
+                                                         int PW, int sh, int sw, int ph, int pw, int ppb) {
+  __shared__ __attribute__((aligned(16))) float tile[kPlaneTile];
+  const int HW = H * W, PHW = PH * PW;
+  const int p0 = blockIdx.x * ppb;
+  const int np = min(ppb, planes - p0);
+  const float* src = x + (int64_t)p0 * HW;
+  const int n_in = np * HW;
+  if ((reinterpret_cast<uintptr_t>(src) & 15u) == 0) {
+    const int n4 = n_in >> 2;
+    for (int i = threadIdx.x; i < n4; i += 256)
+      reinterpret_cast<float4*>(tile)[i] = reinterpret_cast<const float4*>(src)[i];
+    for (int i = (n4 << 2) + threadIdx.x; i < n_in; i += 256) tile[i] = src[i];
+  } else {
+    for (int i = threadIdx.x; i < n_in; i += 256) tile[i] = src[i];
+  }
+  __syncthreads();
+  const int n_out = np * PHW;
+  float* dst = y + (int64_t)p0 * PHW;
+  for (int o = threadIdx.x; o < n_out; o += 256) {
+    const int pl = o / PHW, r = o - pl * PHW;
+    const int phi = r / PW, pwi = r - phi * PW;
+    const int hs = phi * sh - ph, ws = pwi * sw - pw;
+    const float* t = tile + pl * HW;
+    float mv = -FLT_MAX;
+    int mi = -1;
+#pragma unroll
+    for (int a = 0; a < K; ++a)
+#pragma unroll
+      for (int b = 0; b < K; ++b) {
+        const int h = hs + a, w = ws + b;
+        const bool ok = static_cast<unsigned>(h) < static_cast<unsigned>(H) &&
+                        static_cast<unsigned>(w) < static_cast<unsigned>(W);
+        const float v = t[ok ? h * W + w : 0];
+        if (ok && v > mv) {
+          mv = v;
+          mi = h * W + w;
+        }
+      }
+    dst[o] = mv;
+    if (mask) mask[(int64_t)p0 * PHW + o] = mi;
   }
 }
 
@@ -480,7 +534,20 @@ int rram_pool_fwd(const float* x, float* y, int* mask, int num, int C, int H, in
   RRAM_REQUIRE_I32(total, "layer kernel");
   if (total == 0) return RRAM_OK;
   RRAM_REQUIRE(x && y, "pool_fwd: NULL");
-  if (method == RRAM_POOL_MAX && kh == kw && kh == 3)
+  const int planes = num * C;
+  if (method == RRAM_POOL_MAX && kh == kw && (kh == 3 || kh == 2) && H * W <= kPlaneTile &&
+      getenv("RRAM_POOL_NO_PLANES") == nullptr) {
+    // planes per block: fill the LDS tile, but keep >= 2048 blocks when possible
+    int ppb = kPlaneTile / (H * W);
+    while (ppb > 1 && (planes + ppb - 1) / ppb < 2048) --ppb;
+    const dim3 grid(static_cast<unsigned>((planes + ppb - 1) / ppb));
+    if (kh == 3)
+      hipLaunchKernelGGL(k_pool_max_planes<3>, grid, dim3(kThreads), 0, as_stream(s), x, y, mask, planes, H, W, PH,
+                         PW, sh, sw, ph, pw, ppb);
+    else
+      hipLaunchKernelGGL(k_pool_max_planes<2>, grid, dim3(kThreads), 0, as_stream(s), x, y, mask, planes, H, W, PH,
+                         PW, sh, sw, ph, pw, ppb);
+  } else if (method == RRAM_POOL_MAX && kh == kw && kh == 3)
     hipLaunchKernelGGL(k_pool_max_fixed<3>, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), x, y,
                        mask, num, C, H, W, PH, PW, sh, sw, ph, pw);
   else if (method == RRAM_POOL_MAX && kh == kw && kh == 2)

@@ -487,6 +487,32 @@ class MonteCarlo:
         return dict(sums=[sums[i] for i in range(n_out)], broken=[broken[i] for i in range(nb.value)],
                     per_map=pm, maps=mr.value)
 
+    def summary(self, z: float = 1.96):
+        """Per-output statistics over the maps run: mean, sample
+        std and the normal-approximation confidence half-width z*std/sqrt(n) from
+        the per-map records, plus the mean broken cells per faultable blob."""
+        st = self.stats()
+        names = [k for k, v in self.net.outputs().items() if v.numel() == 1]
+        pm = st["per_map"]
+        n = len(pm)
+        out = {}
+        for k, name in enumerate(names[:len(st["sums"])]):
+            vals = [row[k] for row in pm]
+            mean = st["sums"][k] / max(st["maps"], 1)
+            std = (sum((v - sum(vals) / n) ** 2 for v in vals) / (n - 1)) ** 0.5 if n > 1 else 0.0
+            out[name] = dict(mean=mean, std=std, ci=z * std / n ** 0.5 if n > 1 else float("inf"), maps=st["maps"])
+        out["_broken_per_map"] = [b / max(st["maps"], 1) for b in st["broken"]]
+        return out
+
+    def log_lines(self, iteration: int = 0) -> List[str]:
+        """The reference's Solver::Test lines (solver.cpp:440-456) for the map
+        means, which examples/cifar10/plot_pic.py and tools/extra/parse_log.py read."""
+        s = self.summary()
+        lines = [f"Iteration {iteration}, Testing net (#0)"]
+        for k, (name, v) in enumerate((n, v) for n, v in s.items() if not n.startswith("_")):
+            lines.append(f"    Test net output #{k}: {name} = {v['mean']:g}")
+        return lines
+
     def close(self):
         if self.h:
             self._lib.rram_mc_destroy(self.h)

@@ -224,6 +224,17 @@ def test_mc_broken_fraction_binomial(rs):
     st = mc.stats()
     tot = 50 * n
     assert abs(sum(st["broken"]) / tot - p) <= 3.8 * math.sqrt(p * (1 - p) / tot)
+    # per-map statistics and the reference's Test-net log lines (plot_pic.py's regex)
+    sm = mc.summary()
+    acc = [row[0] for row in st["per_map"]]
+    assert sm["accuracy"]["maps"] == 50
+    assert abs(sm["accuracy"]["mean"] - sum(acc) / 50) < 1e-6
+    assert abs(sm["accuracy"]["std"] - float(np.std(acc, ddof=1))) < 1e-5
+    assert abs(sm["accuracy"]["ci"] - 1.96 * float(np.std(acc, ddof=1)) / math.sqrt(50)) < 1e-5
+    import re
+    text = "\n".join(mc.log_lines(100))
+    m = re.search(r"accuracy = (?P<acc>[\d\.]+).*?loss = (?P<loss>[\d\.]+)", text, re.DOTALL)
+    assert m and abs(float(m.group("acc")) - sm["accuracy"]["mean"]) < 1e-4
     mc.close()
     net.close()
 

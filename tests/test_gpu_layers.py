@@ -58,7 +58,7 @@ def _caffe_pool_ref(x, k, s, p, method):
     return torch.stack(rows, -2)
 
 
-@pytest.mark.parametrize("method,k,s,p", [("MAX", 3, 2, 0), ("MAX", 2, 2, 0), ("MAX", 3, 2, 1),
+@pytest.mark.parametrize("method,k,s,p", [("MAX", 3, 2, 0), ("MAX", 2, 2, 0), ("MAX", 3, 2, 1), ("MAX", 3, 1, 1),
                                           ("AVE", 3, 2, 1), ("AVE", 5, 3, 0), ("AVE", 3, 1, 1)])
 def test_pool_fwd_bwd_vs_autograd(device, method, k, s, p):
     import torch
@@ -78,6 +78,41 @@ def test_pool_fwd_bwd_vs_autograd(device, method, k, s, p):
     ops.pool_bwd(dy, mask, dx, geom, m)
     torch.testing.assert_close(y, ref.detach(), rtol=1e-6, atol=1e-6)
     torch.testing.assert_close(dx, x.grad, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("shape,k,s,p", [((8, 64, 28, 28), 3, 1, 1), ((4, 48, 27, 27), 3, 2, 0),
+                                         ((3, 7, 64, 64), 2, 2, 0), ((2, 9, 7, 7), 3, 2, 1)])
+def test_max_pool_plane_kernel_equals_direct(device, shape, k, s, p):
+    """LDS-plane max pool (several planes per block) == the direct kernel, values
+    and argmax mask, bit for bit."""
+    import os
+    import torch
+    from rramsim import ops
+    torch.manual_seed(4)
+    x = torch.randn(*shape, device=device)
+    x[0, 0, :3, :3] = 1.0                            # ties: first index wins in both
+    N, C, H, W = shape
+    PH = -(-(H + 2 * p - k) // s) + 1
+    PW = -(-(W + 2 * p - k) // s) + 1
+    if (PH - 1) * s >= H + p:
+        PH -= 1
+    if (PW - 1) * s >= W + p:
+        PW -= 1
+    geom = (N, C, H, W, PH, PW, k, k, s, s, p, p)
+    outs = []
+    for direct in (False, True):
+        if direct:
+            os.environ["RRAM_POOL_NO_PLANES"] = "1"
+        try:
+            y = torch.full((N, C, PH, PW), float("nan"), device=device)
+            m = torch.full((N, C, PH, PW), -7, dtype=torch.int32, device=device)
+            ops.pool_fwd(x, y, m, geom, 0)
+            torch.cuda.synchronize()
+            outs.append((y, m))
+        finally:
+            os.environ.pop("RRAM_POOL_NO_PLANES", None)
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    torch.testing.assert_close(outs[0][0], _caffe_pool_ref(x, k, s, p, "MAX"), rtol=0, atol=0)
 
 
 def _lrn_across_ref(x, size, alpha, beta, k):
