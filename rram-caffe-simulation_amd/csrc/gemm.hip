@@ -30,6 +30,7 @@ namespace rram {
 namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 // K-tile depth is a template parameter KB (16 or 32); LDS rows are padded to
 // KB + 4 floats (80 / 144 B: 16-B aligned, conflict-free ds_read_b128 for 16
@@ -405,6 +406,17 @@ __global__ void __launch_bounds__(256) k_gemm(Params P) {
     col.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(vb.p), 0, P.cv.in_bytes, 0x00020000);
   }
 
+#ifdef RRAM_V_MFMA16
+  // v_mfma_f32_16x16x4_f32 variant: the wave tile as (2 MI) x (2 NI) 16x16 tiles
+  floatx4 acc[2 * MI][2 * NI];
+#pragma unroll
+  for (int i = 0; i < 2 * MI; ++i)
+#pragma unroll
+    for (int j = 0; j < 2 * NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[i][j][r] = 0.0f;
+  const int l16 = threadIdx.x & 15, g16 = (threadIdx.x & 63) >> 4;
+#else
   floatx16 acc[MI][NI];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -412,6 +424,7 @@ __global__ void __launch_bounds__(256) k_gemm(Params P) {
     for (int j = 0; j < NI; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+#endif
 
   Loader<BMr, KB> la;
   Loader<BNr, KB> lb;
@@ -424,8 +437,12 @@ __global__ void __launch_bounds__(256) k_gemm(Params P) {
   }
   __syncthreads();
 
+#ifndef RRAM_V_MFMA16
   const int lr = lane & 31;
   const int lh = lane >> 5;
+#else
+  (void)lane;  // measured 6 % slower than the 32x32x2 form on AlexNet b256 (scripts/gpu_variants.sh)
+#endif
   for (int t = 0; t < ntiles; ++t) {
     const int cur = t & 1;
     const bool more = (t + 1) < ntiles;
@@ -439,6 +456,26 @@ __global__ void __launch_bounds__(256) k_gemm(Params P) {
       load_tile<AM, BMr, KB>(la, va, P.cv, col, m0, kn, kend);
       load_tile<BMODE, BNr, KB>(lb, vb, P.cv, col, n0, kn, kend);
     }
+#ifdef RRAM_V_MFMA16
+    // lane group g at step s of sub-block q uses k = 16q + 4g + s (A and B alike)
+#pragma unroll
+    for (int q = 0; q < KB / 16; ++q) {
+      float4 af[2 * MI], bf[2 * NI];
+#pragma unroll
+      for (int i = 0; i < 2 * MI; ++i)
+        af[i] = *reinterpret_cast<const float4*>(&As[cur][(wm * MI * 32 + i * 16 + l16) * LDK + q * 16 + g16 * 4]);
+#pragma unroll
+      for (int j = 0; j < 2 * NI; ++j)
+        bf[j] = *reinterpret_cast<const float4*>(&Bs[cur][(wn * NI * 32 + j * 16 + l16) * LDK + q * 16 + g16 * 4]);
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+        for (int i = 0; i < 2 * MI; ++i)
+#pragma unroll
+          for (int j = 0; j < 2 * NI; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(pick(af[i], s4), pick(bf[j], s4), acc[i][j], 0, 0, 0);
+    }
+#else
 #pragma unroll
     for (int q = 0; q < KB / 16; ++q) {
       float4 af[MI][2], bf[NI][2];
@@ -465,6 +502,7 @@ __global__ void __launch_bounds__(256) k_gemm(Params P) {
         }
       }
     }
+#endif
     // Interleave the next tile's global loads with the first MFMAs (a wave
     // issues VALU / VMEM while its MFMAs run): one load, then NMF MFMAs.
 #ifndef RRAM_V_NOSCHED
@@ -495,6 +533,41 @@ __global__ void __launch_bounds__(256) k_gemm(Params P) {
     __syncthreads();
   }
 
+#ifdef RRAM_V_MFMA16
+  // epilogue: acc[i][j][r] -> row = 16 i + 4 g + r, col = 16 j + l16
+#pragma unroll
+  for (int j = 0; j < 2 * NI; ++j) {
+    const int n = n0 + wn * NI * 32 + j * 16 + l16;
+    if (n >= P.N) continue;
+    int64_t cbase = 0;
+    if (OM == OUT_NCHW && part == nullptr) {
+      const uint32_t im = fdiv(static_cast<uint32_t>(n), ep.hw);
+      const uint32_t s = static_cast<uint32_t>(n) - im * ep.hw.d;
+      cbase = (int64_t)im * ep.cimg + s;
+    }
+#pragma unroll
+    for (int i = 0; i < 2 * MI; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * MI * 32 + i * 16 + 4 * g16 + r;
+        if (m >= P.M) continue;
+        const float v = acc[i][j][r];
+        if (part != nullptr) {
+          part[(int64_t)m * P.N + n] = v;
+          continue;
+        }
+        float* dst = (OM == OUT_NCHW) ? (ep.C + cbase + (int64_t)m * ep.ldc)
+                                      : (ep.C + (int64_t)m * ep.ldc + n);
+        float o = ep.alpha * v;
+        if (ep.beta != 0.0f) o += ep.beta * *dst;
+        if (ep.bias_mode == RRAM_BIAS_ROW) o += ep.bias[m];
+        else if (ep.bias_mode == RRAM_BIAS_COL) o += ep.bias[n];
+        if (ep.relu) o = fmaxf(o, 0.0f);
+        *dst = o;
+      }
+    }
+  }
+#else
   // epilogue: acc[i][j][r] -> row = (r&3) + 8*(r>>2) + 4*lh, col = lr
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
@@ -528,6 +601,7 @@ __global__ void __launch_bounds__(256) k_gemm(Params P) {
       }
     }
   }
+#endif
 }
 
 // split-K reduction + epilogue (row-major C only)
