@@ -141,6 +141,16 @@ int rram_inject_rng_batched(const rram_inject_seg* segs, int nsegs,
                             uint64_t seed, uint32_t map_id,
                             unsigned long long* counters, rram_stream_t stream);
 
+/* Monte-Carlo statistics of one map in one launch (the MC analogue of
+ * Solver::Test's score accumulation, src/caffe/solver.cpp:410-430):
+ * sums[k] += p[k][0] and per_map_row[k] = p[k][0] (per_map_row nullable). */
+#define RRAM_MC_MAX_OUTPUTS 8
+typedef struct {
+  const float* p[RRAM_MC_MAX_OUTPUTS]; /* device scalars (the net's 1-element outputs) */
+  int n;
+} rram_mc_outputs;
+int rram_mc_accumulate(const rram_mc_outputs* outs, float* sums, float* per_map_row, rram_stream_t stream);
+
 /* ------------------------------------------------------------------------
  * Strategy / solver elementwise
  * ---------------------------------------------------------------------- */

@@ -388,6 +388,16 @@ __global__ void __launch_bounds__(256)
   if (cur >= 0) block_count_flush(nb, counters ? counters + cur : nullptr);
 }
 
+// Monte-Carlo statistics of one map: sums[k] += out_k[0]; per_map[k] = out_k[0].
+__global__ void k_mc_accumulate(rram_mc_outputs o, float* __restrict__ sums, float* __restrict__ per_map) {
+  const int k = threadIdx.x;
+  if (k < o.n) {
+    const float v = o.p[k][0];
+    sums[k] += v;
+    if (per_map) per_map[k] = v;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // a3 / a4
 // ---------------------------------------------------------------------------
@@ -754,6 +764,13 @@ int rram_inject_rng(const float* w_clean, float* w_out, int64_t n, const rram_in
   sg.layer_id = layer_id;
   sg.cfg = *cfg;
   return rram_inject_rng_batched(&sg, 1, seed, map_id, counters, s);
+}
+
+int rram_mc_accumulate(const rram_mc_outputs* outs, float* sums, float* per_map_row, rram_stream_t s) {
+  RRAM_REQUIRE(outs && sums && outs->n >= 0 && outs->n <= RRAM_MC_MAX_OUTPUTS, "mc_accumulate: bad arguments");
+  if (outs->n == 0) return RRAM_OK;
+  hipLaunchKernelGGL(k_mc_accumulate, dim3(1), dim3(64), 0, as_stream(s), *outs, sums, per_map_row);
+  return launch_status("mc_accumulate");
 }
 
 int rram_threshold_strategy(float* dw, int64_t n, float thr, unsigned long long* cleared,

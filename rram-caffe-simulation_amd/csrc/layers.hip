@@ -484,6 +484,50 @@ __global__ void __launch_bounds__(256) k_accuracy(const float* __restrict__ x, c
     if (N) atomicAdd(count, static_cast<float>(N));
   }
 }
+// Single-launch form for up to kAccSmall columns (every TEST batch of the
+// configs): one block walks all columns, reduces in LDS and writes correct,
+// count and the ratio — no memsets, no atomics, no second launch.
+constexpr int kAccSmall = 1 << 16;
+__global__ void __launch_bounds__(1024) k_accuracy_small(const float* __restrict__ x, const float* __restrict__ label,
+                                                         float* correct, float* count, float* ratio, int outer, int C,
+                                                         int inner, int top_k, int ignore) {
+  __shared__ int sa[16], sc[16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int cols = outer * inner;
+  int hits = 0, cnt = 0;
+  for (int col = wave; col < cols; col += 16) {
+    const int o = col / inner, q = col - o * inner;
+    const int lv = static_cast<int>(label[col]);
+    if (ignore >= 0 && lv == ignore) continue;  // wave-uniform
+    const float* xs = x + (int64_t)o * C * inner + q;
+    const float v = xs[(int64_t)lv * inner];
+    int rank = 0;
+    for (int c = lane; c < C; c += 64) {
+      const float u = xs[(int64_t)c * inner];
+      rank += (u > v) || (u == v && c > lv);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) rank += __shfl_xor(rank, off, 64);
+    hits += rank < top_k;
+    cnt += 1;
+  }
+  if (lane == 0) {
+    sa[wave] = hits;
+    sc[wave] = cnt;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int A = 0, N = 0;
+    for (int w = 0; w < 16; ++w) {
+      A += sa[w];
+      N += sc[w];
+    }
+    correct[0] = static_cast<float>(A);
+    count[0] = static_cast<float>(N);
+    if (ratio) ratio[0] = static_cast<float>(A) / fmaxf(static_cast<float>(N), 1.0f);
+  }
+}
+
 __global__ void k_accuracy_ratio(const float* correct, const float* count, float* ratio) {
   ratio[0] = correct[0] / fmaxf(count[0], 1.0f);
 }
@@ -680,6 +724,11 @@ int rram_accuracy(const float* x, const float* label, float* correct, float* cou
   RRAM_REQUIRE(outer == 0 || (x && label), "accuracy: NULL");
   const int64_t cols = (int64_t)outer * inner;
   RRAM_REQUIRE(cols < (1ll << 24), "accuracy: more than 2^24 samples (float counts would round)");
+  if (cols <= kAccSmall) {
+    hipLaunchKernelGGL(k_accuracy_small, dim3(1), dim3(1024), 0, as_stream(s), x, label, correct, count, ratio,
+                       outer, C, inner, top_k, ignore);
+    return launch_status("accuracy");
+  }
   RRAM_HIP_RET(hipMemsetAsync(correct, 0, sizeof(float), as_stream(s)));
   RRAM_HIP_RET(hipMemsetAsync(count, 0, sizeof(float), as_stream(s)));
   if (cols > 0)

@@ -598,11 +598,13 @@ void MonteCarlo<Dtype>::Run(uint32_t map_begin, uint32_t map_count) {
     } else {
       net_->Forward(false);
     }
-    for (size_t k = 0; k < no; ++k) {
-      RRAM_CALL(rram_axpy(1, Dtype(1), outs_[k]->gpu_data(), d_sums_ + k, Caffe::stream()));
-      if (maps_run_ < max_maps_)
-        HIP_CALL(hipMemcpyAsync(d_per_map_ + (size_t)maps_run_ * no + k, outs_[k]->gpu_data(), sizeof(Dtype),
-                                hipMemcpyDeviceToDevice, Caffe::hip_stream()));
+    for (size_t k0 = 0; k0 < no; k0 += RRAM_MC_MAX_OUTPUTS) {
+      rram_mc_outputs mo{};
+      mo.n = static_cast<int>(std::min<size_t>(RRAM_MC_MAX_OUTPUTS, no - k0));
+      for (int k = 0; k < mo.n; ++k) mo.p[k] = outs_[k0 + k]->gpu_data();
+      RRAM_CALL(rram_mc_accumulate(&mo, d_sums_ + k0,
+                                   maps_run_ < max_maps_ ? d_per_map_ + (size_t)maps_run_ * no + k0 : nullptr,
+                                   Caffe::stream()));
     }
     ++maps_run_;
   }

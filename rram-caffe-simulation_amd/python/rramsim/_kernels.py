@@ -72,6 +72,7 @@ SIGNATURES = {
     "rram_inject_rng_batched": (I, [P, I, U64, U32, P, P]),
     "rram_threshold_strategy": (I, [P, I64, F, P, P]),
     "rram_stuck_zero_counts": (I, [P, P, I, I, P, P, P]),
+    "rram_mc_accumulate": (I, [P, P, P, P]),
     "rram_permute_rows": (I, [P, P, I64, P, P, I, P]),
     "rram_permute_cols": (I, [P, P, I, I, P, P, I, P]),
     "rram_permute_elems": (I, [P, P, P, P, I, P]),
