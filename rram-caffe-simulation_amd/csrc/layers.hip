@@ -484,36 +484,40 @@ __global__ void __launch_bounds__(256) k_accuracy(const float* __restrict__ x, c
     if (N) atomicAdd(count, static_cast<float>(N));
   }
 }
-// Single-launch form for up to kAccSmall columns (every TEST batch of the
-// configs): one block walks all columns, reduces in LDS and writes correct,
-// count and the ratio — no memsets, no atomics, no second launch.
+// Single-launch form for small heads (columns x classes <= kAccSmall, classes
+// <= 64: the configs' TEST batches of CIFAR / LeNet): one block, a thread per
+// column looping over the classes (independent loads, so one memory latency),
+// block reduction, then correct / count / ratio written directly — no memsets,
+// no atomics, no second launch.
 constexpr int kAccSmall = 1 << 16;
 __global__ void __launch_bounds__(1024) k_accuracy_small(const float* __restrict__ x, const float* __restrict__ label,
                                                          float* correct, float* count, float* ratio, int outer, int C,
                                                          int inner, int top_k, int ignore) {
   __shared__ int sa[16], sc[16];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int cols = outer * inner;
   int hits = 0, cnt = 0;
-  for (int col = wave; col < cols; col += 16) {
+  for (int col = threadIdx.x; col < cols; col += 1024) {
     const int o = col / inner, q = col - o * inner;
     const int lv = static_cast<int>(label[col]);
-    if (ignore >= 0 && lv == ignore) continue;  // wave-uniform
+    if (ignore >= 0 && lv == ignore) continue;
     const float* xs = x + (int64_t)o * C * inner + q;
     const float v = xs[(int64_t)lv * inner];
-    int rank = 0;
-    for (int c = lane; c < C; c += 64) {
+    int rank = 0;  // #classes ahead of the label in Caffe's (value, index) descending order
+    for (int c = 0; c < C; ++c) {
       const float u = xs[(int64_t)c * inner];
       rank += (u > v) || (u == v && c > lv);
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) rank += __shfl_xor(rank, off, 64);
     hits += rank < top_k;
     cnt += 1;
   }
-  if (lane == 0) {
-    sa[wave] = hits;
-    sc[wave] = cnt;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    hits += __shfl_xor(hits, off, 64);
+    cnt += __shfl_xor(cnt, off, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    sa[threadIdx.x >> 6] = hits;
+    sc[threadIdx.x >> 6] = cnt;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -724,7 +728,7 @@ int rram_accuracy(const float* x, const float* label, float* correct, float* cou
   RRAM_REQUIRE(outer == 0 || (x && label), "accuracy: NULL");
   const int64_t cols = (int64_t)outer * inner;
   RRAM_REQUIRE(cols < (1ll << 24), "accuracy: more than 2^24 samples (float counts would round)");
-  if (cols <= kAccSmall) {
+  if (cols * C <= kAccSmall && C <= 64) {
     hipLaunchKernelGGL(k_accuracy_small, dim3(1), dim3(1024), 0, as_stream(s), x, label, correct, count, ratio,
                        outer, C, inner, top_k, ignore);
     return launch_status("accuracy");

@@ -404,6 +404,34 @@ def test_im2col_col2im_vs_oracle(device, oracle_mod):
 
 
 # ---------------------------------------------------------- support layers
+@pytest.mark.parametrize("outer,C,inner,ignore", [(100, 10, 1, -1), (7, 10, 5, 3), (64, 64, 1, -1), (1, 2, 1, -1)])
+def test_accuracy_small_head_single_launch(device, oracle_mod, outer, C, inner, ignore):
+    """The one-block accuracy (classes <= 64) == the oracle, with ties, an ignore
+    label, spatial positions, and the ratio output (top-1 and top-3)."""
+    import torch
+    from rramsim import ops
+    rng = np.random.default_rng(outer + C)
+    x = rng.integers(-3, 4, (outer, C, inner)).astype(np.float32)   # many exact ties
+    label = rng.integers(0, C, (outer, inner)).astype(np.float32)
+    for k in (1, 3):
+        if k > C:
+            continue
+        cor, cnt, ratio = (torch.full((1,), -5.0, device=device) for _ in range(3))
+        ops.accuracy(T(x, device), T(label, device), cor, cnt, outer, C, inner, top_k=k, ignore=ignore, ratio=ratio)
+        hit = n = 0
+        for o in range(outer):
+            for q in range(inner):
+                lv = int(label[o, q])
+                if ignore >= 0 and lv == ignore:
+                    continue
+                col = x[o, :, q]
+                rank = int(np.sum((col > col[lv]) | ((col == col[lv]) & (np.arange(C) > lv))))
+                hit += rank < k
+                n += 1
+        assert int(N(cor)[0]) == hit and int(N(cnt)[0]) == n
+        assert abs(float(N(ratio)[0]) - hit / max(n, 1)) < 1e-6
+
+
 def test_pool_lrn_softmax_accuracy_vs_oracle(device, oracle_mod):
     import torch
     from rramsim import ops
