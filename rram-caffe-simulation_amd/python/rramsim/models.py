@@ -55,7 +55,8 @@ W1B2 = [dict(lr_mult=1, decay_mult=1), dict(lr_mult=2, decay_mult=0)]
 W1B2_NODECAY = [dict(lr_mult=1), dict(lr_mult=2)]
 
 
-def _data(p, scale=None, mean=False, crop=None, train_batch=64, test_batch=100, phases=("TRAIN", "TEST")):
+def _data(p, scale=None, mean=False, crop=None, train_batch=64, test_batch=100, phases=("TRAIN", "TEST"),
+          name="data"):
     for ph, bs in zip(("TRAIN", "TEST"), (train_batch, test_batch)):
         if ph not in phases:
             continue
@@ -67,7 +68,7 @@ def _data(p, scale=None, mean=False, crop=None, train_batch=64, test_batch=100, 
             tp["crop_size"] = crop
         if mean:
             tp["mean_file"] = "mean.binaryproto"
-        d = dict(name="data" if len(phases) == 1 else ("data" if ph == "TRAIN" else "data"), type="Data",
+        d = dict(name=name, type="Data",
                  top=["data", "label"], include=dict(phase=ph))
         if tp:
             d["transform_param"] = tp
@@ -133,7 +134,7 @@ def _heads(p, bottom, acc_top5=False):
 def lenet(train_batch=64, test_batch=100) -> str:
     """examples/mnist/lenet_train_test.prototxt (C1)."""
     p = _P("LeNet")
-    _data(p, scale=0.00390625, train_batch=train_batch, test_batch=test_batch)
+    _data(p, scale=0.00390625, train_batch=train_batch, test_batch=test_batch, name="mnist")
     _conv(p, "conv1", "data", 20, 5, param=W1B2_NODECAY)
     _pool(p, "pool1", "conv1", "MAX", 2, 2)
     _conv(p, "conv2", "pool1", 50, 5, param=W1B2_NODECAY)
@@ -148,7 +149,7 @@ def lenet(train_batch=64, test_batch=100) -> str:
 def cifar10_quick(train_batch=100, test_batch=100) -> str:
     """examples/cifar10/cifar10_quick_train_test.prototxt (C2)."""
     p = _P("CIFAR10_quick")
-    _data(p, mean=True, train_batch=train_batch, test_batch=test_batch)
+    _data(p, mean=True, train_batch=train_batch, test_batch=test_batch, name="cifar")
     g = lambda s: dict(type="gaussian", std=s)  # noqa: E731
     _conv(p, "conv1", "data", 32, 5, pad=2, wf=g(0.0001), param=W1B2_NODECAY)
     _pool(p, "pool1", "conv1", "MAX", 3, 2)
@@ -168,7 +169,7 @@ def cifar10_quick(train_batch=100, test_batch=100) -> str:
 def cifar10_full(train_batch=100, test_batch=100) -> str:
     """examples/cifar10/cifar10_full_train_test.prototxt (C4)."""
     p = _P("CIFAR10_full")
-    _data(p, mean=True, train_batch=train_batch, test_batch=test_batch)
+    _data(p, mean=True, train_batch=train_batch, test_batch=test_batch, name="cifar")
     g = lambda s: dict(type="gaussian", std=s)  # noqa: E731
     _conv(p, "conv1", "data", 32, 5, pad=2, wf=g(0.0001), param=W1B2_NODECAY)
     _pool(p, "pool1", "conv1", "MAX", 3, 2)
@@ -266,8 +267,10 @@ def _aux(p, idx, bottom):
     p.layer(name=f"{b}/drop_fc", type="Dropout", bottom=f"{b}/fc", top=f"{b}/fc",
             dropout_param=dict(dropout_ratio=0.7))
     _ip(p, f"{b}/classifier", f"{b}/fc", 1000, wf=x, bf=dict(type="constant", value=0), param=W1B2)
+    # the reference names both auxiliary loss tops "loss<k>/loss1"
+    # (models/bvlc_googlenet/train_val.prototxt), kept for log parity
     p.layer(name=f"{b}/loss", type="SoftmaxWithLoss", bottom=[f"{b}/classifier", "label"],
-            top=f"{b}/loss{idx}", loss_weight=0.3)
+            top=f"{b}/loss1", loss_weight=0.3)
     p.layer(name=f"{b}/top-1", type="Accuracy", bottom=[f"{b}/classifier", "label"], top=f"{b}/top-1",
             include=dict(phase="TEST"))
     p.layer(name=f"{b}/top-5", type="Accuracy", bottom=[f"{b}/classifier", "label"], top=f"{b}/top-5",
