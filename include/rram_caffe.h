@@ -149,6 +149,13 @@ int rram_caffemodel_describe(const char* caffemodel, char* out, size_t cap, size
 /* Host-only: parse a binary proto file and serialise it again
  * (kind 0 NetParameter, 1 SolverState, 2 BlobProtoVector). */
 int rram_proto_rewrite(const char* in_path, const char* out_path, int kind);
+/* Host-only: the fault-related fields of a SolverParameter text with
+ * caffe.proto's defaults applied, one tab-separated line each:
+ *   failure_pattern  type mean std neg zero pos
+ *   failure_strategy type threshold start period prune_order_file switch_time
+ *                    prune_net_file prune_model_file
+ *   solver           lr_policy base_lr max_iter snapshot snapshot_prefix */
+int rram_solver_describe(const char* solver_prototxt, char* out, size_t cap, size_t* needed);
 /* Host-only: n outputs of glibc's rand() after srand(seed) (the genetic
  * strategy's generator, strategy.cpp:170-175). */
 int rram_glibc_rand(uint32_t seed, int n, int* out);

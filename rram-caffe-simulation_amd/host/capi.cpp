@@ -1,6 +1,7 @@
 // extern "C" face of the host runtime (include/rram_caffe.h).  Exceptions
 // (the reference's fatal CHECKs) become status codes + a thread-local message.
 #include <cstring>
+#include <sstream>
 #include <string>
 
 #include "rram_caffe.h"
@@ -479,6 +480,37 @@ int rram_proto_rewrite(const char* in, const char* out, int kind) {
     else if (kind == 1) WriteFileBytes(out, SerializeSolverState(ParseSolverState(b)));
     else if (kind == 2) WriteFileBytes(out, SerializeBlobProtoVector(ParseBlobProtoVector(b)));
     else throw Error("rram_proto_rewrite: kind must be 0, 1 or 2");
+  });
+}
+int rram_solver_describe(const char* solver_prototxt, char* out, size_t cap, size_t* needed) {
+  return guarded([&] {
+    NEED(solver_prototxt);
+    const Msg sp = parse_prototxt(solver_prototxt);
+    std::ostringstream o;
+    o.precision(9);
+    // caffe.proto defaults (FailurePatternParameter :252-262, FailureProbParameter :264-268,
+    // FailureStrategyParameter :271-290)
+    if (const Msg* fp = sp.sub("failure_pattern")) {
+      const Msg& pr = fp->sub_or_empty("failure_prob");
+      o << "failure_pattern\t" << fp->str("type", "gaussian") << '\t' << fp->num("mean", 10000) << '\t'
+        << fp->num("std", 100) << '\t' << pr.integer("neg", 10) << '\t' << pr.integer("zero", 20) << '\t'
+        << pr.integer("pos", 10) << '\n';
+    }
+    for (const Msg* st : sp.subs("failure_strategy")) {
+      o << "failure_strategy\t" << st->str("type") << '\t' << st->num("threshold", 0.001) << '\t'
+        << st->integer("start", 0) << '\t' << st->integer("period", 100) << '\t' << st->str("prune_order_file")
+        << '\t' << st->integer("switch_time", 100) << '\t' << st->str("prune_net_file") << '\t'
+        << st->str("prune_model_file") << '\n';
+    }
+    o << "solver\t" << sp.str("lr_policy", "fixed") << '\t' << sp.num("base_lr", 0.01) << '\t'
+      << sp.integer("max_iter", 0) << '\t' << sp.integer("snapshot", 0) << '\t' << sp.str("snapshot_prefix") << '\n';
+    const std::string d = o.str();
+    if (needed) *needed = d.size() + 1;
+    if (out && cap > 0) {
+      const size_t k = std::min(d.size(), cap - 1);
+      std::memcpy(out, d.data(), k);
+      out[k] = '\0';
+    }
   });
 }
 int rram_glibc_rand(uint32_t seed, int n, int* out) {

@@ -74,6 +74,7 @@ SIGNATURES = {
     "rram_caffemodel_describe": (I, [C.c_char_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "rram_proto_rewrite": (I, [C.c_char_p, C.c_char_p, I]),
     "rram_glibc_rand": (I, [U32, I, PI]),
+    "rram_solver_describe": (I, [C.c_char_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "rram_mc_create": (I, [P, P, I, U64, I, PP]),
     "rram_mc_destroy": (I, [P]),
     "rram_mc_run": (I, [P, U32, U32]),
@@ -170,6 +171,17 @@ def proto_rewrite(src: str, dst: str, kind: str = "net"):
     """Host-only: parse a binary proto and serialise it again (net | solverstate | blobs)."""
     k = {"net": 0, "solverstate": 1, "blobs": 2}[kind]
     check(load().rram_proto_rewrite(str(src).encode(), str(dst).encode(), k), "proto_rewrite")
+
+
+def solver_describe(solver_prototxt: str) -> List[List[str]]:
+    """Host-only: the failure_pattern / failure_strategy / solver key fields of
+    a SolverParameter text as this build parses them (caffe.proto defaults applied)."""
+    lib = load()
+    need = C.c_size_t()
+    check(lib.rram_solver_describe(solver_prototxt.encode(), None, 0, C.byref(need)), "solver_describe")
+    buf = C.create_string_buffer(need.value)
+    check(lib.rram_solver_describe(solver_prototxt.encode(), buf, need.value, None), "solver_describe")
+    return [line.split("\t") for line in buf.value.decode().splitlines()]
 
 
 def glibc_rand(seed: int, n: int) -> List[int]:

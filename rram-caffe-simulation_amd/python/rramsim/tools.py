@@ -43,6 +43,44 @@ def write_prune_order_file(path: str, orders: Sequence[np.ndarray]) -> None:
             wf.write("\n")
 
 
+def experiment_solver(template: str, mean: float, std: float, threshold: float = 0.0, remapping: str = "",
+                      genetic: str = "", prob: int = -1, snapshot_prefix: str = "") -> str:
+    """SolverParameter text for one fault experiment, as
+    examples/cifar10/gaussian_failure/run_gaussian_exp.py:50-103 derives it from
+    a template: failure_pattern mean/std; `threshold` > 0 appends a threshold
+    strategy; `remapping` = "order_file[,period[,start]]"; `genetic` =
+    "prune_net,prune_model[,switch_time[,period[,start]]]"; `prob` >= 0 sets the
+    stuck-at split to (prob, 100 - 2 prob, prob)."""
+    lines = [l for l in template.splitlines()
+             if not l.strip().startswith(("failure_pattern", "snapshot_prefix"))]
+    text = "\n".join(lines)
+    fp = f"failure_pattern {{ mean: {mean} std: {std}"
+    if prob >= 0:
+        assert prob < 50
+        fp += f" failure_prob {{ neg: {prob} zero: {100 - 2 * prob} pos: {prob} }}"
+    out = [text, fp + " }"]
+    if snapshot_prefix:
+        out.append(f'snapshot_prefix: "{snapshot_prefix}/"')
+    if threshold > 0:
+        out.append(f'failure_strategy {{ type: "threshold" threshold: {threshold} }}')
+    if remapping:
+        st = remapping.split(",")
+        s_ = f'failure_strategy {{ type: "remapping" prune_order_file: "{st[0]}"'
+        if len(st) > 1:
+            s_ += f" period: {int(st[1])}"
+        if len(st) > 2:
+            s_ += f" start: {int(st[2])}"
+        out.append(s_ + " }")
+    if genetic:
+        st = genetic.split(",")
+        s_ = f'failure_strategy {{ type: "genetic" prune_net_file: "{st[0]}" prune_model_file: "{st[1]}"'
+        for k, key in ((2, "switch_time"), (3, "period"), (4, "start")):
+            if len(st) > k:
+                s_ += f" {key}: {int(st[k])}"
+        out.append(s_ + " }")
+    return "\n".join(out) + "\n"
+
+
 def _fc_weights_of(prototxt_path: str, caffemodel: str, options=None) -> List[np.ndarray]:
     """FC weight matrices ("fc*" layers with params, net order) of a TEST net."""
     from . import caffe

@@ -31,3 +31,25 @@ def test_magnitude_prune_ratio_edges():
     assert not tools.magnitude_prune(w, 1.0).any()
     p = tools.magnitude_prune(-w, 0.3)              # int(10 * 0.3) = 3 smallest |w|
     assert np.array_equal(p.ravel()[:3], [0, 0, 0]) and (p.ravel()[3:] != 0).all()
+
+
+def test_experiment_solver_like_run_gaussian_exp():
+    """run_gaussian_exp.py:50-103 semantics through this build's solver parser
+    (caffe.proto defaults applied by rram_solver_describe)."""
+    from rramsim import caffe, models, tools
+    tpl = models.solver(base_lr=0.005, lr_policy="step", stepsize=10000, gamma=0.1, max_iter=50000,
+                        failure_mean=1.0, failure_std=1.0)
+    txt = tools.experiment_solver(tpl, 5e6, 1.5e6, threshold=1e-3, remapping="order.txt,50,1000",
+                                  genetic="pnet.prototxt,pmodel.caffemodel,300", prob=5, snapshot_prefix="snap")
+    rows = caffe.solver_describe(txt)
+    fp = [r for r in rows if r[0] == "failure_pattern"]
+    assert len(fp) == 1 and fp[0][1:] == ["gaussian", "5000000", "1500000", "5", "90", "5"]
+    st = [r[1:] for r in rows if r[0] == "failure_strategy"]
+    assert st[0][:2] == ["threshold", "0.001"]
+    assert st[1] == ["remapping", "0.001", "1000", "50", "order.txt", "100", "", ""]
+    assert st[2] == ["genetic", "0.001", "0", "100", "", "300", "pnet.prototxt", "pmodel.caffemodel"]
+    sv = [r for r in rows if r[0] == "solver"][0]
+    assert sv[1:] == ["step", "0.005", "50000", "0", "snap/"]
+    # defaults with no failure_prob: (10, 20, 10) (caffe.proto:264-268)
+    rows = caffe.solver_describe(tools.experiment_solver(tpl, 100.0, 10.0))
+    assert [r for r in rows if r[0] == "failure_pattern"][0][4:] == ["10", "20", "10"]
