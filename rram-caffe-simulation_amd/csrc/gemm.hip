@@ -739,6 +739,12 @@ int launch(const Params& P, int gz, hipStream_t s, bool force_big) {
     return e ? atoi(e) : 0;
   }();
   if (forced == 6464) return launch_cfg<2, 2, 1, 1, AM, BMODE, OM, KB>(P, gz, s);
+  // thin M (CIFAR / LeNet convolutions, M = 20..32): a 32 x 128 tile wastes no
+  // MFMA rows (64 x 64 would pad half of them)
+  if constexpr (KB == 32) {
+    if (P.M <= 32 && forced != 64 && forced != 96 && forced != 128 && forced != 192)
+      return launch_cfg<1, 4, 1, 1, AM, BMODE, OM, KB>(P, gz, s);
+  }
   const int64_t ntn = (P.N + 127) / 128;
   const int cands[4] = {128, 192, 96, 64};  // ties keep 128 (2 blocks per CU)
   int best = 0;
