@@ -43,7 +43,11 @@ constexpr int ldk_of() { return KB + 4; }
 // CONVT = CONV with a per-k offset/tap table (conv_table below) read by scalar
 // loads: no (c, kh, kw) stepping and no multiplies in the gather.
 // CONVT64: the same with a 64-bit tap mask (kh*kw <= 63, e.g. 7 x 7 with padding)
-enum Mode : int { KC = 0, RC = 1, CONV = 2, NCHW = 3, NCHWT = 4, KCV = 5, CONVT = 6, CONVT64 = 7 };
+// KCU = KC with 16-byte raw buffer loads at any 4-byte alignment (row stride K
+// not a multiple of 4, e.g. AlexNet conv1 K = 363): a float4 may run into the
+// next row (or past the buffer end, where the per-dword range check returns
+// 0); the elements at k >= K are zeroed when the tile is written to LDS.
+enum Mode : int { KC = 0, RC = 1, CONV = 2, NCHW = 3, NCHWT = 4, KCV = 5, CONVT = 6, CONVT64 = 7, KCU = 8 };
 enum OutMode : int { OUT_ROWMAJOR = 0, OUT_NCHW = 1 };
 
 // Fast unsigned division by a runtime constant (x < 2^31).
@@ -126,6 +130,7 @@ template <int ROWS, int KB>
 struct Loader {
   static constexpr int EPT = ROWS * KB / 256;
   float v[EPT];
+  int kn[EPT / 4 > 0 ? EPT / 4 : 1];  // KCU: valid elements of float4 i (K - k, may be <= 0 or >= 4)
 };
 
 // Branch-free guarded loads: an out-of-range element loads from the view's
@@ -192,6 +197,33 @@ __device__ __forceinline__ void load_tile(Loader<ROWS, KB>& L, const View& vw, c
       L.v[4 * i + 1] = x.y;
       L.v[4 * i + 2] = x.z;
       L.v[4 * i + 3] = x.w;
+    }
+    return;
+  }
+  if (MODE == KCU) {
+    // float4 q -> (row = q / (KB/4), k4 = q % (KB/4)) as KCV, but the row
+    // stride is only 4-byte aligned: raw buffer loads over the operand
+    // (uniform descriptor, exact byte range), rows past the view get an
+    // all-ones offset (out of range: zeros)
+    const uint32_t range = static_cast<uint32_t>(((int64_t)(vw.rows - 1) * vw.ld + vw.kdim) * 4);
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(vw.p), 0, static_cast<int>(range), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < EPT / 4; ++i) {
+      const int q = threadIdx.x + i * 256;
+      const int r = q / (KB / 4);
+      const int k = k0 + 4 * (q % (KB / 4));
+      const bool ok = row0 + r < vw.rows;
+      const uint32_t off = static_cast<uint32_t>(((int64_t)(row0 + r) * vw.ld + k) * 4) | (ok ? 0u : 0xFFFFFFFFu);
+      // whole-vector bit cast: extracting the u32 lanes one by one made this
+      // ROCm 7.2 clang shrink the load to one dword while still reading
+      // four registers (observed on gfx950)
+      const floatx4 x = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0));
+      L.v[4 * i] = x.x;
+      L.v[4 * i + 1] = x.y;
+      L.v[4 * i + 2] = x.z;
+      L.v[4 * i + 3] = x.w;
+      L.kn[i] = kend - k;
     }
     return;
   }
@@ -278,7 +310,7 @@ __device__ __forceinline__ void load_tile(Loader<ROWS, KB>& L, const View& vw, c
 // global load instructions one thread issues per K-tile
 template <int MODE, int ROWS, int KB>
 constexpr int vmem_per_tile() {
-  return MODE == KCV ? Loader<ROWS, KB>::EPT / 4 : Loader<ROWS, KB>::EPT;
+  return (MODE == KCV || MODE == KCU) ? Loader<ROWS, KB>::EPT / 4 : Loader<ROWS, KB>::EPT;
 }
 
 template <int MODE, int ROWS, int KB>
@@ -292,6 +324,19 @@ __device__ __forceinline__ void store_tile(const Loader<ROWS, KB>& L, float* lds
 #pragma unroll
     for (int i = 0; i < EPT / 4; ++i)
       *reinterpret_cast<float4*>(dst + 4 * i) = make_float4(L.v[4 * i], L.v[4 * i + 1], L.v[4 * i + 2], L.v[4 * i + 3]);
+    return;
+  }
+  if (MODE == KCU) {
+    // the K tail (and the next row's elements a float4 ran into) become 0;
+    // selected here, after the MFMAs, so the loads are not waited on early
+#pragma unroll
+    for (int i = 0; i < EPT / 4; ++i) {
+      const int q = threadIdx.x + i * 256;
+      const int n = L.kn[i];
+      *reinterpret_cast<float4*>(lds + (q / (KB / 4)) * LDK + 4 * (q % (KB / 4))) =
+          make_float4(n > 0 ? L.v[4 * i] : 0.0f, n > 1 ? L.v[4 * i + 1] : 0.0f, n > 2 ? L.v[4 * i + 2] : 0.0f,
+                      n > 3 ? L.v[4 * i + 3] : 0.0f);
+    }
     return;
   }
   if (MODE == KCV) {
@@ -794,6 +839,7 @@ int dispatch(int am, int bm, int om, const Params& P, int gz, hipStream_t s, boo
   if (bm == CONVT && om == OUT_NCHW && conv_kb(P.K) == 16) {
     if (am == KC) return launch<KC, CONVT, OUT_NCHW, 16>(P, gz, s, force_big);
     if (am == KCV) return launch<KCV, CONVT, OUT_NCHW, 16>(P, gz, s, force_big);
+    if (am == KCU) return launch<KCU, CONVT, OUT_NCHW, 16>(P, gz, s, force_big);
   }
   if (bm == CONVT64 && om == OUT_NCHW && conv_kb(P.K) == 16) {
     if (am == KC) return launch<KC, CONVT64, OUT_NCHW, 16>(P, gz, s, force_big);
@@ -814,6 +860,7 @@ int dispatch(int am, int bm, int om, const Params& P, int gz, hipStream_t s, boo
   RRAM_D(KCV, CONV, OUT_NCHW)
   RRAM_D(KC, CONVT, OUT_NCHW)
   RRAM_D(KCV, CONVT, OUT_NCHW)
+  RRAM_D(KCU, CONVT, OUT_NCHW)
   RRAM_D(KC, CONVT64, OUT_NCHW)
   RRAM_D(KCV, CONVT64, OUT_NCHW)
   RRAM_D(NCHW, KC, OUT_ROWMAJOR)
@@ -993,7 +1040,13 @@ int conv_fwd_core(const rram_conv_desc* d, const float* x, const float* w, const
     cv.taps = padded ? taps : 0;
     if (cv.tbl) bmode = wide ? CONVT64 : CONVT;
   }
-  return dispatch(vec_ok(w, K, K, P.grp_a) ? KCV : KC, bmode, OUT_NCHW, P, g, s);
+  // A: 16-byte loads when the rows are 16-byte aligned; else (K % 4 != 0) the
+  // unaligned raw-buffer form for the table gather (RRAM_CONV_NO_KCU: scalar)
+  int amode = vec_ok(w, K, K, P.grp_a) ? KCV : KC;
+  if (amode == KC && bmode == CONVT && (reinterpret_cast<uintptr_t>(w) & 3u) == 0 &&
+      (int64_t)g * cout_g * K * 4 < (1ll << 31) && getenv("RRAM_CONV_NO_KCU") == nullptr)
+    amode = KCU;
+  return dispatch(amode, bmode, OUT_NCHW, P, g, s);
 }
 
 // Split-K factor of the weight-gradient GEMM: M = Cout/g and N = Cin/g*kh*kw

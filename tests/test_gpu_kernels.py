@@ -347,6 +347,31 @@ def test_conv_fwd_vs_oracle(device, oracle_mod, cs):
     np.testing.assert_allclose(N(y), np.maximum(ref, 0), atol=1e-4, rtol=1e-4)
 
 
+@pytest.mark.parametrize("cs", [CONV_CASES[0], CONV_CASES[1], CONV_CASES[4], CONV_CASES[12]])
+def test_conv_fwd_unaligned_weights_nan_tail(device, oracle_mod, cs):
+    """K % 4 != 0 (the unaligned 16-byte weight loader): the weights sit at a
+    4-byte (not 16-byte) offset inside a NaN-filled buffer, so a float4 that
+    runs past a row / group / the tensor end reads NaN; those lanes must be
+    zeroed, and the last row's valid elements must survive the range check."""
+    import torch
+    from rramsim import ops
+    rng = np.random.default_rng(7)
+    x = rng.standard_normal(cs["x"]).astype(np.float32)
+    w = (rng.standard_normal((cs["cout"], cs["x"][1] // cs["g"], cs["k"], cs["k"])) * 0.1).astype(np.float32)
+    b = rng.standard_normal(cs["cout"]).astype(np.float32)
+    d = ops.conv_desc(cs["x"], cs["cout"], cs["k"], cs["s"], cs["p"], cs["d"], cs["g"])
+    big = torch.full((w.size + 9,), float("nan"), device=device)
+    big[1:1 + w.size] = T(w.ravel(), device)
+    wv = big[1:1 + w.size].view(w.shape)
+    y = torch.empty((cs["x"][0], cs["cout"], d.out_h, d.out_w), device=device)
+    ops.conv2d_fwd(d, T(x, device), wv, T(b, device), y)
+    if np.prod(cs["x"]) * cs["cout"] * cs["k"] ** 2 < 5e7:
+        ref = oracle_mod.conv_naive(x, w, b, cs["s"], cs["p"], cs["d"], cs["g"])
+    else:
+        ref = oracle_mod.conv_im2col(x, w, b, cs["s"], cs["p"], cs["d"], cs["g"])
+    np.testing.assert_allclose(N(y), ref, atol=1e-4, rtol=1e-4)
+
+
 @pytest.mark.parametrize("cs", CONV_CASES[:4] + [CONV_CASES[8]])
 def test_conv_bwd_vs_torch(device, cs):
     import torch
