@@ -361,8 +361,18 @@ __device__ __forceinline__ float pick(const float4& q, int s) {
   return (s & 3) == 0 ? q.x : (s & 3) == 1 ? q.y : (s & 3) == 2 ? q.z : q.w;
 }
 
+// Occupancy target 4 waves per SIMD: the 128 x 128 / KB = 16 conv tile then
+// keeps its accumulators in VGPRs (116 VGPRs, no AGPRs, no spills) instead of
+// 80 VGPRs + 64 AGPRs at 3 waves; 4 blocks x 40 KB fill the 160 KB LDS.
+// Measured on MI355X (scripts/gpu_variants.sh): AlexNet b256 GEMMs 3.760 ->
+// 3.667 ms.  RRAM_V_WPE_OFF builds the compiler's own choice for A/B runs.
+#ifndef RRAM_V_WPE_OFF
+#define RRAM_GEMM_OCC __attribute__((amdgpu_waves_per_eu(4)))
+#else
+#define RRAM_GEMM_OCC
+#endif
 template <int WM, int WN, int MI, int NI, int AM, int BMODE, int OM, int KB>
-__global__ void __launch_bounds__(256) k_gemm(Params P) {
+__global__ void __launch_bounds__(256) RRAM_GEMM_OCC k_gemm(Params P) {
   constexpr int BMr = WM * MI * 32;
   constexpr int BNr = WN * NI * 32;
   constexpr int LDK = ldk_of<KB>();
