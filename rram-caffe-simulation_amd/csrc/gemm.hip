@@ -379,8 +379,19 @@ __global__ void __launch_bounds__(256) RRAM_GEMM_OCC k_gemm(Params P) {
   static_assert(WM * WN == 4, "4 waves per block");
   static_assert(KB == 16 || KB == 32, "K-tile depth");
   static_assert(BMr * KB % 1024 == 0 && BNr * KB % 1024 == 0, "tile/threads");
-  __shared__ __attribute__((aligned(16))) float As[2][BMr * LDK];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BNr * LDK];
+  // Table-gather convolutions with 32-deep K-tiles (AlexNet conv1, the CIFAR /
+  // LeNet convolutions) use ONE LDS buffer: two barriers per K-tile, but half
+  // the LDS, so 4 blocks per CU instead of 2 hide the strided gather's latency
+  // (MI355X: conv1 0.720 -> 0.672 ms).  The IP GEMMs measured slower that way
+  // (VGPR spills at 4 waves) and the 16-deep tiles already fit 4 blocks.
+  // RRAM_V_DOUBLE keeps every kernel double-buffered for A/B runs.
+#ifndef RRAM_V_DOUBLE
+  constexpr int NBUF = (KB == 32 && (BMODE == CONVT || BMODE == CONVT64)) ? 1 : 2;
+#else
+  constexpr int NBUF = 2;
+#endif
+  __shared__ __attribute__((aligned(16))) float As[NBUF][BMr * LDK];
+  __shared__ __attribute__((aligned(16))) float Bs[NBUF][BNr * LDK];
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -499,7 +510,7 @@ __global__ void __launch_bounds__(256) RRAM_GEMM_OCC k_gemm(Params P) {
   (void)lane;  // measured 6 % slower than the 32x32x2 form on AlexNet b256 (scripts/gpu_variants.sh)
 #endif
   for (int t = 0; t < ntiles; ++t) {
-    const int cur = t & 1;
+    const int cur = NBUF == 2 ? (t & 1) : 0;
     const bool more = (t + 1) < ntiles;
 #ifdef RRAM_V_PRIO
     __builtin_amdgcn_s_setprio(1);
@@ -581,9 +592,10 @@ __global__ void __launch_bounds__(256) RRAM_GEMM_OCC k_gemm(Params P) {
 #ifdef RRAM_V_PRIO
     __builtin_amdgcn_s_setprio(0);
 #endif
+    if (NBUF == 1) __syncthreads();  // every wave is done reading the single buffer
     if (more) {
-      store_tile<AM, BMr, KB>(la, As[cur ^ 1]);
-      store_tile<BMODE, BNr, KB>(lb, Bs[cur ^ 1]);
+      store_tile<AM, BMr, KB>(la, As[NBUF == 2 ? cur ^ 1 : 0]);
+      store_tile<BMODE, BNr, KB>(lb, Bs[NBUF == 2 ? cur ^ 1 : 0]);
     }
     __syncthreads();
   }
