@@ -33,9 +33,8 @@ template <int K, int SIZE, int G>
 __global__ void __launch_bounds__(256)
     k_lrn_maxpool_band(const float* __restrict__ x, float* __restrict__ y, int C, int H, int W, int PH, int PW,
                        int sh, int sw, int ph, int pw, int RB, float alpha_over_size, float beta, float k) {
-  constexpr int PRE = (SIZE - 1) / 2, POST = SIZE - PRE - 1;
+  constexpr int PRE = (SIZE - 1) / 2;
   constexpr int D = G;
-  constexpr int R = SIZE + 2 * D;  // ring: the SIZE-window, this group's D new channels, the next group's
   constexpr int PPT = kBandPix / 256;
   __shared__ float ybuf[2][D][kBandPix];
   const int n = blockIdx.y;
@@ -54,8 +53,14 @@ __global__ void __launch_bounds__(256)
     own[q] = pix[q] < NP;
   }
   auto ld = [&](int q, int cc) { return (cc >= 0 && cc < C && own[q]) ? xb[(int64_t)cc * HW + pix[q]] : 0.0f; };
-  // win[q][j] = x at channel (c0 - PRE + j) of pixel q, zero outside [0, C)
-  float win[PPT][R];
+  // win[q][j] = x at channel (c0 - PRE + j) of pixel q, zero outside [0, C).
+  // The entering channels of group g + 2 are loaded at the top of group g
+  // into one of two staging arrays (st0 / st1, alternating by group parity so
+  // the registers are named statically) and moved into the ring at the bottom
+  // of group g + 1: two groups of loads stay in flight across the LDS / pool
+  // work, instead of one group whose loads the ring shift waits for.
+  float win[PPT][SIZE + D];
+  float st0[D][PPT], st1[D][PPT];
   float acc[PPT];
 #pragma unroll
   for (int q = 0; q < PPT; ++q) {
@@ -65,6 +70,10 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
     for (int j = PRE; j < SIZE; ++j) acc[q] = lrn_sq_add(acc[q], win[q][j]);
   }
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+#pragma unroll
+    for (int q = 0; q < PPT; ++q) st1[d][q] = ld(q, SIZE + D - PRE + d);  // group 1's entering channels
   const int NO = (pr1 - pr0) * PW;  // pooled outputs of the band per channel
   const int64_t PHW = (int64_t)PH * PW;
   float* yn = y + (int64_t)n * C * PHW;
@@ -95,13 +104,12 @@ __global__ void __launch_bounds__(256)
     it_out[i] = (pr0 + prl) * PW + pwi;
     it_ok[i] = ok;
   }
-  for (int c0 = 0, g = 0; c0 < C; c0 += D, ++g) {
-    // next group's entering channels, in flight during this group's work
+  // one channel group: c0 = its first channel, yb = its LDS plane buffer
+  auto group = [&](int c0, float (*yb)[kBandPix], float (&load_into)[D][PPT], const float (&fill_from)[D][PPT]) {
 #pragma unroll
     for (int d = 0; d < D; ++d)
 #pragma unroll
-      for (int q = 0; q < PPT; ++q) win[q][SIZE + D + d] = ld(q, c0 + D + POST + 1 + d);
-    float(*yb)[kBandPix] = ybuf[g & 1];
+      for (int q = 0; q < PPT; ++q) load_into[d][q] = ld(q, c0 - PRE + SIZE + 2 * D + d);
 #pragma unroll
     for (int d = 0; d < D; ++d) {
 #pragma unroll
@@ -134,9 +142,16 @@ __global__ void __launch_bounds__(256)
       }
     }
 #pragma unroll
-    for (int q = 0; q < PPT; ++q)
+    for (int q = 0; q < PPT; ++q) {
 #pragma unroll
-      for (int j = 0; j < SIZE + D; ++j) win[q][j] = win[q][j + D];
+      for (int j = 0; j < SIZE; ++j) win[q][j] = win[q][j + D];
+#pragma unroll
+      for (int d = 0; d < D; ++d) win[q][SIZE + d] = fill_from[d][q];
+    }
+  };
+  for (int c0 = 0; c0 < C; c0 += 2 * D) {
+    group(c0, ybuf[0], st0, st1);
+    if (c0 + D < C) group(c0 + D, ybuf[1], st1, st0);
   }
 }
 
