@@ -131,7 +131,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--profile-layers", action="store_true", help="print the per-layer table to stderr")
     ap.add_argument("--workload", default="alexnet_mc",
-                    choices=["alexnet_mc", "cifar10_quick_mc", "cifar10_full_train", "googlenet_sweep", "lenet_train"],
+                    choices=["alexnet_mc", "cifar10_quick_mc", "cifar10_full_train", "googlenet_sweep", "lenet_train",
+                             "lenet_mc"],
                     help="alexnet_mc is the headline (BASELINE.json metric); the others are the remaining configs")
     args = ap.parse_args()
 

@@ -11,6 +11,10 @@ barrier + synchronize, max over ranks, whole-job throughput.
   googlenet_sweep    C5: GoogLeNet b256 inference sweep over fault rate
                      0.1 .. 10 %, per-layer SA0/SA1 (neg/zero/pos) ratios
   lenet_train        C1's net (LeNet, stuck-at faults) trained on the GPU
+  lenet_mc           C1: LeNet stuck-at Monte-Carlo fault maps (1 map = one
+                     100-image batch), with the Caffe-CPU-mode restatement
+                     (oracle inject + per-image im2col + OpenBLAS sgemm) timed
+                     beside it on rank 0 at N = 1
 """
 from __future__ import annotations
 
@@ -46,6 +50,58 @@ def _base(metric, unit, value, world, args, el, dtype="f32", **cfg):
             "scaling": "weak", "vs_baseline": None, "dtype": dtype, "data": "synthetic", "config": cfg}
 
 
+def lenet_cpu_baseline(batch, p_fault, seed, budget_s=10.0):
+    """Caffe CPU mode for C1 (restated in oracle/): one stuck-at map injected
+    into LeNet's 405,510 IP weights by the scalar C oracle, then single-image
+    forwards (im2col + sgemm per conv, as conv_layer.cpp:7-27) until the budget
+    is spent; images/s extrapolated to one `batch`-image map."""
+    import os
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "oracle"))
+    import numpy as np
+    import oracle
+    from rramsim import make_inject_cfg
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("internal_api") == "openblas"]
+                      or [1])
+    except Exception:  # pragma: no cover
+        threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    rng = np.random.default_rng(seed)
+    w1 = (rng.standard_normal((20, 1, 5, 5)) * 0.1).astype(np.float32)
+    w2 = (rng.standard_normal((50, 20, 5, 5)) * 0.05).astype(np.float32)
+    b1, b2 = np.zeros(20, np.float32), np.zeros(50, np.float32)
+    fw = {"ip1": (rng.standard_normal((500, 800)) * 0.05).astype(np.float32),
+          "ip2": (rng.standard_normal((10, 500)) * 0.05).astype(np.float32)}
+    fb = {"ip1": np.zeros(500, np.float32), "ip2": np.zeros(10, np.float32)}
+    c = make_inject_cfg(p_fault)
+    oc = oracle.InjectCfg(c.thr_fault, c.thr_neg, c.thr_zero, c.thr_sa1, 1.0, 0.0, 0, 0.0, 0, 0)
+    t0 = time.perf_counter()
+    for lid, k in enumerate(fw):
+        fw[k], _ = oracle.inject(fw[k], oc, seed, 0, 2 * lid)
+        fb[k], _ = oracle.inject(fb[k], oc, seed, 0, 2 * lid + 1)
+    t_inject = time.perf_counter() - t0
+    x_all = (rng.integers(0, 256, (batch, 1, 28, 28)) * 0.00390625).astype(np.float32)
+
+    def fwd(x):
+        y = oracle.pool(oracle.conv_im2col(x, w1, b1), 2, 2)
+        y = oracle.pool(oracle.conv_im2col(y, w2, b2), 2, 2).reshape(x.shape[0], -1)
+        y = np.maximum(y @ fw["ip1"].T + fb["ip1"], 0)
+        return oracle.softmax(y @ fw["ip2"].T + fb["ip2"])
+
+    n, t1 = 0, time.perf_counter()
+    while n < 2 or (time.perf_counter() - t1 < budget_s and n < 200 * batch):
+        fwd(x_all[n % batch:n % batch + 1])
+        n += 1
+    t_img = (time.perf_counter() - t1) / n
+    return {"value": round(batch / (t_inject + batch * t_img), 3), "unit": "images/s", "cores": threads,
+            "kind": "port",
+            "sample": f"1 fault map (C oracle inject of 405,510 IP weights: {t_inject * 1e3:.1f} ms) + {n} "
+                      f"single-image LeNet forwards (im2col + OpenBLAS sgemm: {t_img * 1e3:.3f} ms/img), "
+                      f"extrapolated to one {batch}-image map"}
+
+
 def run_workload(args, world, rank, dev):
     import torch
     import torch.distributed as dist
@@ -76,6 +132,27 @@ def run_workload(args, world, rank, dev):
         res["mc_mean_outputs"] = [x / max(tot[-1], 1) for x in tot[:-1]]
         mc.close()
         net.close()
+        return res
+
+    if args.workload == "lenet_mc":
+        batch = 100
+        net = caffe.Net(models.lenet(test_batch=batch), "test", models.net_options("lenet"))
+        mc = caffe.MonteCarlo(net, make_inject_cfg(args.p_fault), seed=args.seed,
+                              max_maps=(args.steps + args.warmup) * 10 + 8)
+        maps_per_step = 10
+        el = _timed(world, dev, lambda i: mc.run((rank + world * i) * maps_per_step, maps_per_step),
+                    args.steps, args.warmup)
+        st = mc.stats()
+        tot = allreduce_stats(st["sums"] + [st["maps"]], dev)
+        n_img = world * args.steps * maps_per_step * batch
+        res = _base("Monte Carlo fault-map inferences/sec, LeNet stuck-at", "images/s", n_img / el, world, args, el,
+                    workload="lenet_mc_stuckat", model="LeNet (lenet_train_test TEST)", global_batch=batch * world,
+                    maps_per_step=maps_per_step * world, p_fault=args.p_fault)
+        res["mc_mean_outputs"] = [x / max(tot[-1], 1) for x in tot[:-1]]
+        mc.close()
+        net.close()
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = lenet_cpu_baseline(batch, args.p_fault, args.seed)
         return res
 
     if args.workload in ("cifar10_full_train", "lenet_train"):
