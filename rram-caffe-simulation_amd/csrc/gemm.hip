@@ -179,6 +179,25 @@ __device__ __forceinline__ void tile_coord(int e, int& row, int& k) {
   }
 }
 
+// float4 q of a KCV tile -> (row, float4 column).  With 16-deep K-tiles a row
+// is 4 float4 and LDK = 20 dwords, so 16 consecutive lanes on 4 consecutive
+// rows span 80 dwords and wrap onto the same banks (2-way conflicts on every
+// ds_write_b128 of the tile, measured as ~20 % of the LDS cycles of the KB = 16
+// GEMMs).  Lanes are instead dealt to rows b, b+4, b+8, b+12 of a 16-row block
+// (20 * 4 = 80 = 16 mod 64: disjoint bank quads); a wave still covers the same
+// 16 rows, so the global loads touch the same cache lines.
+template <int ROWS, int KB>
+__device__ __forceinline__ void kcv_coord(int q, int& r, int& k4) {
+  if (KB == 16 && ROWS % 16 == 0) {
+    const int g = q >> 4;
+    r = (g >> 2) * 16 + ((q >> 2) & 3) * 4 + (g & 3);
+    k4 = q & 3;
+  } else {
+    r = q / (KB / 4);
+    k4 = q % (KB / 4);
+  }
+}
+
 template <int MODE, int ROWS, int KB>
 __device__ __forceinline__ void load_tile(Loader<ROWS, KB>& L, const View& vw, const ConvGeom& cv,
                                           const ConvCol& col, int row0, int k0, int kend) {
@@ -189,8 +208,9 @@ __device__ __forceinline__ void load_tile(Loader<ROWS, KB>& L, const View& vw, c
 #pragma unroll
     for (int i = 0; i < EPT / 4; ++i) {
       const int q = threadIdx.x + i * 256;
-      const int r = q / (KB / 4);
-      const int k = k0 + 4 * (q % (KB / 4));
+      int r, k4;
+      kcv_coord<ROWS, KB>(q, r, k4);
+      const int k = k0 + 4 * k4;
       const bool ok = row0 + r < vw.rows && k < kend;
       const float4 x = *reinterpret_cast<const float4*>(ok ? vw.p + (int64_t)(row0 + r) * vw.ld + k : g_zero4);
       L.v[4 * i] = x.x;
@@ -343,7 +363,9 @@ __device__ __forceinline__ void store_tile(const Loader<ROWS, KB>& L, float* lds
 #pragma unroll
     for (int i = 0; i < EPT / 4; ++i) {
       const int q = threadIdx.x + i * 256;
-      *reinterpret_cast<float4*>(lds + (q / (KB / 4)) * LDK + 4 * (q % (KB / 4))) =
+      int r, k4;
+      kcv_coord<ROWS, KB>(q, r, k4);
+      *reinterpret_cast<float4*>(lds + r * LDK + 4 * k4) =
           make_float4(L.v[4 * i], L.v[4 * i + 1], L.v[4 * i + 2], L.v[4 * i + 3]);
     }
     return;
