@@ -51,7 +51,7 @@ def test_fail_apply_golden_bit_exact(device):
         assert int(N(cnt)[0]) == c["broken"]
 
 
-@pytest.mark.parametrize("n", [1, 3, 4097, 1 << 20, 3_000_001])
+@pytest.mark.parametrize("n", [0, 1, 3, 4097, 1 << 20, 3_000_001])
 def test_fail_apply_random_vs_oracle(device, oracle_mod, n):
     from rramsim import ops
     rng = np.random.default_rng(n)
@@ -70,11 +70,12 @@ def test_fail_apply_random_vs_oracle(device, oracle_mod, n):
 
 def test_fail_apply_batched_unaligned_segments(device, oracle_mod):
     """Segments at odd float offsets of one flat buffer (the P2PSync-style
-    aliasing of params, parallel.cpp:25-67) take the scalar path."""
+    aliasing of params, parallel.cpp:25-67) take the scalar path; an empty
+    segment (a zero-size blob) in the middle is skipped and counts 0."""
     import torch
     from rramsim import ops
     rng = np.random.default_rng(9)
-    sizes = [4096 * 9, 4096, 1001, 1000, 37, 1]
+    sizes = [4096 * 9, 4096, 0, 1001, 1000, 37, 1]
     tot = sum(sizes) + 1
     e = rng.normal(150, 100, tot).astype(np.float32)
     v = rng.integers(-1, 2, tot).astype(np.float32)
@@ -128,7 +129,7 @@ def _cfg_pair(p, **kw):
     return c, oc
 
 
-@pytest.mark.parametrize("n", [1, 2, 7, 4096, 100_003, 4096 * 1000 + 3])
+@pytest.mark.parametrize("n", [0, 1, 2, 7, 4096, 100_003, 4096 * 1000 + 3])
 @pytest.mark.parametrize("mode", ["stuck", "quant", "stuck_scaled"])
 def test_inject_bit_exact_vs_oracle(device, oracle_mod, n, mode):
     import torch
