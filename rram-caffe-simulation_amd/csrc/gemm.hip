@@ -1008,8 +1008,14 @@ int gemm_core(int trans_a, int trans_b, int M, int N, int K, float alpha, const 
   // split-K when the 128x128 grid is far below the CU count and K is long
   const int64_t tiles = (int64_t)((N + 127) / 128) * ((M + 127) / 128);
   int split = 1;
-  if (ws != nullptr && tiles < 256 && K >= 1024) {
-    split = static_cast<int>(256 / (tiles > 0 ? tiles : 1));
+  // split-K target grid (A/B knob RRAM_SPLITK_TARGET, default 256 blocks)
+  static const int target = [] {
+    const char* e = getenv("RRAM_SPLITK_TARGET");
+    const int v = e ? atoi(e) : 0;
+    return v >= 64 && v <= 4096 ? v : 256;
+  }();
+  if (ws != nullptr && tiles < target && K >= 1024) {
+    split = static_cast<int>(target / (tiles > 0 ? tiles : 1));
     if (split > 16) split = 16;
     while (split > 1 && (K / split) < 256) --split;
     while (split > 1 && (size_t)split * M * N * sizeof(float) > ws_bytes) --split;
