@@ -68,6 +68,33 @@ def test_fail_apply_random_vs_oracle(device, oracle_mod, n):
     assert bits_equal(N(tw), w) and bits_equal(N(te), e) and int(N(cnt)[0]) == nb
 
 
+def test_fail_apply_beyond_2e31_elements(device, oracle_mod):
+    """Maximum size: Fail() over one blob of 2^31 + 4099 cells (4 x 8.6 GB,
+    int64 addressing past 2^31).  Windows at the start, across 2^31 and at the
+    ragged tail match the oracle bit for bit (Fail is element-wise); the
+    broken counter equals the number of cells left at endurance <= 0."""
+    import torch
+    from rramsim import ops
+    n = (1 << 31) + 4099
+    g = torch.Generator(device=device).manual_seed(3)
+    e = torch.randn(n, device=device, generator=g).mul_(150).add_(120)
+    v = torch.randint(-1, 2, (n,), device=device, generator=g).float()
+    w = torch.randn(n, device=device, generator=g)
+    dw = torch.randn(n, device=device, generator=g).mul_(1e-3)
+    dw[::3] = 0.0
+    wins = [(lo, min(n, lo + 1003)) for lo in (0, (1 << 31) - 1000, n - 1003)]
+    before = [tuple(N(t[lo:hi]).copy() for t in (dw, w, e, v)) for lo, hi in wins]
+    cnt = ops.counters(1, device)
+    ops.fail_apply(dw, w, e, v, counter=cnt)
+    torch.cuda.synchronize()
+    for (lo, hi), (dw0, w0, e0, v0) in zip(wins, before):
+        w1, e1, _ = oracle_mod.fail_apply(dw0, w0, e0, v0)
+        assert bits_equal(N(w[lo:hi]), w1) and bits_equal(N(e[lo:hi]), e1), lo
+    assert int(N(cnt)[0]) == int((e <= 0).sum().item())
+    del e, v, w, dw
+    torch.cuda.empty_cache()
+
+
 def test_fail_apply_batched_unaligned_segments(device, oracle_mod):
     """Segments at odd float offsets of one flat buffer (the P2PSync-style
     aliasing of params, parallel.cpp:25-67) take the scalar path; an empty
@@ -145,6 +172,46 @@ def test_inject_bit_exact_vs_oracle(device, oracle_mod, n, mode):
     ref, nb = oracle_mod.inject(src, oc, 1701, 3, 5)
     assert bits_equal(N(out), ref)
     assert int(N(cnt)[0]) == nb
+
+
+def test_inject_beyond_2e31_elements(device, oracle_mod):
+    """Maximum size: one blob of 2^31 + 4099 weights (8.6 GB in, 8.6 GB out;
+    int64 element addressing past 2^31).  Windows at the start, across the
+    2^31 boundary and at the ragged tail are checked element by element
+    against the oracle's Philox stream and stuck-at rule (oracle.c draw /
+    stuck_value), the broken count against the 3.8-sigma binomial bound
+    (test_random_number_generator.cpp:17-19)."""
+    import math
+    import torch
+    from rramsim import ops
+    n = (1 << 31) + 4099
+    p = 0.01
+    c, _ = _cfg_pair(p, neg=10, zero=20, pos=10)
+    src = torch.randn(n, device=device)
+    out = torch.empty_like(src)
+    cnt = ops.counters(1, device)
+    seed, map_id, layer_id = 1701, 5, 3
+    ops.inject(src, out, c, seed=seed, map_id=map_id, layer_id=layer_id, counter=cnt)
+    torch.cuda.synchronize()
+    for lo in (0, (1 << 31) - 1000, n - 1003):
+        hi = min(n, lo + 1003)
+        s_w = N(src[lo:hi])
+        o_w = N(out[lo:hi])
+        for i in range(lo, hi):
+            pr = i >> 1
+            r = oracle_mod.philox([pr & 0xFFFFFFFF, pr >> 32, map_id, (layer_id << 4) | 0],
+                                  [seed & 0xFFFFFFFF, seed >> 32])
+            rf, rv = (r[2], r[3]) if i & 1 else (r[0], r[1])
+            if rf < c.thr_fault:
+                want = np.float32(-1.0 if rv < c.thr_neg else (0.0 if rv < c.thr_zero else 1.0))
+            else:
+                want = s_w[i - lo]
+            assert np.float32(o_w[i - lo]).view(np.uint32) == np.float32(want).view(np.uint32), i
+    nb = int(N(cnt)[0])
+    q = c.thr_fault / 2.0 ** 32
+    assert abs(nb - n * q) <= 3.8 * math.sqrt(n * q * (1 - q)), (nb, n * q)
+    del src, out
+    torch.cuda.empty_cache()
 
 
 @pytest.mark.parametrize("mode", ["var", "quant_var", "pair", "pair_quant_var"])
