@@ -26,6 +26,7 @@ extern "C" {
 typedef struct rram_net_s* rram_net_t;
 typedef struct rram_solver_s* rram_solver_t;
 typedef struct rram_mc_s* rram_mc_t;
+typedef struct rram_syncedmem_s* rram_syncedmem_t;
 
 enum { RRAM_PHASE_TRAIN = 0, RRAM_PHASE_TEST = 1 };
 
@@ -37,6 +38,25 @@ int rram_caffe_set_stream(rram_stream_t stream);
  * fault draws. */
 int rram_caffe_set_random_seed(uint64_t seed);
 int rram_caffe_synchronize(void);
+
+/* --------------------------------------------------------- SyncedMemory
+ * caffe::SyncedMemory (syncedmem.hpp:45-83, syncedmem.cpp:25-153): lazy
+ * host/device mirror with the head states below (== SyncedMemory::SyncedHead).
+ * cpu_data / mutable_cpu_data on an UNINITIALIZED or HEAD_AT_CPU buffer touch
+ * no device; gpu_* calls allocate / copy on the calling thread's stream and
+ * synchronise it (syncedmem.cpp:51-77).  set_*_data borrow caller memory that
+ * the buffer never frees (syncedmem.cpp:84-122). */
+enum { RRAM_HEAD_UNINITIALIZED = 0, RRAM_HEAD_AT_CPU = 1, RRAM_HEAD_AT_GPU = 2, RRAM_HEAD_SYNCED = 3 };
+int rram_syncedmem_create(size_t size, rram_syncedmem_t* out);
+int rram_syncedmem_destroy(rram_syncedmem_t m);
+int rram_syncedmem_head(rram_syncedmem_t m, int* head);
+int rram_syncedmem_size(rram_syncedmem_t m, size_t* size);
+int rram_syncedmem_cpu_data(rram_syncedmem_t m, const void** p);
+int rram_syncedmem_gpu_data(rram_syncedmem_t m, const void** p);
+int rram_syncedmem_mutable_cpu_data(rram_syncedmem_t m, void** p);
+int rram_syncedmem_mutable_gpu_data(rram_syncedmem_t m, void** p);
+int rram_syncedmem_set_cpu_data(rram_syncedmem_t m, void* p);
+int rram_syncedmem_set_gpu_data(rram_syncedmem_t m, void* p);
 
 /* ---------------------------------------------------------------- Net
  * net_prototxt: NetParameter text (caffe.proto); options: text-format
@@ -108,6 +128,12 @@ int rram_solver_test(rram_solver_t s, int test_net, float* scores, int cap, int*
  * called once per iteration after backward, before the update. */
 typedef void (*rram_callback_t)(void* user);
 int rram_solver_set_gradient_callback(rram_solver_t s, rram_callback_t cb, void* user);
+/* Per-layer backward hook of the train net: cb(layer_index, user) after each
+ * layer's Backward, in backward order (every layer index, with or without
+ * params).  Lets a data-parallel driver start bucketed gradient all-reduces
+ * while earlier layers are still in backward. NULL = off. */
+typedef void (*rram_layer_callback_t)(int layer, void* user);
+int rram_solver_set_backward_callback(rram_solver_t s, rram_layer_callback_t cb, void* user);
 /* log lines in the reference's format ("Iteration N, loss = ...",
  * "    Test net output #k: name = v"), delivered to cb (NULL = silent). */
 typedef void (*rram_log_callback_t)(const char* line, void* user);

@@ -36,6 +36,10 @@ const char* rram_kernels_version(void);
 const char* rram_last_error(void);
 /* hipDeviceSynchronize + error check (host-side convenience). */
 int rram_device_synchronize(void);
+/* Frees the per-geometry convolution gather tables the conv kernels cache per
+ * HIP device (lazily built on first use).  Synchronises every device that
+ * holds one; call only when no kernel of this library is in flight. */
+int rram_release_caches(void);
 
 /* ------------------------------------------------------------------------
  * Fault model

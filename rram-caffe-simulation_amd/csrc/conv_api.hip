@@ -20,6 +20,7 @@ int col2im_core(const float* col, int64_t ldcol, int nimg, const rram_conv_desc*
                 int64_t im_img, int accumulate, hipStream_t s);
 int gemv_core(int trans, int M, int N, float alpha, const float* A, const float* x, float beta,
               float* y, hipStream_t s);
+int release_conv_tables();
 
 namespace {
 
@@ -98,6 +99,8 @@ int check_desc(const rram_conv_desc* d) {
 using namespace rram;
 
 extern "C" {
+
+int rram_release_caches(void) { return rram::release_conv_tables(); }
 
 int rram_gemm_f32_ex(int trans_a, int trans_b, int M, int N, int K, float alpha, const float* A,
                      int lda, const float* B, int ldb, float beta, float* C, int ldc,

@@ -416,6 +416,10 @@ __global__ void __launch_bounds__(256)
 
 __global__ void __launch_bounds__(256)
     k_sgd_update(float* __restrict__ g, float* __restrict__ h, int64_t n, float mom, float lr) {
+  // Caffe's CPU path forms momentum*h and local_rate*g as separate products
+  // (caffe_cpu_axpby = scal + axpy, sgd_solver.cpp:222-228); the oracle does the
+  // same, so no FMA contraction here or in the fused tail / axpby below.
+#pragma clang fp contract(off)
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const float v = mom * h[i] + lr * g[i];
@@ -429,6 +433,7 @@ __global__ void __launch_bounds__(256)
                         float* __restrict__ e, const float* __restrict__ v, int64_t n, float decay,
                         float mom, float lr, int apply_thr, float thr, float dec, float eps,
                         unsigned long long* counter) {
+#pragma clang fp contract(off)
   unsigned cnt = 0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -458,6 +463,7 @@ __global__ void __launch_bounds__(256)
 // ---------------------------------------------------------------------------
 __global__ void k_axpby(int64_t n, float a, const float* __restrict__ x, float b,
                         float* __restrict__ y, int mode) {
+#pragma clang fp contract(off)
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     if (mode == 0) y[i] = a * x[i] + y[i];       // axpy

@@ -952,11 +952,22 @@ View make_view(const float* p, int64_t ld, int rows, int kdim) {
 // kh*KW + kw (0 for pad-free convolutions, whose taps are always inside the
 // image); entries past K (the last tile's tail and the one-tile prefetch
 // overrun) hold tap 31, which no column marks valid.
-const int2* conv_table(const ConvGeom& cv, int K, bool padded, bool wide, hipStream_t s) {
+// Keyed by the current HIP device too: the table lives in that device's HBM.
+std::mutex& conv_table_mutex() {
   static std::mutex mu;
-  static std::map<std::array<int, 10>, int2*> cache;
-  const std::array<int, 10> key{cv.C, cv.H, cv.W, cv.KH, cv.KW, cv.dh, cv.dw, padded ? 1 : 0, K, wide ? 1 : 0};
-  std::lock_guard<std::mutex> g(mu);
+  return mu;
+}
+std::map<std::array<int, 11>, int2*>& conv_table_cache() {
+  static std::map<std::array<int, 11>, int2*> cache;
+  return cache;
+}
+
+const int2* conv_table(const ConvGeom& cv, int K, bool padded, bool wide, hipStream_t s) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  auto& cache = conv_table_cache();
+  const std::array<int, 11> key{dev, cv.C, cv.H, cv.W, cv.KH, cv.KW, cv.dh, cv.dw, padded ? 1 : 0, K, wide ? 1 : 0};
+  std::lock_guard<std::mutex> g(conv_table_mutex());
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
   const int len = (K + BK - 1) / BK * BK + 2 * BK;
@@ -979,6 +990,22 @@ const int2* conv_table(const ConvGeom& cv, int K, bool padded, bool wide, hipStr
 }
 
 }  // namespace
+
+// Frees every cached gather table (all devices).  Called by
+// rram_release_caches(); the caller guarantees no launch still reads them.
+int release_conv_tables() {
+  std::lock_guard<std::mutex> g(conv_table_mutex());
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  for (auto& kv : conv_table_cache()) {
+    (void)hipSetDevice(kv.first[0]);
+    (void)hipDeviceSynchronize();
+    (void)hipFree(kv.second);
+  }
+  conv_table_cache().clear();
+  (void)hipSetDevice(cur);
+  return RRAM_OK;
+}
 
 // Shared by the C-ABI entry points in conv_api.hip.
 int gemm_core(int trans_a, int trans_b, int M, int N, int K, float alpha, const float* A, int lda,

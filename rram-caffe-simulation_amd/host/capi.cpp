@@ -18,11 +18,16 @@ struct rram_solver_s {
   std::vector<rram_net_s> tests;
   rram_callback_t grad_cb = nullptr;
   void* grad_user = nullptr;
+  rram_layer_callback_t bwd_cb = nullptr;
+  void* bwd_user = nullptr;
   rram_log_callback_t log_cb = nullptr;
   void* log_user = nullptr;
 };
 struct rram_mc_s {
   std::unique_ptr<MonteCarlo<float>> mc;
+};
+struct rram_syncedmem_s {
+  std::unique_ptr<SyncedMemory> mem;
 };
 
 static thread_local std::string g_caffe_err;
@@ -66,6 +71,73 @@ int rram_caffe_set_random_seed(uint64_t seed) {
 }
 int rram_caffe_synchronize(void) {
   return guarded([&] { Caffe::synchronize(); });
+}
+
+// ---------------------------------------------------------- SyncedMemory
+int rram_syncedmem_create(size_t size, rram_syncedmem_t* out) {
+  return guarded([&] {
+    NEED(out);
+    auto* h = new rram_syncedmem_s;
+    h->mem = std::make_unique<SyncedMemory>(size);
+    *out = h;
+  });
+}
+int rram_syncedmem_destroy(rram_syncedmem_t m) {
+  return guarded([&] { delete m; });
+}
+int rram_syncedmem_head(rram_syncedmem_t m, int* head) {
+  return guarded([&] {
+    NEED(m);
+    NEED(head);
+    *head = static_cast<int>(m->mem->head());
+  });
+}
+int rram_syncedmem_size(rram_syncedmem_t m, size_t* size) {
+  return guarded([&] {
+    NEED(m);
+    NEED(size);
+    *size = m->mem->size();
+  });
+}
+int rram_syncedmem_cpu_data(rram_syncedmem_t m, const void** p) {
+  return guarded([&] {
+    NEED(m);
+    NEED(p);
+    *p = m->mem->cpu_data();
+  });
+}
+int rram_syncedmem_gpu_data(rram_syncedmem_t m, const void** p) {
+  return guarded([&] {
+    NEED(m);
+    NEED(p);
+    *p = m->mem->gpu_data();
+  });
+}
+int rram_syncedmem_mutable_cpu_data(rram_syncedmem_t m, void** p) {
+  return guarded([&] {
+    NEED(m);
+    NEED(p);
+    *p = m->mem->mutable_cpu_data();
+  });
+}
+int rram_syncedmem_mutable_gpu_data(rram_syncedmem_t m, void** p) {
+  return guarded([&] {
+    NEED(m);
+    NEED(p);
+    *p = m->mem->mutable_gpu_data();
+  });
+}
+int rram_syncedmem_set_cpu_data(rram_syncedmem_t m, void* p) {
+  return guarded([&] {
+    NEED(m);
+    m->mem->set_cpu_data(p);
+  });
+}
+int rram_syncedmem_set_gpu_data(rram_syncedmem_t m, void* p) {
+  return guarded([&] {
+    NEED(m);
+    m->mem->set_gpu_data(p);
+  });
 }
 
 // ------------------------------------------------------------------- Net
@@ -360,6 +432,15 @@ int rram_solver_set_gradient_callback(rram_solver_t s, rram_callback_t cb, void*
     s->grad_user = user;
     if (cb) s->solver->on_gradients_ready = [s] { s->grad_cb(s->grad_user); };
     else s->solver->on_gradients_ready = nullptr;
+  });
+}
+int rram_solver_set_backward_callback(rram_solver_t s, rram_layer_callback_t cb, void* user) {
+  return guarded([&] {
+    NEED(s);
+    s->bwd_cb = cb;
+    s->bwd_user = user;
+    if (cb) s->solver->net()->on_backward_layer = [s](int i) { s->bwd_cb(i, s->bwd_user); };
+    else s->solver->net()->on_backward_layer = nullptr;
   });
 }
 int rram_solver_set_log_callback(rram_solver_t s, rram_log_callback_t cb, void* user) {

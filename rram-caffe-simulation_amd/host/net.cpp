@@ -341,8 +341,10 @@ Dtype Net<Dtype>::Forward(bool compute_loss) {
 
 template <typename Dtype>
 void Net<Dtype>::Backward() {
-  for (int i = static_cast<int>(layers_.size()) - 1; i >= 0; --i)
+  for (int i = static_cast<int>(layers_.size()) - 1; i >= 0; --i) {
     if (layer_need_backward_[i]) layers_[i]->Backward(top_vecs_[i], bottom_need_backward_[i], bottom_vecs_[i]);
+    if (on_backward_layer) on_backward_layer(i);
+  }
 }
 
 template <typename Dtype>

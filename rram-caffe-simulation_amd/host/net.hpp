@@ -4,6 +4,7 @@
 // the 2-D ones (net.cpp:482-493, net.hpp:181-186).
 #pragma once
 
+#include <functional>
 #include <map>
 #include <memory>
 #include <string>
@@ -70,6 +71,11 @@ class Net {
   // param into them, so one all-reduce covers all gradients.
   int64_t flat_param_count() const;
   void alias_flat_params(Dtype* data, Dtype* diff);
+
+  // Called after layer i's Backward (in backward order, every layer index),
+  // so a data-parallel driver can start reducing the gradients that are final
+  // while earlier layers still run backward.
+  std::function<void(int)> on_backward_layer;
 
   void set_iter(uint64_t it) {
     for (auto& l : layers_) l->iter = it;

@@ -125,7 +125,9 @@ float ThresholdFailureStrategy<Dtype>::threshold_for(int i) const {
   const auto& lr = this->net_->params_lr();
   const int idx = reference_lr_index ? i : this->net_->failure_learnable_param_ids()[i];
   CAFFE_CHECK(idx < (int)lr.size(), "params_lr index out of range");
-  return threshold() * static_cast<float>(lr[idx]) * static_cast<float>(this->solver_->GetLearningRate());
+  // strategy.cpp:13-14: rate = params_lr * lr (fp32), threshold = threshold_ * rate
+  const float rate = static_cast<float>(lr[idx]) * static_cast<float>(this->solver_->GetLearningRate());
+  return threshold() * rate;
 }
 
 // strategy.cpp:7-33, on the device (no D2H/H2D round trip)
@@ -201,22 +203,39 @@ void Solver<Dtype>::InitFailurePattern(const Msg& fp) {
 // sgd_solver.cpp GetLearningRate
 template <typename Dtype>
 Dtype Solver<Dtype>::GetLearningRate() const {
+  // sgd_solver.cpp:27-63.  base_lr / gamma / power are `optional float` in
+  // caffe.proto, so they are rounded to fp32 first; the fp32 sub-expressions
+  // (1 + gamma*iter, 1 - iter/max_iter) stay fp32 and pow/exp run in double
+  // (the C library ::pow the unqualified calls bind to), as in the reference.
   const std::string policy = param_.str("lr_policy", "fixed");
-  const double base = param_.num("base_lr", 0.01), gamma = param_.num("gamma", 0.0), power = param_.num("power", 0.0);
-  const double it = iter_;
+  const float base = static_cast<float>(param_.num("base_lr", 0.01));
+  const float gamma = static_cast<float>(param_.num("gamma", 0.0));
+  const float power = static_cast<float>(param_.num("power", 0.0));
+  const int it = iter_;
   if (policy == "fixed") return (Dtype)base;
-  if (policy == "step") return (Dtype)(base * std::pow(gamma, std::floor(it / (double)param_.integer("stepsize", 1))));
-  if (policy == "exp") return (Dtype)(base * std::pow(gamma, it));
-  if (policy == "inv") return (Dtype)(base * std::pow(1.0 + gamma * it, -power));
+  if (policy == "step") {
+    const int step = it / (int)param_.integer("stepsize", 1);
+    return (Dtype)((double)base * std::pow((double)gamma, (double)step));
+  }
+  if (policy == "exp") return (Dtype)((double)base * std::pow((double)gamma, (double)it));
+  if (policy == "inv") {
+    const float b = 1.0f + gamma * static_cast<float>(it);
+    return (Dtype)((double)base * std::pow((double)b, (double)-power));
+  }
   if (policy == "multistep") {
     auto sv = param_.nums("stepvalue");
     int step = 0;
     while (step < (int)sv.size() && it >= sv[step]) ++step;
-    return (Dtype)(base * std::pow(gamma, step));
+    return (Dtype)((double)base * std::pow((double)gamma, (double)step));
   }
-  if (policy == "poly") return (Dtype)(base * std::pow(1.0 - it / (double)param_.integer("max_iter", 1), power));
-  if (policy == "sigmoid")
-    return (Dtype)(base * (1.0 / (1.0 + std::exp(-gamma * (it - (double)param_.integer("stepsize", 1))))));
+  if (policy == "poly") {
+    const float b = 1.0f - static_cast<float>(it) / static_cast<float>(param_.integer("max_iter", 1));
+    return (Dtype)((double)base * std::pow((double)b, (double)power));
+  }
+  if (policy == "sigmoid") {
+    const float x = -gamma * (static_cast<float>(it) - static_cast<float>(param_.integer("stepsize", 1)));
+    return (Dtype)((double)base * (1.0 / (1.0 + std::exp((double)x))));
+  }
   throw Error("Unknown learning rate policy: " + policy);
 }
 
@@ -302,8 +321,10 @@ void Solver<Dtype>::FusedTail() {
   const auto& fids = net_->failure_learnable_param_ids();
   const Dtype mom = (Dtype)param_.num("momentum", 0.0);
   const Dtype wd = (Dtype)param_.num("weight_decay", 0.0);
-  ThresholdFailureStrategy<Dtype>* thr = nullptr;
-  for (auto& s : strategys_) thr = dynamic_cast<ThresholdFailureStrategy<Dtype>*>(s.get());
+  // only reached when every configured strategy is a ThresholdFailureStrategy
+  // and there is at most one (Step's can_fuse); anything else runs unfused
+  ThresholdFailureStrategy<Dtype>* thr =
+      strategys_.empty() ? nullptr : dynamic_cast<ThresholdFailureStrategy<Dtype>*>(strategys_[0].get());
   auto* gm = dynamic_cast<GaussianFailureMaker<Dtype>*>(fmaker_.get());
   std::vector<Blob<Dtype>*> fi = fmaker_ ? fmaker_->fail_iterations() : std::vector<Blob<Dtype>*>();
   unsigned long long* counts = fmaker_ ? fmaker_->device_counts() : nullptr;
@@ -331,8 +352,15 @@ void Solver<Dtype>::Step(int iters) {
   const int test_interval = (int)param_.integer("test_interval", 0);
   const int average_loss = (int)param_.integer("average_loss", 1);
   const int iter_size = (int)param_.integer("iter_size", 1);
-  const bool can_fuse = fused_update_ && param_.num("clip_gradients", -1.0) < 0 && iter_size == 1 &&
-                        param_.str("regularization_type", "L2") == "L2";
+  // The fused tail folds Regularize(L2) + SGDUpdate + threshold + Update +
+  // Fail into one pass; remapping / genetic strategies (and more than one
+  // strategy) need the reference order ComputeUpdate -> ApplyStrategy ->
+  // ApplyUpdate -> Fail (solver.cpp:300-305), so they disable fusion.
+  bool fusable_strategies = strategys_.size() <= 1;
+  for (auto& st : strategys_)
+    fusable_strategies = fusable_strategies && dynamic_cast<ThresholdFailureStrategy<Dtype>*>(st.get()) != nullptr;
+  const bool can_fuse = fused_update_ && fusable_strategies && param_.num("clip_gradients", -1.0) < 0 &&
+                        iter_size == 1 && param_.str("regularization_type", "L2") == "L2";
   while (iter_ < stop) {
     net_->ClearParamDiffs();
     if (test_interval && iter_ % test_interval == 0 && (iter_ > 0 || param_.boolean("test_initialization", true)))

@@ -17,6 +17,7 @@ PI64 = C.POINTER(C.c_int64)
 PF = C.POINTER(C.c_float)
 CB = C.CFUNCTYPE(None, C.c_void_p)
 LOGCB = C.CFUNCTYPE(None, C.c_char_p, C.c_void_p)
+LAYERCB = C.CFUNCTYPE(None, C.c_int, C.c_void_p)
 
 SIGNATURES = {
     "rram_caffe_last_error": (C.c_char_p, []),
@@ -61,6 +62,7 @@ SIGNATURES = {
     "rram_solver_test": (I, [P, I, PF, I, PI]),
     "rram_solver_set_gradient_callback": (I, [P, CB, P]),
     "rram_solver_set_log_callback": (I, [P, LOGCB, P]),
+    "rram_solver_set_backward_callback": (I, [P, LAYERCB, P]),
     "rram_solver_num_fail_blobs": (I, [P, PI]),
     "rram_solver_fail_state": (I, [P, I, PP, PP, PI64]),
     "rram_solver_broken_counts": (I, [P, C.POINTER(C.c_ulonglong), I, PI]),
@@ -75,6 +77,16 @@ SIGNATURES = {
     "rram_proto_rewrite": (I, [C.c_char_p, C.c_char_p, I]),
     "rram_glibc_rand": (I, [U32, I, PI]),
     "rram_solver_describe": (I, [C.c_char_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "rram_syncedmem_create": (I, [C.c_size_t, PP]),
+    "rram_syncedmem_destroy": (I, [P]),
+    "rram_syncedmem_head": (I, [P, PI]),
+    "rram_syncedmem_size": (I, [P, C.POINTER(C.c_size_t)]),
+    "rram_syncedmem_cpu_data": (I, [P, PP]),
+    "rram_syncedmem_gpu_data": (I, [P, PP]),
+    "rram_syncedmem_mutable_cpu_data": (I, [P, PP]),
+    "rram_syncedmem_mutable_gpu_data": (I, [P, PP]),
+    "rram_syncedmem_set_cpu_data": (I, [P, P]),
+    "rram_syncedmem_set_gpu_data": (I, [P, P]),
     "rram_mc_create": (I, [P, P, I, U64, I, PP]),
     "rram_mc_destroy": (I, [P]),
     "rram_mc_run": (I, [P, U32, U32]),
@@ -202,6 +214,63 @@ def _wrap_device(ptr: int, shape):
     if len(shape) == 0:
         shape = (1,)
     return torch.as_tensor(_Iface(ptr, shape), device="cuda")
+
+
+class SyncedMemory:
+    """caffe::SyncedMemory (syncedmem.hpp:45-83): head() is one of
+    UNINITIALIZED / HEAD_AT_CPU / HEAD_AT_GPU / SYNCED; the *_data calls
+    return raw addresses (host or device) exactly like the C++ accessors."""
+    UNINITIALIZED, HEAD_AT_CPU, HEAD_AT_GPU, SYNCED = range(4)
+
+    def __init__(self, size: int):
+        self._lib = load()
+        h = C.c_void_p()
+        check(self._lib.rram_syncedmem_create(size, C.byref(h)), "syncedmem_create")
+        self.h = h
+
+    def _ptr(self, fn) -> int:
+        p = C.c_void_p()
+        check(getattr(self._lib, fn)(self.h, C.byref(p)), fn)
+        return p.value or 0
+
+    def head(self) -> int:
+        v = C.c_int()
+        check(self._lib.rram_syncedmem_head(self.h, C.byref(v)), "syncedmem_head")
+        return v.value
+
+    def size(self) -> int:
+        v = C.c_size_t()
+        check(self._lib.rram_syncedmem_size(self.h, C.byref(v)), "syncedmem_size")
+        return v.value
+
+    def cpu_data(self) -> int:
+        return self._ptr("rram_syncedmem_cpu_data")
+
+    def gpu_data(self) -> int:
+        return self._ptr("rram_syncedmem_gpu_data")
+
+    def mutable_cpu_data(self) -> int:
+        return self._ptr("rram_syncedmem_mutable_cpu_data")
+
+    def mutable_gpu_data(self) -> int:
+        return self._ptr("rram_syncedmem_mutable_gpu_data")
+
+    def set_cpu_data(self, addr: int):
+        check(self._lib.rram_syncedmem_set_cpu_data(self.h, C.c_void_p(addr)), "syncedmem_set_cpu_data")
+
+    def set_gpu_data(self, addr: int):
+        check(self._lib.rram_syncedmem_set_gpu_data(self.h, C.c_void_p(addr)), "syncedmem_set_gpu_data")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._lib.rram_syncedmem_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Net:
@@ -437,6 +506,15 @@ class Solver:
     def set_gradient_callback(self, fn):
         self._cb = CB(lambda _u: fn())
         check(self._lib.rram_solver_set_gradient_callback(self.h, self._cb, None), "set_gradient_callback")
+
+    def set_backward_callback(self, fn):
+        """fn(layer_index) after each train-net layer's Backward (None = off)."""
+        if fn is None:
+            self._bwdcb = None
+            check(self._lib.rram_solver_set_backward_callback(self.h, LAYERCB(), None), "set_backward_callback")
+            return
+        self._bwdcb = LAYERCB(lambda i, _u: fn(i))
+        check(self._lib.rram_solver_set_backward_callback(self.h, self._bwdcb, None), "set_backward_callback")
 
     def fail_state(self):
         n = C.c_int()

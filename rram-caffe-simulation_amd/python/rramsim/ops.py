@@ -116,6 +116,15 @@ def sgd_update(g, h, momentum, local_rate):
             "sgd_update")
 
 
+def axpy(alpha, x, y):
+    """y = alpha*x + y (caffe_gpu_axpy, math_functions.cu:65-69)."""
+    _f32(x, "x")
+    _f32(y, "y")
+    if x.numel() != y.numel():
+        raise K.RramError("axpy: size mismatch")
+    K.check(_lib().rram_axpy(x.numel(), alpha, _p(x), _p(y), _stream()), "axpy")
+
+
 def fused_update_fail(w, g, h, e, v, decay, momentum, lr, apply_thr, thr, decrement=100.0,
                       eps=1e-20, counter=None):
     K.check(_lib().rram_fused_update_fail(_p(w), _p(g), _p(h), _p(e), _p(v), w.numel(), decay,

@@ -16,6 +16,7 @@ collective is the final all-reduce of the statistics vector.
 from __future__ import annotations
 
 import os
+import re
 from typing import Dict, List, Optional
 
 
@@ -37,6 +38,36 @@ def average_gradients(flat, world: int, group=None):
         flat.mul_(1.0 / world)
 
 
+def plan_buckets(layer_ranges: List[List[tuple]], n_layers: int, bucket_elems: int) -> Dict[int, tuple]:
+    """Bucketed gradient all-reduce schedule for backward order.
+
+    layer_ranges[i] lists the [begin, end) flat-buffer ranges of layer i's
+    learnable params; the flat buffer holds them in forward layer order
+    (Net::alias_flat_params, the GPUParams layout of parallel.cpp:25-115), so
+    after layers n-1 ... i have run backward the final gradients form one
+    suffix [lo, n) of the buffer.  Returns {layer index: (begin, end)}: after
+    that layer's Backward, all-reduce flat[begin:end].  Each bucket holds at
+    least bucket_elems elements (except the last, which on_gradients_ready
+    launches for whatever is left, so it is not in the plan).  Requires every
+    layer's ranges to be contiguous with its neighbours' (no shared params)."""
+    plan = {}
+    hi = None            # end of the not-yet-reduced suffix
+    lo = None
+    for i in range(n_layers - 1, -1, -1):
+        rs = layer_ranges[i] if i < len(layer_ranges) else []
+        if not rs:
+            continue
+        b, e = min(r[0] for r in rs), max(r[1] for r in rs)
+        if hi is None:
+            hi = e
+        lo = b if lo is None else min(lo, b)
+        if hi - lo >= bucket_elems and i > 0:
+            plan[i] = (lo, hi)
+            hi = lo
+            lo = None
+    return plan
+
+
 def allreduce_stats(values: List[float], device, group=None) -> List[float]:
     """One all-reduce (sum, fp64) of a small statistics vector."""
     import torch
@@ -51,7 +82,7 @@ class DataParallelSolver:
     """Fault-aware data-parallel SGD (C4) on top of caffe.Solver."""
 
     def __init__(self, solver_prototxt: str, net_prototxt: str, options: Optional[Dict] = None, seed: int = 1701,
-                 group=None, log=None):
+                 group=None, log=None, overlap: bool = False, bucket_mb: float = 4.0):
         import torch
         import torch.distributed as dist
 
@@ -75,9 +106,62 @@ class DataParallelSolver:
             dist.broadcast(self.flat_data, 0, group=group)    # on_start broadcast (parallel.cpp:286-322)
         self.solver.set_gradient_callback(self._on_gradients_ready)
         self.allreduce_calls = 0
+        self.bucket_calls = 0
+        self._pending = []
+        self._plan = {}
+        self._reduced_lo = n
+        # iter_size > 1 runs several backward passes per update: only the last
+        # one holds the final gradients, so the per-layer buckets stay off
+        m = re.search(r"^\s*iter_size\s*:\s*(\d+)", solver_prototxt, re.M)
+        self.overlap = bool(overlap) and self.world > 1 and not (m and int(m.group(1)) > 1)
+        if self.overlap:
+            self._plan = self._make_plan(net, int(bucket_mb * (1 << 20)) // 4)
+            if self._plan:
+                self.solver.set_backward_callback(self._on_layer_backward)
+            else:
+                self.overlap = False
+
+    def _make_plan(self, net, bucket_elems):
+        base = self.flat_data.data_ptr()
+        params = net.params()
+        ranges, k = [], 0
+        for _name, _typ, npar in net.layers():
+            rs = []
+            for p in params[k:k + npar]:
+                b = (p["data"].data_ptr() - base) // 4
+                rs.append((b, b + p["data"].numel()))
+            ranges.append(rs)
+            k += npar
+        if k != len(params):          # shared params: the suffix property does not hold
+            return {}
+        return plan_buckets(ranges, len(ranges), bucket_elems)
+
+    def _on_layer_backward(self, layer):
+        # gradients of layers >= `layer` are final: reduce this bucket on the
+        # collective stream while backward continues on the compute stream
+        import torch.distributed as dist
+        r = self._plan.get(layer)
+        if r is None:
+            return
+        b, e = r
+        self._pending.append(dist.all_reduce(self.flat_diff[b:e], group=self.group, async_op=True))
+        self._reduced_lo = b
+        self.bucket_calls += 1
 
     def _on_gradients_ready(self):
-        average_gradients(self.flat_diff, self.world, self.group)
+        if self.overlap:
+            import torch.distributed as dist
+            if self._reduced_lo > 0:
+                self._pending.append(dist.all_reduce(self.flat_diff[:self._reduced_lo], group=self.group,
+                                                     async_op=True))
+                self.bucket_calls += 1
+            for w in self._pending:
+                w.wait()              # the compute stream waits for the collective stream
+            self._pending = []
+            self._reduced_lo = self.flat_diff.numel()
+            self.flat_diff.mul_(1.0 / self.world)
+        else:
+            average_gradients(self.flat_diff, self.world, self.group)
         self.allreduce_calls += 1
 
     def step(self, iters: int):

@@ -298,23 +298,44 @@ def test_threshold_strategy_bit_exact(device, oracle_mod):
 
 
 def test_sgd_update_and_fused_tail(device, oracle_mod):
+    """SGDUpdate (sgd_solver.cu:6-12 with the CPU path's separate products,
+    sgd_solver.cpp:222-228) and the fused Regularize + SGDUpdate + threshold +
+    Update + Fail tail are bit-exact against the oracle's plain IEEE sequence
+    (no FMA contraction on either side), including |update| exactly at the
+    threshold and exactly at eps = 1e-20."""
     from rramsim import ops
     rng = np.random.default_rng(8)
-    n = 100_000
+    n = 100_003
     w, g, h = (rng.standard_normal(n).astype(np.float32) for _ in range(3))
     e = rng.normal(150, 100, n).astype(np.float32)
+    e[:64] = 100.0                                    # exactly-zero crossings
     v = rng.integers(-1, 2, n).astype(np.float32)
+    # boundary cells: zero history and decay so the update is exactly lr*g
+    lr, thr = np.float32(0.01), np.float32(1e-3)
+    h[:16] = 0.0
+    g[:8] = thr / lr                                  # |update| ~ thr (ties resolved by rounding)
+    g[8:16] = np.float32(1e-20) / lr
     tg, th = T(g, device), T(h, device)
     ops.sgd_update(tg, th, 0.9, 0.01)
     g2, h2 = oracle_mod.sgd_update(g, h, 0.9, 0.01)
-    np.testing.assert_allclose(N(tg), g2, rtol=1e-6, atol=1e-7)   # fma contraction allowed
-    tw, tg, th, te = T(w, device), T(g, device), T(h, device), T(e, device)
-    cnt = ops.counters(1, device)
-    ops.fused_update_fail(tw, tg, th, te, T(v, device), 0.004, 0.9, 0.01, True, 1e-3, counter=cnt)
-    w3, g3, h3, e3, nb = oracle_mod.fused_update_fail(w, g, h, e, v, 0.004, 0.9, 0.01, True, 1e-3)
-    np.testing.assert_allclose(N(tw), w3, rtol=1e-5, atol=1e-6)
-    # endurance decisions may flip only where |g| sits within rounding of thr / eps
-    assert abs(int(N(cnt)[0]) - nb) <= 2
+    assert bits_equal(N(tg), g2) and bits_equal(N(th), h2)
+    for decay in (0.0, 0.004):
+        tw, tg, th, te = T(w, device), T(g, device), T(h, device), T(e, device)
+        cnt = ops.counters(1, device)
+        ops.fused_update_fail(tw, tg, th, te, T(v, device), decay, 0.9, 0.01, True, 1e-3, counter=cnt)
+        w3, g3, h3, e3, nb = oracle_mod.fused_update_fail(w, g, h, e, v, decay, 0.9, 0.01, True, 1e-3)
+        assert bits_equal(N(tw), w3) and bits_equal(N(tg), g3) and bits_equal(N(th), h3)
+        assert bits_equal(N(te), e3) and int(N(cnt)[0]) == nb
+        # the unfused kernels in the reference order give the same bits
+        uw, ug, uh, ue = T(w, device), T(g, device), T(h, device), T(e, device)
+        if decay:
+            ops.axpy(decay, uw, ug)
+        ops.sgd_update(ug, uh, 0.9, 0.01)
+        ops.threshold_strategy(ug, 1e-3)
+        ops.axpy(-1.0, ug, uw)
+        c2 = ops.counters(1, device)
+        ops.fail_apply(ug, uw, ue, T(v, device), counter=c2)
+        assert bits_equal(N(uw), w3) and bits_equal(N(ue), e3) and int(N(c2)[0]) == nb
 
 
 # ------------------------------------------------------------------ GEMM
@@ -440,18 +461,31 @@ def test_conv_fwd_unaligned_weights_nan_tail(device, oracle_mod, cs):
     np.testing.assert_allclose(N(y), ref, atol=1e-4, rtol=1e-4)
 
 
-@pytest.mark.parametrize("cs", CONV_CASES[:4] + [CONV_CASES[8]])
-def test_conv_bwd_vs_torch(device, cs):
+def _bwd_ref64(fwd, inputs, dy):
+    """float64 gradients of fwd(*inputs) for upstream dy, and their error scale:
+    the same backward evaluated on |inputs| and |dy| (= Σ|a·b| of each gradient
+    contraction, test_convolution_layer.cpp:256 tolerance made scale-aware)."""
+    import torch
+    xs = [t.double().clone().requires_grad_(True) for t in inputs]
+    fwd(*xs).backward(dy.double())
+    xa = [t.double().abs().clone().requires_grad_(True) for t in inputs]
+    fwd(*xa).backward(dy.double().abs())
+    return [t.grad.numpy() for t in xs], [t.grad.numpy() for t in xa]
+
+
+@pytest.mark.parametrize("cs", CONV_CASES[:4] + [CONV_CASES[8], CONV_CASES[6], CONV_CASES[12]])
+def test_conv_bwd_vs_fp64(device, cs):
+    """Convolution backward (conv_layer.cu:26-56: weight GEMM accumulate, bias
+    sum, data GEMM + col2im) within 1e-4 of Σ|a·b| of a float64 reference."""
     import torch
     from rramsim import ops
     torch.manual_seed(0)
     x = torch.randn(cs["x"], dtype=torch.float32)
     w = torch.randn(cs["cout"], cs["x"][1] // cs["g"], cs["k"], cs["k"]) * 0.1
     b = torch.randn(cs["cout"])
-    xr, wr, br = (t.clone().requires_grad_(True) for t in (x, w, b))
-    yr = torch.nn.functional.conv2d(xr, wr, br, cs["s"], cs["p"], cs["d"], cs["g"])
-    dy = torch.randn_like(yr)
-    yr.backward(dy)
+    fwd = lambda xx, ww, bb: torch.nn.functional.conv2d(xx, ww, bb, cs["s"], cs["p"], cs["d"], cs["g"])  # noqa: E731
+    dy = torch.randn_like(fwd(x, w, b))
+    (gx, gw, gb), (sx, sw, sb) = _bwd_ref64(fwd, (x, w, b), dy)
     d = ops.conv_desc(cs["x"], cs["cout"], cs["k"], cs["s"], cs["p"], cs["d"], cs["g"])
     dw = torch.zeros_like(w, device=device)
     db = torch.zeros_like(b, device=device)
@@ -459,27 +493,30 @@ def test_conv_bwd_vs_torch(device, cs):
     ws = torch.empty(ops.conv2d_bwd_workspace(d, 2) // 4 + 1, device=device)   # forces chunking
     ops.conv2d_bwd(d, x.to(device), w.to(device), dy.to(device), dw, db, dx, ws)
     torch.cuda.synchronize()
-    for got, ref in ((dw, wr.grad), (db, br.grad), (dx, xr.grad)):
-        np.testing.assert_allclose(got.cpu().numpy(), ref.numpy(), atol=1e-3, rtol=1e-4)
+    import _ref64 as R
+    for got, ref, sc, nm in ((dw, gw, sw, "dW"), (db, gb, sb, "db"), (dx, gx, sx, "dX")):
+        R.assert_scaled(got.cpu().numpy(), ref, sc, nm)
 
 
-def test_ip_bwd_vs_torch(device):
+def test_ip_bwd_vs_fp64(device):
+    """InnerProduct backward (inner_product_layer.cu:40-75) at LeNet ip1 and
+    AlexNet fc6 shapes within 1e-4 of Σ|a·b| of a float64 reference."""
     import torch
+    import _ref64 as R
     from rramsim import ops
     torch.manual_seed(1)
-    M, Nn, K = 64, 500, 800                  # LeNet ip1
-    x, w, b = torch.randn(M, K), torch.randn(Nn, K) * 0.05, torch.randn(Nn)
-    xr, wr, br = (t.clone().requires_grad_(True) for t in (x, w, b))
-    y = xr @ wr.T + br
-    dy = torch.randn_like(y)
-    y.backward(dy)
-    dw = torch.zeros(Nn, K, device=device)
-    db = torch.zeros(Nn, device=device)
-    dx = torch.empty(M, K, device=device)
-    ops.ip_bwd(x.to(device), w.to(device), dy.to(device), dw, db, dx, M, Nn, K)
-    torch.cuda.synchronize()
-    for got, ref in ((dw, wr.grad), (db, br.grad), (dx, xr.grad)):
-        np.testing.assert_allclose(got.cpu().numpy(), ref.numpy(), atol=1e-3, rtol=1e-4)
+    for M, Nn, K in ((64, 500, 800), (256, 4096, 9216)):
+        x, w, b = torch.randn(M, K), torch.randn(Nn, K) * 0.05, torch.randn(Nn)
+        fwd = lambda xx, ww, bb: xx @ ww.T + bb  # noqa: E731
+        dy = torch.randn(M, Nn)
+        (gx, gw, gb), (sx, sw, sb) = _bwd_ref64(fwd, (x, w, b), dy)
+        dw = torch.zeros(Nn, K, device=device)
+        db = torch.zeros(Nn, device=device)
+        dx = torch.empty(M, K, device=device)
+        ops.ip_bwd(x.to(device), w.to(device), dy.to(device), dw, db, dx, M, Nn, K)
+        torch.cuda.synchronize()
+        for got, ref, sc, nm in ((dw, gw, sw, "dW"), (db, gb, sb, "db"), (dx, gx, sx, "dX")):
+            R.assert_scaled(got.cpu().numpy(), ref, sc, f"{nm} {M}x{Nn}x{K}")
 
 
 def test_im2col_col2im_vs_oracle(device, oracle_mod):

@@ -63,3 +63,90 @@ def test_two_ranks_stay_identical(device):
     assert d0 != d1                            # different data shards per rank
     assert w0 == w1 and ww0 == ww1             # bitwise-identical replicas
     assert e0 == e1 and b0 == b1               # identical fault state
+
+
+def _equiv_worker(rank, world, port, q, data, label, overlap):
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    sys.path.insert(0, str(root / "rram-caffe-simulation_amd" / "python"))
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from rramsim import models
+    from rramsim.parallel import DataParallelSolver
+    dp = DataParallelSolver(_equiv_solver(), models.lenet(train_batch=32, test_batch=32),
+                            models.net_options("lenet"), seed=7, overlap=overlap, bucket_mb=0.25)
+    net = dp.solver.net
+    b = data.shape[0] // world
+    net.blob("data").copy_(torch.from_numpy(data[rank * b:(rank + 1) * b]).reshape(net.blob("data").shape))
+    net.blob("label").copy_(torch.from_numpy(label[rank * b:(rank + 1) * b]))
+    dp.step(3)
+    torch.cuda.synchronize()
+    w = dp.flat_data.cpu().numpy().copy()
+    e = torch.cat([s[0] for s in dp.solver.fail_state()]).cpu().numpy().copy()
+    q.put((rank, w, e, dp.solver.broken_counts(), dp.allreduce_calls, dp.bucket_calls, dp.overlap))
+    dist.barrier()
+    dp.close()
+    dist.destroy_process_group()
+
+
+def _equiv_solver():
+    from rramsim import models
+    return models.solver(base_lr=0.01, momentum=0.9, weight_decay=0.0005, max_iter=10,
+                         failure_mean=250.0, failure_std=150.0)
+
+
+def _run_equiv(data, label, overlap):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_equiv_worker, args=(r, 2, port, q, data, label, overlap)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted((q.get(timeout=300) for _ in ps), key=lambda t: t[0])
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    return res
+
+
+def test_dp_two_ranks_equal_one_process_double_batch(device):
+    """P2PSync semantics (parallel.cpp:324-380: sum of the ranks' gradients,
+    scaled by 1/N on the root) make 2 ranks x batch 32 the same SGD as one
+    process x batch 64 holding both shards (the reference's multi-GPU solver
+    test pattern, test_gradient_based_solver.cpp:191-209,456-486).  After 3
+    iterations with stuck-at faults: weights within 1e-6 relative (gradient
+    summation order differs), endurance and broken counts bit-exact.  The
+    bucketed all-reduce overlapped with backward gives the
+    same bits as the single flat all-reduce."""
+    import numpy as np
+    import torch
+    from rramsim import caffe, models
+    caffe.set_stream_from_torch()
+    caffe.set_random_seed(7)
+    s = caffe.Solver(_equiv_solver(), models.lenet(train_batch=64, test_batch=64), models.net_options("lenet"))
+    data = s.net.blob("data").cpu().numpy().copy()
+    label = s.net.blob("label").cpu().numpy().copy()
+    s.step(3)
+    torch.cuda.synchronize()
+    w_ref = torch.cat([p["data"] for p in s.net.params()]).cpu().numpy()
+    e_ref = torch.cat([f[0] for f in s.fail_state()]).cpu().numpy()
+    b_ref = s.broken_counts()
+    s.close()
+    assert sum(b_ref) > 0                                  # faults fired during the 3 steps
+    flat = _run_equiv(data, label, overlap=False)
+    for rank, w, e, b, calls, bcalls, ov in flat:
+        assert calls == 3 and not ov
+        np.testing.assert_allclose(w, w_ref, rtol=1e-6, atol=1e-7 * float(np.abs(w_ref).max()))
+        assert np.array_equal(e.view(np.uint32), e_ref.view(np.uint32)), rank
+        assert b == b_ref
+    assert np.array_equal(flat[0][1], flat[1][1])
+    over = _run_equiv(data, label, overlap=True)
+    for (rank, w, e, b, calls, bcalls, ov), f in zip(over, flat):
+        assert ov and calls == 3 and bcalls > 3            # more than one bucket per iteration
+        assert np.array_equal(w.view(np.uint32), f[1].view(np.uint32)), rank
+        assert np.array_equal(e.view(np.uint32), f[2].view(np.uint32)) and b == f[3]

@@ -52,3 +52,76 @@ def test_shard_maps_partition():
     for world in (1, 2, 4, 8):
         allm = sorted(m for r in range(world) for m in shard_maps(37, r, world))
         assert allm == list(range(37))
+
+
+def test_plan_buckets_suffixes_in_backward_order():
+    """The bucket plan covers the flat gradient buffer as disjoint suffix
+    slices in backward order; the remainder [0, last lo) is left to
+    on_gradients_ready; paramless layers are skipped."""
+    from rramsim.parallel import plan_buckets
+    # layers: data, conv1(w,b), pool, conv2(w,b), ip1(w,b), relu, ip2(w,b), loss
+    sizes = {1: (500, 20), 3: (25000, 50), 4: (400000, 500), 6: (5000, 10)}
+    ranges, off = [], 0
+    for i in range(8):
+        rs = []
+        for n in sizes.get(i, ()):
+            rs.append((off, off + n))
+            off += n
+        ranges.append(rs)
+    total = off
+    for be in (1, 1000, 30000, 10 ** 9):
+        plan = plan_buckets(ranges, 8, be)
+        hi = total
+        for layer in sorted(plan, reverse=True):
+            b, e = plan[layer]
+            assert e == hi and b < e and (e - b >= be)
+            assert b == min(r[0] for r in ranges[layer])     # bucket ends at this layer's first param
+            hi = b
+        assert hi >= 0 and 0 not in plan                      # layer 0's remainder goes at gradients-ready
+    assert plan_buckets(ranges, 8, 10 ** 9) == {}
+    off = {1: 0, 3: 520, 4: 25570, 6: 426070}
+    p1 = plan_buckets(ranges, 8, 1)                        # every param layer its own bucket
+    assert p1 == {6: (426070, total), 4: (25570, 426070), 3: (520, 25570), 1: (0, 520)}
+    assert off[6] == 426070
+    p2 = plan_buckets(ranges, 8, 30000)                    # small tail layers merge upward
+    assert p2 == {4: (25570, total)}                       # [0, 25570) is the gradients-ready remainder
+
+
+def _bucket_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from rramsim.parallel import average_gradients, plan_buckets
+    g = torch.arange(10_000, dtype=torch.float32) * (rank + 1) / 7.0
+    ref = g.clone()
+    average_gradients(ref, world)
+    ranges = [[], [(0, 3000)], [], [(3000, 9000), (9000, 9100)], [(9100, 10_000)]]
+    plan = plan_buckets(ranges, len(ranges), 2000)
+    works, lo = [], g.numel()
+    for layer in range(len(ranges) - 1, -1, -1):            # backward order
+        if layer in plan:
+            b, e = plan[layer]
+            works.append(dist.all_reduce(g[b:e], async_op=True))
+            lo = b
+    if lo > 0:
+        works.append(dist.all_reduce(g[:lo], async_op=True))
+    for w in works:
+        w.wait()
+    g.mul_(1.0 / world)
+    q.put((rank, bool(torch.equal(g, ref)), sorted(plan.items())))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_bucketed_allreduce_equals_flat():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_bucket_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][1] and res[1][1]
+    assert res[0][2] == [(1, (0, 3000)), (3, (3000, 10_000))]
