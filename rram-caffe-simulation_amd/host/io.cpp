@@ -82,6 +82,7 @@ void read_floats(Reader& r, int wt, std::vector<float>& out) {
     CAFFE_CHECK((s.end - s.p) % 4 == 0, "protobuf: packed float payload not a multiple of 4");
     const size_t n = (s.end - s.p) / 4;
     const size_t o = out.size();
+    if (n == 0) return;  // memcpy with a null destination is UB even for 0 bytes
     out.resize(o + n);
     std::memcpy(out.data() + o, s.p, n * 4);
   } else {

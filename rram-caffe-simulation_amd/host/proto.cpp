@@ -99,7 +99,12 @@ class Lexer {
   int line_ = 1, col_ = 1;
 };
 
-void parse_body(Lexer& lx, Msg& m, bool top) {
+// protobuf's text parser stops at 100 levels of nesting (its default
+// recursion limit); deeper input is rejected instead of exhausting the stack
+constexpr int kMaxDepth = 100;
+
+void parse_body(Lexer& lx, Msg& m, bool top, int depth = 0) {
+  if (depth > kMaxDepth) lx.fail("message nesting deeper than 100 levels");
   while (true) {
     if (top) {
       if (lx.eof()) return;
@@ -117,7 +122,7 @@ void parse_body(Lexer& lx, Msg& m, bool top) {
       lx.expect(c);
       v.is_msg = true;
       v.msg = std::make_shared<Msg>();
-      parse_body(lx, *v.msg, false);
+      parse_body(lx, *v.msg, false, depth + 1);
       lx.expect(close);
     } else {
       if (!colon) lx.fail("expected ':' after field '" + key + "'");
@@ -196,7 +201,10 @@ double Msg::num(const std::string& k, double def) const {
   return to_num(v->scalar, k);
 }
 long long Msg::integer(const std::string& k, long long def) const {
-  return static_cast<long long>(num(k, static_cast<double>(def)));
+  const double d = num(k, static_cast<double>(def));
+  // out-of-range (or NaN) -> error, never an undefined float->int conversion
+  if (!(d >= -9.2e18 && d <= 9.2e18)) throw std::runtime_error("field '" + k + "': integer out of range");
+  return static_cast<long long>(d);
 }
 bool Msg::boolean(const std::string& k, bool def) const {
   std::string s = str(k, def ? "true" : "false");
