@@ -12,8 +12,8 @@ Prints ONE JSON line (rank 0):
   value = images classified under faults per second, summed over ranks
   roofline = the conv/IP GEMMs (dominant kernels) vs the fp32 MFMA peak
   roofline_inject = the injection kernel vs HBM peak
-  cpu_baseline = Caffe CPU mode restated (per-image im2col + OpenBLAS sgemm,
-                 oracle fault injection) on a bounded sample, rank 0 at N=1.
+  cpu_baseline = Caffe CPU mode restated in C (oracle/caffe_cpu.c: per-image
+                 im2col + cblas_sgemm, Fail_cpu) over one full map, rank 0 at N=1.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]
         torchrun --nproc-per-node N bench.py --gpus N ...  (one rank per GPU, RCCL)
@@ -46,66 +46,22 @@ def alexnet_gemm_table(batch):
     return t
 
 
-def cpu_baseline(batch, p_fault, seed, budget_s=12.0):
-    """Caffe CPU mode (restated in oracle/): per-image im2col + sgemm on
-    numpy's OpenBLAS, scalar C fault injection.  Bounded sample: one fault map
-    injected into all 58.6M IP weights, then as many single-image forwards as
-    fit in ~budget_s; images/s extrapolated to a 256-image map."""
+def cpu_baseline(batch, p_fault, seed):
+    """Caffe CPU mode restated in C (oracle/caffe_cpu.c): one
+    full Monte-Carlo map of AlexNet b`batch` on this host's cores — the
+    GaussianFailureMaker draws + Fail_cpu over the 58,631,144 IP cells, then
+    the TEST forward of all `batch` images in the reference's layer order
+    (per-image im2col_cpu + cblas_sgemm per group, single-threaded LRN /
+    pool / ReLU loops).  Not extrapolated: the whole map is timed."""
     sys.path.insert(0, str(ROOT / "oracle"))
-    import numpy as np
     import oracle
-    from rramsim import make_inject_cfg
-
-    try:
-        from threadpoolctl import threadpool_info
-        threads = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("internal_api") == "openblas"]
-                      or [1])
-    except Exception:  # pragma: no cover
-        threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
-    rng = np.random.default_rng(seed)
-    W = {"conv1": (96, 3, 11), "conv2": (256, 48, 5), "conv3": (384, 256, 3), "conv4": (384, 192, 3),
-         "conv5": (256, 192, 3)}
-    w = {k: (rng.standard_normal((co, ci, kk, kk)) * 0.01).astype(np.float32) for k, (co, ci, kk) in W.items()}
-    b = {k: np.zeros(W[k][0], np.float32) for k in W}
-    fc = {"fc6": (4096, 9216), "fc7": (4096, 4096), "fc8": (1000, 4096)}
-    fw = {k: (rng.standard_normal(s) * 0.005).astype(np.float32) for k, s in fc.items()}
-    fb = {k: np.full(s[0], 0.1, np.float32) for k, s in fc.items()}
-    c = make_inject_cfg(p_fault)
-    oc = oracle.InjectCfg(c.thr_fault, c.thr_neg, c.thr_zero, c.thr_sa1, 1.0, 0.0, 0, 0.0, 0, 0)
-    t0 = time.perf_counter()
-    lid = 0
-    for k in fc:
-        fw[k], _ = oracle.inject(fw[k], oc, seed, 0, lid)
-        fb[k], _ = oracle.inject(fb[k], oc, seed, 0, lid + 1)
-        lid += 2
-    t_inject = time.perf_counter() - t0
-    x_all = (rng.integers(0, 256, (batch, 3, 227, 227)) - 128).astype(np.float32)
-
-    def fwd(x):
-        y = oracle.relu(oracle.conv_im2col(x, w["conv1"], b["conv1"], 4, 0))
-        y = oracle.pool(oracle.lrn(y, 5, 1e-4, 0.75), 3, 2)
-        y = oracle.relu(oracle.conv_im2col(y, w["conv2"], b["conv2"], 1, 2, 1, 2))
-        y = oracle.pool(oracle.lrn(y, 5, 1e-4, 0.75), 3, 2)
-        y = oracle.relu(oracle.conv_im2col(y, w["conv3"], b["conv3"], 1, 1))
-        y = oracle.relu(oracle.conv_im2col(y, w["conv4"], b["conv4"], 1, 1, 1, 2))
-        y = oracle.relu(oracle.conv_im2col(y, w["conv5"], b["conv5"], 1, 1, 1, 2))
-        y = oracle.pool(y, 3, 2).reshape(x.shape[0], -1)
-        for k in ("fc6", "fc7", "fc8"):
-            y = y @ fw[k].T + fb[k]
-            if k != "fc8":
-                y = np.maximum(y, 0)
-        return oracle.softmax(y)
-
-    n, t1 = 0, time.perf_counter()
-    while n < 2 or (time.perf_counter() - t1 < budget_s and n < 4 * batch):
-        fwd(x_all[n % batch:n % batch + 1])        # cycles over the map's images until the budget is spent
-        n += 1
-    t_img = (time.perf_counter() - t1) / n
-    per_map = t_inject + batch * t_img
-    return {"value": round(batch / per_map, 3), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"1 fault map (C oracle inject of 58,631,144 IP weights: {t_inject:.2f} s) + {n} "
-                      f"single-image AlexNet forwards (im2col + OpenBLAS sgemm: {t_img * 1e3:.0f} ms/img), "
-                      f"extrapolated to one {batch}-image map"}
+    t, meta = oracle.caffe_cpu_alexnet_map(batch=batch, p_fault=p_fault, seed=seed)
+    total = sum(t.values())
+    return {"value": round(batch / total, 3), "unit": "images/s", "cores": meta["threads"], "kind": "port",
+            "sample": f"1 full fault map: {meta['broken_cells']} of 58,631,144 IP cells broken + {batch}-image "
+                      f"AlexNet TEST forward, {total:.2f} s; sgemm = {meta['blas']} on {meta['threads']} threads "
+                      f"(host affinity {meta['affinity_cpus']} CPUs), other layers single-threaded as in Caffe",
+            "layers_ms": {k: round(v * 1e3, 1) for k, v in t.items()}}
 
 
 def load_traffic():
@@ -128,7 +84,6 @@ def main():
     ap.add_argument("--p-fault", type=float, default=0.01)
     ap.add_argument("--seed", type=int, default=1701)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--profile-layers", action="store_true", help="print the per-layer table to stderr")
     ap.add_argument("--workload", default="alexnet_mc",
                     choices=["alexnet_mc", "cifar10_quick_mc", "cifar10_full_train", "googlenet_sweep", "lenet_train",
@@ -247,7 +202,7 @@ def main():
                      "broken_cells": int(stats[len(st["sums"])].item())},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(args.batch, args.p_fault, args.seed, args.cpu_budget)
+        res["cpu_baseline"] = cpu_baseline(args.batch, args.p_fault, args.seed)
     elif rank == 0:
         res["cpu_baseline"] = None
     if rank == 0:

@@ -387,3 +387,177 @@ def genetic_apply(fc_ids, fail_e, prune, weights, rand, switch_time, compat=Fals
                 m[:, [n1, n2]] = m[:, [n2, n1]]
             pout[:, [n1, n2]] = pout[:, [n2, n1]]
     return Wt, P, before, overall(), accepted
+
+
+# ----------------------------------------------------------------------------
+# Caffe CPU mode in C (caffe_cpu.c) — the CPU baseline of bench.py
+# ----------------------------------------------------------------------------
+def blas_candidates():
+    """BLAS libraries on this host the Caffe-CPU restatement can drive:
+    numpy's bundled OpenBLAS (ILP64, scipy_ prefix) first, then an LP64
+    cblas_sgemm (MKL runtime)."""
+    import glob
+    import os
+    out = []
+    for d in {os.path.join(os.path.dirname(np.__file__), os.pardir, "numpy.libs")}:
+        out += [(p, 0, "OpenBLAS (numpy bundled, ILP64)") for p in sorted(glob.glob(os.path.join(d, "libscipy_openblas64_*.so")))]
+    for p in ("/opt/conda/lib/libmkl_rt.so", "/opt/conda/lib/libmkl_rt.so.1"):
+        if os.path.exists(p):
+            out.append((p, 1, "MKL runtime (LP64 cblas_sgemm)"))
+    return out
+
+
+_cc_ready = None
+
+
+def cc_init(threads):
+    """Bind caffe_cpu.c to the first loadable BLAS; returns its description."""
+    global _cc_ready
+    L = lib()
+    P, I, I64, F = C.c_void_p, C.c_int, C.c_int64, C.c_float
+    L.cc_init.argtypes = [C.c_char_p, I, I]
+    L.cc_init.restype = I
+    L.cc_gemm.argtypes = [I, I, I, I, I, F, P, P, F, P]
+    L.cc_conv_forward.argtypes = [P, I, I, I, I, P, P, I, I, I, I, I, P, P, P]
+    L.cc_ip_forward.argtypes = [P, I, I, P, P, I, P, P]
+    L.cc_relu.argtypes = [P, I64]
+    L.cc_lrn.argtypes = [P, P, I, I, I, I, I, F, F, F, P, P]
+    L.cc_maxpool.argtypes = [P, P, P, I, I, I, I, I, I]
+    L.cc_softmax.argtypes = [P, P, I, I]
+    for path, mode, desc in blas_candidates():
+        if L.cc_init(path.encode(), mode, int(threads)) == 0:
+            _cc_ready = desc
+            return desc
+    raise RuntimeError("no usable BLAS for the Caffe-CPU restatement")
+
+
+def cc_conv(x, w, b, stride=1, pad=0, group=1):
+    x, w = f32(x), f32(w)
+    N, Cc, H, W = x.shape
+    Cout, cg, k, _ = w.shape
+    Ho, Wo = out_size(H, k, pad, stride), out_size(W, k, pad, stride)
+    y = np.empty((N, Cout, Ho, Wo), np.float32)
+    col = np.empty(Cc * k * k * Ho * Wo, np.float32)
+    ones = np.ones(Ho * Wo, np.float32)
+    bp = _ptr(f32(b)) if b is not None else None
+    lib().cc_conv_forward(_ptr(x), N, Cc, H, W, _ptr(w), bp, Cout, k, pad, stride, group, _ptr(y), _ptr(col),
+                          _ptr(ones))
+    return y
+
+
+def cc_ip(x, w, b):
+    x, w = f32(x.reshape(len(x), -1)), f32(w)
+    M, K = x.shape
+    N = w.shape[0]
+    y = np.empty((M, N), np.float32)
+    ones = np.ones(M, np.float32)
+    lib().cc_ip_forward(_ptr(x), M, K, _ptr(w), _ptr(f32(b)) if b is not None else None, N, _ptr(y), _ptr(ones))
+    return y
+
+
+def cc_relu(x):
+    x = f32(x)
+    lib().cc_relu(_ptr(x), x.size)
+    return x
+
+
+def cc_lrn(x, size, alpha, beta, k=1.0):
+    x = f32(x)
+    n, c, h, w = x.shape
+    y = np.empty_like(x)
+    scale = np.empty_like(x)
+    padded = np.empty((c + size - 1) * h * w, np.float32)
+    lib().cc_lrn(_ptr(x), _ptr(y), n, c, h, w, size, alpha, beta, k, _ptr(scale), _ptr(padded))
+    return y
+
+
+def cc_maxpool(x, k, s):
+    x = f32(x)
+    n, c, h, w = x.shape
+    ph, pw = pool_out(h, k, 0, s), pool_out(w, k, 0, s)
+    y = np.empty((n, c, ph, pw), np.float32)
+    mask = np.empty((n, c, ph, pw), np.int32)
+    lib().cc_maxpool(_ptr(x), _ptr(y), _ptr(mask), n, c, h, w, k, s)
+    return y
+
+
+def cc_softmax(x):
+    x = f32(x.reshape(len(x), -1))
+    y = np.empty_like(x)
+    lib().cc_softmax(_ptr(x), _ptr(y), x.shape[0], x.shape[1])
+    return y
+
+
+def caffe_cpu_alexnet_map(batch=256, p_fault=0.01, seed=1701, threads=None, images=None):
+    """One Monte-Carlo fault map of AlexNet b`batch` in Caffe CPU mode
+    (SURVEY.md §3.3 / §8d): the GaussianFailureMaker draws for all 58,631,144
+    IP cells (mean = -Phi^-1(p)·std so P(endurance <= 0) = p), Fail_cpu at a
+    zero update (failure_maker.cpp:55-81: every broken cell takes its stuck
+    value), then the TEST forward of `images` (default: all) of the batch in
+    the reference's layer order.  Returns (per-layer seconds, metadata)."""
+    import os
+    import time
+    from statistics import NormalDist
+    if threads is None:
+        aff = len(os.sched_getaffinity(0))
+        env = os.environ.get("OMP_NUM_THREADS")
+        threads = min(aff, int(env)) if env and env.isdigit() else aff
+    blas = cc_init(threads)
+    rng = np.random.default_rng(seed)
+    conv = {"conv1": (96, 3, 11, 4, 0, 1), "conv2": (256, 48, 5, 1, 2, 2), "conv3": (384, 256, 3, 1, 1, 1),
+            "conv4": (384, 192, 3, 1, 1, 2), "conv5": (256, 192, 3, 1, 1, 2)}
+    w = {k: (rng.standard_normal((co, ci, kk, kk)) * 0.01).astype(np.float32) for k, (co, ci, kk, *_r) in conv.items()}
+    b = {k: np.full(conv[k][0], 0.1, np.float32) for k in conv}
+    fcs = {"fc6": (4096, 9216, 0.005), "fc7": (4096, 4096, 0.005), "fc8": (1000, 4096, 0.01)}
+    fw = {k: (rng.standard_normal(s[:2]) * s[2]).astype(np.float32) for k, s in fcs.items()}
+    fb = {k: np.full(s[0], 0.1, np.float32) for k, s in fcs.items()}
+    n_img = batch if images is None else images
+    x = (rng.integers(0, 256, (n_img, 3, 227, 227)) - 128).astype(np.float32)
+    # warm the BLAS thread pool (its first call spawns the threads), untimed
+    cc_conv(x[:1], w["conv1"], b["conv1"], 4, 0, 1)
+    t = {}
+    std = 1e6
+    mean = -NormalDist().inv_cdf(p_fault) * std
+    neg, zero, tot = 10, 20, 40
+    thr_neg = (neg * (1 << 32) + tot - 1) // tot
+    thr_zero = ((neg + zero) * (1 << 32) + tot - 1) // tot
+    t0 = time.perf_counter()
+    broken = 0
+    lid = 0
+    for k in fcs:
+        for arr in (fw, fb):
+            a = arr[k].reshape(-1)
+            e, v = fault_init(a.size, mean, std, thr_neg, thr_zero, seed, 0, lid)
+            dw = np.zeros_like(a)
+            nw, _, nb = fail_apply(dw, a, e, v)
+            arr[k] = nw.reshape(arr[k].shape)
+            broken += nb
+            lid += 1
+    t["fault map (ctor draws + Fail_cpu)"] = time.perf_counter() - t0
+
+    def tick(name, fn, *a):
+        s = time.perf_counter()
+        r = fn(*a)
+        t[name] = t.get(name, 0.0) + time.perf_counter() - s
+        return r
+
+    y = tick("conv1", cc_conv, x, w["conv1"], b["conv1"], 4, 0, 1)
+    y = tick("relu1", cc_relu, y)
+    y = tick("norm1", cc_lrn, y, 5, 1e-4, 0.75)
+    y = tick("pool1", cc_maxpool, y, 3, 2)
+    for i, k in enumerate(("conv2", "conv3", "conv4", "conv5"), start=2):
+        co, ci, kk, s, p, g = conv[k]
+        y = tick(k, cc_conv, y, w[k], b[k], s, p, g)
+        y = tick(f"relu{i}", cc_relu, y)
+        if k == "conv2":
+            y = tick("norm2", cc_lrn, y, 5, 1e-4, 0.75)
+            y = tick("pool2", cc_maxpool, y, 3, 2)
+    y = tick("pool5", cc_maxpool, y, 3, 2)
+    for i, k in enumerate(fcs, start=6):
+        y = tick(k, cc_ip, y, fw[k], fb[k])
+        if k != "fc8":
+            y = tick(f"relu{i}", cc_relu, y)
+    prob = tick("prob (softmax)", cc_softmax, y)
+    meta = dict(blas=blas, threads=threads, affinity_cpus=len(os.sched_getaffinity(0)), images=n_img,
+                broken_cells=broken, finite=bool(np.isfinite(prob).all()))
+    return t, meta

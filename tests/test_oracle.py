@@ -176,3 +176,38 @@ def test_pool_out_rule(oracle_mod):
     assert oracle_mod.pool_out(55, 3, 0, 2) == 27
     assert oracle_mod.pool_out(112, 3, 0, 2) == 56
     assert oracle_mod.pool_out(7, 3, 1, 2) == 4
+
+
+def test_caffe_cpu_restatement_matches_numpy_oracle():
+    """oracle/caffe_cpu.c (bench.py's CPU baseline) computes the same layers as
+    the numpy restatements: conv (per-image im2col + group sgemm + bias sgemm),
+    IP, ReLU, cross-channel LRN, MAX pooling, softmax."""
+    import numpy as np
+    import oracle
+    oracle.cc_init(2)
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((3, 8, 15, 13)).astype(np.float32)
+    for (co, k, s, p, g) in ((6, 3, 1, 1, 1), (8, 5, 2, 2, 2), (4, 1, 1, 0, 1), (6, 3, 2, 0, 2)):
+        w = rng.standard_normal((co, 8 // g, k, k)).astype(np.float32)
+        b = rng.standard_normal(co).astype(np.float32)
+        np.testing.assert_allclose(oracle.cc_conv(x, w, b, s, p, g), oracle.conv_naive(x, w, b, s, p, 1, g),
+                                   rtol=1e-5, atol=1e-5)
+    xi = rng.standard_normal((5, 40)).astype(np.float32)
+    wi = rng.standard_normal((7, 40)).astype(np.float32)
+    bi = rng.standard_normal(7).astype(np.float32)
+    np.testing.assert_allclose(oracle.cc_ip(xi, wi, bi), xi @ wi.T + bi, rtol=1e-5, atol=1e-5)
+    np.testing.assert_array_equal(oracle.cc_relu(x.copy()), oracle.relu(x))
+    np.testing.assert_allclose(oracle.cc_lrn(x, 5, 1e-4, 0.75), oracle.lrn(x, 5, 1e-4, 0.75), rtol=1e-5, atol=1e-6)
+    np.testing.assert_array_equal(oracle.cc_maxpool(x, 3, 2), oracle.pool(x, 3, 2))
+    np.testing.assert_allclose(oracle.cc_softmax(xi), oracle.softmax(xi), rtol=1e-5, atol=1e-7)
+
+
+def test_caffe_cpu_alexnet_map_small():
+    """The CPU-baseline pipeline runs end to end (2 images) and its fault map
+    breaks ~p of the 58.6M IP cells (3.8 sigma binomial bound)."""
+    import math
+    import oracle
+    t, meta = oracle.caffe_cpu_alexnet_map(batch=256, images=2, threads=2, p_fault=0.01)
+    n = 58_631_144
+    assert abs(meta["broken_cells"] / n - 0.01) <= 3.8 * math.sqrt(0.01 * 0.99 / n)
+    assert meta["finite"] and {"conv1", "fc8", "norm1", "pool5"} <= set(t)
