@@ -657,37 +657,89 @@ __global__ void __launch_bounds__(256) RRAM_GEMM_OCC k_gemm(Params P) {
     }
   }
 #else
-  // epilogue: acc[i][j][r] -> row = (r&3) + 8*(r>>2) + 4*lh, col = lr
+  // epilogue: acc[i][j][r] -> row = (r&3) + 8*(r>>2) + 4*lh, col = lr.
+  // Every mode flag is block-uniform, so each loop below is free of
+  // per-element waits: bias values are fetched with address selects (a select
+  // on a loaded value makes the compiler branch around each load and wait for
+  // it: one L2 round trip per output element), alpha and the row bias are
+  // folded into the accumulators once per row, and only edge tiles mask rows.
+  const int mw = m0 + wm * MI * 32 + 4 * lh;           // this lane's first row
+  const bool rows_full = m0 + wm * MI * 32 + MI * 32 <= P.M;
+  if (part != nullptr) {                               // split-K partial slab [M][N]
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int n = n0 + wn * NI * 32 + j * 32 + lr;
+      if (n >= P.N) continue;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = mw + i * 32 + (r & 3) + 8 * (r >> 2);
+          if (rows_full || m < P.M) part[(int64_t)m * P.N + n] = acc[i][j][r];
+        }
+    }
+    return;
+  }
+  const bool row_bias = ep.bias_mode == RRAM_BIAS_ROW, col_bias = ep.bias_mode == RRAM_BIAS_COL;
+  const bool relu = ep.relu != 0;
+  const float alpha = ep.alpha, beta = ep.beta;
+  if (beta == 0.0f) {
+    // o = alpha*v + bias: one bias load per row, shared by the NI column tiles
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = mw + i * 32 + (r & 3) + 8 * (r >> 2);
+        const float b = *((row_bias && m < P.M) ? ep.bias + m : g_zero4);
+#pragma unroll
+        for (int j = 0; j < NI; ++j) acc[i][j][r] = alpha * acc[i][j][r] + b;
+      }
+  }
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
     const int n = n0 + wn * NI * 32 + j * 32 + lr;
     if (n >= P.N) continue;
-    int64_t cbase = 0;
-    if (OM == OUT_NCHW && part == nullptr) {
+    const float cb = *(col_bias ? ep.bias + n : g_zero4);
+    float* cj;
+    if (OM == OUT_NCHW) {
       const uint32_t im = fdiv(static_cast<uint32_t>(n), ep.hw);
-      const uint32_t s = static_cast<uint32_t>(n) - im * ep.hw.d;
-      cbase = (int64_t)im * ep.cimg + s;
+      const uint32_t sp = static_cast<uint32_t>(n) - im * ep.hw.d;
+      cj = ep.C + (int64_t)im * ep.cimg + sp;
+    } else {
+      cj = ep.C + n;
     }
+    const int64_t ld = ep.ldc;
+    if (beta != 0.0f) {
+      // accumulate into C (backward GEMMs): ((alpha*v) + beta*C) + bias
 #pragma unroll
-    for (int i = 0; i < MI; ++i) {
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * MI * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-        if (m >= P.M) continue;
-        const float v = acc[i][j][r];
-        if (part != nullptr) {
-          part[(int64_t)m * P.N + n] = v;
-          continue;
+        for (int r = 0; r < 16; ++r) {
+          const int m = mw + i * 32 + (r & 3) + 8 * (r >> 2);
+          if (!rows_full && m >= P.M) continue;
+          float* dst = cj + (int64_t)m * ld;
+          float o = alpha * acc[i][j][r] + beta * *dst;
+          o += *(row_bias ? ep.bias + m : g_zero4) + cb;
+          *dst = relu ? fmaxf(o, 0.0f) : o;
         }
-        float* dst = (OM == OUT_NCHW) ? (ep.C + cbase + (int64_t)m * ep.ldc)
-                                      : (ep.C + (int64_t)m * ep.ldc + n);
-        float o = ep.alpha * v;
-        if (ep.beta != 0.0f) o += ep.beta * *dst;
-        if (ep.bias_mode == RRAM_BIAS_ROW) o += ep.bias[m];
-        else if (ep.bias_mode == RRAM_BIAS_COL) o += ep.bias[n];
-        if (ep.relu) o = fmaxf(o, 0.0f);
-        *dst = o;
-      }
+    } else if (rows_full) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = mw + i * 32 + (r & 3) + 8 * (r >> 2);
+          const float o = acc[i][j][r] + cb;
+          cj[(int64_t)m * ld] = relu ? fmaxf(o, 0.0f) : o;
+        }
+    } else {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = mw + i * 32 + (r & 3) + 8 * (r >> 2);
+          const float o = acc[i][j][r] + cb;
+          if (m < P.M) cj[(int64_t)m * ld] = relu ? fmaxf(o, 0.0f) : o;
+        }
     }
   }
 #endif
