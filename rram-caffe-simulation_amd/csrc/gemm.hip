@@ -389,7 +389,9 @@ __device__ __forceinline__ float pick(const float4& q, int s) {
 // Measured on MI355X (scripts/gpu_variants.sh): AlexNet b256 GEMMs 3.760 ->
 // 3.667 ms.  RRAM_V_WPE_OFF builds the compiler's own choice for A/B runs.
 #ifndef RRAM_V_WPE_OFF
-#define RRAM_GEMM_OCC __attribute__((amdgpu_waves_per_eu(4)))
+// wave tiles of more than 4 accumulators (MI * NI > 4) need > 128 VGPRs: they
+// target 2 waves per SIMD instead of spilling
+#define RRAM_GEMM_OCC __attribute__((amdgpu_waves_per_eu(MI * NI > 4 ? 2 : 4)))
 #else
 #define RRAM_GEMM_OCC
 #endif
@@ -880,12 +882,23 @@ int launch(const Params& P, int gz, hipStream_t s, bool force_big) {
     return e ? atoi(e) : 0;
   }();
   if (forced == 6464) return launch_cfg<2, 2, 1, 1, AM, BMODE, OM, KB>(P, gz, s);
+  if (forced == 128256) return launch_cfg<2, 2, 2, 4, AM, BMODE, OM, KB>(P, gz, s);  // 128 x 256, 2 waves/SIMD
+  if (forced == 256128) return launch_cfg<2, 2, 4, 2, AM, BMODE, OM, KB>(P, gz, s);  // 256 x 128, 2 waves/SIMD
   // thin M (CIFAR / LeNet convolutions, M = 20..32): a 32 x 128 tile wastes no
   // MFMA rows (64 x 64 would pad half of them)
   if constexpr (KB == 32) {
     if (P.M <= 32 && forced != 64 && forced != 96 && forced != 128 && forced != 192)
       return launch_cfg<1, 4, 1, 1, AM, BMODE, OM, KB>(P, gz, s);
   }
+  // 128 x 256 at 2 waves per SIMD (8 accumulators per wave: half the LDS and
+  // L2 bytes per MFMA of 128 x 128) when M fills whole 128-row tiles and the
+  // grid still gives every CU >= 2 rounds of its 2 resident blocks.  MI355X,
+  // AlexNet b256: conv2 (M = 128 per group, N = 186,624) 1.08 -> 1.04 ms;
+  // conv3 (507 such tiles, one round) 0.70 -> 0.69 ms is within noise, and
+  // conv4 / conv5 / conv1 (fewer tiles or M % 128 != 0) are slower, so they
+  // keep the policy below.
+  if (KB == 16 && !forced && P.M % 128 == 0 && (int64_t)(P.M / 128) * ((P.N + 255) / 256) * gz >= 1024)
+    return launch_cfg<2, 2, 2, 4, AM, BMODE, OM, KB>(P, gz, s);
   const int64_t ntn = (P.N + 127) / 128;
   const int cands[4] = {128, 192, 96, 64};  // ties keep 128 (2 blocks per CU)
   int best = 0;

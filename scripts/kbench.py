@@ -43,6 +43,10 @@ def micro(dev):
     blocks, iters = 256 * 8, 2000
     t = timeit(lambda: lib.micro_mfma_f32(C.c_void_p(o.data_ptr()), blocks, iters, st()), iters=5, warm=2)
     out["mfma_f32_peak_TFs"] = blocks * 4 * iters * 16 * 32 * 32 * 2 * 2 / t / 1e12
+    t = timeit(lambda: lib.micro_mfma_f32_rand(C.c_void_p(o.data_ptr()), blocks, iters // 2, st()), iters=5, warm=2)
+    out["mfma_f32_rand_TFs"] = blocks * 4 * (iters // 2) * 32 * 32 * 32 * 2 * 2 / t / 1e12
+    t = timeit(lambda: lib.micro_lds_mfma(C.c_void_p(o.data_ptr()), 1024, 2000, st()), iters=5, warm=2)
+    out["lds_mfma_core_TFs"] = 1024 * 2000 * 2.0 * 128 * 128 * 16 / t / 1e12
     n = 58_631_144 // 4 * 4
     x = torch.randn(n, device=dev)
     y = torch.empty_like(x)
@@ -90,6 +94,17 @@ def main():
         y = torch.empty_like(x)
         t = timeit(lambda: y.copy_(x))
         res["copy_GBps"] = 8 * n / t / 1e9
+    if a.only == "dense":
+        # the conv layers' GEMM shapes with dense operands (C = A B^T, float4 loads on
+        # both sides): what the same MFMA core reaches without the implicit-im2col gather
+        for name, M, N, K in (("dense_conv3", 384, 43264, 2304), ("dense_conv2g", 128, 186624, 1200),
+                              ("dense_conv1", 96, 774400, 364), ("dense_4096", 4096, 4096, 4096)):
+            A = torch.randn(M, K, device=dev) * 0.01
+            Bm = torch.randn(N, K, device=dev)
+            Cm = torch.empty(M, N, device=dev)
+            t = timeit(lambda: ops.gemm(0, 1, M, N, K, 1.0, A, Bm, 0.0, Cm), iters=5)
+            res[f"{name}_TFs"] = 2.0 * M * N * K / t / 1e12
+            res[f"{name}_ms"] = t * 1e3
     if a.only in ("", "gemm"):
         B = 256
         convs = [("conv1", (B, 3, 227, 227), 96, 11, 4, 0, 1), ("conv2", (B, 96, 27, 27), 256, 5, 1, 2, 2),

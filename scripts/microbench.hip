@@ -26,6 +26,91 @@ __global__ void __launch_bounds__(256) k_mfma(float* out, int iters) {
   if (s == 12345.678f) out[0] = s;  // keep the chain live
 }
 
+// Same chains on random operands: every lane holds 8 random A and 8 random B
+// values (hash of lane, block) used in rotation, so the multipliers toggle as
+// they do in a real GEMM (the DVFS clock depends on the data, MI355X_MICROARCH.md
+// 'DVFS give-back').
+__device__ __forceinline__ float hrand(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+  return (float)(x >> 8) * (2.0f / 16777216.0f) - 1.0f;
+}
+__global__ void __launch_bounds__(256) k_mfma_rand(float* out, int iters) {
+  floatx16 acc[4];
+  for (int i = 0; i < 4; ++i)
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.0f;
+  float a[8], b[8];
+  const uint32_t seed = (blockIdx.x * 256u + threadIdx.x) * 16u;
+  for (int u = 0; u < 8; ++u) {
+    a[u] = hrand(seed + u);
+    b[u] = hrand(seed + 8 + u);
+  }
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], b[(u + i) & 7], acc[i], 0, 0, 0);
+  }
+  float s = 0.f;
+  for (int i = 0; i < 4; ++i)
+    for (int r = 0; r < 16; ++r) s += acc[i][r];
+  if (s == 12345.678f) out[0] = s;  // keep the chain live
+}
+
+// The GEMM core's LDS structure alone (no global traffic): a 128 x 128 block
+// tile, 4 waves of 2 x 2 32x32 accumulators, 16-deep K-tiles padded to 20
+// floats, 8 ds_read_b128 + 32 MFMAs + one barrier per K-tile, double-buffered
+// LDS (the buffers are rewritten from registers each tile, as in k_gemm).
+typedef float floatx4v __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_lds_mfma(float* out, int iters) {
+  __shared__ __attribute__((aligned(16))) float As[2][128 * 20];
+  __shared__ __attribute__((aligned(16))) float Bs[2][128 * 20];
+  for (int i = threadIdx.x; i < 128 * 20; i += 256) {
+    As[0][i] = hrand(i * 3u + blockIdx.x); Bs[0][i] = hrand(i * 5u + blockIdx.x);
+    As[1][i] = hrand(i * 7u + blockIdx.x); Bs[1][i] = hrand(i * 11u + blockIdx.x);
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wm = wave >> 1, wn = wave & 1;
+  const int lr = lane & 31, lh = lane >> 5;
+  floatx16 acc[2][2];
+  for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 2; ++j)
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+  float4 stA = make_float4(1.f, 2.f, 3.f, 4.f), stB = stA;
+  for (int t = 0; t < iters; ++t) {
+    const int cur = t & 1;
+    float4 af[2][2], bf[2][2];
+    for (int i = 0; i < 2; ++i) {
+      const float* pa = &As[cur][(wm * 64 + i * 32 + lr) * 20 + lh * 8];
+      af[i][0] = *reinterpret_cast<const float4*>(pa);
+      af[i][1] = *reinterpret_cast<const float4*>(pa + 4);
+      const float* pb = &Bs[cur][(wn * 64 + i * 32 + lr) * 20 + lh * 8];
+      bf[i][0] = *reinterpret_cast<const float4*>(pb);
+      bf[i][1] = *reinterpret_cast<const float4*>(pb + 4);
+    }
+#pragma unroll
+    for (int s8 = 0; s8 < 8; ++s8) {
+      const int q = s8 >> 2, e = s8 & 3;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const float a = e == 0 ? af[i][q].x : e == 1 ? af[i][q].y : e == 2 ? af[i][q].z : af[i][q].w;
+          const float b = e == 0 ? bf[j][q].x : e == 1 ? bf[j][q].y : e == 2 ? bf[j][q].z : bf[j][q].w;
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[i][j], 0, 0, 0);
+        }
+    }
+    // restage: 2 float4 per thread per operand into the other buffer
+    *reinterpret_cast<float4*>(&As[cur ^ 1][(threadIdx.x >> 2) * 20 + (threadIdx.x & 3) * 4]) = stA;
+    *reinterpret_cast<float4*>(&Bs[cur ^ 1][(threadIdx.x >> 2) * 20 + (threadIdx.x & 3) * 4]) = stB;
+    __syncthreads();
+  }
+  float s = 0.f;
+  for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 2; ++j)
+      for (int r = 0; r < 16; ++r) s += acc[i][j][r];
+  if (s == 12345.678f) out[0] = s;
+}
+
 __global__ void __launch_bounds__(256) k_copy(const float4* __restrict__ x, float4* __restrict__ y, int64_t n4) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x)
     y[i] = x[i];
@@ -62,6 +147,14 @@ __global__ void __launch_bounds__(256) k_philox(uint32_t* out, int64_t calls_per
 extern "C" {
 int micro_mfma_f32(float* out, int blocks, int iters, void* s) {
   hipLaunchKernelGGL(k_mfma, dim3(blocks), dim3(256), 0, (hipStream_t)s, out, iters);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+int micro_mfma_f32_rand(float* out, int blocks, int iters, void* s) {
+  hipLaunchKernelGGL(k_mfma_rand, dim3(blocks), dim3(256), 0, (hipStream_t)s, out, iters);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+int micro_lds_mfma(float* out, int blocks, int iters, void* s) {
+  hipLaunchKernelGGL(k_lds_mfma, dim3(blocks), dim3(256), 0, (hipStream_t)s, out, iters);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 int micro_copy_f32(const float* x, float* y, int64_t n, int blocks, void* s) {
