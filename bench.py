@@ -98,10 +98,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; RRAM_BENCH_DIST_BACKEND=gloo (test hook) lets a box with
+    # fewer GPUs than ranks rehearse the N > 1 path, ranks then share devices
+    backend = os.environ.get("RRAM_BENCH_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     caffe.set_stream_from_torch()
     caffe.set_random_seed(args.seed)
     if args.workload != "alexnet_mc":

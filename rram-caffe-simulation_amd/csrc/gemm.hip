@@ -897,7 +897,11 @@ int launch(const Params& P, int gz, hipStream_t s, bool force_big) {
   // conv3 (507 such tiles, one round) 0.70 -> 0.69 ms is within noise, and
   // conv4 / conv5 / conv1 (fewer tiles or M % 128 != 0) are slower, so they
   // keep the policy below.
-  if (KB == 16 && !forced && P.M % 128 == 0 && (int64_t)(P.M / 128) * ((P.N + 255) / 256) * gz >= 1024)
+  static const bool wide = [] {
+    const char* e = getenv("RRAM_GEMM_WIDE");  // tuning knob: 0 disables the 128 x 256 tile
+    return !(e && atoi(e) == 0);
+  }();
+  if (KB == 16 && wide && !forced && P.M % 128 == 0 && (int64_t)(P.M / 128) * ((P.N + 255) / 256) * gz >= 1024)
     return launch_cfg<2, 2, 2, 4, AM, BMODE, OM, KB>(P, gz, s);
   const int64_t ntn = (P.N + 127) / 128;
   const int cands[4] = {128, 192, 96, 64};  // ties keep 128 (2 blocks per CU)

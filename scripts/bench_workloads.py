@@ -167,12 +167,14 @@ def run_workload(args, world, rank, dev):
                                power=0.75, max_iter=100000, failure_mean=5e3, failure_std=1e3,
                                failure_prob=(10, 20, 10))
         opts = dict(opts, fused_update=True)
-        dp = DataParallelSolver(sp, net_txt, opts, seed=args.seed)
+        # bucketed gradient all-reduce overlapped with backward (world > 1 only)
+        dp = DataParallelSolver(sp, net_txt, opts, seed=args.seed, overlap=True)
         el = _timed(world, dev, lambda i: dp.step(1), args.steps, args.warmup)
         res = _base(f"fault-aware training images/sec, {args.workload}", "images/s",
                     world * args.steps * batch / el, world, args, el, workload=args.workload,
                     model=args.workload.split("_")[0], global_batch=batch * world,
-                    parallelism=f"dp{world} (RCCL all-reduce of {dp.num_params} fp32 grads)")
+                    parallelism=f"dp{world} (RCCL all-reduce of {dp.num_params} fp32 grads"
+                                f"{', bucketed, overlapped with backward' if dp.overlap else ''})")
         res["broken_cells"] = sum(dp.solver.broken_counts())
         dp.close()
         return res

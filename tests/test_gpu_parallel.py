@@ -150,3 +150,34 @@ def test_dp_two_ranks_equal_one_process_double_batch(device):
         assert ov and calls == 3 and bcalls > 3            # more than one bucket per iteration
         assert np.array_equal(w.view(np.uint32), f[1].view(np.uint32)), rank
         assert np.array_equal(e.view(np.uint32), f[2].view(np.uint32)) and b == f[3]
+
+
+@pytest.mark.parametrize("workload", ["alexnet_mc", "cifar10_full_train"])
+def test_bench_two_ranks_rehearsal(device, workload):
+    """bench.py's N > 1 path end to end (torch.distributed.run, 2 ranks, map /
+    batch sharding, barrier + max-over-ranks timing, stats all-reduce, the
+    overlapped gradient buckets of the training workload) on this box's one
+    GPU: RRAM_BENCH_DIST_BACKEND=gloo lets both ranks share it (the driver's
+    multi-GPU runs use RCCL, one GPU per rank)."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    env = dict(os.environ, RRAM_BENCH_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(root / "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--workload", workload]
+    if workload == "alexnet_mc":
+        cmd += ["--batch", "64"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=str(root))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout                     # rank 0 prints exactly one JSON line
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["steps"] == 3 and res["value"] > 0
+    if workload == "alexnet_mc":
+        assert res["mc_stats"]["maps"] == 6              # 3 maps on each of the 2 ranks
+        assert res["config"]["global_batch"] == 128 and res["cpu_baseline"] is None
+    else:
+        assert "overlapped" in res["config"]["parallelism"]
