@@ -152,23 +152,28 @@ int rram_solver_apply_strategies(rram_solver_t s);
 /* Strategy i's type and counters: genetic -> (dist before, dist after,
  * accepted swaps) of its last Apply(); others -> zeros. */
 int rram_solver_strategy_info(rram_solver_t s, int i, char* type, int cap, int* a, int* b, int* c);
-/* Solver::Snapshot (solver.cpp:461-518, BINARYPROTO): writes
- * <snapshot_prefix>_iter_N.{caffemodel,solverstate,faultstate}; the
- * .solverstate path is copied into path_out (cap bytes, nullable). */
+/* Solver::Snapshot (solver.cpp:461-518, sgd_solver.cpp:249-305): writes
+ * <snapshot_prefix>_iter_N.{caffemodel,solverstate} (snapshot_format
+ * BINARYPROTO) or .{caffemodel.h5,solverstate.h5} (HDF5), plus .faultstate;
+ * the solver-state path is copied into path_out (cap bytes, nullable). */
 int rram_solver_snapshot(rram_solver_t s, char* path_out, int cap);
-/* Solver::Restore (sgd_solver.cpp:309-326) from a .solverstate; the fault
- * maps are restored when the matching .faultstate exists. */
+/* Solver::Restore (solver.cpp:520-530, sgd_solver.cpp:307-351) from a
+ * .solverstate or .solverstate.h5; the fault maps are restored when the
+ * matching .faultstate exists. */
 int rram_solver_restore(rram_solver_t s, const char* state_file);
 /* Solver::Solve(resume_file) (solver.cpp:328-370); resume_file nullable. */
 int rram_solver_solve_from(rram_solver_t s, const char* resume_file);
 
 /* ------------------------------------------------------ weight files
- * Net::CopyTrainedLayersFrom (net.cpp:765-818) for a binary .caffemodel
- * (NetParameter `layer` or V1 `layers`), and Net::ToProto + write
- * (net.cpp:871-880): name/type/bottom/top/blobs of every layer. */
+ * Net::CopyTrainedLayersFrom (net.cpp:765-860) for a binary .caffemodel
+ * (NetParameter `layer` or V1 `layers`) or, for a name ending in ".h5", the
+ * HDF5 layout (group "data" / layer name / dataset "<blob index>"); and
+ * Net::ToProto + write (net.cpp:871-880) or Net::ToHDF5 (net.cpp:862-932,
+ * ".h5" names).  HDF5 goes through libhdf5 / libhdf5_hl loaded at run time
+ * (RRAM_HDF5_LIB_DIR); without them the .h5 paths return RRAM_EINVAL. */
 int rram_net_copy_trained_layers_from(rram_net_t net, const char* caffemodel);
 int rram_net_save_weights(rram_net_t net, const char* caffemodel, int write_diff);
-/* Host-only (no device): one line per blob of a .caffemodel,
+/* Host-only (no device): one line per blob of a .caffemodel (or .h5: type "-"),
  * "layer\ttype\tindex\tshape\tcount\tdata_sum\tdiff_count"; *needed = bytes
  * including the terminator. */
 int rram_caffemodel_describe(const char* caffemodel, char* out, size_t cap, size_t* needed);

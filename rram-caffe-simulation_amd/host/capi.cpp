@@ -5,6 +5,7 @@
 #include <string>
 
 #include "rram_caffe.h"
+#include "hdf5.hpp"
 #include "solver.hpp"
 
 using namespace caffe;
@@ -537,13 +538,17 @@ int rram_net_save_weights(rram_net_t n, const char* path, int write_diff) {
   return guarded([&] {
     NEED(n);
     NEED(path);
-    WriteFileBytes(path, SerializeNetParameter(n->net->ToProto(write_diff != 0)));
+    const std::string p(path);
+    if (p.size() >= 3 && p.compare(p.size() - 3, 3, ".h5") == 0) n->net->ToHDF5(p, write_diff != 0);
+    else WriteFileBytes(p, SerializeNetParameter(n->net->ToProto(write_diff != 0)));
   });
 }
 int rram_caffemodel_describe(const char* path, char* out, size_t cap, size_t* needed) {
   return guarded([&] {
     NEED(path);
-    const std::string d = DescribeNetProto(ParseNetParameter(ReadFileBytes(path)));
+    const std::string p(path);
+    const bool h5file = p.size() >= 3 && p.compare(p.size() - 3, 3, ".h5") == 0;
+    const std::string d = DescribeNetProto(h5file ? h5::read_net(p) : ParseNetParameter(ReadFileBytes(p)));
     if (needed) *needed = d.size() + 1;
     if (out && cap > 0) {
       const size_t k = std::min(d.size(), cap - 1);

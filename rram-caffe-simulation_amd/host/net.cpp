@@ -1,5 +1,7 @@
 #include "net.hpp"
 
+#include "hdf5.hpp"
+
 #include <algorithm>
 #include <set>
 #include <sstream>
@@ -269,6 +271,8 @@ void Net<Dtype>::AppendParam(int layer_id, int param_id, const Msg& lp) {
   const std::string pname = spec ? spec->str("name", "") : "";
   const int net_param_id = static_cast<int>(params_.size());
   params_.push_back(layers_[layer_id]->blobs()[param_id]);
+  if ((int)param_id_vecs_.size() <= layer_id) param_id_vecs_.resize(layer_id + 1);
+  param_id_vecs_[layer_id].push_back(net_param_id);
   if (!pname.empty() && param_names_index_.count(pname)) {
     // shared parameter: alias the owner's storage (net.cpp:497-540)
     const int owner = param_names_index_[pname];
@@ -433,12 +437,72 @@ void Net<Dtype>::CopyTrainedLayersFrom(const NetProtoData& param) {
   }
 }
 
-// net.cpp:803-818 (binary proto; HDF5 weights are out of scope)
+// net.cpp:803-818
 template <typename Dtype>
 void Net<Dtype>::CopyTrainedLayersFrom(const std::string& path) {
-  CAFFE_CHECK(path.size() < 3 || path.compare(path.size() - 3, 3, ".h5") != 0,
-              "HDF5 weight files are not supported by this build: " << path);
+  if (path.size() >= 3 && path.compare(path.size() - 3, 3, ".h5") == 0) {
+    CopyTrainedLayersFromHDF5(path);
+    return;
+  }
   CopyTrainedLayersFrom(ParseNetParameter(ReadFileBytes(path)));
+}
+
+// net.cpp:819-860 (CopyTrainedLayersFromHDF5).  The reference reshapes the
+// target blob to the dataset's dims; here the element count must match (the
+// target keeps its shape, so legacy 4-D and N-D forms of one blob both load).
+template <typename Dtype>
+void Net<Dtype>::CopyTrainedLayersFromHDF5(const std::string& path) {
+  h5::Handle file = h5::open_file(path);
+  CAFFE_CHECK(h5::link_exists(file.id(), "data"), "Error reading weights from " << path);
+  h5::Handle data = h5::open_group(file.id(), "data");
+  const int num_layers = h5::num_links(data.id());
+  for (int i = 0; i < num_layers; ++i) {
+    const std::string name = h5::name_by_idx(data.id(), i);
+    auto it = layer_names_index_.find(name);
+    if (it == layer_names_index_.end()) continue;  // "Ignoring source layer"
+    const int lid = it->second;
+    auto& target = layers_[lid]->blobs();
+    h5::Handle layer = h5::open_group(data.id(), name);
+    CAFFE_CHECK(h5::num_links(layer.id()) <= (int)target.size(), "Incompatible number of blobs for layer " << name);
+    for (size_t j = 0; j < target.size(); ++j) {
+      const std::string ds = std::to_string(j);
+      if (!h5::link_exists(layer.id(), ds)) {
+        const int npid = param_id_vecs_[lid][j];
+        CAFFE_CHECK(param_owners_[npid] != -1, "Incompatible number of blobs for layer " << name);
+        continue;  // weight-shared in the target: the owner's dataset fills it
+      }
+      std::vector<int64_t> dims;
+      BlobProtoData p;
+      p.data = h5::load_floats(layer.id(), ds, &dims);
+      CAFFE_CHECK((int64_t)p.data.size() == target[j]->count(),
+                  "Cannot copy param " << j << " weights from layer '" << name << "'; " << p.data.size()
+                                       << " elements, target param shape is " << target[j]->shape_string());
+      BlobFromProto(target[j].get(), p);
+    }
+  }
+}
+
+// net.cpp:862-932 (ToHDF5): only params that own themselves are written to
+// "data"; "diff" holds every param's gradient when write_diff
+template <typename Dtype>
+void Net<Dtype>::ToHDF5(const std::string& path, bool write_diff) const {
+  h5::Handle file = h5::create_file(path);
+  h5::Handle data = h5::create_group(file.id(), "data");
+  h5::Handle diff;
+  if (write_diff) diff = h5::create_group(file.id(), "diff");
+  for (size_t lid = 0; lid < layers_.size(); ++lid) {
+    h5::Handle ld = h5::create_group(data.id(), layer_names_[lid]);
+    h5::Handle lg;
+    if (write_diff) lg = h5::create_group(diff.id(), layer_names_[lid]);
+    const auto& blobs = layers_[lid]->blobs();
+    for (size_t j = 0; j < blobs.size(); ++j) {
+      const int npid = lid < param_id_vecs_.size() && j < param_id_vecs_[lid].size() ? param_id_vecs_[lid][j] : -1;
+      const BlobProtoData p = BlobToProto(blobs[j].get(), write_diff);
+      const std::vector<int64_t> dims(blobs[j]->shape().begin(), blobs[j]->shape().end());
+      if (npid < 0 || param_owners_[npid] == -1) h5::save_floats(ld.id(), std::to_string(j), dims, p.data.data());
+      if (write_diff) h5::save_floats(lg.id(), std::to_string(j), dims, p.diff.data());
+    }
+  }
 }
 
 // net.cpp:871-880 / layer.hpp ToProto: name, type, bottoms, tops and blobs of

@@ -42,8 +42,12 @@ class Net {
   void ShareTrainedLayersWith(const Net* other);
   // .caffemodel weights (net.cpp:765-880, binary proto only; io.hpp)
   void CopyTrainedLayersFrom(const NetProtoData& param);
+  // binary proto, or HDF5 when the name ends in ".h5" (net.cpp:803-860)
   void CopyTrainedLayersFrom(const std::string& path);
+  void CopyTrainedLayersFromHDF5(const std::string& path);
   NetProtoData ToProto(bool write_diff = false) const;
+  // net.cpp:862-932: group "data" (and "diff") / layer name / dataset "<param index>"
+  void ToHDF5(const std::string& path, bool write_diff = false) const;
 
   const std::string& name() const { return name_; }
   Phase phase() const { return phase_; }
@@ -110,6 +114,7 @@ class Net {
   std::vector<Blob<Dtype>*> learnable_params_;
   std::vector<float> params_lr_, params_weight_decay_;
   std::vector<int> param_owners_;
+  std::vector<std::vector<int>> param_id_vecs_;  // per layer: net param id of each of its blobs
   std::map<std::string, int> param_names_index_;
   std::vector<Blob<Dtype>*> failure_learnable_params_;
   std::vector<int> failure_learnable_layer_ids_, failure_learnable_param_ids_;

@@ -1,5 +1,7 @@
 #include "solver.hpp"
 
+#include "hdf5.hpp"
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -426,21 +428,44 @@ void Solver<Dtype>::Solve(const char* resume_file) {
   emit("Optimization Done.");
 }
 
+// solver.cpp:461-495 + sgd_solver.cpp:249-305: weights then solver state, as
+// binary proto (.caffemodel / .solverstate) or HDF5 (.caffemodel.h5 /
+// .solverstate.h5); the fault maps go to <prefix>_iter_N.faultstate either way
 template <typename Dtype>
 std::string Solver<Dtype>::Snapshot() {
-  CAFFE_CHECK(param_.str("snapshot_format", "BINARYPROTO") == "BINARYPROTO",
-              "only snapshot_format: BINARYPROTO is supported by this build (HDF5: DESIGN.md §6)");
-  const std::string model = SnapshotFilename(".caffemodel");
-  emit("Snapshotting to binary proto file " + model);
-  WriteFileBytes(model, SerializeNetParameter(net_->ToProto(param_.boolean("snapshot_diff", false))));
-  SolverStateData st;
-  st.iter = iter_;
-  st.learned_net = model;
-  st.current_step = current_step_;
-  for (auto& h : history_) st.history.push_back(BlobToProto(h.get(), false));
-  const std::string state = SnapshotFilename(".solverstate");
-  emit("Snapshotting solver state to binary proto file " + state);
-  WriteFileBytes(state, SerializeSolverState(st));
+  const std::string fmt = param_.str("snapshot_format", "BINARYPROTO");
+  CAFFE_CHECK(fmt == "BINARYPROTO" || fmt == "HDF5", "Unsupported snapshot format " << fmt);
+  const bool diff = param_.boolean("snapshot_diff", false);
+  std::string state;
+  if (fmt == "HDF5") {
+    const std::string model = SnapshotFilename(".caffemodel.h5");
+    emit("Snapshotting to HDF5 file " + model);
+    net_->ToHDF5(model, diff);
+    state = SnapshotFilename(".solverstate.h5");
+    emit("Snapshotting solver state to HDF5 file " + state);
+    h5::Handle f = h5::create_file(state);
+    h5::save_int(f.id(), "iter", iter_);
+    h5::save_string(f.id(), "learned_net", model);
+    h5::save_int(f.id(), "current_step", current_step_);
+    h5::Handle hg = h5::create_group(f.id(), "history");
+    for (size_t i = 0; i < history_.size(); ++i) {
+      const BlobProtoData p = BlobToProto(history_[i].get(), false);
+      h5::save_floats(hg.id(), std::to_string(i),
+                      std::vector<int64_t>(history_[i]->shape().begin(), history_[i]->shape().end()), p.data.data());
+    }
+  } else {
+    const std::string model = SnapshotFilename(".caffemodel");
+    emit("Snapshotting to binary proto file " + model);
+    WriteFileBytes(model, SerializeNetParameter(net_->ToProto(diff)));
+    SolverStateData st;
+    st.iter = iter_;
+    st.learned_net = model;
+    st.current_step = current_step_;
+    for (auto& h : history_) st.history.push_back(BlobToProto(h.get(), false));
+    state = SnapshotFilename(".solverstate");
+    emit("Snapshotting solver state to binary proto file " + state);
+    WriteFileBytes(state, SerializeSolverState(st));
+  }
   if (fmaker_) {
     std::vector<BlobProtoData> fs;
     for (auto* b : fmaker_->fail_iterations()) fs.push_back(BlobToProto(b, true));  // data = e, diff = v
@@ -449,33 +474,54 @@ std::string Solver<Dtype>::Snapshot() {
   return state;
 }
 
+static bool ends_with(const std::string& s, const std::string& suf) {
+  return s.size() >= suf.size() && s.compare(s.size() - suf.size(), suf.size(), suf) == 0;
+}
+
+// solver.cpp:520-530 + sgd_solver.cpp:307-351
 template <typename Dtype>
 void Solver<Dtype>::Restore(const std::string& state_file) {
-  CAFFE_CHECK(state_file.size() < 3 || state_file.compare(state_file.size() - 3, 3, ".h5") != 0,
-              "HDF5 solver states are not supported by this build: " << state_file);
-  const SolverStateData st = ParseSolverState(ReadFileBytes(state_file));
-  iter_ = st.iter;
-  if (!st.learned_net.empty()) net_->CopyTrainedLayersFrom(st.learned_net);
-  current_step_ = st.current_step;
-  CAFFE_CHECK(st.history.size() == history_.size(), "Incorrect length of history blobs.");
-  for (size_t i = 0; i < history_.size(); ++i) {
-    CAFFE_CHECK(ShapeEquals(history_[i]->shape(), st.history[i]), "history blob " << i << ": shape mismatch");
-    BlobFromProto(history_[i].get(), st.history[i]);
+  std::string fault_file;
+  if (ends_with(state_file, ".h5")) {
+    h5::Handle f = h5::open_file(state_file);
+    iter_ = h5::load_int(f.id(), "iter");
+    if (h5::dataset_exists(f.id(), "learned_net")) net_->CopyTrainedLayersFrom(h5::load_string(f.id(), "learned_net"));
+    current_step_ = h5::load_int(f.id(), "current_step");
+    h5::Handle hg = h5::open_group(f.id(), "history");
+    CAFFE_CHECK(h5::num_links(hg.id()) == (int)history_.size(), "Incorrect length of history blobs.");
+    for (size_t i = 0; i < history_.size(); ++i) {
+      std::vector<int64_t> dims;
+      BlobProtoData p;
+      p.data = h5::load_floats(hg.id(), std::to_string(i), &dims);
+      CAFFE_CHECK((int64_t)p.data.size() == history_[i]->count(), "history blob " << i << ": size mismatch");
+      BlobFromProto(history_[i].get(), p);
+    }
+    if (ends_with(state_file, ".solverstate.h5"))
+      fault_file = state_file.substr(0, state_file.size() - 15) + ".faultstate";
+  } else {
+    const SolverStateData st = ParseSolverState(ReadFileBytes(state_file));
+    iter_ = st.iter;
+    if (!st.learned_net.empty()) net_->CopyTrainedLayersFrom(st.learned_net);
+    current_step_ = st.current_step;
+    CAFFE_CHECK(st.history.size() == history_.size(), "Incorrect length of history blobs.");
+    for (size_t i = 0; i < history_.size(); ++i) {
+      CAFFE_CHECK(ShapeEquals(history_[i]->shape(), st.history[i]), "history blob " << i << ": shape mismatch");
+      BlobFromProto(history_[i].get(), st.history[i]);
+    }
+    if (ends_with(state_file, ".solverstate"))
+      fault_file = state_file.substr(0, state_file.size() - 12) + ".faultstate";
   }
-  const std::string suffix = ".solverstate";
-  if (fmaker_ && state_file.size() > suffix.size() &&
-      state_file.compare(state_file.size() - suffix.size(), suffix.size(), suffix) == 0) {
-    const std::string fpath = state_file.substr(0, state_file.size() - suffix.size()) + ".faultstate";
-    std::ifstream probe(fpath, std::ios::binary);
+  if (fmaker_ && !fault_file.empty()) {
+    std::ifstream probe(fault_file, std::ios::binary);
     if (probe.good()) {
-      const auto fs = ParseBlobProtoVector(ReadFileBytes(fpath));
+      const auto fs = ParseBlobProtoVector(ReadFileBytes(fault_file));
       auto fi = fmaker_->fail_iterations();
       CAFFE_CHECK(fs.size() == fi.size(), "fault state: " << fs.size() << " blobs, net has " << fi.size());
       for (size_t i = 0; i < fi.size(); ++i) {
         CAFFE_CHECK(ShapeEquals(fi[i]->shape(), fs[i]) && !fs[i].diff.empty(), "fault state blob " << i << ": mismatch");
         BlobFromProto(fi[i], fs[i]);
       }
-      emit("Restored fault state from " + fpath);
+      emit("Restored fault state from " + fault_file);
     }
   }
 }

@@ -262,12 +262,16 @@ layer { name: "ip2" type: "InnerProduct" bottom: "ip1" top: "ip2" inner_product_
 
 
 # ----------------------------------------------------- snapshot / restore
-def test_snapshot_restore_resumes_bit_exact(rs, tmp_path):
+@pytest.mark.parametrize("fmt", ["BINARYPROTO", "HDF5"])
+def test_snapshot_restore_resumes_bit_exact(rs, tmp_path, fmt):
     """Snapshot at iter 3 (weights, momentum history, fault maps), restore into
-    a fresh solver, continue: identical to the uninterrupted run."""
+    a fresh solver, continue: identical to the uninterrupted run, in both of
+    the reference's snapshot formats (solver.cpp:461-530, sgd_solver.cpp:249-351;
+    cifar10_full_solver.prototxt itself asks for HDF5)."""
     caffe, models = rs
     prefix = tmp_path / "snap"
-    extra = f'snapshot_prefix: "{prefix}"\n'
+    extra = f'snapshot_prefix: "{prefix}"\nsnapshot_format: {fmt}\n'
+    h5 = ".h5" if fmt == "HDF5" else ""
     kw = dict(failure_mean=300.0, failure_std=200.0, failure_prob=(10, 20, 10))
 
     def make(seed):
@@ -277,8 +281,8 @@ def test_snapshot_restore_resumes_bit_exact(rs, tmp_path):
     a = make(5)
     a.step(3)
     state = a.snapshot()
-    assert state.endswith("snap_iter_3.solverstate")
-    for ext in (".caffemodel", ".solverstate", ".faultstate"):
+    assert state.endswith("snap_iter_3.solverstate" + h5)
+    for ext in (".caffemodel" + h5, ".solverstate" + h5, ".faultstate"):
         assert (tmp_path / f"snap_iter_3{ext}").exists()
     a.step(2)
     b = make(5)                                      # same synthetic data; scramble what restore must bring back
