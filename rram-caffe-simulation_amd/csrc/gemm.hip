@@ -22,6 +22,7 @@
 #include <array>
 #include <map>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 #include "rram_common.hpp"
@@ -383,6 +384,98 @@ __device__ __forceinline__ float pick(const float4& q, int s) {
   return (s & 3) == 0 ? q.x : (s & 3) == 1 ? q.y : (s & 3) == 2 ? q.z : q.w;
 }
 
+// Epilogue of one wave's MI x NI tiles of 32x32 (v_mfma_f32_32x32x2_f32
+// accumulator layout): acc[i][j][r] -> row = mwave + 32 i + (r&3) + 8*(r>>2) + 4*lh,
+// col = nwave + 32 j + lr.  Shared by k_gemm and k_gemm2.
+template <int MI, int NI, int OM>
+__device__ __forceinline__ void gemm_epilogue(floatx16 (&acc)[MI][NI], const Params& P, const Epi& ep, float* part,
+                                              int mwave, int nwave, int lr, int lh) {
+  // Every mode flag is block-uniform, so each loop below is free of
+  // per-element waits: bias values are fetched with address selects (a select
+  // on a loaded value makes the compiler branch around each load and wait for
+  // it: one L2 round trip per output element), alpha and the row bias are
+  // folded into the accumulators once per row, and only edge tiles mask rows.
+  const int mw = mwave + 4 * lh;                       // this lane's first row
+  const bool rows_full = mwave + MI * 32 <= P.M;
+  if (part != nullptr) {                               // split-K partial slab [M][N]
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int n = nwave + j * 32 + lr;
+      if (n >= P.N) continue;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = mw + i * 32 + (r & 3) + 8 * (r >> 2);
+          if (rows_full || m < P.M) part[(int64_t)m * P.N + n] = acc[i][j][r];
+        }
+    }
+    return;
+  }
+  const bool row_bias = ep.bias_mode == RRAM_BIAS_ROW, col_bias = ep.bias_mode == RRAM_BIAS_COL;
+  const bool relu = ep.relu != 0;
+  const float alpha = ep.alpha, beta = ep.beta;
+  if (beta == 0.0f) {
+    // o = alpha*v + bias: one bias load per row, shared by the NI column tiles
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = mw + i * 32 + (r & 3) + 8 * (r >> 2);
+        const float b = *((row_bias && m < P.M) ? ep.bias + m : g_zero4);
+#pragma unroll
+        for (int j = 0; j < NI; ++j) acc[i][j][r] = alpha * acc[i][j][r] + b;
+      }
+  }
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int n = nwave + j * 32 + lr;
+    if (n >= P.N) continue;
+    const float cb = *(col_bias ? ep.bias + n : g_zero4);
+    float* cj;
+    if (OM == OUT_NCHW) {
+      const uint32_t im = fdiv(static_cast<uint32_t>(n), ep.hw);
+      const uint32_t sp = static_cast<uint32_t>(n) - im * ep.hw.d;
+      cj = ep.C + (int64_t)im * ep.cimg + sp;
+    } else {
+      cj = ep.C + n;
+    }
+    const int64_t ld = ep.ldc;
+    if (beta != 0.0f) {
+      // accumulate into C (backward GEMMs): ((alpha*v) + beta*C) + bias
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = mw + i * 32 + (r & 3) + 8 * (r >> 2);
+          if (!rows_full && m >= P.M) continue;
+          float* dst = cj + (int64_t)m * ld;
+          float o = alpha * acc[i][j][r] + beta * *dst;
+          o += *(row_bias ? ep.bias + m : g_zero4) + cb;
+          *dst = relu ? fmaxf(o, 0.0f) : o;
+        }
+    } else if (rows_full) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = mw + i * 32 + (r & 3) + 8 * (r >> 2);
+          const float o = acc[i][j][r] + cb;
+          cj[(int64_t)m * ld] = relu ? fmaxf(o, 0.0f) : o;
+        }
+    } else {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = mw + i * 32 + (r & 3) + 8 * (r >> 2);
+          const float o = acc[i][j][r] + cb;
+          if (m < P.M) cj[(int64_t)m * ld] = relu ? fmaxf(o, 0.0f) : o;
+        }
+    }
+  }
+}
+
 // Occupancy target 4 waves per SIMD: the 128 x 128 / KB = 16 conv tile then
 // keeps its accumulators in VGPRs (116 VGPRs, no AGPRs, no spills) instead of
 // 80 VGPRs + 64 AGPRs at 3 waves; 4 blocks x 40 KB fill the 160 KB LDS.
@@ -659,92 +752,372 @@ __global__ void __launch_bounds__(256) RRAM_GEMM_OCC k_gemm(Params P) {
     }
   }
 #else
-  // epilogue: acc[i][j][r] -> row = (r&3) + 8*(r>>2) + 4*lh, col = lr.
-  // Every mode flag is block-uniform, so each loop below is free of
-  // per-element waits: bias values are fetched with address selects (a select
-  // on a loaded value makes the compiler branch around each load and wait for
-  // it: one L2 round trip per output element), alpha and the row bias are
-  // folded into the accumulators once per row, and only edge tiles mask rows.
-  const int mw = m0 + wm * MI * 32 + 4 * lh;           // this lane's first row
-  const bool rows_full = m0 + wm * MI * 32 + MI * 32 <= P.M;
-  if (part != nullptr) {                               // split-K partial slab [M][N]
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int n = n0 + wn * NI * 32 + j * 32 + lr;
-      if (n >= P.N) continue;
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = mw + i * 32 + (r & 3) + 8 * (r >> 2);
-          if (rows_full || m < P.M) part[(int64_t)m * P.N + n] = acc[i][j][r];
-        }
-    }
-    return;
-  }
-  const bool row_bias = ep.bias_mode == RRAM_BIAS_ROW, col_bias = ep.bias_mode == RRAM_BIAS_COL;
-  const bool relu = ep.relu != 0;
-  const float alpha = ep.alpha, beta = ep.beta;
-  if (beta == 0.0f) {
-    // o = alpha*v + bias: one bias load per row, shared by the NI column tiles
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = mw + i * 32 + (r & 3) + 8 * (r >> 2);
-        const float b = *((row_bias && m < P.M) ? ep.bias + m : g_zero4);
-#pragma unroll
-        for (int j = 0; j < NI; ++j) acc[i][j][r] = alpha * acc[i][j][r] + b;
-      }
-  }
-#pragma unroll
-  for (int j = 0; j < NI; ++j) {
-    const int n = n0 + wn * NI * 32 + j * 32 + lr;
-    if (n >= P.N) continue;
-    const float cb = *(col_bias ? ep.bias + n : g_zero4);
-    float* cj;
-    if (OM == OUT_NCHW) {
-      const uint32_t im = fdiv(static_cast<uint32_t>(n), ep.hw);
-      const uint32_t sp = static_cast<uint32_t>(n) - im * ep.hw.d;
-      cj = ep.C + (int64_t)im * ep.cimg + sp;
-    } else {
-      cj = ep.C + n;
-    }
-    const int64_t ld = ep.ldc;
-    if (beta != 0.0f) {
-      // accumulate into C (backward GEMMs): ((alpha*v) + beta*C) + bias
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = mw + i * 32 + (r & 3) + 8 * (r >> 2);
-          if (!rows_full && m >= P.M) continue;
-          float* dst = cj + (int64_t)m * ld;
-          float o = alpha * acc[i][j][r] + beta * *dst;
-          o += *(row_bias ? ep.bias + m : g_zero4) + cb;
-          *dst = relu ? fmaxf(o, 0.0f) : o;
-        }
-    } else if (rows_full) {
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = mw + i * 32 + (r & 3) + 8 * (r >> 2);
-          const float o = acc[i][j][r] + cb;
-          cj[(int64_t)m * ld] = relu ? fmaxf(o, 0.0f) : o;
-        }
-    } else {
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = mw + i * 32 + (r & 3) + 8 * (r >> 2);
-          const float o = acc[i][j][r] + cb;
-          if (m < P.M) cj[(int64_t)m * ld] = relu ? fmaxf(o, 0.0f) : o;
-        }
-    }
-  }
+  gemm_epilogue<MI, NI, OM>(acc, P, ep, part, m0 + wm * MI * 32, n0 + wn * NI * 32, lr, lh);
 #endif
+}
+
+// ---------------------------------------------------------------------------
+// k_gemm2: the same contraction at one 128 x 128 tile per 4-wave workgroup and
+// ONE wave per SIMD (3-stage LDS ring, ~97 KB: one workgroup per CU), for the
+// 16-byte operands (A = KCV; B = KCV or the CONVT gather).  What it changes
+// against k_gemm (hipBLASLt's fp32 kernels run the same regime: 1 WG/CU,
+// 128x128, K-tiles of 64, pipelined loads; 128-133 TFLOP/s on this box):
+//   * 32-deep K-tiles loaded as whole 128-byte row pieces (k_gemm's 16-deep
+//     tiles fetch every row line in two halves, in two K-tiles);
+//   * LDS-DMA (buffer_load ... lds): no staging VGPRs, no ds_write pass; an
+//     out-of-range offset (rows past M/N, k past the chunk, padding taps) lands
+//     zeros;
+//   * tiles are issued NST-1 ahead and only the oldest is waited for (counted
+//     vmcnt + raw s_barrier: __syncthreads() would drain the ring);
+//   * one barrier per K-tile, in the middle of it: the fragments of the next
+//     tile's first half are read while the second half's MFMAs run.
+// Stage images (one __shared__ array):
+//   A      [128 rows][32 k], 16-byte quad q of row r at quad position q ^ ((r>>1)&7)
+//          (conflict-free ds_read_b128 for 16 consecutive rows; the swizzle is
+//          applied on the global source address, the DMA destination stays
+//          lane-linear);
+//   B KCV  the same image;
+//   B CONVT [32 k][130]: column n at n, rows padded so the two lane halves
+//          (k and k + 16) read disjoint bank halves with ds_read_b32.
+// K order inside a tile: lane half h at step s uses k = 16 h + s (A and B).
+namespace g2 {
+constexpr int BM = 128, BN = 128, KT = 32, LDN = 130;
+constexpr int A_FL = BM * KT;
+template <int BMODE>
+constexpr int b_fl() { return BMODE == CONVT ? KT * LDN : BN * KT; }
+template <int BMODE>
+constexpr int stage_fl() { return A_FL + b_fl<BMODE>(); }
+// LDS-DMA instructions one wave issues per K-tile: A 4 pieces of 1 KB; B 4 more
+// (KCV) or 16 gathered rows of 64 columns x 4 B (CONVT)
+template <int BMODE>
+constexpr int vm_per_tile() { return 4 + (BMODE == CONVT ? 16 : 4); }
+
+typedef int int4v __attribute__((ext_vector_type(4)));
+
+// Raw buffer descriptor as four SGPR words (base, stride 0, byte range, raw
+// untyped dword format): offsets at or past the range load zeros.
+__device__ __forceinline__ int4v make_rsrc(const float* p, uint32_t range) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  int4v r;
+  r.x = static_cast<int>(static_cast<uint32_t>(a));
+  r.y = static_cast<int>(static_cast<uint32_t>(a >> 32) & 0xFFFFu);
+  r.z = static_cast<int>(range);
+  r.w = 0x00020000;
+  return r;
+}
+// LDS-DMA loads (buffer_load ... lds) in inline asm: the compiler then neither
+// drains the ring with vmcnt(0) before every ds_read (it cannot tell the DMA
+// destination from the stage being read) nor demotes the uniform table loads
+// to vector loads.  Their completion is tracked by hand (wait_vm + barrier).
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void dma_b128(const int4v& rs, uint32_t voff, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs), "s"(lds)
+               : "m0");
+}
+__device__ __forceinline__ void dma_b32(const int4v& rs, uint32_t voff, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dword %0, %1, 0 offen lds" ::"v"(voff), "s"(rs), "s"(lds)
+               : "m0");
+}
+#pragma clang diagnostic pop
+
+// Loader of a K-contiguous operand (rows x k): this lane's byte offset of row
+// r = 32 w + 8 i + (lane >> 3) for piece i (bit 31 set when the row is out of
+// range) and the k offset (floats) of the quad it fetches.
+struct RowLd {
+  int4v rsrc;
+  uint32_t rb[4];
+  int kq[4];
+};
+__device__ __forceinline__ RowLd make_rowld(const View& vw, int row0, int wave, int lane) {
+  RowLd L;
+  L.rsrc = make_rsrc(vw.p, static_cast<uint32_t>(((int64_t)(vw.rows - 1) * vw.ld + vw.kdim) * 4));
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = 32 * wave + 8 * i + (lane >> 3);
+    const int q = (lane & 7) ^ ((r >> 1) & 7);
+    const bool ok = row0 + r < vw.rows;
+    L.rb[i] = ok ? static_cast<uint32_t>((int64_t)(row0 + r) * vw.ld * 4) : 0x80000000u;
+    L.kq[i] = 4 * q;
+  }
+  return L;
+}
+// piece i of the tile at k0 into the image at LDS byte address img
+__device__ __forceinline__ void issue_row_piece(const RowLd& L, uint32_t img, int wave, int i, int k0, int kend) {
+  const int k = k0 + L.kq[i];
+  const uint32_t off = (L.rb[i] + static_cast<uint32_t>(k) * 4u) | (k < kend ? 0u : 0x80000000u);
+  dma_b128(L.rsrc, off, img + static_cast<uint32_t>((32 * wave + 8 * i) * KT * 4));
+}
+
+// Gather loader (CONVT): this lane's two columns n0 + 64 h + lane.
+struct ColLd {
+  int4v rsrc;
+  uint32_t pb4[2];  // byte offset of the column's (image, ho*sh - ph, wo*sw - pw) input corner
+  uint32_t bad[2];  // bit t: tap t reads padding (bit 31 always set; all set past N)
+};
+__device__ __forceinline__ ColLd make_colld(const Params& P, const float* base, int n0, int lane) {
+  ColLd C;
+  C.rsrc = make_rsrc(base, static_cast<uint32_t>(P.cv.in_bytes));
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int p = n0 + 64 * h + lane;
+    C.pb4[h] = 0;
+    C.bad[h] = 0xFFFFFFFFu;
+    if (p < P.N) {
+      const uint32_t im = fdiv(static_cast<uint32_t>(p), P.cv.howo);
+      const uint32_t sp = static_cast<uint32_t>(p) - im * P.cv.howo.d;
+      const uint32_t ho = fdiv(sp, P.cv.wo_div);
+      const uint32_t wo = sp - ho * P.cv.wo_div.d;
+      const int hb = static_cast<int>(ho) * P.cv.sh - P.cv.ph;
+      const int wb = static_cast<int>(wo) * P.cv.sw - P.cv.pw;
+      C.pb4[h] = static_cast<uint32_t>(static_cast<int>(im * P.cv.chw) + hb * P.cv.W + wb) * 4u;
+      uint32_t good = 1u;  // pad-free: every tap is inside the image
+      if (P.cv.taps > 0) {
+        good = 0;
+        for (int t = 0; t < P.cv.taps; ++t) {
+          const int kh = t / P.cv.KW, kw = t - kh * P.cv.KW;
+          good |= static_cast<uint32_t>(static_cast<unsigned>(hb + kh * P.cv.dh) < static_cast<unsigned>(P.cv.H) &&
+                                        static_cast<unsigned>(wb + kw * P.cv.dw) < static_cast<unsigned>(P.cv.W))
+                  << t;
+        }
+      }
+      C.bad[h] = ~good | 0x80000000u;
+    }
+  }
+  return C;
+}
+// k-row 8 w + kk of the tile, 64-column half h (table entry t, wave-uniform)
+__device__ __forceinline__ void issue_col_row(const ColLd& C, int2 t, uint32_t img, int wave, int kk, int h) {
+  const uint32_t bad = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(C.bad[h]), t.y & 31, 1));
+  dma_b32(C.rsrc, (C.pb4[h] + static_cast<uint32_t>(t.x)) | bad,
+          img + static_cast<uint32_t>(((8 * wave + kk) * LDN + 64 * h) * 4));
+}
+
+// the wave's 8 gather-table entries of a K-tile, as one scalar load into
+// SGPRs (inline asm: the memory-clobbering waits below would otherwise turn
+// the uniform loads into vector loads); completed by the next lgkmcnt(0)
+typedef int int16v __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ int16v sload_table(const int2* p) {
+  int16v r;
+  asm volatile("s_load_dwordx16 %0, %1, 0x0" : "=s"(r) : "s"(p));
+  return r;
+}
+__device__ __forceinline__ int2 tentry(const int16v& v, int kk) {
+  return make_int2(v[2 * kk], v[2 * kk + 1]);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 20) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else static_assert(N < 0, "add this vmcnt");
+}
+
+// fragments of one K-half (8 k-steps) of a wave's 64 x 64 tile
+template <int BMODE>
+struct Frag {
+  float4 a[2][2];
+  float4 b[2][2];   // KCV
+  float bc[2][8];   // CONVT
+};
+// fragment read item e of a K-half: A quads (4), then B quads (4, KCV) or
+// B k-rows (16, CONVT, two per step)
+template <int BMODE>
+constexpr int frag_items() { return BMODE == CONVT ? 20 : 8; }
+template <int BMODE>
+__device__ __forceinline__ void read_item(Frag<BMODE>& F, const float* As, const float* Bs, int wm, int wn, int lr,
+                                          int lh, int hf, int e) {
+  if (e < 4) {
+    const int i = e >> 1, u = e & 1;
+    const int m = wm * 64 + i * 32 + lr;
+    F.a[i][u] = *reinterpret_cast<const float4*>(As + m * KT + (((4 * lh + 2 * hf + u) ^ ((m >> 1) & 7)) << 2));
+  } else if constexpr (BMODE == CONVT) {
+    const int j = (e - 4) >> 3, sx = (e - 4) & 7;
+    F.bc[j][sx] = Bs[(16 * lh + 8 * hf + sx) * LDN + wn * 64 + j * 32 + lr];
+  } else {
+    const int j = (e - 4) >> 1, u = (e - 4) & 1;
+    const int n = wn * 64 + j * 32 + lr;
+    F.b[j][u] = *reinterpret_cast<const float4*>(Bs + n * KT + (((4 * lh + 2 * hf + u) ^ ((n >> 1) & 7)) << 2));
+  }
+}
+// MFMA pair p (0..15) of a K-half: step p >> 1, row tile p & 1, both column tiles
+template <int BMODE>
+__device__ __forceinline__ void mfma_pair(floatx16 (&acc)[2][2], const Frag<BMODE>& F, int p) {
+  const int sx = p >> 1, i = p & 1;
+  const float a = pick(F.a[i][sx >> 2], sx);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const float b = BMODE == CONVT ? F.bc[j][sx] : pick(F.b[j][sx >> 2], sx);
+    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[i][j], 0, 0, 0);
+  }
+}
+}  // namespace g2
+
+template <int AM, int BMODE, int OM, int NST>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) k_gemm2(Params P) {
+  using namespace g2;
+  static_assert(AM == KCV && (BMODE == KCV || BMODE == CONVT), "k_gemm2 operand modes");
+  static_assert(NST == 2 || NST == 3, "stages");
+  constexpr int SF = stage_fl<BMODE>();
+  constexpr int NVM = vm_per_tile<BMODE>();
+  constexpr int NFR = frag_items<BMODE>();
+  __shared__ __attribute__((aligned(16))) float smem[NST * SF];
+  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)smem));
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int lr = lane & 31, lh = lane >> 5;
+
+  // XCD-aware tile order, as k_gemm
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, loc = bid >> 3;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int tid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const int tm = __builtin_amdgcn_readfirstlane(tid % P.tiles_m);
+  const int tn = __builtin_amdgcn_readfirstlane((tid / P.tiles_m) % P.tiles_n);
+  const int z = __builtin_amdgcn_readfirstlane(tid / (P.tiles_m * P.tiles_n));
+  const int n0 = tn * BN;
+  const int m0 = tm * BM;
+
+  View va = P.a, vb = P.b;
+  Epi ep = P.e;
+  int kbeg = 0, kend = P.K;
+  float* part = nullptr;
+  if (P.split > 1) {
+    kbeg = z * P.k_chunk;
+    kend = min(P.K, kbeg + P.k_chunk);
+    part = P.ws + (int64_t)z * P.M * P.N;
+  } else if (z > 0) {  // conv group
+    va.p += z * P.grp_a;
+    vb.p += z * P.grp_b;
+    ep.C += z * P.grp_c;
+    if (ep.bias) ep.bias += z * P.grp_bias;
+  }
+
+  const RowLd la = make_rowld(va, m0, wave, lane);
+  RowLd lb;
+  ColLd lc;
+  if constexpr (BMODE == CONVT) lc = make_colld(P, vb.p, n0, lane);
+  else lb = make_rowld(vb, n0, wave, lane);
+
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+  const int nt = (kend - kbeg + KT - 1) / KT;
+  // load item e (0 .. NVM-1) of K-tile at k0 into the stage at LDS address img;
+  // te: the tile's gather-table entries for k-rows 8 w .. 8 w + 7 (SGPRs)
+  auto item = [&](int e, uint32_t img, int k0, const int16v& te) {
+    if (e < 4) {
+      issue_row_piece(la, img, wave, e, k0, kend);
+    } else if constexpr (BMODE == CONVT) {
+      issue_col_row(lc, tentry(te, (e - 4) >> 1), img + A_FL * 4, wave, (e - 4) >> 1, (e - 4) & 1);
+    } else {
+      issue_row_piece(lb, img + A_FL * 4, wave, e - 4, k0, kend);
+    }
+  };
+  auto table = [&](int k0) {
+    int16v v{};
+    if constexpr (BMODE == CONVT) v = sload_table(P.cv.tbl + k0 + 8 * wave);
+    return v;
+  };
+
+  Frag<BMODE> f1, f2;
+  int16v tnext{};  // table entries of the tile the next phase A issues
+  if (nt > 0) {
+    {
+      const int16v te = table(kbeg);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int e = 0; e < NVM; ++e) item(e, lds0, kbeg, te);
+    }
+    if (NST == 3 && nt > 1) {
+      const int16v te = table(kbeg + KT);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int e = 0; e < NVM; ++e) item(e, lds0 + SF * 4, kbeg + KT, te);
+    }
+    if (NST - 1 < nt) tnext = table(kbeg + (NST - 1) * KT);
+    if (NST == 3 && nt > 1) wait_vm<NVM>();
+    else wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int e = 0; e < NFR; ++e) read_item<BMODE>(f1, smem, smem + A_FL, wm, wn, lr, lh, 0, e);
+  }
+  int st = 0;                 // stage of tile t
+  int sn = NST == 3 ? 2 : 1;  // stage the next issued tile goes to
+  // One K-tile.  LOADS: issue tile t + NST - 1 (phase A); NEXT: tile t + 1
+  // exists (phase B waits for it, with WAITN younger tiles still in flight).
+  auto step = [&](int t, auto loads_c, auto next_c, auto waitn_c) {
+    constexpr bool LOADS = decltype(loads_c)::value;
+    constexpr bool NEXT = decltype(next_c)::value;
+    constexpr int WAITN = decltype(waitn_c)::value;
+    const float* As = smem + st * SF;
+    // phase A: first-half MFMAs of tile t (16 slots of one MFMA pair), the
+    // DMA items of tile t + NST - 1 spread over them, and from slot 8 on the
+    // second-half fragment reads
+    const int kn = kbeg + (t + NST - 1) * KT;
+    const uint32_t img = lds0 + static_cast<uint32_t>(sn * SF * 4);
+    const int16v te = tnext;
+#pragma unroll
+    for (int p = 0; p < 16; ++p) {
+      mfma_pair<BMODE>(acc, f1, p);
+      if constexpr (LOADS) {
+#pragma unroll
+        for (int e = (p * NVM + 15) / 16; e < ((p + 1) * NVM + 15) / 16; ++e) item(e, img, kn, te);
+      }
+      if (p >= 8) {
+#pragma unroll
+        for (int e = (p - 8) * NFR / 8; e < (p - 7) * NFR / 8; ++e)
+          read_item<BMODE>(f2, As, As + A_FL, wm, wn, lr, lh, 1, e);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // phase B: the next tile is complete and visible; its first half is read
+    // while this tile's second half runs
+    const int st1 = st + 1 == NST ? 0 : st + 1;
+    if constexpr (NEXT) {
+      if (LOADS && t + NST < nt) tnext = table(kbeg + (t + NST) * KT);
+      wait_vm<WAITN>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      const float* An = smem + st1 * SF;
+#pragma unroll
+      for (int p = 0; p < 16; ++p) {
+#pragma unroll
+        for (int e = p * NFR / 16; e < (p + 1) * NFR / 16; ++e)
+          read_item<BMODE>(f1, An, An + A_FL, wm, wn, lr, lh, 0, e);
+        mfma_pair<BMODE>(acc, f2, p);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < 16; ++p) mfma_pair<BMODE>(acc, f2, p);
+    }
+    st = st1;
+    sn = sn + 1 == NST ? 0 : sn + 1;
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  // steady state: every tile issues the one NST - 1 ahead
+  int t = 0;
+  for (; t + NST - 1 < nt; ++t) step(t, T_{}, T_{}, std::integral_constant<int, NST == 3 ? NVM : 0>{});
+  // drain: no more loads; the last tile has no successor
+  if (NST == 3 && t + 1 < nt) {
+    step(t, F_{}, T_{}, std::integral_constant<int, 0>{});
+    ++t;
+  }
+  if (t < nt) step(t, F_{}, F_{}, std::integral_constant<int, 0>{});
+  gemm_epilogue<2, 2, OM>(acc, P, ep, part, m0 + wm * 64, n0 + wn * 64, lr, lh);
 }
 
 // split-K reduction + epilogue (row-major C only)
@@ -931,6 +1304,49 @@ int launch(const Params& P, int gz, hipStream_t s, bool force_big) {
   }
 }
 
+template <int AM, int BMODE, int OM>
+int launch2(Params P, int gz, hipStream_t s, int nst) {
+  P.tiles_m = (P.M + g2::BM - 1) / g2::BM;
+  P.tiles_n = (P.N + g2::BN - 1) / g2::BN;
+  P.tiles_z = gz;
+  const int64_t nwg = (int64_t)P.tiles_m * P.tiles_n * gz;
+  RRAM_REQUIRE(nwg < (1ll << 31), "gemm: grid too large");
+  if (nst == 2)
+    hipLaunchKernelGGL((k_gemm2<AM, BMODE, OM, 2>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, P);
+  else
+    hipLaunchKernelGGL((k_gemm2<AM, BMODE, OM, 3>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, P);
+  return launch_status("gemm2");
+}
+
+// k_gemm2 policy (tuning knob RRAM_GEMM_V2 = 0 off | 2 | 3 LDS stages, default 3):
+// 16-byte A and B (the IP layers), M padded by at most 1/8 in 128-row tiles,
+// N > 64, and operands addressable with 32-bit buffer offsets.  MI355X,
+// AlexNet b256 (scripts/gpu_g2.sh, kbench): fc6 111 -> 119 TFLOP/s, fc7 100 ->
+// 109.  The table-gather convolutions stay on k_gemm: at one wave per SIMD the
+// gather's 16 four-byte LDS-DMA issues per wave and K-tile cap it at 68 % MFMA
+// busy (conv3 109 -> 100 TFLOP/s; RRAM_GEMM_V2_CONV=1 selects it for A/B runs).
+int gemm2_stages() {
+  static const int v = [] {
+    const char* e = getenv("RRAM_GEMM_V2");
+    const int x = e ? atoi(e) : 3;
+    return x == 0 || x == 2 || x == 3 ? x : 3;
+  }();
+  return v;
+}
+bool gemm2_ok(int am, int bm, const Params& P) {
+  static const bool conv = [] {
+    const char* e = getenv("RRAM_GEMM_V2_CONV");
+    return e && atoi(e) == 1;
+  }();
+  if (gemm2_stages() == 0 || am != KCV || (bm != KCV && !(conv && bm == CONVT))) return false;
+  const int64_t mt = (P.M + g2::BM - 1) / g2::BM * g2::BM;
+  if (P.N <= 64 || (mt - P.M) * 8 > mt) return false;
+  auto fits = [](const View& v) { return ((int64_t)(v.rows - 1) * v.ld + v.kdim) * 4 < (1ll << 31); };
+  if (!fits(P.a)) return false;
+  if (bm == KCV && !fits(P.b)) return false;
+  return true;
+}
+
 // K-tile depth of the implicit-GEMM convolution (tuning knob RRAM_GEMM_KB = 16 | 32)
 // Measured on MI355X (scripts/gpu_sweep.sh, AlexNet b256): K >= 1024 runs
 // faster with 16-deep K-tiles (half the LDS and loader registers: 3 waves per
@@ -945,6 +1361,11 @@ int conv_kb(int K) {
 }
 
 int dispatch(int am, int bm, int om, const Params& P, int gz, hipStream_t s, bool force_big = false) {
+  if (gemm2_ok(am, bm, P)) {
+    const int nst = gemm2_stages();
+    if (bm == CONVT && om == OUT_NCHW) return launch2<KCV, CONVT, OUT_NCHW>(P, gz, s, nst);
+    if (bm == KCV && om == OUT_ROWMAJOR) return launch2<KCV, KCV, OUT_ROWMAJOR>(P, gz, s, nst);
+  }
   if (bm == CONV && om == OUT_NCHW && conv_kb(P.K) == 16) {
     if (am == KC) return launch<KC, CONV, OUT_NCHW, 16>(P, gz, s, force_big);
     if (am == KCV) return launch<KCV, CONV, OUT_NCHW, 16>(P, gz, s, force_big);

@@ -105,6 +105,38 @@ def main():
             t = timeit(lambda: ops.gemm(0, 1, M, N, K, 1.0, A, Bm, 0.0, Cm), iters=5)
             res[f"{name}_TFs"] = 2.0 * M * N * K / t / 1e12
             res[f"{name}_ms"] = t * 1e3
+    if a.only == "vendor":
+        # the vendor libraries on the same box, for reference only (never on the product
+        # path): torch.mm = hipBLASLt / rocBLAS sgemm, F.conv2d = MIOpen, all fp32
+        torch.backends.cuda.matmul.allow_tf32 = False
+        torch.backends.cudnn.allow_tf32 = False
+        for name, M, N, K in (("sq4096", 4096, 4096, 4096), ("dense_conv3", 384, 43264, 2304),
+                              ("dense_conv2g", 128, 186624, 1200), ("fc6", 256, 4096, 9216),
+                              ("fc7", 256, 4096, 4096), ("fc8", 256, 1000, 4096)):
+            A = torch.randn(M, K, device=dev)
+            Bm = torch.randn(N, K, device=dev)
+            t = timeit(lambda: torch.mm(A, Bm.t()), iters=5)
+            res[f"vendor_mm_{name}_TFs"] = 2.0 * M * N * K / t / 1e12
+        import torch.nn.functional as F
+        B = 256
+        tot_f = tot_t = 0.0
+        for name, xs, co, k, s, p, g in (("conv1", (B, 3, 227, 227), 96, 11, 4, 0, 1),
+                                         ("conv2", (B, 96, 27, 27), 256, 5, 1, 2, 2),
+                                         ("conv3", (B, 256, 13, 13), 384, 3, 1, 1, 1),
+                                         ("conv4", (B, 384, 13, 13), 384, 3, 1, 1, 2),
+                                         ("conv5", (B, 384, 13, 13), 256, 3, 1, 1, 2)):
+            x = torch.randn(xs, device=dev)
+            w = torch.randn(co, xs[1] // g, k, k, device=dev) * 0.01
+            b = torch.randn(co, device=dev)
+            y = F.conv2d(x, w, b, stride=s, padding=p, groups=g)
+            t = timeit(lambda: F.conv2d(x, w, b, stride=s, padding=p, groups=g), iters=5)
+            fl = 2.0 * B * co * y.shape[2] * y.shape[3] * (xs[1] // g) * k * k
+            res[f"vendor_conv_{name}_TFs"] = fl / t / 1e12
+            res[f"vendor_conv_{name}_ms"] = t * 1e3
+            tot_f += fl
+            tot_t += t
+        res["vendor_conv_total_ms"] = tot_t * 1e3
+        res["vendor_conv_TFs"] = tot_f / tot_t / 1e12
     if a.only in ("", "gemm"):
         B = 256
         convs = [("conv1", (B, 3, 227, 227), 96, 11, 4, 0, 1), ("conv2", (B, 96, 27, 27), 256, 5, 1, 2, 2),

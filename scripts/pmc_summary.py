@@ -12,9 +12,9 @@ dur = defaultdict(list)
 for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
-        m = re.search(r"k_gemm<([^>]*)>", name) or re.search(r"k_gemmILi(\d)ELi(\d)ELi(\d)ELi(\d)ELi(\d)ELi(\d)ELi(\d)", name)
+        m = re.search(r"k_gemm(2?)<([^>]*)>", name)
         if m:
-            short = "gemm<" + (m.group(1).replace(" ", "") if m.lastindex == 1 else ",".join(m.groups())) + ">"
+            short = f"gemm{m.group(1)}<" + m.group(2).replace(" ", "") + ">"
         else:
             short = re.sub(r"\(anonymous namespace\)::", "", name)
             short = re.sub(r"\(.*", "", short).replace("void ", "").split("::")[-1][:40]
