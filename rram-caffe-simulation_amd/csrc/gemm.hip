@@ -906,12 +906,12 @@ __device__ __forceinline__ int2 tentry(const int16v& v, int kk) {
   return make_int2(v[2 * kk], v[2 * kk + 1]);
 }
 
+// wait until at most N of this wave's vector-memory operations (LDS-DMA
+// included) are outstanding
 template <int N>
 __device__ __forceinline__ void wait_vm() {
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N == 20) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
-  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else static_assert(N < 0, "add this vmcnt");
+  static_assert(N >= 0 && N <= 63, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 // fragments of one K-half (8 k-steps) of a wave's 64 x 64 tile
@@ -1118,6 +1118,287 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
   }
   if (t < nt) step(t, F_{}, F_{}, std::integral_constant<int, 0>{});
   gemm_epilogue<2, 2, OM>(acc, P, ep, part, m0 + wm * 64, n0 + wn * 64, lr, lh);
+}
+
+// ---------------------------------------------------------------------------
+// k_conv_patch: stride-1 convolution with the input staged in LDS as a
+// padded patch instead of an im2col gather.  A 128-position tile of one or two
+// images needs only the input rows those positions touch (+ KH - 1), so per
+// K-tile (2 CPH input channels) it loads ~2 CPH x rows x (W + 2 pw) floats
+// where the table gather loads 128 x 2 CPH x KH x KW (5-10x fewer, and in
+// whole rows).  The weights are repacked once per call into K-tile slabs
+// ([group][m-tile][k-tile][64 MI rows][RL]: the 2 CPH x KH x KW taps of the
+// K-tile split in two lane halves of HP floats, padded) so their tile is one
+// linear LDS-DMA copy.  Structure as k_gemm2: one 4-wave workgroup per CU,
+// 3-stage ring, one barrier in the middle of each K-tile.
+// K order: lane half h at step s = (cc, kh, kw) uses input channel
+// kt*2CPH + h*CPH + cc and tap (kh, kw), in A and B alike.
+namespace cp {
+constexpr int BN = 128, NST = 3;
+template <int KH, int KW, int CPH>
+struct Shape {
+  static constexpr int T = KH * KW;
+  static constexpr int S = CPH * T;                              // MFMA steps per K-tile
+  static constexpr int S1 = (S / 2) / 4 * 4;                     // steps of the first half
+  static constexpr int HP = (S + 3) / 4 * 4;                     // packed half (floats)
+  static constexpr int RL = ((2 * HP / 4) % 2 == 0) ? 2 * HP + 4 : 2 * HP;  // row: RL/4 odd = conflict-free b128
+  static constexpr int Q0 = 0, Q1 = S1 / 4, QE = (S + 3) / 4;   // A quads of the halves
+};
+// per-tile patch geometry (uniform)
+struct PatchGeo {
+  int img0, a0, rows0, img1;  // segment 0: image, first output row, patch rows; segment 1 starts at row 0
+};
+}  // namespace cp
+
+template <int KH, int KW, int CPH, int MI, int PD, int NST>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NST == 2 ? 2 : 1, NST == 2 ? 2 : 1)))
+k_conv_patch(Params P, const float* __restrict__ wpack, int PW, int CS) {
+  using namespace g2;
+  using Sh = cp::Shape<KH, KW, CPH>;
+  constexpr int BMc = 64 * MI;
+  constexpr int A_FL = BMc * Sh::RL;
+  constexpr int A_DMA = ((A_FL + 255) / 256 + 3) / 4;   // x4 pieces per wave
+  constexpr int A_REG = A_DMA * 4 * 256;                // floats reserved for A in a stage
+  constexpr int P_REG = PD * 4 * 64;                    // patch floats per stage (PD dword pieces per wave)
+  constexpr int SF = A_REG + P_REG;
+  constexpr int NVM = A_DMA + PD;
+  static_assert(NST == 2 || NST == 3, "stages");
+  static_assert(NST * SF * 4 <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) float smem[NST * SF];
+  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)smem));
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int lr = lane & 31, lh = lane >> 5;
+
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, loc = bid >> 3;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int tid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const int tm = __builtin_amdgcn_readfirstlane(tid % P.tiles_m);
+  const int tn = __builtin_amdgcn_readfirstlane((tid / P.tiles_m) % P.tiles_n);
+  const int z = __builtin_amdgcn_readfirstlane(tid / (P.tiles_m * P.tiles_n));
+  const int n0 = tn * cp::BN;
+  const int m0 = tm * BMc;
+
+  const ConvGeom& cv = P.cv;
+  const int HW = cv.howo.d, OW = cv.wo_div.d;
+  const int ktiles = cv.C / (2 * CPH);
+  const float* xin = P.b.p + z * P.grp_b;
+  Epi ep = P.e;
+  if (z > 0) {
+    ep.C += z * P.grp_c;
+    if (ep.bias) ep.bias += z * P.grp_bias;
+  }
+  // A: this tile's packed slabs, one per K-tile, each A_FL floats
+  const float* abase = wpack + ((int64_t)z * P.tiles_m + tm) * ktiles * A_FL;
+  const int4v arsrc = make_rsrc(abase, static_cast<uint32_t>((int64_t)ktiles * A_FL * 4));
+  uint32_t aoff[A_DMA];
+#pragma unroll
+  for (int i = 0; i < A_DMA; ++i) {
+    const int f = (wave * A_DMA + i) * 256 + lane * 4;
+    aoff[i] = f < A_FL ? static_cast<uint32_t>(f * 4) : 0x80000000u;
+  }
+
+  // patch geometry of this tile (positions n0 .. n0 + 127, at most two images)
+  const int plast = min(n0 + cp::BN, P.N) - 1;
+  const int img0 = n0 / HW, img1 = plast / HW;
+  const int a0 = (n0 - img0 * HW) / OW;
+  const int b0 = img1 == img0 ? (plast - img0 * HW) / OW : cv.Ho - 1;
+  const int rows0 = b0 - a0 + KH;
+  const int rows1 = img1 == img0 ? 0 : (plast - img1 * HW) / OW + KH;
+  const int R = rows0 + rows1;
+  // per-lane source of the patch pieces: patch float f = (ch, prow, pcol)
+  const int4v xrsrc = make_rsrc(xin, static_cast<uint32_t>(cv.in_bytes));
+  const uint32_t HW4 = static_cast<uint32_t>(cv.H * cv.W * 4);
+  uint32_t poff[PD];
+#pragma unroll
+  for (int i = 0; i < PD; ++i) {
+    const int f = (wave * PD + i) * 64 + lane;
+    const int ch = f / CS, w = f - ch * CS;
+    const int prow = w / PW, pcol = w - prow * PW;
+    uint32_t off = 0x80000000u;
+    if (ch < 2 * CPH && prow < R) {
+      const bool s1 = prow >= rows0;
+      const int img = s1 ? img1 : img0;
+      const int y = (s1 ? prow - rows0 : a0 + prow) - cv.ph;
+      const int x = pcol - cv.pw;
+      if (y >= 0 && y < cv.H && x >= 0 && x < cv.W)
+        off = static_cast<uint32_t>((int64_t)img * cv.chw * 4) + static_cast<uint32_t>(ch) * HW4 +
+              static_cast<uint32_t>((y * cv.W + x) * 4);
+    }
+    poff[i] = off;
+  }
+  // per-lane B fragment base (floats) of columns j = 0, 1 inside the patch
+  int pb[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = min(n0 + wn * 64 + j * 32 + lr, plast);
+    const int img = n / HW, sp = n - img * HW;
+    const int oh = sp / OW, ow = sp - oh * OW;
+    const int prow = img == img0 ? oh - a0 : rows0 + oh;
+    pb[j] = prow * PW + ow + lh * CPH * CS;
+  }
+
+  floatx16 acc[MI][2];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+  auto issue = [&](int kt, int stg, int e) {  // DMA item e of K-tile kt into stage stg
+    const uint32_t img = lds0 + static_cast<uint32_t>(stg * SF * 4);
+    if (e < A_DMA) {
+      dma_b128(arsrc, aoff[e] + static_cast<uint32_t>(kt * A_FL * 4),
+               img + static_cast<uint32_t>((wave * A_DMA + e) * 1024));
+    } else {
+      const int i = e - A_DMA;
+      dma_b32(xrsrc, poff[i] + static_cast<uint32_t>(kt * 2 * CPH) * HW4,
+              img + static_cast<uint32_t>((A_REG + (wave * PD + i) * 64) * 4));
+    }
+  };
+  // fragments: A quads [q0, q1) and B steps [s0, s1) of one half
+  constexpr int QA = Sh::QE - Sh::Q1 > Sh::Q1 ? Sh::QE - Sh::Q1 : Sh::Q1;
+  constexpr int SB = Sh::S - Sh::S1 > Sh::S1 ? Sh::S - Sh::S1 : Sh::S1;
+  struct Fr {
+    float4 a[MI][QA];
+    float b[2][SB];
+  };
+  auto read_a = [&](Fr& F, const float* st, int q, int qb) {  // quad q into slot q - qb
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int m = wm * 32 * MI + i * 32 + lr;
+      F.a[i][q - qb] = *reinterpret_cast<const float4*>(st + m * Sh::RL + lh * Sh::HP + 4 * q);
+    }
+  };
+  auto read_b = [&](Fr& F, const float* st, int sx, int sb) {  // step sx into slot sx - sb
+    const int cc = sx / Sh::T, tp = sx - cc * Sh::T, kh = tp / KW, kw = tp - kh * KW;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) F.b[j][sx - sb] = st[A_REG + pb[j] + cc * CS + kh * PW + kw];
+  };
+  auto mfma_step = [&](const Fr& F, int sx, int qb, int sb) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const float a = pick(F.a[i][(sx >> 2) - qb], sx);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, F.b[j][sx - sb], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  Fr f1, f2;
+  const int nt = ktiles;
+  if (nt > 0) {
+#pragma unroll
+    for (int e = 0; e < NVM; ++e) issue(0, 0, e);
+    if (NST == 3 && nt > 1) {
+#pragma unroll
+      for (int e = 0; e < NVM; ++e) issue(1, 1, e);
+      wait_vm<NVM>();
+    } else {
+      wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int q = Sh::Q0; q < Sh::Q1; ++q) read_a(f1, smem, q, Sh::Q0);
+#pragma unroll
+    for (int sx = 0; sx < Sh::S1; ++sx) read_b(f1, smem, sx, 0);
+  }
+  int st = 0, sn = NST - 1;
+  auto step = [&](int t, auto loads_c, auto next_c, auto waitn_c) {
+    constexpr bool LOADS = decltype(loads_c)::value;
+    constexpr bool NEXT = decltype(next_c)::value;
+    constexpr int WAITN = decltype(waitn_c)::value;
+    const float* cur = smem + st * SF;
+    // phase A: first-half MFMAs, DMA of tile t + 2, second-half reads
+#pragma unroll
+    for (int sx = 0; sx < Sh::S1; ++sx) {
+      mfma_step(f1, sx, Sh::Q0, 0);
+      if constexpr (LOADS) {
+#pragma unroll
+        for (int e = (sx * NVM + Sh::S1 - 1) / Sh::S1; e < ((sx + 1) * NVM + Sh::S1 - 1) / Sh::S1; ++e)
+          issue(t + NST - 1, sn, e);
+      }
+      if (sx == Sh::S1 / 2) {
+#pragma unroll
+        for (int q = Sh::Q1; q < Sh::QE; ++q) read_a(f2, cur, q, Sh::Q1);
+      }
+      if (sx >= Sh::S1 / 2) {
+#pragma unroll
+        for (int u = Sh::S1 + (sx - Sh::S1 / 2) * (Sh::S - Sh::S1) / (Sh::S1 - Sh::S1 / 2);
+             u < Sh::S1 + (sx + 1 - Sh::S1 / 2) * (Sh::S - Sh::S1) / (Sh::S1 - Sh::S1 / 2); ++u)
+          read_b(f2, cur, u, Sh::S1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const int st1 = st + 1 == NST ? 0 : st + 1;
+    if constexpr (NEXT) {
+      wait_vm<WAITN>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      const float* nx = smem + st1 * SF;
+      constexpr int S2 = Sh::S - Sh::S1;
+#pragma unroll
+      for (int sx = Sh::S1; sx < Sh::S; ++sx) {
+        const int v = sx - Sh::S1;
+        if (v == 0) {
+#pragma unroll
+          for (int q = Sh::Q0; q < Sh::Q1; ++q) read_a(f1, nx, q, Sh::Q0);
+        }
+#pragma unroll
+        for (int u = v * Sh::S1 / S2; u < (v + 1) * Sh::S1 / S2; ++u) read_b(f1, nx, u, 0);
+        mfma_step(f2, sx, Sh::Q1, Sh::S1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+#pragma unroll
+      for (int sx = Sh::S1; sx < Sh::S; ++sx) mfma_step(f2, sx, Sh::Q1, Sh::S1);
+    }
+    st = st1;
+    sn = sn + 1 == NST ? 0 : sn + 1;
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  int t = 0;
+  for (; t + NST - 1 < nt; ++t) step(t, T_{}, T_{}, std::integral_constant<int, NST == 3 ? NVM : 0>{});
+  if (NST == 3 && t + 1 < nt) {
+    step(t, F_{}, T_{}, std::integral_constant<int, 0>{});
+    ++t;
+  }
+  if (t < nt) step(t, F_{}, F_{}, std::integral_constant<int, 0>{});
+  gemm_epilogue<MI, 2, OUT_NCHW>(acc, P, ep, nullptr, m0 + wm * 32 * MI, n0 + wn * 64, lr, lh);
+}
+
+// Weight repack for k_conv_patch: w [G*M][C*T] -> [G][tiles_m][ktiles][64 MI][RL],
+// row layout [half 0: CPH*T taps, zero pad to HP][half 1 ...][pad to RL].
+__global__ void __launch_bounds__(256) k_conv_patch_pack(const float* __restrict__ w, float* __restrict__ out, int G,
+                                                         int M, int C, int T, int CPH, int HP, int RL, int BMc,
+                                                         int tiles_m, int ktiles, int64_t total) {
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = idx;
+    const int col = static_cast<int>(r % RL);
+    r /= RL;
+    const int row = static_cast<int>(r % BMc);
+    r /= BMc;
+    const int kt = static_cast<int>(r % ktiles);
+    r /= ktiles;
+    const int tm = static_cast<int>(r % tiles_m);
+    const int g = static_cast<int>(r / tiles_m);
+    const int m = tm * BMc + row;
+    const int h = col / HP, u = col - h * HP;
+    float v = 0.0f;
+    if (h < 2 && u < CPH * T && m < M) {
+      const int c = kt * 2 * CPH + h * CPH + u / T;
+      v = w[((int64_t)g * M + m) * C * T + (int64_t)c * T + (u % T)];
+    }
+    out[idx] = v;
+  }
 }
 
 // split-K reduction + epilogue (row-major C only)
@@ -1554,6 +1835,132 @@ int gemm_core(int trans_a, int trans_b, int M, int N, int K, float alpha, const 
 }
 
 
+// Packed-weight buffers of k_conv_patch, one per (device, stream), grown on
+// demand and reused by every later call on that stream (stream order keeps a
+// launch from overwriting a buffer an earlier launch still reads).
+std::mutex& pack_mutex() {
+  static std::mutex mu;
+  return mu;
+}
+std::map<std::pair<int, hipStream_t>, std::pair<float*, size_t>>& pack_cache() {
+  static std::map<std::pair<int, hipStream_t>, std::pair<float*, size_t>> cache;
+  return cache;
+}
+float* pack_buffer(size_t floats, hipStream_t s) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> g(pack_mutex());
+  auto& e = pack_cache()[{dev, s}];
+  if (e.second >= floats) return e.first;
+  if (e.first) {
+    if (hipStreamSynchronize(s) != hipSuccess) return nullptr;
+    (void)hipFree(e.first);
+    e = {nullptr, 0};
+  }
+  float* p = nullptr;
+  if (hipMalloc(&p, floats * sizeof(float)) != hipSuccess) return nullptr;
+  e = {p, floats};
+  return p;
+}
+
+template <int KH, int KW, int CPH, int MI, int PD>
+int launch_patch(Params P, const float* wpack, int PW, int CS, int gz, hipStream_t s) {
+  // LDS stages: 2 (two workgroups per CU, 2 waves per SIMD) unless the
+  // 192-row tile's registers need the whole SIMD; RRAM_CONV_PATCH_NST = 2 | 3
+  static const int nst_env = [] {
+    const char* e = getenv("RRAM_CONV_PATCH_NST");
+    return e ? atoi(e) : 0;
+  }();
+  // default: 2 stages whenever two workgroups' 2-stage rings fit the 160 KB LDS
+  using Sh = cp::Shape<KH, KW, CPH>;
+  constexpr int a_reg = ((64 * MI * Sh::RL + 255) / 256 + 3) / 4 * 4 * 256;
+  constexpr int sf = a_reg + PD * 4 * 64;
+  constexpr bool two_fit = 2 * 2 * sf * 4 <= 160 * 1024;
+  const int nst = (nst_env == 2 && two_fit) || nst_env == 3 ? nst_env : (two_fit ? 2 : 3);
+  P.tiles_m = (P.M + 64 * MI - 1) / (64 * MI);
+  P.tiles_n = (P.N + cp::BN - 1) / cp::BN;
+  P.tiles_z = gz;
+  const int64_t nwg = (int64_t)P.tiles_m * P.tiles_n * gz;
+  RRAM_REQUIRE(nwg < (1ll << 31), "conv: grid too large");
+  bool done = false;
+  if constexpr (two_fit) {
+    if (nst == 2) {
+      hipLaunchKernelGGL((k_conv_patch<KH, KW, CPH, MI, PD, 2>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, P,
+                         wpack, PW, CS);
+      done = true;
+    }
+  }
+  if (!done)
+    hipLaunchKernelGGL((k_conv_patch<KH, KW, CPH, MI, PD, 3>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, P,
+                       wpack, PW, CS);
+  return launch_status("conv patch");
+}
+
+// k_conv_patch for a stride-1, undilated 3x3 / 5x5 convolution whose output
+// planes hold >= 128 positions.  Returns 1 when it ran, 0 when the shape is
+// not covered (the caller falls back to the implicit-im2col GEMM), < 0 on
+// error.  Tuning knob RRAM_CONV_PATCH = 0 disables it.
+int conv_patch_fwd(const rram_conv_desc* d, const float* w, Params& P, hipStream_t s) {
+  static const bool on = [] {
+    const char* e = getenv("RRAM_CONV_PATCH");
+    return !(e && atoi(e) == 0);
+  }();
+  if (!on) return 0;
+  const int KH = d->kernel_h, KW = d->kernel_w;
+  if (d->stride_h != 1 || d->stride_w != 1 || d->dilation_h != 1 || d->dilation_w != 1) return 0;
+  if (!((KH == 3 && KW == 3) || (KH == 5 && KW == 5))) return 0;
+  const int CPH = KH == 3 ? 2 : 1;
+  const int G = d->group, Cg = d->channels / G, M = d->num_output / G;
+  const int HW = d->out_h * d->out_w, OW = d->out_w, OH = d->out_h;
+  if (HW < 128 || Cg % (2 * CPH) != 0 || Cg == 0) return 0;
+  if ((reinterpret_cast<uintptr_t>(w) & 3u) != 0) return 0;
+  // M tile: 128 or 192 rows, whichever pads less (<= 1/8 padded rows)
+  const int t128 = (M + 127) / 128 * 128, t192 = (M + 191) / 192 * 192;
+  const int MI = (t192 - M) < (t128 - M) ? 3 : 2;
+  const int BMc = 64 * MI, mt = MI == 3 ? t192 : t128;
+  if ((mt - M) * 8 > mt) return 0;
+  // patch rows: the most any 128-position tile needs
+  const int N = P.N;
+  int rmax = 0;
+  for (int n0 = 0; n0 < N; n0 += cp::BN) {
+    const int pl = std::min(n0 + cp::BN, N) - 1;
+    const int i0 = n0 / HW, i1 = pl / HW;
+    if (i1 > i0 + 1) return 0;
+    const int a0 = (n0 - i0 * HW) / OW;
+    const int b0 = i1 == i0 ? (pl - i0 * HW) / OW : OH - 1;
+    const int r = (b0 - a0 + KH) + (i1 == i0 ? 0 : (pl - i1 * HW) / OW + KH);
+    rmax = std::max(rmax, r);
+  }
+  const int PW = d->width + 2 * d->pad_w;
+  // channel stride: >= rmax * PW, with CPH * CS = 32 (mod 64) so the two lane
+  // halves read disjoint bank halves
+  int CS = rmax * PW;
+  while ((CPH * CS) % 64 != 32) ++CS;
+  const int pfl = 2 * CPH * CS;
+  const int PD = pfl <= 1024 ? 4 : pfl <= 1536 ? 6 : pfl <= 2048 ? 8 : 0;
+  if (PD == 0) return 0;
+  if (KH == 5 && MI == 3 && PD != 4) return 0;  // LDS
+  // repack the weights
+  const int T = KH * KW, S = CPH * T, HP = (S + 3) / 4 * 4;
+  const int RL = ((2 * HP / 4) % 2 == 0) ? 2 * HP + 4 : 2 * HP;
+  const int tiles_m = mt / BMc, ktiles = Cg / (2 * CPH);
+  const int64_t total = (int64_t)G * tiles_m * ktiles * BMc * RL;
+  RRAM_REQUIRE(total * 4 < (1ll << 31), "conv: packed weights must be < 2 GiB");
+  float* wp = pack_buffer(static_cast<size_t>(total), s);
+  RRAM_REQUIRE(wp != nullptr, "conv: packed-weight buffer allocation failed");
+  hipLaunchKernelGGL(k_conv_patch_pack, dim3(stream_blocks(total)), dim3(256), 0, s, w, wp, G, M, Cg, T, CPH, HP, RL,
+                     BMc, tiles_m, ktiles, total);
+  int rc = launch_status("conv weight pack");
+  if (rc) return rc;
+#define RRAM_P(KH_, CPH_, MI_, PD_) \
+  if (KH == KH_ && MI == MI_ && PD == PD_) rc = launch_patch<KH_, KH_, CPH_, MI_, PD_>(P, wp, PW, CS, G, s); else
+  RRAM_P(3, 2, 2, 4) RRAM_P(3, 2, 2, 6) RRAM_P(3, 2, 2, 8) RRAM_P(3, 2, 3, 4) RRAM_P(3, 2, 3, 6) RRAM_P(3, 2, 3, 8)
+  RRAM_P(5, 1, 2, 4) RRAM_P(5, 1, 2, 6) RRAM_P(5, 1, 2, 8) RRAM_P(5, 1, 3, 4)
+  return 0;
+#undef RRAM_P
+  return rc ? rc : 1;
+}
+
 int conv_fwd_core(const rram_conv_desc* d, const float* x, const float* w, const float* bias,
                   float* y, int relu, hipStream_t s) {
   const int g = d->group;
@@ -1596,6 +2003,10 @@ int conv_fwd_core(const rram_conv_desc* d, const float* x, const float* w, const
   P.grp_b = (int64_t)cin_g * d->height * d->width;
   P.grp_c = (int64_t)cout_g * HoWo;
   P.grp_bias = cout_g;
+  {
+    const int rc = conv_patch_fwd(d, w, P, s);
+    if (rc != 0) return rc < 0 ? rc : RRAM_OK;
+  }
   // table-driven gather when the taps fit the 31-bit (or 63-bit) validity mask (or no padding)
   const bool padded = d->pad_h > 0 || d->pad_w > 0;
   const int taps = d->kernel_h * d->kernel_w;

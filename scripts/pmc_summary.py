@@ -12,9 +12,9 @@ dur = defaultdict(list)
 for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
-        m = re.search(r"k_gemm(2?)<([^>]*)>", name)
+        m = re.search(r"k_(gemm2?|conv_patch)<([^>]*)>", name)
         if m:
-            short = f"gemm{m.group(1)}<" + m.group(2).replace(" ", "") + ">"
+            short = f"{m.group(1)}<" + m.group(2).replace(" ", "") + ">"
         else:
             short = re.sub(r"\(anonymous namespace\)::", "", name)
             short = re.sub(r"\(.*", "", short).replace("void ", "").split("::")[-1][:40]
