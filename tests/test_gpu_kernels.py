@@ -436,6 +436,41 @@ def test_conv_fwd_vs_oracle(device, oracle_mod, cs):
     np.testing.assert_allclose(N(y), np.maximum(ref, 0), atol=1e-4, rtol=1e-4)
 
 
+# Shapes aimed at the LDS-patch convolution (k_conv_patch: stride 1, 3x3 / 5x5,
+# >= 128 output positions per image): 192-row weight tiles, 128-position tiles
+# spanning two images, wide rows (56 x 56: 6 patch pieces per wave), padded M
+# tiles, no padding, groups; and shapes it must leave to the im2col GEMM.
+PATCH_CASES = [
+    dict(x=(3, 8, 13, 13), cout=192, k=3, p=1, g=1),    # M = 192 tile, 169-position images
+    dict(x=(2, 4, 56, 56), cout=128, k=3, p=1, g=1),    # wide rows
+    dict(x=(2, 12, 28, 28), cout=224, k=5, p=2, g=1),   # 5x5, M padded to 256
+    dict(x=(5, 8, 10, 13), cout=256, k=3, p=1, g=2),    # 130 positions: most tiles span two images
+    dict(x=(2, 4, 20, 20), cout=128, k=5, p=0, g=1),    # 5x5 without padding (16 x 16 out)
+    dict(x=(2, 6, 13, 13), cout=128, k=3, p=1, g=1),    # C % 4 != 0: im2col path
+    dict(x=(2, 8, 12, 12), cout=128, k=3, p=0, g=1),    # 100 positions per image: im2col path
+]
+
+
+@pytest.mark.parametrize("cs", PATCH_CASES)
+def test_conv_patch_shapes_vs_fp64(device, cs):
+    """Forward convolution at the patch kernel's edges within 1e-4 of
+    Σ|a·b| of a float64 reference (north_star tolerance, scale-aware), plain
+    and with the fused ReLU."""
+    import torch
+    from rramsim import ops
+    from _ref64 import check_conv
+    rng = np.random.default_rng(99)
+    x = rng.standard_normal(cs["x"]).astype(np.float32)
+    w = (rng.standard_normal((cs["cout"], cs["x"][1] // cs["g"], cs["k"], cs["k"])) * 0.1).astype(np.float32)
+    b = rng.standard_normal(cs["cout"]).astype(np.float32)
+    d = ops.conv_desc(cs["x"], cs["cout"], cs["k"], 1, cs["p"], 1, cs["g"])
+    y = torch.empty((cs["x"][0], cs["cout"], d.out_h, d.out_w), device=device)
+    for relu in (False, True):
+        ops.conv2d_fwd(d, T(x, device), T(w, device), T(b, device), y, relu=relu)
+        torch.cuda.synchronize()
+        check_conv(N(y), x, w, b, 1, cs["p"], cs["g"], relu=relu, what=f"conv {cs} relu={relu}")
+
+
 @pytest.mark.parametrize("cs", [CONV_CASES[0], CONV_CASES[1], CONV_CASES[4], CONV_CASES[12]])
 def test_conv_fwd_unaligned_weights_nan_tail(device, oracle_mod, cs):
     """K % 4 != 0 (the unaligned 16-byte weight loader): the weights sit at a
