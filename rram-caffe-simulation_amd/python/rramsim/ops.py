@@ -157,6 +157,22 @@ def conv_desc(x_shape, num_output, kernel, stride=1, pad=0, dilation=1, group=1)
     return d
 
 
+ENGINE_F32, ENGINE_BF16X6 = 0, 1
+
+
+def set_conv_engine(engine):
+    """Matrix-core engine of the stride-1 3x3 / 5x5 convolution forward
+    (rram_set_conv_engine); returns the previous one."""
+    prev = _lib().rram_set_conv_engine(int(engine))
+    if prev < 0:
+        K.check(prev, "set_conv_engine")
+    return prev
+
+
+def get_conv_engine():
+    return _lib().rram_get_conv_engine()
+
+
 def conv2d_fwd(d, x, w, bias, y, relu=False):
     K.check(_lib().rram_conv2d_fwd(C.byref(d), _p(x), _p(w), _p(bias), _p(y), int(relu),
                                    _stream()), "conv2d_fwd")

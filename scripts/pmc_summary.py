@@ -12,7 +12,7 @@ dur = defaultdict(list)
 for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
-        m = re.search(r"k_(gemm2?|conv_patch)<([^>]*)>", name)
+        m = re.search(r"k_(gemm2?|conv_patch(?:_x6)?)<([^>]*)>", name)
         if m:
             short = f"{m.group(1)}<" + m.group(2).replace(" ", "") + ">"
         else:

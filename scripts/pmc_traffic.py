@@ -7,7 +7,9 @@ in KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced
 streaming read, so it is doubled; WRITE_SIZE is exact for 16-B stores.
 
 Per-launch traffic for the injection kernel; per-step traffic for the
-conv/IP GEMM set (all k_gemm + k_splitk_reduce dispatches / forwards run).
+conv/IP GEMM set (all k_gemm* / k_conv_patch* / k_splitk_reduce dispatches /
+forwards run), next to the algorithmic bytes of AlexNet b256's conv1-5 + fc6-8
+(each layer's input activation + weights read once, output written once).
 Writes JSON to stdout (bench.py reads the committed copy in profiles/)."""
 import csv
 import glob
@@ -26,13 +28,20 @@ for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
             continue
         if "k_inject_batched" in name:
             k = "inject"
-        elif "k_gemm" in name or "k_splitk_reduce" in name:
+        elif "k_gemm" in name or "k_conv_patch" in name or "k_splitk_reduce" in name:
             k = "gemm"
         else:
             continue
         tot[(k, c)] += float(r["Counter_Value"])
         cnt[(k, c)] += 1
 KIB = 1024.0
+# AlexNet b256 (bvlc_alexnet TEST): (input elems, weight elems, output elems) per image-batch
+B = 256
+ALEX = [(3*227*227*B, 96*363, 96*55*55*B), (96*27*27*B, 256*48*25, 256*27*27*B),
+        (256*13*13*B, 384*256*9, 384*13*13*B), (384*13*13*B, 384*192*9, 384*13*13*B),
+        (384*13*13*B, 256*192*9, 256*13*13*B), (9216*B, 4096*9216, 4096*B),
+        (4096*B, 4096*4096, 4096*B), (4096*B, 1000*4096, 1000*B)]
+ALG_BYTES = 4.0 * sum(a + w + o for a, w, o in ALEX)
 out = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py --steps 3 --warmup 1 ({root})",
        "correction": "bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 (gfx950 FETCH_SIZE half-count)"}
 if cnt[("inject", "FETCH_SIZE")] and cnt[("inject", "WRITE_SIZE")]:
@@ -44,5 +53,7 @@ if cnt[("gemm", "FETCH_SIZE")] and cnt[("gemm", "WRITE_SIZE")]:
     fb = 2 * KIB * tot[("gemm", "FETCH_SIZE")] / forwards
     wb = KIB * tot[("gemm", "WRITE_SIZE")] / forwards
     out["gemm"] = {"bytes_per_step": fb + wb, "read_bytes": fb, "write_bytes": wb,
-                   "dispatches_per_step": cnt[("gemm", "FETCH_SIZE")] / forwards}
+                   "dispatches_per_step": cnt[("gemm", "FETCH_SIZE")] / forwards,
+                   "algorithmic_bytes_per_step": ALG_BYTES,
+                   "ratio_to_algorithmic": (fb + wb) / ALG_BYTES}
 print(json.dumps(out, indent=1))

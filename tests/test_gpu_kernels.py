@@ -451,11 +451,22 @@ PATCH_CASES = [
 ]
 
 
+@pytest.fixture(params=["f32", "bf16x6"])
+def conv_engine(request):
+    """Runs a test under each matrix-core engine of the convolution forward
+    (rram_set_conv_engine) and restores the previous one."""
+    from rramsim import ops
+    eng = ops.ENGINE_F32 if request.param == "f32" else ops.ENGINE_BF16X6
+    prev = ops.set_conv_engine(eng)
+    yield request.param
+    ops.set_conv_engine(prev)
+
+
 @pytest.mark.parametrize("cs", PATCH_CASES)
-def test_conv_patch_shapes_vs_fp64(device, cs):
-    """Forward convolution at the patch kernel's edges within 1e-4 of
+def test_conv_patch_shapes_vs_fp64(device, cs, conv_engine):
+    """Forward convolution at the patch kernels' edges within 1e-4 of
     Σ|a·b| of a float64 reference (north_star tolerance, scale-aware), plain
-    and with the fused ReLU."""
+    and with the fused ReLU, on both engines (fp32 MFMA and the bf16x6 split)."""
     import torch
     from rramsim import ops
     from _ref64 import check_conv
@@ -468,7 +479,48 @@ def test_conv_patch_shapes_vs_fp64(device, cs):
     for relu in (False, True):
         ops.conv2d_fwd(d, T(x, device), T(w, device), T(b, device), y, relu=relu)
         torch.cuda.synchronize()
-        check_conv(N(y), x, w, b, 1, cs["p"], cs["g"], relu=relu, what=f"conv {cs} relu={relu}")
+        check_conv(N(y), x, w, b, 1, cs["p"], cs["g"], relu=relu, what=f"conv {cs} relu={relu} {conv_engine}")
+
+
+# AlexNet conv2 / conv3 / conv4 / conv5 at 4 images (Caffe-filler-like weight scale)
+ENGINE_CASES = [
+    dict(x=(4, 96, 27, 27), cout=256, k=5, p=2, g=2),
+    dict(x=(4, 256, 13, 13), cout=384, k=3, p=1, g=1),
+    dict(x=(4, 384, 13, 13), cout=384, k=3, p=1, g=2),
+    dict(x=(4, 384, 13, 13), cout=256, k=3, p=1, g=2),
+]
+
+
+@pytest.mark.parametrize("cs", ENGINE_CASES)
+def test_conv_engine_bf16x6_accuracy_vs_f32(device, cs):
+    """The bf16x6 engine is fp32-accurate, not reduced precision: against a
+    float64 evaluation its error (in units of Σ|a·b|) is of the same size as
+    the fp32-MFMA engine's, far inside the 1e-4 bound.  Prints both."""
+    import torch
+    from rramsim import ops
+    from _ref64 import conv64
+    rng = np.random.default_rng(7)
+    x = np.maximum(rng.standard_normal(cs["x"]), 0).astype(np.float32)   # post-ReLU activations
+    w = (rng.standard_normal((cs["cout"], cs["x"][1] // cs["g"], cs["k"], cs["k"])) * 0.01).astype(np.float32)
+    b = rng.standard_normal(cs["cout"]).astype(np.float32)
+    d = ops.conv_desc(cs["x"], cs["cout"], cs["k"], 1, cs["p"], 1, cs["g"])
+    ref, scale = conv64(x, w, b, 1, cs["p"], cs["g"])
+    err = {}
+    prev = ops.get_conv_engine()
+    try:
+        for eng in (ops.ENGINE_F32, ops.ENGINE_BF16X6):
+            ops.set_conv_engine(eng)
+            y = torch.empty((cs["x"][0], cs["cout"], d.out_h, d.out_w), device=device)
+            ops.conv2d_fwd(d, T(x, device), T(w, device), T(b, device), y)
+            torch.cuda.synchronize()
+            r = np.abs(N(y).astype(np.float64) - ref) / scale
+            err[eng] = (float(r.max()), float(r.mean()))
+    finally:
+        ops.set_conv_engine(prev)
+    f32, x6 = err[ops.ENGINE_F32], err[ops.ENGINE_BF16X6]
+    print(f"{cs}: max/mean err / Σ|a·b|: f32 {f32[0]:.2e}/{f32[1]:.2e}  bf16x6 {x6[0]:.2e}/{x6[1]:.2e}")
+    assert x6[0] < 1e-6 and f32[0] < 1e-6          # fp32 level (the test bound is 1e-4)
+    assert x6[0] <= 2.0 * f32[0] and x6[1] <= 2.0 * f32[1]
 
 
 @pytest.mark.parametrize("cs", [CONV_CASES[0], CONV_CASES[1], CONV_CASES[4], CONV_CASES[12]])
