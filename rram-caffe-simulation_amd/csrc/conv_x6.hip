@@ -1,0 +1,469 @@
+// Convolution forward with fp32 products on the bf16 matrix cores
+// (RRAM_ENGINE_BF16X6, include/rram_kernels.h): the LDS-patch convolution of
+// gemm.hip's k_conv_patch re-tiled for v_mfma_f32_32x32x16_bf16.
+#include <stdlib.h>
+
+#include <algorithm>
+#include <atomic>
+#include <type_traits>
+
+#include "gemm_common.hpp"
+
+namespace rram {
+namespace {
+
+// ---------------------------------------------------------------------------
+// k_conv_patch_x6: the patch convolution with each fp32 product formed on the
+// bf16 matrix cores.  Every fp32 operand is split exactly into three bf16
+// terms, x = xh + xm + xl (round-to-nearest at each step; the remainders are
+// exact in fp32 and the third term holds the last 8 significand bits), and
+// a*b is accumulated in fp32 as the six terms
+//   al*bh + ah*bl + am*bm + am*bh + ah*bm + ah*bh
+// (v_mfma_f32_32x32x16_bf16: a product of two bf16 is exact in fp32).  The
+// dropped terms am*bl, al*bm, al*bl are below 2^-25 |a*b| with independent
+// signs, under the fp32 rounding of the accumulation itself, so the result
+// carries fp32 accuracy (tests compare it with a float64 evaluation at the
+// same bound as the fp32-MFMA kernels) while a 32x32x16 bf16 MFMA does the
+// work of eight 32x32x2 fp32 MFMAs in half their cycles: six of them cost
+// 192 cycles where the fp32 form of the same 32x32x16 block costs 512.
+// The weights are split once per call by the repack kernel (three bf16
+// planes, fragment order); the activations are split in registers after the
+// LDS reads of the patch (4-5 VALU per element, hidden between MFMAs).
+// K order: a K-tile holds 2 CPH input channels (half h: channels
+// kt*2CPH + h*CPH + cc) x KH*KW taps = S steps per half, padded to G8 groups
+// of 8; MFMA group g takes steps 8g .. 8g+7 of both halves (lane half h holds
+// k = 8h + j of the 32x32x16 operand).  Padded steps have zero weights and
+// read no activations.
+namespace x6 {
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float float2v __attribute__((ext_vector_type(2)));
+struct Parts {
+  bf16x8 h, m, l;
+};
+// exact three-term split of 8 floats (round to nearest even at each step)
+__device__ __forceinline__ void split8(const float (&x)[8], Parts& r) {
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const float2v v = {x[2 * p], x[2 * p + 1]};
+    const bf16x2 h = __builtin_convertvector(v, bf16x2);
+    const float2v r1 = v - __builtin_convertvector(h, float2v);
+    const bf16x2 m = __builtin_convertvector(r1, bf16x2);
+    const float2v r2 = r1 - __builtin_convertvector(m, float2v);
+    const bf16x2 l = __builtin_convertvector(r2, bf16x2);
+    r.h[2 * p] = h[0];
+    r.h[2 * p + 1] = h[1];
+    r.m[2 * p] = m[0];
+    r.m[2 * p + 1] = m[1];
+    r.l[2 * p] = l[0];
+    r.l[2 * p + 1] = l[1];
+  }
+}
+// term p (0 = high, 1 = middle, 2 = low) of the split of v, as bf16 bits
+__device__ __forceinline__ uint16_t split_term(float v, int p) {
+  const __bf16 h = static_cast<__bf16>(v);
+  const float r1 = v - static_cast<float>(h);
+  const __bf16 m = static_cast<__bf16>(r1);
+  const __bf16 l = static_cast<__bf16>(r1 - static_cast<float>(m));
+  const __bf16 t = p == 0 ? h : p == 1 ? m : l;
+  return __builtin_bit_cast(uint16_t, t);
+}
+__device__ __forceinline__ floatx16 mfma6(const Parts& a, const Parts& b, floatx16 c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.l, b.h, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.l, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, b.m, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, b.h, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.m, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.h, c, 0, 0, 0);
+}
+template <int KH, int KW, int CPH>
+struct Shape {
+  static constexpr int T = KH * KW;
+  static constexpr int S = CPH * T;         // steps per half
+  static constexpr int G8 = (S + 7) / 8;    // MFMA groups per K-tile
+  static constexpr int RLB = G8 * 96 + 16;  // bytes per packed weight row ([g][half][term][8 bf16] + pad: RLB/16 odd)
+};
+constexpr int BN = 256;  // workgroup tile columns (rows: 32 MI, MI = 3 | 4)
+}  // namespace x6
+
+template <int KH, int KW, int CPH, int MI, int PD>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+k_conv_patch_x6(Params P, const uint16_t* __restrict__ wpack, int PW, int CS) {
+  using namespace g2;
+  using Sh = x6::Shape<KH, KW, CPH>;
+  // 32 MI x 256 tile; wave w owns all 32 MI rows x columns 64 w .. 64 w + 63,
+  // so the B split (the VALU of the main loop) is shared by MI row blocks and
+  // each weight byte staged in LDS feeds 256 columns
+  constexpr int BMc = 32 * MI, BNc = x6::BN;
+  constexpr int A_B = BMc * Sh::RLB;                    // weight slab bytes per K-tile
+  constexpr int A_DMA = ((A_B + 1023) / 1024 + 3) / 4;  // 1 KB pieces per wave
+  constexpr int A_REGB = A_DMA * 4 * 1024;
+  constexpr int SFB = A_REGB + PD * 4 * 64 * 4;         // stage bytes (weights + patch)
+  constexpr int NVM = A_DMA + PD;
+  constexpr int G8 = Sh::G8;
+  static_assert(2 * SFB <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[2 * SFB];
+  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem));
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lr = lane & 31, lh = lane >> 5;
+
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, loc = bid >> 3;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int tid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const int tm = __builtin_amdgcn_readfirstlane(tid % P.tiles_m);
+  const int tn = __builtin_amdgcn_readfirstlane((tid / P.tiles_m) % P.tiles_n);
+  const int z = __builtin_amdgcn_readfirstlane(tid / (P.tiles_m * P.tiles_n));
+  const int n0 = tn * BNc;
+  const int m0 = tm * BMc;
+
+  const ConvGeom& cv = P.cv;
+  const int HW = cv.howo.d, OW = cv.wo_div.d;
+  const int ktiles = cv.C / (2 * CPH);
+  const float* xin = P.b.p + z * P.grp_b;
+  Epi ep = P.e;
+  if (z > 0) {
+    ep.C += z * P.grp_c;
+    if (ep.bias) ep.bias += z * P.grp_bias;
+  }
+  const uint16_t* abase = wpack + ((int64_t)z * P.tiles_m + tm) * ktiles * (A_B / 2);
+  const int4v arsrc = make_rsrc(reinterpret_cast<const float*>(abase), static_cast<uint32_t>((int64_t)ktiles * A_B));
+  uint32_t aoff[A_DMA];
+#pragma unroll
+  for (int i = 0; i < A_DMA; ++i) {
+    const int f = ((wave * A_DMA + i) * 64 + lane) * 16;
+    aoff[i] = f < A_B ? static_cast<uint32_t>(f) : 0x80000000u;
+  }
+
+  // patch: positions n0 .. plast cover images img0 .. img0 + nseg - 1 (<= 3);
+  // segment s holds output rows f_s .. l_s of its image plus the KH - 1 halo,
+  // at patch rows p_s .. p_{s+1} - 1
+  const int plast = min(n0 + BNc, P.N) - 1;
+  const int img0 = n0 / HW, nseg = plast / HW - img0 + 1;
+  const int f0 = (n0 - img0 * HW) / OW;
+  auto seg_last = [&](int s) { return s == nseg - 1 ? (plast - (img0 + s) * HW) / OW : cv.Ho - 1; };
+  const int p1 = seg_last(0) - f0 + KH;
+  const int p2 = p1 + (nseg > 1 ? seg_last(1) + KH : 0);
+  const int R = p2 + (nseg > 2 ? seg_last(2) + KH : 0);
+  const int4v xrsrc = make_rsrc(xin, static_cast<uint32_t>(cv.in_bytes));
+  const uint32_t HW4 = static_cast<uint32_t>(cv.H * cv.W * 4);
+  uint32_t poff[PD];
+#pragma unroll
+  for (int i = 0; i < PD; ++i) {
+    const int f = (wave * PD + i) * 64 + lane;
+    const int ch = f / CS, w = f - ch * CS;
+    const int prow = w / PW, pcol = w - prow * PW;
+    uint32_t off = 0x80000000u;
+    if (ch < 2 * CPH && prow < R) {
+      const int sg = prow >= p2 ? 2 : prow >= p1 ? 1 : 0;
+      const int y = (sg == 0 ? f0 + prow : prow - (sg == 1 ? p1 : p2)) - cv.ph;
+      const int x = pcol - cv.pw;
+      if (y >= 0 && y < cv.H && x >= 0 && x < cv.W)
+        off = static_cast<uint32_t>((int64_t)(img0 + sg) * cv.chw * 4) + static_cast<uint32_t>(ch) * HW4 +
+              static_cast<uint32_t>((y * cv.W + x) * 4);
+    }
+    poff[i] = off;
+  }
+  int pb[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = min(n0 + wave * 64 + j * 32 + lr, plast);
+    const int img = n / HW, sp = n - img * HW;
+    const int oh = sp / OW, ow = sp - oh * OW;
+    const int sg = img - img0;
+    const int prow = sg == 0 ? oh - f0 : (sg == 1 ? p1 : p2) + oh;
+    pb[j] = prow * PW + ow + lh * CPH * CS;
+  }
+
+  floatx16 acc[MI][2];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+  auto issue = [&](int kt, int stg, int e) {  // DMA item e of K-tile kt into stage stg
+    const uint32_t img = lds0 + static_cast<uint32_t>(stg * SFB);
+    if (e < A_DMA) {
+      dma_b128(arsrc, aoff[e] + static_cast<uint32_t>(kt * A_B), img + static_cast<uint32_t>((wave * A_DMA + e) * 1024));
+    } else {
+      const int i = e - A_DMA;
+      dma_b32(xrsrc, poff[i] + static_cast<uint32_t>(kt * 2 * CPH) * HW4,
+              img + static_cast<uint32_t>(A_REGB + (wave * PD + i) * 64 * 4));
+    }
+  };
+  struct Fr {
+    x6::bf16x8 a[MI][3];  // this lane's 8 k of rows 32 i + lr: high, middle, low terms
+    float b[2][8];        // raw activations of columns j
+    x6::Parts bp[2];      // their split
+  };
+  auto read_a = [&](Fr& F, const char* st, int g, int i) {
+    const char* p = st + (i * 32 + lr) * Sh::RLB + (g * 2 + lh) * 48;
+#pragma unroll
+    for (int t = 0; t < 3; ++t) F.a[i][t] = *reinterpret_cast<const x6::bf16x8*>(p + 16 * t);
+  };
+  auto read_b = [&](Fr& F, const char* st, int g) {
+    const float* pt = reinterpret_cast<const float*>(st + A_REGB);
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const int sx = 8 * g + jj;
+      if (sx < Sh::S) {
+        const int cc = sx / Sh::T, tp = sx - cc * Sh::T, kh = tp / KW, kw = tp - kh * KW;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) F.b[j][jj] = pt[pb[j] + cc * CS + kh * PW + kw];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) F.b[j][jj] = 0.0f;
+      }
+    }
+  };
+
+  const int nt = ktiles;  // >= 1 (host)
+  // fragments ping-pong between F[0] and F[1] by group parity (compile-time
+  // indices, no register copies); with an odd group count tiles go in pairs
+  Fr F[2];
+#pragma unroll
+  for (int e = 0; e < NVM; ++e) issue(0, 0, e);
+  wait_vm<0>();
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int i = 0; i < MI; ++i) read_a(F[0], smem, 0, i);
+  read_b(F[0], smem, 0);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) x6::split8(F[0].b[j], F[0].bp[j]);
+
+  // one K-tile; PAR: parity of its first group's fragments; MORE: tile t + 1 exists
+  auto tile = [&](int t, auto par_c, auto more_c) {
+    constexpr int PAR = decltype(par_c)::value;
+    constexpr bool MORE = decltype(more_c)::value;
+    const char* cur = smem + (t & 1) * SFB;
+    const char* nxt = smem + ((t + 1) & 1) * SFB;
+#pragma unroll
+    for (int g = 0; g < G8; ++g) {
+      Fr& fc = F[(g + PAR) & 1];
+      Fr& fn = F[(g + 1 + PAR) & 1];
+      const bool last = g == G8 - 1;
+      // the next group's fragments: this tile's group g + 1, or group 0 of
+      // tile t + 1 once its DMA has landed (wait + barrier: every wave is then
+      // also done reading the stage the next DMA overwrites)
+      if (last && MORE) {
+        wait_vm<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      const bool rd = !last || MORE;
+      const char* src = last ? nxt : cur;
+      const int gn = last ? 0 : g + 1;
+      constexpr int NB = 2 * MI;  // MFMA blocks (6 MFMAs each) of a group
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        const int i = q >> 1, j = q & 1;
+        acc[i][j] = x6::mfma6(x6::Parts{fc.a[i][0], fc.a[i][1], fc.a[i][2]}, fc.bp[j], acc[i][j]);
+        if (rd) {
+          if (q == 0) read_b(fn, src, gn);
+          if (q >= 1 && q <= MI) read_a(fn, src, gn, q - 1);
+          if (q == NB - 3) x6::split8(fn.b[0], fn.bp[0]);
+          if (q == NB - 1) x6::split8(fn.b[1], fn.bp[1]);
+        }
+        // DMA of tile t + 1 spread over the blocks of groups 0 .. G8-2
+        if (!last && MORE) {
+          constexpr int SL = (G8 - 1) * NB;
+          const int sl = g * NB + q;
+#pragma unroll
+          for (int e = 0; e < NVM; ++e)
+            if ((e * SL) / NVM == sl) issue(t + 1, (t + 1) & 1, e);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  using P0 = std::integral_constant<int, 0>;
+  using P1 = std::integral_constant<int, 1>;
+  if constexpr (G8 % 2 == 0) {
+    int t = 0;
+    for (; t + 1 < nt; ++t) tile(t, P0{}, T_{});
+    tile(t, P0{}, F_{});
+  } else {
+    int t = 0;
+    for (; t + 2 < nt; t += 2) {
+      tile(t, P0{}, T_{});
+      tile(t + 1, P1{}, T_{});
+    }
+    if (t + 1 < nt) {
+      tile(t, P0{}, T_{});
+      tile(t + 1, P1{}, F_{});
+    } else {
+      tile(t, P0{}, F_{});
+    }
+  }
+  gemm_epilogue<MI, 2, OUT_NCHW>(acc, P, ep, nullptr, m0, n0 + wave * 64, lr, lh);
+}
+
+// Weight repack for k_conv_patch_x6: w [G*M][C*T] -> bf16 terms
+// [G][tiles_m][ktiles][64 MI][RLB/2]: row = [group g][half h][term][8 steps] + pad.
+__global__ void __launch_bounds__(256) k_conv_patch_pack_x6(const float* __restrict__ w, uint16_t* __restrict__ out,
+                                                            int G, int M, int C, int T, int CPH, int G8, int RLH,
+                                                            int BMc, int tiles_m, int ktiles, int64_t total) {
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = idx;
+    const int col = static_cast<int>(r % RLH);
+    r /= RLH;
+    const int row = static_cast<int>(r % BMc);
+    r /= BMc;
+    const int kt = static_cast<int>(r % ktiles);
+    r /= ktiles;
+    const int tm = static_cast<int>(r % tiles_m);
+    const int g = static_cast<int>(r / tiles_m);
+    const int m = tm * BMc + row;
+    uint16_t v = 0;
+    if (col < G8 * 48 && m < M) {
+      const int gg = col / 48, rem = col - gg * 48;
+      const int h = rem / 24, p = (rem - h * 24) / 8, j = rem & 7;
+      const int s = 8 * gg + j;
+      if (s < CPH * T) {
+        const int c = kt * 2 * CPH + h * CPH + s / T;
+        v = x6::split_term(w[((int64_t)g * M + m) * C * T + (int64_t)c * T + (s % T)], p);
+      }
+    }
+    out[idx] = v;
+  }
+}
+
+}  // namespace
+
+float* pack_buffer(size_t floats, hipStream_t s);  // gemm.hip
+
+// most patch rows (output rows + KH - 1 halo per image segment) any BN-position
+// tile of an OH x OW output needs; -1 when a tile spans more than maxseg images
+int patch_rows(int N, int HW, int OW, int OH, int KH, int BN, int maxseg) {
+  int rmax = 0;
+  for (int n0 = 0; n0 < N; n0 += BN) {
+    const int pl = std::min(n0 + BN, N) - 1;
+    const int i0 = n0 / HW, i1 = pl / HW;
+    if (i1 - i0 + 1 > maxseg) return -1;
+    int r = 0;
+    for (int i = i0; i <= i1; ++i) {
+      const int f = i == i0 ? (n0 - i0 * HW) / OW : 0;
+      const int l = i == i1 ? (pl - i1 * HW) / OW : OH - 1;
+      r += l - f + KH;
+    }
+    rmax = std::max(rmax, r);
+  }
+  return rmax;
+}
+
+template <int KH, int CPH, int MI, int PD>
+int launch_patch_x6(Params P, const uint16_t* wpack, int PW, int CS, int gz, hipStream_t s) {
+  P.tiles_m = (P.M + 32 * MI - 1) / (32 * MI);
+  P.tiles_n = (P.N + x6::BN - 1) / x6::BN;
+  P.tiles_z = gz;
+  const int64_t nwg = (int64_t)P.tiles_m * P.tiles_n * gz;
+  RRAM_REQUIRE(nwg < (1ll << 31), "conv: grid too large");
+  hipLaunchKernelGGL((k_conv_patch_x6<KH, KH, CPH, MI, PD>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, P, wpack,
+                     PW, CS);
+  return launch_status("conv patch x6");
+}
+
+// engine of the stride-1 3x3 / 5x5 convolutions (rram_set_conv_engine)
+std::atomic<int>& conv_engine() {
+  static std::atomic<int> eng{[] {
+    const char* e = getenv("RRAM_CONV_X6");
+    return (e && atoi(e) == 0) ? static_cast<int>(RRAM_ENGINE_F32) : static_cast<int>(RRAM_ENGINE_BF16X6);
+  }()};
+  return eng;
+}
+
+// k_conv_patch_x6 (fp32 products on the bf16 matrix cores, see the kernel):
+// stride-1 undilated 3x3 / 5x5 convolutions with >= 128 positions per output
+// plane and <= 1/8 padded rows in the 96- or 128-row M tiles.  Returns 1 when it ran,
+// 0 when not covered, < 0 on error.  RRAM_CONV_X6 = 0 keeps the fp32-MFMA kernels.
+int conv_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const float* bias, float* y, int relu,
+                hipStream_t s) {
+  if (conv_engine().load(std::memory_order_relaxed) != RRAM_ENGINE_BF16X6) return 0;
+  const int KH = d->kernel_h, KW = d->kernel_w;
+  if (d->stride_h != 1 || d->stride_w != 1 || d->dilation_h != 1 || d->dilation_w != 1) return 0;
+  if (!((KH == 3 && KW == 3) || (KH == 5 && KW == 5))) return 0;
+  const int G = d->group, Cg = d->channels / G, M = d->num_output / G;
+  const int HW = d->out_h * d->out_w, OW = d->out_w, OH = d->out_h;
+  const int CPH = KH == 5 ? 1 : (Cg % 8 == 0 ? 4 : 2);
+  if (HW < 128 || Cg == 0 || Cg % (2 * CPH) != 0) return 0;
+  if ((reinterpret_cast<uintptr_t>(w) & 3u) != 0) return 0;
+  // M tile 128 or 96 rows, whichever pads less (<= 1/8 padded rows)
+  const int t128 = (M + 127) / 128 * 128, t96 = (M + 95) / 96 * 96;
+  const int MI = (t96 - M) < (t128 - M) ? 3 : 4;
+  const int mt = MI == 3 ? t96 : t128;
+  if ((mt - M) * 8 > mt) return 0;
+  Params P{};
+  P.M = M;
+  P.N = d->num * HW;
+  P.K = Cg * KH * KW;
+  P.split = 1;
+  P.b = make_view(x, 0, P.N, P.K);
+  ConvGeom& cv = P.cv;
+  cv.C = Cg;
+  cv.H = d->height;
+  cv.W = d->width;
+  cv.KH = KH;
+  cv.KW = KW;
+  cv.ph = d->pad_h;
+  cv.pw = d->pad_w;
+  cv.sh = cv.sw = cv.dh = cv.dw = 1;
+  cv.Ho = OH;
+  cv.Wo = OW;
+  cv.howo = make_fastdiv(HW);
+  cv.wo_div = make_fastdiv(OW);
+  cv.chw = (int64_t)d->channels * d->height * d->width;
+  if ((int64_t)d->num * cv.chw * 4 >= (1ll << 31)) return 0;  // 32-bit buffer offsets
+  cv.in_bytes = static_cast<int>((int64_t)d->num * cv.chw * 4);
+  P.e = make_epi(y, HW, 1.0f, 0.0f, bias, RRAM_BIAS_ROW, relu);
+  P.e.cimg = (int64_t)d->num_output * HW;
+  P.e.hw = make_fastdiv(HW);
+  P.grp_b = (int64_t)Cg * d->height * d->width;
+  P.grp_c = (int64_t)M * HW;
+  P.grp_bias = M;
+  const int rmax = patch_rows(P.N, HW, OW, OH, KH, x6::BN, 3);
+  if (rmax < 0) return 0;
+  const int PW = d->width + 2 * d->pad_w;
+  // channel stride >= rmax * PW with CPH * CS = 32 (mod 64): the two lane
+  // halves read disjoint bank halves
+  int CS = rmax * PW;
+  while ((CPH * CS) % 64 != 32) ++CS;
+  const int need = (2 * CPH * CS + 255) / 256;  // 256-float patch pieces
+  static const int pd5[] = {4, 8, 12}, pd3q[] = {8, 12, 16}, pd3h[] = {4, 8, 16};
+  const int* pds = KH == 5 ? pd5 : CPH == 4 ? pd3q : pd3h;
+  int PD = 0;
+  for (int i = 2; i >= 0; --i)
+    if (pds[i] >= need) PD = pds[i];
+  if (PD == 0) return 0;
+  const int T = KH * KW, S = CPH * T, G8 = (S + 7) / 8, RLH = (G8 * 96 + 16) / 2;
+  const int BMc = 32 * MI, tiles_m = mt / BMc, ktiles = Cg / (2 * CPH);
+  const int64_t total = (int64_t)G * tiles_m * ktiles * BMc * RLH;
+  RRAM_REQUIRE(total * 2 < (1ll << 31), "conv: packed weights must be < 2 GiB");
+  uint16_t* wp = reinterpret_cast<uint16_t*>(pack_buffer(static_cast<size_t>((total + 1) / 2), s));
+  RRAM_REQUIRE(wp != nullptr, "conv: packed-weight buffer allocation failed");
+  hipLaunchKernelGGL(k_conv_patch_pack_x6, dim3(stream_blocks(total)), dim3(256), 0, s, w, wp, G, M, Cg, T, CPH, G8,
+                     RLH, BMc, tiles_m, ktiles, total);
+  int rc = launch_status("conv weight pack x6");
+  if (rc) return rc;
+#define RRAM_P(KH_, CPH_, PD_)                                                                           \
+  if (KH == KH_ && CPH == CPH_ && PD == PD_)                                                             \
+    rc = MI == 3 ? launch_patch_x6<KH_, CPH_, 3, PD_>(P, wp, PW, CS, G, s)                               \
+                 : launch_patch_x6<KH_, CPH_, 4, PD_>(P, wp, PW, CS, G, s);                              \
+  else
+  RRAM_P(5, 1, 4) RRAM_P(5, 1, 8) RRAM_P(5, 1, 12)
+  RRAM_P(3, 4, 8) RRAM_P(3, 4, 12) RRAM_P(3, 4, 16)
+  RRAM_P(3, 2, 4) RRAM_P(3, 2, 8) RRAM_P(3, 2, 16)
+  return 0;
+#undef RRAM_P
+  return rc ? rc : 1;
+}
+
+}  // namespace rram

@@ -20,120 +20,16 @@
 
 #include <algorithm>
 #include <array>
-#include <atomic>
 #include <map>
 #include <mutex>
 #include <type_traits>
 #include <vector>
 
-#include "rram_common.hpp"
+#include "gemm_common.hpp"
 
 namespace rram {
 namespace {
 
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-typedef float floatx4 __attribute__((ext_vector_type(4)));
-
-// K-tile depth is a template parameter KB (16 or 32); LDS rows are padded to
-// KB + 4 floats (80 / 144 B: 16-B aligned, conflict-free ds_read_b128 for 16
-// consecutive rows).  BK is the split-K chunk granularity (multiple of both).
-constexpr int BK = 32;
-template <int KB>
-constexpr int ldk_of() { return KB + 4; }
-
-// KCV = KC with 16-byte global loads (row stride, base and K all multiples of 4 floats)
-// CONVT = CONV with a per-k offset/tap table (conv_table below) read by scalar
-// loads: no (c, kh, kw) stepping and no multiplies in the gather.
-// CONVT64: the same with a 64-bit tap mask (kh*kw <= 63, e.g. 7 x 7 with padding)
-// KCU = KC with 16-byte raw buffer loads at any 4-byte alignment (row stride K
-// not a multiple of 4, e.g. AlexNet conv1 K = 363): a float4 may run into the
-// next row (or past the buffer end, where the per-dword range check returns
-// 0); the elements at k >= K are zeroed when the tile is written to LDS.
-enum Mode : int { KC = 0, RC = 1, CONV = 2, NCHW = 3, NCHWT = 4, KCV = 5, CONVT = 6, CONVT64 = 7, KCU = 8 };
-enum OutMode : int { OUT_ROWMAJOR = 0, OUT_NCHW = 1 };
-
-// Fast unsigned division by a runtime constant (x < 2^31).
-struct FastDiv {
-  uint32_t d, m, s;
-};
-static FastDiv make_fastdiv(uint32_t d) {
-  FastDiv f{d, 0, 0};
-  if (d <= 1) {
-    f.m = 0;
-    f.s = 0;
-    return f;
-  }
-  uint32_t s = 0;
-  while ((1ull << s) < d) ++s;
-  f.s = s;
-  f.m = static_cast<uint32_t>(((1ull << 32) * ((1ull << s) - d)) / d + 1);
-  return f;
-}
-// d == 1 is encoded as m = 0, s = 0, so no branch is needed
-__device__ __forceinline__ uint32_t fdiv(uint32_t x, const FastDiv& f) {
-  const uint32_t t = __umulhi(x, f.m);
-  return (t + x) >> f.s;
-}
-
-// Operand view: element (row, k).
-struct View {
-  const float* p;
-  int64_t ld;        // KC: row stride; RC: k stride; NCHW(T): channel stride (= HW)
-  int64_t img;       // NCHW/NCHWT/CONV: image stride
-  int rows, kdim;    // logical extent
-  FastDiv hw;        // NCHW/NCHWT: spatial size
-};
-
-struct ConvGeom {
-  int C, H, W, KH, KW, ph, pw, sh, sw, dh, dw, Ho, Wo;
-  FastDiv khkw, kw_div, howo, wo_div;
-  int64_t chw;  // image stride of the input (C*H*W)
-  int in_bytes; // bytes addressable from the group's input base (buffer range)
-  const int2* tbl;  // CONVT: per k {4*(c*H*W + kh*dh*W + kw*dw), tap}; tap 31 = never valid
-  int taps;         // CONVT: kh*kw taps tracked in the per-column validity mask (0: pad-free)
-};
-
-struct Epi {
-  float* C;
-  int64_t ldc;       // ROWMAJOR: row stride; NCHW: channel stride (= HW)
-  int64_t cimg;      // NCHW: image stride (Cout*HW)
-  FastDiv hw;        // NCHW: spatial size
-  float alpha, beta;
-  const float* bias;
-  int bias_mode;
-  int relu;
-};
-
-struct Params {
-  View a, b;
-  ConvGeom cv;
-  Epi e;
-  int M, N, K;
-  int k_chunk;               // split-K chunk length (multiple of BK)
-  float* ws;                 // split-K partials [split][M][N] (nullptr: direct)
-  int64_t grp_a, grp_b, grp_c;  // per-group pointer offsets (z = group)
-  int64_t grp_bias;
-  int split;                 // number of K splits (z = split when > 1)
-  int tiles_m, tiles_n, tiles_z;
-};
-
-// Per-thread constant data of the B loader for the CONV view.
-struct ConvCol {
-  int64_t base;  // image offset of this thread's column (n*C*H*W)
-  int hb, wb;    // ho*sh - ph, wo*sw - pw
-  bool valid;
-  int pbase;     // n*C*H*W + hb*W + wb (element offset inside the group's input)
-  __amdgpu_buffer_rsrc_t rsrc;  // raw buffer over the group's input (OOB loads return 0)
-  uint32_t bad;     // CONVT: bit t set = tap t of this column reads padding (bit 31 always set)
-  uint32_t bad_hi;  // CONVT64: taps 32..63 (bit 63 always set)
-};
-
-template <int ROWS, int KB>
-struct Loader {
-  static constexpr int EPT = ROWS * KB / 256;
-  float v[EPT];
-  int kn[EPT / 4 > 0 ? EPT / 4 : 1];  // KCU: valid elements of float4 i (K - k, may be <= 0 or >= 4)
-};
 
 // Branch-free guarded loads: an out-of-range element loads from the view's
 // base (always valid) and is replaced by 0, so the load stream has no
@@ -141,7 +37,6 @@ struct Loader {
 // The guard selects the ADDRESS (a 16-byte zero block for out-of-range
 // elements), never the loaded value: a select on the value would force an
 // s_waitcnt right after the load and serialise the prefetch behind it.
-__device__ __attribute__((aligned(16))) float g_zero4[4] = {0.f, 0.f, 0.f, 0.f};
 __device__ __forceinline__ float ld_guard(const float* p, int64_t off, bool ok) {
   return *(ok ? p + off : g_zero4);
 }
@@ -381,101 +276,6 @@ __device__ __forceinline__ void store_tile(const Loader<ROWS, KB>& L, float* lds
   }
 }
 
-__device__ __forceinline__ float pick(const float4& q, int s) {
-  return (s & 3) == 0 ? q.x : (s & 3) == 1 ? q.y : (s & 3) == 2 ? q.z : q.w;
-}
-
-// Epilogue of one wave's MI x NI tiles of 32x32 (v_mfma_f32_32x32x2_f32
-// accumulator layout): acc[i][j][r] -> row = mwave + 32 i + (r&3) + 8*(r>>2) + 4*lh,
-// col = nwave + 32 j + lr.  Shared by k_gemm and k_gemm2.
-template <int MI, int NI, int OM>
-__device__ __forceinline__ void gemm_epilogue(floatx16 (&acc)[MI][NI], const Params& P, const Epi& ep, float* part,
-                                              int mwave, int nwave, int lr, int lh) {
-  // Every mode flag is block-uniform, so each loop below is free of
-  // per-element waits: bias values are fetched with address selects (a select
-  // on a loaded value makes the compiler branch around each load and wait for
-  // it: one L2 round trip per output element), alpha and the row bias are
-  // folded into the accumulators once per row, and only edge tiles mask rows.
-  const int mw = mwave + 4 * lh;                       // this lane's first row
-  const bool rows_full = mwave + MI * 32 <= P.M;
-  if (part != nullptr) {                               // split-K partial slab [M][N]
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int n = nwave + j * 32 + lr;
-      if (n >= P.N) continue;
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = mw + i * 32 + (r & 3) + 8 * (r >> 2);
-          if (rows_full || m < P.M) part[(int64_t)m * P.N + n] = acc[i][j][r];
-        }
-    }
-    return;
-  }
-  const bool row_bias = ep.bias_mode == RRAM_BIAS_ROW, col_bias = ep.bias_mode == RRAM_BIAS_COL;
-  const bool relu = ep.relu != 0;
-  const float alpha = ep.alpha, beta = ep.beta;
-  if (beta == 0.0f) {
-    // o = alpha*v + bias: one bias load per row, shared by the NI column tiles
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = mw + i * 32 + (r & 3) + 8 * (r >> 2);
-        const float b = *((row_bias && m < P.M) ? ep.bias + m : g_zero4);
-#pragma unroll
-        for (int j = 0; j < NI; ++j) acc[i][j][r] = alpha * acc[i][j][r] + b;
-      }
-  }
-#pragma unroll
-  for (int j = 0; j < NI; ++j) {
-    const int n = nwave + j * 32 + lr;
-    if (n >= P.N) continue;
-    const float cb = *(col_bias ? ep.bias + n : g_zero4);
-    float* cj;
-    if (OM == OUT_NCHW) {
-      const uint32_t im = fdiv(static_cast<uint32_t>(n), ep.hw);
-      const uint32_t sp = static_cast<uint32_t>(n) - im * ep.hw.d;
-      cj = ep.C + (int64_t)im * ep.cimg + sp;
-    } else {
-      cj = ep.C + n;
-    }
-    const int64_t ld = ep.ldc;
-    if (beta != 0.0f) {
-      // accumulate into C (backward GEMMs): ((alpha*v) + beta*C) + bias
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = mw + i * 32 + (r & 3) + 8 * (r >> 2);
-          if (!rows_full && m >= P.M) continue;
-          float* dst = cj + (int64_t)m * ld;
-          float o = alpha * acc[i][j][r] + beta * *dst;
-          o += *(row_bias ? ep.bias + m : g_zero4) + cb;
-          *dst = relu ? fmaxf(o, 0.0f) : o;
-        }
-    } else if (rows_full) {
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = mw + i * 32 + (r & 3) + 8 * (r >> 2);
-          const float o = acc[i][j][r] + cb;
-          cj[(int64_t)m * ld] = relu ? fmaxf(o, 0.0f) : o;
-        }
-    } else {
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = mw + i * 32 + (r & 3) + 8 * (r >> 2);
-          const float o = acc[i][j][r] + cb;
-          if (m < P.M) cj[(int64_t)m * ld] = relu ? fmaxf(o, 0.0f) : o;
-        }
-    }
-  }
-}
 
 // Occupancy target 4 waves per SIMD: the 128 x 128 / KB = 16 conv tile then
 // keeps its accumulators in VGPRs (116 VGPRs, no AGPRs, no spills) instead of
@@ -793,34 +593,6 @@ constexpr int stage_fl() { return A_FL + b_fl<BMODE>(); }
 template <int BMODE>
 constexpr int vm_per_tile() { return 4 + (BMODE == CONVT ? 16 : 4); }
 
-typedef int int4v __attribute__((ext_vector_type(4)));
-
-// Raw buffer descriptor as four SGPR words (base, stride 0, byte range, raw
-// untyped dword format): offsets at or past the range load zeros.
-__device__ __forceinline__ int4v make_rsrc(const float* p, uint32_t range) {
-  const uint64_t a = reinterpret_cast<uint64_t>(p);
-  int4v r;
-  r.x = static_cast<int>(static_cast<uint32_t>(a));
-  r.y = static_cast<int>(static_cast<uint32_t>(a >> 32) & 0xFFFFu);
-  r.z = static_cast<int>(range);
-  r.w = 0x00020000;
-  return r;
-}
-// LDS-DMA loads (buffer_load ... lds) in inline asm: the compiler then neither
-// drains the ring with vmcnt(0) before every ds_read (it cannot tell the DMA
-// destination from the stage being read) nor demotes the uniform table loads
-// to vector loads.  Their completion is tracked by hand (wait_vm + barrier).
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-__device__ __forceinline__ void dma_b128(const int4v& rs, uint32_t voff, uint32_t lds) {
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs), "s"(lds)
-               : "m0");
-}
-__device__ __forceinline__ void dma_b32(const int4v& rs, uint32_t voff, uint32_t lds) {
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dword %0, %1, 0 offen lds" ::"v"(voff), "s"(rs), "s"(lds)
-               : "m0");
-}
-#pragma clang diagnostic pop
 
 // Loader of a K-contiguous operand (rows x k): this lane's byte offset of row
 // r = 32 w + 8 i + (lane >> 3) for piece i (bit 31 set when the row is out of
@@ -907,13 +679,6 @@ __device__ __forceinline__ int2 tentry(const int16v& v, int kk) {
   return make_int2(v[2 * kk], v[2 * kk + 1]);
 }
 
-// wait until at most N of this wave's vector-memory operations (LDS-DMA
-// included) are outstanding
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  static_assert(N >= 0 && N <= 63, "vmcnt range");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
 
 // fragments of one K-half (8 k-steps) of a wave's 64 x 64 tile
 template <int BMODE>
@@ -1135,7 +900,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))
 // K order: lane half h at step s = (cc, kh, kw) uses input channel
 // kt*2CPH + h*CPH + cc and tap (kh, kw), in A and B alike.
 namespace cp {
-constexpr int BN = 128, NST = 3;
+constexpr int BN = 128;
 template <int KH, int KW, int CPH>
 struct Shape {
   static constexpr int T = KH * KW;
@@ -1397,331 +1162,6 @@ __global__ void __launch_bounds__(256) k_conv_patch_pack(const float* __restrict
     if (h < 2 && u < CPH * T && m < M) {
       const int c = kt * 2 * CPH + h * CPH + u / T;
       v = w[((int64_t)g * M + m) * C * T + (int64_t)c * T + (u % T)];
-    }
-    out[idx] = v;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// k_conv_patch_x6: the patch convolution with each fp32 product formed on the
-// bf16 matrix cores.  Every fp32 operand is split exactly into three bf16
-// terms, x = xh + xm + xl (round-to-nearest at each step; the remainders are
-// exact in fp32 and the third term holds the last 8 significand bits), and
-// a*b is accumulated in fp32 as the six terms
-//   al*bh + ah*bl + am*bm + am*bh + ah*bm + ah*bh
-// (v_mfma_f32_32x32x16_bf16: a product of two bf16 is exact in fp32).  The
-// dropped terms am*bl, al*bm, al*bl are below 2^-25 |a*b| with independent
-// signs, under the fp32 rounding of the accumulation itself, so the result
-// carries fp32 accuracy (tests compare it with a float64 evaluation at the
-// same bound as the fp32-MFMA kernels) while a 32x32x16 bf16 MFMA does the
-// work of eight 32x32x2 fp32 MFMAs in half their cycles: six of them cost
-// 192 cycles where the fp32 form of the same 32x32x16 block costs 512.
-// The weights are split once per call by the repack kernel (three bf16
-// planes, fragment order); the activations are split in registers after the
-// LDS reads of the patch (4-5 VALU per element, hidden between MFMAs).
-// K order: a K-tile holds 2 CPH input channels (half h: channels
-// kt*2CPH + h*CPH + cc) x KH*KW taps = S steps per half, padded to G8 groups
-// of 8; MFMA group g takes steps 8g .. 8g+7 of both halves (lane half h holds
-// k = 8h + j of the 32x32x16 operand).  Padded steps have zero weights and
-// read no activations.
-namespace x6 {
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef float float2v __attribute__((ext_vector_type(2)));
-struct Parts {
-  bf16x8 h, m, l;
-};
-// exact three-term split of 8 floats (round to nearest even at each step)
-__device__ __forceinline__ void split8(const float (&x)[8], Parts& r) {
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const float2v v = {x[2 * p], x[2 * p + 1]};
-    const bf16x2 h = __builtin_convertvector(v, bf16x2);
-    const float2v r1 = v - __builtin_convertvector(h, float2v);
-    const bf16x2 m = __builtin_convertvector(r1, bf16x2);
-    const float2v r2 = r1 - __builtin_convertvector(m, float2v);
-    const bf16x2 l = __builtin_convertvector(r2, bf16x2);
-    r.h[2 * p] = h[0];
-    r.h[2 * p + 1] = h[1];
-    r.m[2 * p] = m[0];
-    r.m[2 * p + 1] = m[1];
-    r.l[2 * p] = l[0];
-    r.l[2 * p + 1] = l[1];
-  }
-}
-// term p (0 = high, 1 = middle, 2 = low) of the split of v, as bf16 bits
-__device__ __forceinline__ uint16_t split_term(float v, int p) {
-  const __bf16 h = static_cast<__bf16>(v);
-  const float r1 = v - static_cast<float>(h);
-  const __bf16 m = static_cast<__bf16>(r1);
-  const __bf16 l = static_cast<__bf16>(r1 - static_cast<float>(m));
-  const __bf16 t = p == 0 ? h : p == 1 ? m : l;
-  return __builtin_bit_cast(uint16_t, t);
-}
-__device__ __forceinline__ floatx16 mfma6(const Parts& a, const Parts& b, floatx16 c) {
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.l, b.h, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.l, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, b.m, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, b.h, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.m, c, 0, 0, 0);
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.h, c, 0, 0, 0);
-}
-template <int KH, int KW, int CPH>
-struct Shape {
-  static constexpr int T = KH * KW;
-  static constexpr int S = CPH * T;         // steps per half
-  static constexpr int G8 = (S + 7) / 8;    // MFMA groups per K-tile
-  static constexpr int RLB = G8 * 96 + 16;  // bytes per packed weight row ([g][half][term][8 bf16] + pad: RLB/16 odd)
-};
-constexpr int BM = 128, BN = 256;  // workgroup tile
-}  // namespace x6
-
-template <int KH, int KW, int CPH, int PD>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
-k_conv_patch_x6(Params P, const uint16_t* __restrict__ wpack, int PW, int CS) {
-  using namespace g2;
-  using Sh = x6::Shape<KH, KW, CPH>;
-  // 128 x 256 tile; wave w owns all 128 rows x columns 64 w .. 64 w + 63, so
-  // the B split (the VALU of the main loop) is shared by four row blocks and
-  // each weight byte staged in LDS feeds 256 columns
-  constexpr int BMc = x6::BM, BNc = x6::BN, MI = 4;
-  constexpr int A_B = BMc * Sh::RLB;                    // weight slab bytes per K-tile
-  constexpr int A_DMA = ((A_B + 1023) / 1024 + 3) / 4;  // 1 KB pieces per wave
-  constexpr int A_REGB = A_DMA * 4 * 1024;
-  constexpr int SFB = A_REGB + PD * 4 * 64 * 4;         // stage bytes (weights + patch)
-  constexpr int NVM = A_DMA + PD;
-  constexpr int G8 = Sh::G8;
-  static_assert(2 * SFB <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) char smem[2 * SFB];
-  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem));
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lr = lane & 31, lh = lane >> 5;
-
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, loc = bid >> 3;
-  const int q8 = nwg >> 3, r8 = nwg & 7;
-  const int tid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
-  const int tm = __builtin_amdgcn_readfirstlane(tid % P.tiles_m);
-  const int tn = __builtin_amdgcn_readfirstlane((tid / P.tiles_m) % P.tiles_n);
-  const int z = __builtin_amdgcn_readfirstlane(tid / (P.tiles_m * P.tiles_n));
-  const int n0 = tn * BNc;
-  const int m0 = tm * BMc;
-
-  const ConvGeom& cv = P.cv;
-  const int HW = cv.howo.d, OW = cv.wo_div.d;
-  const int ktiles = cv.C / (2 * CPH);
-  const float* xin = P.b.p + z * P.grp_b;
-  Epi ep = P.e;
-  if (z > 0) {
-    ep.C += z * P.grp_c;
-    if (ep.bias) ep.bias += z * P.grp_bias;
-  }
-  const uint16_t* abase = wpack + ((int64_t)z * P.tiles_m + tm) * ktiles * (A_B / 2);
-  const int4v arsrc = make_rsrc(reinterpret_cast<const float*>(abase), static_cast<uint32_t>((int64_t)ktiles * A_B));
-  uint32_t aoff[A_DMA];
-#pragma unroll
-  for (int i = 0; i < A_DMA; ++i) {
-    const int f = ((wave * A_DMA + i) * 64 + lane) * 16;
-    aoff[i] = f < A_B ? static_cast<uint32_t>(f) : 0x80000000u;
-  }
-
-  // patch: positions n0 .. plast cover images img0 .. img0 + nseg - 1 (<= 3);
-  // segment s holds output rows f_s .. l_s of its image plus the KH - 1 halo,
-  // at patch rows p_s .. p_{s+1} - 1
-  const int plast = min(n0 + BNc, P.N) - 1;
-  const int img0 = n0 / HW, nseg = plast / HW - img0 + 1;
-  const int f0 = (n0 - img0 * HW) / OW;
-  auto seg_last = [&](int s) { return s == nseg - 1 ? (plast - (img0 + s) * HW) / OW : cv.Ho - 1; };
-  const int p1 = seg_last(0) - f0 + KH;
-  const int p2 = p1 + (nseg > 1 ? seg_last(1) + KH : 0);
-  const int R = p2 + (nseg > 2 ? seg_last(2) + KH : 0);
-  const int4v xrsrc = make_rsrc(xin, static_cast<uint32_t>(cv.in_bytes));
-  const uint32_t HW4 = static_cast<uint32_t>(cv.H * cv.W * 4);
-  uint32_t poff[PD];
-#pragma unroll
-  for (int i = 0; i < PD; ++i) {
-    const int f = (wave * PD + i) * 64 + lane;
-    const int ch = f / CS, w = f - ch * CS;
-    const int prow = w / PW, pcol = w - prow * PW;
-    uint32_t off = 0x80000000u;
-    if (ch < 2 * CPH && prow < R) {
-      const int sg = prow >= p2 ? 2 : prow >= p1 ? 1 : 0;
-      const int y = (sg == 0 ? f0 + prow : prow - (sg == 1 ? p1 : p2)) - cv.ph;
-      const int x = pcol - cv.pw;
-      if (y >= 0 && y < cv.H && x >= 0 && x < cv.W)
-        off = static_cast<uint32_t>((int64_t)(img0 + sg) * cv.chw * 4) + static_cast<uint32_t>(ch) * HW4 +
-              static_cast<uint32_t>((y * cv.W + x) * 4);
-    }
-    poff[i] = off;
-  }
-  int pb[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int n = min(n0 + wave * 64 + j * 32 + lr, plast);
-    const int img = n / HW, sp = n - img * HW;
-    const int oh = sp / OW, ow = sp - oh * OW;
-    const int sg = img - img0;
-    const int prow = sg == 0 ? oh - f0 : (sg == 1 ? p1 : p2) + oh;
-    pb[j] = prow * PW + ow + lh * CPH * CS;
-  }
-
-  floatx16 acc[MI][2];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-
-  auto issue = [&](int kt, int stg, int e) {  // DMA item e of K-tile kt into stage stg
-    const uint32_t img = lds0 + static_cast<uint32_t>(stg * SFB);
-    if (e < A_DMA) {
-      dma_b128(arsrc, aoff[e] + static_cast<uint32_t>(kt * A_B), img + static_cast<uint32_t>((wave * A_DMA + e) * 1024));
-    } else {
-      const int i = e - A_DMA;
-      dma_b32(xrsrc, poff[i] + static_cast<uint32_t>(kt * 2 * CPH) * HW4,
-              img + static_cast<uint32_t>(A_REGB + (wave * PD + i) * 64 * 4));
-    }
-  };
-  struct Fr {
-    x6::bf16x8 a[MI][3];  // this lane's 8 k of rows 32 i + lr: high, middle, low terms
-    float b[2][8];        // raw activations of columns j
-    x6::Parts bp[2];      // their split
-  };
-  auto read_a = [&](Fr& F, const char* st, int g, int i) {
-    const char* p = st + (i * 32 + lr) * Sh::RLB + (g * 2 + lh) * 48;
-#pragma unroll
-    for (int t = 0; t < 3; ++t) F.a[i][t] = *reinterpret_cast<const x6::bf16x8*>(p + 16 * t);
-  };
-  auto read_b = [&](Fr& F, const char* st, int g) {
-    const float* pt = reinterpret_cast<const float*>(st + A_REGB);
-#pragma unroll
-    for (int jj = 0; jj < 8; ++jj) {
-      const int sx = 8 * g + jj;
-      if (sx < Sh::S) {
-        const int cc = sx / Sh::T, tp = sx - cc * Sh::T, kh = tp / KW, kw = tp - kh * KW;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) F.b[j][jj] = pt[pb[j] + cc * CS + kh * PW + kw];
-      } else {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) F.b[j][jj] = 0.0f;
-      }
-    }
-  };
-
-  const int nt = ktiles;  // >= 1 (host)
-  // fragments ping-pong between F[0] and F[1] by group parity (compile-time
-  // indices, no register copies); with an odd group count tiles go in pairs
-  Fr F[2];
-#pragma unroll
-  for (int e = 0; e < NVM; ++e) issue(0, 0, e);
-  wait_vm<0>();
-  __builtin_amdgcn_s_barrier();
-#pragma unroll
-  for (int i = 0; i < MI; ++i) read_a(F[0], smem, 0, i);
-  read_b(F[0], smem, 0);
-#pragma unroll
-  for (int j = 0; j < 2; ++j) x6::split8(F[0].b[j], F[0].bp[j]);
-
-  // one K-tile; PAR: parity of its first group's fragments; MORE: tile t + 1 exists
-  auto tile = [&](int t, auto par_c, auto more_c) {
-    constexpr int PAR = decltype(par_c)::value;
-    constexpr bool MORE = decltype(more_c)::value;
-    const char* cur = smem + (t & 1) * SFB;
-    const char* nxt = smem + ((t + 1) & 1) * SFB;
-#pragma unroll
-    for (int g = 0; g < G8; ++g) {
-      Fr& fc = F[(g + PAR) & 1];
-      Fr& fn = F[(g + 1 + PAR) & 1];
-      const bool last = g == G8 - 1;
-      // the next group's fragments: this tile's group g + 1, or group 0 of
-      // tile t + 1 once its DMA has landed (wait + barrier: every wave is then
-      // also done reading the stage the next DMA overwrites)
-      if (last && MORE) {
-        wait_vm<0>();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      const bool rd = !last || MORE;
-      const char* src = last ? nxt : cur;
-      const int gn = last ? 0 : g + 1;
-      constexpr int NB = 2 * MI;  // MFMA blocks (6 MFMAs each) of a group
-#pragma unroll
-      for (int q = 0; q < NB; ++q) {
-        const int i = q >> 1, j = q & 1;
-        acc[i][j] = x6::mfma6(x6::Parts{fc.a[i][0], fc.a[i][1], fc.a[i][2]}, fc.bp[j], acc[i][j]);
-        if (rd) {
-          if (q == 0) read_b(fn, src, gn);
-          if (q >= 1 && q <= MI) read_a(fn, src, gn, q - 1);
-          if (q == NB - 3) x6::split8(fn.b[0], fn.bp[0]);
-          if (q == NB - 1) x6::split8(fn.b[1], fn.bp[1]);
-        }
-        // DMA of tile t + 1 spread over the blocks of groups 0 .. G8-2
-        if (!last && MORE) {
-          constexpr int SL = (G8 - 1) * NB;
-          const int sl = g * NB + q;
-#pragma unroll
-          for (int e = 0; e < NVM; ++e)
-            if ((e * SL) / NVM == sl) issue(t + 1, (t + 1) & 1, e);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  };
-  using T_ = std::true_type;
-  using F_ = std::false_type;
-  using P0 = std::integral_constant<int, 0>;
-  using P1 = std::integral_constant<int, 1>;
-  if constexpr (G8 % 2 == 0) {
-    int t = 0;
-    for (; t + 1 < nt; ++t) tile(t, P0{}, T_{});
-    tile(t, P0{}, F_{});
-  } else {
-    int t = 0;
-    for (; t + 2 < nt; t += 2) {
-      tile(t, P0{}, T_{});
-      tile(t + 1, P1{}, T_{});
-    }
-    if (t + 1 < nt) {
-      tile(t, P0{}, T_{});
-      tile(t + 1, P1{}, F_{});
-    } else {
-      tile(t, P0{}, F_{});
-    }
-  }
-  gemm_epilogue<MI, 2, OUT_NCHW>(acc, P, ep, nullptr, m0, n0 + wave * 64, lr, lh);
-}
-
-// Weight repack for k_conv_patch_x6: w [G*M][C*T] -> bf16 terms
-// [G][tiles_m][ktiles][64 MI][RLB/2]: row = [group g][half h][term][8 steps] + pad.
-__global__ void __launch_bounds__(256) k_conv_patch_pack_x6(const float* __restrict__ w, uint16_t* __restrict__ out,
-                                                            int G, int M, int C, int T, int CPH, int G8, int RLH,
-                                                            int BMc, int tiles_m, int ktiles, int64_t total) {
-  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    int64_t r = idx;
-    const int col = static_cast<int>(r % RLH);
-    r /= RLH;
-    const int row = static_cast<int>(r % BMc);
-    r /= BMc;
-    const int kt = static_cast<int>(r % ktiles);
-    r /= ktiles;
-    const int tm = static_cast<int>(r % tiles_m);
-    const int g = static_cast<int>(r / tiles_m);
-    const int m = tm * BMc + row;
-    uint16_t v = 0;
-    if (col < G8 * 48 && m < M) {
-      const int gg = col / 48, rem = col - gg * 48;
-      const int h = rem / 24, p = (rem - h * 24) / 8, j = rem & 7;
-      const int s = 8 * gg + j;
-      if (s < CPH * T) {
-        const int c = kt * 2 * CPH + h * CPH + s / T;
-        v = x6::split_term(w[((int64_t)g * M + m) * C * T + (int64_t)c * T + (s % T)], p);
-      }
     }
     out[idx] = v;
   }
@@ -2017,32 +1457,6 @@ bool vec_ok(const float* p, int64_t ld, int K, int64_t grp = 0) {
   return (reinterpret_cast<uintptr_t>(p) & 15u) == 0 && (ld & 3) == 0 && (K & 3) == 0 && (grp & 3) == 0;
 }
 
-Epi make_epi(float* C, int64_t ldc, float alpha, float beta, const float* bias, int bias_mode,
-             int relu) {
-  Epi e{};
-  e.C = C;
-  e.ldc = ldc;
-  e.cimg = 0;
-  e.hw = make_fastdiv(1);
-  e.alpha = alpha;
-  e.beta = beta;
-  e.bias = bias;
-  e.bias_mode = bias ? bias_mode : RRAM_BIAS_NONE;
-  e.relu = relu;
-  return e;
-}
-
-View make_view(const float* p, int64_t ld, int rows, int kdim) {
-  View v{};
-  v.p = p;
-  v.ld = ld;
-  v.img = 0;
-  v.rows = rows;
-  v.kdim = kdim;
-  v.hw = make_fastdiv(1);
-  return v;
-}
-
 // Per-geometry gather table of the CONVT loader, built once per process and
 // cached (a few KB per conv geometry; never freed).  Entry k < K holds the
 // input offset of reduction index k = (c, kh, kw) in bytes and its tap
@@ -2172,6 +1586,9 @@ std::map<std::pair<int, hipStream_t>, std::pair<float*, size_t>>& pack_cache() {
   static std::map<std::pair<int, hipStream_t>, std::pair<float*, size_t>> cache;
   return cache;
 }
+int conv_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const float* bias, float* y, int relu,
+                hipStream_t s);
+
 float* pack_buffer(size_t floats, hipStream_t s) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
@@ -2222,95 +1639,6 @@ int launch_patch(Params P, const float* wpack, int PW, int CS, int gz, hipStream
   return launch_status("conv patch");
 }
 
-// most patch rows (output rows + KH - 1 halo per image segment) any BN-position
-// tile of an OH x OW output needs; -1 when a tile spans more than maxseg images
-int patch_rows(int N, int HW, int OW, int OH, int KH, int BN, int maxseg) {
-  int rmax = 0;
-  for (int n0 = 0; n0 < N; n0 += BN) {
-    const int pl = std::min(n0 + BN, N) - 1;
-    const int i0 = n0 / HW, i1 = pl / HW;
-    if (i1 - i0 + 1 > maxseg) return -1;
-    int r = 0;
-    for (int i = i0; i <= i1; ++i) {
-      const int f = i == i0 ? (n0 - i0 * HW) / OW : 0;
-      const int l = i == i1 ? (pl - i1 * HW) / OW : OH - 1;
-      r += l - f + KH;
-    }
-    rmax = std::max(rmax, r);
-  }
-  return rmax;
-}
-
-template <int KH, int CPH, int PD>
-int launch_patch_x6(Params P, const uint16_t* wpack, int PW, int CS, int gz, hipStream_t s) {
-  P.tiles_m = (P.M + x6::BM - 1) / x6::BM;
-  P.tiles_n = (P.N + x6::BN - 1) / x6::BN;
-  P.tiles_z = gz;
-  const int64_t nwg = (int64_t)P.tiles_m * P.tiles_n * gz;
-  RRAM_REQUIRE(nwg < (1ll << 31), "conv: grid too large");
-  hipLaunchKernelGGL((k_conv_patch_x6<KH, KH, CPH, PD>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, P, wpack,
-                     PW, CS);
-  return launch_status("conv patch x6");
-}
-
-// k_conv_patch_x6 (fp32 products on the bf16 matrix cores, see the kernel):
-// stride-1 undilated 3x3 / 5x5 convolutions with >= 128 positions per output
-// plane and <= 1/8 padded rows in the 128-row M tiles.  Returns 1 when it ran,
-// 0 when not covered, < 0 on error.  RRAM_CONV_X6 = 0 keeps the fp32-MFMA kernels.
-std::atomic<int>& conv_engine() {
-  static std::atomic<int> eng{[] {
-    const char* e = getenv("RRAM_CONV_X6");
-    return (e && atoi(e) == 0) ? static_cast<int>(RRAM_ENGINE_F32) : static_cast<int>(RRAM_ENGINE_BF16X6);
-  }()};
-  return eng;
-}
-
-int conv_patch_x6_fwd(const rram_conv_desc* d, const float* w, Params& P, hipStream_t s) {
-  if (conv_engine().load(std::memory_order_relaxed) != RRAM_ENGINE_BF16X6) return 0;
-  const int KH = d->kernel_h, KW = d->kernel_w;
-  if (d->stride_h != 1 || d->stride_w != 1 || d->dilation_h != 1 || d->dilation_w != 1) return 0;
-  if (!((KH == 3 && KW == 3) || (KH == 5 && KW == 5))) return 0;
-  const int G = d->group, Cg = d->channels / G, M = d->num_output / G;
-  const int HW = d->out_h * d->out_w, OW = d->out_w, OH = d->out_h;
-  const int CPH = KH == 5 ? 1 : (Cg % 8 == 0 ? 4 : 2);
-  if (HW < 128 || Cg == 0 || Cg % (2 * CPH) != 0) return 0;
-  if ((reinterpret_cast<uintptr_t>(w) & 3u) != 0) return 0;
-  const int mt = (M + x6::BM - 1) / x6::BM * x6::BM;
-  if ((mt - M) * 8 > mt) return 0;
-  const int rmax = patch_rows(P.N, HW, OW, OH, KH, x6::BN, 3);
-  if (rmax < 0) return 0;
-  const int PW = d->width + 2 * d->pad_w;
-  // channel stride >= rmax * PW with CPH * CS = 32 (mod 64): the two lane
-  // halves read disjoint bank halves
-  int CS = rmax * PW;
-  while ((CPH * CS) % 64 != 32) ++CS;
-  const int need = (2 * CPH * CS + 255) / 256;  // 256-float patch pieces
-  static const int pd5[] = {4, 6, 8, 12}, pd3q[] = {8, 12, 14, 16}, pd3h[] = {4, 8, 12, 16};
-  const int* pds = KH == 5 ? pd5 : CPH == 4 ? pd3q : pd3h;
-  int PD = 0;
-  for (int i = 3; i >= 0; --i)
-    if (pds[i] >= need) PD = pds[i];
-  if (PD == 0) return 0;
-  const int T = KH * KW, S = CPH * T, G8 = (S + 7) / 8, RLH = (G8 * 96 + 16) / 2;
-  const int BMc = x6::BM, tiles_m = mt / BMc, ktiles = Cg / (2 * CPH);
-  const int64_t total = (int64_t)G * tiles_m * ktiles * BMc * RLH;
-  RRAM_REQUIRE(total * 2 < (1ll << 31), "conv: packed weights must be < 2 GiB");
-  uint16_t* wp = reinterpret_cast<uint16_t*>(pack_buffer(static_cast<size_t>((total + 1) / 2), s));
-  RRAM_REQUIRE(wp != nullptr, "conv: packed-weight buffer allocation failed");
-  hipLaunchKernelGGL(k_conv_patch_pack_x6, dim3(stream_blocks(total)), dim3(256), 0, s, w, wp, G, M, Cg, T, CPH, G8,
-                     RLH, BMc, tiles_m, ktiles, total);
-  int rc = launch_status("conv weight pack x6");
-  if (rc) return rc;
-#define RRAM_P(KH_, CPH_, PD_) \
-  if (KH == KH_ && CPH == CPH_ && PD == PD_) rc = launch_patch_x6<KH_, CPH_, PD_>(P, wp, PW, CS, G, s); else
-  RRAM_P(5, 1, 4) RRAM_P(5, 1, 6) RRAM_P(5, 1, 8) RRAM_P(5, 1, 12)
-  RRAM_P(3, 4, 8) RRAM_P(3, 4, 12) RRAM_P(3, 4, 14) RRAM_P(3, 4, 16)
-  RRAM_P(3, 2, 4) RRAM_P(3, 2, 8) RRAM_P(3, 2, 12) RRAM_P(3, 2, 16)
-  return 0;
-#undef RRAM_P
-  return rc ? rc : 1;
-}
-
 // k_conv_patch for a stride-1, undilated 3x3 / 5x5 convolution whose output
 // planes hold >= 128 positions.  Returns 1 when it ran, 0 when the shape is
 // not covered (the caller falls back to the implicit-im2col GEMM), < 0 on
@@ -2321,10 +1649,6 @@ int conv_patch_fwd(const rram_conv_desc* d, const float* w, Params& P, hipStream
     return !(e && atoi(e) == 0);
   }();
   if (!on) return 0;
-  {
-    const int rc = conv_patch_x6_fwd(d, w, P, s);
-    if (rc != 0) return rc;
-  }
   const int KH = d->kernel_h, KW = d->kernel_w;
   if (d->stride_h != 1 || d->stride_w != 1 || d->dilation_h != 1 || d->dilation_w != 1) return 0;
   if (!((KH == 3 && KW == 3) || (KH == 5 && KW == 5))) return 0;
@@ -2382,6 +1706,10 @@ int conv_patch_fwd(const rram_conv_desc* d, const float* w, Params& P, hipStream
 
 int conv_fwd_core(const rram_conv_desc* d, const float* x, const float* w, const float* bias,
                   float* y, int relu, hipStream_t s) {
+  {
+    const int rc = conv_x6_fwd(d, x, w, bias, y, relu, s);  // conv_x6.hip
+    if (rc != 0) return rc < 0 ? rc : RRAM_OK;
+  }
   const int g = d->group;
   const int cin_g = d->channels / g, cout_g = d->num_output / g;
   const int K = cin_g * d->kernel_h * d->kernel_w;
