@@ -274,19 +274,21 @@ int rram_conv_out_shape(rram_conv_desc* d);
 int rram_conv2d_fwd(const rram_conv_desc* d, const float* x, const float* w,
                     const float* bias, float* y, int relu, rram_stream_t stream);
 
-/* Matrix-core engine of the fp32 convolution forward (no reference
+/* Matrix-core engine of the fp32 forward contractions (no reference
  * counterpart: the reference's engine is cuBLAS SGEMM, math_functions.cu:13-27).
- *   RRAM_ENGINE_F32   v_mfma_f32_32x32x2_f32 (fp32 operands).
+ *   RRAM_ENGINE_F32    v_mfma_f32_32x32x2_f32 (fp32 operands).
  *   RRAM_ENGINE_BF16X6 (default) each fp32 operand split exactly into three
- *                     bf16 terms, six cross products accumulated in fp32 on
- *                     v_mfma_f32_32x32x16_bf16 (fp32-accurate products, ~2x
- *                     the fp32 matrix-core rate); used by the stride-1 3x3 /
- *                     5x5 convolutions, the others stay on RRAM_ENGINE_F32.
- * The initial value comes from RRAM_CONV_X6 (0 = F32).  Returns the previous
+ *                      bf16 terms, six cross products accumulated in fp32 on
+ *                      v_mfma_f32_32x32x16_bf16 (fp32-accurate products, ~2x
+ *                      the fp32 matrix-core rate).  Used by the stride-1
+ *                      3x3 / 5x5 convolution forward and the InnerProduct /
+ *                      NoTrans x Trans GEMM forward (rram_ip_fwd); every
+ *                      other contraction stays on RRAM_ENGINE_F32.
+ * The initial value comes from RRAM_X6 (0 = F32).  Returns the previous
  * engine, or RRAM_EINVAL for an unknown one. */
 enum { RRAM_ENGINE_F32 = 0, RRAM_ENGINE_BF16X6 = 1 };
-int rram_set_conv_engine(int engine);
-int rram_get_conv_engine(void);
+int rram_set_f32_engine(int engine);
+int rram_get_f32_engine(void);
 
 /* Bytes of device workspace the backward passes need for `images_per_chunk`
  * images (explicit im2col/col2im buffer). */

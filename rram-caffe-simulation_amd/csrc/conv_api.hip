@@ -23,7 +23,7 @@ int col2im_core(const float* col, int64_t ldcol, int nimg, const rram_conv_desc*
 int gemv_core(int trans, int M, int N, float alpha, const float* A, const float* x, float beta,
               float* y, hipStream_t s);
 int release_conv_tables();
-std::atomic<int>& conv_engine();
+std::atomic<int>& f32_engine();
 
 namespace {
 
@@ -105,12 +105,12 @@ extern "C" {
 
 int rram_release_caches(void) { return rram::release_conv_tables(); }
 
-int rram_set_conv_engine(int engine) {
+int rram_set_f32_engine(int engine) {
   RRAM_REQUIRE(engine == RRAM_ENGINE_F32 || engine == RRAM_ENGINE_BF16X6, "conv engine: unknown engine");
-  return rram::conv_engine().exchange(engine);
+  return rram::f32_engine().exchange(engine);
 }
 
-int rram_get_conv_engine(void) { return rram::conv_engine().load(); }
+int rram_get_f32_engine(void) { return rram::f32_engine().load(); }
 
 int rram_gemm_f32_ex(int trans_a, int trans_b, int M, int N, int K, float alpha, const float* A,
                      int lda, const float* B, int ldb, float beta, float* C, int ldc,

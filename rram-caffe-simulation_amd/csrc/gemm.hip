@@ -1167,25 +1167,6 @@ __global__ void __launch_bounds__(256) k_conv_patch_pack(const float* __restrict
   }
 }
 
-// split-K reduction + epilogue (row-major C only)
-__global__ void __launch_bounds__(256) k_splitk_reduce(const float* __restrict__ ws, int split, int M,
-                                                       int N, Epi ep) {
-  const int64_t total = (int64_t)M * N;
-  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    float s = 0.0f;
-    for (int z = 0; z < split; ++z) s += ws[(int64_t)z * total + idx];
-    const int m = static_cast<int>(idx / N);
-    const int n = static_cast<int>(idx - (int64_t)m * N);
-    float* dst = ep.C + (int64_t)m * ep.ldc + n;
-    float o = ep.alpha * s;
-    if (ep.beta != 0.0f) o += ep.beta * *dst;
-    if (ep.bias_mode == RRAM_BIAS_ROW) o += ep.bias[m];
-    else if (ep.bias_mode == RRAM_BIAS_COL) o += ep.bias[n];
-    if (ep.relu) o = fmaxf(o, 0.0f);
-    *dst = o;
-  }
-}
 
 // y = alpha * op(A) x + beta * y, one wave per output element row
 __global__ void __launch_bounds__(256) k_gemv(int trans, int M, int N, float alpha,
@@ -1519,6 +1500,10 @@ int release_conv_tables() {
 }
 
 // Shared by the C-ABI entry points in conv_api.hip.
+int gemm_x6_nt(int M, int N, int K, float alpha, const float* A, int lda, const float* B, int ldb, float beta,
+               float* C, int ldc, const float* bias, int bias_mode, int relu, void* ws, size_t ws_bytes,
+               hipStream_t s);
+
 int gemm_core(int trans_a, int trans_b, int M, int N, int K, float alpha, const float* A, int lda,
               const float* B, int ldb, float beta, float* C, int ldc, const float* bias,
               int bias_mode, int relu, void* ws, size_t ws_bytes, hipStream_t s) {
@@ -1529,6 +1514,10 @@ int gemm_core(int trans_a, int trans_b, int M, int N, int K, float alpha, const 
   RRAM_REQUIRE(ldc >= N, "gemm: ldc < N");
   RRAM_REQUIRE(trans_a ? lda >= M : lda >= K || K == 0, "gemm: lda too small");
   RRAM_REQUIRE(trans_b ? ldb >= K || K == 0 : ldb >= N, "gemm: ldb too small");
+  if (!trans_a && trans_b) {  // InnerProduct forward: the bf16x6 engine when it covers the shape
+    const int rc = gemm_x6_nt(M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, bias, bias_mode, relu, ws, ws_bytes, s);
+    if (rc != 0) return rc < 0 ? rc : RRAM_OK;
+  }
   Params P{};
   P.a = make_view(A, lda, M, K);
   P.b = make_view(B, ldb, N, K);
@@ -1707,7 +1696,7 @@ int conv_patch_fwd(const rram_conv_desc* d, const float* w, Params& P, hipStream
 int conv_fwd_core(const rram_conv_desc* d, const float* x, const float* w, const float* bias,
                   float* y, int relu, hipStream_t s) {
   {
-    const int rc = conv_x6_fwd(d, x, w, bias, y, relu, s);  // conv_x6.hip
+    const int rc = conv_x6_fwd(d, x, w, bias, y, relu, s);  // x6.hip
     if (rc != 0) return rc < 0 ? rc : RRAM_OK;
   }
   const int g = d->group;

@@ -1,5 +1,5 @@
 // Shared pieces of the fp32 GEMM / convolution kernels (gemm.hip) and the
-// bf16x6 convolution kernels (conv_x6.hip): operand views, convolution
+// bf16x6 convolution kernels (x6.hip): operand views, convolution
 // geometry, epilogue parameters, raw-buffer LDS-DMA helpers and the MFMA
 // 32x32 accumulator epilogue.  Included into an anonymous namespace by each
 // translation unit.
@@ -238,6 +238,26 @@ View make_view(const float* p, int64_t ld, int rows, int kdim) {
   v.kdim = kdim;
   v.hw = make_fastdiv(1);
   return v;
+}
+
+// split-K reduction + epilogue (row-major C only)
+__global__ void __launch_bounds__(256) k_splitk_reduce(const float* __restrict__ ws, int split, int M,
+                                                       int N, Epi ep) {
+  const int64_t total = (int64_t)M * N;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.0f;
+    for (int z = 0; z < split; ++z) s += ws[(int64_t)z * total + idx];
+    const int m = static_cast<int>(idx / N);
+    const int n = static_cast<int>(idx - (int64_t)m * N);
+    float* dst = ep.C + (int64_t)m * ep.ldc + n;
+    float o = ep.alpha * s;
+    if (ep.beta != 0.0f) o += ep.beta * *dst;
+    if (ep.bias_mode == RRAM_BIAS_ROW) o += ep.bias[m];
+    else if (ep.bias_mode == RRAM_BIAS_COL) o += ep.bias[n];
+    if (ep.relu) o = fmaxf(o, 0.0f);
+    *dst = o;
+  }
 }
 
 namespace g2 {

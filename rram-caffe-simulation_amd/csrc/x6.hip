@@ -337,6 +337,204 @@ __global__ void __launch_bounds__(256) k_conv_patch_pack_x6(const float* __restr
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// k_gemm_x6: C[M][N] = A[M][K] . B[N][K]^T (the InnerProduct forward,
+// inner_product_layer.cu:9-30, and any NoTrans x Trans GEMM) on the bf16
+// matrix cores with the same exact three-term split as k_conv_patch_x6.
+// A (the activations: M = images) is split once by k_pack_rows_x6 into K-tile
+// slabs of bf16 terms in fragment order; B (the weights, streamed from HBM
+// once per forward) is loaded fp32 by LDS-DMA and split in registers after
+// the LDS read.  Tile 32 MI x 256: wave w owns all rows x columns
+// 64 w .. 64 w + 63; K-tiles of 32 (two MFMA groups); split-K over z with
+// partial slabs reduced by k_splitk_reduce.
+// K order inside a K-tile: group g, lane half h holds k = 16 h + 8 g + j
+// (the B rows' 16-byte quads 4h + 2g + u, u = 0, 1, swizzled as k_gemm2).
+namespace gx6 {
+constexpr int BN = 256, KT = 32;
+constexpr int RLB = 2 * 96 + 16;  // packed A row bytes per K-tile ([g][h][term][8 bf16] + pad, RLB/16 odd)
+}  // namespace gx6
+
+template <int MI>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+k_gemm_x6(Params P, const uint16_t* __restrict__ apack, int ktiles_all, int ktc) {
+  using namespace g2;
+  constexpr int BMc = 32 * MI, BNc = gx6::BN, KT = gx6::KT;
+  constexpr int A_B = BMc * gx6::RLB;
+  constexpr int A_DMA = ((A_B + 1023) / 1024 + 3) / 4;
+  constexpr int A_REGB = A_DMA * 4 * 1024;
+  constexpr int B_DMA = BNc * KT * 4 / 1024 / 4;        // 1 KB pieces per wave (8)
+  constexpr int SFB = A_REGB + BNc * KT * 4;
+  constexpr int NVM = A_DMA + B_DMA;
+  static_assert(2 * SFB <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[2 * SFB];
+  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem));
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lr = lane & 31, lh = lane >> 5;
+
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, loc = bid >> 3;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int tid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const int tm = __builtin_amdgcn_readfirstlane(tid % P.tiles_m);
+  const int tn = __builtin_amdgcn_readfirstlane((tid / P.tiles_m) % P.tiles_n);
+  const int z = __builtin_amdgcn_readfirstlane(tid / (P.tiles_m * P.tiles_n));
+  const int n0 = tn * BNc, m0 = tm * BMc;
+  const int kt0 = z * ktc;
+  const int nt = min(ktiles_all, kt0 + ktc) - kt0;  // >= 1 (host)
+  float* part = P.split > 1 ? P.ws + (int64_t)z * P.M * P.N : nullptr;
+
+  const uint16_t* abase = apack + ((int64_t)tm * ktiles_all + kt0) * (A_B / 2);
+  const int4v arsrc = make_rsrc(reinterpret_cast<const float*>(abase), static_cast<uint32_t>((int64_t)nt * A_B));
+  uint32_t aoff[A_DMA];
+#pragma unroll
+  for (int i = 0; i < A_DMA; ++i) {
+    const int f = ((wave * A_DMA + i) * 64 + lane) * 16;
+    aoff[i] = f < A_B ? static_cast<uint32_t>(f) : 0x80000000u;
+  }
+  // B rows n0 + 64 w + 8 i + (lane >> 3), quad lane & 7 (stored swizzled)
+  const View& vb = P.b;
+  const int4v brsrc = make_rsrc(vb.p, static_cast<uint32_t>(((int64_t)(vb.rows - 1) * vb.ld + vb.kdim) * 4));
+  uint32_t boff[B_DMA];
+  int bkq[B_DMA];
+#pragma unroll
+  for (int i = 0; i < B_DMA; ++i) {
+    const int r = 64 * wave + 8 * i + (lane >> 3);
+    const int q = (lane & 7) ^ ((r >> 1) & 7);
+    boff[i] = n0 + r < vb.rows ? static_cast<uint32_t>((int64_t)(n0 + r) * vb.ld * 4) : 0x80000000u;
+    bkq[i] = 4 * q;
+  }
+  const int kend = P.K;
+
+  floatx16 acc[MI][2];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+  auto issue = [&](int t, int stg, int e) {  // DMA item e of local K-tile t into stage stg
+    const uint32_t img = lds0 + static_cast<uint32_t>(stg * SFB);
+    if (e < A_DMA) {
+      dma_b128(arsrc, aoff[e] + static_cast<uint32_t>(t * A_B), img + static_cast<uint32_t>((wave * A_DMA + e) * 1024));
+    } else {
+      const int i = e - A_DMA;
+      const int k = (kt0 + t) * KT + bkq[i];
+      const uint32_t off = (boff[i] + static_cast<uint32_t>(k) * 4u) | (k < kend ? 0u : 0x80000000u);
+      dma_b128(brsrc, off, img + static_cast<uint32_t>(A_REGB + (64 * wave + 8 * i) * KT * 4));
+    }
+  };
+  struct Fr {
+    x6::bf16x8 a[MI][3];
+    float b[2][8];
+    x6::Parts bp[2];
+  };
+  auto read_a = [&](Fr& F, const char* st, int g, int i) {
+    const char* p = st + (i * 32 + lr) * gx6::RLB + (g * 2 + lh) * 48;
+#pragma unroll
+    for (int t = 0; t < 3; ++t) F.a[i][t] = *reinterpret_cast<const x6::bf16x8*>(p + 16 * t);
+  };
+  auto read_b = [&](Fr& F, const char* st, int g) {
+    const float* bs = reinterpret_cast<const float*>(st + A_REGB);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = 64 * wave + 32 * j + lr;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const float4 q = *reinterpret_cast<const float4*>(bs + n * KT + (((4 * lh + 2 * g + u) ^ ((n >> 1) & 7)) << 2));
+        F.b[j][4 * u] = q.x;
+        F.b[j][4 * u + 1] = q.y;
+        F.b[j][4 * u + 2] = q.z;
+        F.b[j][4 * u + 3] = q.w;
+      }
+    }
+  };
+
+  Fr F[2];
+#pragma unroll
+  for (int e = 0; e < NVM; ++e) issue(0, 0, e);
+  wait_vm<0>();
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int i = 0; i < MI; ++i) read_a(F[0], smem, 0, i);
+  read_b(F[0], smem, 0);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) x6::split8(F[0].b[j], F[0].bp[j]);
+
+  auto tile = [&](int t, auto more_c) {
+    constexpr bool MORE = decltype(more_c)::value;
+    const char* cur = smem + (t & 1) * SFB;
+    const char* nxt = smem + ((t + 1) & 1) * SFB;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      Fr& fc = F[g];
+      Fr& fn = F[g ^ 1];
+      const bool last = g == 1;
+      if (last && MORE) {
+        wait_vm<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      const bool rd = !last || MORE;
+      const char* src = last ? nxt : cur;
+      const int gn = last ? 0 : 1;
+      constexpr int NB = 2 * MI;
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        const int i = q >> 1, j = q & 1;
+        acc[i][j] = x6::mfma6(x6::Parts{fc.a[i][0], fc.a[i][1], fc.a[i][2]}, fc.bp[j], acc[i][j]);
+        if (rd) {
+          if (q == 0) read_b(fn, src, gn);
+          if (q >= 1 && q <= MI) read_a(fn, src, gn, q - 1);
+          if (q == NB - 3) x6::split8(fn.b[0], fn.bp[0]);
+          if (q == NB - 1) x6::split8(fn.b[1], fn.bp[1]);
+        }
+        if (!last && MORE) {
+#pragma unroll
+          for (int e = 0; e < NVM; ++e)
+            if ((e * NB) / NVM == q) issue(t + 1, (t + 1) & 1, e);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+  int t = 0;
+  for (; t + 1 < nt; ++t) tile(t, std::true_type{});
+  tile(t, std::false_type{});
+  gemm_epilogue<MI, 2, OUT_ROWMAJOR>(acc, P, P.e, part, m0, n0 + wave * 64, lr, lh);
+}
+
+// A [M][lda] fp32 -> K-tile slabs of bf16 terms [tiles_m][ktiles][32 MI][RLB/2]
+// for k_gemm_x6 (zero past M and K)
+__global__ void __launch_bounds__(256) k_pack_rows_x6(const float* __restrict__ a, int64_t lda, int M, int K,
+                                                      uint16_t* __restrict__ out, int BMc, int ktiles, int64_t total) {
+  constexpr int RLH = gx6::RLB / 2;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = idx;
+    const int col = static_cast<int>(r % RLH);
+    r /= RLH;
+    const int row = static_cast<int>(r % BMc);
+    r /= BMc;
+    const int kt = static_cast<int>(r % ktiles);
+    const int tm = static_cast<int>(r / ktiles);
+    const int m = tm * BMc + row;
+    uint16_t v = 0;
+    if (col < 96 && m < M) {
+      const int g = col / 48, rem = col - g * 48;
+      const int h = rem / 24, p = (rem - h * 24) / 8, j = rem & 7;
+      const int k = kt * gx6::KT + 16 * h + 8 * g + j;
+      if (k < K) v = x6::split_term(a[(int64_t)m * lda + k], p);
+    }
+    out[idx] = v;
+  }
+}
+
 }  // namespace
 
 float* pack_buffer(size_t floats, hipStream_t s);  // gemm.hip
@@ -372,10 +570,10 @@ int launch_patch_x6(Params P, const uint16_t* wpack, int PW, int CS, int gz, hip
   return launch_status("conv patch x6");
 }
 
-// engine of the stride-1 3x3 / 5x5 convolutions (rram_set_conv_engine)
-std::atomic<int>& conv_engine() {
+// engine of the stride-1 3x3 / 5x5 convolutions (rram_set_f32_engine)
+std::atomic<int>& f32_engine() {
   static std::atomic<int> eng{[] {
-    const char* e = getenv("RRAM_CONV_X6");
+    const char* e = getenv("RRAM_X6");
     return (e && atoi(e) == 0) ? static_cast<int>(RRAM_ENGINE_F32) : static_cast<int>(RRAM_ENGINE_BF16X6);
   }()};
   return eng;
@@ -384,10 +582,10 @@ std::atomic<int>& conv_engine() {
 // k_conv_patch_x6 (fp32 products on the bf16 matrix cores, see the kernel):
 // stride-1 undilated 3x3 / 5x5 convolutions with >= 128 positions per output
 // plane and <= 1/8 padded rows in the 96- or 128-row M tiles.  Returns 1 when it ran,
-// 0 when not covered, < 0 on error.  RRAM_CONV_X6 = 0 keeps the fp32-MFMA kernels.
+// 0 when not covered, < 0 on error.  RRAM_X6 = 0 keeps the fp32-MFMA kernels.
 int conv_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const float* bias, float* y, int relu,
                 hipStream_t s) {
-  if (conv_engine().load(std::memory_order_relaxed) != RRAM_ENGINE_BF16X6) return 0;
+  if (f32_engine().load(std::memory_order_relaxed) != RRAM_ENGINE_BF16X6) return 0;
   const int KH = d->kernel_h, KW = d->kernel_w;
   if (d->stride_h != 1 || d->stride_w != 1 || d->dilation_h != 1 || d->dilation_w != 1) return 0;
   if (!((KH == 3 && KW == 3) || (KH == 5 && KW == 5))) return 0;
@@ -464,6 +662,69 @@ int conv_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const f
   return 0;
 #undef RRAM_P
   return rc ? rc : 1;
+}
+
+
+// k_gemm_x6 for C = act(alpha * A . B^T + bias) with A [M][lda], B [N][ldb]
+// row-major fp32 (16-byte aligned rows), beta = 0.  Returns 1 when it ran, 0
+// when not covered (the caller runs the fp32-MFMA GEMM), < 0 on error.
+int gemm_x6_nt(int M, int N, int K, float alpha, const float* A, int lda, const float* B, int ldb, float beta,
+               float* C, int ldc, const float* bias, int bias_mode, int relu, void* ws, size_t ws_bytes,
+               hipStream_t s) {
+  if (f32_engine().load(std::memory_order_relaxed) != RRAM_ENGINE_BF16X6) return 0;
+  if (beta != 0.0f || K < 256 || (int64_t)M * N * K < (1ll << 24)) return 0;
+  auto al16 = [](const void* p, int ld) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0 && ld % 4 == 0; };
+  if (!al16(A, lda) || !al16(B, ldb) || K % 4 != 0) return 0;
+  if ((int64_t)(N - 1) * ldb * 4 + (int64_t)K * 4 >= (1ll << 32)) return 0;  // 32-bit buffer offsets
+  // M tile 128 or 96 rows, whichever pads less
+  const int t128 = (M + 127) / 128 * 128, t96 = (M + 95) / 96 * 96;
+  const int MI = (t96 - M) < (t128 - M) ? 3 : 4;
+  const int BMc = 32 * MI, tiles_m = (M + BMc - 1) / BMc, tiles_n = (N + gx6::BN - 1) / gx6::BN;
+  const int ktiles = (K + gx6::KT - 1) / gx6::KT;
+  // split-K toward 256 workgroups, >= 8 K-tiles (256 k) per split
+  const int64_t tiles = (int64_t)tiles_m * tiles_n;
+  int split = 1;
+  if (ws != nullptr && tiles < 256) {
+    split = static_cast<int>(std::min<int64_t>(16, 256 / tiles));
+    while (split > 1 && ktiles / split < 8) --split;
+    while (split > 1 && (size_t)split * M * N * sizeof(float) > ws_bytes) --split;
+  }
+  const int ktc = (ktiles + split - 1) / split;
+  split = (ktiles + ktc - 1) / ktc;
+  if (tiles * split < 192) return 0;  // under ~3/4 of the CUs busy: the fp32 kernel's smaller tiles fill more
+  const int64_t total = (int64_t)tiles_m * ktiles * BMc * (gx6::RLB / 2);
+  if (total * 2 >= (1ll << 31)) return 0;
+  uint16_t* ap = reinterpret_cast<uint16_t*>(pack_buffer(static_cast<size_t>((total + 1) / 2), s));
+  RRAM_REQUIRE(ap != nullptr, "gemm x6: packed-operand buffer allocation failed");
+  hipLaunchKernelGGL(k_pack_rows_x6, dim3(stream_blocks(total)), dim3(256), 0, s, A, (int64_t)lda, M, K, ap, BMc,
+                     ktiles, total);
+  int rc = launch_status("gemm x6 pack");
+  if (rc) return rc;
+  Params P{};
+  P.M = M;
+  P.N = N;
+  P.K = K;
+  P.b = make_view(B, ldb, N, K);
+  P.e = make_epi(C, ldc, alpha, 0.0f, bias, bias_mode, relu);
+  P.split = split;
+  P.ws = split > 1 ? static_cast<float*>(ws) : nullptr;
+  P.tiles_m = tiles_m;
+  P.tiles_n = tiles_n;
+  P.tiles_z = split;
+  const unsigned nwg = static_cast<unsigned>(tiles * split);
+  if (MI == 3)
+    hipLaunchKernelGGL((k_gemm_x6<3>), dim3(nwg), dim3(256), 0, s, P, ap, ktiles, ktc);
+  else
+    hipLaunchKernelGGL((k_gemm_x6<4>), dim3(nwg), dim3(256), 0, s, P, ap, ktiles, ktc);
+  rc = launch_status("gemm x6");
+  if (rc) return rc;
+  if (split > 1) {
+    hipLaunchKernelGGL(k_splitk_reduce, dim3(stream_blocks((int64_t)M * N)), dim3(256), 0, s, P.ws, split, M, N,
+                       P.e);
+    rc = launch_status("gemm x6 splitk reduce");
+    if (rc) return rc;
+  }
+  return 1;
 }
 
 }  // namespace rram

@@ -160,17 +160,17 @@ def conv_desc(x_shape, num_output, kernel, stride=1, pad=0, dilation=1, group=1)
 ENGINE_F32, ENGINE_BF16X6 = 0, 1
 
 
-def set_conv_engine(engine):
+def set_f32_engine(engine):
     """Matrix-core engine of the stride-1 3x3 / 5x5 convolution forward
-    (rram_set_conv_engine); returns the previous one."""
-    prev = _lib().rram_set_conv_engine(int(engine))
+    (rram_set_f32_engine); returns the previous one."""
+    prev = _lib().rram_set_f32_engine(int(engine))
     if prev < 0:
-        K.check(prev, "set_conv_engine")
+        K.check(prev, "set_f32_engine")
     return prev
 
 
-def get_conv_engine():
-    return _lib().rram_get_conv_engine()
+def get_f32_engine():
+    return _lib().rram_get_f32_engine()
 
 
 def conv2d_fwd(d, x, w, bias, y, relu=False):

@@ -1,12 +1,13 @@
 #!/bin/bash
-# A/B of the bf16x6 patch convolution: parity tests on the conv kernels, then
-# the bench with per-layer times with the x6 path off and on.
+# A/B of the bf16x6 engine: the GPU parity suite, then the bench with
+# per-layer times with the engine off (RRAM_X6=0) and on.
 set -o pipefail
 O=gpurun_out/x6
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_configs.py -m gpu -x -q --timeout 300 --timeout-method thread -k "conv or c3_" > $O/pytest.log 2>&1
-rc=$?; tail -15 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q -rP --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > $O/pytest.log 2>&1
+rc=$?; tail -3 $O/pytest.log; [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED" $O/pytest.log | head -20; exit $rc; }
+grep "bf16x6 .*e-" $O/pytest.log | head -8
 for x in 0 1; do
-  RRAM_CONV_X6=$x timeout -k 10 300 python bench.py --no-cpu-baseline --profile-layers > $O/bench_$x.json 2> $O/layers_$x.txt || exit 1
+  RRAM_X6=$x timeout -k 10 300 python bench.py --no-cpu-baseline --profile-layers > $O/bench_$x.json 2> $O/layers_$x.txt || exit 1
   cut -c1-200 $O/bench_$x.json
 done

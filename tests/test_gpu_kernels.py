@@ -454,12 +454,12 @@ PATCH_CASES = [
 @pytest.fixture(params=["f32", "bf16x6"])
 def conv_engine(request):
     """Runs a test under each matrix-core engine of the convolution forward
-    (rram_set_conv_engine) and restores the previous one."""
+    (rram_set_f32_engine) and restores the previous one."""
     from rramsim import ops
     eng = ops.ENGINE_F32 if request.param == "f32" else ops.ENGINE_BF16X6
-    prev = ops.set_conv_engine(eng)
+    prev = ops.set_f32_engine(eng)
     yield request.param
-    ops.set_conv_engine(prev)
+    ops.set_f32_engine(prev)
 
 
 @pytest.mark.parametrize("cs", PATCH_CASES)
@@ -506,17 +506,17 @@ def test_conv_engine_bf16x6_accuracy_vs_f32(device, cs):
     d = ops.conv_desc(cs["x"], cs["cout"], cs["k"], 1, cs["p"], 1, cs["g"])
     ref, scale = conv64(x, w, b, 1, cs["p"], cs["g"])
     err = {}
-    prev = ops.get_conv_engine()
+    prev = ops.get_f32_engine()
     try:
         for eng in (ops.ENGINE_F32, ops.ENGINE_BF16X6):
-            ops.set_conv_engine(eng)
+            ops.set_f32_engine(eng)
             y = torch.empty((cs["x"][0], cs["cout"], d.out_h, d.out_w), device=device)
             ops.conv2d_fwd(d, T(x, device), T(w, device), T(b, device), y)
             torch.cuda.synchronize()
             r = np.abs(N(y).astype(np.float64) - ref) / scale
             err[eng] = (float(r.max()), float(r.mean()))
     finally:
-        ops.set_conv_engine(prev)
+        ops.set_f32_engine(prev)
     f32, x6 = err[ops.ENGINE_F32], err[ops.ENGINE_BF16X6]
     print(f"{cs}: max/mean err / Σ|a·b|: f32 {f32[0]:.2e}/{f32[1]:.2e}  bf16x6 {x6[0]:.2e}/{x6[1]:.2e}")
     assert x6[0] < 1e-6 and f32[0] < 1e-6          # fp32 level (the test bound is 1e-4)
