@@ -4,13 +4,16 @@
 One step = one fault map on every rank: inject a fresh stuck-at fault map into
 the clean InnerProduct weights (counter-based RNG, HBM-bound kernel), then run
 the full AlexNet forward over the 256-image eval batch (implicit-GEMM conv and
-IP GEMMs on fp32 MFMA, LRN/pool/softmax/accuracy), accumulating accuracy and
+IP GEMMs with fp32 products on the matrix cores — fp32 MFMA, or the exact
+bf16x6 split for the 3x3 / 5x5 convolutions and fc6/fc7 —,
+LRN/pool/softmax/accuracy), accumulating accuracy and
 loss on the device.  Maps are sharded across ranks (map m on rank m mod N; no
 data-path collective); one RCCL all-reduce of the statistics closes the job.
 
 Prints ONE JSON line (rank 0):
   value = images classified under faults per second, summed over ranks
-  roofline = the conv/IP GEMMs (dominant kernels) vs the fp32 MFMA peak
+  roofline = the conv/IP contractions (dominant kernels) vs the peak of the
+             engine each runs on (fp32 MFMA, or the bf16x6 split: bf16 peak / 6)
   roofline_inject = the injection kernel vs HBM peak
   cpu_baseline = Caffe CPU mode restated in C (oracle/caffe_cpu.c: per-image
                  im2col + cblas_sgemm, Fail_cpu) over one full map, rank 0 at N=1.
@@ -31,6 +34,10 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "rram-caffe-simulation_amd" / "python"))
 
 MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: fp32 MFMA = fp32 vector peak (dense)
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: bf16 dense MFMA (no sparsity)
+# the bf16x6 engine (include/rram_kernels.h) spends 6 bf16 MFMA products per
+# fp32 product: its roofline is the bf16 dense peak / 6 in fp32 FLOPs
+MFMA_X6_PEAK_TFLOPS = MFMA_BF16_PEAK_TFLOPS / 6.0
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 
 
@@ -44,6 +51,20 @@ def alexnet_gemm_table(batch):
     for name, n, k in (("fc6", 4096, 9216), ("fc7", 4096, 4096), ("fc8", 1000, 4096)):
         t[name] = 2.0 * batch * n * k
     return t
+
+
+def alexnet_engines(batch):
+    """Engine each AlexNet conv / IP layer runs on (rram_f32_engine_for_*)."""
+    from rramsim import ops
+    convs = {"conv1": ((batch, 3, 227, 227), 96, 11, 4, 0, 1), "conv2": ((batch, 96, 27, 27), 256, 5, 1, 2, 2),
+             "conv3": ((batch, 256, 13, 13), 384, 3, 1, 1, 1), "conv4": ((batch, 384, 13, 13), 384, 3, 1, 1, 2),
+             "conv5": ((batch, 384, 13, 13), 256, 3, 1, 1, 2)}
+    eng = {}
+    for name, (x, co, k, st, pd, g) in convs.items():
+        eng[name] = ops.f32_engine_for_conv(ops.conv_desc(x, co, k, st, pd, 1, g))
+    for name, n, k in (("fc6", 4096, 9216), ("fc7", 4096, 4096), ("fc8", 1000, 4096)):
+        eng[name] = ops.f32_engine_for_ip(batch, n, k)
+    return {k: ("bf16x6" if v == ops.ENGINE_BF16X6 else "f32") for k, v in eng.items()}
 
 
 def cpu_baseline(batch, p_fault, seed):
@@ -163,9 +184,18 @@ def main():
     # ---- roofline from the live hipEvent layer timings of the timed region
     lt = net.layer_times()
     flops = alexnet_gemm_table(args.batch)
+    engines = alexnet_engines(args.batch)
     gemm_ms = sum(ms for (name, typ, ms, cnt) in lt if name in flops) / args.steps
     gemm_flops = sum(flops.values())
     achieved_tf = gemm_flops / (gemm_ms * 1e-3) / 1e12
+    # the roofline of the mixed-engine layer set: each layer's FLOPs at its
+    # engine's peak; effective peak = total FLOPs / that minimum time
+    peak_of = {"f32": MFMA_F32_PEAK_TFLOPS, "bf16x6": MFMA_X6_PEAK_TFLOPS}
+    t_min = sum(f / (peak_of[engines[n]] * 1e12) for n, f in flops.items())
+    peak_tf = gemm_flops / t_min / 1e12
+    layers = {name: {"engine": engines[name], "ms": round(ms / args.steps, 4),
+                     "tflops": round(flops[name] / (ms / args.steps * 1e-3) / 1e12, 1)}
+              for (name, typ, ms, cnt) in lt if name in flops}
     inj_ms, inj_n, inj_w = mc.inject_times()
     inj_ms_per = inj_ms / max(inj_n, 1)
     inj_gbps = 8.0 * inj_w / (inj_ms_per * 1e-3) / 1e9
@@ -195,12 +225,17 @@ def main():
         "config": {"workload": "alexnet_b256_mc_faultmap_inference", "model": "AlexNet (bvlc_alexnet train_val, TEST)",
                    "global_batch": args.batch * world, "batch_per_map": args.batch, "maps_per_step": world,
                    "p_fault": args.p_fault, "stuck_split_neg_zero_pos": [10, 20, 10],
-                   "fault_layers": "InnerProduct (58,631,144 weights)", "parallelism": f"mc-maps x{world} (RCCL stats all-reduce)"},
-        "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 2), "peak": MFMA_F32_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(achieved_tf / MFMA_F32_PEAK_TFLOPS, 4),
+                   "fault_layers": "InnerProduct (58,631,144 weights)", "parallelism": f"mc-maps x{world} (RCCL stats all-reduce)",
+                   "f32_engine": "bf16x6 (exact 3-term bf16 split, 6 products, fp32 accumulation)"
+                   if "bf16x6" in engines.values() else "f32 MFMA"},
+        "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 2), "peak": round(peak_tf, 1),
+                     "unit": "TFLOP/s", "frac": round(achieved_tf / peak_tf, 4),
                      "traffic": traffic.get("gemm", {}).get("bytes_per_step"),
-                     "kernel": "conv1-5 implicit-GEMM + fc6-8 GEMM (fp32 MFMA 32x32x2), per step",
-                     "algorithmic_flops_per_step": gemm_flops, "avg_ms_per_step": round(gemm_ms, 4)},
+                     "kernel": "conv1-5 + fc6-8 forward contractions per step; peak = each layer's engine peak "
+                               "(f32: v_mfma_f32_32x32x2_f32 157.3; bf16x6: bf16 dense 2500 / 6 products = 416.7)",
+                     "frac_of_f32_mfma_peak": round(achieved_tf / MFMA_F32_PEAK_TFLOPS, 4),
+                     "algorithmic_flops_per_step": gemm_flops, "avg_ms_per_step": round(gemm_ms, 4),
+                     "layers": layers},
         "roofline_inject": {"bound": "hbm", "achieved": round(inj_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                             "frac": round(inj_gbps / HBM_PEAK_GBPS, 4),
                             "traffic": traffic.get("inject", {}).get("bytes_per_launch"),

@@ -289,6 +289,10 @@ int rram_conv2d_fwd(const rram_conv_desc* d, const float* x, const float* w,
 enum { RRAM_ENGINE_F32 = 0, RRAM_ENGINE_BF16X6 = 1 };
 int rram_set_f32_engine(int engine);
 int rram_get_f32_engine(void);
+/* The engine rram_conv2d_fwd / rram_ip_fwd (transpose = 0, 16-byte aligned
+ * operands, workspace of ws_bytes) would use for this shape right now. */
+int rram_f32_engine_for_conv(const rram_conv_desc* d);
+int rram_f32_engine_for_ip(int M, int N, int K, size_t ws_bytes);
 
 /* Bytes of device workspace the backward passes need for `images_per_chunk`
  * images (explicit im2col/col2im buffer). */

@@ -583,22 +583,53 @@ std::atomic<int>& f32_engine() {
 // stride-1 undilated 3x3 / 5x5 convolutions with >= 128 positions per output
 // plane and <= 1/8 padded rows in the 96- or 128-row M tiles.  Returns 1 when it ran,
 // 0 when not covered, < 0 on error.  RRAM_X6 = 0 keeps the fp32-MFMA kernels.
+// shape plan of the x6 convolution (false: not covered)
+struct ConvPlan {
+  int CPH, MI, mt, PW, CS, PD;
+};
+bool conv_x6_plan(const rram_conv_desc* d, ConvPlan& pl) {
+  const int KH = d->kernel_h, KW = d->kernel_w;
+  if (d->stride_h != 1 || d->stride_w != 1 || d->dilation_h != 1 || d->dilation_w != 1) return false;
+  if (!((KH == 3 && KW == 3) || (KH == 5 && KW == 5))) return false;
+  const int G = d->group, Cg = d->channels / G, M = d->num_output / G;
+  const int HW = d->out_h * d->out_w, OW = d->out_w, OH = d->out_h;
+  pl.CPH = KH == 5 ? 1 : (Cg % 8 == 0 ? 4 : 2);
+  if (HW < 128 || Cg == 0 || Cg % (2 * pl.CPH) != 0) return false;
+  if ((int64_t)d->num * d->channels * d->height * d->width * 4 >= (1ll << 31)) return false;  // 32-bit offsets
+  // M tile 128 or 96 rows, whichever pads less (<= 1/8 padded rows)
+  const int t128 = (M + 127) / 128 * 128, t96 = (M + 95) / 96 * 96;
+  pl.MI = (t96 - M) < (t128 - M) ? 3 : 4;
+  pl.mt = pl.MI == 3 ? t96 : t128;
+  if ((pl.mt - M) * 8 > pl.mt) return false;
+  const int rmax = patch_rows(d->num * HW, HW, OW, OH, KH, x6::BN, 3);
+  if (rmax < 0) return false;
+  pl.PW = d->width + 2 * d->pad_w;
+  // channel stride >= rmax * PW with CPH * CS = 32 (mod 64): the two lane
+  // halves read disjoint bank halves
+  pl.CS = rmax * pl.PW;
+  while ((pl.CPH * pl.CS) % 64 != 32) ++pl.CS;
+  const int need = (2 * pl.CPH * pl.CS + 255) / 256;  // 256-float patch pieces
+  static const int pd5[] = {4, 8, 12}, pd3q[] = {8, 12, 16}, pd3h[] = {4, 8, 16};
+  const int* pds = KH == 5 ? pd5 : pl.CPH == 4 ? pd3q : pd3h;
+  pl.PD = 0;
+  for (int i = 2; i >= 0; --i)
+    if (pds[i] >= need) pl.PD = pds[i];
+  if (pl.PD == 0) return false;
+  const int64_t total = (int64_t)G * (pl.mt / (32 * pl.MI)) * (Cg / (2 * pl.CPH)) * 32 * pl.MI *
+                        (((KH * KW * pl.CPH + 7) / 8 * 96 + 16) / 2);
+  return total * 2 < (1ll << 31);
+}
+
 int conv_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const float* bias, float* y, int relu,
                 hipStream_t s) {
   if (f32_engine().load(std::memory_order_relaxed) != RRAM_ENGINE_BF16X6) return 0;
+  if ((reinterpret_cast<uintptr_t>(w) & 3u) != 0) return 0;
+  ConvPlan pl;
+  if (!conv_x6_plan(d, pl)) return 0;
   const int KH = d->kernel_h, KW = d->kernel_w;
-  if (d->stride_h != 1 || d->stride_w != 1 || d->dilation_h != 1 || d->dilation_w != 1) return 0;
-  if (!((KH == 3 && KW == 3) || (KH == 5 && KW == 5))) return 0;
   const int G = d->group, Cg = d->channels / G, M = d->num_output / G;
   const int HW = d->out_h * d->out_w, OW = d->out_w, OH = d->out_h;
-  const int CPH = KH == 5 ? 1 : (Cg % 8 == 0 ? 4 : 2);
-  if (HW < 128 || Cg == 0 || Cg % (2 * CPH) != 0) return 0;
-  if ((reinterpret_cast<uintptr_t>(w) & 3u) != 0) return 0;
-  // M tile 128 or 96 rows, whichever pads less (<= 1/8 padded rows)
-  const int t128 = (M + 127) / 128 * 128, t96 = (M + 95) / 96 * 96;
-  const int MI = (t96 - M) < (t128 - M) ? 3 : 4;
-  const int mt = MI == 3 ? t96 : t128;
-  if ((mt - M) * 8 > mt) return 0;
+  const int CPH = pl.CPH, MI = pl.MI, mt = pl.mt, PW = pl.PW, CS = pl.CS, PD = pl.PD;
   Params P{};
   P.M = M;
   P.N = d->num * HW;
@@ -619,7 +650,6 @@ int conv_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const f
   cv.howo = make_fastdiv(HW);
   cv.wo_div = make_fastdiv(OW);
   cv.chw = (int64_t)d->channels * d->height * d->width;
-  if ((int64_t)d->num * cv.chw * 4 >= (1ll << 31)) return 0;  // 32-bit buffer offsets
   cv.in_bytes = static_cast<int>((int64_t)d->num * cv.chw * 4);
   P.e = make_epi(y, HW, 1.0f, 0.0f, bias, RRAM_BIAS_ROW, relu);
   P.e.cimg = (int64_t)d->num_output * HW;
@@ -627,24 +657,9 @@ int conv_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const f
   P.grp_b = (int64_t)Cg * d->height * d->width;
   P.grp_c = (int64_t)M * HW;
   P.grp_bias = M;
-  const int rmax = patch_rows(P.N, HW, OW, OH, KH, x6::BN, 3);
-  if (rmax < 0) return 0;
-  const int PW = d->width + 2 * d->pad_w;
-  // channel stride >= rmax * PW with CPH * CS = 32 (mod 64): the two lane
-  // halves read disjoint bank halves
-  int CS = rmax * PW;
-  while ((CPH * CS) % 64 != 32) ++CS;
-  const int need = (2 * CPH * CS + 255) / 256;  // 256-float patch pieces
-  static const int pd5[] = {4, 8, 12}, pd3q[] = {8, 12, 16}, pd3h[] = {4, 8, 16};
-  const int* pds = KH == 5 ? pd5 : CPH == 4 ? pd3q : pd3h;
-  int PD = 0;
-  for (int i = 2; i >= 0; --i)
-    if (pds[i] >= need) PD = pds[i];
-  if (PD == 0) return 0;
   const int T = KH * KW, S = CPH * T, G8 = (S + 7) / 8, RLH = (G8 * 96 + 16) / 2;
   const int BMc = 32 * MI, tiles_m = mt / BMc, ktiles = Cg / (2 * CPH);
   const int64_t total = (int64_t)G * tiles_m * ktiles * BMc * RLH;
-  RRAM_REQUIRE(total * 2 < (1ll << 31), "conv: packed weights must be < 2 GiB");
   uint16_t* wp = reinterpret_cast<uint16_t*>(pack_buffer(static_cast<size_t>((total + 1) / 2), s));
   RRAM_REQUIRE(wp != nullptr, "conv: packed-weight buffer allocation failed");
   hipLaunchKernelGGL(k_conv_patch_pack_x6, dim3(stream_blocks(total)), dim3(256), 0, s, w, wp, G, M, Cg, T, CPH, G8,
@@ -665,35 +680,49 @@ int conv_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const f
 }
 
 
+// shape plan of the x6 GEMM (false: not covered)
+struct GemmPlan {
+  int MI, tiles_m, tiles_n, ktiles, split, ktc;
+};
+bool gemm_x6_plan(int M, int N, int K, size_t ws_bytes, GemmPlan& pl) {
+  if (K < 256 || K % 4 != 0 || (int64_t)M * N * K < (1ll << 24)) return false;
+  // M tile 128 or 96 rows, whichever pads less
+  const int t128 = (M + 127) / 128 * 128, t96 = (M + 95) / 96 * 96;
+  pl.MI = (t96 - M) < (t128 - M) ? 3 : 4;
+  const int BMc = 32 * pl.MI;
+  pl.tiles_m = (M + BMc - 1) / BMc;
+  pl.tiles_n = (N + gx6::BN - 1) / gx6::BN;
+  pl.ktiles = (K + gx6::KT - 1) / gx6::KT;
+  // split-K toward 256 workgroups, >= 8 K-tiles (256 k) per split
+  const int64_t tiles = (int64_t)pl.tiles_m * pl.tiles_n;
+  int split = 1;
+  if (ws_bytes > 0 && tiles < 256) {
+    split = static_cast<int>(std::min<int64_t>(16, 256 / tiles));
+    while (split > 1 && pl.ktiles / split < 8) --split;
+    while (split > 1 && (size_t)split * M * N * sizeof(float) > ws_bytes) --split;
+  }
+  pl.ktc = (pl.ktiles + split - 1) / split;
+  pl.split = (pl.ktiles + pl.ktc - 1) / pl.ktc;
+  if (tiles * pl.split < 192) return false;  // under ~3/4 of the CUs busy: the fp32 kernel's smaller tiles fill more
+  return (int64_t)pl.tiles_m * pl.ktiles * BMc * gx6::RLB < (1ll << 31);
+}
+
 // k_gemm_x6 for C = act(alpha * A . B^T + bias) with A [M][lda], B [N][ldb]
 // row-major fp32 (16-byte aligned rows), beta = 0.  Returns 1 when it ran, 0
 // when not covered (the caller runs the fp32-MFMA GEMM), < 0 on error.
 int gemm_x6_nt(int M, int N, int K, float alpha, const float* A, int lda, const float* B, int ldb, float beta,
                float* C, int ldc, const float* bias, int bias_mode, int relu, void* ws, size_t ws_bytes,
                hipStream_t s) {
-  if (f32_engine().load(std::memory_order_relaxed) != RRAM_ENGINE_BF16X6) return 0;
-  if (beta != 0.0f || K < 256 || (int64_t)M * N * K < (1ll << 24)) return 0;
+  if (f32_engine().load(std::memory_order_relaxed) != RRAM_ENGINE_BF16X6 || beta != 0.0f) return 0;
   auto al16 = [](const void* p, int ld) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0 && ld % 4 == 0; };
-  if (!al16(A, lda) || !al16(B, ldb) || K % 4 != 0) return 0;
+  if (!al16(A, lda) || !al16(B, ldb)) return 0;
   if ((int64_t)(N - 1) * ldb * 4 + (int64_t)K * 4 >= (1ll << 32)) return 0;  // 32-bit buffer offsets
-  // M tile 128 or 96 rows, whichever pads less
-  const int t128 = (M + 127) / 128 * 128, t96 = (M + 95) / 96 * 96;
-  const int MI = (t96 - M) < (t128 - M) ? 3 : 4;
-  const int BMc = 32 * MI, tiles_m = (M + BMc - 1) / BMc, tiles_n = (N + gx6::BN - 1) / gx6::BN;
-  const int ktiles = (K + gx6::KT - 1) / gx6::KT;
-  // split-K toward 256 workgroups, >= 8 K-tiles (256 k) per split
+  GemmPlan pl;
+  if (!gemm_x6_plan(M, N, K, ws != nullptr ? ws_bytes : 0, pl)) return 0;
+  const int MI = pl.MI, BMc = 32 * MI, tiles_m = pl.tiles_m, tiles_n = pl.tiles_n, ktiles = pl.ktiles;
+  const int split = pl.split, ktc = pl.ktc;
   const int64_t tiles = (int64_t)tiles_m * tiles_n;
-  int split = 1;
-  if (ws != nullptr && tiles < 256) {
-    split = static_cast<int>(std::min<int64_t>(16, 256 / tiles));
-    while (split > 1 && ktiles / split < 8) --split;
-    while (split > 1 && (size_t)split * M * N * sizeof(float) > ws_bytes) --split;
-  }
-  const int ktc = (ktiles + split - 1) / split;
-  split = (ktiles + ktc - 1) / ktc;
-  if (tiles * split < 192) return 0;  // under ~3/4 of the CUs busy: the fp32 kernel's smaller tiles fill more
   const int64_t total = (int64_t)tiles_m * ktiles * BMc * (gx6::RLB / 2);
-  if (total * 2 >= (1ll << 31)) return 0;
   uint16_t* ap = reinterpret_cast<uint16_t*>(pack_buffer(static_cast<size_t>((total + 1) / 2), s));
   RRAM_REQUIRE(ap != nullptr, "gemm x6: packed-operand buffer allocation failed");
   hipLaunchKernelGGL(k_pack_rows_x6, dim3(stream_blocks(total)), dim3(256), 0, s, A, (int64_t)lda, M, K, ap, BMc,
@@ -728,3 +757,22 @@ int gemm_x6_nt(int M, int N, int K, float alpha, const float* A, int lda, const 
 }
 
 }  // namespace rram
+
+extern "C" {
+
+int rram_f32_engine_for_conv(const rram_conv_desc* d) {
+  RRAM_REQUIRE(d != nullptr, "engine query: desc is NULL");
+  rram::ConvPlan pl;
+  return rram::f32_engine().load() == RRAM_ENGINE_BF16X6 && rram::conv_x6_plan(d, pl) ? RRAM_ENGINE_BF16X6
+                                                                                    : RRAM_ENGINE_F32;
+}
+
+int rram_f32_engine_for_ip(int M, int N, int K, size_t ws_bytes) {
+  RRAM_REQUIRE(M >= 0 && N >= 0 && K >= 0, "engine query: negative size");
+  rram::GemmPlan pl;
+  return rram::f32_engine().load() == RRAM_ENGINE_BF16X6 && rram::gemm_x6_plan(M, N, K, ws_bytes, pl)
+             ? RRAM_ENGINE_BF16X6
+             : RRAM_ENGINE_F32;
+}
+
+}  // extern "C"

@@ -173,6 +173,16 @@ def get_f32_engine():
     return _lib().rram_get_f32_engine()
 
 
+def f32_engine_for_conv(d):
+    """Engine rram_conv2d_fwd would use for this descriptor now."""
+    return _lib().rram_f32_engine_for_conv(C.byref(d))
+
+
+def f32_engine_for_ip(M, N, K, ws_bytes=256 << 20):
+    """Engine rram_ip_fwd (W [N][K], aligned operands) would use now."""
+    return _lib().rram_f32_engine_for_ip(int(M), int(N), int(K), int(ws_bytes))
+
+
 def conv2d_fwd(d, x, w, bias, y, relu=False):
     K.check(_lib().rram_conv2d_fwd(C.byref(d), _p(x), _p(w), _p(bias), _p(y), int(relu),
                                    _stream()), "conv2d_fwd")
