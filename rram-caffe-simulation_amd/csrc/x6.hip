@@ -306,6 +306,202 @@ k_conv_patch_x6(Params P, const uint16_t* __restrict__ wpack, int PW, int CS) {
   gemm_epilogue<MI, 2, OUT_NCHW>(acc, P, ep, nullptr, m0, n0 + wave * 64, lr, lh);
 }
 
+
+// ---------------------------------------------------------------------------
+// k_conv_wide_x6: a large-kernel, strided, unpadded convolution with few input
+// channels (AlexNet conv1: 3 x 11 x 11, stride 4, 96 filters) on the bf16x6
+// engine.  All input channels of a 256-position tile stay resident in LDS as
+// whole input rows (one contiguous block per image segment and channel,
+// copied by 16-byte LDS-DMA), so the im2col view is read from LDS with
+// immediate offsets; the pre-split weights stream through a 3-slot LDS ring,
+// one MFMA group (16 k) per slot.  Tile = 96 filters x 256 positions; wave w
+// owns all 96 rows x positions 64 w .. 64 w + 63.
+// K order: lane half h takes kernel rows 6h .. 6h + 5 (row 11 is a zero
+// weight row), item s = 8 g + j of group g is channel s / (6 KW), kernel row
+// 6h + (s / KW) % 6, column s % KW; so the two halves differ by a constant
+// 6 input rows and every B read is (channel base) + immediate.
+namespace wx6 {
+constexpr int BM = 96, BN = 256, NSLOT = 3;
+constexpr int SLOT_ROW = 112;                  // bytes per weight row of a group: [h][term][8 bf16] + pad (7 quads)
+constexpr int SLOT_B = BM * SLOT_ROW;          // 10752
+constexpr int SLOT_DMA = 3;                    // 1 KB pieces per wave per slot (12 KB >= SLOT_B)
+constexpr int SLOT_REGB = SLOT_DMA * 4 * 1024;
+template <int KH, int KW, int C>
+struct Shape {
+  static constexpr int HR = (KH + 1) / 2;      // kernel rows per lane half
+  static constexpr int S = C * HR * KW;        // items per half
+  static constexpr int G = (S + 7) / 8;        // MFMA groups
+};
+}  // namespace wx6
+
+template <int KH, int KW, int ST, int C, int PFL>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+k_conv_wide_x6(Params P, const uint16_t* __restrict__ wpack, int CHS) {
+  using namespace g2;
+  using Sh = wx6::Shape<KH, KW, C>;
+  constexpr int G = Sh::G, MI = 3;
+  constexpr int PATCH_B = PFL * 4;
+  static_assert(PATCH_B + wx6::NSLOT * wx6::SLOT_REGB <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[PATCH_B + wx6::NSLOT * wx6::SLOT_REGB];
+  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem));
+  const float* patch = reinterpret_cast<const float*>(smem);
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lr = lane & 31, lh = lane >> 5;
+  // XCD-grouped tile order
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, loc = bid >> 3;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int tn = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const int n0 = tn * wx6::BN;
+
+  const ConvGeom& cv = P.cv;
+  const int HW = cv.howo.d, OW = cv.wo_div.d, W = cv.W;
+  // image segments of positions n0 .. plast (<= 2): output rows f_s .. l_s,
+  // input rows f_s ST .. f_s ST + R_s - 1 (R_s = (l_s - f_s) ST + 2 HR)
+  const int plast = min(n0 + wx6::BN, P.N) - 1;
+  const int img0 = n0 / HW, img1 = plast / HW;
+  const int f0 = (n0 - img0 * HW) / OW;
+  const int l0 = img1 == img0 ? (plast - img0 * HW) / OW : cv.Ho - 1;
+  const int l1 = (plast - img1 * HW) / OW;
+  const int len0 = ((l0 - f0) * ST + 2 * Sh::HR) * W;
+  const int len1 = img1 == img0 ? 0 : (l1 * ST + 2 * Sh::HR) * W;
+  const int sb1 = (len0 + 255) / 256 * 256;    // LDS float offset of segment 1 in a channel block
+  const int np0 = (len0 + 255) / 256, np1 = (len1 + 255) / 256;
+  const int npc = np0 + np1;                   // 1 KB pieces per channel
+  const int4v xrsrc = make_rsrc(P.b.p, static_cast<uint32_t>(cv.in_bytes));
+  // patch DMA: piece p of channel c, spread over the waves
+  for (int q = wave; q < C * npc; q += 4) {
+    const int c = q / npc, p = q - c * npc;
+    const bool s1 = p >= np0;
+    const int pp = s1 ? p - np0 : p;
+    const int len = s1 ? len1 : len0;
+    const int64_t g0 = ((int64_t)((s1 ? img1 : img0) * C + c) * cv.H + (s1 ? 0 : f0 * ST)) * W;
+    const int e = pp * 256 + lane * 4;
+    const uint32_t off = e < len ? static_cast<uint32_t>((g0 + e) * 4) : 0x80000000u;
+    dma_b128(xrsrc, off, lds0 + static_cast<uint32_t>((c * CHS + (s1 ? sb1 : 0) + pp * 256) * 4));
+  }
+  // per-lane B bases: column j of this wave, channel c (floats)
+  int bb[2][C];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = min(n0 + wave * 64 + j * 32 + lr, plast);
+    const int img = n / HW, sp = n - img * HW;
+    const int oh = sp / OW, ow = sp - oh * OW;
+    const int pr = img == img0 ? (oh - f0) * ST : oh * ST;
+    const int pb = (img == img0 ? 0 : sb1) + (pr + lh * Sh::HR) * W + ow * ST;
+#pragma unroll
+    for (int c = 0; c < C; ++c) bb[j][c] = pb + c * CHS;
+  }
+  // weight ring: group g in slot g % NSLOT
+  const int4v arsrc = make_rsrc(reinterpret_cast<const float*>(wpack), static_cast<uint32_t>(G * wx6::SLOT_B));
+  auto issue_a = [&](int g) {
+    const uint32_t img = lds0 + static_cast<uint32_t>(PATCH_B + (g % wx6::NSLOT) * wx6::SLOT_REGB);
+#pragma unroll
+    for (int i = 0; i < wx6::SLOT_DMA; ++i) {
+      const int f = ((wave * wx6::SLOT_DMA + i) * 64 + lane) * 16;
+      const uint32_t off = f < wx6::SLOT_B ? static_cast<uint32_t>(g * wx6::SLOT_B + f) : 0x80000000u;
+      dma_b128(arsrc, off, img + static_cast<uint32_t>((wave * wx6::SLOT_DMA + i) * 1024));
+    }
+  };
+
+  floatx16 acc[MI][2];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+  struct Fr {
+    x6::bf16x8 a[MI][3];
+    float b[2][8];
+    x6::Parts bp[2];
+  };
+  auto read_a = [&](Fr& F, int g, int i) {
+    const char* p = smem + PATCH_B + (g % wx6::NSLOT) * wx6::SLOT_REGB + (i * 32 + lr) * wx6::SLOT_ROW + lh * 48;
+#pragma unroll
+    for (int t = 0; t < 3; ++t) F.a[i][t] = *reinterpret_cast<const x6::bf16x8*>(p + 16 * t);
+  };
+  auto read_b = [&](Fr& F, int g) {
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const int sx = 8 * g + jj;
+      if (sx < Sh::S) {
+        const int c = sx / (Sh::HR * KW), r = (sx / KW) % Sh::HR, kw = sx % KW;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) F.b[j][jj] = patch[bb[j][c] + r * W + kw];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) F.b[j][jj] = 0.0f;
+      }
+    }
+  };
+
+  Fr F[2];
+  issue_a(0);
+  issue_a(1);
+  wait_vm<0>();
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int i = 0; i < MI; ++i) read_a(F[0], 0, i);
+  read_b(F[0], 0);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) x6::split8(F[0].b[j], F[0].bp[j]);
+  // group g: slot of g + 1 is visible (wait + barrier; every wave is then also
+  // done with group g - 1's slot, which the DMA of group g + 2 overwrites)
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    Fr& fc = F[g & 1];
+    Fr& fn = F[(g + 1) & 1];
+    const bool rd = g + 1 < G;
+    if (g > 0 && rd) {
+      wait_vm<0>();
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (g + 2 < G) issue_a(g + 2);
+    constexpr int NB = 2 * MI;
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const int i = q >> 1, j = q & 1;
+      acc[i][j] = x6::mfma6(x6::Parts{fc.a[i][0], fc.a[i][1], fc.a[i][2]}, fc.bp[j], acc[i][j]);
+      if (rd) {
+        if (q == 0) read_b(fn, g + 1);
+        if (q >= 1 && q <= MI) read_a(fn, g + 1, q - 1);
+        if (q == NB - 2) x6::split8(fn.b[0], fn.bp[0]);
+        if (q == NB - 1) x6::split8(fn.b[1], fn.bp[1]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  gemm_epilogue<MI, 2, OUT_NCHW>(acc, P, P.e, nullptr, 0, n0 + wave * 64, lr, lh);
+}
+
+// Weight repack for k_conv_wide_x6: w [M][C][KH][KW] -> bf16 terms [G][96][SLOT_ROW/2]
+__global__ void __launch_bounds__(256) k_conv_wide_pack_x6(const float* __restrict__ w, uint16_t* __restrict__ out,
+                                                           int M, int C, int KH, int KW, int HR, int S, int64_t total) {
+  constexpr int RLH = wx6::SLOT_ROW / 2;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int col = static_cast<int>(idx % RLH);
+    const int row = static_cast<int>((idx / RLH) % wx6::BM);
+    const int g = static_cast<int>(idx / ((int64_t)RLH * wx6::BM));
+    uint16_t v = 0;
+    if (col < 48 && row < M) {
+      const int h = col / 24, p = (col - h * 24) / 8, j = col & 7;
+      const int sx = 8 * g + j;
+      if (sx < S) {
+        const int c = sx / (HR * KW), kh = h * HR + (sx / KW) % HR, kw = sx % KW;
+        if (kh < KH) v = x6::split_term(w[(((int64_t)row * C + c) * KH + kh) * KW + kw], p);
+      }
+    }
+    out[idx] = v;
+  }
+}
+
 // Weight repack for k_conv_patch_x6: w [G*M][C*T] -> bf16 terms
 // [G][tiles_m][ktiles][64 MI][RLB/2]: row = [group g][half h][term][8 steps] + pad.
 __global__ void __launch_bounds__(256) k_conv_patch_pack_x6(const float* __restrict__ w, uint16_t* __restrict__ out,
@@ -570,6 +766,77 @@ int launch_patch_x6(Params P, const uint16_t* wpack, int PW, int CS, int gz, hip
   return launch_status("conv patch x6");
 }
 
+
+// ---- k_conv_wide_x6 (AlexNet conv1 shape family) ----
+constexpr int WIDE_PFL = 3 * 9728;  // patch floats (3 channels x the largest block pair)
+struct WidePlan {
+  int CHS;
+};
+bool conv_wide_plan(const rram_conv_desc* d, WidePlan& pl) {
+  if (d->group != 1 || d->channels != 3 || d->kernel_h != 11 || d->kernel_w != 11 || d->stride_h != 4 ||
+      d->stride_w != 4 || d->pad_h != 0 || d->pad_w != 0 || d->dilation_h != 1 || d->dilation_w != 1)
+    return false;
+  if (d->num_output > wx6::BM) return false;
+  const int HW = d->out_h * d->out_w, OW = d->out_w, N = d->num * HW;
+  if (HW < wx6::BN) return false;
+  if ((int64_t)d->num * d->channels * d->height * d->width * 4 >= (1ll << 31)) return false;
+  const int HR = 6;
+  int chs = 0;
+  for (int n0 = 0; n0 < N; n0 += wx6::BN) {
+    const int pl_ = std::min(n0 + wx6::BN, N) - 1;
+    const int i0 = n0 / HW, i1 = pl_ / HW;
+    const int f0 = (n0 - i0 * HW) / OW;
+    const int l0 = i1 == i0 ? (pl_ - i0 * HW) / OW : d->out_h - 1;
+    const int len0 = ((l0 - f0) * 4 + 2 * HR) * d->width;
+    const int len1 = i1 == i0 ? 0 : ((pl_ - i1 * HW) / OW * 4 + 2 * HR) * d->width;
+    chs = std::max(chs, (len0 + 255) / 256 * 256 + (len1 + 255) / 256 * 256);
+  }
+  pl.CHS = chs;
+  return 3 * chs <= WIDE_PFL;
+}
+
+int conv_wide_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const float* bias, float* y, int relu,
+                     hipStream_t s) {
+  WidePlan pl;
+  if (!conv_wide_plan(d, pl)) return 0;
+  if ((reinterpret_cast<uintptr_t>(w) & 3u) != 0) return 0;
+  using Sh = wx6::Shape<11, 11, 3>;
+  const int HW = d->out_h * d->out_w;
+  Params P{};
+  P.M = d->num_output;
+  P.N = d->num * HW;
+  P.K = 3 * 121;
+  P.split = 1;
+  P.b = make_view(x, 0, P.N, P.K);
+  ConvGeom& cv = P.cv;
+  cv.C = 3;
+  cv.H = d->height;
+  cv.W = d->width;
+  cv.KH = cv.KW = 11;
+  cv.sh = cv.sw = 4;
+  cv.dh = cv.dw = 1;
+  cv.Ho = d->out_h;
+  cv.Wo = d->out_w;
+  cv.howo = make_fastdiv(HW);
+  cv.wo_div = make_fastdiv(d->out_w);
+  cv.chw = (int64_t)3 * d->height * d->width;
+  cv.in_bytes = static_cast<int>((int64_t)d->num * cv.chw * 4);
+  P.e = make_epi(y, HW, 1.0f, 0.0f, bias, RRAM_BIAS_ROW, relu);
+  P.e.cimg = (int64_t)d->num_output * HW;
+  P.e.hw = make_fastdiv(HW);
+  const int64_t total = (int64_t)Sh::G * wx6::BM * (wx6::SLOT_ROW / 2);
+  uint16_t* wp = reinterpret_cast<uint16_t*>(pack_buffer(static_cast<size_t>((total + 1) / 2), s));
+  RRAM_REQUIRE(wp != nullptr, "conv: packed-weight buffer allocation failed");
+  hipLaunchKernelGGL(k_conv_wide_pack_x6, dim3(stream_blocks(total)), dim3(256), 0, s, w, wp, d->num_output, 3, 11,
+                     11, Sh::HR, Sh::S, total);
+  int rc = launch_status("conv wide weight pack x6");
+  if (rc) return rc;
+  const unsigned nwg = static_cast<unsigned>((P.N + wx6::BN - 1) / wx6::BN);
+  hipLaunchKernelGGL((k_conv_wide_x6<11, 11, 4, 3, WIDE_PFL>), dim3(nwg), dim3(256), 0, s, P, wp, pl.CHS);
+  rc = launch_status("conv wide x6");
+  return rc ? rc : 1;
+}
+
 // engine of the stride-1 3x3 / 5x5 convolutions (rram_set_f32_engine)
 std::atomic<int>& f32_engine() {
   static std::atomic<int> eng{[] {
@@ -624,6 +891,10 @@ int conv_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const f
                 hipStream_t s) {
   if (f32_engine().load(std::memory_order_relaxed) != RRAM_ENGINE_BF16X6) return 0;
   if ((reinterpret_cast<uintptr_t>(w) & 3u) != 0) return 0;
+  {
+    const int rc = conv_wide_x6_fwd(d, x, w, bias, y, relu, s);
+    if (rc != 0) return rc;
+  }
   ConvPlan pl;
   if (!conv_x6_plan(d, pl)) return 0;
   const int KH = d->kernel_h, KW = d->kernel_w;
@@ -763,8 +1034,10 @@ extern "C" {
 int rram_f32_engine_for_conv(const rram_conv_desc* d) {
   RRAM_REQUIRE(d != nullptr, "engine query: desc is NULL");
   rram::ConvPlan pl;
-  return rram::f32_engine().load() == RRAM_ENGINE_BF16X6 && rram::conv_x6_plan(d, pl) ? RRAM_ENGINE_BF16X6
-                                                                                    : RRAM_ENGINE_F32;
+  rram::WidePlan wpl;
+  return rram::f32_engine().load() == RRAM_ENGINE_BF16X6 && (rram::conv_x6_plan(d, pl) || rram::conv_wide_plan(d, wpl))
+             ? RRAM_ENGINE_BF16X6
+             : RRAM_ENGINE_F32;
 }
 
 int rram_f32_engine_for_ip(int M, int N, int K, size_t ws_bytes) {

@@ -484,6 +484,7 @@ def test_conv_patch_shapes_vs_fp64(device, cs, conv_engine):
 
 # AlexNet conv2 / conv3 / conv4 / conv5 at 4 images (Caffe-filler-like weight scale)
 ENGINE_CASES = [
+    dict(x=(2, 3, 227, 227), cout=96, k=11, p=0, g=1, s=4),    # conv1 (k_conv_wide_x6)
     dict(x=(4, 96, 27, 27), cout=256, k=5, p=2, g=2),
     dict(x=(4, 256, 13, 13), cout=384, k=3, p=1, g=1),
     dict(x=(4, 384, 13, 13), cout=384, k=3, p=1, g=2),
@@ -503,13 +504,15 @@ def test_conv_engine_bf16x6_accuracy_vs_f32(device, cs):
     x = np.maximum(rng.standard_normal(cs["x"]), 0).astype(np.float32)   # post-ReLU activations
     w = (rng.standard_normal((cs["cout"], cs["x"][1] // cs["g"], cs["k"], cs["k"])) * 0.01).astype(np.float32)
     b = rng.standard_normal(cs["cout"]).astype(np.float32)
-    d = ops.conv_desc(cs["x"], cs["cout"], cs["k"], 1, cs["p"], 1, cs["g"])
-    ref, scale = conv64(x, w, b, 1, cs["p"], cs["g"])
+    st = cs.get("s", 1)
+    d = ops.conv_desc(cs["x"], cs["cout"], cs["k"], st, cs["p"], 1, cs["g"])
+    ref, scale = conv64(x, w, b, st, cs["p"], cs["g"])
     err = {}
     prev = ops.get_f32_engine()
     try:
         for eng in (ops.ENGINE_F32, ops.ENGINE_BF16X6):
             ops.set_f32_engine(eng)
+            assert ops.f32_engine_for_conv(d) == eng      # the shape really runs on that engine
             y = torch.empty((cs["x"][0], cs["cout"], d.out_h, d.out_w), device=device)
             ops.conv2d_fwd(d, T(x, device), T(w, device), T(b, device), y)
             torch.cuda.synchronize()
