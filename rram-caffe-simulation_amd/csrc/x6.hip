@@ -68,6 +68,14 @@ __device__ __forceinline__ uint16_t split_term(float v, int p) {
   const __bf16 t = p == 0 ? h : p == 1 ? m : l;
   return __builtin_bit_cast(uint16_t, t);
 }
+// the three bf16 terms of 8 floats as 3 x 16 bytes at dst (16-byte aligned)
+__device__ __forceinline__ void store_terms8(const float (&v)[8], char* dst) {
+  Parts t;
+  split8(v, t);
+  *reinterpret_cast<bf16x8*>(dst) = t.h;
+  *reinterpret_cast<bf16x8*>(dst + 16) = t.m;
+  *reinterpret_cast<bf16x8*>(dst + 32) = t.l;
+}
 __device__ __forceinline__ floatx16 mfma6(const Parts& a, const Parts& b, floatx16 c) {
   c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.l, b.h, c, 0, 0, 0);
   c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.l, c, 0, 0, 0);
@@ -503,33 +511,37 @@ __global__ void __launch_bounds__(256) k_conv_wide_pack_x6(const float* __restri
 }
 
 // Weight repack for k_conv_patch_x6: w [G*M][C*T] -> bf16 terms
-// [G][tiles_m][ktiles][64 MI][RLB/2]: row = [group g][half h][term][8 steps] + pad.
-__global__ void __launch_bounds__(256) k_conv_patch_pack_x6(const float* __restrict__ w, uint16_t* __restrict__ out,
-                                                            int G, int M, int C, int T, int CPH, int G8, int RLH,
-                                                            int BMc, int tiles_m, int ktiles, int64_t total) {
-  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    int64_t r = idx;
-    const int col = static_cast<int>(r % RLH);
-    r /= RLH;
-    const int row = static_cast<int>(r % BMc);
+// [G][tiles_m][ktiles][64 MI][RLB]: row = [group g][half h][term][8 steps] + pad.
+// One thread per (row, group, half): 8 weights in, 48 bytes out.
+__global__ void __launch_bounds__(256) k_conv_patch_pack_x6(const float* __restrict__ w, char* __restrict__ out, int G,
+                                                            int M, int C, int T, int CPH, int G8, int RLB, int BMc,
+                                                            int tiles_m, int ktiles, int units) {
+  for (int u = blockIdx.x * blockDim.x + threadIdx.x; u < units; u += gridDim.x * blockDim.x) {
+    int r = u;
+    const int h = r & 1;
+    r >>= 1;
+    const int gg = r % G8;
+    r /= G8;
+    const int row = r % BMc;
     r /= BMc;
-    const int kt = static_cast<int>(r % ktiles);
+    const int kt = r % ktiles;
     r /= ktiles;
-    const int tm = static_cast<int>(r % tiles_m);
-    const int g = static_cast<int>(r / tiles_m);
+    const int tm = r % tiles_m;
+    const int g = r / tiles_m;
     const int m = tm * BMc + row;
-    uint16_t v = 0;
-    if (col < G8 * 48 && m < M) {
-      const int gg = col / 48, rem = col - gg * 48;
-      const int h = rem / 24, p = (rem - h * 24) / 8, j = rem & 7;
-      const int s = 8 * gg + j;
-      if (s < CPH * T) {
-        const int c = kt * 2 * CPH + h * CPH + s / T;
-        v = x6::split_term(w[((int64_t)g * M + m) * C * T + (int64_t)c * T + (s % T)], p);
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int sx = 8 * gg + j;
+      v[j] = 0.0f;
+      if (sx < CPH * T && m < M) {
+        const int c = kt * 2 * CPH + h * CPH + sx / T;
+        v[j] = w[((int64_t)g * M + m) * C * T + (int64_t)c * T + (sx % T)];
       }
     }
-    out[idx] = v;
+    char* rowp = out + ((((int64_t)g * tiles_m + tm) * ktiles + kt) * BMc + row) * RLB;
+    x6::store_terms8(v, rowp + (gg * 2 + h) * 48);
+    if (gg == G8 - 1 && h == 1) *reinterpret_cast<uint4*>(rowp + G8 * 96) = make_uint4(0, 0, 0, 0);
   }
 }
 
@@ -705,29 +717,31 @@ k_gemm_x6(Params P, const uint16_t* __restrict__ apack, int ktiles_all, int ktc)
   gemm_epilogue<MI, 2, OUT_ROWMAJOR>(acc, P, P.e, part, m0, n0 + wave * 64, lr, lh);
 }
 
-// A [M][lda] fp32 -> K-tile slabs of bf16 terms [tiles_m][ktiles][32 MI][RLB/2]
-// for k_gemm_x6 (zero past M and K)
+// A [M][lda] fp32 -> K-tile slabs of bf16 terms [tiles_m][ktiles][32 MI][RLB]
+// for k_gemm_x6 (zero past M and K; lda, K multiples of 4, A 16-byte aligned).
+// One thread per (row, K-tile, group, half): two float4 in, 48 bytes out.
 __global__ void __launch_bounds__(256) k_pack_rows_x6(const float* __restrict__ a, int64_t lda, int M, int K,
-                                                      uint16_t* __restrict__ out, int BMc, int ktiles, int64_t total) {
-  constexpr int RLH = gx6::RLB / 2;
-  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    int64_t r = idx;
-    const int col = static_cast<int>(r % RLH);
-    r /= RLH;
-    const int row = static_cast<int>(r % BMc);
-    r /= BMc;
-    const int kt = static_cast<int>(r % ktiles);
-    const int tm = static_cast<int>(r / ktiles);
-    const int m = tm * BMc + row;
-    uint16_t v = 0;
-    if (col < 96 && m < M) {
-      const int g = col / 48, rem = col - g * 48;
-      const int h = rem / 24, p = (rem - h * 24) / 8, j = rem & 7;
-      const int k = kt * gx6::KT + 16 * h + 8 * g + j;
-      if (k < K) v = x6::split_term(a[(int64_t)m * lda + k], p);
+                                                      char* __restrict__ out, int BMc, int ktiles, int units) {
+  for (int u = blockIdx.x * blockDim.x + threadIdx.x; u < units; u += gridDim.x * blockDim.x) {
+    const int h = u & 1, g = (u >> 1) & 1;
+    const int r = u >> 2;
+    const int kt = r % ktiles;
+    const int mrow = r / ktiles;  // tm * BMc + row
+    const int k = kt * gx6::KT + 16 * h + 8 * g;
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (mrow < M && k + 4 * q < K) f = *reinterpret_cast<const float4*>(a + (int64_t)mrow * lda + k + 4 * q);
+      v[4 * q] = f.x;
+      v[4 * q + 1] = f.y;
+      v[4 * q + 2] = f.z;
+      v[4 * q + 3] = f.w;
     }
-    out[idx] = v;
+    const int tm = mrow / BMc, row = mrow - tm * BMc;
+    char* rowp = out + (((int64_t)tm * ktiles + kt) * BMc + row) * gx6::RLB;
+    x6::store_terms8(v, rowp + (g * 2 + h) * 48);
+    if (g == 1 && h == 1) *reinterpret_cast<uint4*>(rowp + 192) = make_uint4(0, 0, 0, 0);
   }
 }
 
@@ -933,8 +947,9 @@ int conv_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const f
   const int64_t total = (int64_t)G * tiles_m * ktiles * BMc * RLH;
   uint16_t* wp = reinterpret_cast<uint16_t*>(pack_buffer(static_cast<size_t>((total + 1) / 2), s));
   RRAM_REQUIRE(wp != nullptr, "conv: packed-weight buffer allocation failed");
-  hipLaunchKernelGGL(k_conv_patch_pack_x6, dim3(stream_blocks(total)), dim3(256), 0, s, w, wp, G, M, Cg, T, CPH, G8,
-                     RLH, BMc, tiles_m, ktiles, total);
+  const int units = G * tiles_m * ktiles * BMc * G8 * 2;
+  hipLaunchKernelGGL(k_conv_patch_pack_x6, dim3(stream_blocks(units)), dim3(256), 0, s, w, reinterpret_cast<char*>(wp),
+                     G, M, Cg, T, CPH, G8, 2 * RLH, BMc, tiles_m, ktiles, units);
   int rc = launch_status("conv weight pack x6");
   if (rc) return rc;
 #define RRAM_P(KH_, CPH_, PD_)                                                                           \
@@ -996,8 +1011,9 @@ int gemm_x6_nt(int M, int N, int K, float alpha, const float* A, int lda, const 
   const int64_t total = (int64_t)tiles_m * ktiles * BMc * (gx6::RLB / 2);
   uint16_t* ap = reinterpret_cast<uint16_t*>(pack_buffer(static_cast<size_t>((total + 1) / 2), s));
   RRAM_REQUIRE(ap != nullptr, "gemm x6: packed-operand buffer allocation failed");
-  hipLaunchKernelGGL(k_pack_rows_x6, dim3(stream_blocks(total)), dim3(256), 0, s, A, (int64_t)lda, M, K, ap, BMc,
-                     ktiles, total);
+  const int units = tiles_m * BMc * ktiles * 4;
+  hipLaunchKernelGGL(k_pack_rows_x6, dim3(stream_blocks(units)), dim3(256), 0, s, A, (int64_t)lda, M, K,
+                     reinterpret_cast<char*>(ap), BMc, ktiles, units);
   int rc = launch_status("gemm x6 pack");
   if (rc) return rc;
   Params P{};
