@@ -204,15 +204,18 @@ k_conv_patch_x6(Params P, const uint16_t* __restrict__ wpack, int PW, int CS) {
               img + static_cast<uint32_t>(A_REGB + (wave * PD + i) * 64 * 4));
     }
   };
+  // weight fragments (this lane's 8 k of rows 32 i + lr: high, middle, low
+  // terms) are single-buffered: row block i of the next group is read as soon
+  // as both column blocks of the current group have consumed it
+  x6::bf16x8 fa[MI][3];
   struct Fr {
-    x6::bf16x8 a[MI][3];  // this lane's 8 k of rows 32 i + lr: high, middle, low terms
     float b[2][8];        // raw activations of columns j
     x6::Parts bp[2];      // their split
   };
-  auto read_a = [&](Fr& F, const char* st, int g, int i) {
+  auto read_a = [&](const char* st, int g, int i) {
     const char* p = st + (i * 32 + lr) * Sh::RLB + (g * 2 + lh) * 48;
 #pragma unroll
-    for (int t = 0; t < 3; ++t) F.a[i][t] = *reinterpret_cast<const x6::bf16x8*>(p + 16 * t);
+    for (int t = 0; t < 3; ++t) fa[i][t] = *reinterpret_cast<const x6::bf16x8*>(p + 16 * t);
   };
   auto read_b = [&](Fr& F, const char* st, int g) {
     const float* pt = reinterpret_cast<const float*>(st + A_REGB);
@@ -239,7 +242,7 @@ k_conv_patch_x6(Params P, const uint16_t* __restrict__ wpack, int PW, int CS) {
   wait_vm<0>();
   __builtin_amdgcn_s_barrier();
 #pragma unroll
-  for (int i = 0; i < MI; ++i) read_a(F[0], smem, 0, i);
+  for (int i = 0; i < MI; ++i) read_a(smem, 0, i);
   read_b(F[0], smem, 0);
 #pragma unroll
   for (int j = 0; j < 2; ++j) x6::split8(F[0].b[j], F[0].bp[j]);
@@ -271,10 +274,10 @@ k_conv_patch_x6(Params P, const uint16_t* __restrict__ wpack, int PW, int CS) {
 #pragma unroll
       for (int q = 0; q < NB; ++q) {
         const int i = q >> 1, j = q & 1;
-        acc[i][j] = x6::mfma6(x6::Parts{fc.a[i][0], fc.a[i][1], fc.a[i][2]}, fc.bp[j], acc[i][j]);
+        acc[i][j] = x6::mfma6(x6::Parts{fa[i][0], fa[i][1], fa[i][2]}, fc.bp[j], acc[i][j]);
         if (rd) {
           if (q == 0) read_b(fn, src, gn);
-          if (q >= 1 && q <= MI) read_a(fn, src, gn, q - 1);
+          if (j == 1) read_a(src, gn, i);
           if (q == NB - 3) x6::split8(fn.b[0], fn.bp[0]);
           if (q == NB - 1) x6::split8(fn.b[1], fn.bp[1]);
         }
@@ -423,15 +426,15 @@ k_conv_wide_x6(Params P, const uint16_t* __restrict__ wpack, int CHS) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
+  x6::bf16x8 fa[MI][3];  // single-buffered weight fragments (see k_conv_patch_x6)
   struct Fr {
-    x6::bf16x8 a[MI][3];
     float b[2][8];
     x6::Parts bp[2];
   };
-  auto read_a = [&](Fr& F, int g, int i) {
+  auto read_a = [&](int g, int i) {
     const char* p = smem + PATCH_B + (g % wx6::NSLOT) * wx6::SLOT_REGB + (i * 32 + lr) * wx6::SLOT_ROW + lh * 48;
 #pragma unroll
-    for (int t = 0; t < 3; ++t) F.a[i][t] = *reinterpret_cast<const x6::bf16x8*>(p + 16 * t);
+    for (int t = 0; t < 3; ++t) fa[i][t] = *reinterpret_cast<const x6::bf16x8*>(p + 16 * t);
   };
   auto read_b = [&](Fr& F, int g) {
 #pragma unroll
@@ -454,7 +457,7 @@ k_conv_wide_x6(Params P, const uint16_t* __restrict__ wpack, int CHS) {
   wait_vm<0>();
   __builtin_amdgcn_s_barrier();
 #pragma unroll
-  for (int i = 0; i < MI; ++i) read_a(F[0], 0, i);
+  for (int i = 0; i < MI; ++i) read_a(0, i);
   read_b(F[0], 0);
 #pragma unroll
   for (int j = 0; j < 2; ++j) x6::split8(F[0].b[j], F[0].bp[j]);
@@ -475,10 +478,10 @@ k_conv_wide_x6(Params P, const uint16_t* __restrict__ wpack, int CHS) {
 #pragma unroll
     for (int q = 0; q < NB; ++q) {
       const int i = q >> 1, j = q & 1;
-      acc[i][j] = x6::mfma6(x6::Parts{fc.a[i][0], fc.a[i][1], fc.a[i][2]}, fc.bp[j], acc[i][j]);
+      acc[i][j] = x6::mfma6(x6::Parts{fa[i][0], fa[i][1], fa[i][2]}, fc.bp[j], acc[i][j]);
       if (rd) {
         if (q == 0) read_b(fn, g + 1);
-        if (q >= 1 && q <= MI) read_a(fn, g + 1, q - 1);
+        if (j == 1) read_a(g + 1, i);
         if (q == NB - 2) x6::split8(fn.b[0], fn.bp[0]);
         if (q == NB - 1) x6::split8(fn.b[1], fn.bp[1]);
       }
@@ -559,19 +562,20 @@ __global__ void __launch_bounds__(256) k_conv_patch_pack_x6(const float* __restr
 // K order inside a K-tile: group g, lane half h holds k = 16 h + 8 g + j
 // (the B rows' 16-byte quads 4h + 2g + u, u = 0, 1, swizzled as k_gemm2).
 namespace gx6 {
-constexpr int BN = 256, KT = 32;
+constexpr int KT = 32;
 constexpr int RLB = 2 * 96 + 16;  // packed A row bytes per K-tile ([g][h][term][8 bf16] + pad, RLB/16 odd)
 }  // namespace gx6
 
-template <int MI>
+template <int MI, int NJ>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 k_gemm_x6(Params P, const uint16_t* __restrict__ apack, int ktiles_all, int ktc) {
   using namespace g2;
-  constexpr int BMc = 32 * MI, BNc = gx6::BN, KT = gx6::KT;
+  // tile 32 MI x 128 NJ: wave w owns all rows x columns 32 NJ w .. 32 NJ w + 32 NJ - 1
+  constexpr int BMc = 32 * MI, BNc = 128 * NJ, KT = gx6::KT;
   constexpr int A_B = BMc * gx6::RLB;
   constexpr int A_DMA = ((A_B + 1023) / 1024 + 3) / 4;
   constexpr int A_REGB = A_DMA * 4 * 1024;
-  constexpr int B_DMA = BNc * KT * 4 / 1024 / 4;        // 1 KB pieces per wave (8)
+  constexpr int B_DMA = 4 * NJ;                          // 1 KB pieces (8 rows x 32 k) per wave
   constexpr int SFB = A_REGB + BNc * KT * 4;
   constexpr int NVM = A_DMA + B_DMA;
   static_assert(2 * SFB <= 160 * 1024, "LDS");
@@ -603,25 +607,25 @@ k_gemm_x6(Params P, const uint16_t* __restrict__ apack, int ktiles_all, int ktc)
     const int f = ((wave * A_DMA + i) * 64 + lane) * 16;
     aoff[i] = f < A_B ? static_cast<uint32_t>(f) : 0x80000000u;
   }
-  // B rows n0 + 64 w + 8 i + (lane >> 3), quad lane & 7 (stored swizzled)
+  // B rows n0 + 32 NJ w + 8 i + (lane >> 3), quad lane & 7 (stored swizzled)
   const View& vb = P.b;
   const int4v brsrc = make_rsrc(vb.p, static_cast<uint32_t>(((int64_t)(vb.rows - 1) * vb.ld + vb.kdim) * 4));
   uint32_t boff[B_DMA];
   int bkq[B_DMA];
 #pragma unroll
   for (int i = 0; i < B_DMA; ++i) {
-    const int r = 64 * wave + 8 * i + (lane >> 3);
+    const int r = 32 * NJ * wave + 8 * i + (lane >> 3);
     const int q = (lane & 7) ^ ((r >> 1) & 7);
     boff[i] = n0 + r < vb.rows ? static_cast<uint32_t>((int64_t)(n0 + r) * vb.ld * 4) : 0x80000000u;
     bkq[i] = 4 * q;
   }
   const int kend = P.K;
 
-  floatx16 acc[MI][2];
+  floatx16 acc[MI][NJ];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
@@ -633,24 +637,24 @@ k_gemm_x6(Params P, const uint16_t* __restrict__ apack, int ktiles_all, int ktc)
       const int i = e - A_DMA;
       const int k = (kt0 + t) * KT + bkq[i];
       const uint32_t off = (boff[i] + static_cast<uint32_t>(k) * 4u) | (k < kend ? 0u : 0x80000000u);
-      dma_b128(brsrc, off, img + static_cast<uint32_t>(A_REGB + (64 * wave + 8 * i) * KT * 4));
+      dma_b128(brsrc, off, img + static_cast<uint32_t>(A_REGB + (32 * NJ * wave + 8 * i) * KT * 4));
     }
   };
+  x6::bf16x8 fa[MI][3];  // single-buffered activation fragments (see k_conv_patch_x6)
   struct Fr {
-    x6::bf16x8 a[MI][3];
-    float b[2][8];
-    x6::Parts bp[2];
+    float b[NJ][8];
+    x6::Parts bp[NJ];
   };
-  auto read_a = [&](Fr& F, const char* st, int g, int i) {
+  auto read_a = [&](const char* st, int g, int i) {
     const char* p = st + (i * 32 + lr) * gx6::RLB + (g * 2 + lh) * 48;
 #pragma unroll
-    for (int t = 0; t < 3; ++t) F.a[i][t] = *reinterpret_cast<const x6::bf16x8*>(p + 16 * t);
+    for (int t = 0; t < 3; ++t) fa[i][t] = *reinterpret_cast<const x6::bf16x8*>(p + 16 * t);
   };
   auto read_b = [&](Fr& F, const char* st, int g) {
     const float* bs = reinterpret_cast<const float*>(st + A_REGB);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = 64 * wave + 32 * j + lr;
+    for (int j = 0; j < NJ; ++j) {
+      const int n = 32 * NJ * wave + 32 * j + lr;
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const float4 q = *reinterpret_cast<const float4*>(bs + n * KT + (((4 * lh + 2 * g + u) ^ ((n >> 1) & 7)) << 2));
@@ -668,10 +672,10 @@ k_gemm_x6(Params P, const uint16_t* __restrict__ apack, int ktiles_all, int ktc)
   wait_vm<0>();
   __builtin_amdgcn_s_barrier();
 #pragma unroll
-  for (int i = 0; i < MI; ++i) read_a(F[0], smem, 0, i);
+  for (int i = 0; i < MI; ++i) read_a(smem, 0, i);
   read_b(F[0], smem, 0);
 #pragma unroll
-  for (int j = 0; j < 2; ++j) x6::split8(F[0].b[j], F[0].bp[j]);
+  for (int j = 0; j < NJ; ++j) x6::split8(F[0].b[j], F[0].bp[j]);
 
   auto tile = [&](int t, auto more_c) {
     constexpr bool MORE = decltype(more_c)::value;
@@ -691,16 +695,17 @@ k_gemm_x6(Params P, const uint16_t* __restrict__ apack, int ktiles_all, int ktc)
       const bool rd = !last || MORE;
       const char* src = last ? nxt : cur;
       const int gn = last ? 0 : 1;
-      constexpr int NB = 2 * MI;
+      constexpr int NB = MI * NJ;
 #pragma unroll
       for (int q = 0; q < NB; ++q) {
-        const int i = q >> 1, j = q & 1;
-        acc[i][j] = x6::mfma6(x6::Parts{fc.a[i][0], fc.a[i][1], fc.a[i][2]}, fc.bp[j], acc[i][j]);
+        const int i = q / NJ, j = q % NJ;
+        acc[i][j] = x6::mfma6(x6::Parts{fa[i][0], fa[i][1], fa[i][2]}, fc.bp[j], acc[i][j]);
         if (rd) {
           if (q == 0) read_b(fn, src, gn);
-          if (q >= 1 && q <= MI) read_a(fn, src, gn, q - 1);
-          if (q == NB - 3) x6::split8(fn.b[0], fn.bp[0]);
-          if (q == NB - 1) x6::split8(fn.b[1], fn.bp[1]);
+          if (j == NJ - 1) read_a(src, gn, i);
+#pragma unroll
+          for (int jj = 0; jj < NJ; ++jj)
+            if (q == NB - NJ + jj) x6::split8(fn.b[jj], fn.bp[jj]);
         }
         if (!last && MORE) {
 #pragma unroll
@@ -714,7 +719,7 @@ k_gemm_x6(Params P, const uint16_t* __restrict__ apack, int ktiles_all, int ktc)
   int t = 0;
   for (; t + 1 < nt; ++t) tile(t, std::true_type{});
   tile(t, std::false_type{});
-  gemm_epilogue<MI, 2, OUT_ROWMAJOR>(acc, P, P.e, part, m0, n0 + wave * 64, lr, lh);
+  gemm_epilogue<MI, NJ, OUT_ROWMAJOR>(acc, P, P.e, part, m0, n0 + 32 * NJ * wave, lr, lh);
 }
 
 // A [M][lda] fp32 -> K-tile slabs of bf16 terms [tiles_m][ktiles][32 MI][RLB]
@@ -968,16 +973,23 @@ int conv_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const f
 
 // shape plan of the x6 GEMM (false: not covered)
 struct GemmPlan {
-  int MI, tiles_m, tiles_n, ktiles, split, ktc;
+  int MI, NJ, tiles_m, tiles_n, ktiles, split, ktc;
 };
 bool gemm_x6_plan(int M, int N, int K, size_t ws_bytes, GemmPlan& pl) {
   if (K < 256 || K % 4 != 0 || (int64_t)M * N * K < (1ll << 24)) return false;
-  // M tile 128 or 96 rows, whichever pads less
-  const int t128 = (M + 127) / 128 * 128, t96 = (M + 95) / 96 * 96;
-  pl.MI = (t96 - M) < (t128 - M) ? 3 : 4;
-  const int BMc = 32 * pl.MI;
+  // 256 x 128 tiles (every weight row read by one tile row) when <= 1/4 of
+  // the rows pad, else 128 (or 96) x 256
+  const int t256 = (M + 255) / 256 * 256, t128 = (M + 127) / 128 * 128, t96 = (M + 95) / 96 * 96;
+  if ((t256 - M) * 4 <= t256) {
+    pl.MI = 8;
+    pl.NJ = 1;
+  } else {
+    pl.MI = (t96 - M) < (t128 - M) ? 3 : 4;
+    pl.NJ = 2;
+  }
+  const int BMc = 32 * pl.MI, BNc = 128 * pl.NJ;
   pl.tiles_m = (M + BMc - 1) / BMc;
-  pl.tiles_n = (N + gx6::BN - 1) / gx6::BN;
+  pl.tiles_n = (N + BNc - 1) / BNc;
   pl.ktiles = (K + gx6::KT - 1) / gx6::KT;
   // split-K toward 256 workgroups, >= 8 K-tiles (256 k) per split
   const int64_t tiles = (int64_t)pl.tiles_m * pl.tiles_n;
@@ -1028,10 +1040,12 @@ int gemm_x6_nt(int M, int N, int K, float alpha, const float* A, int lda, const 
   P.tiles_n = tiles_n;
   P.tiles_z = split;
   const unsigned nwg = static_cast<unsigned>(tiles * split);
-  if (MI == 3)
-    hipLaunchKernelGGL((k_gemm_x6<3>), dim3(nwg), dim3(256), 0, s, P, ap, ktiles, ktc);
+  if (MI == 8)
+    hipLaunchKernelGGL((k_gemm_x6<8, 1>), dim3(nwg), dim3(256), 0, s, P, ap, ktiles, ktc);
+  else if (MI == 3)
+    hipLaunchKernelGGL((k_gemm_x6<3, 2>), dim3(nwg), dim3(256), 0, s, P, ap, ktiles, ktc);
   else
-    hipLaunchKernelGGL((k_gemm_x6<4>), dim3(nwg), dim3(256), 0, s, P, ap, ktiles, ktc);
+    hipLaunchKernelGGL((k_gemm_x6<4, 2>), dim3(nwg), dim3(256), 0, s, P, ap, ktiles, ktc);
   rc = launch_status("gemm x6");
   if (rc) return rc;
   if (split > 1) {

@@ -446,6 +446,10 @@ PATCH_CASES = [
     dict(x=(2, 12, 28, 28), cout=224, k=5, p=2, g=1),   # 5x5, M padded to 256
     dict(x=(5, 8, 10, 13), cout=256, k=3, p=1, g=2),    # 130 positions: most tiles span two images
     dict(x=(2, 4, 20, 20), cout=128, k=5, p=0, g=1),    # 5x5 without padding (16 x 16 out)
+    dict(x=(3, 32, 13, 13), cout=192, k=3, p=1, g=1),   # 16 | C: streamed x6 kernel, 96-row tiles, 2 super-tiles
+    dict(x=(2, 16, 28, 28), cout=224, k=5, p=2, g=1),   # streamed 5x5, M padded to 256
+    dict(x=(5, 32, 10, 13), cout=256, k=3, p=1, g=2),   # streamed, 130 positions: tiles over three images
+    dict(x=(2, 16, 20, 20), cout=128, k=5, p=0, g=1),   # streamed 5x5 without padding
     dict(x=(2, 6, 13, 13), cout=128, k=3, p=1, g=1),    # C % 4 != 0: im2col path
     dict(x=(2, 8, 12, 12), cout=128, k=3, p=0, g=1),    # 100 positions per image: im2col path
 ]
