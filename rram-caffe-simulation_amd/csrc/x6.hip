@@ -319,6 +319,315 @@ k_conv_patch_x6(Params P, const uint16_t* __restrict__ wpack, int PW, int CS) {
 
 
 // ---------------------------------------------------------------------------
+// k_conv_cb_x6: stride-1 KH x KW convolution on the bf16x6 engine with the
+// activations split ONCE, outside the main loop, into a channel-octet layout
+// (k_pack_octets_x6: [img][C/8][H][W][term][8 channels] bf16), so the main
+// loop does no VALU split and no per-element gather: every B fragment term is
+// one ds_read_b128 of 8 channels at one tap, and a K-tile is 16 channels x
+// all KH*KW taps (no padded steps; k_conv_patch_x6 pads 5x5's 25 taps to 32).
+// K order: MFMA group (kt, s) = channels 16 kt .. 16 kt + 15 at tap s; lane
+// half h holds channel octet 2 kt + h.
+// Tile 32 WR x 32 NB (4 / WR): wave w owns rows 32 (w % WR) .. + 31 and
+// columns 32 NB (w / WR) .. + 32 NB - 1.  Its weight fragments (pre-split and
+// fragment-ordered by k_conv_cb_pack_x6, 3 KB per group) come straight from
+// L2 into registers one group ahead; the input patch of a K-tile (both
+// octet planes, R rows x RPC 16-byte chunks) is LDS-DMA'd into a 2-stage
+// ring, one barrier per K-tile.  A position is 3 16-byte chunks; the patch
+// row pitch RPC (chunks) is >= 3 PW with RPC = 3 OW (mod 16), so the chunk of
+// output column n is 3 n (mod 16) and the 16 consecutive columns of a
+// ds_read_b128 lane group hit 16 disjoint bank quads (across row wraps too).  Per group a wave issues NB x 6 MFMAs, 3 NB ds_read_b128 and 3
+// global loads: the loop is MFMA-paced.
+namespace cbx6 {
+constexpr int FRAG = 3 * 64;  // bf16x8 units per pre-split weight fragment (3 terms x 64 lanes)
+// weight prefetch distance (groups) and LDS bytes of a (KH, NB, PD) instance
+constexpr int dist(int NB) { return NB == 8 ? 2 : 3; }
+constexpr int lds_bytes(int NB, int PD) { return 2 * PD * 4096 + 4 * (dist(NB) + 1) * 3072; }
+// first patch piece of K-tile kt + 1 issued at tap s (pieces spread evenly
+// over taps 0 .. T - 2, so the last tap's weight load is younger than all)
+constexpr int piece_lo(int s, int PD, int T) { return s >= T - 1 ? PD : (s * PD + T - 2) / (T - 1); }
+constexpr int pieces(int s, int PD, int T, bool more) { return more ? piece_lo(s + 1, PD, T) - piece_lo(s, PD, T) : 0; }
+// memory operations issued after group q + 1's weight pieces, counted at the
+// end of tap s (q = kt T + s): the patch pieces of taps max(0, s + 1 - D) .. s
+// (those of the previous K-tile are not counted: waiting on fewer is safe)
+// and the 3-piece weight loads of groups q + 2 .. q + D that exist
+constexpr int after_a(int s, int PD, int T, int D, bool more) {
+  int n = 0;
+  for (int t = s + 1 - D < 0 ? 0 : s + 1 - D; t <= s; ++t) n += pieces(t, PD, T, more);
+  int na = more ? D - 1 : ((T - 1 - s < D ? T - 1 - s : D) - 1);
+  return n + 3 * (na > 0 ? na : 0);
+}
+// operations issued after the last patch piece of K-tile kt + 1: the weight
+// loads of the taps after it
+constexpr int after_patch(int PD, int T) {
+  int sl = 0;
+  for (int t = 0; t < T; ++t)
+    if (pieces(t, PD, T, true) > 0) sl = t;
+  return 3 * (T - 1 - sl);
+}
+}  // namespace cbx6
+
+// s_waitcnt vmcnt(n) for an n the compiler folds to a constant after unrolling
+__device__ __forceinline__ void wait_vm_n(int n) {
+  switch (n) {
+#define RRAM_W(k) \
+  case k:         \
+    g2::wait_vm<k>(); \
+    break;
+    RRAM_W(0) RRAM_W(1) RRAM_W(2) RRAM_W(3) RRAM_W(4) RRAM_W(5) RRAM_W(6) RRAM_W(7) RRAM_W(8) RRAM_W(9)
+    RRAM_W(10) RRAM_W(11) RRAM_W(12) RRAM_W(13) RRAM_W(14) RRAM_W(15) RRAM_W(16) RRAM_W(17) RRAM_W(18)
+    RRAM_W(19) RRAM_W(20) RRAM_W(21) RRAM_W(22) RRAM_W(23) RRAM_W(24)
+#undef RRAM_W
+    default:
+      g2::wait_vm<24>();  // n > 24: waiting on fewer is safe
+  }
+}
+
+template <int KH, int KW, int WR, int NB, int PD>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __restrict__ xpack, int octb, int rpc,
+             uint32_t xrange, int ximg) {
+  using namespace g2;
+  constexpr int T = KH * KW, WC = 4 / WR, BMc = 32 * WR, BNc = 32 * NB * WC, SFB = PD * 4 * 1024;
+  constexpr int D = cbx6::dist(NB), NSA = D + 1;
+  static_assert(cbx6::lds_bytes(NB, PD) <= 160 * 1024 && D < T, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[cbx6::lds_bytes(NB, PD)];
+  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem));
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lr = lane & 31, lh = lane >> 5;
+  const int wr = wave % WR, wc = wave / WR;
+
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, loc = bid >> 3;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int tid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const int tm = __builtin_amdgcn_readfirstlane(tid % P.tiles_m);
+  const int tn = __builtin_amdgcn_readfirstlane((tid / P.tiles_m) % P.tiles_n);
+  const int z = __builtin_amdgcn_readfirstlane(tid / (P.tiles_m * P.tiles_n));
+  const int n0 = tn * BNc, m0 = tm * BMc;
+
+  const ConvGeom& cv = P.cv;
+  const int HW = cv.howo.d, OW = cv.wo_div.d;
+  const int KT = cv.C >> 4;                      // K-tiles of 16 channels (>= 1, host)
+  const uint32_t PL = static_cast<uint32_t>(cv.H * cv.W * 48);  // bytes per octet plane of the packed input
+  Epi ep = P.e;
+  if (z > 0) {
+    ep.C += z * P.grp_c;
+    if (ep.bias) ep.bias += z * P.grp_bias;
+  }
+  // this group's octets start at octet z C/8 of every image
+  const uint16_t* xg = xpack + (int64_t)z * (cv.C >> 3) * (PL >> 1);
+  const int4v xrsrc = make_rsrc(reinterpret_cast<const float*>(xg), xrange - static_cast<uint32_t>(z * (cv.C >> 3)) * PL);
+
+  // patch: positions n0 .. plast cover images img0 .. img0 + nseg - 1 (<= 3);
+  // segment s holds output rows f_s .. l_s of its image plus the KH - 1 halo
+  const int plast = min(n0 + BNc, P.N) - 1;
+  const int img0 = n0 / HW, nseg = plast / HW - img0 + 1;
+  const int f0 = (n0 - img0 * HW) / OW;
+  auto seg_last = [&](int s) { return s == nseg - 1 ? (plast - (img0 + s) * HW) / OW : cv.Ho - 1; };
+  const int p1 = seg_last(0) - f0 + KH;
+  const int p2 = p1 + (nseg > 1 ? seg_last(1) + KH : 0);
+  const int R = p2 + (nseg > 2 ? seg_last(2) + KH : 0);
+  const int PW = cv.W + 2 * cv.pw;
+  // LDS stage = [octet h][patch row: rpc chunks = positions x 3 terms + pad];
+  // chunk c (16 B) of piece i of this wave = DMA lane's slot
+  uint32_t poff[PD];
+#pragma unroll
+  for (int i = 0; i < PD; ++i) {
+    const int c = (wave * PD + i) * 64 + lane;
+    const int h = c / (octb >> 4), rem = c - h * (octb >> 4);
+    const int prow = rem / rpc, pc = rem - prow * rpc;
+    const int pcol = pc / 3, t = pc - pcol * 3;
+    uint32_t off = 0x80000000u;
+    if (h < 2 && prow < R && pcol < PW) {
+      const int sg = prow >= p2 ? 2 : prow >= p1 ? 1 : 0;
+      const int y = (sg == 0 ? f0 + prow : prow - (sg == 1 ? p1 : p2)) - cv.ph;
+      const int x = pcol - cv.pw;
+      if (y >= 0 && y < cv.H && x >= 0 && x < cv.W)
+        off = static_cast<uint32_t>(img0 + sg) * static_cast<uint32_t>(ximg) + static_cast<uint32_t>(h) * PL +
+              static_cast<uint32_t>((y * cv.W + x) * 48 + t * 16);
+    }
+    poff[i] = off;
+  }
+  // B fragment bases (bytes into a stage) of this lane's column in block j
+  int bb[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int n = min(n0 + wc * 32 * NB + 32 * j + lr, plast);
+    const int img = n / HW, sp = n - img * HW;
+    const int oh = sp / OW, ow = sp - oh * OW;
+    const int sg = img - img0;
+    const int prow = sg == 0 ? oh - f0 : (sg == 1 ? p1 : p2) + oh;
+    bb[j] = lh * octb + prow * rpc * 16 + ow * 48;
+  }
+  // this wave's weight fragment stream (group q = kt T + s at byte
+  // q 3072 + t 1024), LDS-DMA'd D groups ahead into a wave-private ring of
+  // NSA slots: every global access of the loop is an LDS-DMA whose
+  // completion is counted by hand (vmcnt), so no compiler-placed vmcnt(0)
+  // waits on the patch pieces in flight
+  const int Q = KT * T;
+  const int4v arsrc = make_rsrc(
+      reinterpret_cast<const float*>(wpack + ((int64_t)((z * P.tiles_m + tm) * WR + wr) * KT) * T * cbx6::FRAG),
+      static_cast<uint32_t>(Q * 3072));
+  const uint32_t aring = lds0 + static_cast<uint32_t>(2 * SFB + wave * NSA * 3072);
+  const char* aring_p = smem + 2 * SFB + wave * NSA * 3072 + lane * 16;
+  const uint32_t lane16 = static_cast<uint32_t>(lane * 16);
+
+  floatx16 acc[1][NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[0][j][r] = 0.0f;
+
+  auto issue = [&](int kt, int stg, int i) {
+    dma_b128(xrsrc, poff[i] + static_cast<uint32_t>(kt) * 2u * PL,
+             lds0 + static_cast<uint32_t>(stg * SFB + (wave * PD + i) * 1024));
+  };
+  auto issue_a = [&](int q) {
+    const uint32_t sl = aring + static_cast<uint32_t>(q % NSA) * 3072u;
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+      dma_b128(arsrc, lane16 + static_cast<uint32_t>(q * 3072 + t * 1024), sl + static_cast<uint32_t>(t * 1024));
+  };
+  x6::bf16x8 fa[2][3], fb[2][3];
+  auto read_a = [&](x6::bf16x8 (&f)[3], int q) {
+    const char* p = aring_p + (q % NSA) * 3072;
+#pragma unroll
+    for (int t = 0; t < 3; ++t) f[t] = *reinterpret_cast<const x6::bf16x8*>(p + 1024 * t);
+  };
+  auto read_b = [&](x6::bf16x8 (&f)[3], const char* st, int s, int j) {
+    const int kh = s / KW, kw = s - kh * KW;
+    const char* p = st + bb[j] + kh * rpc * 16 + kw * 48;
+#pragma unroll
+    for (int t = 0; t < 3; ++t) f[t] = *reinterpret_cast<const x6::bf16x8*>(p + 16 * t);
+  };
+
+#pragma unroll
+  for (int i = 0; i < PD; ++i) issue(0, 0, i);
+#pragma unroll
+  for (int d = 0; d < D; ++d) issue_a(d);  // Q >= T > D
+  wait_vm<0>();
+  __builtin_amdgcn_s_barrier();
+  read_a(fa[0], 0);
+  read_b(fb[0], smem, 0, 0);
+
+  // one K-tile; PAR: parity of its first group's weight fragments; MORE: K-tile kt + 1 exists
+  auto ktile = [&](int kt, auto par_c, auto more_c) {
+    constexpr int PAR = decltype(par_c)::value;
+    constexpr bool MORE = decltype(more_c)::value;
+    const char* cur = smem + (kt & 1) * SFB;
+    const char* nxt = smem + ((kt + 1) & 1) * SFB;
+#pragma unroll
+    for (int s = 0; s < T; ++s) {
+      const int pa = (s + PAR) & 1;
+      const int q = kt * T + s;
+      // block 0: weights of group q + D, then the patch pieces of K-tile
+      // kt + 1 for this tap
+      if (MORE || s + D < T) issue_a(q + D);
+      if (MORE) {
+#pragma unroll
+        for (int i = cbx6::piece_lo(s, PD, T); i < cbx6::piece_lo(s + 1, PD, T); ++i) issue(kt + 1, (kt + 1) & 1, i);
+      }
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const bool last = s == T - 1 && j == NB - 1;
+        if (j == NB - 1 && (s + 1 < T || MORE)) {
+          // group q + 1's weights have landed: at most n_after(...) younger
+          // operations may still be in flight
+          const int na = cbx6::after_a(s, PD, T, D, MORE);
+          if (last && MORE) {
+            wait_vm_n(min(na, cbx6::after_patch(PD, T)));
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+          } else {
+            wait_vm_n(na);
+          }
+          read_a(fa[pa ^ 1], q + 1);
+        }
+        if (!last)
+          read_b(fb[(j + 1) & 1], cur, j + 1 < NB ? s : s + 1, j + 1 < NB ? j + 1 : 0);
+        else if (MORE)
+          read_b(fb[0], nxt, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);  // the reads go out ahead of this block's MFMAs
+        acc[0][j] = x6::mfma6(x6::Parts{fa[pa][0], fa[pa][1], fa[pa][2]},
+                              x6::Parts{fb[j & 1][0], fb[j & 1][1], fb[j & 1][2]}, acc[0][j]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  using P0 = std::integral_constant<int, 0>;
+  using P1 = std::integral_constant<int, 1>;
+  if constexpr (T % 2 == 0) {
+    int kt = 0;
+    for (; kt + 1 < KT; ++kt) ktile(kt, P0{}, T_{});
+    ktile(kt, P0{}, F_{});
+  } else {
+    int kt = 0;
+    for (; kt + 2 < KT; kt += 2) {
+      ktile(kt, P0{}, T_{});
+      ktile(kt + 1, P1{}, T_{});
+    }
+    if (kt + 1 < KT) {
+      ktile(kt, P0{}, T_{});
+      ktile(kt + 1, P1{}, F_{});
+    } else {
+      ktile(kt, P0{}, F_{});
+    }
+  }
+  gemm_epilogue<1, NB, OUT_NCHW>(acc, P, ep, nullptr, m0 + 32 * wr, n0 + wc * 32 * NB, lr, lh);
+}
+
+// x [img][C][H][W] fp32 -> bf16 terms [img][C/8][H][W][3][8] (k_conv_cb_x6's
+// input).  One thread per (image, octet, position): 8 strided loads (coalesced
+// across the threads), 48 bytes out.
+__global__ void __launch_bounds__(256) k_pack_octets_x6(const float* __restrict__ x, char* __restrict__ out, int C8,
+                                                        int HWi, int units) {
+  for (int u = blockIdx.x * blockDim.x + threadIdx.x; u < units; u += gridDim.x * blockDim.x) {
+    const int r = u / HWi, p = u - r * HWi;  // r = img C8 + octet
+    const float* src = x + (int64_t)r * 8 * HWi + p;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = src[(int64_t)e * HWi];
+    x6::store_terms8(v, out + (int64_t)u * 48);
+  }
+}
+
+// w [G*M][Cg][T] -> fragments [G][tiles_m][WR][Cg/16][T][term][64 lanes][8]:
+// lane (lr, h) of fragment (kt, s) holds row 32 (tm WR + wr) + lr, channels
+// 16 kt + 8 h .. + 7 at tap s.  One thread per (fragment, lane).
+__global__ void __launch_bounds__(256) k_conv_cb_pack_x6(const float* __restrict__ w, char* __restrict__ out, int M,
+                                                         int Cg, int T, int rblocks, int units) {
+  const int KT = Cg >> 4;
+  for (int u = blockIdx.x * blockDim.x + threadIdx.x; u < units; u += gridDim.x * blockDim.x) {
+    const int lane = u & 63;
+    int r = u >> 6;
+    const int s = r % T;
+    r /= T;
+    const int kt = r % KT;
+    r /= KT;
+    const int rb = r % rblocks;  // tm WR + wr
+    const int g = r / rblocks;
+    const int m = rb * 32 + (lane & 31), c0 = kt * 16 + (lane >> 5) * 8;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      v[e] = m < M ? w[((int64_t)g * M + m) * Cg * T + (int64_t)(c0 + e) * T + s] : 0.0f;
+    x6::Parts t;
+    x6::split8(v, t);
+    char* f = out + (int64_t)(u >> 6) * 3072 + lane * 16;
+    *reinterpret_cast<x6::bf16x8*>(f) = t.h;
+    *reinterpret_cast<x6::bf16x8*>(f + 1024) = t.m;
+    *reinterpret_cast<x6::bf16x8*>(f + 2048) = t.l;
+  }
+}
+
+
+// ---------------------------------------------------------------------------
 // k_conv_wide_x6: a large-kernel, strided, unpadded convolution with few input
 // channels (AlexNet conv1: 3 x 11 x 11, stride 4, 96 filters) on the bf16x6
 // engine.  All input channels of a 256-position tile stay resident in LDS as
@@ -906,12 +1215,146 @@ bool conv_x6_plan(const rram_conv_desc* d, ConvPlan& pl) {
   return total * 2 < (1ll << 31);
 }
 
+// ---- k_conv_cb_x6 (channel-octet pre-split activations) ----
+// RRAM_CONV_CB = 0 leaves these shapes to k_conv_patch_x6 (A/B switch)
+bool conv_cb_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("RRAM_CONV_CB");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+struct CbPlan {
+  int WR, NB, RPC, PD, octb, tiles_m, tiles_n;
+};
+// instantiated (KH, WR, NB, PD) combinations
+#define RRAM_CB_LIST(X)                                                                                      \
+  X(5, 4, 8, 15) X(5, 4, 4, 12) X(5, 4, 4, 14) X(5, 2, 4, 14) X(3, 4, 8, 12) X(3, 4, 8, 15) X(3, 4, 4, 8) \
+  X(3, 4, 4, 12) X(3, 2, 4, 12) X(3, 2, 4, 14)
+bool cb_instantiated(int KH, int WR, int NB, int PD) {
+#define RRAM_X(kh, wr, nb, pd) \
+  if (KH == kh && WR == wr && NB == nb && PD == pd) return true;
+  RRAM_CB_LIST(RRAM_X)
+#undef RRAM_X
+  return false;
+}
+bool conv_cb_plan(const rram_conv_desc* d, CbPlan& pl) {
+  const int KH = d->kernel_h, KW = d->kernel_w;
+  if (d->stride_h != 1 || d->stride_w != 1 || d->dilation_h != 1 || d->dilation_w != 1) return false;
+  if (!((KH == 3 && KW == 3) || (KH == 5 && KW == 5))) return false;
+  const int G = d->group, Cg = d->channels / G, M = d->num_output / G;
+  const int HW = d->out_h * d->out_w, OW = d->out_w, OH = d->out_h, N = d->num * HW;
+  if (Cg % 16 != 0 || M == 0 || HW < 64) return false;
+  const int PW = d->width + 2 * d->pad_w;
+  // row pitch in 16-byte chunks: >= 3 PW, = 3 OW (mod 16) (bank-conflict-free reads)
+  int RPC = 3 * PW;
+  while ((RPC - 3 * OW) % 16 != 0) ++RPC;
+  // packed input < 2 GB (32-bit buffer offsets)
+  if ((int64_t)d->num * d->channels * d->height * d->width * 6 >= (1ll << 31)) return false;
+  // tile (WR, NB) with the least makespan (rounds of 256 workgroups x tile
+  // area); ties: taller tiles (weights fetched by one wave)
+  static const int cfg[3][2] = {{4, 8}, {4, 4}, {2, 4}};
+  int64_t best = -1;
+  for (const auto& c : cfg) {
+    const int WR = c[0], NB = c[1], BM = 32 * WR, BN = 32 * NB * (4 / WR);
+    const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+    if ((tiles_m * BM - M) * 4 > tiles_m * BM) continue;  // > 1/4 padded rows
+    const int rmax = patch_rows(N, HW, OW, OH, KH, BN, 3);
+    if (rmax < 0) continue;
+    const int octb = rmax * RPC * 16;
+    const int need = (2 * octb / 16 + 255) / 256;  // 1 KB pieces per wave
+    int PD = 0;
+    for (int p : {8, 12, 14, 15})
+      if (PD == 0 && p >= need && cb_instantiated(KH, WR, NB, p)) PD = p;
+    if (PD == 0) continue;
+    const int64_t nwg = (int64_t)G * tiles_m * tiles_n;
+    if (nwg >= (1ll << 31)) continue;
+    const int64_t cost = (nwg + 255) / 256 * BM * BN;
+    if (best < 0 || cost < best) {
+      best = cost;
+      pl = CbPlan{WR, NB, RPC, PD, octb, tiles_m, tiles_n};
+    }
+  }
+  return best > 0;
+}
+
+int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const float* bias, float* y, int relu,
+                   hipStream_t s) {
+  if (!conv_cb_enabled()) return 0;
+  CbPlan pl;
+  if (!conv_cb_plan(d, pl)) return 0;
+  const int KH = d->kernel_h, KW = d->kernel_w, T = KH * KW;
+  const int G = d->group, Cg = d->channels / G, M = d->num_output / G;
+  const int HW = d->out_h * d->out_w, HWi = d->height * d->width;
+  Params P{};
+  P.M = M;
+  P.N = d->num * HW;
+  P.K = Cg * T;
+  P.split = 1;
+  ConvGeom& cv = P.cv;
+  cv.C = Cg;
+  cv.H = d->height;
+  cv.W = d->width;
+  cv.KH = KH;
+  cv.KW = KW;
+  cv.ph = d->pad_h;
+  cv.pw = d->pad_w;
+  cv.sh = cv.sw = cv.dh = cv.dw = 1;
+  cv.Ho = d->out_h;
+  cv.Wo = d->out_w;
+  cv.howo = make_fastdiv(HW);
+  cv.wo_div = make_fastdiv(d->out_w);
+  P.e = make_epi(y, HW, 1.0f, 0.0f, bias, RRAM_BIAS_ROW, relu);
+  P.e.cimg = (int64_t)d->num_output * HW;
+  P.e.hw = make_fastdiv(HW);
+  P.grp_c = (int64_t)M * HW;
+  P.grp_bias = M;
+  P.tiles_m = pl.tiles_m;
+  P.tiles_n = pl.tiles_n;
+  P.tiles_z = G;
+  // one scratch buffer: packed input, then the weight fragments
+  const int64_t xbytes = (int64_t)d->num * d->channels * HWi * 6;
+  const int rblocks = pl.tiles_m * pl.WR;
+  const int64_t wfrags = (int64_t)G * rblocks * (Cg / 16) * T;
+  const int64_t xb_al = (xbytes + 255) / 256 * 256;
+  char* buf = reinterpret_cast<char*>(pack_buffer(static_cast<size_t>((xb_al + wfrags * 3072) / 4), s));
+  RRAM_REQUIRE(buf != nullptr, "conv: packed-operand buffer allocation failed");
+  const int xunits = d->num * (d->channels / 8) * HWi;
+  hipLaunchKernelGGL(k_pack_octets_x6, dim3(stream_blocks(xunits)), dim3(256), 0, s, x, buf, d->channels / 8, HWi,
+                     xunits);
+  int rc = launch_status("conv input pack x6");
+  if (rc) return rc;
+  const int wunits = static_cast<int>(wfrags * 64);
+  hipLaunchKernelGGL(k_conv_cb_pack_x6, dim3(stream_blocks(wunits)), dim3(256), 0, s, w, buf + xb_al, M, Cg, T,
+                     rblocks, wunits);
+  rc = launch_status("conv weight pack x6 (octets)");
+  if (rc) return rc;
+  const auto* wp = reinterpret_cast<const x6::bf16x8*>(buf + xb_al);
+  const auto* xp = reinterpret_cast<const uint16_t*>(buf);
+  const int ximg = d->channels / 8 * HWi * 48;
+  const unsigned nwg = static_cast<unsigned>((int64_t)G * pl.tiles_m * pl.tiles_n);
+  const uint32_t xrange = static_cast<uint32_t>(xbytes);  // whole packed input (the kernel narrows it per group)
+#define RRAM_X(kh, wr, nb, pd)                                                                                \
+  if (KH == kh && pl.WR == wr && pl.NB == nb && pl.PD == pd) {                                                \
+    hipLaunchKernelGGL((k_conv_cb_x6<kh, kh, wr, nb, pd>), dim3(nwg), dim3(256), 0, s, P, wp, xp, pl.octb, pl.RPC, \
+                       xrange, ximg);                                                                         \
+  } else
+  RRAM_CB_LIST(RRAM_X) { return 0; }
+#undef RRAM_X
+  rc = launch_status("conv cb x6");
+  return rc ? rc : 1;
+}
+
 int conv_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const float* bias, float* y, int relu,
                 hipStream_t s) {
   if (f32_engine().load(std::memory_order_relaxed) != RRAM_ENGINE_BF16X6) return 0;
   if ((reinterpret_cast<uintptr_t>(w) & 3u) != 0) return 0;
   {
     const int rc = conv_wide_x6_fwd(d, x, w, bias, y, relu, s);
+    if (rc != 0) return rc;
+  }
+  {
+    const int rc = conv_cb_x6_fwd(d, x, w, bias, y, relu, s);
     if (rc != 0) return rc;
   }
   ConvPlan pl;
@@ -1065,7 +1508,10 @@ int rram_f32_engine_for_conv(const rram_conv_desc* d) {
   RRAM_REQUIRE(d != nullptr, "engine query: desc is NULL");
   rram::ConvPlan pl;
   rram::WidePlan wpl;
-  return rram::f32_engine().load() == RRAM_ENGINE_BF16X6 && (rram::conv_x6_plan(d, pl) || rram::conv_wide_plan(d, wpl))
+  rram::CbPlan cpl;
+  return rram::f32_engine().load() == RRAM_ENGINE_BF16X6 &&
+                 (rram::conv_x6_plan(d, pl) || rram::conv_wide_plan(d, wpl) ||
+                  (rram::conv_cb_enabled() && rram::conv_cb_plan(d, cpl)))
              ? RRAM_ENGINE_BF16X6
              : RRAM_ENGINE_F32;
 }

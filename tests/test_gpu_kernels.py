@@ -450,6 +450,10 @@ PATCH_CASES = [
     dict(x=(2, 16, 28, 28), cout=224, k=5, p=2, g=1),   # streamed 5x5, M padded to 256
     dict(x=(5, 32, 10, 13), cout=256, k=3, p=1, g=2),   # streamed, 130 positions: tiles over three images
     dict(x=(2, 16, 20, 20), cout=128, k=5, p=0, g=1),   # streamed 5x5 without padding
+    dict(x=(3, 48, 27, 27), cout=256, k=5, p=2, g=2),   # AlexNet conv2 per-group shape: channel-octet x6 kernel, 128 x 256 tiles
+    dict(x=(2, 32, 13, 13), cout=96, k=3, p=1, g=1),    # octet kernel: 96 of 128 rows (row masking), tiles over 2-3 images
+    dict(x=(5, 16, 10, 13), cout=64, k=5, p=2, g=1),    # octet kernel: 5x5, 17-wide padded rows, 130 positions per image
+    dict(x=(3, 64, 13, 13), cout=192, k=3, p=1, g=2),   # octet kernel: 64-row tiles (M = 96 per group), 4 K-tiles
     dict(x=(2, 6, 13, 13), cout=128, k=3, p=1, g=1),    # C % 4 != 0: im2col path
     dict(x=(2, 8, 12, 12), cout=128, k=3, p=0, g=1),    # 100 positions per image: im2col path
 ]
