@@ -274,6 +274,24 @@ int rram_conv_out_shape(rram_conv_desc* d);
 int rram_conv2d_fwd(const rram_conv_desc* d, const float* x, const float* w,
                     const float* bias, float* y, int relu, rram_stream_t stream);
 
+/* rram_conv2d_fwd with channel-octet companions (no reference counterpart:
+ * an inference-time layout of this build).  The octet companion of an NCHW
+ * fp32 tensor [num][C][H][W] (C % 8 == 0) is [num][C/8][H][W][3][8] bf16:
+ * the exact three-term bf16 split (x = xh + xm + xl) of 8 consecutive
+ * channels at one position, the operand form of the bf16x6 convolution.
+ *   x_oct  NULL, or x's companion (saves the convolution its input pack);
+ *   y_oct  NULL, or num*num_output*out_h*out_w*6 bytes that receive y's
+ *          companion (written by the convolution's epilogue when the
+ *          channel-octet kernel runs, else packed from y).
+ * y is bit-identical to rram_conv2d_fwd's. */
+int rram_conv2d_fwd_octets(const rram_conv_desc* d, const float* x, const void* x_oct, const float* w,
+                           const float* bias, float* y, void* y_oct, int relu, rram_stream_t stream);
+/* 1 when rram_conv2d_fwd_octets would read an x_oct for this shape now. */
+int rram_conv_input_octets(const rram_conv_desc* d);
+/* oct = the octet companion of x (channels % 8 == 0). */
+int rram_pack_octets(const float* x, void* oct, int num, int channels, int height, int width,
+                     rram_stream_t stream);
+
 /* Matrix-core engine of the fp32 forward contractions (no reference
  * counterpart: the reference's engine is cuBLAS SGEMM, math_functions.cu:13-27).
  *   RRAM_ENGINE_F32    v_mfma_f32_32x32x2_f32 (fp32 operands).
@@ -379,6 +397,13 @@ int rram_lrn_maxpool_fwd(const float* x, float* y, int num, int channels, int he
                          int pooled_h, int pooled_w, int kernel, int stride_h, int stride_w,
                          int pad_h, int pad_w, int size, float alpha, float beta, float k,
                          rram_stream_t s);
+
+/* rram_lrn_maxpool_fwd that also writes y's channel-octet companion
+ * (y_oct nullable; channels % 8 == 0), see rram_conv2d_fwd_octets. */
+int rram_lrn_maxpool_fwd_octets(const float* x, float* y, void* y_oct, int num, int channels, int height,
+                                int width, int pooled_h, int pooled_w, int kernel, int stride_h, int stride_w,
+                                int pad_h, int pad_w, int size, float alpha, float beta, float k,
+                                rram_stream_t s);
 
 /* Softmax over `channels` for [outer][channels][inner]. */
 int rram_softmax_fwd(const float* x, float* y, int outer, int channels, int inner, rram_stream_t s);

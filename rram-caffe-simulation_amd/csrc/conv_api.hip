@@ -23,6 +23,9 @@ int col2im_core(const float* col, int64_t ldcol, int nimg, const rram_conv_desc*
 int gemv_core(int trans, int M, int N, float alpha, const float* A, const float* x, float beta,
               float* y, hipStream_t s);
 int release_conv_tables();
+int conv_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, const float* w, const float* bias,
+                float* y, void* y_oct, int relu, hipStream_t s);
+int pack_octets(const float* x, void* oct, int num, int C, int HWi, hipStream_t s);
 std::atomic<int>& f32_engine();
 
 namespace {
@@ -155,6 +158,24 @@ int rram_conv2d_fwd(const rram_conv_desc* d_in, const float* x, const float* w, 
   RRAM_REQUIRE(x && w && y, "conv2d_fwd: NULL pointer");
   RRAM_REQUIRE((int64_t)d.num * d.out_h * d.out_w < (1ll << 31), "conv2d_fwd: too many output positions");
   return conv_fwd_core(&d, x, w, bias, y, relu, as_stream(s));
+}
+
+int rram_conv2d_fwd_octets(const rram_conv_desc* d_in, const float* x, const void* x_oct, const float* w,
+                           const float* bias, float* y, void* y_oct, int relu, rram_stream_t s) {
+  rram_conv_desc d = *d_in;
+  int rc = rram_conv_out_shape(&d);
+  if (rc) return rc;
+  if (d.num == 0) return RRAM_OK;
+  RRAM_REQUIRE(x && w && y, "conv2d_fwd_octets: NULL pointer");
+  RRAM_REQUIRE((int64_t)d.num * d.out_h * d.out_w < (1ll << 31), "conv2d_fwd_octets: too many output positions");
+  RRAM_REQUIRE(x_oct == nullptr || d.channels % 8 == 0, "conv2d_fwd_octets: input octets need channels %% 8 == 0");
+  RRAM_REQUIRE(y_oct == nullptr || d.num_output % 8 == 0, "conv2d_fwd_octets: output octets need num_output %% 8 == 0");
+  rc = conv_x6_fwd(&d, x, x_oct, w, bias, y, y_oct, relu, as_stream(s));
+  if (rc < 0) return rc;
+  if (rc > 0) return RRAM_OK;
+  rc = conv_fwd_core(&d, x, w, bias, y, relu, as_stream(s));
+  if (rc == 0 && y_oct != nullptr) rc = pack_octets(y, y_oct, d.num, d.num_output, d.out_h * d.out_w, as_stream(s));
+  return rc;
 }
 
 namespace {

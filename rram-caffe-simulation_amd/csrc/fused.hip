@@ -5,6 +5,7 @@
 #include <math.h>
 
 #include "rram_common.hpp"
+#include "split3.hpp"
 
 namespace rram {
 namespace {
@@ -29,14 +30,20 @@ constexpr int kBandPix = 512;  // input pixels per band (PPT = 2 per thread)
 
 // G channels per barrier; the loads run one group ahead.  Measured on MI355X
 // (AlexNet b256): G = 2 for norm1 (55 x 55 planes), G = 4 for norm2 (27 x 27).
-template <int K, int SIZE, int G>
+// OCT: also write y's channel-octet companion yo (the next convolution's
+// pre-split input, x6.hip k_pack_octets_x6 layout [num][C/8][PH][PW][3][8]
+// bf16): the pooled values of 8 channels are gathered in an LDS plane and
+// split by the band's output threads (C % 8 == 0).
+template <int K, int SIZE, int G, bool OCT>
 __global__ void __launch_bounds__(256)
-    k_lrn_maxpool_band(const float* __restrict__ x, float* __restrict__ y, int C, int H, int W, int PH, int PW,
-                       int sh, int sw, int ph, int pw, int RB, float alpha_over_size, float beta, float k) {
+    k_lrn_maxpool_band(const float* __restrict__ x, float* __restrict__ y, char* __restrict__ yo, int C, int H, int W,
+                       int PH, int PW, int sh, int sw, int ph, int pw, int RB, float alpha_over_size, float beta,
+                       float k) {
   constexpr int PRE = (SIZE - 1) / 2;
   constexpr int D = G;
   constexpr int PPT = kBandPix / 256;
   __shared__ float ybuf[2][D][kBandPix];
+  __shared__ float obuf[OCT ? 8 : 1][OCT ? 256 : 1];
   const int n = blockIdx.y;
   const int pr0 = blockIdx.x * RB;
   const int pr1 = min(PH, pr0 + RB);
@@ -139,6 +146,7 @@ __global__ void __launch_bounds__(256)
             if (ok && v > mv) mv = v;
           }
         yn[(int64_t)(c0 + d) * PHW + it_out[i]] = mv;
+        if (OCT) obuf[(c0 + d) & 7][it_out[i] - pr0 * PW] = mv;
       }
     }
 #pragma unroll
@@ -149,9 +157,31 @@ __global__ void __launch_bounds__(256)
       for (int d = 0; d < D; ++d) win[q][SIZE + d] = fill_from[d][q];
     }
   };
-  for (int c0 = 0; c0 < C; c0 += 2 * D) {
-    group(c0, ybuf[0], st0, st1);
-    if (c0 + D < C) group(c0 + D, ybuf[1], st1, st0);
+  if (!OCT) {
+    for (int c0 = 0; c0 < C; c0 += 2 * D) {
+      group(c0, ybuf[0], st0, st1);
+      if (c0 + D < C) group(c0 + D, ybuf[1], st1, st0);
+    }
+    return;
+  }
+  // OCT: 8 channels per step (an even number of groups), then the octet
+  char* yon = yo + (int64_t)n * (C / 8) * PHW * 48;
+  for (int c0 = 0; c0 < C; c0 += 8) {
+#pragma unroll
+    for (int g = 0; g < 8; g += 2 * D) {
+      group(c0 + g, ybuf[0], st0, st1);
+      group(c0 + g + D, ybuf[1], st1, st0);
+    }
+    __syncthreads();  // obuf complete (the next group's barrier orders its rewrite)
+    const int o = threadIdx.x;
+    if (o < NO) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = obuf[e][o];
+      const int prl = o / PW;
+      const int64_t out = (int64_t)(pr0 + prl) * PW + (o - prl * PW);
+      x6::store_terms8(v, yon + ((int64_t)(c0 / 8) * PHW + out) * 48);
+    }
   }
 }
 
@@ -165,6 +195,14 @@ extern "C" {
 int rram_lrn_maxpool_fwd(const float* x, float* y, int num, int C, int H, int W, int PH, int PW,
                          int kernel, int sh, int sw, int ph, int pw, int size, float alpha, float beta,
                          float k, rram_stream_t s) {
+  return rram_lrn_maxpool_fwd_octets(x, y, nullptr, num, C, H, W, PH, PW, kernel, sh, sw, ph, pw, size, alpha, beta,
+                                     k, s);
+}
+
+int rram_lrn_maxpool_fwd_octets(const float* x, float* y, void* y_oct, int num, int C, int H, int W, int PH, int PW,
+                                int kernel, int sh, int sw, int ph, int pw, int size, float alpha, float beta,
+                                float k, rram_stream_t s) {
+  RRAM_REQUIRE(y_oct == nullptr || C % 8 == 0, "lrn_maxpool_fwd_octets: octets need channels %% 8 == 0");
   RRAM_REQUIRE(num >= 0 && C > 0 && H > 0 && W > 0 && PH > 0 && PW > 0 && sh > 0 && sw > 0 && ph >= 0 &&
                    pw >= 0,
                "lrn_maxpool_fwd: bad geometry");
@@ -188,18 +226,26 @@ int rram_lrn_maxpool_fwd(const float* x, float* y, int num, int C, int H, int W,
   const dim3 grid(static_cast<unsigned>((PH + rb - 1) / rb), static_cast<unsigned>(num));
   const float aos = alpha / size;
   const bool big = H * W >= 1024;
-#define RRAM_LP(K_, S_)                                                                                     \
-  if (kernel == K_ && size == S_) {                                                                         \
-    if (big)                                                                                                \
-      hipLaunchKernelGGL((k_lrn_maxpool_band<K_, S_, 2>), grid, dim3(kThreads), 0, as_stream(s), x, y, C, H, \
-                         W, PH, PW, sh, sw, ph, pw, rb, aos, beta, k);                                      \
-    else                                                                                                    \
-      hipLaunchKernelGGL((k_lrn_maxpool_band<K_, S_, 4>), grid, dim3(kThreads), 0, as_stream(s), x, y, C, H, \
-                         W, PH, PW, sh, sw, ph, pw, rb, aos, beta, k);                                      \
+  char* yo = static_cast<char*>(y_oct);
+#define RRAM_LP2(K_, S_, G_)                                                                                  \
+  if (yo)                                                                                                     \
+    hipLaunchKernelGGL((k_lrn_maxpool_band<K_, S_, G_, true>), grid, dim3(kThreads), 0, as_stream(s), x, y, yo, \
+                       C, H, W, PH, PW, sh, sw, ph, pw, rb, aos, beta, k);                                    \
+  else                                                                                                        \
+    hipLaunchKernelGGL((k_lrn_maxpool_band<K_, S_, G_, false>), grid, dim3(kThreads), 0, as_stream(s), x, y,    \
+                       yo, C, H, W, PH, PW, sh, sw, ph, pw, rb, aos, beta, k);
+#define RRAM_LP(K_, S_)          \
+  if (kernel == K_ && size == S_) { \
+    if (big) {                   \
+      RRAM_LP2(K_, S_, 2)        \
+    } else {                     \
+      RRAM_LP2(K_, S_, 4)        \
+    }                            \
   }
   RRAM_LP(3, 5)
   else RRAM_LP(3, 3) else RRAM_LP(2, 5) else RRAM_LP(2, 3)
 #undef RRAM_LP
+#undef RRAM_LP2
   return launch_status("lrn_maxpool_fwd");
 }
 

@@ -1575,8 +1575,8 @@ std::map<std::pair<int, hipStream_t>, std::pair<float*, size_t>>& pack_cache() {
   static std::map<std::pair<int, hipStream_t>, std::pair<float*, size_t>> cache;
   return cache;
 }
-int conv_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const float* bias, float* y, int relu,
-                hipStream_t s);
+int conv_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, const float* w, const float* bias,
+                float* y, void* y_oct, int relu, hipStream_t s);
 
 float* pack_buffer(size_t floats, hipStream_t s) {
   int dev = 0;
@@ -1696,7 +1696,7 @@ int conv_patch_fwd(const rram_conv_desc* d, const float* w, Params& P, hipStream
 int conv_fwd_core(const rram_conv_desc* d, const float* x, const float* w, const float* bias,
                   float* y, int relu, hipStream_t s) {
   {
-    const int rc = conv_x6_fwd(d, x, w, bias, y, relu, s);  // x6.hip
+    const int rc = conv_x6_fwd(d, x, nullptr, w, bias, y, nullptr, relu, s);  // x6.hip
     if (rc != 0) return rc < 0 ? rc : RRAM_OK;
   }
   const int g = d->group;

@@ -8,6 +8,7 @@
 #include <type_traits>
 
 #include "gemm_common.hpp"
+#include "split3.hpp"
 
 namespace rram {
 namespace {
@@ -35,47 +36,6 @@ namespace {
 // k = 8h + j of the 32x32x16 operand).  Padded steps have zero weights and
 // read no activations.
 namespace x6 {
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef float float2v __attribute__((ext_vector_type(2)));
-struct Parts {
-  bf16x8 h, m, l;
-};
-// exact three-term split of 8 floats (round to nearest even at each step)
-__device__ __forceinline__ void split8(const float (&x)[8], Parts& r) {
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const float2v v = {x[2 * p], x[2 * p + 1]};
-    const bf16x2 h = __builtin_convertvector(v, bf16x2);
-    const float2v r1 = v - __builtin_convertvector(h, float2v);
-    const bf16x2 m = __builtin_convertvector(r1, bf16x2);
-    const float2v r2 = r1 - __builtin_convertvector(m, float2v);
-    const bf16x2 l = __builtin_convertvector(r2, bf16x2);
-    r.h[2 * p] = h[0];
-    r.h[2 * p + 1] = h[1];
-    r.m[2 * p] = m[0];
-    r.m[2 * p + 1] = m[1];
-    r.l[2 * p] = l[0];
-    r.l[2 * p + 1] = l[1];
-  }
-}
-// term p (0 = high, 1 = middle, 2 = low) of the split of v, as bf16 bits
-__device__ __forceinline__ uint16_t split_term(float v, int p) {
-  const __bf16 h = static_cast<__bf16>(v);
-  const float r1 = v - static_cast<float>(h);
-  const __bf16 m = static_cast<__bf16>(r1);
-  const __bf16 l = static_cast<__bf16>(r1 - static_cast<float>(m));
-  const __bf16 t = p == 0 ? h : p == 1 ? m : l;
-  return __builtin_bit_cast(uint16_t, t);
-}
-// the three bf16 terms of 8 floats as 3 x 16 bytes at dst (16-byte aligned)
-__device__ __forceinline__ void store_terms8(const float (&v)[8], char* dst) {
-  Parts t;
-  split8(v, t);
-  *reinterpret_cast<bf16x8*>(dst) = t.h;
-  *reinterpret_cast<bf16x8*>(dst + 16) = t.m;
-  *reinterpret_cast<bf16x8*>(dst + 32) = t.l;
-}
 __device__ __forceinline__ floatx16 mfma6(const Parts& a, const Parts& b, floatx16 c) {
   c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.l, b.h, c, 0, 0, 0);
   c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.l, c, 0, 0, 0);
@@ -385,7 +345,7 @@ __device__ __forceinline__ void wait_vm_n(int n) {
 template <int KH, int KW, int WR, int NB, int PD>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __restrict__ xpack, int octb, int rpc,
-             uint32_t xrange, int ximg) {
+             uint32_t xrange, int ximg, char* __restrict__ yoct, int cout8) {
   using namespace g2;
   constexpr int T = KH * KW, WC = 4 / WR, BMc = 32 * WR, BNc = 32 * NB * WC, SFB = PD * 4 * 1024;
   constexpr int D = cbx6::dist(NB), NSA = D + 1;
@@ -580,6 +540,42 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
     }
   }
   gemm_epilogue<1, NB, OUT_NCHW>(acc, P, ep, nullptr, m0 + 32 * wr, n0 + wc * 32 * NB, lr, lh);
+  if (yoct != nullptr) {
+    // the output's channel-octet companion (the next convolution's input,
+    // k_pack_octets_x6 layout): the split of the stored values (bias and
+    // ReLU applied; gemm_epilogue folded the bias into acc).  Lane (lr, h)
+    // holds channels 8 k + 4 h .. + 3 of octets k = 0..3 of its 32 rows; the
+    // two halves trade halves (lane ^ 32) so that half 0 owns octets 0, 1 and
+    // half 1 octets 2, 3, whole.
+    const int mw = m0 + 32 * wr;
+    const bool relu = ep.relu != 0;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int n = n0 + wc * 32 * NB + 32 * j + lr;
+      float o[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[r] = relu ? fmaxf(acc[0][j][r], 0.0f) : acc[0][j][r];
+      float rcv[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) rcv[r] = __shfl_xor(lh ? o[r] : o[8 + r], 32);
+      if (n >= P.N) continue;
+      const uint32_t im = fdiv(static_cast<uint32_t>(n), ep.hw);
+      const int sp = n - static_cast<int>(im) * HW;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int k = 2 * lh + u;
+        if (mw + 8 * k >= P.M) continue;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = lh ? rcv[4 * u + e] : o[4 * u + e];
+          v[4 + e] = lh ? o[8 + 4 * u + e] : rcv[4 * u + e];
+        }
+        const int oct = (z * P.M + mw) / 8 + k;
+        x6::store_terms8(v, yoct + (((int64_t)im * cout8 + oct) * HW + sp) * 48);
+      }
+    }
+  }
 }
 
 // x [img][C][H][W] fp32 -> bf16 terms [img][C/8][H][W][3][8] (k_conv_cb_x6's
@@ -1215,6 +1211,16 @@ bool conv_x6_plan(const rram_conv_desc* d, ConvPlan& pl) {
   return total * 2 < (1ll << 31);
 }
 
+// x [num][C][HWi] fp32 -> its octet companion (C % 8 == 0)
+int pack_octets(const float* x, void* oct, int num, int C, int HWi, hipStream_t s) {
+  RRAM_REQUIRE(C % 8 == 0 && (int64_t)num * C * HWi * 6 < (1ll << 31), "pack_octets: C %% 8 != 0 or too large");
+  const int units = num * (C / 8) * HWi;
+  if (units == 0) return RRAM_OK;
+  hipLaunchKernelGGL(k_pack_octets_x6, dim3(stream_blocks(units)), dim3(256), 0, s, x, static_cast<char*>(oct), C / 8,
+                     HWi, units);
+  return launch_status("octet pack x6");
+}
+
 // ---- k_conv_cb_x6 (channel-octet pre-split activations) ----
 // RRAM_CONV_CB = 0 leaves these shapes to k_conv_patch_x6 (A/B switch)
 bool conv_cb_enabled() {
@@ -1278,11 +1284,12 @@ bool conv_cb_plan(const rram_conv_desc* d, CbPlan& pl) {
   return best > 0;
 }
 
-int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const float* bias, float* y, int relu,
-                   hipStream_t s) {
+int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, const float* w, const float* bias,
+                   float* y, void* y_oct, int relu, hipStream_t s) {
   if (!conv_cb_enabled()) return 0;
   CbPlan pl;
   if (!conv_cb_plan(d, pl)) return 0;
+  if (y_oct != nullptr && d->num_output % 8 != 0) return 0;
   const int KH = d->kernel_h, KW = d->kernel_w, T = KH * KW;
   const int G = d->group, Cg = d->channels / G, M = d->num_output / G;
   const int HW = d->out_h * d->out_w, HWi = d->height * d->width;
@@ -1312,32 +1319,33 @@ int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, cons
   P.tiles_m = pl.tiles_m;
   P.tiles_n = pl.tiles_n;
   P.tiles_z = G;
-  // one scratch buffer: packed input, then the weight fragments
+  // one scratch buffer: packed input (unless the caller hands over the
+  // input's octet companion), then the weight fragments
   const int64_t xbytes = (int64_t)d->num * d->channels * HWi * 6;
   const int rblocks = pl.tiles_m * pl.WR;
   const int64_t wfrags = (int64_t)G * rblocks * (Cg / 16) * T;
-  const int64_t xb_al = (xbytes + 255) / 256 * 256;
+  const int64_t xb_al = x_oct != nullptr ? 0 : (xbytes + 255) / 256 * 256;
   char* buf = reinterpret_cast<char*>(pack_buffer(static_cast<size_t>((xb_al + wfrags * 3072) / 4), s));
   RRAM_REQUIRE(buf != nullptr, "conv: packed-operand buffer allocation failed");
-  const int xunits = d->num * (d->channels / 8) * HWi;
-  hipLaunchKernelGGL(k_pack_octets_x6, dim3(stream_blocks(xunits)), dim3(256), 0, s, x, buf, d->channels / 8, HWi,
-                     xunits);
-  int rc = launch_status("conv input pack x6");
-  if (rc) return rc;
+  int rc = 0;
+  if (x_oct == nullptr) {
+    rc = pack_octets(x, buf, d->num, d->channels, HWi, s);
+    if (rc) return rc;
+  }
   const int wunits = static_cast<int>(wfrags * 64);
   hipLaunchKernelGGL(k_conv_cb_pack_x6, dim3(stream_blocks(wunits)), dim3(256), 0, s, w, buf + xb_al, M, Cg, T,
                      rblocks, wunits);
   rc = launch_status("conv weight pack x6 (octets)");
   if (rc) return rc;
   const auto* wp = reinterpret_cast<const x6::bf16x8*>(buf + xb_al);
-  const auto* xp = reinterpret_cast<const uint16_t*>(buf);
+  const auto* xp = reinterpret_cast<const uint16_t*>(x_oct != nullptr ? x_oct : buf);
   const int ximg = d->channels / 8 * HWi * 48;
   const unsigned nwg = static_cast<unsigned>((int64_t)G * pl.tiles_m * pl.tiles_n);
   const uint32_t xrange = static_cast<uint32_t>(xbytes);  // whole packed input (the kernel narrows it per group)
 #define RRAM_X(kh, wr, nb, pd)                                                                                \
   if (KH == kh && pl.WR == wr && pl.NB == nb && pl.PD == pd) {                                                \
     hipLaunchKernelGGL((k_conv_cb_x6<kh, kh, wr, nb, pd>), dim3(nwg), dim3(256), 0, s, P, wp, xp, pl.octb, pl.RPC, \
-                       xrange, ximg);                                                                         \
+                       xrange, ximg, static_cast<char*>(y_oct), d->num_output / 8);                           \
   } else
   RRAM_CB_LIST(RRAM_X) { return 0; }
 #undef RRAM_X
@@ -1345,18 +1353,32 @@ int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, cons
   return rc ? rc : 1;
 }
 
-int conv_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const float* bias, float* y, int relu,
-                hipStream_t s) {
+int conv_patch_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const float* bias, float* y, int relu,
+                      hipStream_t s);
+// The bf16x6 convolution forward.  x_oct: NULL or the octet companion of x
+// (k_pack_octets_x6 layout; the channel-octet kernel then skips its input
+// pack); y_oct: NULL or a buffer that receives y's octet companion (written
+// by the channel-octet kernel's epilogue, else packed from y afterwards).
+// Returns 1 when it ran, 0 when not covered (nothing written), < 0 on error.
+int conv_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, const float* w, const float* bias,
+                float* y, void* y_oct, int relu, hipStream_t s) {
   if (f32_engine().load(std::memory_order_relaxed) != RRAM_ENGINE_BF16X6) return 0;
   if ((reinterpret_cast<uintptr_t>(w) & 3u) != 0) return 0;
   {
-    const int rc = conv_wide_x6_fwd(d, x, w, bias, y, relu, s);
+    const int rc = conv_cb_x6_fwd(d, x, x_oct, w, bias, y, y_oct, relu, s);
     if (rc != 0) return rc;
   }
-  {
-    const int rc = conv_cb_x6_fwd(d, x, w, bias, y, relu, s);
-    if (rc != 0) return rc;
+  int rc = conv_wide_x6_fwd(d, x, w, bias, y, relu, s);
+  if (rc == 0) rc = conv_patch_x6_fwd(d, x, w, bias, y, relu, s);
+  if (rc > 0 && y_oct != nullptr) {
+    const int pr = pack_octets(y, y_oct, d->num, d->num_output, d->out_h * d->out_w, s);
+    if (pr) return pr;
   }
+  return rc;
+}
+
+int conv_patch_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const float* bias, float* y, int relu,
+                      hipStream_t s) {
   ConvPlan pl;
   if (!conv_x6_plan(d, pl)) return 0;
   const int KH = d->kernel_h, KW = d->kernel_w;
@@ -1514,6 +1536,20 @@ int rram_f32_engine_for_conv(const rram_conv_desc* d) {
                   (rram::conv_cb_enabled() && rram::conv_cb_plan(d, cpl)))
              ? RRAM_ENGINE_BF16X6
              : RRAM_ENGINE_F32;
+}
+
+int rram_conv_input_octets(const rram_conv_desc* d) {
+  RRAM_REQUIRE(d != nullptr, "octet query: desc is NULL");
+  rram::CbPlan cpl;
+  return rram::f32_engine().load() == RRAM_ENGINE_BF16X6 && rram::conv_cb_enabled() && rram::conv_cb_plan(d, cpl) ? 1
+                                                                                                                  : 0;
+}
+
+int rram_pack_octets(const float* x, void* oct, int num, int channels, int height, int width, rram_stream_t s) {
+  RRAM_REQUIRE(num >= 0 && channels > 0 && height > 0 && width > 0, "pack_octets: bad shape");
+  if (num == 0) return RRAM_OK;
+  RRAM_REQUIRE(x != nullptr && oct != nullptr, "pack_octets: NULL");
+  return rram::pack_octets(x, oct, num, channels, height * width, rram::as_stream(s));
 }
 
 int rram_f32_engine_for_ip(int M, int N, int K, size_t ws_bytes) {

@@ -29,6 +29,31 @@ void Caffe::synchronize() { HIP_CALL(hipStreamSynchronize(hip_stream())); }
 SyncedMemory::~SyncedMemory() {
   if (own_cpu_ && cpu_ptr_) std::free(cpu_ptr_);
   if (own_gpu_ && gpu_ptr_) (void)hipFree(gpu_ptr_);
+  if (oct_ptr_) (void)hipFree(oct_ptr_);
+}
+
+void* SyncedMemory::octets(size_t bytes) {
+  if (bytes > oct_bytes_) {
+    if (oct_ptr_) {
+      HIP_CALL(hipStreamSynchronize(Caffe::hip_stream()));
+      HIP_CALL(hipFree(oct_ptr_));
+    }
+    oct_ptr_ = nullptr;
+    HIP_CALL(hipMalloc(&oct_ptr_, bytes));
+    oct_bytes_ = bytes;
+    oct_valid_ = false;
+  }
+  return oct_ptr_;
+}
+const void* SyncedMemory::valid_octets(const int (&shape)[4]) const {
+  if (!oct_valid_) return nullptr;
+  for (int i = 0; i < 4; ++i)
+    if (shape[i] != oct_shape_[i]) return nullptr;
+  return oct_ptr_;
+}
+void SyncedMemory::set_octets_valid(const int (&shape)[4]) {
+  for (int i = 0; i < 4; ++i) oct_shape_[i] = shape[i];
+  oct_valid_ = oct_ptr_ != nullptr;
 }
 
 void SyncedMemory::to_cpu() {
@@ -85,17 +110,20 @@ const void* SyncedMemory::gpu_data() {
   return gpu_ptr_;
 }
 void* SyncedMemory::mutable_cpu_data() {
+  oct_valid_ = false;
   to_cpu();
   head_ = HEAD_AT_CPU;
   return cpu_ptr_;
 }
 void* SyncedMemory::mutable_gpu_data() {
+  oct_valid_ = false;
   to_gpu();
   head_ = HEAD_AT_GPU;
   return gpu_ptr_;
 }
 void SyncedMemory::set_cpu_data(void* data) {
   CAFFE_CHECK(data, "set_cpu_data(NULL)");
+  oct_valid_ = false;
   if (own_cpu_ && cpu_ptr_) std::free(cpu_ptr_);
   cpu_ptr_ = data;
   own_cpu_ = false;
@@ -103,6 +131,7 @@ void SyncedMemory::set_cpu_data(void* data) {
 }
 void SyncedMemory::set_gpu_data(void* data) {
   CAFFE_CHECK(data, "set_gpu_data(NULL)");
+  oct_valid_ = false;
   if (own_gpu_ && gpu_ptr_) (void)hipFree(gpu_ptr_);
   gpu_ptr_ = data;
   own_gpu_ = false;

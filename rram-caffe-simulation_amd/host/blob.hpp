@@ -32,6 +32,15 @@ class SyncedMemory {
   SyncedHead head() const { return head_; }
   size_t size() const { return size_; }
 
+  // Channel-octet companion (rram_conv2d_fwd_octets): a device buffer with the
+  // pre-split bf16x3 form of this memory's NCHW contents.  It is valid only
+  // while the data is unchanged since a producer wrote both (every mutable_* /
+  // set_* access invalidates it) and only for the shape it was written for.
+  void* octets(size_t bytes);  // the buffer, grown to `bytes`
+  const void* valid_octets(const int (&shape)[4]) const;
+  void set_octets_valid(const int (&shape)[4]);
+  bool wants_octets = false;  // a consumer would read the companion
+
  private:
   void to_cpu();
   void to_gpu();
@@ -40,6 +49,10 @@ class SyncedMemory {
   size_t size_;
   SyncedHead head_ = UNINITIALIZED;
   bool own_cpu_ = false, own_gpu_ = false;
+  void* oct_ptr_ = nullptr;
+  size_t oct_bytes_ = 0;
+  bool oct_valid_ = false;
+  int oct_shape_[4] = {0, 0, 0, 0};
 };
 
 template <typename Dtype>

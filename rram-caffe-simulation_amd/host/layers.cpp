@@ -2,6 +2,7 @@
 #include "layers.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 
@@ -172,15 +173,56 @@ void ConvolutionLayer<Dtype>::Reshape(const std::vector<Blob<Dtype>*>& bottom,
   desc_.width = bottom[0]->shape(3);
   RRAM_CALL(rram_conv_out_shape(&desc_));
   top[0]->Reshape({desc_.num, desc_.num_output, desc_.out_h, desc_.out_w});
+  const int eng = rram_get_f32_engine();
+  if (desc_.num != oct_key_[0] || desc_.height != oct_key_[1] || desc_.width != oct_key_[2] || eng != oct_key_[3]) {
+    want_in_oct_ = rram_conv_input_octets(&desc_) == 1;
+    oct_key_[0] = desc_.num;
+    oct_key_[1] = desc_.height;
+    oct_key_[2] = desc_.width;
+    oct_key_[3] = eng;
+  }
+  // ask the producer of the input for its octet companion
+  if (want_in_oct_) bottom[0]->data()->wants_octets = true;
+}
+
+// the octet companion a producer writes next to top (nullptr: not wanted)
+// RRAM_OCTETS = 1: producers write the companions their consumers read.
+// Off by default: measured on MI355X (AlexNet b256, per-layer hipEvents),
+// writing the companion in the producer costs about what it saves the
+// consumer (pool1 +35 us / conv2 -39 us, pool2 +13 / conv3 -35, conv3's
+// epilogue +40 / conv4 -35, conv4's +40 / conv5 -32: -11 us per step, 99.6 /
+// 100.0k vs 99.5 / 99.8k images/s), so the convolutions pack their inputs.
+bool octets_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("RRAM_OCTETS");
+    return e && std::atoi(e) != 0;
+  }();
+  return on;
+}
+template <typename Dtype>
+void* octets_for(Blob<Dtype>* top) {
+  SyncedMemory* m = top->data().get();
+  if (!octets_enabled() || !m->wants_octets || top->num_axes() != 4 || top->shape(1) % 8 != 0) return nullptr;
+  return m->octets(static_cast<size_t>(top->count()) * 6);
+}
+template <typename Dtype>
+void mark_octets(Blob<Dtype>* top) {
+  const int shp[4] = {top->shape(0), top->shape(1), top->shape(2), top->shape(3)};
+  top->data()->set_octets_valid(shp);
 }
 
 template <typename Dtype>
 void ConvolutionLayer<Dtype>::Forward_gpu(const std::vector<Blob<Dtype>*>& bottom,
                                           const std::vector<Blob<Dtype>*>& top) {
   CAFFE_CHECK(bottom[0] != top[0], this->name() << ": in-place convolution is not allowed");
-  RRAM_CALL(rram_conv2d_fwd(&desc_, bottom[0]->gpu_data(), this->blobs_[0]->gpu_data(),
-                            bias_term_ ? this->blobs_[1]->gpu_data() : nullptr,
-                            top[0]->mutable_gpu_data(), fused_relu ? 1 : 0, Caffe::stream()));
+  const int shp[4] = {desc_.num, desc_.channels, desc_.height, desc_.width};
+  const void* xo = want_in_oct_ ? bottom[0]->data()->valid_octets(shp) : nullptr;
+  float* y = top[0]->mutable_gpu_data();  // invalidates top's companion
+  void* yo = octets_for(top[0]);
+  RRAM_CALL(rram_conv2d_fwd_octets(&desc_, bottom[0]->gpu_data(), xo, this->blobs_[0]->gpu_data(),
+                                   bias_term_ ? this->blobs_[1]->gpu_data() : nullptr, y, yo, fused_relu ? 1 : 0,
+                                   Caffe::stream()));
+  if (yo) mark_octets(top[0]);
 }
 
 template <typename Dtype>
@@ -355,9 +397,12 @@ class PoolingLayer : public Layer<Dtype> {
  protected:
   void Forward_gpu(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
     if (lrn_src_ != nullptr) {  // LRN folded into this pool (Net::Net, TEST phase)
-      RRAM_CALL(rram_lrn_maxpool_fwd(lrn_src_->gpu_data(), top[0]->mutable_gpu_data(), bottom[0]->shape(0), C_, H_,
-                                     W_, PH_, PW_, kh_, sh_, sw_, ph_, pw_, lrn_size_, lrn_alpha_, lrn_beta_, lrn_k_,
-                                     Caffe::stream()));
+      float* y = top[0]->mutable_gpu_data();
+      void* yo = octets_for(top[0]);
+      RRAM_CALL(rram_lrn_maxpool_fwd_octets(lrn_src_->gpu_data(), y, yo, bottom[0]->shape(0), C_, H_, W_, PH_, PW_,
+                                            kh_, sh_, sw_, ph_, pw_, lrn_size_, lrn_alpha_, lrn_beta_, lrn_k_,
+                                            Caffe::stream()));
+      if (yo) mark_octets(top[0]);
       return;
     }
     int* mask = (method_ == RRAM_POOL_MAX && this->phase_ == TRAIN)

@@ -29,6 +29,9 @@ class ConvolutionLayer : public Layer<Dtype> {
                     const std::vector<Blob<Dtype>*>& bottom) override;
   rram_conv_desc desc_{};
   bool bias_term_ = true;
+  // the forward reads its input's channel-octet companion (cached per input shape / engine)
+  bool want_in_oct_ = false;
+  int oct_key_[4] = {-1, -1, -1, -1};
 };
 
 // ★ InnerProduct (inner_product_layer.cpp:9-141, .cu:9-75).

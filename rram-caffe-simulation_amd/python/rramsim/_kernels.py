@@ -97,6 +97,9 @@ SIGNATURES = {
     "rram_gemv_f32": (I, [I, I, I, F, P, P, F, P, P]),
     "rram_conv_out_shape": (I, [P]),
     "rram_conv2d_fwd": (I, [P, P, P, P, P, I, P]),
+    "rram_conv2d_fwd_octets": (I, [P, P, P, P, P, P, P, I, P]),
+    "rram_conv_input_octets": (I, [P]),
+    "rram_pack_octets": (I, [P, P, I, I, I, I, P]),
     "rram_conv2d_bwd_workspace": (SZ, [P, I]),
     "rram_conv2d_bwd": (I, [P, P, P, P, P, P, P, P, SZ, P]),
     "rram_im2col": (I, [P, I, I, I, I, I, I, I, I, I, I, I, P, P]),
@@ -112,6 +115,7 @@ SIGNATURES = {
     "rram_lrn_within_fwd": (I, [P, P, P, I, I, I, I, I, F, F, P]),
     "rram_lrn_within_bwd": (I, [P, P, P, P, I, I, I, I, I, F, F, P]),
     "rram_lrn_maxpool_fwd": (I, [P, P, I, I, I, I, I, I, I, I, I, I, I, I, F, F, F, P]),
+    "rram_lrn_maxpool_fwd_octets": (I, [P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, F, F, F, P]),
     "rram_softmax_fwd": (I, [P, P, I, I, I, P]),
     "rram_softmax_loss_fwd": (I, [P, P, P, I, I, I, I, P]),
     "rram_softmax_loss_bwd": (I, [P, P, P, I, I, I, I, F, P]),

@@ -188,6 +188,22 @@ def conv2d_fwd(d, x, w, bias, y, relu=False):
                                    _stream()), "conv2d_fwd")
 
 
+def conv2d_fwd_octets(d, x, x_oct, w, bias, y, y_oct, relu=False):
+    """rram_conv2d_fwd with channel-octet companions (x_oct / y_oct: uint8
+    tensors of 6 bytes per element, or None)."""
+    K.check(_lib().rram_conv2d_fwd_octets(C.byref(d), _p(x), _p(x_oct), _p(w), _p(bias), _p(y), _p(y_oct),
+                                          int(relu), _stream()), "conv2d_fwd_octets")
+
+
+def conv_input_octets(d):
+    """1 when rram_conv2d_fwd_octets would read an input companion for d now."""
+    return _lib().rram_conv_input_octets(C.byref(d))
+
+
+def pack_octets(x, oct_, n, c, h, w):
+    K.check(_lib().rram_pack_octets(_p(x), _p(oct_), n, c, h, w, _stream()), "pack_octets")
+
+
 def conv2d_bwd(d, x, w, dy, dw=None, db=None, dx=None, workspace=None):
     wsb = workspace.numel() * workspace.element_size() if workspace is not None else 0
     K.check(_lib().rram_conv2d_bwd(C.byref(d), _p(x), _p(w), _p(dy), _p(dw), _p(db), _p(dx),
@@ -240,6 +256,11 @@ def lrn_bwd(x, y, scale, dy, dx, n, c, h, w, size, alpha, beta):
 def lrn_maxpool_fwd(x, y, n, c, h, w, ph, pw, kernel, stride, pad, size, alpha, beta, k=1.0):
     K.check(_lib().rram_lrn_maxpool_fwd(_p(x), _p(y), n, c, h, w, ph, pw, kernel, stride, stride, pad, pad,
                                         size, alpha, beta, k, _stream()), "lrn_maxpool_fwd")
+
+
+def lrn_maxpool_fwd_octets(x, y, y_oct, n, c, h, w, ph, pw, kernel, stride, pad, size, alpha, beta, k=1.0):
+    K.check(_lib().rram_lrn_maxpool_fwd_octets(_p(x), _p(y), _p(y_oct), n, c, h, w, ph, pw, kernel, stride, stride,
+                                               pad, pad, size, alpha, beta, k, _stream()), "lrn_maxpool_fwd_octets")
 
 
 def lrn_within_fwd(x, y, scale, n, c, h, w, size, alpha, beta):

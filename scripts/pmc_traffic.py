@@ -7,8 +7,8 @@ in KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced
 streaming read, so it is doubled; WRITE_SIZE is exact for 16-B stores.
 
 Per-launch traffic for the injection kernel; per-step traffic for the
-conv/IP GEMM set (all k_gemm* / k_conv_patch* / k_splitk_reduce dispatches /
-forwards run), next to the algorithmic bytes of AlexNet b256's conv1-5 + fc6-8
+conv/IP GEMM set (all k_gemm* / k_conv_* / k_splitk_reduce dispatches and
+the x6 operand packs / forwards run), next to the algorithmic bytes of AlexNet b256's conv1-5 + fc6-8
 (each layer's input activation + weights read once, output written once).
 Writes JSON to stdout (bench.py reads the committed copy in profiles/)."""
 import csv
@@ -28,7 +28,9 @@ for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
             continue
         if "k_inject_batched" in name:
             k = "inject"
-        elif "k_gemm" in name or "k_conv_patch" in name or "k_splitk_reduce" in name:
+        elif any(t in name for t in ("k_gemm", "k_conv_", "k_splitk_reduce", "k_pack_rows_x6", "k_pack_octets_x6")):
+            # every kernel of the conv1-5 + fc6-8 contractions, their operand
+            # packs (weights split per call, inputs split into octets) included
             k = "gemm"
         else:
             continue
