@@ -1,6 +1,7 @@
 // Convolution forward with fp32 products on the bf16 matrix cores
 // (RRAM_ENGINE_BF16X6, include/rram_kernels.h): the LDS-patch convolution of
 // gemm.hip's k_conv_patch re-tiled for v_mfma_f32_32x32x16_bf16.
+#include <stdio.h>
 #include <stdlib.h>
 
 #include <algorithm>
@@ -650,15 +651,20 @@ struct Shape {
 };
 }  // namespace wx6
 
-template <int KH, int KW, int ST, int C, int PFL>
+// GA: the weight fragments come from L2 straight into registers two groups
+// ahead (wpack in fragment order, k_conv_wide_pack_ga_x6): no LDS ring, no
+// barrier in the loop (the patch is loaded once per tile); else the 3-slot
+// LDS ring with one barrier per group.
+template <int KH, int KW, int ST, int C, int PFL, bool GA>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 k_conv_wide_x6(Params P, const uint16_t* __restrict__ wpack, int CHS) {
   using namespace g2;
   using Sh = wx6::Shape<KH, KW, C>;
   constexpr int G = Sh::G, MI = 3;
   constexpr int PATCH_B = PFL * 4;
-  static_assert(PATCH_B + wx6::NSLOT * wx6::SLOT_REGB <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) char smem[PATCH_B + wx6::NSLOT * wx6::SLOT_REGB];
+  constexpr int RING_B = GA ? 0 : wx6::NSLOT * wx6::SLOT_REGB;
+  static_assert(PATCH_B + RING_B <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[PATCH_B + RING_B];
   const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem));
   const float* patch = reinterpret_cast<const float*>(smem);
 
@@ -757,43 +763,109 @@ k_conv_wide_x6(Params P, const uint16_t* __restrict__ wpack, int CHS) {
   };
 
   Fr F[2];
-  issue_a(0);
-  issue_a(1);
-  wait_vm<0>();
-  __builtin_amdgcn_s_barrier();
+  if constexpr (GA) {
+    // fragment (g, i, t) of this lane at ((g MI + i) 3 + t) 64 + lane (16-byte units)
+    const x6::bf16x8* ap = reinterpret_cast<const x6::bf16x8*>(wpack) + lane;
+    x6::bf16x8 fg[3][MI][3];
+    auto load_a = [&](x6::bf16x8 (&f)[MI][3], int g) {
 #pragma unroll
-  for (int i = 0; i < MI; ++i) read_a(0, i);
-  read_b(F[0], 0);
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-  for (int j = 0; j < 2; ++j) x6::split8(F[0].b[j], F[0].bp[j]);
-  // group g: slot of g + 1 is visible (wait + barrier; every wave is then also
-  // done with group g - 1's slot, which the DMA of group g + 2 overwrites)
+        for (int t = 0; t < 3; ++t) f[i][t] = ap[((g * MI + i) * 3 + t) * 64];
+    };
+    load_a(fg[0], 0);
+    load_a(fg[1], 1);
+    wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    read_b(F[0], 0);
 #pragma unroll
-  for (int g = 0; g < G; ++g) {
-    Fr& fc = F[g & 1];
-    Fr& fn = F[(g + 1) & 1];
-    const bool rd = g + 1 < G;
-    if (g > 0 && rd) {
-      wait_vm<0>();
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (g + 2 < G) issue_a(g + 2);
-    constexpr int NB = 2 * MI;
+    for (int j = 0; j < 2; ++j) x6::split8(F[0].b[j], F[0].bp[j]);
 #pragma unroll
-    for (int q = 0; q < NB; ++q) {
-      const int i = q >> 1, j = q & 1;
-      acc[i][j] = x6::mfma6(x6::Parts{fa[i][0], fa[i][1], fa[i][2]}, fc.bp[j], acc[i][j]);
-      if (rd) {
-        if (q == 0) read_b(fn, g + 1);
-        if (j == 1) read_a(g + 1, i);
-        if (q == NB - 2) x6::split8(fn.b[0], fn.bp[0]);
-        if (q == NB - 1) x6::split8(fn.b[1], fn.bp[1]);
+    for (int g = 0; g < G; ++g) {
+      Fr& fc = F[g & 1];
+      Fr& fn = F[(g + 1) & 1];
+      const bool rd = g + 1 < G;
+      if (g + 2 < G) load_a(fg[(g + 2) % 3], g + 2);
+      constexpr int NB = 2 * MI;
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        const int i = q >> 1, j = q & 1;
+        const auto& fa_ = fg[g % 3][i];
+        acc[i][j] = x6::mfma6(x6::Parts{fa_[0], fa_[1], fa_[2]}, fc.bp[j], acc[i][j]);
+        if (rd) {
+          if (q == 0) read_b(fn, g + 1);
+          if (q == NB - 2) x6::split8(fn.b[0], fn.bp[0]);
+          if (q == NB - 1) x6::split8(fn.b[1], fn.bp[1]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
-      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
+    issue_a(0);
+    issue_a(1);
+    wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+  #pragma unroll
+    for (int i = 0; i < MI; ++i) read_a(0, i);
+    read_b(F[0], 0);
+  #pragma unroll
+    for (int j = 0; j < 2; ++j) x6::split8(F[0].b[j], F[0].bp[j]);
+    // group g: slot of g + 1 is visible (wait + barrier; every wave is then also
+    // done with group g - 1's slot, which the DMA of group g + 2 overwrites)
+  #pragma unroll
+    for (int g = 0; g < G; ++g) {
+      Fr& fc = F[g & 1];
+      Fr& fn = F[(g + 1) & 1];
+      const bool rd = g + 1 < G;
+      if (g > 0 && rd) {
+        wait_vm<0>();
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (g + 2 < G) issue_a(g + 2);
+      constexpr int NB = 2 * MI;
+  #pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        const int i = q >> 1, j = q & 1;
+        acc[i][j] = x6::mfma6(x6::Parts{fa[i][0], fa[i][1], fa[i][2]}, fc.bp[j], acc[i][j]);
+        if (rd) {
+          if (q == 0) read_b(fn, g + 1);
+          if (j == 1) read_a(g + 1, i);
+          if (q == NB - 2) x6::split8(fn.b[0], fn.bp[0]);
+          if (q == NB - 1) x6::split8(fn.b[1], fn.bp[1]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
   }
   gemm_epilogue<MI, 2, OUT_NCHW>(acc, P, P.e, nullptr, 0, n0 + wave * 64, lr, lh);
+}
+
+// Weight repack for k_conv_wide_x6<GA = true>: w [M][C][KH][KW] -> fragments
+// [G][3 row blocks][3 terms][64 lanes][8 bf16]; lane (lr, h) of fragment
+// (g, i): row 32 i + lr, items 8 g + j of half h (same K order as below).
+__global__ void __launch_bounds__(256) k_conv_wide_pack_ga_x6(const float* __restrict__ w, char* __restrict__ out,
+                                                              int M, int C, int KH, int KW, int HR, int S, int units) {
+  for (int u = blockIdx.x * blockDim.x + threadIdx.x; u < units; u += gridDim.x * blockDim.x) {
+    const int lane = u & 63, i = (u >> 6) % 3, g = (u >> 6) / 3;
+    const int row = 32 * i + (lane & 31), h = lane >> 5;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int sx = 8 * g + j;
+      v[j] = 0.0f;
+      if (sx < S && row < M) {
+        const int c = sx / (HR * KW), kh = h * HR + (sx / KW) % HR, kw = sx % KW;
+        if (kh < KH) v[j] = w[(((int64_t)row * C + c) * KH + kh) * KW + kw];
+      }
+    }
+    x6::Parts t;
+    x6::split8(v, t);
+    char* f = out + (int64_t)(u >> 6) * 3072 + lane * 16;
+    *reinterpret_cast<x6::bf16x8*>(f) = t.h;
+    *reinterpret_cast<x6::bf16x8*>(f + 1024) = t.m;
+    *reinterpret_cast<x6::bf16x8*>(f + 2048) = t.l;
+  }
 }
 
 // Weight repack for k_conv_wide_x6: w [M][C][KH][KW] -> bf16 terms [G][96][SLOT_ROW/2]
@@ -1148,15 +1220,28 @@ int conv_wide_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, co
   P.e = make_epi(y, HW, 1.0f, 0.0f, bias, RRAM_BIAS_ROW, relu);
   P.e.cimg = (int64_t)d->num_output * HW;
   P.e.hw = make_fastdiv(HW);
+  // RRAM_WIDE_GA = 0: the LDS weight ring (A/B switch)
+  static const bool ga = [] {
+    const char* e = getenv("RRAM_WIDE_GA");
+    return !(e && atoi(e) == 0);
+  }();
   const int64_t total = (int64_t)Sh::G * wx6::BM * (wx6::SLOT_ROW / 2);
-  uint16_t* wp = reinterpret_cast<uint16_t*>(pack_buffer(static_cast<size_t>((total + 1) / 2), s));
+  const int64_t gunits = (int64_t)Sh::G * 3 * 64;  // GA: 3 KB fragments
+  uint16_t* wp = reinterpret_cast<uint16_t*>(pack_buffer(static_cast<size_t>(std::max(total, gunits * 24)), s));
   RRAM_REQUIRE(wp != nullptr, "conv: packed-weight buffer allocation failed");
-  hipLaunchKernelGGL(k_conv_wide_pack_x6, dim3(stream_blocks(total)), dim3(256), 0, s, w, wp, d->num_output, 3, 11,
-                     11, Sh::HR, Sh::S, total);
+  if (ga)
+    hipLaunchKernelGGL(k_conv_wide_pack_ga_x6, dim3(stream_blocks(gunits)), dim3(256), 0, s, w,
+                       reinterpret_cast<char*>(wp), d->num_output, 3, 11, 11, Sh::HR, Sh::S, static_cast<int>(gunits));
+  else
+    hipLaunchKernelGGL(k_conv_wide_pack_x6, dim3(stream_blocks(total)), dim3(256), 0, s, w, wp, d->num_output, 3, 11,
+                       11, Sh::HR, Sh::S, total);
   int rc = launch_status("conv wide weight pack x6");
   if (rc) return rc;
   const unsigned nwg = static_cast<unsigned>((P.N + wx6::BN - 1) / wx6::BN);
-  hipLaunchKernelGGL((k_conv_wide_x6<11, 11, 4, 3, WIDE_PFL>), dim3(nwg), dim3(256), 0, s, P, wp, pl.CHS);
+  if (ga)
+    hipLaunchKernelGGL((k_conv_wide_x6<11, 11, 4, 3, WIDE_PFL, true>), dim3(nwg), dim3(256), 0, s, P, wp, pl.CHS);
+  else
+    hipLaunchKernelGGL((k_conv_wide_x6<11, 11, 4, 3, WIDE_PFL, false>), dim3(nwg), dim3(256), 0, s, P, wp, pl.CHS);
   rc = launch_status("conv wide x6");
   return rc ? rc : 1;
 }
@@ -1260,9 +1345,16 @@ bool conv_cb_plan(const rram_conv_desc* d, CbPlan& pl) {
   // tile (WR, NB) with the least makespan (rounds of 256 workgroups x tile
   // area); ties: taller tiles (weights fetched by one wave)
   static const int cfg[3][2] = {{4, 8}, {4, 4}, {2, 4}};
+  // RRAM_CB_CFG = "WR,NB": only that tile (A/B knob)
+  static const int force = [] {
+    const char* e = getenv("RRAM_CB_CFG");
+    int wr = 0, nb = 0;
+    return e && sscanf(e, "%d,%d", &wr, &nb) == 2 ? wr * 100 + nb : 0;
+  }();
   int64_t best = -1;
   for (const auto& c : cfg) {
     const int WR = c[0], NB = c[1], BM = 32 * WR, BN = 32 * NB * (4 / WR);
+    if (force != 0 && force != WR * 100 + NB) continue;
     const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
     if ((tiles_m * BM - M) * 4 > tiles_m * BM) continue;  // > 1/4 padded rows
     const int rmax = patch_rows(N, HW, OW, OH, KH, BN, 3);
