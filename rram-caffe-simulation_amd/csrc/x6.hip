@@ -943,6 +943,12 @@ constexpr int KT = 32;
 constexpr int RLB = 2 * 96 + 16;  // packed A row bytes per K-tile ([g][h][term][8 bf16] + pad, RLB/16 odd)
 }  // namespace gx6
 
+// The activation slabs (L2-resident) are double-buffered one K-tile ahead;
+// the weights (streamed from HBM) go through a 3-stage ring two K-tiles
+// ahead, so their HBM latency has 1.5 K-tiles to land: per K-tile the A
+// pieces of t + 1 are issued first, then the B pieces of t + 2, and the end
+// of the tile waits with vmcnt(B pieces) (the B of t + 1, issued a tile
+// earlier, and the A of t + 1 have then landed).
 template <int MI, int NJ>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 k_gemm_x6(Params P, const uint16_t* __restrict__ apack, int ktiles_all, int ktc) {
@@ -953,10 +959,10 @@ k_gemm_x6(Params P, const uint16_t* __restrict__ apack, int ktiles_all, int ktc)
   constexpr int A_DMA = ((A_B + 1023) / 1024 + 3) / 4;
   constexpr int A_REGB = A_DMA * 4 * 1024;
   constexpr int B_DMA = 4 * NJ;                          // 1 KB pieces (8 rows x 32 k) per wave
-  constexpr int SFB = A_REGB + BNc * KT * 4;
+  constexpr int B_REGB = BNc * KT * 4, NBS = 3;
   constexpr int NVM = A_DMA + B_DMA;
-  static_assert(2 * SFB <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) char smem[2 * SFB];
+  static_assert(2 * A_REGB + NBS * B_REGB <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[2 * A_REGB + NBS * B_REGB];
   const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem));
 
   const int lane = threadIdx.x & 63;
@@ -1006,17 +1012,19 @@ k_gemm_x6(Params P, const uint16_t* __restrict__ apack, int ktiles_all, int ktc)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
-  auto issue = [&](int t, int stg, int e) {  // DMA item e of local K-tile t into stage stg
-    const uint32_t img = lds0 + static_cast<uint32_t>(stg * SFB);
-    if (e < A_DMA) {
-      dma_b128(arsrc, aoff[e] + static_cast<uint32_t>(t * A_B), img + static_cast<uint32_t>((wave * A_DMA + e) * 1024));
-    } else {
-      const int i = e - A_DMA;
-      const int k = (kt0 + t) * KT + bkq[i];
-      const uint32_t off = (boff[i] + static_cast<uint32_t>(k) * 4u) | (k < kend ? 0u : 0x80000000u);
-      dma_b128(brsrc, off, img + static_cast<uint32_t>(A_REGB + (32 * NJ * wave + 8 * i) * KT * 4));
-    }
+  // A piece e of local K-tile t into A stage t & 1; B piece i into B stage t % NBS
+  auto issue_a = [&](int t, int e) {
+    dma_b128(arsrc, aoff[e] + static_cast<uint32_t>(t * A_B),
+             lds0 + static_cast<uint32_t>((t & 1) * A_REGB + (wave * A_DMA + e) * 1024));
   };
+  auto issue_b = [&](int t, int i) {
+    const int k = (kt0 + t) * KT + bkq[i];
+    const uint32_t off = (boff[i] + static_cast<uint32_t>(k) * 4u) | (k < kend ? 0u : 0x80000000u);
+    dma_b128(brsrc, off,
+             lds0 + static_cast<uint32_t>(2 * A_REGB + (t % NBS) * B_REGB + (32 * NJ * wave + 8 * i) * KT * 4));
+  };
+  auto a_st = [&](int t) { return smem + (t & 1) * A_REGB; };
+  auto b_st = [&](int t) { return smem + 2 * A_REGB + (t % NBS) * B_REGB; };
   x6::bf16x8 fa[MI][3];  // single-buffered activation fragments (see k_conv_patch_x6)
   struct Fr {
     float b[NJ][8];
@@ -1028,7 +1036,7 @@ k_gemm_x6(Params P, const uint16_t* __restrict__ apack, int ktiles_all, int ktc)
     for (int t = 0; t < 3; ++t) fa[i][t] = *reinterpret_cast<const x6::bf16x8*>(p + 16 * t);
   };
   auto read_b = [&](Fr& F, const char* st, int g) {
-    const float* bs = reinterpret_cast<const float*>(st + A_REGB);
+    const float* bs = reinterpret_cast<const float*>(st);
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int n = 32 * NJ * wave + 32 * j + lr;
@@ -1045,32 +1053,43 @@ k_gemm_x6(Params P, const uint16_t* __restrict__ apack, int ktiles_all, int ktc)
 
   Fr F[2];
 #pragma unroll
-  for (int e = 0; e < NVM; ++e) issue(0, 0, e);
-  wait_vm<0>();
+  for (int e = 0; e < A_DMA; ++e) issue_a(0, e);
+#pragma unroll
+  for (int i = 0; i < B_DMA; ++i) issue_b(0, i);
+  if (nt > 1) {
+#pragma unroll
+    for (int i = 0; i < B_DMA; ++i) issue_b(1, i);
+    wait_vm<B_DMA>();
+  } else {
+    wait_vm<0>();
+  }
   __builtin_amdgcn_s_barrier();
 #pragma unroll
-  for (int i = 0; i < MI; ++i) read_a(smem, 0, i);
-  read_b(F[0], smem, 0);
+  for (int i = 0; i < MI; ++i) read_a(a_st(0), 0, i);
+  read_b(F[0], b_st(0), 0);
 #pragma unroll
   for (int j = 0; j < NJ; ++j) x6::split8(F[0].b[j], F[0].bp[j]);
 
   auto tile = [&](int t, auto more_c) {
     constexpr bool MORE = decltype(more_c)::value;
-    const char* cur = smem + (t & 1) * SFB;
-    const char* nxt = smem + ((t + 1) & 1) * SFB;
+    const bool more2 = t + 2 < nt;  // B of K-tile t + 2 to fetch
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
       Fr& fc = F[g];
       Fr& fn = F[g ^ 1];
       const bool last = g == 1;
       if (last && MORE) {
-        wait_vm<0>();
+        if (more2)
+          wait_vm<B_DMA>();
+        else
+          wait_vm<0>();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
       }
       const bool rd = !last || MORE;
-      const char* src = last ? nxt : cur;
+      const char* asrc = last ? a_st(t + 1) : a_st(t);
+      const char* bsrc = last ? b_st(t + 1) : b_st(t);
       const int gn = last ? 0 : 1;
       constexpr int NB = MI * NJ;
 #pragma unroll
@@ -1078,16 +1097,21 @@ k_gemm_x6(Params P, const uint16_t* __restrict__ apack, int ktiles_all, int ktc)
         const int i = q / NJ, j = q % NJ;
         acc[i][j] = x6::mfma6(x6::Parts{fa[i][0], fa[i][1], fa[i][2]}, fc.bp[j], acc[i][j]);
         if (rd) {
-          if (q == 0) read_b(fn, src, gn);
-          if (j == NJ - 1) read_a(src, gn, i);
+          if (q == 0) read_b(fn, bsrc, gn);
+          if (j == NJ - 1) read_a(asrc, gn, i);
 #pragma unroll
           for (int jj = 0; jj < NJ; ++jj)
             if (q == NB - NJ + jj) x6::split8(fn.b[jj], fn.bp[jj]);
         }
-        if (!last && MORE) {
+        if (!last && MORE) {  // A of t + 1, then B of t + 2, spread over the group's blocks
 #pragma unroll
           for (int e = 0; e < NVM; ++e)
-            if ((e * NB) / NVM == q) issue(t + 1, (t + 1) & 1, e);
+            if ((e * NB) / NVM == q) {
+              if (e < A_DMA)
+                issue_a(t + 1, e);
+              else if (more2)
+                issue_b(t + 2, e - A_DMA);
+            }
         }
         __builtin_amdgcn_sched_barrier(0);
       }
