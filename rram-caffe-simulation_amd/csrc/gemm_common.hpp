@@ -214,6 +214,69 @@ __device__ __forceinline__ void gemm_epilogue(floatx16 (&acc)[MI][NI], const Par
   }
 }
 
+// Epilogue of the bf16x6 convolution kernels (beta = 0, no split-K, NCHW
+// output): the same arithmetic as gemm_epilogue's beta = 0 path, stored with
+// raw buffer stores whose row offsets are wave-uniform (scalar soffset: the
+// lane's rows are mwave + 4 h + (r & 3) + 8 (r >> 2) + 32 i), so a store
+// costs no per-element address arithmetic (the generic epilogue spent
+// ~3000 VALU per wave on 64-bit addresses, exposed at one wave per SIMD).
+// acc is left holding the stored values before the ReLU.
+template <int MI, int NI>
+__device__ __forceinline__ void conv_epilogue_nchw(floatx16 (&acc)[MI][NI], const Params& P, const Epi& ep,
+                                                   int mwave, int nwave, int lr, int lh) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(ep.C, 0, 0x7FFFFFFF, 0x00020000);
+  const int HWo = static_cast<int>(ep.hw.d);
+  const int mw = mwave + 4 * lh;  // this lane's first row
+  const bool rows_full = mwave + MI * 32 <= P.M;
+  const bool row_bias = ep.bias_mode == RRAM_BIAS_ROW, col_bias = ep.bias_mode == RRAM_BIAS_COL;
+  const bool relu = ep.relu != 0;
+  const float alpha = ep.alpha;
+  float bz[MI][16];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = mw + i * 32 + (r & 3) + 8 * (r >> 2);
+      bz[i][r] = *((row_bias && m < P.M) ? ep.bias + m : g_zero4);
+    }
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int n = nwave + j * 32 + lr;
+    if (n >= P.N) continue;
+    const float cb = *(col_bias ? ep.bias + n : g_zero4);
+    const uint32_t im = fdiv(static_cast<uint32_t>(n), ep.hw);
+    const uint32_t sp = static_cast<uint32_t>(n) - im * ep.hw.d;
+    const uint32_t base = static_cast<uint32_t>((im * ep.cimg + sp + static_cast<int64_t>(mw) * HWo) * 4);
+    float ov[MI][16];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float o = (alpha * acc[i][j][r] + bz[i][r]) + cb;
+        acc[i][j][r] = o;  // the stored value before the ReLU (k_conv_cb_x6's octet companion splits it)
+        ov[i][r] = relu ? fmaxf(o, 0.0f) : o;
+      }
+    if (rows_full) {  // uniform: no per-store exec masking
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, ov[i][r]), rs, static_cast<int>(base),
+                                                (i * 32 + (r & 3) + 8 * (r >> 2)) * HWo * 4, 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int dr = i * 32 + (r & 3) + 8 * (r >> 2);
+          if (mw + dr < P.M)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, ov[i][r]), rs, static_cast<int>(base),
+                                                  dr * HWo * 4, 0);
+        }
+    }
+  }
+}
+
 Epi make_epi(float* C, int64_t ldc, float alpha, float beta, const float* bias, int bias_mode,
              int relu) {
   Epi e{};

@@ -275,7 +275,7 @@ k_conv_patch_x6(Params P, const uint16_t* __restrict__ wpack, int PW, int CS) {
       tile(t, P0{}, F_{});
     }
   }
-  gemm_epilogue<MI, 2, OUT_NCHW>(acc, P, ep, nullptr, m0, n0 + wave * 64, lr, lh);
+  conv_epilogue_nchw<MI, 2>(acc, P, ep, m0, n0 + wave * 64, lr, lh);
 }
 
 
@@ -346,7 +346,7 @@ __device__ __forceinline__ void wait_vm_n(int n) {
 template <int KH, int KW, int WR, int NB, int PD>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __restrict__ xpack, int octb, int rpc,
-             uint32_t xrange, int ximg, char* __restrict__ yoct, int cout8) {
+             uint32_t xrange, int ximg, char* __restrict__ yoct, int cout8, FastDiv oct_div, FastDiv rpc_div) {
   using namespace g2;
   constexpr int T = KH * KW, WC = 4 / WR, BMc = 32 * WR, BNc = 32 * NB * WC, SFB = PD * 4 * 1024;
   constexpr int D = cbx6::dist(NB), NSA = D + 1;
@@ -398,8 +398,8 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
 #pragma unroll
   for (int i = 0; i < PD; ++i) {
     const int c = (wave * PD + i) * 64 + lane;
-    const int h = c / (octb >> 4), rem = c - h * (octb >> 4);
-    const int prow = rem / rpc, pc = rem - prow * rpc;
+    const int h = static_cast<int>(fdiv(static_cast<uint32_t>(c), oct_div)), rem = c - h * (octb >> 4);
+    const int prow = static_cast<int>(fdiv(static_cast<uint32_t>(rem), rpc_div)), pc = rem - prow * rpc;
     const int pcol = pc / 3, t = pc - pcol * 3;
     uint32_t off = 0x80000000u;
     if (h < 2 && prow < R && pcol < PW) {
@@ -417,8 +417,8 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
     const int n = min(n0 + wc * 32 * NB + 32 * j + lr, plast);
-    const int img = n / HW, sp = n - img * HW;
-    const int oh = sp / OW, ow = sp - oh * OW;
+    const int img = static_cast<int>(fdiv(static_cast<uint32_t>(n), cv.howo)), sp = n - img * HW;
+    const int oh = static_cast<int>(fdiv(static_cast<uint32_t>(sp), cv.wo_div)), ow = sp - oh * OW;
     const int sg = img - img0;
     const int prow = sg == 0 ? oh - f0 : (sg == 1 ? p1 : p2) + oh;
     bb[j] = lh * octb + prow * rpc * 16 + ow * 48;
@@ -540,11 +540,11 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
       ktile(kt, P0{}, F_{});
     }
   }
-  gemm_epilogue<1, NB, OUT_NCHW>(acc, P, ep, nullptr, m0 + 32 * wr, n0 + wc * 32 * NB, lr, lh);
+  conv_epilogue_nchw<1, NB>(acc, P, ep, m0 + 32 * wr, n0 + wc * 32 * NB, lr, lh);
   if (yoct != nullptr) {
     // the output's channel-octet companion (the next convolution's input,
     // k_pack_octets_x6 layout): the split of the stored values (bias and
-    // ReLU applied; gemm_epilogue folded the bias into acc).  Lane (lr, h)
+    // ReLU applied; conv_epilogue_nchw left them in acc).  Lane (lr, h)
     // holds channels 8 k + 4 h .. + 3 of octets k = 0..3 of its 32 rows; the
     // two halves trade halves (lane ^ 32) so that half 0 owns octets 0, 1 and
     // half 1 octets 2, 3, whole.
@@ -838,7 +838,7 @@ k_conv_wide_x6(Params P, const uint16_t* __restrict__ wpack, int CHS) {
       }
     }
   }
-  gemm_epilogue<MI, 2, OUT_NCHW>(acc, P, P.e, nullptr, 0, n0 + wave * 64, lr, lh);
+  conv_epilogue_nchw<MI, 2>(acc, P, P.e, 0, n0 + wave * 64, lr, lh);
 }
 
 // Weight repack for k_conv_wide_x6<GA = true>: w [M][C][KH][KW] -> fragments
@@ -1461,7 +1461,8 @@ int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, c
 #define RRAM_X(kh, wr, nb, pd)                                                                                \
   if (KH == kh && pl.WR == wr && pl.NB == nb && pl.PD == pd) {                                                \
     hipLaunchKernelGGL((k_conv_cb_x6<kh, kh, wr, nb, pd>), dim3(nwg), dim3(256), 0, s, P, wp, xp, pl.octb, pl.RPC, \
-                       xrange, ximg, static_cast<char*>(y_oct), d->num_output / 8);                           \
+                       xrange, ximg, static_cast<char*>(y_oct), d->num_output / 8,                            \
+                       make_fastdiv(static_cast<uint32_t>(pl.octb >> 4)), make_fastdiv(static_cast<uint32_t>(pl.RPC))); \
   } else
   RRAM_CB_LIST(RRAM_X) { return 0; }
 #undef RRAM_X
