@@ -343,7 +343,12 @@ __device__ __forceinline__ void wait_vm_n(int n) {
   }
 }
 
-template <int KH, int KW, int WR, int NB, int PD>
+// VL: the loop's global reads are compiler-visible register loads (weights
+// straight into the fragment registers one group ahead; patch pieces into
+// staging registers, written to LDS one tap later) instead of LDS-DMA, whose
+// issue cost (~100 cycles per piece among MFMAs) the weight ring paid 3 times
+// per group.
+template <int KH, int KW, int WR, int NB, int PD, bool VL>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __restrict__ xpack, int octb, int rpc,
              uint32_t xrange, int ximg, char* __restrict__ yoct, int cout8, FastDiv oct_div, FastDiv rpc_div) {
@@ -351,7 +356,7 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
   constexpr int T = KH * KW, WC = 4 / WR, BMc = 32 * WR, BNc = 32 * NB * WC, SFB = PD * 4 * 1024;
   constexpr int D = cbx6::dist(NB), NSA = D + 1;
   static_assert(cbx6::lds_bytes(NB, PD) <= 160 * 1024 && D < T, "LDS");
-  __shared__ __attribute__((aligned(16))) char smem[cbx6::lds_bytes(NB, PD)];
+  __shared__ __attribute__((aligned(16))) char smem[VL ? 2 * SFB : cbx6::lds_bytes(NB, PD)];
   const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem));
 
   const int lane = threadIdx.x & 63;
@@ -465,6 +470,89 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
     for (int t = 0; t < 3; ++t) f[t] = *reinterpret_cast<const x6::bf16x8*>(p + 16 * t);
   };
 
+  if constexpr (VL) {
+    const x6::bf16x8* ap = wpack + ((int64_t)((z * P.tiles_m + tm) * WR + wr) * KT) * T * cbx6::FRAG + lane;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint16_t*>(xg), 0, static_cast<int>(xrange - static_cast<uint32_t>(z * (cv.C >> 3)) * PL), 0x00020000);
+    auto load_a = [&](x6::bf16x8 (&f)[3], int q) {
+#pragma unroll
+      for (int t = 0; t < 3; ++t) f[t] = ap[q * cbx6::FRAG + t * 64];
+    };
+    constexpr int PMAX = (PD + T - 2) / (T - 1);  // patch pieces per tap
+    typedef int int4x __attribute__((ext_vector_type(4)));
+    int4x stg[2][PMAX];
+#pragma unroll
+    for (int i = 0; i < PD; ++i) issue(0, 0, i);
+    load_a(fa[0], 0);
+    wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    read_b(fb[0], smem, 0, 0);
+    auto vtile = [&](int kt, auto par_c, auto more_c) {
+      constexpr int PAR = decltype(par_c)::value;
+      constexpr bool MORE = decltype(more_c)::value;
+      const char* cur = smem + (kt & 1) * SFB;
+      const char* nxt = smem + ((kt + 1) & 1) * SFB;
+      char* nst = smem + ((kt + 1) & 1) * SFB + wave * PD * 1024 + lane * 16;
+#pragma unroll
+      for (int s = 0; s < T; ++s) {
+        const int pa = (s + PAR) & 1;
+        const int q = kt * T + s;
+        if (MORE) {
+          // block 0: the pieces loaded at tap s - 1 into the next stage, this
+          // tap's pieces into staging registers
+          if (s > 0) {
+#pragma unroll
+            for (int i = cbx6::piece_lo(s - 1, PD, T); i < cbx6::piece_lo(s, PD, T); ++i)
+              *reinterpret_cast<int4x*>(nst + i * 1024) = stg[(s - 1) & 1][i - cbx6::piece_lo(s - 1, PD, T)];
+          }
+#pragma unroll
+          for (int i = cbx6::piece_lo(s, PD, T); i < cbx6::piece_lo(s + 1, PD, T); ++i)
+            stg[s & 1][i - cbx6::piece_lo(s, PD, T)] = __builtin_bit_cast(
+                int4x, __builtin_amdgcn_raw_buffer_load_b128(
+                           xr, static_cast<int>(poff[i] + static_cast<uint32_t>(kt + 1) * 2u * PL), 0, 0));
+        }
+        if (s + 1 < T || MORE) load_a(fa[pa ^ 1], q + 1);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          const bool last = s == T - 1 && j == NB - 1;
+          if (last && MORE) {  // the next stage is complete
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          if (!last)
+            read_b(fb[(j + 1) & 1], cur, j + 1 < NB ? s : s + 1, j + 1 < NB ? j + 1 : 0);
+          else if (MORE)
+            read_b(fb[0], nxt, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          acc[0][j] = x6::mfma6(x6::Parts{fa[pa][0], fa[pa][1], fa[pa][2]},
+                                x6::Parts{fb[j & 1][0], fb[j & 1][1], fb[j & 1][2]}, acc[0][j]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    };
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    using P0 = std::integral_constant<int, 0>;
+    using P1 = std::integral_constant<int, 1>;
+    if constexpr (T % 2 == 0) {
+      int kt = 0;
+      for (; kt + 1 < KT; ++kt) vtile(kt, P0{}, T_{});
+      vtile(kt, P0{}, F_{});
+    } else {
+      int kt = 0;
+      for (; kt + 2 < KT; kt += 2) {
+        vtile(kt, P0{}, T_{});
+        vtile(kt + 1, P1{}, T_{});
+      }
+      if (kt + 1 < KT) {
+        vtile(kt, P0{}, T_{});
+        vtile(kt + 1, P1{}, F_{});
+      } else {
+        vtile(kt, P0{}, F_{});
+      }
+    }
+  } else {
 #pragma unroll
   for (int i = 0; i < PD; ++i) issue(0, 0, i);
 #pragma unroll
@@ -540,6 +628,7 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
       ktile(kt, P0{}, F_{});
     }
   }
+  }  // VL
   conv_epilogue_nchw<1, NB>(acc, P, ep, m0 + 32 * wr, n0 + wc * 32 * NB, lr, lh);
   if (yoct != nullptr) {
     // the output's channel-octet companion (the next convolution's input,
@@ -1331,6 +1420,14 @@ int pack_octets(const float* x, void* oct, int num, int C, int HWi, hipStream_t 
 }
 
 // ---- k_conv_cb_x6 (channel-octet pre-split activations) ----
+// RRAM_CB_VL = 0: the LDS-DMA weight ring (A/B switch of k_conv_cb_x6's VL)
+bool cb_vl() {
+  static const bool on = [] {
+    const char* e = getenv("RRAM_CB_VL");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
 // RRAM_CONV_CB = 0 leaves these shapes to k_conv_patch_x6 (A/B switch)
 bool conv_cb_enabled() {
   static const bool on = [] {
@@ -1460,7 +1557,12 @@ int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, c
   const uint32_t xrange = static_cast<uint32_t>(xbytes);  // whole packed input (the kernel narrows it per group)
 #define RRAM_X(kh, wr, nb, pd)                                                                                \
   if (KH == kh && pl.WR == wr && pl.NB == nb && pl.PD == pd) {                                                \
-    hipLaunchKernelGGL((k_conv_cb_x6<kh, kh, wr, nb, pd>), dim3(nwg), dim3(256), 0, s, P, wp, xp, pl.octb, pl.RPC, \
+    if (cb_vl())                                                                                             \
+      hipLaunchKernelGGL((k_conv_cb_x6<kh, kh, wr, nb, pd, true>), dim3(nwg), dim3(256), 0, s, P, wp, xp, pl.octb,  \
+                         pl.RPC, xrange, ximg, static_cast<char*>(y_oct), d->num_output / 8,                   \
+                         make_fastdiv(static_cast<uint32_t>(pl.octb >> 4)), make_fastdiv(static_cast<uint32_t>(pl.RPC))); \
+    else                                                                                                     \
+    hipLaunchKernelGGL((k_conv_cb_x6<kh, kh, wr, nb, pd, false>), dim3(nwg), dim3(256), 0, s, P, wp, xp, pl.octb, pl.RPC, \
                        xrange, ximg, static_cast<char*>(y_oct), d->num_output / 8,                            \
                        make_fastdiv(static_cast<uint32_t>(pl.octb >> 4)), make_fastdiv(static_cast<uint32_t>(pl.RPC))); \
   } else
