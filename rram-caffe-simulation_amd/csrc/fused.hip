@@ -3,6 +3,7 @@
 // the unfused kernels produce, only its round trip through HBM disappears.
 #include <float.h>
 #include <math.h>
+#include <stdlib.h>
 
 #include "rram_common.hpp"
 #include "split3.hpp"
@@ -225,7 +226,13 @@ int rram_lrn_maxpool_fwd_octets(const float* x, float* y, void* y_oct, int num, 
   while (rb > 1 && (int64_t)num * ((PH + rb - 1) / rb) < 1024 && fits(rb - 1) && (rb - 1) * sh >= kernel) --rb;
   const dim3 grid(static_cast<unsigned>((PH + rb - 1) / rb), static_cast<unsigned>(num));
   const float aos = alpha / size;
-  const bool big = H * W >= 1024;
+  // channels per barrier: measured G = 2 for 55 x 55 planes, 4 for 27 x 27;
+  // RRAM_LRN_G overrides (2 | 4 | 8) for A/B
+  static const int g_env = [] {
+    const char* e = getenv("RRAM_LRN_G");
+    return e ? atoi(e) : 0;
+  }();
+  const int gsel = g_env == 2 || g_env == 4 || g_env == 8 ? g_env : (H * W >= 1024 ? 2 : 4);
   char* yo = static_cast<char*>(y_oct);
 #define RRAM_LP2(K_, S_, G_)                                                                                  \
   if (yo)                                                                                                     \
@@ -236,10 +243,12 @@ int rram_lrn_maxpool_fwd_octets(const float* x, float* y, void* y_oct, int num, 
                        yo, C, H, W, PH, PW, sh, sw, ph, pw, rb, aos, beta, k);
 #define RRAM_LP(K_, S_)          \
   if (kernel == K_ && size == S_) { \
-    if (big) {                   \
+    if (gsel == 2) {             \
       RRAM_LP2(K_, S_, 2)        \
-    } else {                     \
+    } else if (gsel == 4) {      \
       RRAM_LP2(K_, S_, 4)        \
+    } else {                     \
+      RRAM_LP2(K_, S_, 8)        \
     }                            \
   }
   RRAM_LP(3, 5)

@@ -65,3 +65,32 @@ def test_caffe_header_symbols_exported():
     lib = ctypes.CDLL(str(K.CAFFE_SO))
     missing = [n for n in declared(hdr) if not hasattr(lib, n)]
     assert not missing, missing
+
+
+def test_engine_plans_host_side():
+    """The engine / kernel plans are host logic (no GPU): AlexNet conv2-5 at
+    b256 take the channel-octet kernel (their inputs would read an octet
+    companion), conv1 the wide bf16x6 kernel, and shapes outside the octet
+    kernel's range (Cin/group % 16 != 0, stride 2, 7x7, 1x1) do not."""
+    from rramsim import ops
+    octet = [((256, 96, 27, 27), 256, 5, 2, 2), ((256, 256, 13, 13), 384, 3, 1, 1),
+             ((256, 384, 13, 13), 384, 3, 1, 2), ((256, 384, 13, 13), 256, 3, 1, 2),
+             ((8, 64, 28, 28), 128, 3, 1, 1)]
+    for x, cout, k, p, g in octet:
+        d = ops.conv_desc(x, cout, k, 1, p, 1, g)
+        assert ops.conv_input_octets(d) == 1, (x, cout, k)
+        assert ops.f32_engine_for_conv(d) == ops.ENGINE_BF16X6
+    not_octet = [((256, 3, 227, 227), 96, 11, 0, 1, 4), ((4, 24, 28, 28), 64, 3, 1, 1, 1),
+                 ((4, 64, 28, 28), 64, 3, 1, 1, 2), ((4, 3, 224, 224), 64, 7, 3, 1, 2),
+                 ((4, 64, 28, 28), 64, 1, 0, 1, 1)]
+    for x, cout, k, p, g, s in not_octet:
+        d = ops.conv_desc(x, cout, k, s, p, 1, g)
+        assert ops.conv_input_octets(d) == 0, (x, cout, k, s)
+    conv1 = ops.conv_desc((256, 3, 227, 227), 96, 11, 4, 0, 1, 1)
+    assert ops.f32_engine_for_conv(conv1) == ops.ENGINE_BF16X6
+    prev = ops.set_f32_engine(ops.ENGINE_F32)
+    try:
+        assert ops.conv_input_octets(ops.conv_desc(*octet[0][:2], 5, 1, 2, 1, 2)) == 0
+        assert ops.f32_engine_for_conv(conv1) == ops.ENGINE_F32
+    finally:
+        ops.set_f32_engine(prev)
