@@ -1685,7 +1685,13 @@ bool gemm_x6_plan(int M, int N, int K, size_t ws_bytes, GemmPlan& pl) {
   }
   pl.ktc = (pl.ktiles + split - 1) / split;
   pl.split = (pl.ktiles + pl.ktc - 1) / pl.ktc;
-  if (tiles * pl.split < 192) return false;  // under ~3/4 of the CUs busy: the fp32 kernel's smaller tiles fill more
+  // under ~half of the CUs busy: the fp32 kernel's smaller tiles fill more
+  // (RRAM_X6_GEMM_MINWG overrides the bound for A/B)
+  static const int min_wg = [] {
+    const char* e = getenv("RRAM_X6_GEMM_MINWG");
+    return e ? atoi(e) : 192;
+  }();
+  if (tiles * pl.split < min_wg) return false;
   return (int64_t)pl.tiles_m * pl.ktiles * BMc * gx6::RLB < (1ll << 31);
 }
 
