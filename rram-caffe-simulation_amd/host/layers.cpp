@@ -185,24 +185,26 @@ void ConvolutionLayer<Dtype>::Reshape(const std::vector<Blob<Dtype>*>& bottom,
   if (want_in_oct_) bottom[0]->data()->wants_octets = true;
 }
 
-// the octet companion a producer writes next to top (nullptr: not wanted)
-// RRAM_OCTETS = 1: producers write the companions their consumers read.
-// Off by default: measured on MI355X (AlexNet b256, per-layer hipEvents),
-// writing the companion in the producer costs about what it saves the
-// consumer (pool1 +35 us / conv2 -39 us, pool2 +13 / conv3 -35, conv3's
-// epilogue +40 / conv4 -35, conv4's +40 / conv5 -32: -11 us per step, 99.6 /
-// 100.0k vs 99.5 / 99.8k images/s), so the convolutions pack their inputs.
-bool octets_enabled() {
-  static const bool on = [] {
+// the octet companion a producer writes next to top (nullptr: not wanted).
+// RRAM_OCTETS selects the producers: 0 none (every convolution packs its
+// input), 1 all, 2 (default) the fused LRN + max pool only.  Measured on
+// MI355X (AlexNet b256, per-layer hipEvents, profiles/r02_ab_octets.txt): the
+// companion write costs the producer pool1 +35 us / saves conv2 39 us, pool2
+// +13 / conv3 -35, conv3's epilogue +40 / conv4 -35, conv4's +40 / conv5 -32,
+// so only the pooling producers pay off.
+enum OctetProducer { kOctConv = 1, kOctPool = 2 };
+bool octets_enabled(int producer) {
+  static const int mode = [] {
     const char* e = std::getenv("RRAM_OCTETS");
-    return e && std::atoi(e) != 0;
+    return e ? std::atoi(e) : 2;
   }();
-  return on;
+  return mode == 1 || (mode == 2 && producer == kOctPool);
 }
 template <typename Dtype>
-void* octets_for(Blob<Dtype>* top) {
+void* octets_for(Blob<Dtype>* top, int producer) {
   SyncedMemory* m = top->data().get();
-  if (!octets_enabled() || !m->wants_octets || top->num_axes() != 4 || top->shape(1) % 8 != 0) return nullptr;
+  if (!octets_enabled(producer) || !m->wants_octets || top->num_axes() != 4 || top->shape(1) % 8 != 0)
+    return nullptr;
   return m->octets(static_cast<size_t>(top->count()) * 6);
 }
 template <typename Dtype>
@@ -218,7 +220,7 @@ void ConvolutionLayer<Dtype>::Forward_gpu(const std::vector<Blob<Dtype>*>& botto
   const int shp[4] = {desc_.num, desc_.channels, desc_.height, desc_.width};
   const void* xo = want_in_oct_ ? bottom[0]->data()->valid_octets(shp) : nullptr;
   float* y = top[0]->mutable_gpu_data();  // invalidates top's companion
-  void* yo = octets_for(top[0]);
+  void* yo = octets_for(top[0], kOctConv);
   RRAM_CALL(rram_conv2d_fwd_octets(&desc_, bottom[0]->gpu_data(), xo, this->blobs_[0]->gpu_data(),
                                    bias_term_ ? this->blobs_[1]->gpu_data() : nullptr, y, yo, fused_relu ? 1 : 0,
                                    Caffe::stream()));
@@ -398,7 +400,7 @@ class PoolingLayer : public Layer<Dtype> {
   void Forward_gpu(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
     if (lrn_src_ != nullptr) {  // LRN folded into this pool (Net::Net, TEST phase)
       float* y = top[0]->mutable_gpu_data();
-      void* yo = octets_for(top[0]);
+      void* yo = octets_for(top[0], kOctPool);
       RRAM_CALL(rram_lrn_maxpool_fwd_octets(lrn_src_->gpu_data(), y, yo, bottom[0]->shape(0), C_, H_, W_, PH_, PW_,
                                             kh_, sh_, sw_, ph_, pw_, lrn_size_, lrn_alpha_, lrn_beta_, lrn_k_,
                                             Caffe::stream()));
