@@ -239,7 +239,10 @@ def main():
         "roofline_inject": {"bound": "hbm", "achieved": round(inj_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                             "frac": round(inj_gbps / HBM_PEAK_GBPS, 4),
                             "traffic": traffic.get("inject", {}).get("bytes_per_launch"),
-                            "algorithmic_bytes_per_launch": 8 * inj_w, "avg_us_per_launch": round(inj_ms_per * 1e3, 2)},
+                            "algorithmic_bytes_per_launch": 8 * inj_w, "avg_us_per_launch": round(inj_ms_per * 1e3, 2),
+                            "note": ("launched on a side stream, overlapped with conv1-5 of the same map (they share "
+                                     "the CUs, so the launch stretches; RRAM_MC_OVERLAP=0 times it alone)"
+                                     if os.environ.get("RRAM_MC_OVERLAP", "1") != "0" else "serial")},
         "traffic_source": traffic.get("source"),
         "mc_stats": {"maps": int(stats[len(st["sums"]) + 1].item()), "mean_outputs": mean_out,
                      "broken_cells": int(stats[len(st["sums"])].item())},

@@ -600,9 +600,14 @@ MonteCarlo<Dtype>::MonteCarlo(std::shared_ptr<Net<Dtype>> net, const std::vector
   HIP_CALL(hipMalloc(reinterpret_cast<void**>(&d_broken_), params_.size() * sizeof(unsigned long long)));
   const auto& fl = net_->failure_learnable_layer_ids();
   first_fault_layer_ = *std::min_element(fl.begin(), fl.end());
-  // opt-in (RRAM_MC_OVERLAP=1): measured +0.5 % maps/s on AlexNet b256, but the
-  // injection then shares the chip with conv1 (86 -> 146 us per launch)
-  overlap_ = getenv("RRAM_MC_OVERLAP") != nullptr && first_fault_layer_ > 0;
+  // on by default (RRAM_MC_OVERLAP=0: serial): round 1 measured it flat
+  // (the injection shares the chip with conv1, 86 -> 120-146 us per launch,
+  // and slowed the fp32 GEMMs); with the bf16x6 kernels it is +0.1..2.4 %
+  // maps/s on AlexNet b256 (profiles/r02_ab_mc_overlap.txt)
+  {
+    const char* e = getenv("RRAM_MC_OVERLAP");
+    overlap_ = !(e && atoi(e) == 0) && first_fault_layer_ > 0;
+  }
   if (overlap_) {
     HIP_CALL(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
     HIP_CALL(hipEventCreateWithFlags(&ev_free_, hipEventDisableTiming));
