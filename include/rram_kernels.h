@@ -141,6 +141,11 @@ typedef struct {
   rram_inject_cfg cfg;
 } rram_inject_seg;
 /* All faultable blobs of a net in one launch; counters[i] for segment i. */
+/* Grid (blocks) of the injection launches: 0 = the default persistent grid
+ * (2048); returns the previous setting.  A smaller grid suits an injection
+ * that runs beside other kernels (MonteCarlo overlaps it with the layers
+ * before the first faultable one). */
+int rram_set_inject_grid(int blocks);
 int rram_inject_rng_batched(const rram_inject_seg* segs, int nsegs,
                             uint64_t seed, uint32_t map_id,
                             unsigned long long* counters, rram_stream_t stream);

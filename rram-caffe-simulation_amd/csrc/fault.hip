@@ -3,6 +3,7 @@
 // strategy and the SGD / fused training tail.  All are HBM-streaming kernels:
 // 16-byte (float4) loads and stores per lane where the pointers allow it,
 // 256-thread blocks, grid-stride, wave-level ballot reductions for counters.
+#include <atomic>
 #include <math.h>
 #include <stdlib.h>
 
@@ -215,6 +216,12 @@ struct InjectSegs {
 
 constexpr int kInjChunk = 256 * 4 * 4;  // elements per block-chunk (4 float4 per lane)
 constexpr int kInjectGrid = 2048;      // default persistent grid (RRAM_INJECT_GRID overrides)
+// rram_set_inject_grid: a caller-chosen grid (0: kInjectGrid), e.g. a smaller
+// one when the injection runs beside other kernels (MonteCarlo's overlap)
+std::atomic<int>& inject_grid() {
+  static std::atomic<int> g{0};
+  return g;
+}
 
 __device__ __forceinline__ float quantize_sym(float w, const InjectSeg& g) {
   // uniform levels over [-g_max, g_max]
@@ -718,6 +725,11 @@ int rram_broken_count(const float* e, int64_t n, unsigned long long* counter, rr
   return launch_status("broken_count");
 }
 
+int rram_set_inject_grid(int blocks) {
+  RRAM_REQUIRE(blocks >= 0, "set_inject_grid: negative grid");
+  return rram::inject_grid().exchange(blocks);
+}
+
 int rram_inject_rng_batched(const rram_inject_seg* segs, int nsegs, uint64_t seed,
                             uint32_t map_id, unsigned long long* counters, rram_stream_t s) {
   RRAM_REQUIRE(nsegs >= 0 && nsegs <= RRAM_MAX_SEGS, "inject: nsegs out of range");
@@ -742,11 +754,15 @@ int rram_inject_rng_batched(const rram_inject_seg* segs, int nsegs, uint64_t see
   // (190 vs 100 us): every block ends in a same-address counter atomic, and
   // the serialised atomics, not HBM, set the pace.  RRAM_INJECT_GRID (tuning
   // knob) overrides the grid.
-  static const int64_t grid_cap = [] {
+  static const int64_t grid_env = [] {
     const char* e = getenv("RRAM_INJECT_GRID");
     const long v = e ? atol(e) : 0;
-    return v > 0 ? static_cast<int64_t>(v) : static_cast<int64_t>(kInjectGrid);
+    return v > 0 ? static_cast<int64_t>(v) : static_cast<int64_t>(0);
   }();
+  const int64_t grid_cap = grid_env > 0 ? grid_env
+                           : inject_grid().load(std::memory_order_relaxed) > 0
+                               ? static_cast<int64_t>(inject_grid().load(std::memory_order_relaxed))
+                               : static_cast<int64_t>(kInjectGrid);
   const int grid = static_cast<int>(total < grid_cap ? total : grid_cap);
   bool fast = true;
   for (int i = 0; i < nsegs; ++i) fast = fast && is.s[i].mode == 0;

@@ -656,6 +656,10 @@ void MonteCarlo<Dtype>::Run(uint32_t map_begin, uint32_t map_count) {
     segs[i] = rram_inject_seg{clean_[i], params_[i]->mutable_gpu_data(), params_[i]->count(), (uint32_t)i, 0, cfgs_[i]};
   const size_t no = outs_.size();
   const int L = static_cast<int>(net_->layers().size());
+  // overlapped, the injection gets a 512-block grid: it then holds fewer CUs
+  // while conv1 runs beside it (conv1 0.400 -> 0.386 ms, +0.9 % maps/s;
+  // profiles/r02_ab_mc_overlap.txt); serial, the default 2048
+  const int prev_grid = rram_set_inject_grid(overlap_ ? 512 : 0);
   for (uint32_t m = map_begin; m < map_begin + map_count; ++m) {
     hipStream_t is = Caffe::hip_stream();
     if (overlap_) {
@@ -687,6 +691,7 @@ void MonteCarlo<Dtype>::Run(uint32_t map_begin, uint32_t map_count) {
     }
     ++maps_run_;
   }
+  rram_set_inject_grid(prev_grid);
 }
 
 template <typename Dtype>

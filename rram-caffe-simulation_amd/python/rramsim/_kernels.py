@@ -74,6 +74,7 @@ SIGNATURES = {
     "rram_fail_apply_batched": (I, [P, I, F, F, P, P]),
     "rram_broken_count": (I, [P, I64, P, P]),
     "rram_inject_rng": (I, [P, P, I64, P, U64, U32, U32, P, P]),
+    "rram_set_inject_grid": (I, [I]),
     "rram_inject_rng_batched": (I, [P, I, U64, U32, P, P]),
     "rram_threshold_strategy": (I, [P, I64, F, P, P]),
     "rram_stuck_zero_counts": (I, [P, P, I, I, P, P, P]),
