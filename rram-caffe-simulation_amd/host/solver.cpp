@@ -662,7 +662,15 @@ void MonteCarlo<Dtype>::Run(uint32_t map_begin, uint32_t map_count) {
   const int prev_grid = rram_set_inject_grid(overlap_ ? 512 : 0);
   for (uint32_t m = map_begin; m < map_begin + map_count; ++m) {
     hipStream_t is = Caffe::hip_stream();
+    // RRAM_MC_INJECT_AFTER = k (A/B knob): the overlapped injection starts
+    // once layers 0 .. k-1 of this map have run (default 0: at once)
+    static const int inj_after = [] {
+      const char* e = getenv("RRAM_MC_INJECT_AFTER");
+      return e ? atoi(e) : 0;
+    }();
+    const int k0 = overlap_ ? std::max(0, std::min(inj_after, first_fault_layer_)) : 0;
     if (overlap_) {
+      if (k0 > 0) net_->ForwardFromTo(0, k0 - 1, false);
       HIP_CALL(hipEventRecord(ev_free_, Caffe::hip_stream()));  // previous map's forward is done with the weights
       HIP_CALL(hipStreamWaitEvent(side_, ev_free_, 0));
       is = side_;
@@ -675,7 +683,7 @@ void MonteCarlo<Dtype>::Run(uint32_t map_begin, uint32_t map_count) {
     if (timing_) timer_.stop(0, is);
     if (overlap_) {
       HIP_CALL(hipEventRecord(ev_injected_, side_));
-      net_->ForwardFromTo(0, first_fault_layer_ - 1, false);     // convolutions run under the injection
+      if (k0 < first_fault_layer_) net_->ForwardFromTo(k0, first_fault_layer_ - 1, false);  // convolutions run under the injection
       HIP_CALL(hipStreamWaitEvent(Caffe::hip_stream(), ev_injected_, 0));
       net_->ForwardFromTo(first_fault_layer_, L - 1, false);
     } else {
