@@ -376,6 +376,46 @@ __global__ void __launch_bounds__(256) k_softmax(const float* __restrict__ x, fl
   }
 }
 
+// k_softmax with the column held in registers (C <= 64 R): one load pass and
+// one store pass instead of three loads; the same per-lane partial order and
+// shuffle trees, so the results are k_softmax's bit for bit.
+template <int R>
+__global__ void __launch_bounds__(256) k_softmax_reg(const float* __restrict__ x, float* __restrict__ y, int outer,
+                                                     int C, int inner) {
+  const int lane = threadIdx.x & 63;
+  const int64_t cols = (int64_t)outer * inner;
+  for (int64_t col = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; col < cols;
+       col += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+    const int64_t o = col / inner, q = col - o * inner;
+    const float* xs = x + o * C * inner + q;
+    float* ys = y + o * C * inner + q;
+    float v[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int c = lane + 64 * i;
+      v[i] = c < C ? xs[(int64_t)c * inner] : -FLT_MAX;
+    }
+    float m = -FLT_MAX;
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+      if (lane + 64 * i < C) m = fmaxf(m, v[i]);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+    float s = 0.0f;
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+      if (lane + 64 * i < C) {
+        v[i] = expf(v[i] - m);
+        s += v[i];
+      }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+      if (lane + 64 * i < C) ys[(int64_t)(lane + 64 * i) * inner] = v[i] / s;
+  }
+}
+
 // softmax_loss_layer.cpp:95-112 (single block, deterministic)
 __global__ void __launch_bounds__(1024) k_softmax_loss_fwd(const float* __restrict__ prob,
                                                            const float* __restrict__ label,
@@ -683,7 +723,10 @@ int rram_softmax_fwd(const float* x, float* y, int outer, int C, int inner, rram
   RRAM_REQUIRE(x && y, "softmax: NULL");
   int blocks = static_cast<int>((cols + 3) / 4);
   if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL(k_softmax, dim3(blocks), dim3(256), 0, as_stream(s), x, y, outer, C, inner);
+  if (C <= 64 * 16)
+    hipLaunchKernelGGL(k_softmax_reg<16>, dim3(blocks), dim3(256), 0, as_stream(s), x, y, outer, C, inner);
+  else
+    hipLaunchKernelGGL(k_softmax, dim3(blocks), dim3(256), 0, as_stream(s), x, y, outer, C, inner);
   return launch_status("softmax");
 }
 
