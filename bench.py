@@ -126,7 +126,10 @@ def main():
         local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # under torch.distributed.run the process group exists at every world
+    # size (N = 1 included), so the collectives below are the ones N > 1 runs
+    distributed = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ
+    if distributed:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -139,7 +142,7 @@ def main():
         res = run_workload(args, world, rank, dev)
         if rank == 0:
             print(json.dumps(res), flush=True)
-        if world > 1:
+        if distributed:
             dist.destroy_process_group()
         return
 
@@ -160,7 +163,7 @@ def main():
     mc.set_timing(True)
 
     stats = torch.zeros(8, dtype=torch.float64, device=dev)
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -174,7 +177,7 @@ def main():
     vals = st["sums"] + [float(sum(st["broken"])), float(st["maps"])]
     stats[:len(vals)] = torch.tensor(vals, dtype=torch.float64)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
+    if distributed:
         dist.all_reduce(stats)                     # RCCL: accuracy / loss / broken-cell sums
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.barrier()
@@ -225,7 +228,8 @@ def main():
         "config": {"workload": "alexnet_b256_mc_faultmap_inference", "model": "AlexNet (bvlc_alexnet train_val, TEST)",
                    "global_batch": args.batch * world, "batch_per_map": args.batch, "maps_per_step": world,
                    "p_fault": args.p_fault, "stuck_split_neg_zero_pos": [10, 20, 10],
-                   "fault_layers": "InnerProduct (58,631,144 weights)", "parallelism": f"mc-maps x{world} (RCCL stats all-reduce)",
+                   "fault_layers": "InnerProduct (58,631,144 weights)", "parallelism": (f"mc-maps x{world} ({'RCCL' if backend == 'nccl' else backend} stats all-reduce)"
+                                   if distributed else "mc-maps x1 (single process, no collective)"),
                    "f32_engine": "bf16x6 (exact 3-term bf16 split, 6 products, fp32 accumulation)"
                    if "bf16x6" in engines.values() else "f32 MFMA"},
         "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 2), "peak": round(peak_tf, 1),
@@ -255,7 +259,7 @@ def main():
         print(json.dumps(res), flush=True)
     mc.close()
     net.close()
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

@@ -145,6 +145,10 @@ int rram_solver_num_fail_blobs(rram_solver_t s, int* n);
 int rram_solver_fail_state(rram_solver_t s, int i, float** endurance, float** values, int64_t* count);
 /* broken cells per faultable blob after the last Fail() (device count, one D2H) */
 int rram_solver_broken_counts(rram_solver_t s, unsigned long long* out, int cap, int* n);
+/* SGDSolver::history() (sgd_solver.hpp:29, sgd_solver.cpp:16-26): the momentum
+ * history blob of learnable param i (device pointer, count). */
+int rram_solver_num_history(rram_solver_t s, int* n);
+int rram_solver_history(rram_solver_t s, int i, float** data, int64_t* count);
 
 /* Solver::ApplyStrategy (solver.cpp:25-33): run every failure_strategy's
  * Apply() once, outside Step (threshold / remapping / genetic). */

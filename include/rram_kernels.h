@@ -373,6 +373,10 @@ int rram_pool_bwd(const float* dy, const int* mask, float* dx, int num,
                   int pooled_w, int kernel_h, int kernel_w, int stride_h,
                   int stride_w, int pad_h, int pad_w, int method, rram_stream_t s);
 
+/* y[i] = (float)x[i]: a MAX pool's int32 argmax as the float top mask
+ * (pooling_layer.cu:30-34, the optional second top). */
+int rram_i32_to_f32(const int* x, float* y, int64_t n, rram_stream_t s);
+
 /* LRN ACROSS_CHANNELS (lrn_layer.cu): scale = k + alpha/size * sum x^2,
  * y = x * scale^-beta.  scale (nullable) keeps the scale for backward. */
 int rram_lrn_fwd(const float* x, float* y, float* scale, int num, int channels,
@@ -426,7 +430,16 @@ int rram_softmax_loss_bwd(const float* prob, const float* label, float* dx,
 int rram_accuracy(const float* x, const float* label, float* correct_out,
                   float* count_out, float* ratio_out, int outer, int channels,
                   int inner, int top_k, int ignore_label, rram_stream_t s);
-/* Concat along axis 1 (copy one bottom into its slot). */
+/* EuclideanLoss (euclidean_loss_layer.cu:9-38): diff = a - b,
+ * loss_out[0] = sum(diff^2) / num / 2 (device scalar, the layer's top);
+ * backward dx = alpha * diff with alpha = +-loss_weight / num. */
+int rram_euclidean_loss_fwd(const float* a, const float* b, float* diff, float* loss_out, int64_t n, int num,
+                            rram_stream_t s);
+int rram_euclidean_loss_bwd(const float* diff, float* dx, int64_t n, float alpha, rram_stream_t s);
+/* Concat / Slice copy (concat_layer.cu, slice_layer.cu): one bottom's
+ * [num][src_channels_x_inner] block into its slot of the
+ * [num][dst_channels_x_inner] top at offset_x_inner (backward != 0: the
+ * reverse copy, dst slot -> src). */
 int rram_concat_copy(const float* src, float* dst, int num, int src_channels_x_inner,
                      int dst_channels_x_inner, int offset_x_inner, int backward,
                      rram_stream_t s);

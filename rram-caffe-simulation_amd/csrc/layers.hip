@@ -588,6 +588,37 @@ __global__ void k_concat(const float* __restrict__ src, float* __restrict__ dst,
   }
 }
 
+// euclidean_loss_layer.cu:9-20: diff = a - b; loss = dot(diff, diff) / num / 2
+// (one block: loss layers see one blob, the summation order is fixed)
+__global__ void __launch_bounds__(1024) k_euclidean_fwd(const float* __restrict__ a, const float* __restrict__ b,
+                                                      float* __restrict__ diff, float* __restrict__ loss,
+                                                      int64_t n, int num) {
+  __shared__ float part[16];
+  float acc = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const float d = a[i] - b[i];
+    diff[i] = d;
+    acc += d * d;
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += part[w];
+    loss[0] = t / static_cast<float>(num) / 2.0f;
+  }
+}
+
+__global__ void k_i32_to_f32(const int* __restrict__ x, float* __restrict__ y, int64_t n) {
+  GRID_LOOP(i, n) y[i] = static_cast<float>(x[i]);
+}
+
+// euclidean_loss_layer.cu:23-38: dx = alpha * diff (caffe_gpu_axpby with beta 0)
+__global__ void k_scale_copy(const float* __restrict__ x, float* __restrict__ y, int64_t n, float alpha) {
+  GRID_LOOP(i, n) y[i] = alpha * x[i];
+}
+
 }  // namespace
 }  // namespace rram
 
@@ -783,6 +814,32 @@ int rram_accuracy(const float* x, const float* label, float* correct, float* cou
                        label, correct, count, outer, C, inner, top_k, ignore);
   if (ratio) hipLaunchKernelGGL(k_accuracy_ratio, dim3(1), dim3(1), 0, as_stream(s), correct, count, ratio);
   return launch_status("accuracy");
+}
+
+int rram_i32_to_f32(const int* x, float* y, int64_t n, rram_stream_t s) {
+  RRAM_REQUIRE(n >= 0, "i32_to_f32: n < 0");
+  RRAM_REQUIRE_I32(n, "i32_to_f32");
+  if (n == 0) return RRAM_OK;
+  RRAM_REQUIRE(x && y, "i32_to_f32: NULL");
+  hipLaunchKernelGGL(k_i32_to_f32, dim3(stream_blocks(n)), dim3(kThreads), 0, as_stream(s), x, y, n);
+  return launch_status("i32_to_f32");
+}
+
+int rram_euclidean_loss_fwd(const float* a, const float* b, float* diff, float* loss_out, int64_t n, int num,
+                            rram_stream_t s) {
+  RRAM_REQUIRE(n >= 0 && num > 0 && loss_out, "euclidean_loss_fwd: bad args");
+  RRAM_REQUIRE(n == 0 || (a && b && diff), "euclidean_loss_fwd: NULL");
+  hipLaunchKernelGGL(k_euclidean_fwd, dim3(1), dim3(1024), 0, as_stream(s), a, b, diff, loss_out, n, num);
+  return launch_status("euclidean_loss_fwd");
+}
+
+int rram_euclidean_loss_bwd(const float* diff, float* dx, int64_t n, float alpha, rram_stream_t s) {
+  RRAM_REQUIRE(n >= 0, "euclidean_loss_bwd: n < 0");
+  RRAM_REQUIRE_I32(n, "euclidean_loss_bwd");
+  if (n == 0) return RRAM_OK;
+  RRAM_REQUIRE(diff && dx, "euclidean_loss_bwd: NULL");
+  hipLaunchKernelGGL(k_scale_copy, dim3(stream_blocks(n)), dim3(kThreads), 0, as_stream(s), diff, dx, n, alpha);
+  return launch_status("euclidean_loss_bwd");
 }
 
 int rram_concat_copy(const float* src, float* dst, int num, int sci, int dci, int off, int backward,

@@ -473,6 +473,22 @@ int rram_solver_fail_state(rram_solver_t s, int i, float** e, float** v, int64_t
     if (count) *count = fi[i]->count();
   });
 }
+int rram_solver_num_history(rram_solver_t s, int* n) {
+  return guarded([&] {
+    NEED(s);
+    NEED(n);
+    *n = (int)s->solver->history().size();
+  });
+}
+int rram_solver_history(rram_solver_t s, int i, float** data, int64_t* count) {
+  return guarded([&] {
+    NEED(s);
+    const auto& h = s->solver->history();
+    if (i < 0 || i >= (int)h.size()) throw Error("history index out of range");
+    if (data) *data = h[i]->mutable_gpu_data();
+    if (count) *count = h[i]->count();
+  });
+}
 int rram_solver_broken_counts(rram_solver_t s, unsigned long long* out, int cap, int* n) {
   return guarded([&] {
     NEED(s);

@@ -5,6 +5,9 @@
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
+#include <fstream>
+
+#include "hdf5.hpp"
 
 namespace caffe {
 
@@ -352,12 +355,16 @@ class PoolingLayer : public Layer<Dtype> {
   explicit PoolingLayer(const Msg& p) : Layer<Dtype>(p) {}
   const char* type() const override { return "Pooling"; }
   int ExactNumBottomBlobs() const override { return 1; }
-  int ExactNumTopBlobs() const override { return 1; }
-  void LayerSetUp(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>&) override {
+  int MinTopBlobs() const override { return 1; }
+  void LayerSetUp(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
     const Msg& pp = this->layer_param_.sub_or_empty("pooling_param");
     const std::string pool = pp.str("pool", "MAX");
     CAFFE_CHECK(pool == "MAX" || pool == "AVE", this->name() << ": pool " << pool << " not supported");
     method_ = pool == "MAX" ? RRAM_POOL_MAX : RRAM_POOL_AVE;
+    // pooling_layer.hpp:29-33: MAX may publish its argmax as a second top
+    CAFFE_CHECK(top.size() == 1 || (top.size() == 2 && method_ == RRAM_POOL_MAX),
+                this->name() << ": Pooling produces 1 top (2 for MAX: output and mask)");
+    top_mask_ = top.size() > 1;
     global_ = pp.boolean("global_pooling", false);
     hw_param(pp, "kernel", 0, kh_, kw_);
     hw_param(pp, "stride", 1, sh_, sw_);
@@ -381,11 +388,12 @@ class PoolingLayer : public Layer<Dtype> {
       if ((PW_ - 1) * sw_ >= W_ + pw_) --PW_;
     }
     top[0]->Reshape({bottom[0]->shape(0), C_, PH_, PW_});
+    if (top.size() > 1) top[1]->ReshapeLike(*top[0]);
     if (method_ == RRAM_POOL_MAX) mask_.Reshape(top[0]->shape());
   }
 
   bool fuse_lrn_before(Blob<Dtype>* lrn_bottom, int size, float alpha, float beta, float k) override {
-    if (this->phase_ != TEST || method_ != RRAM_POOL_MAX || global_ || kh_ != kw_ || (kh_ != 2 && kh_ != 3) ||
+    if (this->phase_ != TEST || method_ != RRAM_POOL_MAX || global_ || top_mask_ || kh_ != kw_ || (kh_ != 2 && kh_ != 3) ||
         ph_ >= kh_ || pw_ >= kw_ || (size != 3 && size != 5))
       return false;
     lrn_src_ = lrn_bottom;
@@ -407,10 +415,13 @@ class PoolingLayer : public Layer<Dtype> {
       if (yo) mark_octets(top[0]);
       return;
     }
-    int* mask = (method_ == RRAM_POOL_MAX && this->phase_ == TRAIN)
+    const bool top_mask = top.size() > 1;
+    int* mask = (method_ == RRAM_POOL_MAX && (this->phase_ == TRAIN || top_mask))
                     ? reinterpret_cast<int*>(mask_.mutable_gpu_data()) : nullptr;
     RRAM_CALL(rram_pool_fwd(bottom[0]->gpu_data(), top[0]->mutable_gpu_data(), mask, bottom[0]->shape(0),
                             C_, H_, W_, PH_, PW_, kh_, kw_, sh_, sw_, ph_, pw_, method_, Caffe::stream()));
+    // the top mask holds the argmax index as a float (pooling_layer.cu:30-34)
+    if (top_mask) RRAM_CALL(rram_i32_to_f32(mask, top[1]->mutable_gpu_data(), top[1]->count(), Caffe::stream()));
   }
   void Backward_gpu(const std::vector<Blob<Dtype>*>& top, const std::vector<bool>& pd,
                     const std::vector<Blob<Dtype>*>& bottom) override {
@@ -423,7 +434,7 @@ class PoolingLayer : public Layer<Dtype> {
   }
   int method_ = RRAM_POOL_MAX, kh_ = 0, kw_ = 0, sh_ = 1, sw_ = 1, ph_ = 0, pw_ = 0;
   int C_ = 0, H_ = 0, W_ = 0, PH_ = 0, PW_ = 0;
-  bool global_ = false;
+  bool global_ = false, top_mask_ = false;
   Blob<Dtype> mask_;
   Blob<Dtype>* lrn_src_ = nullptr;  // bottom of a folded LRN (nullptr: unfused)
   int lrn_size_ = 5;
@@ -655,6 +666,10 @@ class AccuracyLayer : public Layer<Dtype> {
 };
 
 // ----------------------------------------------------------------- Concat
+// concat_layer.cpp:9-67 / .cu:22-66: any axis; bottom i occupies the slot
+// [off, off + shape_i(axis)) of every [outer] row of the top
+static int canon_axis(int axis, int num_axes) { return axis < 0 ? axis + num_axes : axis; }
+
 template <typename Dtype>
 class ConcatLayer : public Layer<Dtype> {
  public:
@@ -664,41 +679,158 @@ class ConcatLayer : public Layer<Dtype> {
   int ExactNumTopBlobs() const override { return 1; }
   void Reshape(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
     const Msg& cp = this->layer_param_.sub_or_empty("concat_param");
-    int axis = (int)cp.integer("axis", cp.integer("concat_dim", 1));
-    CAFFE_CHECK(axis == 1, this->name() << ": only channel concatenation is supported");
+    // concat_dim is the V1 spelling of axis (concat_layer.cpp:16-21)
+    axis_ = canon_axis((int)cp.integer("axis", cp.integer("concat_dim", 1)), bottom[0]->num_axes());
+    CAFFE_CHECK(axis_ >= 0 && axis_ < bottom[0]->num_axes(), this->name() << ": concat axis out of range");
     std::vector<int> s = bottom[0]->shape();
-    int ch = 0;
+    int along = 0;
     for (auto* b : bottom) {
-      CAFFE_CHECK(b->num_axes() == (int)s.size() && b->shape(0) == s[0] && b->count(2) == bottom[0]->count(2),
-                  this->name() << ": bottom shapes must match except along the concat axis");
-      ch += b->shape(1);
+      CAFFE_CHECK(b->num_axes() == (int)s.size(), this->name() << ": all inputs must have the same #axes");
+      for (int a = 0; a < (int)s.size(); ++a)
+        if (a != axis_)
+          CAFFE_CHECK(b->shape(a) == s[a], this->name() << ": all inputs must have the same shape, except at concat_axis");
+      along += b->shape(axis_);
     }
-    s[1] = ch;
+    s[axis_] = along;
     top[0]->Reshape(s);
+    if (bottom.size() == 1) top[0]->ShareData(*bottom[0]), top[0]->ShareDiff(*bottom[0]);
   }
 
  protected:
   void Forward_gpu(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
-    const int inner = (int)top[0]->count(2), dci = top[0]->shape(1) * inner, num = top[0]->shape(0);
+    if (bottom.size() == 1) return;
+    const int inner = (int)top[0]->count(axis_ + 1), outer = (int)top[0]->count(0, axis_);
+    const int dci = top[0]->shape(axis_) * inner;
     int off = 0;
     for (auto* b : bottom) {
-      const int sci = b->shape(1) * inner;
-      RRAM_CALL(rram_concat_copy(b->gpu_data(), top[0]->mutable_gpu_data(), num, sci, dci, off, 0, Caffe::stream()));
+      const int sci = b->shape(axis_) * inner;
+      RRAM_CALL(rram_concat_copy(b->gpu_data(), top[0]->mutable_gpu_data(), outer, sci, dci, off, 0, Caffe::stream()));
       off += sci;
     }
   }
   void Backward_gpu(const std::vector<Blob<Dtype>*>& top, const std::vector<bool>& pd,
                     const std::vector<Blob<Dtype>*>& bottom) override {
-    const int inner = (int)top[0]->count(2), dci = top[0]->shape(1) * inner, num = top[0]->shape(0);
+    if (bottom.size() == 1) return;
+    const int inner = (int)top[0]->count(axis_ + 1), outer = (int)top[0]->count(0, axis_);
+    const int dci = top[0]->shape(axis_) * inner;
     int off = 0;
     for (size_t i = 0; i < bottom.size(); ++i) {
-      const int sci = bottom[i]->shape(1) * inner;
+      const int sci = bottom[i]->shape(axis_) * inner;
       if (i < pd.size() && pd[i])
-        RRAM_CALL(rram_concat_copy(bottom[i]->mutable_gpu_diff(), const_cast<float*>(top[0]->gpu_diff()), num,
+        RRAM_CALL(rram_concat_copy(bottom[i]->mutable_gpu_diff(), const_cast<float*>(top[0]->gpu_diff()), outer,
                                    sci, dci, off, 1, Caffe::stream()));
       off += sci;
     }
   }
+  int axis_ = 1;
+};
+
+// ------------------------------------------------------------------ Slice
+// slice_layer.cpp:9-94 / .cu:22-66: the inverse of Concat (slice_point list or
+// an even split; slice_dim is the V1 spelling of axis)
+template <typename Dtype>
+class SliceLayer : public Layer<Dtype> {
+ public:
+  explicit SliceLayer(const Msg& p) : Layer<Dtype>(p) {}
+  const char* type() const override { return "Slice"; }
+  int ExactNumBottomBlobs() const override { return 1; }
+  int MinTopBlobs() const override { return 1; }
+  void Reshape(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
+    const Msg& sp = this->layer_param_.sub_or_empty("slice_param");
+    axis_ = canon_axis((int)sp.integer("axis", sp.integer("slice_dim", 1)), bottom[0]->num_axes());
+    CAFFE_CHECK(axis_ >= 0 && axis_ < bottom[0]->num_axes(), this->name() << ": slice axis out of range");
+    const int along = bottom[0]->shape(axis_);
+    const auto pts = ints_of(sp, "slice_point");
+    sizes_.clear();
+    if (!pts.empty()) {
+      CAFFE_CHECK(pts.size() == top.size() - 1, this->name() << ": need one slice_point fewer than tops");
+      int prev = 0;
+      for (int p : pts) {
+        CAFFE_CHECK(p > prev, this->name() << ": slice points must be increasing");
+        sizes_.push_back(p - prev);
+        prev = p;
+      }
+      CAFFE_CHECK(along > prev, this->name() << ": last slice point beyond the axis");
+      sizes_.push_back(along - prev);
+    } else {
+      CAFFE_CHECK(along % (int)top.size() == 0, this->name() << ": number of top blobs (" << top.size()
+                                                             << ") should evenly divide input slice axis (" << along << ")");
+      sizes_.assign(top.size(), along / (int)top.size());
+    }
+    std::vector<int> s = bottom[0]->shape();
+    for (size_t i = 0; i < top.size(); ++i) {
+      s[axis_] = sizes_[i];
+      top[i]->Reshape(s);
+    }
+    if (top.size() == 1) top[0]->ShareData(*bottom[0]), top[0]->ShareDiff(*bottom[0]);
+  }
+
+ protected:
+  void Forward_gpu(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
+    if (top.size() == 1) return;
+    const int inner = (int)bottom[0]->count(axis_ + 1), outer = (int)bottom[0]->count(0, axis_);
+    const int dci = bottom[0]->shape(axis_) * inner;
+    int off = 0;
+    for (size_t i = 0; i < top.size(); ++i) {
+      const int sci = sizes_[i] * inner;
+      RRAM_CALL(rram_concat_copy(top[i]->mutable_gpu_data(), const_cast<float*>(bottom[0]->gpu_data()), outer, sci,
+                                 dci, off, 1, Caffe::stream()));
+      off += sci;
+    }
+  }
+  void Backward_gpu(const std::vector<Blob<Dtype>*>& top, const std::vector<bool>& pd,
+                    const std::vector<Blob<Dtype>*>& bottom) override {
+    if (top.size() == 1 || !pd.size() || !pd[0]) return;
+    const int inner = (int)bottom[0]->count(axis_ + 1), outer = (int)bottom[0]->count(0, axis_);
+    const int dci = bottom[0]->shape(axis_) * inner;
+    int off = 0;
+    for (size_t i = 0; i < top.size(); ++i) {
+      const int sci = sizes_[i] * inner;
+      RRAM_CALL(rram_concat_copy(top[i]->gpu_diff(), bottom[0]->mutable_gpu_diff(), outer, sci, dci, off, 0,
+                                 Caffe::stream()));
+      off += sci;
+    }
+  }
+  int axis_ = 1;
+  std::vector<int> sizes_;
+};
+
+// ---------------------------------------------------------- EuclideanLoss
+// euclidean_loss_layer.cpp:9-20, .cu:9-38: loss = ||a - b||^2 / (2 num);
+// d/da = +loss_weight / num * (a - b), d/db = -loss_weight / num * (a - b)
+template <typename Dtype>
+class EuclideanLossLayer : public Layer<Dtype> {
+ public:
+  explicit EuclideanLossLayer(const Msg& p) : Layer<Dtype>(p) {}
+  const char* type() const override { return "EuclideanLoss"; }
+  int ExactNumBottomBlobs() const override { return 2; }
+  int ExactNumTopBlobs() const override { return 1; }
+  bool IsLoss() const override { return true; }
+  void Reshape(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
+    CAFFE_CHECK(bottom[0]->shape(0) == bottom[1]->shape(0),
+                "The data and label should have the same first dimension.");  // loss_layer.cpp:22-24
+    CAFFE_CHECK(bottom[0]->count(1) == bottom[1]->count(1), "Inputs must have the same dimension.");
+    top[0]->Reshape({});
+    diff_.ReshapeLike(*bottom[0]);
+  }
+
+ protected:
+  void Forward_gpu(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
+    RRAM_CALL(rram_euclidean_loss_fwd(bottom[0]->gpu_data(), bottom[1]->gpu_data(), diff_.mutable_gpu_data(),
+                                      top[0]->mutable_gpu_data(), bottom[0]->count(), bottom[0]->shape(0),
+                                      Caffe::stream()));
+  }
+  void Backward_gpu(const std::vector<Blob<Dtype>*>&, const std::vector<bool>& pd,
+                    const std::vector<Blob<Dtype>*>& bottom) override {
+    for (int i = 0; i < 2; ++i) {
+      if ((int)pd.size() <= i || !pd[i]) continue;
+      // the top diff of a loss layer is its loss weight (net.cpp:BackwardFromTo seeds it)
+      const Dtype alpha = (i == 0 ? Dtype(1) : Dtype(-1)) * this->loss(0) / bottom[i]->shape(0);
+      RRAM_CALL(rram_euclidean_loss_bwd(diff_.gpu_data(), bottom[i]->mutable_gpu_diff(), bottom[i]->count(), alpha,
+                                        Caffe::stream()));
+    }
+  }
+  Blob<Dtype> diff_;
 };
 
 // ----------------------------------------------------- data-like layers
@@ -754,7 +886,7 @@ class DummyDataLayer : public Layer<Dtype> {
                     const std::vector<Blob<Dtype>*>&) override {}
 };
 
-// Data / ImageData / HDF5Data / MemoryData / WindowData: the configs' LMDB /
+// Data / ImageData / MemoryData / WindowData: the configs' LMDB /
 // LevelDB / image sources are out of scope, so these tops are
 // synthetic tensors of the shape the source would produce:
 // integer pixels U{0..255}, minus 128 when the layer subtracts a mean, times
@@ -769,7 +901,7 @@ class SyntheticDataLayer : public Layer<Dtype> {
   void LayerSetUp(const std::vector<Blob<Dtype>*>&, const std::vector<Blob<Dtype>*>& top) override {
     const Msg& p = this->layer_param_;
     const Msg* dp = nullptr;
-    for (const char* k : {"data_param", "image_data_param", "hdf5_data_param", "memory_data_param", "window_data_param"})
+    for (const char* k : {"data_param", "image_data_param", "memory_data_param", "window_data_param"})
       if (p.sub(k)) dp = p.sub(k);
     const int batch = dp ? (int)dp->integer("batch_size", 1) : 1;
     const Msg& tp = p.sub_or_empty("transform_param");
@@ -800,6 +932,91 @@ class SyntheticDataLayer : public Layer<Dtype> {
                     const std::vector<Blob<Dtype>*>&) override {}
 };
 
+// HDF5Data (hdf5_data_layer.cpp:20-122, .cu:17-46): every top is the dataset
+// of the same name in the .h5 files the `source` list names, read through
+// libhdf5 (host/hdf5.cpp) and kept resident on the device; a Forward copies
+// batch_size rows, cycling the files in list order (shuffle is not part of
+// this build).  Under data-parallel training rank r of N takes only the rows
+// whose running index is r mod N (Caffe 1.0's HDF5DataLayer::Skip), so N
+// ranks x batch B see exactly the rows one process x batch N*B sees.
+template <typename Dtype>
+class HDF5DataLayer : public Layer<Dtype> {
+ public:
+  explicit HDF5DataLayer(const Msg& p) : Layer<Dtype>(p) {}
+  ~HDF5DataLayer() override {
+    for (float* d : dev_) (void)hipFree(d);
+  }
+  const char* type() const override { return "HDF5Data"; }
+  int ExactNumBottomBlobs() const override { return 0; }
+  int MinTopBlobs() const override { return 1; }
+  void LayerSetUp(const std::vector<Blob<Dtype>*>&, const std::vector<Blob<Dtype>*>& top) override {
+    const Msg& hp = this->layer_param_.sub_or_empty("hdf5_data_param");
+    batch_ = (int)hp.integer("batch_size", 0);
+    CAFFE_CHECK(batch_ > 0, this->name() << ": hdf5_data_param.batch_size must be > 0");
+    CAFFE_CHECK(!hp.boolean("shuffle", false), this->name() << ": hdf5_data_param.shuffle is not supported");
+    const std::string source = hp.str("source", "");
+    std::ifstream list(source);
+    CAFFE_CHECK(list.good(), "Failed to open source file " << source);
+    std::vector<std::string> files;
+    for (std::string line; std::getline(list, line);) {
+      const size_t a = line.find_first_not_of(" \t\r"), b = line.find_last_not_of(" \t\r");
+      if (a != std::string::npos) files.push_back(line.substr(a, b - a + 1));
+    }
+    CAFFE_CHECK(!files.empty(), "No HDF5 files listed in " << source);
+    const auto tops = this->layer_param_.strs("top");
+    std::vector<std::vector<float>> host(top.size());
+    rows_ = 0;
+    for (const auto& f : files) {
+      h5::Handle fh = h5::open_file(f);
+      int64_t frows = -1;
+      for (size_t j = 0; j < top.size(); ++j) {
+        std::vector<int64_t> dims;
+        std::vector<float> v = h5::load_floats(fh.id(), tops[j], &dims);
+        CAFFE_CHECK(!dims.empty(), f << ": dataset " << tops[j] << " has no axes");
+        if (frows < 0) frows = dims[0];
+        CAFFE_CHECK(dims[0] == frows, f << ": datasets must have the same number of rows");  // hdf5_data_layer.cpp:57-60
+        std::vector<int> shape(dims.begin(), dims.end());
+        shape[0] = batch_;
+        if (shapes_.size() <= j) shapes_.push_back(shape);
+        CAFFE_CHECK(shapes_[j] == shape, f << ": dataset " << tops[j] << " row shape differs between files");
+        host[j].insert(host[j].end(), v.begin(), v.end());
+      }
+      rows_ += frows;
+    }
+    CAFFE_CHECK(rows_ > 0, this->name() << ": the HDF5 files hold no rows");
+    for (size_t j = 0; j < top.size(); ++j) {
+      float* d = nullptr;
+      HIP_CALL(hipMalloc(&d, host[j].size() * sizeof(float)));
+      HIP_CALL(hipMemcpy(d, host[j].data(), host[j].size() * sizeof(float), hipMemcpyHostToDevice));
+      dev_.push_back(d);
+      row_elems_.push_back((int64_t)(host[j].size() / rows_));
+      top[j]->Reshape(shapes_[j]);
+    }
+    rank_ = (int)this->layer_param_.integer("rram_solver_rank", 0);
+    world_ = std::max(1, (int)this->layer_param_.integer("rram_solver_count", 1));
+    if (this->phase_ == TEST) rank_ = 0, world_ = 1;  // Skip() never skips in TEST
+  }
+  void Reshape(const std::vector<Blob<Dtype>*>&, const std::vector<Blob<Dtype>*>&) override {}
+
+ protected:
+  void Forward_gpu(const std::vector<Blob<Dtype>*>&, const std::vector<Blob<Dtype>*>& top) override {
+    for (int i = 0; i < batch_; ++i) {
+      while (offset_++ % world_ != rank_) row_ = (row_ + 1) % rows_;
+      for (size_t j = 0; j < top.size(); ++j)
+        HIP_CALL(hipMemcpyAsync(top[j]->mutable_gpu_data() + i * row_elems_[j], dev_[j] + row_ * row_elems_[j],
+                                row_elems_[j] * sizeof(float), hipMemcpyDeviceToDevice, Caffe::hip_stream()));
+      row_ = (row_ + 1) % rows_;
+    }
+  }
+  void Backward_gpu(const std::vector<Blob<Dtype>*>&, const std::vector<bool>&,
+                    const std::vector<Blob<Dtype>*>&) override {}
+  int batch_ = 0, rank_ = 0, world_ = 1;
+  int64_t rows_ = 0, row_ = 0, offset_ = 0;
+  std::vector<std::vector<int>> shapes_;
+  std::vector<int64_t> row_elems_;
+  std::vector<float*> dev_;
+};
+
 REGISTER_LAYER_CLASS(Convolution);
 REGISTER_LAYER_CLASS(InnerProduct);
 REGISTER_LAYER_CLASS(ReLU);
@@ -813,10 +1030,12 @@ REGISTER_LAYER_CLASS(Accuracy);
 REGISTER_LAYER_CLASS(Concat);
 REGISTER_LAYER_CLASS(Input);
 REGISTER_LAYER_CLASS(DummyData);
+REGISTER_LAYER_CLASS(Slice);
+REGISTER_LAYER_CLASS(EuclideanLoss);
+REGISTER_LAYER_CLASS(HDF5Data);
 static ::caffe::LayerRegisterer<float> g_data_aliases[] = {
     {"Data", [](const Msg& p) -> std::shared_ptr<Layer<float>> { return std::make_shared<SyntheticDataLayer<float>>(p); }},
     {"ImageData", [](const Msg& p) -> std::shared_ptr<Layer<float>> { return std::make_shared<SyntheticDataLayer<float>>(p); }},
-    {"HDF5Data", [](const Msg& p) -> std::shared_ptr<Layer<float>> { return std::make_shared<SyntheticDataLayer<float>>(p); }},
     {"MemoryData", [](const Msg& p) -> std::shared_ptr<Layer<float>> { return std::make_shared<SyntheticDataLayer<float>>(p); }},
     {"WindowData", [](const Msg& p) -> std::shared_ptr<Layer<float>> { return std::make_shared<SyntheticDataLayer<float>>(p); }},
 };

@@ -159,10 +159,14 @@ Net<Dtype>::Net(const Msg& in_param, Phase phase, const Msg& options) : phase_(p
     Msg lp = *lp_const;
     lp.set("phase", phase == TRAIN ? "TRAIN" : "TEST");
     const std::string type = lp.str("type");
-    if (type == "Data" || type == "ImageData" || type == "HDF5Data" || type == "MemoryData" || type == "WindowData") {
+    if (type == "Data" || type == "ImageData" || type == "MemoryData" || type == "WindowData") {
       for (int d : data_shape) lp.add("rram_data_shape", std::to_string(d));
       lp.set("rram_num_classes", options.str("num_classes", "10"));
       lp.set("rram_data_seed", options.str("data_seed", "0"));
+    }
+    if (type == "HDF5Data") {  // data-parallel row split (HDF5DataLayer::Skip)
+      lp.set("rram_solver_rank", options.str("solver_rank", "0"));
+      lp.set("rram_solver_count", options.str("solver_count", "1"));
     }
     auto layer = LayerRegistry<Dtype>::CreateLayer(lp);
     layer->layer_id = static_cast<uint32_t>(lid);

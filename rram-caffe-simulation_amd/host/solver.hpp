@@ -193,6 +193,8 @@ class Solver {
   std::shared_ptr<FailureMaker<Dtype>> failure_maker() { return fmaker_; }
   const std::vector<std::shared_ptr<FailureStrategy<Dtype>>>& strategies() const { return strategys_; }
   Dtype smoothed_loss() const { return smoothed_loss_; }
+  // SGDSolver::history() (sgd_solver.hpp:29): momentum history, one blob per learnable param
+  const std::vector<std::unique_ptr<Blob<Dtype>>>& history() const { return history_; }
   // Solver::Callback::on_gradients_ready (solver.hpp:80-91): the data-parallel
   // hook (RCCL all-reduce of the flat gradient buffer).
   std::function<void()> on_gradients_ready;

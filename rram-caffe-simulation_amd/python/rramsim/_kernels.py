@@ -122,6 +122,9 @@ SIGNATURES = {
     "rram_softmax_loss_bwd": (I, [P, P, P, I, I, I, I, F, P]),
     "rram_accuracy": (I, [P, P, P, P, P, I, I, I, I, I, P]),
     "rram_concat_copy": (I, [P, P, I, I, I, I, I, P]),
+    "rram_euclidean_loss_fwd": (I, [P, P, P, P, I64, I, P]),
+    "rram_euclidean_loss_bwd": (I, [P, P, I64, F, P]),
+    "rram_i32_to_f32": (I, [P, P, I64, P]),
     "rram_dropout_fwd": (I, [P, P, P, I64, F, U64, U32, U64, P]),
     "rram_dropout_bwd": (I, [P, P, P, I64, F, P]),
     "rram_bias_add": (I, [P, P, I, I, I, P]),

@@ -66,6 +66,8 @@ SIGNATURES = {
     "rram_solver_num_fail_blobs": (I, [P, PI]),
     "rram_solver_fail_state": (I, [P, I, PP, PP, PI64]),
     "rram_solver_broken_counts": (I, [P, C.POINTER(C.c_ulonglong), I, PI]),
+    "rram_solver_num_history": (I, [P, PI]),
+    "rram_solver_history": (I, [P, I, PP, PI64]),
     "rram_solver_apply_strategies": (I, [P]),
     "rram_solver_strategy_info": (I, [P, I, C.c_char_p, I, PI, PI, PI]),
     "rram_solver_snapshot": (I, [P, C.c_char_p, I]),
@@ -531,6 +533,17 @@ class Solver:
         n = C.c_int()
         check(self._lib.rram_solver_broken_counts(self.h, buf, 256, C.byref(n)), "broken_counts")
         return [buf[i] for i in range(n.value)]
+
+    def history(self):
+        """SGDSolver::history(): momentum blob per learnable param (device views)."""
+        n = C.c_int()
+        check(self._lib.rram_solver_num_history(self.h, C.byref(n)), "num_history")
+        out = []
+        for i in range(n.value):
+            d, cnt = C.c_void_p(), C.c_int64()
+            check(self._lib.rram_solver_history(self.h, i, C.byref(d), C.byref(cnt)), "history")
+            out.append(_wrap_device(d.value, (cnt.value,)))
+        return out
 
 
 class MonteCarlo:

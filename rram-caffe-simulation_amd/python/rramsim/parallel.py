@@ -31,10 +31,13 @@ def shard_maps(total_maps: int, rank: int, world: int) -> List[int]:
 
 
 def average_gradients(flat, world: int, group=None):
-    """Sum-all-reduce the flat gradient buffer and scale by 1/world."""
+    """Sum-all-reduce the flat gradient buffer and scale by 1/world.  With a
+    process group of one rank the all-reduce still runs (the collective path
+    is the one a multi-GPU job takes; the sum of one rank is exact)."""
     import torch.distributed as dist
-    if world > 1:
+    if world > 1 or (dist.is_available() and dist.is_initialized()):
         dist.all_reduce(flat, group=group)
+    if world > 1:
         flat.mul_(1.0 / world)
 
 
@@ -73,7 +76,7 @@ def allreduce_stats(values: List[float], device, group=None) -> List[float]:
     import torch
     import torch.distributed as dist
     t = torch.tensor(values, dtype=torch.float64, device=device)
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_available() and dist.is_initialized():
         dist.all_reduce(t, group=group)
     return t.tolist()
 
@@ -95,6 +98,8 @@ class DataParallelSolver:
         caffe.set_random_seed(seed)            # identical weights and fault maps on every rank
         opts = dict(options or {})
         opts["data_seed"] = self.rank           # a different synthetic data shard per rank
+        opts["solver_rank"] = self.rank         # HDF5Data row split (HDF5DataLayer::Skip)
+        opts["solver_count"] = self.world
         self.solver = caffe.Solver(solver_prototxt, net_prototxt, opts, log=log if self.rank == 0 else None)
         net = self.solver.net
         n = net.flat_param_count()

@@ -24,13 +24,18 @@ import time
 MFMA_F32_PEAK_TFLOPS = 157.3
 
 
+def _dist_on():
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
+
+
 def _timed(world, dev, fn, steps, warmup):
     import torch
     import torch.distributed as dist
     for i in range(warmup):
         fn(i)
     torch.cuda.synchronize()
-    if world > 1:
+    if _dist_on():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -39,7 +44,7 @@ def _timed(world, dev, fn, steps, warmup):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     t = torch.tensor([el], dtype=torch.float64, device=dev)
-    if world > 1:
+    if _dist_on():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 

@@ -182,3 +182,34 @@ def test_bench_two_ranks_rehearsal(device, workload):
     else:
         # 89,578 fp32 grads fit one 4 MB bucket: a single all-reduce, no overlap plan
         assert res["config"]["parallelism"].startswith("dp2 (RCCL all-reduce of 89578 fp32 grads")
+
+
+@pytest.mark.parametrize("workload", ["alexnet_mc", "cifar10_full_train"])
+def test_bench_rccl_world1(device, workload):
+    """bench.py under torch.distributed.run with the default backend (RCCL):
+    world size 1 on this box's GPU runs init_process_group("nccl",
+    device_id=...), the barriers, the stats / max-time all-reduces and (for
+    training) the gradient all-reduce — the collectives an 8-GPU job issues
+    (replaces parallel.cpp:324-380)."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k != "RRAM_BENCH_DIST_BACKEND"}
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(root / "bench.py"),
+           "--gpus", "1", "--steps", "3", "--warmup", "1", "--workload", workload, "--no-cpu-baseline"]
+    if workload == "alexnet_mc":
+        cmd += ["--batch", "64"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=str(root))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 1 and res["value"] > 0
+    if workload == "alexnet_mc":
+        assert res["config"]["parallelism"] == "mc-maps x1 (RCCL stats all-reduce)"
+        assert res["mc_stats"]["maps"] == 3
+    else:
+        assert res["config"]["parallelism"].startswith("dp1 (RCCL all-reduce")
