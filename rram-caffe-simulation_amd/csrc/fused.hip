@@ -13,39 +13,50 @@ namespace {
 
 // LRN ACROSS_CHANNELS followed by MAX pooling with a K x K window.
 //
-// Block = one image x a band of RB pooled rows; it walks all channels once.
-// Per channel, every thread produces the LRN value of up to PPT input pixels of
-// the band (the band's input rows are contiguous in memory, so the loads are
-// coalesced), keeping for each pixel the SIZE-channel ring of x and the running
-// sum of squares, updated exactly as k_lrn_fwd_slide / LRNFillScale
-// (lrn_layer.cu:9-51: add the channel entering the window, then subtract the
-// one leaving it), so each LRN value x * (k + alpha/size * sum)^-beta
-// (lrn_layer.cu:72-78) is the unfused kernel's bit for bit.  The values go to
-// an LDS plane (double-buffered: one barrier per channel) from which the
-// band's pooled outputs take the max over their window exactly as
-// MaxPoolForward (pooling_layer.cu:11-47): window clipped to the image,
-// -FLT_MAX start, strict ">" in row-major order.
-// HBM traffic: x read once (plus the one shared input row between adjacent
-// bands), y written once; the LRN output never leaves the CU.
+// Block = one image x a band of RB pooled rows x a chunk of CC channels
+// (blockIdx.z): the chunks give the grid several block waves (one image x
+// band per block, walking all channels, left AlexNet's norm2 at 512 blocks,
+// latency-bound).  Per channel, every thread produces the LRN value of up to
+// PPT input pixels of the band (the band's input rows are contiguous in
+// memory, so the loads are coalesced), from a register ring of the SIZE
+// channels around it: scale = k + alpha/size * sum of the SIZE squares in
+// channel order (lrn_sq_add, the unfused k_lrn_fwd_slide's sum, so each LRN
+// value x * scale^-beta (lrn_layer.cu:72-78) is the unfused kernel's bit for
+// bit, whatever chunk it falls in).  A chunk reads its PRE / POST halo
+// channels too (AlexNet: 4 of 36 per chunk, mostly L2 / MALL hits).  The
+// values go to an LDS plane (double-buffered: one barrier per group of G
+// channels) from which the band's pooled outputs take the max over their
+// window exactly as MaxPoolForward (pooling_layer.cu:11-47): window clipped to
+// the image, -FLT_MAX start, strict ">" in row-major order.
+// HBM traffic: x read once (plus the shared input row between adjacent bands
+// and the chunk halos), y written once; the LRN output never leaves the CU.
 constexpr int kBandPix = 512;  // input pixels per band (PPT = 2 per thread)
+// target grid of the LRN + pool fusion: several block waves of 256 CUs
+static int kLrnBlocks = [] {
+  const char* e = getenv("RRAM_LRN_BLOCKS");
+  return e ? atoi(e) : 4096;
+}();
 
 // G channels per barrier; the loads run one group ahead.  Measured on MI355X
 // (AlexNet b256): G = 2 for norm1 (55 x 55 planes), G = 4 for norm2 (27 x 27).
 // OCT: also write y's channel-octet companion yo (the next convolution's
 // pre-split input, x6.hip k_pack_octets_x6 layout [num][C/8][PH][PW][3][8]
 // bf16): the pooled values of 8 channels are gathered in an LDS plane and
-// split by the band's output threads (C % 8 == 0).
+// split by the band's output threads (C % 8 == 0 and CC % 8 == 0; G divides 8).
 template <int K, int SIZE, int G, bool OCT>
 __global__ void __launch_bounds__(256)
     k_lrn_maxpool_band(const float* __restrict__ x, float* __restrict__ y, char* __restrict__ yo, int C, int H, int W,
-                       int PH, int PW, int sh, int sw, int ph, int pw, int RB, float alpha_over_size, float beta,
-                       float k) {
+                       int PH, int PW, int sh, int sw, int ph, int pw, int RB, int CC, float alpha_over_size,
+                       float beta, float k) {
+  static_assert(!OCT || (8 % (2 * G) == 0), "the octet walk needs G in {2, 4}");
   constexpr int PRE = (SIZE - 1) / 2;
   constexpr int D = G;
   constexpr int PPT = kBandPix / 256;
   __shared__ float ybuf[2][D][kBandPix];
   __shared__ float obuf[OCT ? 8 : 1][OCT ? 256 : 1];
   const int n = blockIdx.y;
+  const int cb = blockIdx.z * CC;
+  const int ce = min(C, cb + CC);
   const int pr0 = blockIdx.x * RB;
   const int pr1 = min(PH, pr0 + RB);
   const int h0 = max(0, pr0 * sh - ph);
@@ -69,19 +80,14 @@ __global__ void __launch_bounds__(256)
   // work, instead of one group whose loads the ring shift waits for.
   float win[PPT][SIZE + D];
   float st0[D][PPT], st1[D][PPT];
-  float acc[PPT];
 #pragma unroll
-  for (int q = 0; q < PPT; ++q) {
+  for (int q = 0; q < PPT; ++q)
 #pragma unroll
-    for (int j = 0; j < SIZE + D; ++j) win[q][j] = ld(q, j - PRE);
-    acc[q] = 0.0f;
-#pragma unroll
-    for (int j = PRE; j < SIZE; ++j) acc[q] = lrn_sq_add(acc[q], win[q][j]);
-  }
+    for (int j = 0; j < SIZE + D; ++j) win[q][j] = ld(q, cb + j - PRE);
 #pragma unroll
   for (int d = 0; d < D; ++d)
 #pragma unroll
-    for (int q = 0; q < PPT; ++q) st1[d][q] = ld(q, SIZE + D - PRE + d);  // group 1's entering channels
+    for (int q = 0; q < PPT; ++q) st1[d][q] = ld(q, cb + SIZE + D - PRE + d);  // group 1's entering channels
   const int NO = (pr1 - pr0) * PW;  // pooled outputs of the band per channel
   const int64_t PHW = (int64_t)PH * PW;
   float* yn = y + (int64_t)n * C * PHW;
@@ -123,15 +129,17 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
       for (int q = 0; q < PPT; ++q) {
         // the helpers k_lrn_fwd_slide uses, in the same order
-        const float v = lrn_out(win[q][d + PRE], lrn_scale(acc[q], alpha_over_size, k), beta);
+        float acc = 0.0f;
+#pragma unroll
+        for (int j = 0; j < SIZE; ++j) acc = lrn_sq_add(acc, win[q][d + j]);
+        const float v = lrn_out(win[q][d + PRE], lrn_scale(acc, alpha_over_size, k), beta);
         if (own[q]) yb[d][pix[q]] = v;
-        acc[q] = lrn_slide(acc[q], win[q][d + SIZE], win[q][d]);
       }
     }
     __syncthreads();
     // pool the group's D channels (MaxPoolForward: -FLT_MAX start, strict ">"
     // in row-major window order over the taps inside the image)
-    const int nd = min(D, C - c0);
+    const int nd = min(D, ce - c0);
 #pragma unroll
     for (int i = 0; i < MAXI; ++i) {
       const int d = it_d[i];
@@ -159,15 +167,15 @@ __global__ void __launch_bounds__(256)
     }
   };
   if (!OCT) {
-    for (int c0 = 0; c0 < C; c0 += 2 * D) {
+    for (int c0 = cb; c0 < ce; c0 += 2 * D) {
       group(c0, ybuf[0], st0, st1);
-      if (c0 + D < C) group(c0 + D, ybuf[1], st1, st0);
+      if (c0 + D < ce) group(c0 + D, ybuf[1], st1, st0);
     }
     return;
   }
   // OCT: 8 channels per step (an even number of groups), then the octet
   char* yon = yo + (int64_t)n * (C / 8) * PHW * 48;
-  for (int c0 = 0; c0 < C; c0 += 8) {
+  for (int c0 = cb; c0 < ce; c0 += 8) {
 #pragma unroll
     for (int g = 0; g < 8; g += 2 * D) {
       group(c0 + g, ybuf[0], st0, st1);
@@ -215,7 +223,7 @@ int rram_lrn_maxpool_fwd_octets(const float* x, float* y, void* y_oct, int num, 
   if (num == 0) return RRAM_OK;
   RRAM_REQUIRE(x && y, "lrn_maxpool_fwd: NULL");
   // band height: input rows of RB pooled rows must fit the block's pixel
-  // budget and RB * PW outputs its threads; prefer >= 1024 blocks
+  // budget and RB * PW outputs its threads
   auto fits = [&](int rb) {
     const int rows = min(H, (rb - 1) * sh + kernel);
     return rb * PW <= kThreads && rows * W <= kBandPix;
@@ -223,32 +231,33 @@ int rram_lrn_maxpool_fwd_octets(const float* x, float* y, void* y_oct, int num, 
   RRAM_REQUIRE(fits(1), "lrn_maxpool_fwd: a pooled row needs more than %d input pixels", kBandPix);
   int rb = 1;
   while (rb < PH && fits(rb + 1)) ++rb;
-  while (rb > 1 && (int64_t)num * ((PH + rb - 1) / rb) < 1024 && fits(rb - 1) && (rb - 1) * sh >= kernel) --rb;
-  const dim3 grid(static_cast<unsigned>((PH + rb - 1) / rb), static_cast<unsigned>(num));
+  // channels per barrier: measured G = 2 for 55 x 55 planes, 4 for 27 x 27
+  const int gsel = H * W >= 1024 ? 2 : 4;
+  // channel chunks: as few as give >= kLrnBlocks blocks (each chunk re-reads
+  // SIZE - 1 halo channels), equal sizes in multiples of 8 (2 * G without octets)
+  const int step = y_oct ? 8 : 2 * gsel;
+  const int64_t bands = (PH + rb - 1) / rb;
+  const int64_t tiles = (int64_t)num * bands;  // > 0
+  const int64_t want = ((int64_t)kLrnBlocks + tiles - 1) / tiles;
+  const int64_t most = (C + step - 1) / step;
+  const int chunks = static_cast<int>(want < 1 ? 1 : (want > most ? most : want));
+  const int cc = ((C + chunks - 1) / chunks + step - 1) / step * step;
+  const dim3 grid(static_cast<unsigned>(bands), static_cast<unsigned>(num), static_cast<unsigned>((C + cc - 1) / cc));
   const float aos = alpha / size;
-  // channels per barrier: measured G = 2 for 55 x 55 planes, 4 for 27 x 27;
-  // RRAM_LRN_G overrides (2 | 4 | 8) for A/B
-  static const int g_env = [] {
-    const char* e = getenv("RRAM_LRN_G");
-    return e ? atoi(e) : 0;
-  }();
-  const int gsel = g_env == 2 || g_env == 4 || g_env == 8 ? g_env : (H * W >= 1024 ? 2 : 4);
   char* yo = static_cast<char*>(y_oct);
 #define RRAM_LP2(K_, S_, G_)                                                                                  \
   if (yo)                                                                                                     \
     hipLaunchKernelGGL((k_lrn_maxpool_band<K_, S_, G_, true>), grid, dim3(kThreads), 0, as_stream(s), x, y, yo, \
-                       C, H, W, PH, PW, sh, sw, ph, pw, rb, aos, beta, k);                                    \
+                       C, H, W, PH, PW, sh, sw, ph, pw, rb, cc, aos, beta, k);                                \
   else                                                                                                        \
     hipLaunchKernelGGL((k_lrn_maxpool_band<K_, S_, G_, false>), grid, dim3(kThreads), 0, as_stream(s), x, y,    \
-                       yo, C, H, W, PH, PW, sh, sw, ph, pw, rb, aos, beta, k);
+                       yo, C, H, W, PH, PW, sh, sw, ph, pw, rb, cc, aos, beta, k);
 #define RRAM_LP(K_, S_)          \
   if (kernel == K_ && size == S_) { \
     if (gsel == 2) {             \
       RRAM_LP2(K_, S_, 2)        \
-    } else if (gsel == 4) {      \
-      RRAM_LP2(K_, S_, 4)        \
     } else {                     \
-      RRAM_LP2(K_, S_, 8)        \
+      RRAM_LP2(K_, S_, 4)        \
     }                            \
   }
   RRAM_LP(3, 5)

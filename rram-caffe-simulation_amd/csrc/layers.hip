@@ -205,7 +205,12 @@ __global__ void k_pool_bwd(const float* __restrict__ dy, const int* __restrict__
   }
 }
 
-// lrn_layer.cu LRNFillScale + LRNComputeOutput (window sum evaluated directly)
+// lrn_layer.cu LRNFillScale + LRNComputeOutput.  The window sum is evaluated
+// directly, the squares added in channel order (lrn_sq_add), not by the
+// reference's add-entering / subtract-leaving slide: every scale is then a
+// function of its own SIZE inputs only (no cancellation carried along the
+// channel walk), so a kernel may start the walk at any channel (the chunked
+// LRN + pool fusion, fused.hip) and still produce these bits.
 __global__ void k_lrn_fwd(const float* __restrict__ x, float* __restrict__ y, float* __restrict__ scale,
                           int num, int C, int HW, int size, float alpha_over_size, float beta,
                           float k) {
@@ -218,19 +223,16 @@ __global__ void k_lrn_fwd(const float* __restrict__ x, float* __restrict__ y, fl
     const float* xc = x + n * C * HW + s;
     float acc = 0.0f;
     const int c0 = max(c - pre, 0), c1 = min(c - pre + size, C);
-    for (int j = c0; j < c1; ++j) {
-      const float v = xc[(int64_t)j * HW];
-      acc += v * v;
-    }
-    const float sc = k + acc * alpha_over_size;
+    for (int j = c0; j < c1; ++j) acc = lrn_sq_add(acc, xc[(int64_t)j * HW]);
+    const float sc = lrn_scale(acc, alpha_over_size, k);
     if (scale) scale[idx] = sc;
-    y[idx] = x[idx] * pow_pos(sc, -beta);
+    y[idx] = lrn_out(x[idx], sc, beta);
   }
 }
 
-// lrn_layer.cu LRNFillScale's sliding window (same add-then-subtract order):
-// one thread per (n, h, w) column walks the channels with the window in
-// registers, so x is read once and y written once.
+// The same arithmetic for SIZE 3 / 5: one thread per (n, h, w) column walks
+// the channels with the window in registers, so x is read once and y written
+// once.
 template <int SIZE>
 __global__ void __launch_bounds__(256) k_lrn_fwd_slide(const float* __restrict__ x, float* __restrict__ y,
                                                        float* __restrict__ scale, int num, int C, int HW,
@@ -250,9 +252,6 @@ __global__ void __launch_bounds__(256) k_lrn_fwd_slide(const float* __restrict__
     const int cc = j - PRE;
     win[j] = (cc >= 0 && cc < C) ? xc[(int64_t)cc * HW] : 0.0f;
   }
-  float acc = 0.0f;
-#pragma unroll
-  for (int j = PRE; j < SIZE; ++j) acc = lrn_sq_add(acc, win[j]);
   for (int c0 = 0; c0 < C; c0 += D) {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
@@ -263,11 +262,12 @@ __global__ void __launch_bounds__(256) k_lrn_fwd_slide(const float* __restrict__
     for (int d = 0; d < D; ++d) {
       const int c = c0 + d;
       if (c < C) {
-        // same add-then-subtract order as LRNFillScale (lrn_layer.cu:26-43)
+        float acc = 0.0f;  // channels c - PRE .. c + POST in order (zeros outside [0, C) add nothing)
+#pragma unroll
+        for (int j = 0; j < SIZE; ++j) acc = lrn_sq_add(acc, win[d + j]);
         const float sc = lrn_scale(acc, alpha_over_size, k);
         if (scale) scale[base + (int64_t)c * HW] = sc;
         yc[(int64_t)c * HW] = lrn_out(win[d + PRE], sc, beta);
-        acc = lrn_slide(acc, win[d + SIZE], win[d]);
       }
     }
 #pragma unroll

@@ -105,9 +105,6 @@ __host__ __device__ __forceinline__ U32x4 draw(uint64_t seed, uint64_t index, ui
 // kernel (layers.hip) and the LRN+pool fusion (fused.hip) so both produce the
 // same bits: explicit fmaf leaves nothing to the compiler's contraction choice.
 __device__ __forceinline__ float lrn_sq_add(float acc, float v) { return fmaf(v, v, acc); }
-__device__ __forceinline__ float lrn_slide(float acc, float add, float sub) {
-  return fmaf(-sub, sub, fmaf(add, add, acc));  // add the entering channel, then drop the leaving one
-}
 __device__ __forceinline__ float lrn_scale(float acc, float alpha_over_size, float k) {
   return fmaf(acc, alpha_over_size, k);
 }

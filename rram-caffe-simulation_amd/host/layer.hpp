@@ -55,6 +55,9 @@ class Layer {
   virtual bool EqualNumBottomTopBlobs() const { return false; }
   virtual bool AllowForceBackward(int) const { return true; }
   virtual bool IsLoss() const { return false; }
+  // layer.hpp:282-288 / loss_layer.hpp:40: loss layers get an anonymous top
+  // when the prototxt names none (Net allocates it, net.cpp:123-135)
+  virtual bool AutoTopBlobs() const { return false; }
 
   Dtype loss(int top_index) const {
     return top_index < (int)loss_.size() ? loss_[top_index] : Dtype(0);

@@ -588,6 +588,7 @@ class SoftmaxWithLossLayer : public Layer<Dtype> {
   int ExactNumBottomBlobs() const override { return 2; }
   int MinTopBlobs() const override { return 1; }
   bool IsLoss() const override { return true; }
+  bool AutoTopBlobs() const override { return true; }
   void LayerSetUp(const std::vector<Blob<Dtype>*>&, const std::vector<Blob<Dtype>*>&) override {
     const Msg& lp = this->layer_param_.sub_or_empty("loss_param");
     ignore_ = lp.has("ignore_label") ? (int)lp.integer("ignore_label") : -1;
@@ -806,6 +807,7 @@ class EuclideanLossLayer : public Layer<Dtype> {
   int ExactNumBottomBlobs() const override { return 2; }
   int ExactNumTopBlobs() const override { return 1; }
   bool IsLoss() const override { return true; }
+  bool AutoTopBlobs() const override { return true; }
   void Reshape(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
     CAFFE_CHECK(bottom[0]->shape(0) == bottom[1]->shape(0),
                 "The data and label should have the same first dimension.");  // loss_layer.cpp:22-24

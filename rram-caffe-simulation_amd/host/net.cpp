@@ -213,8 +213,21 @@ Net<Dtype>::Net(const Msg& in_param, Phase phase, const Msg& options) : phase_(p
       top_id_vecs_[lid].push_back(id);
       available.insert(tops[j]);
     }
+    // anonymous tops (net.cpp:123-135): not named, so no later layer can read
+    // them and they are not net outputs
+    if (layer->AutoTopBlobs()) {
+      const int needed = std::max(layer->MinTopBlobs(), layer->ExactNumTopBlobs());
+      for (int j = static_cast<int>(tops.size()); j < needed; ++j) {
+        const int id = static_cast<int>(blobs_.size());
+        blobs_.push_back(std::make_shared<Blob<Dtype>>());
+        blob_names_.push_back("(automatic)");
+        blob_need_backward_.push_back(false);
+        top_vecs_[lid].push_back(blobs_[id].get());
+        top_id_vecs_[lid].push_back(id);
+      }
+    }
     layer->SetUp(bottom_vecs_[lid], top_vecs_[lid]);
-    for (size_t j = 0; j < tops.size(); ++j) {
+    for (size_t j = 0; j < top_vecs_[lid].size(); ++j) {
       const float lw = static_cast<float>(layer->loss(static_cast<int>(j)));
       if ((int)blob_loss_weights_.size() <= top_id_vecs_[lid][j]) blob_loss_weights_.resize(top_id_vecs_[lid][j] + 1, 0.f);
       blob_loss_weights_[top_id_vecs_[lid][j]] = lw;
