@@ -704,7 +704,7 @@ __global__ void __launch_bounds__(256) k_conv_cb_pack_x6(const float* __restrict
     for (int e = 0; e < 8; ++e)
       v[e] = m < M ? w[((int64_t)g * M + m) * Cg * T + (int64_t)(c0 + e) * T + s] : 0.0f;
     x6::Parts t;
-    x6::split8(v, t);
+    x6::split8_safe(v, t);
     char* f = out + (int64_t)(u >> 6) * 3072 + lane * 16;
     *reinterpret_cast<x6::bf16x8*>(f) = t.h;
     *reinterpret_cast<x6::bf16x8*>(f + 1024) = t.m;
@@ -930,6 +930,326 @@ k_conv_wide_x6(Params P, const uint16_t* __restrict__ wpack, int CHS) {
   conv_epilogue_nchw<MI, 2>(acc, P, P.e, 0, n0 + wave * 64, lr, lh);
 }
 
+// ---------------------------------------------------------------------------
+// k_conv1_ring_x6: AlexNet conv1 (3 x 11 x 11, stride 4, 227 x 227 input, 96
+// filters) as a persistent kernel whose input is split ONCE per element.
+//
+// One workgroup per CU walks tiles of 96 filters x 256 output positions of
+// one image.  Its LDS holds three channel slots; slot c is the tile's input
+// rows of channel c (32 rows: 6 output rows x stride 4 + 12 kernel rows), each
+// element already split into its three bf16 terms and de-interleaved by
+// input column phase ic % 4: element ic of a row sits at [term][row][ic % 4]
+// [ic / 4].  The im2col value of output column ow, kernel column kw is then
+// [term][row][kw % 4][ow + kw / 4]: consecutive positions read consecutive
+// 16-bit elements (no bank conflicts; the plain fp32 row at stride 4 floats
+// read 4-way conflicted), and a B fragment term is 8 ds_read_u16 at
+// compile-time offsets from one per-lane base — no split and no address
+// arithmetic in the MFMA loop.
+// K order (shared with k_conv_wide_pack_ga_x6): lane half h takes kernel rows
+// 6h .. 6h + 5 (row 11 has zero weights), item s = 8 g + j of group g is
+// channel s / 66, kernel row 6h + (s / 11) % 6, column s % 11 (25 groups).
+// The slots are refilled for the next tile while this one computes: slot 0
+// once group 8 (the last reader of channel 0) is done, slot 1 after group 16,
+// slot 2 at the start of the tile it serves (read from group 16 on); three
+// barriers per tile.  The weight fragments come from L2 into registers two
+// groups ahead (as k_conv_wide_x6).
+// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+namespace c1x6 {
+constexpr int BM = 96, BN = 256;
+constexpr int KW = 11, HR = 6, C = 3, S = C * HR * KW, G = (S + 7) / 8;  // 198 items per half, 25 groups
+constexpr int ROWS = 32;                 // slot rows
+constexpr int PJ = 58;                   // elements per phase row (ic / 4 <= 56, + pad)
+// elements per slot row: 4 phases + pad, ROWE = 14 (mod 16) so that a 32-lane
+// read that wraps from output column 54 of one row to column 0 of the next
+// (+4 input rows = 2 ROWE dwords = 28 (mod 32) banks) lands on the banks the
+// first run left free (ds_read_u16: bank = dword mod 32, 2 lanes per dword)
+constexpr int ROWE = 4 * PJ + 6;
+constexpr int TERMB = ROWS * ROWE * 2;   // bytes per term plane
+constexpr int SLOTB = 3 * TERMB;         // bytes per slot
+constexpr int QP = PJ / 2;               // column-pair chunks (8 input columns) per row
+constexpr int CHUNKS = ROWS * QP;        // chunks per slot
+constexpr int CPT = (CHUNKS + 255) / 256;  // chunks per thread
+static_assert(3 * SLOTB <= 160 * 1024, "LDS");
+// first / last group reading channel c
+constexpr int first_group(int c) { return (c * 66) / 8; }
+constexpr int last_group(int c) { return (c * 66 + 65) / 8; }
+}  // namespace c1x6
+
+template <int W>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img, int tiles) {
+  using namespace c1x6;
+  constexpr int OW = (W - 11) / 4 + 1, MI = 3;
+  static_assert(OW + 2 < PJ, "phase rows too short");
+  __shared__ __attribute__((aligned(16))) char smem[3 * SLOTB];
+  __shared__ float bias_lds[BM];
+  if (threadIdx.x < BM)
+    bias_lds[threadIdx.x] = (P.e.bias != nullptr && (int)threadIdx.x < P.M) ? P.e.bias[threadIdx.x] : 0.0f;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lr = lane & 31, lh = lane >> 5;
+  const int HWo = P.cv.howo.d, H = P.cv.H;
+  const int nwg = gridDim.x;
+  // (the lambdas below capture these, never P: a by-reference capture of the
+  // kernel-argument struct copies all of it into private memory)
+  const float* const xin = P.b.p;
+  const int in_bytes = static_cast<int>(P.cv.in_bytes);
+
+  // ---- staging: chunk k of this thread = (slot row, 8 input columns) ----
+  float sv[2][8];  // two chunks in flight
+  // elements ic >= W of a chunk are never read (4 ow + kw <= 4 (OW - 1) + 10 < W);
+  // slot rows at or past H (kernel row 11 of the last output row: zero weights)
+  // are zero-filled so no Inf / NaN meets a zero weight
+  // branch-free: a chunk outside the slot or the image, or of a tile that does
+  // not exist (t >= tiles: the refill then writes zeros into a slot no later
+  // group reads), loads from past the buffer's range, i.e. zeros
+  // the tile's image and first output row (wave-uniform, kept in SGPRs);
+  // t >= tiles gives img = -1
+  struct TileRef {
+    int img, f;
+  };
+  auto tile_ref = [&](int t) __attribute__((always_inline)) {
+    TileRef r;
+    const int img = t / tiles_per_img, tin = t - img * tiles_per_img;
+    r.img = __builtin_amdgcn_readfirstlane(t < tiles ? img : -1);
+    r.f = __builtin_amdgcn_readfirstlane((tin * BN) / OW);
+    return r;
+  };
+  auto stage_load = [&](const TileRef& tr, int c, int k, float (&v)[8]) {
+    const int q = threadIdx.x + k * 256;
+    const int ri = q / QP, qp = q - ri * QP;
+    const bool ok = tr.img >= 0 && q < CHUNKS && 4 * tr.f + ri < H;
+    const uint32_t voff =
+        ok ? static_cast<uint32_t>((((tr.img * 3 + c) * H + 4 * tr.f + ri) * W + 8 * qp) * 4) : 0x80000000u;
+    // (built here from the kernel argument: a descriptor captured by reference
+    // lands in private memory and every load becomes a waterfall loop)
+    const __amdgpu_buffer_rsrc_t xrs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xin), 0, in_bytes, 0x00020000);
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      v[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xrs, static_cast<int>(voff + 4 * e), 0, 0));
+  };
+  auto stage_store = [&](int c, int k, const float (&v)[8]) {
+    const int q = threadIdx.x + k * 256;
+    if (q >= CHUNKS) return;
+    const int ri = q / QP, qp = q - ri * QP;
+    char* base = smem + c * SLOTB + (ri * ROWE + 2 * qp) * 2;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      // elements ic = 8 qp + b and 8 qp + 4 + b are j = 2 qp, 2 qp + 1 of phase
+      // b: split the pair as split8 does (round to nearest even at each step),
+      // packed as it lands (no per-element bf16 vector access)
+      const x6::float2v pv = {v[b], v[b + 4]};
+      x6::bf16x2 h;
+      const x6::float2v r1 = x6::bf16_high_safe(pv, h);
+      const x6::bf16x2 m = __builtin_convertvector(x6::clamp_bf16(r1), x6::bf16x2);
+      const x6::float2v r2 = r1 - __builtin_convertvector(m, x6::float2v);
+      const x6::bf16x2 l = __builtin_convertvector(r2, x6::bf16x2);
+      *reinterpret_cast<uint32_t*>(base + b * PJ * 2) = __builtin_bit_cast(uint32_t, h);
+      *reinterpret_cast<uint32_t*>(base + TERMB + b * PJ * 2) = __builtin_bit_cast(uint32_t, m);
+      *reinterpret_cast<uint32_t*>(base + 2 * TERMB + b * PJ * 2) = __builtin_bit_cast(uint32_t, l);
+    }
+  };
+  // whole slot at once (first tile)
+  auto fill_slot = [&](const TileRef& tr, int c) __attribute__((always_inline)) {
+    for (int k = 0; k < CPT; ++k) {
+      stage_load(tr, c, k, sv[0]);
+      stage_store(c, k, sv[0]);
+    }
+  };
+  // spread refill: step 0 loads chunks 0, 1; step 1 stores them and loads 2, 3; step 2 stores 2, 3
+  static_assert(CPT <= 4, "refill schedule covers 4 chunks per thread");
+  // one register set u of refill step `step`: store the chunk it loaded in
+  // the previous step, then load its chunk of this step
+  auto refill_part = [&](const TileRef& tr, int c, int step, int u) __attribute__((always_inline)) {
+    if (step > 0 && 2 * (step - 1) + u < CPT) stage_store(c, 2 * (step - 1) + u, sv[u]);
+    if (step < 2 && 2 * step + u < CPT) stage_load(tr, c, 2 * step + u, sv[u]);
+  };
+
+  // the weight fragments are the same for every tile: the base address is
+  // laundered once per tile so the tile loop does not hoist all 25 groups'
+  // loads (900 registers) out of itself
+  const x6::bf16x8* ap = reinterpret_cast<const x6::bf16x8*>(wpack) + lane;
+  auto launder_a = [&]() __attribute__((always_inline)) {
+    int z = 0;
+    asm volatile("" : "+s"(z));
+    ap = reinterpret_cast<const x6::bf16x8*>(wpack) + lane + z;
+  };
+  auto load_a = [&](x6::bf16x8 (&f)[MI][3], int g) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int tt = 0; tt < 3; ++tt) f[i][tt] = ap[((g * MI + i) * 3 + tt) * 64];
+  };
+  auto lds_barrier = [&]() __attribute__((always_inline)) {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done
+    __builtin_amdgcn_s_barrier();
+  };
+
+  int t = blockIdx.x;
+  if (t < tiles) {
+    const TileRef tr = tile_ref(t);
+    fill_slot(tr, 0);
+    fill_slot(tr, 1);
+    fill_slot(tr, 2);
+  }
+  lds_barrier();
+  for (; t < tiles; t += nwg) {
+    const TileRef cur = tile_ref(t), nxt = tile_ref(t + nwg);
+    const int img = cur.img, sp0 = (t - img * tiles_per_img) * BN, f = cur.f;
+    // per-lane slot offsets (bytes, term 0) of this wave's two 32-column blocks
+    uint32_t lb[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int sp = min(sp0 + wave * 64 + j * 32 + lr, HWo - 1);
+      const int oh = sp / OW, ow = sp - oh * OW;
+      lb[j] = static_cast<uint32_t>(((4 * (oh - f) + HR * lh) * ROWE + ow) * 2);
+    }
+    struct Fr {
+      x6::Parts bp[2];
+    };
+    // B fragment term t of column block j for group g ("part" 3 j + t): 8
+    // ds_read_u16 at compile-time offsets, issued one group ahead and packed
+    // two MFMA6 blocks later (whole-vector bit casts: element-wise stores into
+    // a bf16 vector are avoided)
+    uint16_t rb[6][8];
+    auto read_part = [&](int g, int part) __attribute__((always_inline)) {
+      const int j = part / 3, tt = part % 3;
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const int sx = 8 * g + jj;
+        if (sx < S) {
+          const int c = sx / (HR * KW), rr = (sx / KW) % HR, kw = sx % KW;
+          rb[part][jj] = *reinterpret_cast<const uint16_t*>(smem + c * SLOTB + lb[j] + tt * TERMB +
+                                                              (rr * ROWE + (kw & 3) * PJ + (kw >> 2)) * 2);
+        } else {
+          rb[part][jj] = 0;
+        }
+      }
+    };
+    auto pack_part = [&](Fr& F, int part) __attribute__((always_inline)) {
+      typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
+      const u16x8 v = {rb[part][0], rb[part][1], rb[part][2], rb[part][3],
+                       rb[part][4], rb[part][5], rb[part][6], rb[part][7]};
+      const int j = part / 3, tt = part % 3;
+      x6::bf16x8& dst = tt == 0 ? F.bp[j].h : tt == 1 ? F.bp[j].m : F.bp[j].l;
+      dst = __builtin_bit_cast(x6::bf16x8, v);
+    };
+
+    floatx16 acc[MI][2];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+    x6::bf16x8 fg[3][MI][3];
+    launder_a();
+    load_a(fg[0], 0);
+    load_a(fg[1], 1);
+    Fr F[2];
+#pragma unroll
+    for (int part = 0; part < 6; ++part) {
+      read_part(0, part);
+      pack_part(F[0], part);
+    }
+    static_for<0, G>([&](auto gc) {
+      constexpr int g = decltype(gc)::value;
+      Fr& fc = F[g & 1];
+      Fr& fn = F[(g + 1) & 1];
+      if (g + 2 < G) load_a(fg[(g + 2) % 3], g + 2);
+      // slot refills (see the header): channel 2 of this tile at groups 1, 3, 5;
+      // channel 0 / 1 of the next tile two, four and six groups after their last reader
+      auto refill = [&](int u) __attribute__((always_inline)) {
+        // (unconditional: the first tile re-fills slot 2 with what the prologue
+        // put there; past the last tile the loads return zeros into dead slots)
+        if (g >= 1 && g <= 5 && (g & 1)) refill_part(cur, 2, (g - 1) / 2, u);
+        constexpr int d0 = g - last_group(0) - 1, d1 = g - last_group(1) - 1;
+        if (d0 >= 0 && d0 <= 4 && (d0 & 1) == 0) refill_part(nxt, 0, d0 / 2, u);
+        if (d1 >= 0 && d1 <= 4 && (d1 & 1) == 0) refill_part(nxt, 1, d1 / 2, u);
+      };
+#pragma unroll
+      for (int q = 0; q < 2 * MI; ++q) {
+        const int i = q >> 1, j = q & 1;
+        const auto& fa = fg[g % 3][i];
+        acc[i][j] = x6::mfma6(x6::Parts{fa[0], fa[1], fa[2]}, fc.bp[j], acc[i][j]);
+        // the next group's B fragments: part q read under MFMA6 q, packed two
+        // blocks later; parts 4, 5 (column block 1) are packed under block 0
+        // of the next group, before its first column-block-1 MFMA6
+        if (g > 0 && q == 0) {
+          pack_part(fc, 4);
+          pack_part(fc, 5);
+        }
+        if (g + 1 < G) {
+          read_part(g + 1, q);
+          if (q >= 2) pack_part(fn, q - 2);
+        }
+        if (q == 1) refill(0);
+        if (q == 4) refill(1);
+        // interleave the block's LDS reads, packs, staging and weight loads
+        // between its 6 MFMAs (the default schedule clusters 24 ds_reads
+        // behind one MFMA, exposing most of their issue time)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
+          __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // VALU
+          __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);  // DS write
+          __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);  // VMEM read
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // barriers: after the last readers of channel 0 / 1 (their slots are then
+      // refilled) and at the end of the tile
+      if (g == last_group(0) || g == last_group(1)) lds_barrier();
+    });
+    // epilogue (conv_epilogue_nchw's arithmetic: o = acc + bias, optional ReLU)
+    // with the bias read from LDS (a persistent loop would otherwise keep 48
+    // hoisted bias addresses per lane alive)
+    {
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(P.e.C, 0, 0x7FFFFFFF, 0x00020000);
+      const int mw = 4 * lh;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int sp = sp0 + wave * 64 + j * 32 + lr;
+        if (sp >= HWo) continue;
+        const uint32_t base = static_cast<uint32_t>(((int64_t)img * P.e.cimg + sp + (int64_t)mw * HWo) * 4);
+        const bool relu = P.e.relu != 0;
+        if (P.M >= BM) {  // uniform: no per-store exec masking
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int dr = i * 32 + (r & 3) + 8 * (r >> 2);
+              const float o = acc[i][j][r] + bias_lds[mw + dr];
+              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, relu ? fmaxf(o, 0.0f) : o), rs,
+                                                    static_cast<int>(base), dr * HWo * 4, 0);
+            }
+        } else {
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int dr = i * 32 + (r & 3) + 8 * (r >> 2);
+              const float o = acc[i][j][r] + bias_lds[mw + dr];
+              if (mw + dr < P.M)
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, relu ? fmaxf(o, 0.0f) : o), rs,
+                                                      static_cast<int>(base), dr * HWo * 4, 0);
+            }
+        }
+      }
+    }
+    lds_barrier();
+  }
+}
+
 // Weight repack for k_conv_wide_x6<GA = true>: w [M][C][KH][KW] -> fragments
 // [G][3 row blocks][3 terms][64 lanes][8 bf16]; lane (lr, h) of fragment
 // (g, i): row 32 i + lr, items 8 g + j of half h (same K order as below).
@@ -949,7 +1269,7 @@ __global__ void __launch_bounds__(256) k_conv_wide_pack_ga_x6(const float* __res
       }
     }
     x6::Parts t;
-    x6::split8(v, t);
+    x6::split8_safe(v, t);
     char* f = out + (int64_t)(u >> 6) * 3072 + lane * 16;
     *reinterpret_cast<x6::bf16x8*>(f) = t.h;
     *reinterpret_cast<x6::bf16x8*>(f + 1024) = t.m;
@@ -1350,6 +1670,21 @@ int conv_wide_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, co
                        11, Sh::HR, Sh::S, total);
   int rc = launch_status("conv wide weight pack x6");
   if (rc) return rc;
+  // the persistent conv1 kernel (default; RRAM_WIDE_V1=1 selects the per-tile kernel for A/B)
+  static const bool v1 = [] {
+    const char* e = getenv("RRAM_WIDE_V1");
+    return e && atoi(e) == 1;
+  }();
+  if (ga && !v1 && d->width == 227 && d->height >= 11) {
+    const int tpi = (HW + c1x6::BN - 1) / c1x6::BN;
+    const int tiles = d->num * tpi;
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+    const unsigned nwg1 = static_cast<unsigned>(std::min(tiles, cus));
+    hipLaunchKernelGGL((k_conv1_ring_x6<227>), dim3(nwg1), dim3(256), 0, s, P, wp, tpi, tiles);
+    rc = launch_status("conv1 ring x6");
+    return rc ? rc : 1;
+  }
   const unsigned nwg = static_cast<unsigned>((P.N + wx6::BN - 1) / wx6::BN);
   if (ga)
     hipLaunchKernelGGL((k_conv_wide_x6<11, 11, 4, 3, WIDE_PFL, true>), dim3(nwg), dim3(256), 0, s, P, wp, pl.CHS);
@@ -1505,6 +1840,10 @@ int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, c
   if (y_oct != nullptr && d->num_output % 8 != 0) return 0;
   const int KH = d->kernel_h, KW = d->kernel_w, T = KH * KW;
   const int G = d->group, Cg = d->channels / G, M = d->num_output / G;
+  // the epilogue writes whole octets of one group's rows: a group whose row
+  // count is not a multiple of 8 would share octets with its neighbour, so its
+  // companion is packed from y after the kernel instead
+  void* const y_oct_k = (y_oct != nullptr && M % 8 == 0) ? y_oct : nullptr;
   const int HW = d->out_h * d->out_w, HWi = d->height * d->width;
   Params P{};
   P.M = M;
@@ -1559,16 +1898,17 @@ int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, c
   if (KH == kh && pl.WR == wr && pl.NB == nb && pl.PD == pd) {                                                \
     if (cb_vl())                                                                                             \
       hipLaunchKernelGGL((k_conv_cb_x6<kh, kh, wr, nb, pd, true>), dim3(nwg), dim3(256), 0, s, P, wp, xp, pl.octb,  \
-                         pl.RPC, xrange, ximg, static_cast<char*>(y_oct), d->num_output / 8,                   \
+                         pl.RPC, xrange, ximg, static_cast<char*>(y_oct_k), d->num_output / 8,                 \
                          make_fastdiv(static_cast<uint32_t>(pl.octb >> 4)), make_fastdiv(static_cast<uint32_t>(pl.RPC))); \
     else                                                                                                     \
     hipLaunchKernelGGL((k_conv_cb_x6<kh, kh, wr, nb, pd, false>), dim3(nwg), dim3(256), 0, s, P, wp, xp, pl.octb, pl.RPC, \
-                       xrange, ximg, static_cast<char*>(y_oct), d->num_output / 8,                            \
+                       xrange, ximg, static_cast<char*>(y_oct_k), d->num_output / 8,                          \
                        make_fastdiv(static_cast<uint32_t>(pl.octb >> 4)), make_fastdiv(static_cast<uint32_t>(pl.RPC))); \
   } else
   RRAM_CB_LIST(RRAM_X) { return 0; }
 #undef RRAM_X
   rc = launch_status("conv cb x6");
+  if (rc == 0 && y_oct != nullptr && y_oct_k == nullptr) rc = pack_octets(y, y_oct, d->num, d->num_output, HW, s);
   return rc ? rc : 1;
 }
 

@@ -24,7 +24,7 @@ for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
 cols = ["SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_VALU", "SQ_INSTS_MFMA",
         "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_WAIT_ANY", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE",
         "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VMEM_RD", "GRBM_GUI_ACTIVE", "FETCH_SIZE",
-        "WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"]
+        "WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_ANY"]
 for key in sorted(agg, key=lambda k: -sum(dur[k]) / max(len(dur[k]), 1)):
     d = agg[key]
     us = sorted(dur[key])[len(dur[key]) // 2]
