@@ -69,20 +69,33 @@ def alexnet_engines(batch):
 
 def cpu_baseline(batch, p_fault, seed):
     """Caffe CPU mode restated in C (oracle/caffe_cpu.c): one
-    full Monte-Carlo map of AlexNet b`batch` on this host's cores — the
-    GaussianFailureMaker draws + Fail_cpu over the 58,631,144 IP cells, then
-    the TEST forward of all `batch` images in the reference's layer order
-    (per-image im2col_cpu + cblas_sgemm per group, single-threaded LRN /
-    pool / ReLU loops).  Not extrapolated: the whole map is timed."""
+    full Monte-Carlo map of AlexNet b`batch` on this host's physical cores
+    (affinity set / SMT) — the GaussianFailureMaker draws + Fail_cpu over the
+    58,631,144 IP cells, then the TEST forward of all `batch` images in the
+    reference's layer order (per-image im2col_cpu + cblas_sgemm per group,
+    single-threaded LRN / pool / ReLU loops).  Not extrapolated: the whole map
+    is timed.  The same map at the box's per-GPU CPU share (OMP_NUM_THREADS)
+    is reported beside it."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle
-    t, meta = oracle.caffe_cpu_alexnet_map(batch=batch, p_fault=p_fault, seed=seed)
+    phys = oracle.physical_cores()
+    t, meta = oracle.caffe_cpu_alexnet_map(batch=batch, p_fault=p_fault, seed=seed, threads=phys)
     total = sum(t.values())
-    return {"value": round(batch / total, 3), "unit": "images/s", "cores": meta["threads"], "kind": "port",
-            "sample": f"1 full fault map: {meta['broken_cells']} of 58,631,144 IP cells broken + {batch}-image "
-                      f"AlexNet TEST forward, {total:.2f} s; sgemm = {meta['blas']} on {meta['threads']} threads "
-                      f"(host affinity {meta['affinity_cpus']} CPUs), other layers single-threaded as in Caffe",
-            "layers_ms": {k: round(v * 1e3, 1) for k, v in t.items()}}
+    res = {"value": round(batch / total, 3), "unit": "images/s", "cores": meta["threads"], "kind": "port",
+           "sample": f"1 full fault map: {meta['broken_cells']} of 58,631,144 IP cells broken + {batch}-image "
+                     f"AlexNet TEST forward, {total:.2f} s; sgemm = {meta['blas']} on {meta['threads']} threads "
+                     f"(= physical cores of the {meta['affinity_cpus']}-CPU affinity set), other layers "
+                     f"single-threaded as in Caffe",
+           "layers_ms": {k: round(v * 1e3, 1) for k, v in t.items()}}
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    share = int(env) if env.isdigit() else 0
+    if 0 < share < phys:
+        t2, meta2 = oracle.caffe_cpu_alexnet_map(batch=batch, p_fault=p_fault, seed=seed, threads=share)
+        tot2 = sum(t2.values())
+        res["at_cpu_share"] = {"value": round(batch / tot2, 3), "cores": share,
+                               "sample": f"the same map with sgemm on {share} threads (OMP_NUM_THREADS, the box's "
+                                         f"per-GPU CPU share), {tot2:.2f} s"}
+    return res
 
 
 def load_traffic():
@@ -223,7 +236,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f32 (bf16x6 products)" if "bf16x6" in engines.values() else "f32",
         "data": "synthetic (U{0..255}-128 images 3x227x227, random labels; seeded Caffe-filler weights)",
         "config": {"workload": "alexnet_b256_mc_faultmap_inference", "model": "AlexNet (bvlc_alexnet train_val, TEST)",
                    "global_batch": args.batch * world, "batch_per_map": args.batch, "maps_per_step": world,

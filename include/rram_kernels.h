@@ -291,6 +291,25 @@ int rram_conv2d_fwd(const rram_conv_desc* d, const float* x, const float* w,
  * y is bit-identical to rram_conv2d_fwd's. */
 int rram_conv2d_fwd_octets(const rram_conv_desc* d, const float* x, const void* x_oct, const float* w,
                            const float* bias, float* y, void* y_oct, int relu, rram_stream_t stream);
+/* Packed-weight companion (no reference counterpart; the reference re-reads
+ * w through cuBLAS each call, conv_layer.cu:7-25).  The bf16x6 engine splits
+ * w into fragment-order bf16 terms before every forward; a caller whose
+ * weights do not change between calls (Monte-Carlo inference: only the
+ * faultable blobs are rewritten per map) keeps that pack:
+ *   rram_conv_weight_pack_bytes  bytes of the pack for this shape under the
+ *                                current engine (0: the engine taking this
+ *                                shape reads w directly — no pack);
+ *   rram_conv2d_fwd_cached       rram_conv2d_fwd_octets with w_pack (16-byte
+ *                                aligned, rram_conv_weight_pack_bytes bytes):
+ *                                w_pack_valid = 0 packs w into it first,
+ *                                1 uses it as is (the caller guarantees it
+ *                                holds the pack of the same w, same shape and
+ *                                engine).  w_pack NULL = rram_conv2d_fwd_octets.
+ * y is bit-identical to rram_conv2d_fwd_octets'. */
+size_t rram_conv_weight_pack_bytes(const rram_conv_desc* d);
+int rram_conv2d_fwd_cached(const rram_conv_desc* d, const float* x, const void* x_oct, const float* w,
+                           void* w_pack, int w_pack_valid, const float* bias, float* y, void* y_oct, int relu,
+                           rram_stream_t stream);
 /* 1 when rram_conv2d_fwd_octets would read an x_oct for this shape now. */
 int rram_conv_input_octets(const rram_conv_desc* d);
 /* oct = the octet companion of x (channels % 8 == 0). */

@@ -488,6 +488,25 @@ def cc_softmax(x):
     return y
 
 
+def physical_cores():
+    """Physical cores among the CPUs this process may run on: the affinity set
+    divided by SMT (one per distinct (package, core) in the sysfs topology)."""
+    import os
+    cpus = sorted(os.sched_getaffinity(0))
+    seen = set()
+    for c in cpus:
+        base = f"/sys/devices/system/cpu/cpu{c}/topology"
+        try:
+            with open(f"{base}/physical_package_id") as f:
+                pkg = f.read().strip()
+            with open(f"{base}/core_id") as f:
+                core = f.read().strip()
+        except OSError:
+            return len(cpus)
+        seen.add((pkg, core))
+    return len(seen) or len(cpus)
+
+
 def caffe_cpu_alexnet_map(batch=256, p_fault=0.01, seed=1701, threads=None, images=None):
     """One Monte-Carlo fault map of AlexNet b`batch` in Caffe CPU mode
     (SURVEY.md §3.3 / §8d): the GaussianFailureMaker draws for all 58,631,144
@@ -499,9 +518,7 @@ def caffe_cpu_alexnet_map(batch=256, p_fault=0.01, seed=1701, threads=None, imag
     import time
     from statistics import NormalDist
     if threads is None:
-        aff = len(os.sched_getaffinity(0))
-        env = os.environ.get("OMP_NUM_THREADS")
-        threads = min(aff, int(env)) if env and env.isdigit() else aff
+        threads = physical_cores()
     blas = cc_init(threads)
     rng = np.random.default_rng(seed)
     conv = {"conv1": (96, 3, 11, 4, 0, 1), "conv2": (256, 48, 5, 1, 2, 2), "conv3": (384, 256, 3, 1, 1, 1),
@@ -558,6 +575,7 @@ def caffe_cpu_alexnet_map(batch=256, p_fault=0.01, seed=1701, threads=None, imag
         if k != "fc8":
             y = tick(f"relu{i}", cc_relu, y)
     prob = tick("prob (softmax)", cc_softmax, y)
-    meta = dict(blas=blas, threads=threads, affinity_cpus=len(os.sched_getaffinity(0)), images=n_img,
+    meta = dict(blas=blas, threads=threads, affinity_cpus=len(os.sched_getaffinity(0)),
+                physical_cores=physical_cores(), images=n_img,
                 broken_cells=broken, finite=bool(np.isfinite(prob).all()))
     return t, meta

@@ -23,8 +23,6 @@ int col2im_core(const float* col, int64_t ldcol, int nimg, const rram_conv_desc*
 int gemv_core(int trans, int M, int N, float alpha, const float* A, const float* x, float beta,
               float* y, hipStream_t s);
 int release_conv_tables();
-int conv_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, const float* w, const float* bias,
-                float* y, void* y_oct, int relu, hipStream_t s);
 int pack_octets(const float* x, void* oct, int num, int C, int HWi, hipStream_t s);
 std::atomic<int>& f32_engine();
 
@@ -176,6 +174,40 @@ int rram_conv2d_fwd_octets(const rram_conv_desc* d_in, const float* x, const voi
   rc = conv_fwd_core(&d, x, w, bias, y, relu, as_stream(s));
   if (rc == 0 && y_oct != nullptr) rc = pack_octets(y, y_oct, d.num, d.num_output, d.out_h * d.out_w, as_stream(s));
   return rc;
+}
+
+size_t rram_conv_weight_pack_bytes(const rram_conv_desc* d_in) {
+  if (d_in == nullptr) return 0;
+  rram_conv_desc d = *d_in;
+  if (rram_conv_out_shape(&d) != RRAM_OK || d.num == 0) return 0;
+  size_t bytes = 0;
+  WPack q;
+  q.query = &bytes;
+  return conv_x6_fwd(&d, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr, q) > 0 ? bytes : 0;
+}
+
+int rram_conv2d_fwd_cached(const rram_conv_desc* d_in, const float* x, const void* x_oct, const float* w,
+                           void* w_pack, int w_pack_valid, const float* bias, float* y, void* y_oct, int relu,
+                           rram_stream_t s) {
+  RRAM_REQUIRE(w_pack != nullptr || !w_pack_valid, "conv2d_fwd_cached: w_pack_valid without a w_pack buffer");
+  if (w_pack == nullptr) return rram_conv2d_fwd_octets(d_in, x, x_oct, w, bias, y, y_oct, relu, s);
+  rram_conv_desc d = *d_in;
+  int rc = rram_conv_out_shape(&d);
+  if (rc) return rc;
+  if (d.num == 0) return RRAM_OK;
+  RRAM_REQUIRE(x && w && y, "conv2d_fwd_cached: NULL pointer");
+  RRAM_REQUIRE((int64_t)d.num * d.out_h * d.out_w < (1ll << 31), "conv2d_fwd_cached: too many output positions");
+  RRAM_REQUIRE(x_oct == nullptr || d.channels % 8 == 0, "conv2d_fwd_cached: input octets need channels %% 8 == 0");
+  RRAM_REQUIRE(y_oct == nullptr || d.num_output % 8 == 0, "conv2d_fwd_cached: output octets need num_output %% 8 == 0");
+  RRAM_REQUIRE(rram_conv_weight_pack_bytes(&d) > 0, "conv2d_fwd_cached: this shape's engine takes no weight pack");
+  RRAM_REQUIRE((reinterpret_cast<uintptr_t>(w_pack) & 15u) == 0, "conv2d_fwd_cached: w_pack must be 16-byte aligned");
+  WPack wk;
+  wk.p = w_pack;
+  wk.valid = w_pack_valid != 0;
+  rc = conv_x6_fwd(&d, x, x_oct, w, bias, y, y_oct, relu, as_stream(s), wk);
+  if (rc < 0) return rc;
+  RRAM_REQUIRE(rc > 0, "conv2d_fwd_cached: the packed-weight engine did not run (w misaligned?)");
+  return RRAM_OK;
 }
 
 namespace {

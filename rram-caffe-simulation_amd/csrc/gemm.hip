@@ -1575,8 +1575,6 @@ std::map<std::pair<int, hipStream_t>, std::pair<float*, size_t>>& pack_cache() {
   static std::map<std::pair<int, hipStream_t>, std::pair<float*, size_t>> cache;
   return cache;
 }
-int conv_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, const float* w, const float* bias,
-                float* y, void* y_oct, int relu, hipStream_t s);
 
 float* pack_buffer(size_t floats, hipStream_t s) {
   int dev = 0;

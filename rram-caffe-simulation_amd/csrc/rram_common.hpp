@@ -121,4 +121,15 @@ __host__ __device__ __forceinline__ float u01(uint32_t r) {
   return static_cast<float>(r >> 8) * (1.0f / 16777216.0f);
 }
 
+// Packed-weight companion of a convolution (rram_conv2d_fwd_cached): the
+// bf16x6 engine's pre-split fragment form of w in a caller-owned buffer that
+// outlives the call, so weights that do not change between calls (Monte-Carlo
+// inference: only the faultable blobs are rewritten) are split once.
+struct WPack {
+  void* p = nullptr;         // caller's buffer (nullptr: the per-stream scratch buffer)
+  bool valid = false;        // p already holds this shape's pack of w: launch no pack kernel
+  size_t* query = nullptr;   // set: report the pack bytes of the engine that would run, launch nothing
+};
+int conv_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, const float* w, const float* bias,
+                float* y, void* y_oct, int relu, hipStream_t s, const WPack& wk = WPack{});
 }  // namespace rram

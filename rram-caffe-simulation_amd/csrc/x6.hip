@@ -932,27 +932,30 @@ k_conv_wide_x6(Params P, const uint16_t* __restrict__ wpack, int CHS) {
 
 // ---------------------------------------------------------------------------
 // k_conv1_ring_x6: AlexNet conv1 (3 x 11 x 11, stride 4, 227 x 227 input, 96
-// filters) as a persistent kernel whose input is split ONCE per element.
+// filters) as a persistent kernel whose input is split ONCE per element and
+// whose B fragments are plain 8-byte LDS reads.
 //
 // One workgroup per CU walks tiles of 96 filters x 256 output positions of
 // one image.  Its LDS holds three channel slots; slot c is the tile's input
-// rows of channel c (32 rows: 6 output rows x stride 4 + 12 kernel rows), each
-// element already split into its three bf16 terms and de-interleaved by
-// input column phase ic % 4: element ic of a row sits at [term][row][ic % 4]
-// [ic / 4].  The im2col value of output column ow, kernel column kw is then
-// [term][row][kw % 4][ow + kw / 4]: consecutive positions read consecutive
-// 16-bit elements (no bank conflicts; the plain fp32 row at stride 4 floats
-// read 4-way conflicted), and a B fragment term is 8 ds_read_u16 at
-// compile-time offsets from one per-lane base — no split and no address
-// arithmetic in the MFMA loop.
-// K order (shared with k_conv_wide_pack_ga_x6): lane half h takes kernel rows
-// 6h .. 6h + 5 (row 11 has zero weights), item s = 8 g + j of group g is
-// channel s / 66, kernel row 6h + (s / 11) % 6, column s % 11 (25 groups).
+// rows of channel c (32 rows: 6 output rows x stride 4 + 12 kernel rows),
+// each element already split into its three bf16 terms, stored as plain rows
+// [term][row][ic] (ROWE elements per row, columns >= W zero).
+// K order ("quads"): a kernel row is padded to 12 columns = 3 quads of 4
+// consecutive columns; lane half h takes kernel rows 6h .. 6h + 5 (row 11 and
+// column 11 have zero weights), and quad qi = 2g + (j >> 2) of group g is
+// channel qi / 18, kernel row 6h + (qi / 3) % 6, columns 4 (qi % 3) .. + 3
+// (54 quads per half, 27 groups).  The im2col values of one quad at output
+// column ow are input columns 4 ow + 4 kq .. + 3 of one row: 4 consecutive
+// bf16 = one ds_read_b64 at a compile-time offset from a per-lane base, and
+// consecutive lanes (output columns) read consecutive 8-byte words, so a B
+// fragment term is two conflict-free ds_read_b64 with no VALU at all (the
+// per-element u16 gathers of the previous layout cost 1.3 ds_read + 0.7
+// v_perm per MFMA).  The padding costs 27 groups where 363 items need 23.
 // The slots are refilled for the next tile while this one computes: slot 0
-// once group 8 (the last reader of channel 0) is done, slot 1 after group 16,
-// slot 2 at the start of the tile it serves (read from group 16 on); three
+// once group 8 (the last reader of channel 0) is done, slot 1 after group 17,
+// slot 2 at the start of the tile it serves (read from group 18 on); three
 // barriers per tile.  The weight fragments come from L2 into registers two
-// groups ahead (as k_conv_wide_x6).
+// groups ahead (fragment order, k_conv1_pack_x6).
 // compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
 template <int B, int E, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -963,31 +966,35 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 namespace c1x6 {
 constexpr int BM = 96, BN = 256;
-constexpr int KW = 11, HR = 6, C = 3, S = C * HR * KW, G = (S + 7) / 8;  // 198 items per half, 25 groups
+constexpr int HR = 6, KQ = 3, C = 3, QH = C * HR * KQ, G = QH / 2;  // 54 quads per half, 27 groups
 constexpr int ROWS = 32;                 // slot rows
-constexpr int PJ = 58;                   // elements per phase row (ic / 4 <= 56, + pad)
-// elements per slot row: 4 phases + pad, ROWE = 14 (mod 16) so that a 32-lane
-// read that wraps from output column 54 of one row to column 0 of the next
-// (+4 input rows = 2 ROWE dwords = 28 (mod 32) banks) lands on the banks the
-// first run left free (ds_read_u16: bank = dword mod 32, 2 lanes per dword)
-constexpr int ROWE = 4 * PJ + 6;
+// elements per slot row (>= 228: the last quad of output column 54 reads
+// input column 227, which is zero).  ROWE = 24 (mod 32) 8-byte words: a
+// 32-lane ds_read_b64 that wraps from output column 54 of one row to column 0
+// four input rows down continues on the next bank pair but one (2-way on one
+// pair at most), and rows stay 16-byte aligned for the staging writes
+constexpr int ROWE = 248;
 constexpr int TERMB = ROWS * ROWE * 2;   // bytes per term plane
 constexpr int SLOTB = 3 * TERMB;         // bytes per slot
-constexpr int QP = PJ / 2;               // column-pair chunks (8 input columns) per row
+constexpr int QP = ROWE / 8;             // 8-column chunks per row
 constexpr int CHUNKS = ROWS * QP;        // chunks per slot
 constexpr int CPT = (CHUNKS + 255) / 256;  // chunks per thread
-static_assert(3 * SLOTB <= 160 * 1024, "LDS");
+static_assert(3 * SLOTB + BM * 4 <= 160 * 1024, "LDS");
 // first / last group reading channel c
-constexpr int first_group(int c) { return (c * 66) / 8; }
-constexpr int last_group(int c) { return (c * 66 + 65) / 8; }
+constexpr int first_group(int c) { return c * (G / C); }
+constexpr int last_group(int c) { return (c + 1) * (G / C) - 1; }
+// LDS byte offset of quad qi (relative to the lane's base): channel, row, column
+constexpr int quad_off(int qi) {
+  return (qi / (HR * KQ)) * SLOTB + (((qi / KQ) % HR) * ROWE + 4 * (qi % KQ)) * 2;
+}
 }  // namespace c1x6
 
-template <int W>
+template <int W, int DIAG = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img, int tiles) {
   using namespace c1x6;
   constexpr int OW = (W - 11) / 4 + 1, MI = 3;
-  static_assert(OW + 2 < PJ, "phase rows too short");
+  static_assert(4 * (OW - 1) + 4 * KQ <= ROWE, "slot rows too short");
   __shared__ __attribute__((aligned(16))) char smem[3 * SLOTB];
   __shared__ float bias_lds[BM];
   if (threadIdx.x < BM)
@@ -1004,14 +1011,11 @@ k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img,
 
   // ---- staging: chunk k of this thread = (slot row, 8 input columns) ----
   float sv[2][8];  // two chunks in flight
-  // elements ic >= W of a chunk are never read (4 ow + kw <= 4 (OW - 1) + 10 < W);
-  // slot rows at or past H (kernel row 11 of the last output row: zero weights)
-  // are zero-filled so no Inf / NaN meets a zero weight
-  // branch-free: a chunk outside the slot or the image, or of a tile that does
-  // not exist (t >= tiles: the refill then writes zeros into a slot no later
-  // group reads), loads from past the buffer's range, i.e. zeros
-  // the tile's image and first output row (wave-uniform, kept in SGPRs);
-  // t >= tiles gives img = -1
+  // branch-free: an element outside the image row (ic >= W), a row at or past
+  // H (kernel row 11 of the last output row: zero weights, so it must hold no
+  // Inf / NaN), or a chunk of a tile that does not exist (t >= tiles: the
+  // refill then writes zeros into a slot no later group reads) loads from past
+  // the buffer's range, i.e. zero
   struct TileRef {
     int img, f;
   };
@@ -1022,12 +1026,16 @@ k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img,
     r.f = __builtin_amdgcn_readfirstlane((tin * BN) / OW);
     return r;
   };
+  // chunk index: the last thread group's extra chunks (q >= CHUNKS) redo chunk
+  // CHUNKS - 1 (same loads, same values, same LDS bytes: a benign duplicate
+  // write), so the refill has no branch for the scheduler to stop at
+  auto chunk_of = [&](int k) __attribute__((always_inline)) { return min((int)threadIdx.x + k * 256, CHUNKS - 1); };
   auto stage_load = [&](const TileRef& tr, int c, int k, float (&v)[8]) {
-    const int q = threadIdx.x + k * 256;
+    const int q = chunk_of(k);
     const int ri = q / QP, qp = q - ri * QP;
-    const bool ok = tr.img >= 0 && q < CHUNKS && 4 * tr.f + ri < H;
-    const uint32_t voff =
-        ok ? static_cast<uint32_t>((((tr.img * 3 + c) * H + 4 * tr.f + ri) * W + 8 * qp) * 4) : 0x80000000u;
+    const bool ok = tr.img >= 0 && 4 * tr.f + ri < H;
+    const int rowoff = (((tr.img * 3 + c) * H + 4 * tr.f + ri) * W + 8 * qp) * 4;
+    const uint32_t voff = ok ? static_cast<uint32_t>(rowoff) : 0x80000000u;
     // (built here from the kernel argument: a descriptor captured by reference
     // lands in private memory and every load becomes a waterfall loop)
     const __amdgpu_buffer_rsrc_t xrs =
@@ -1036,26 +1044,21 @@ k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img,
     for (int e = 0; e < 8; ++e)
       v[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xrs, static_cast<int>(voff + 4 * e), 0, 0));
   };
-  auto stage_store = [&](int c, int k, const float (&v)[8]) {
-    const int q = threadIdx.x + k * 256;
-    if (q >= CHUNKS) return;
+  auto stage_store = [&](int c, int k, float (&v)[8]) {
+    const int q = chunk_of(k);
     const int ri = q / QP, qp = q - ri * QP;
-    char* base = smem + c * SLOTB + (ri * ROWE + 2 * qp) * 2;
+    // columns past the image row loaded the next row's (or, past the buffer,
+    // zero) values: zero them (kernel column 11's weights are zero, and an
+    // Inf there would make 0 * Inf = NaN)
+    const int nv = W - 8 * qp;
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      // elements ic = 8 qp + b and 8 qp + 4 + b are j = 2 qp, 2 qp + 1 of phase
-      // b: split the pair as split8 does (round to nearest even at each step),
-      // packed as it lands (no per-element bf16 vector access)
-      const x6::float2v pv = {v[b], v[b + 4]};
-      x6::bf16x2 h;
-      const x6::float2v r1 = x6::bf16_high_safe(pv, h);
-      const x6::bf16x2 m = __builtin_convertvector(x6::clamp_bf16(r1), x6::bf16x2);
-      const x6::float2v r2 = r1 - __builtin_convertvector(m, x6::float2v);
-      const x6::bf16x2 l = __builtin_convertvector(r2, x6::bf16x2);
-      *reinterpret_cast<uint32_t*>(base + b * PJ * 2) = __builtin_bit_cast(uint32_t, h);
-      *reinterpret_cast<uint32_t*>(base + TERMB + b * PJ * 2) = __builtin_bit_cast(uint32_t, m);
-      *reinterpret_cast<uint32_t*>(base + 2 * TERMB + b * PJ * 2) = __builtin_bit_cast(uint32_t, l);
-    }
+    for (int e = 0; e < 8; ++e) v[e] = e < nv ? v[e] : 0.0f;
+    char* base = smem + c * SLOTB + (ri * ROWE + 8 * qp) * 2;
+    x6::Parts t;
+    x6::split8_safe(v, t);
+    *reinterpret_cast<x6::bf16x8*>(base) = t.h;
+    *reinterpret_cast<x6::bf16x8*>(base + TERMB) = t.m;
+    *reinterpret_cast<x6::bf16x8*>(base + 2 * TERMB) = t.l;
   };
   // whole slot at once (first tile)
   auto fill_slot = [&](const TileRef& tr, int c) __attribute__((always_inline)) {
@@ -1074,8 +1077,8 @@ k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img,
   };
 
   // the weight fragments are the same for every tile: the base address is
-  // laundered once per tile so the tile loop does not hoist all 25 groups'
-  // loads (900 registers) out of itself
+  // laundered once per tile so the tile loop does not hoist all groups'
+  // loads out of itself
   const x6::bf16x8* ap = reinterpret_cast<const x6::bf16x8*>(wpack) + lane;
   auto launder_a = [&]() __attribute__((always_inline)) {
     int z = 0;
@@ -1101,70 +1104,73 @@ k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img,
     fill_slot(tr, 2);
   }
   lds_barrier();
-  for (; t < tiles; t += nwg) {
+  // Accumulators double-buffered across tiles: tile t computes into acc[c]
+  // while its first 12 groups store tile t - nwg's acc[1 - c] (8 values per
+  // group, between the MFMAs), so the epilogue is not a serial tail per tile.
+  // Stores of lanes past the image's last position, and of the tile before
+  // the first, go to an out-of-range offset (dropped by the buffer range check).
+  floatx16 acc[2][MI][2];
+  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(P.e.C, 0, 0x7FFFFFFF, 0x00020000);
+  const bool relu = P.e.relu != 0;
+  const int mw = 4 * lh;
+  uint32_t obase[2] = {0x80000000u, 0x80000000u};  // per column block: previous tile's output offset (bytes)
+  auto store_part = [&](const floatx16 (&pa)[MI][2], int s8) __attribute__((always_inline)) {
+    // values 8 s8 .. 8 s8 + 7 of the 96 (s8 < 12; block (i, j) = v / 16, row r = v % 16)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int v = 8 * s8 + e, i = (v >> 4) / 2, j = (v >> 4) & 1, r = v & 15;
+      const int dr = i * 32 + (r & 3) + 8 * (r >> 2);
+      const float o = pa[i][j][r] + bias_lds[mw + dr];
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, relu ? fmaxf(o, 0.0f) : o), ors,
+                                            static_cast<int>(obase[j]), dr * HWo * 4, 0);
+    }
+  };
+  auto tile_body = [&](auto cc, int t) __attribute__((always_inline)) {
+    constexpr int CUR = decltype(cc)::value;
     const TileRef cur = tile_ref(t), nxt = tile_ref(t + nwg);
     const int img = cur.img, sp0 = (t - img * tiles_per_img) * BN, f = cur.f;
-    // per-lane slot offsets (bytes, term 0) of this wave's two 32-column blocks
+    // per-lane slot byte offsets (term 0, quad 0) of this wave's two 32-column blocks
     uint32_t lb[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int sp = min(sp0 + wave * 64 + j * 32 + lr, HWo - 1);
       const int oh = sp / OW, ow = sp - oh * OW;
-      lb[j] = static_cast<uint32_t>(((4 * (oh - f) + HR * lh) * ROWE + ow) * 2);
+      lb[j] = static_cast<uint32_t>(((4 * (oh - f) + HR * lh) * ROWE + 4 * ow) * 2);
     }
-    struct Fr {
-      x6::Parts bp[2];
-    };
-    // B fragment term t of column block j for group g ("part" 3 j + t): 8
-    // ds_read_u16 at compile-time offsets, issued one group ahead and packed
-    // two MFMA6 blocks later (whole-vector bit casts: element-wise stores into
-    // a bf16 vector are avoided)
-    uint16_t rb[6][8];
-    auto read_part = [&](int g, int part) __attribute__((always_inline)) {
+    // B fragment term tt of column block j for group g: quads 2g, 2g + 1 =
+    // two ds_read_b64 at compile-time offsets, issued one group ahead
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    auto read_part = [&](x6::Parts (&F)[2], int g, int part) __attribute__((always_inline)) {
       const int j = part / 3, tt = part % 3;
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-        const int sx = 8 * g + jj;
-        if (sx < S) {
-          const int c = sx / (HR * KW), rr = (sx / KW) % HR, kw = sx % KW;
-          rb[part][jj] = *reinterpret_cast<const uint16_t*>(smem + c * SLOTB + lb[j] + tt * TERMB +
-                                                              (rr * ROWE + (kw & 3) * PJ + (kw >> 2)) * 2);
-        } else {
-          rb[part][jj] = 0;
-        }
-      }
+      const char* b = smem + lb[j] + tt * TERMB;
+      const u32x2 lo = *reinterpret_cast<const u32x2*>(b + quad_off(2 * g));
+      const u32x2 hi = *reinterpret_cast<const u32x2*>(b + quad_off(2 * g + 1));
+      const x6::bf16x8 v = __builtin_bit_cast(x6::bf16x8, u32x4{lo[0], lo[1], hi[0], hi[1]});
+      if (tt == 0) F[j].h = v;
+      else if (tt == 1) F[j].m = v;
+      else F[j].l = v;
     };
-    auto pack_part = [&](Fr& F, int part) __attribute__((always_inline)) {
-      typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
-      const u16x8 v = {rb[part][0], rb[part][1], rb[part][2], rb[part][3],
-                       rb[part][4], rb[part][5], rb[part][6], rb[part][7]};
-      const int j = part / 3, tt = part % 3;
-      x6::bf16x8& dst = tt == 0 ? F.bp[j].h : tt == 1 ? F.bp[j].m : F.bp[j].l;
-      dst = __builtin_bit_cast(x6::bf16x8, v);
-    };
-
-    floatx16 acc[MI][2];
+    floatx16 (&ac)[MI][2] = acc[CUR];
+    const floatx16 (&ap_)[MI][2] = acc[1 - CUR];
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+        for (int r = 0; r < 16; ++r) ac[i][j][r] = 0.0f;
     x6::bf16x8 fg[3][MI][3];
     launder_a();
     load_a(fg[0], 0);
     load_a(fg[1], 1);
-    Fr F[2];
+    x6::Parts F[2][2];
 #pragma unroll
-    for (int part = 0; part < 6; ++part) {
-      read_part(0, part);
-      pack_part(F[0], part);
-    }
+    for (int part = 0; part < 6; ++part) read_part(F[0], 0, part);
     static_for<0, G>([&](auto gc) {
       constexpr int g = decltype(gc)::value;
-      Fr& fc = F[g & 1];
-      Fr& fn = F[(g + 1) & 1];
-      if (g + 2 < G) load_a(fg[(g + 2) % 3], g + 2);
+      x6::Parts (&fc)[2] = F[g & 1];
+      x6::Parts (&fn)[2] = F[(g + 1) & 1];
+      if (g + 2 < G && !(DIAG & 1)) load_a(fg[(g + 2) % 3], g + 2);
       // slot refills (see the header): channel 2 of this tile at groups 1, 3, 5;
       // channel 0 / 1 of the next tile two, four and six groups after their last reader
       auto refill = [&](int u) __attribute__((always_inline)) {
@@ -1179,74 +1185,51 @@ k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img,
       for (int q = 0; q < 2 * MI; ++q) {
         const int i = q >> 1, j = q & 1;
         const auto& fa = fg[g % 3][i];
-        acc[i][j] = x6::mfma6(x6::Parts{fa[0], fa[1], fa[2]}, fc.bp[j], acc[i][j]);
-        // the next group's B fragments: part q read under MFMA6 q, packed two
-        // blocks later; parts 4, 5 (column block 1) are packed under block 0
-        // of the next group, before its first column-block-1 MFMA6
-        if (g > 0 && q == 0) {
-          pack_part(fc, 4);
-          pack_part(fc, 5);
+        ac[i][j] = x6::mfma6(x6::Parts{fa[0], fa[1], fa[2]}, fc[j], ac[i][j]);
+        // the next group's B fragment part q under MFMA6 block q
+        if (g + 1 < G && !(DIAG & 8)) read_part(fn, g + 1, q);
+        if (!(DIAG & 4)) {
+          if (q == 1) refill(0);
+          if (q == 4) refill(1);
         }
-        if (g + 1 < G) {
-          read_part(g + 1, q);
-          if (q >= 2) pack_part(fn, q - 2);
-        }
-        if (q == 1) refill(0);
-        if (q == 4) refill(1);
-        // interleave the block's LDS reads, packs, staging and weight loads
-        // between its 6 MFMAs (the default schedule clusters 24 ds_reads
-        // behind one MFMA, exposing most of their issue time)
+        // the previous tile's outputs: groups 0 .. 11, 8 values per group
+        if (g < 12 && q == 3 && !(DIAG & 2)) store_part(ap_, g);
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
-          __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // VALU
-          __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);  // DS write
-          __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);  // VMEM read
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+          __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // VALU
+          __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
+          __builtin_amdgcn_sched_group_barrier(0x020, 3, 0);  // VMEM read
+          __builtin_amdgcn_sched_group_barrier(0x040, 1, 0);  // VMEM write
         }
         __builtin_amdgcn_sched_barrier(0);
       }
       // barriers: after the last readers of channel 0 / 1 (their slots are then
       // refilled) and at the end of the tile
-      if (g == last_group(0) || g == last_group(1)) lds_barrier();
+      if (g == last_group(0) || g == last_group(1) || g == G - 1) lds_barrier();
     });
-    // epilogue (conv_epilogue_nchw's arithmetic: o = acc + bias, optional ReLU)
-    // with the bias read from LDS (a persistent loop would otherwise keep 48
-    // hoisted bias addresses per lane alive)
-    {
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(P.e.C, 0, 0x7FFFFFFF, 0x00020000);
-      const int mw = 4 * lh;
+    // this tile's output offsets, stored under the next tile (bias + ReLU:
+    // conv_epilogue_nchw's arithmetic; the bias from LDS)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int sp = sp0 + wave * 64 + j * 32 + lr;
-        if (sp >= HWo) continue;
-        const uint32_t base = static_cast<uint32_t>(((int64_t)img * P.e.cimg + sp + (int64_t)mw * HWo) * 4);
-        const bool relu = P.e.relu != 0;
-        if (P.M >= BM) {  // uniform: no per-store exec masking
-#pragma unroll
-          for (int i = 0; i < MI; ++i)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int dr = i * 32 + (r & 3) + 8 * (r >> 2);
-              const float o = acc[i][j][r] + bias_lds[mw + dr];
-              __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, relu ? fmaxf(o, 0.0f) : o), rs,
-                                                    static_cast<int>(base), dr * HWo * 4, 0);
-            }
-        } else {
-#pragma unroll
-          for (int i = 0; i < MI; ++i)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int dr = i * 32 + (r & 3) + 8 * (r >> 2);
-              const float o = acc[i][j][r] + bias_lds[mw + dr];
-              if (mw + dr < P.M)
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, relu ? fmaxf(o, 0.0f) : o), rs,
-                                                      static_cast<int>(base), dr * HWo * 4, 0);
-            }
-        }
-      }
+    for (int j = 0; j < 2; ++j) {
+      const int sp = sp0 + wave * 64 + j * 32 + lr;
+      obase[j] = sp < HWo ? static_cast<uint32_t>(((int64_t)img * P.e.cimg + sp + (int64_t)mw * HWo) * 4)
+                          : 0x80000000u;
     }
-    lds_barrier();
+  };
+  for (; t < tiles; t += 2 * nwg) {
+    tile_body(std::integral_constant<int, 0>{}, t);
+    if (t + nwg >= tiles) {
+#pragma unroll
+      for (int s8 = 0; s8 < 12; ++s8) store_part(acc[0], s8);
+      return;
+    }
+    tile_body(std::integral_constant<int, 1>{}, t + nwg);
+  }
+  if (t - nwg < tiles && t != (int)blockIdx.x) {
+#pragma unroll
+    for (int s8 = 0; s8 < 12; ++s8) store_part(acc[1], s8);
   }
 }
 
@@ -1267,6 +1250,33 @@ __global__ void __launch_bounds__(256) k_conv_wide_pack_ga_x6(const float* __res
         const int c = sx / (HR * KW), kh = h * HR + (sx / KW) % HR, kw = sx % KW;
         if (kh < KH) v[j] = w[(((int64_t)row * C + c) * KH + kh) * KW + kw];
       }
+    }
+    x6::Parts t;
+    x6::split8_safe(v, t);
+    char* f = out + (int64_t)(u >> 6) * 3072 + lane * 16;
+    *reinterpret_cast<x6::bf16x8*>(f) = t.h;
+    *reinterpret_cast<x6::bf16x8*>(f + 1024) = t.m;
+    *reinterpret_cast<x6::bf16x8*>(f + 2048) = t.l;
+  }
+}
+
+// Weight repack for k_conv1_ring_x6: w [M][3][11][11] -> fragments
+// [27 groups][3 row blocks][3 terms][64 lanes][8 bf16]; lane (lr, h) of
+// fragment (g, i): row 32 i + lr, items j of half h = quads 2 g, 2 g + 1 in
+// the kernel's quad order (kernel row 6 h + (qi / 3) % 6, columns 4 (qi % 3)
+// .. + 3; row 11 and column 11 zero).
+__global__ void __launch_bounds__(256) k_conv1_pack_x6(const float* __restrict__ w, char* __restrict__ out, int M,
+                                                       int units) {
+  using namespace c1x6;
+  for (int u = blockIdx.x * blockDim.x + threadIdx.x; u < units; u += gridDim.x * blockDim.x) {
+    const int lane = u & 63, i = (u >> 6) % 3, g = (u >> 6) / 3;
+    const int row = 32 * i + (lane & 31), h = lane >> 5;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int qi = 2 * g + (j >> 2);
+      const int c = qi / (HR * KQ), kh = HR * h + (qi / KQ) % HR, kw = 4 * (qi % KQ) + (j & 3);
+      v[j] = (row < M && kh < 11 && kw < 11) ? w[((row * 3 + c) * 11 + kh) * 11 + kw] : 0.0f;
     }
     x6::Parts t;
     x6::split8_safe(v, t);
@@ -1625,7 +1635,7 @@ bool conv_wide_plan(const rram_conv_desc* d, WidePlan& pl) {
 }
 
 int conv_wide_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const float* bias, float* y, int relu,
-                     hipStream_t s) {
+                     hipStream_t s, const WPack& wk) {
   WidePlan pl;
   if (!conv_wide_plan(d, pl)) return 0;
   if ((reinterpret_cast<uintptr_t>(w) & 3u) != 0) return 0;
@@ -1660,30 +1670,59 @@ int conv_wide_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, co
   }();
   const int64_t total = (int64_t)Sh::G * wx6::BM * (wx6::SLOT_ROW / 2);
   const int64_t gunits = (int64_t)Sh::G * 3 * 64;  // GA: 3 KB fragments
-  uint16_t* wp = reinterpret_cast<uint16_t*>(pack_buffer(static_cast<size_t>(std::max(total, gunits * 24)), s));
-  RRAM_REQUIRE(wp != nullptr, "conv: packed-weight buffer allocation failed");
-  if (ga)
-    hipLaunchKernelGGL(k_conv_wide_pack_ga_x6, dim3(stream_blocks(gunits)), dim3(256), 0, s, w,
-                       reinterpret_cast<char*>(wp), d->num_output, 3, 11, 11, Sh::HR, Sh::S, static_cast<int>(gunits));
-  else
-    hipLaunchKernelGGL(k_conv_wide_pack_x6, dim3(stream_blocks(total)), dim3(256), 0, s, w, wp, d->num_output, 3, 11,
-                       11, Sh::HR, Sh::S, total);
-  int rc = launch_status("conv wide weight pack x6");
-  if (rc) return rc;
+  const int64_t qunits = (int64_t)c1x6::G * 3 * 64;  // the ring kernel's fragments
   // the persistent conv1 kernel (default; RRAM_WIDE_V1=1 selects the per-tile kernel for A/B)
   static const bool v1 = [] {
     const char* e = getenv("RRAM_WIDE_V1");
     return e && atoi(e) == 1;
   }();
-  if (ga && !v1 && d->width == 227 && d->height >= 11) {
+  const bool ring = ga && !v1 && d->width == 227 && d->height >= 11 && d->num_output == c1x6::BM;
+  const size_t wbytes = static_cast<size_t>(ring ? qunits * 48 : ga ? gunits * 48 : total * 2);
+  if (wk.query) {
+    *wk.query = wbytes;
+    return 1;
+  }
+  uint16_t* wp = reinterpret_cast<uint16_t*>(wk.p ? wk.p : pack_buffer((wbytes + 3) / 4, s));
+  RRAM_REQUIRE(wp != nullptr, "conv: packed-weight buffer allocation failed");
+  if (ring) {
+    const int units1 = c1x6::G * 3 * 64;
+    if (!wk.valid) {
+      hipLaunchKernelGGL(k_conv1_pack_x6, dim3(stream_blocks(units1)), dim3(256), 0, s, w, reinterpret_cast<char*>(wp),
+                         d->num_output, units1);
+      const int rc = launch_status("conv1 weight pack x6");
+      if (rc) return rc;
+    }
+    int rc = 0;
     const int tpi = (HW + c1x6::BN - 1) / c1x6::BN;
     const int tiles = d->num * tpi;
     int cus = 256;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
     const unsigned nwg1 = static_cast<unsigned>(std::min(tiles, cus));
-    hipLaunchKernelGGL((k_conv1_ring_x6<227>), dim3(nwg1), dim3(256), 0, s, P, wp, tpi, tiles);
+    static const int diag = [] {
+      const char* e = getenv("RRAM_C1_DIAG");
+      return e ? atoi(e) : 0;
+    }();
+    switch (diag) {
+      case 1: hipLaunchKernelGGL((k_conv1_ring_x6<227, 1>), dim3(nwg1), dim3(256), 0, s, P, wp, tpi, tiles); break;
+      case 2: hipLaunchKernelGGL((k_conv1_ring_x6<227, 2>), dim3(nwg1), dim3(256), 0, s, P, wp, tpi, tiles); break;
+      case 4: hipLaunchKernelGGL((k_conv1_ring_x6<227, 4>), dim3(nwg1), dim3(256), 0, s, P, wp, tpi, tiles); break;
+      case 8: hipLaunchKernelGGL((k_conv1_ring_x6<227, 8>), dim3(nwg1), dim3(256), 0, s, P, wp, tpi, tiles); break;
+      case 15: hipLaunchKernelGGL((k_conv1_ring_x6<227, 15>), dim3(nwg1), dim3(256), 0, s, P, wp, tpi, tiles); break;
+      default: hipLaunchKernelGGL((k_conv1_ring_x6<227>), dim3(nwg1), dim3(256), 0, s, P, wp, tpi, tiles);
+    }
     rc = launch_status("conv1 ring x6");
     return rc ? rc : 1;
+  }
+  int rc = 0;
+  if (!wk.valid) {
+    if (ga)
+      hipLaunchKernelGGL(k_conv_wide_pack_ga_x6, dim3(stream_blocks(gunits)), dim3(256), 0, s, w,
+                         reinterpret_cast<char*>(wp), d->num_output, 3, 11, 11, Sh::HR, Sh::S, static_cast<int>(gunits));
+    else
+      hipLaunchKernelGGL(k_conv_wide_pack_x6, dim3(stream_blocks(total)), dim3(256), 0, s, w, wp, d->num_output, 3, 11,
+                         11, Sh::HR, Sh::S, total);
+    rc = launch_status("conv wide weight pack x6");
+    if (rc) return rc;
   }
   const unsigned nwg = static_cast<unsigned>((P.N + wx6::BN - 1) / wx6::BN);
   if (ga)
@@ -1833,7 +1872,7 @@ bool conv_cb_plan(const rram_conv_desc* d, CbPlan& pl) {
 }
 
 int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, const float* w, const float* bias,
-                   float* y, void* y_oct, int relu, hipStream_t s) {
+                   float* y, void* y_oct, int relu, hipStream_t s, const WPack& wk) {
   if (!conv_cb_enabled()) return 0;
   CbPlan pl;
   if (!conv_cb_plan(d, pl)) return 0;
@@ -1876,20 +1915,28 @@ int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, c
   const int64_t xbytes = (int64_t)d->num * d->channels * HWi * 6;
   const int rblocks = pl.tiles_m * pl.WR;
   const int64_t wfrags = (int64_t)G * rblocks * (Cg / 16) * T;
+  if (wk.query) {
+    *wk.query = static_cast<size_t>(wfrags * 3072);
+    return 1;
+  }
   const int64_t xb_al = x_oct != nullptr ? 0 : (xbytes + 255) / 256 * 256;
-  char* buf = reinterpret_cast<char*>(pack_buffer(static_cast<size_t>((xb_al + wfrags * 3072) / 4), s));
-  RRAM_REQUIRE(buf != nullptr, "conv: packed-operand buffer allocation failed");
+  const int64_t scratch = xb_al + (wk.p ? 0 : wfrags * 3072);
+  char* buf = scratch > 0 ? reinterpret_cast<char*>(pack_buffer(static_cast<size_t>(scratch / 4), s)) : nullptr;
+  RRAM_REQUIRE(scratch == 0 || buf != nullptr, "conv: packed-operand buffer allocation failed");
+  char* wbuf = wk.p ? static_cast<char*>(wk.p) : buf + xb_al;
   int rc = 0;
   if (x_oct == nullptr) {
     rc = pack_octets(x, buf, d->num, d->channels, HWi, s);
     if (rc) return rc;
   }
-  const int wunits = static_cast<int>(wfrags * 64);
-  hipLaunchKernelGGL(k_conv_cb_pack_x6, dim3(stream_blocks(wunits)), dim3(256), 0, s, w, buf + xb_al, M, Cg, T,
-                     rblocks, wunits);
-  rc = launch_status("conv weight pack x6 (octets)");
-  if (rc) return rc;
-  const auto* wp = reinterpret_cast<const x6::bf16x8*>(buf + xb_al);
+  if (!wk.valid) {
+    const int wunits = static_cast<int>(wfrags * 64);
+    hipLaunchKernelGGL(k_conv_cb_pack_x6, dim3(stream_blocks(wunits)), dim3(256), 0, s, w, wbuf, M, Cg, T,
+                       rblocks, wunits);
+    rc = launch_status("conv weight pack x6 (octets)");
+    if (rc) return rc;
+  }
+  const auto* wp = reinterpret_cast<const x6::bf16x8*>(wbuf);
   const auto* xp = reinterpret_cast<const uint16_t*>(x_oct != nullptr ? x_oct : buf);
   const int ximg = d->channels / 8 * HWi * 48;
   const unsigned nwg = static_cast<unsigned>((int64_t)G * pl.tiles_m * pl.tiles_n);
@@ -1913,22 +1960,23 @@ int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, c
 }
 
 int conv_patch_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const float* bias, float* y, int relu,
-                      hipStream_t s);
+                      hipStream_t s, const WPack& wk);
 // The bf16x6 convolution forward.  x_oct: NULL or the octet companion of x
 // (k_pack_octets_x6 layout; the channel-octet kernel then skips its input
 // pack); y_oct: NULL or a buffer that receives y's octet companion (written
 // by the channel-octet kernel's epilogue, else packed from y afterwards).
 // Returns 1 when it ran, 0 when not covered (nothing written), < 0 on error.
 int conv_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, const float* w, const float* bias,
-                float* y, void* y_oct, int relu, hipStream_t s) {
+                float* y, void* y_oct, int relu, hipStream_t s, const WPack& wk) {
   if (f32_engine().load(std::memory_order_relaxed) != RRAM_ENGINE_BF16X6) return 0;
-  if ((reinterpret_cast<uintptr_t>(w) & 3u) != 0) return 0;
+  if (wk.query == nullptr && (reinterpret_cast<uintptr_t>(w) & 3u) != 0) return 0;
   {
-    const int rc = conv_cb_x6_fwd(d, x, x_oct, w, bias, y, y_oct, relu, s);
+    const int rc = conv_cb_x6_fwd(d, x, x_oct, w, bias, y, y_oct, relu, s, wk);
     if (rc != 0) return rc;
   }
-  int rc = conv_wide_x6_fwd(d, x, w, bias, y, relu, s);
-  if (rc == 0) rc = conv_patch_x6_fwd(d, x, w, bias, y, relu, s);
+  int rc = conv_wide_x6_fwd(d, x, w, bias, y, relu, s, wk);
+  if (rc == 0) rc = conv_patch_x6_fwd(d, x, w, bias, y, relu, s, wk);
+  if (wk.query) return rc;
   if (rc > 0 && y_oct != nullptr) {
     const int pr = pack_octets(y, y_oct, d->num, d->num_output, d->out_h * d->out_w, s);
     if (pr) return pr;
@@ -1937,7 +1985,7 @@ int conv_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, cons
 }
 
 int conv_patch_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const float* bias, float* y, int relu,
-                      hipStream_t s) {
+                      hipStream_t s, const WPack& wk) {
   ConvPlan pl;
   if (!conv_x6_plan(d, pl)) return 0;
   const int KH = d->kernel_h, KW = d->kernel_w;
@@ -1974,13 +2022,20 @@ int conv_patch_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, c
   const int T = KH * KW, S = CPH * T, G8 = (S + 7) / 8, RLH = (G8 * 96 + 16) / 2;
   const int BMc = 32 * MI, tiles_m = mt / BMc, ktiles = Cg / (2 * CPH);
   const int64_t total = (int64_t)G * tiles_m * ktiles * BMc * RLH;
-  uint16_t* wp = reinterpret_cast<uint16_t*>(pack_buffer(static_cast<size_t>((total + 1) / 2), s));
+  if (wk.query) {
+    *wk.query = static_cast<size_t>(total * 2);
+    return 1;
+  }
+  uint16_t* wp = reinterpret_cast<uint16_t*>(wk.p ? wk.p : pack_buffer(static_cast<size_t>((total + 1) / 2), s));
   RRAM_REQUIRE(wp != nullptr, "conv: packed-weight buffer allocation failed");
-  const int units = G * tiles_m * ktiles * BMc * G8 * 2;
-  hipLaunchKernelGGL(k_conv_patch_pack_x6, dim3(stream_blocks(units)), dim3(256), 0, s, w, reinterpret_cast<char*>(wp),
-                     G, M, Cg, T, CPH, G8, 2 * RLH, BMc, tiles_m, ktiles, units);
-  int rc = launch_status("conv weight pack x6");
-  if (rc) return rc;
+  int rc = 0;
+  if (!wk.valid) {
+    const int units = G * tiles_m * ktiles * BMc * G8 * 2;
+    hipLaunchKernelGGL(k_conv_patch_pack_x6, dim3(stream_blocks(units)), dim3(256), 0, s, w,
+                       reinterpret_cast<char*>(wp), G, M, Cg, T, CPH, G8, 2 * RLH, BMc, tiles_m, ktiles, units);
+    rc = launch_status("conv weight pack x6");
+    if (rc) return rc;
+  }
 #define RRAM_P(KH_, CPH_, PD_)                                                                           \
   if (KH == KH_ && CPH == CPH_ && PD == PD_)                                                             \
     rc = MI == 3 ? launch_patch_x6<KH_, CPH_, 3, PD_>(P, wp, PW, CS, G, s)                               \

@@ -30,6 +30,21 @@ SyncedMemory::~SyncedMemory() {
   if (own_cpu_ && cpu_ptr_) std::free(cpu_ptr_);
   if (own_gpu_ && gpu_ptr_) (void)hipFree(gpu_ptr_);
   if (oct_ptr_) (void)hipFree(oct_ptr_);
+  if (wp_ptr_) (void)hipFree(wp_ptr_);
+}
+
+void* SyncedMemory::wpack(size_t bytes) {
+  if (bytes > wp_bytes_) {
+    if (wp_ptr_) {
+      HIP_CALL(hipStreamSynchronize(Caffe::hip_stream()));
+      HIP_CALL(hipFree(wp_ptr_));
+    }
+    wp_ptr_ = nullptr;
+    HIP_CALL(hipMalloc(&wp_ptr_, bytes));
+    wp_bytes_ = bytes;
+    wp_valid_ = false;
+  }
+  return wp_ptr_;
 }
 
 void* SyncedMemory::octets(size_t bytes) {
@@ -111,12 +126,14 @@ const void* SyncedMemory::gpu_data() {
 }
 void* SyncedMemory::mutable_cpu_data() {
   oct_valid_ = false;
+  wp_valid_ = false;
   to_cpu();
   head_ = HEAD_AT_CPU;
   return cpu_ptr_;
 }
 void* SyncedMemory::mutable_gpu_data() {
   oct_valid_ = false;
+  wp_valid_ = false;
   to_gpu();
   head_ = HEAD_AT_GPU;
   return gpu_ptr_;
@@ -124,6 +141,7 @@ void* SyncedMemory::mutable_gpu_data() {
 void SyncedMemory::set_cpu_data(void* data) {
   CAFFE_CHECK(data, "set_cpu_data(NULL)");
   oct_valid_ = false;
+  wp_valid_ = false;
   if (own_cpu_ && cpu_ptr_) std::free(cpu_ptr_);
   cpu_ptr_ = data;
   own_cpu_ = false;
@@ -132,6 +150,7 @@ void SyncedMemory::set_cpu_data(void* data) {
 void SyncedMemory::set_gpu_data(void* data) {
   CAFFE_CHECK(data, "set_gpu_data(NULL)");
   oct_valid_ = false;
+  wp_valid_ = false;
   if (own_gpu_ && gpu_ptr_) (void)hipFree(gpu_ptr_);
   gpu_ptr_ = data;
   own_gpu_ = false;

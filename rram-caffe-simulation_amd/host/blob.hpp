@@ -41,6 +41,20 @@ class SyncedMemory {
   void set_octets_valid(const int (&shape)[4]);
   bool wants_octets = false;  // a consumer would read the companion
 
+  // Packed-weight companion (rram_conv2d_fwd_cached): the bf16x6 engine's
+  // pre-split form of these weights, valid for one key (the layer's shape and
+  // engine) until the next mutable_* / set_* access, like the octet companion.
+  void* wpack(size_t bytes);  // the buffer, grown to `bytes`
+  bool wpack_valid(uint64_t key) const { return wp_valid_ && !exposed_ && wp_key_ == key; }
+  // the C-ABI handed this memory's device pointer to a caller, who may write
+  // through it at any time without a mutable access: no pack is trusted after
+  void expose() { exposed_ = true; }
+  void set_wpack_valid(uint64_t key) {
+    wp_key_ = key;
+    wp_valid_ = wp_ptr_ != nullptr;
+  }
+  void drop_wpack() { wp_valid_ = false; }
+
  private:
   void to_cpu();
   void to_gpu();
@@ -53,6 +67,11 @@ class SyncedMemory {
   size_t oct_bytes_ = 0;
   bool oct_valid_ = false;
   int oct_shape_[4] = {0, 0, 0, 0};
+  void* wp_ptr_ = nullptr;
+  size_t wp_bytes_ = 0;
+  bool wp_valid_ = false;
+  uint64_t wp_key_ = 0;
+  bool exposed_ = false;
 };
 
 template <typename Dtype>

@@ -241,7 +241,10 @@ int rram_net_param(rram_net_t n, int i, float** data, float** diff, int64_t* cou
     NEED(n);
     const auto& P = n->net->learnable_params();
     if (i < 0 || i >= (int)P.size()) throw Error("param index out of range");
-    if (data) *data = P[i]->mutable_gpu_data();
+    if (data) {
+      *data = P[i]->mutable_gpu_data();
+      P[i]->data()->expose();
+    }
     if (diff) *diff = P[i]->mutable_gpu_diff();
     if (count) *count = P[i]->count();
     if (lr) *lr = n->net->params_lr()[i];
@@ -260,7 +263,10 @@ int rram_net_failure_param(rram_net_t n, int i, float** data, float** diff, int6
     NEED(n);
     const auto& P = n->net->failure_learnable_params();
     if (i < 0 || i >= (int)P.size()) throw Error("failure param index out of range");
-    if (data) *data = P[i]->mutable_gpu_data();
+    if (data) {
+      *data = P[i]->mutable_gpu_data();
+      P[i]->data()->expose();
+    }
     if (diff) *diff = P[i]->mutable_gpu_diff();
     if (count) *count = P[i]->count();
     if (layer_id) *layer_id = n->net->failure_learnable_layer_ids()[i];

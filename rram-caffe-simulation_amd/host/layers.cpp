@@ -224,9 +224,24 @@ void ConvolutionLayer<Dtype>::Forward_gpu(const std::vector<Blob<Dtype>*>& botto
   const void* xo = want_in_oct_ ? bottom[0]->data()->valid_octets(shp) : nullptr;
   float* y = top[0]->mutable_gpu_data();  // invalidates top's companion
   void* yo = octets_for(top[0], kOctConv);
-  RRAM_CALL(rram_conv2d_fwd_octets(&desc_, bottom[0]->gpu_data(), xo, this->blobs_[0]->gpu_data(),
-                                   bias_term_ ? this->blobs_[1]->gpu_data() : nullptr, y, yo, fused_relu ? 1 : 0,
-                                   Caffe::stream()));
+  const float* bias = bias_term_ ? this->blobs_[1]->gpu_data() : nullptr;
+  const size_t wpb = cache_wpack ? rram_conv_weight_pack_bytes(&desc_) : 0;
+  if (wpb > 0) {
+    // the pack is valid for this layer's shape and engine until the weights'
+    // next mutable access (the MC driver's injection, a solver update, ...)
+    SyncedMemory* wm = this->blobs_[0]->data().get();
+    const rram_conv_desc& d = desc_;
+    const uint64_t key = (((((uint64_t)d.num * 131 + d.channels) * 131 + d.height) * 131 + d.width) * 131 +
+                          d.num_output) * 131 + (uint64_t)d.group * 8 + (uint64_t)rram_get_f32_engine();
+    const float* w = this->blobs_[0]->gpu_data();
+    void* wp = wm->wpack(wpb);
+    RRAM_CALL(rram_conv2d_fwd_cached(&desc_, bottom[0]->gpu_data(), xo, w, wp, wm->wpack_valid(key) ? 1 : 0, bias, y,
+                                     yo, fused_relu ? 1 : 0, Caffe::stream()));
+    wm->set_wpack_valid(key);
+  } else {
+    RRAM_CALL(rram_conv2d_fwd_octets(&desc_, bottom[0]->gpu_data(), xo, this->blobs_[0]->gpu_data(), bias, y, yo,
+                                     fused_relu ? 1 : 0, Caffe::stream()));
+  }
   if (yo) mark_octets(top[0]);
 }
 

@@ -21,6 +21,10 @@ class ConvolutionLayer : public Layer<Dtype> {
   int ExactNumBottomBlobs() const override { return 1; }
   int ExactNumTopBlobs() const override { return 1; }
   bool fused_relu = false;
+  // keep the bf16x6 engine's packed weights next to the weight blob
+  // (SyncedMemory::wpack, rram_conv2d_fwd_cached) while the weights are
+  // unchanged; set by Net::set_weight_pack_cache for the Monte-Carlo driver
+  bool cache_wpack = false;
   const rram_conv_desc& desc() const { return desc_; }
 
  protected:

@@ -573,6 +573,15 @@ void Net<Dtype>::alias_flat_params(Dtype* data, Dtype* diff) {
   HIP_CALL(hipStreamSynchronize(Caffe::hip_stream()));
 }
 
+template <typename Dtype>
+void Net<Dtype>::set_weight_pack_cache(bool on) {
+  for (auto& l : layers_)
+    if (auto* c = dynamic_cast<ConvolutionLayer<Dtype>*>(l.get())) {
+      c->cache_wpack = on;
+      if (!on && !c->blobs().empty()) c->blobs()[0]->data()->drop_wpack();
+    }
+}
+
 template class Net<float>;
 
 }  // namespace caffe

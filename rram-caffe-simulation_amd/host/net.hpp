@@ -88,6 +88,9 @@ class Net {
   // per-layer forward timing with hipEvents (`caffe time`, tools/caffe.cpp:334-421):
   // 0 off, 1 every layer, 2 only layers that own parameters (conv / IP)
   void set_timing(int mode) { timing_ = mode; }
+  // convolution layers keep their packed weights between forwards while the
+  // weights are unchanged (ConvolutionLayer::cache_wpack); off drops every pack
+  void set_weight_pack_cache(bool on);
   EventTimer& timer() { return timer_; }
 
  private:

@@ -608,6 +608,11 @@ MonteCarlo<Dtype>::MonteCarlo(std::shared_ptr<Net<Dtype>> net, const std::vector
     const char* e = getenv("RRAM_MC_OVERLAP");
     overlap_ = !(e && atoi(e) == 0) && first_fault_layer_ > 0;
   }
+  // between maps only the injection rewrites weights: the convolutions keep
+  // their packed weights (Net::set_weight_pack_cache) unless a faultable blob
+  // is theirs (the conv-fault extension), which every map's mutable access
+  // invalidates, or a caller was handed the weights' pointer (SyncedMemory::expose)
+  net_->set_weight_pack_cache(true);
   if (overlap_) {
     HIP_CALL(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
     HIP_CALL(hipEventCreateWithFlags(&ev_free_, hipEventDisableTiming));
@@ -620,6 +625,7 @@ template <typename Dtype>
 MonteCarlo<Dtype>::~MonteCarlo() {
   try {
     RestoreClean();
+    net_->set_weight_pack_cache(false);
     Caffe::synchronize();
   } catch (...) {
   }
@@ -661,6 +667,8 @@ void MonteCarlo<Dtype>::Run(uint32_t map_begin, uint32_t map_count) {
   // profiles/r02_ab_mc_overlap.txt); serial, the default 2048
   const int prev_grid = rram_set_inject_grid(overlap_ ? 512 : 0);
   for (uint32_t m = map_begin; m < map_begin + map_count; ++m) {
+    if (m != map_begin)
+      for (auto* p : params_) (void)p->mutable_gpu_data();
     hipStream_t is = Caffe::hip_stream();
     // RRAM_MC_INJECT_AFTER = k (A/B knob): the overlapped injection starts
     // once layers 0 .. k-1 of this map have run (default 0: at once)

@@ -195,6 +195,19 @@ def conv2d_fwd_octets(d, x, x_oct, w, bias, y, y_oct, relu=False):
                                           int(relu), _stream()), "conv2d_fwd_octets")
 
 
+def conv_weight_pack_bytes(d):
+    """Bytes of the bf16x6 engine's packed-weight companion for d (0: no pack)."""
+    return int(_lib().rram_conv_weight_pack_bytes(C.byref(d)))
+
+
+def conv2d_fwd_cached(d, x, x_oct, w, w_pack, w_pack_valid, bias, y, y_oct=None, relu=False):
+    """rram_conv2d_fwd_octets with a packed-weight companion w_pack (uint8
+    tensor of conv_weight_pack_bytes(d) bytes): w_pack_valid False packs w
+    into it first, True uses it as is."""
+    K.check(_lib().rram_conv2d_fwd_cached(C.byref(d), _p(x), _p(x_oct), _p(w), _p(w_pack), int(bool(w_pack_valid)),
+                                          _p(bias), _p(y), _p(y_oct), int(relu), _stream()), "conv2d_fwd_cached")
+
+
 def conv_input_octets(d):
     """1 when rram_conv2d_fwd_octets would read an input companion for d now."""
     return _lib().rram_conv_input_octets(C.byref(d))

@@ -304,3 +304,72 @@ def test_c5_googlenet_sweep_point(rs, oracle_mod, p_fault):
                  what="inception_4a/5x5")
     mc.close()
     net.close()
+
+
+def test_c5_conv_fault_extension(rs, oracle_mod):
+    """SURVEY.md §7's C5 extension: with fault_layers "InnerProduct,Convolution"
+    every Convolution blob is faultable too (the reference faults only the IP
+    blobs, net.cpp:484-489).  GoogLeNet b32, per-layer SA ratios (convolution
+    weights 30/40/30, IP 20/60/20): every blob of every map bit-exact against
+    the oracle's injection with its broken count exact; over 3 maps each conv
+    weight blob's broken fraction and -1/0/+1 split inside the 3.8 sigma bound;
+    and the forward after injection runs on the injected weights — the first
+    fault layer is now conv1, so the MC driver's injection overlap has nothing
+    to hide under, and any packed-weight reuse would show up as a stale
+    convolution (conv1/7x7_s2 and inception_4a/5x5 within 1e-4 of Σ|a·b| of a
+    float64 evaluation with the injected weights)."""
+    from rramsim import make_inject_cfg
+    caffe, models = rs
+    B = 32
+    net = caffe.Net(models.googlenet(test_batch=B), "test",
+                    models.net_options("googlenet", fault_layers="InnerProduct,Convolution"))
+    layers = net.layers()
+    types = {i: t for i, (n, t, k) in enumerate(layers)}
+    fps = net.failure_params()
+    n_conv = sum(1 for n, t, k in layers if t == "Convolution")
+    assert n_conv == 59                                 # trunk 3 + 9 inceptions x 6 + 2 aux heads
+    assert len(fps) == 2 * (n_conv + 5)
+    assert {types[f["layer_id"]] for f in fps} == {"Convolution", "InnerProduct"}
+    p = 0.02
+    ratios = [(30, 40, 30) if types[f["layer_id"]] == "Convolution" else (20, 60, 20) for f in fps]
+    scale = 7.0
+    cfgs = [make_inject_cfg(p, *r, stuck_scale=scale) for r in ratios]
+    clean = [N(f["data"]) for f in fps]
+    mc = caffe.MonteCarlo(net, cfgs, seed=123, max_maps=8)
+    maps = 3
+    broken = np.zeros(len(fps), np.int64)
+    split = np.zeros((len(fps), 3), np.int64)
+    for m in range(maps):
+        mc.reset()
+        mc.run(m, 1)
+        st = mc.stats()
+        for i, f in enumerate(fps):
+            ref, nb = oracle_mod.inject(clean[i], _oracle_cfg(oracle_mod, cfgs[i]), 123, m, i)
+            got = N(f["data"])
+            assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), (m, i)
+            assert st["broken"][i] == nb, (m, i)
+            broken[i] += nb
+            if i % 2 == 0:
+                g = got[~np.isin(clean[i], [-scale, 0.0, scale])]
+                split[i] += [(g == -scale).sum(), (g == 0).sum(), (g == scale).sum()]
+        # the forward of this map ran on its injected weights
+        pl = _params_by_layer(net)
+        R.check_conv(N(net.blob("conv1/7x7_s2"))[:4], N(net.blob("data"))[:4],
+                     pl["conv1/7x7_s2"][0].reshape(64, 3, 7, 7), pl["conv1/7x7_s2"][1], 2, 3, relu=True,
+                     what=f"conv1/7x7_s2 map {m}")
+        R.check_conv(N(net.blob("inception_4a/5x5"))[:4], N(net.blob("inception_4a/5x5_reduce"))[:4],
+                     pl["inception_4a/5x5"][0].reshape(48, 16, 5, 5), pl["inception_4a/5x5"][1], 1, 2, relu=True,
+                     what=f"inception_4a/5x5 map {m}")
+    checked = 0
+    for i, f in enumerate(fps):
+        if types[f["layer_id"]] != "Convolution" or i % 2:
+            continue
+        assert _binom_ok(int(broken[i]), maps * f["count"], p), (i, broken[i])
+        nb_seen = int(split[i].sum())
+        if nb_seen >= 200:
+            for c in range(3):
+                assert _binom_ok(int(split[i][c]), nb_seen, ratios[i][c] / 100), (i, c, split[i])
+            checked += 1
+    assert checked >= 20
+    mc.close()
+    net.close()
