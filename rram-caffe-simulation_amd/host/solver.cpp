@@ -600,13 +600,16 @@ MonteCarlo<Dtype>::MonteCarlo(std::shared_ptr<Net<Dtype>> net, const std::vector
   HIP_CALL(hipMalloc(reinterpret_cast<void**>(&d_broken_), params_.size() * sizeof(unsigned long long)));
   const auto& fl = net_->failure_learnable_layer_ids();
   first_fault_layer_ = *std::min_element(fl.begin(), fl.end());
-  // on by default (RRAM_MC_OVERLAP=0: serial): round 1 measured it flat
-  // (the injection shares the chip with conv1, 86 -> 120-146 us per launch,
-  // and slowed the fp32 GEMMs); with the bf16x6 kernels it is +0.1..2.4 %
-  // maps/s on AlexNet b256 (profiles/r02_ab_mc_overlap.txt)
+  // RRAM_MC_OVERLAP=1 runs each map's injection on a side stream under the
+  // layers before the first faultable one.  Off by default since the
+  // persistent conv1 kernel holds every CU for its whole run (one 160 KB-LDS
+  // workgroup per CU): the injection then only finds room under pool1 / conv2
+  // and stretches to ~480 us, and the serial order measured the same maps/s
+  // (106.3-106.5k vs 104.5-105.5k overlapped, profiles/r03_ab_mc_overlap.txt;
+  // round 2's +0.1..2.4 % came from the non-persistent conv1 kernel)
   {
     const char* e = getenv("RRAM_MC_OVERLAP");
-    overlap_ = !(e && atoi(e) == 0) && first_fault_layer_ > 0;
+    overlap_ = e && atoi(e) == 1 && first_fault_layer_ > 0;
   }
   // between maps only the injection rewrites weights: the convolutions keep
   // their packed weights (Net::set_weight_pack_cache) unless a faultable blob
@@ -670,15 +673,7 @@ void MonteCarlo<Dtype>::Run(uint32_t map_begin, uint32_t map_count) {
     if (m != map_begin)
       for (auto* p : params_) (void)p->mutable_gpu_data();
     hipStream_t is = Caffe::hip_stream();
-    // RRAM_MC_INJECT_AFTER = k (A/B knob): the overlapped injection starts
-    // once layers 0 .. k-1 of this map have run (default 0: at once)
-    static const int inj_after = [] {
-      const char* e = getenv("RRAM_MC_INJECT_AFTER");
-      return e ? atoi(e) : 0;
-    }();
-    const int k0 = overlap_ ? std::max(0, std::min(inj_after, first_fault_layer_)) : 0;
     if (overlap_) {
-      if (k0 > 0) net_->ForwardFromTo(0, k0 - 1, false);
       HIP_CALL(hipEventRecord(ev_free_, Caffe::hip_stream()));  // previous map's forward is done with the weights
       HIP_CALL(hipStreamWaitEvent(side_, ev_free_, 0));
       is = side_;
@@ -691,7 +686,7 @@ void MonteCarlo<Dtype>::Run(uint32_t map_begin, uint32_t map_count) {
     if (timing_) timer_.stop(0, is);
     if (overlap_) {
       HIP_CALL(hipEventRecord(ev_injected_, side_));
-      if (k0 < first_fault_layer_) net_->ForwardFromTo(k0, first_fault_layer_ - 1, false);  // convolutions run under the injection
+      net_->ForwardFromTo(0, first_fault_layer_ - 1, false);  // the layers before the first faultable one run under the injection
       HIP_CALL(hipStreamWaitEvent(Caffe::hip_stream(), ev_injected_, 0));
       net_->ForwardFromTo(first_fault_layer_, L - 1, false);
     } else {

@@ -120,3 +120,24 @@ def test_mc_maps_with_cached_packs(device, conv_faults):
     _conv_outputs_match(net, device, ALEX)
     mc.close()
     net.close()
+
+
+def test_mc_overlapped_injection_equals_serial(device, monkeypatch):
+    """RRAM_MC_OVERLAP=1 (the injection on a side stream under the layers
+    before the first faultable one; off by default) gives the serial order's
+    per-map accuracy / loss and final logits bit for bit."""
+    from rramsim import caffe, make_inject_cfg, models
+    caffe.set_stream_from_torch()
+    res = []
+    for ov in ("0", "1"):
+        monkeypatch.setenv("RRAM_MC_OVERLAP", ov)
+        caffe.set_random_seed(13)
+        net = caffe.Net(models.alexnet(test_batch=16), "test", models.net_options("alexnet"))
+        mc = caffe.MonteCarlo(net, make_inject_cfg(0.02), seed=5, max_maps=8)
+        mc.run(0, 3)
+        st = mc.stats()
+        res.append((st["per_map"], st["broken"], N(net.blob("fc8"))))
+        mc.close()
+        net.close()
+    assert res[0][0] == res[1][0] and res[0][1] == res[1][1]
+    np.testing.assert_array_equal(res[0][2], res[1][2])
