@@ -74,27 +74,29 @@ def cpu_baseline(batch, p_fault, seed):
     58,631,144 IP cells, then the TEST forward of all `batch` images in the
     reference's layer order (per-image im2col_cpu + cblas_sgemm per group,
     single-threaded LRN / pool / ReLU loops).  Not extrapolated: the whole map
-    is timed.  The same map at the box's per-GPU CPU share (OMP_NUM_THREADS)
-    is reported beside it."""
+    is timed.  The same map also runs with sgemm on the box's per-GPU CPU
+    share (OMP_NUM_THREADS); the faster of the two is the baseline and both
+    are reported (`by_threads`)."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle
     phys = oracle.physical_cores()
-    t, meta = oracle.caffe_cpu_alexnet_map(batch=batch, p_fault=p_fault, seed=seed, threads=phys)
-    total = sum(t.values())
-    res = {"value": round(batch / total, 3), "unit": "images/s", "cores": meta["threads"], "kind": "port",
-           "sample": f"1 full fault map: {meta['broken_cells']} of 58,631,144 IP cells broken + {batch}-image "
-                     f"AlexNet TEST forward, {total:.2f} s; sgemm = {meta['blas']} on {meta['threads']} threads "
-                     f"(= physical cores of the {meta['affinity_cpus']}-CPU affinity set), other layers "
-                     f"single-threaded as in Caffe",
-           "layers_ms": {k: round(v * 1e3, 1) for k, v in t.items()}}
     env = os.environ.get("OMP_NUM_THREADS", "")
     share = int(env) if env.isdigit() else 0
-    if 0 < share < phys:
-        t2, meta2 = oracle.caffe_cpu_alexnet_map(batch=batch, p_fault=p_fault, seed=seed, threads=share)
-        tot2 = sum(t2.values())
-        res["at_cpu_share"] = {"value": round(batch / tot2, 3), "cores": share,
-                               "sample": f"the same map with sgemm on {share} threads (OMP_NUM_THREADS, the box's "
-                                         f"per-GPU CPU share), {tot2:.2f} s"}
+    runs = []
+    for th in sorted({phys} | ({share} if 0 < share < phys else set())):
+        t, meta = oracle.caffe_cpu_alexnet_map(batch=batch, p_fault=p_fault, seed=seed, threads=th)
+        runs.append((batch / sum(t.values()), th, t, meta))
+    # the faster thread count is the baseline (OpenBLAS over all physical cores
+    # of a shared box can lose to the per-GPU share on per-image GEMMs)
+    best = max(runs, key=lambda r: r[0])
+    v, th, t, meta = best
+    res = {"value": round(v, 3), "unit": "images/s", "cores": th, "kind": "port",
+           "sample": f"1 full fault map: {meta['broken_cells']} of 58,631,144 IP cells broken + {batch}-image "
+                     f"AlexNet TEST forward, {sum(t.values()):.2f} s; sgemm = {meta['blas']} on {th} threads, other "
+                     f"layers single-threaded as in Caffe; host: {meta['affinity_cpus']} CPUs in the affinity set = "
+                     f"{phys} physical cores, OMP_NUM_THREADS {env or 'unset'}",
+           "layers_ms": {k: round(x * 1e3, 1) for k, x in t.items()},
+           "by_threads": {str(r[1]): round(r[0], 3) for r in runs}}
     return res
 
 
@@ -257,9 +259,10 @@ def main():
                             "frac": round(inj_gbps / HBM_PEAK_GBPS, 4),
                             "traffic": traffic.get("inject", {}).get("bytes_per_launch"),
                             "algorithmic_bytes_per_launch": 8 * inj_w, "avg_us_per_launch": round(inj_ms_per * 1e3, 2),
-                            "note": ("launched on a side stream, overlapped with conv1-5 of the same map (they share "
-                                     "the CUs, so the launch stretches; RRAM_MC_OVERLAP=0 times it alone)"
-                                     if os.environ.get("RRAM_MC_OVERLAP", "1") != "0" else "serial")},
+                            "note": ("launched on a side stream, overlapped with conv1-5 of the same map "
+                                     "(RRAM_MC_OVERLAP=1; they share the CUs, so the launch stretches)"
+                                     if os.environ.get("RRAM_MC_OVERLAP", "0") == "1" else
+                                     "serial: each map's injection runs alone before its forward")},
         "traffic_source": traffic.get("source"),
         "mc_stats": {"maps": int(stats[len(st["sums"]) + 1].item()), "mean_outputs": mean_out,
                      "broken_cells": int(stats[len(st["sums"])].item())},
