@@ -74,6 +74,12 @@ int rram_net_clear_param_diffs(rram_net_t net);
 int rram_net_num_layers(rram_net_t net, int* n);
 /* name/type copied into caller buffers of `cap` bytes */
 int rram_net_layer_info(rram_net_t net, int i, char* name, char* type, int cap, int* num_params);
+/* Forward contraction of layer i at the current shapes (no reference
+ * counterpart; for rooflines): *flops = 2 M N K of its GEMM (Convolution:
+ * num x Cout x Ho Wo x Cin/group kh kw; InnerProduct: M N K; 0 for other
+ * layers) and *engine = the RRAM_ENGINE_* rram_conv2d_fwd / rram_ip_fwd take
+ * for it now (-1 for other layers). */
+int rram_net_layer_contraction(rram_net_t net, int i, double* flops, int* engine);
 int rram_net_num_blobs(rram_net_t net, int* n);
 int rram_net_blob_name(rram_net_t net, int i, char* name, int cap);
 /* device pointers and shape (up to 8 axes) of a named blob */

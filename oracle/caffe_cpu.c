@@ -174,6 +174,43 @@ void cc_maxpool(const float* x, float* y, int* mask, int num, int C, int H, int 
   }
 }
 
+/* PoolingLayer::Forward_cpu with padding, MAX (method 0, pooling_layer.cpp:
+ * 131-171: window clipped to the image, -FLT_MAX start, strict ">") or AVE
+ * (method 1, :172-200: divisor = the window clipped to the padded image).
+ * PH / PW from the caller (pool_out: ceil rule + the padded clip). */
+void cc_pool(const float* x, float* y, int num, int C, int H, int W, int PH, int PW, int k, int stride, int pad,
+             int method) {
+  for (int64_t nc = 0; nc < (int64_t)num * C; ++nc) {
+    const float* xp = x + nc * H * W;
+    float* yp = y + nc * PH * PW;
+    for (int ph = 0; ph < PH; ++ph)
+      for (int pw = 0; pw < PW; ++pw) {
+        int hs = ph * stride - pad, ws = pw * stride - pad;
+        if (method == 0) {
+          const int he = hs + k < H ? hs + k : H, we = ws + k < W ? ws + k : W;
+          hs = hs > 0 ? hs : 0;
+          ws = ws > 0 ? ws : 0;
+          float m = -FLT_MAX;
+          for (int h = hs; h < he; ++h)
+            for (int w = ws; w < we; ++w)
+              if (xp[h * W + w] > m) m = xp[h * W + w];
+          yp[ph * PW + pw] = m;
+        } else {
+          int he = hs + k < H + pad ? hs + k : H + pad, we = ws + k < W + pad ? ws + k : W + pad;
+          const int size = (he - hs) * (we - ws);
+          hs = hs > 0 ? hs : 0;
+          ws = ws > 0 ? ws : 0;
+          he = he < H ? he : H;
+          we = we < W ? we : W;
+          float a = 0.0f;
+          for (int h = hs; h < he; ++h)
+            for (int w = ws; w < we; ++w) a += xp[h * W + w];
+          yp[ph * PW + pw] = a / size;
+        }
+      }
+  }
+}
+
 /* SoftmaxLayer::Forward_cpu over [outer, C] */
 void cc_softmax(const float* x, float* y, int outer, int C) {
   for (int o = 0; o < outer; ++o) {

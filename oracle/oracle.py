@@ -424,6 +424,7 @@ def cc_init(threads):
     L.cc_lrn.argtypes = [P, P, I, I, I, I, I, F, F, F, P, P]
     L.cc_maxpool.argtypes = [P, P, P, I, I, I, I, I, I]
     L.cc_softmax.argtypes = [P, P, I, I]
+    L.cc_pool.argtypes = [P, P, I, I, I, I, I, I, I, I, I, I]
     for path, mode, desc in blas_candidates():
         if L.cc_init(path.encode(), mode, int(threads)) == 0:
             _cc_ready = desc
@@ -478,6 +479,16 @@ def cc_maxpool(x, k, s):
     y = np.empty((n, c, ph, pw), np.float32)
     mask = np.empty((n, c, ph, pw), np.int32)
     lib().cc_maxpool(_ptr(x), _ptr(y), _ptr(mask), n, c, h, w, k, s)
+    return y
+
+
+def cc_pool(x, k, s, p=0, method="MAX"):
+    """pooling_layer.cpp Forward_cpu with padding, MAX or AVE (caffe_cpu.c)."""
+    x = f32(x)
+    n, c, h, w = x.shape
+    ph, pw = pool_out(h, k, p, s), pool_out(w, k, p, s)
+    y = np.empty((n, c, ph, pw), np.float32)
+    lib().cc_pool(_ptr(x), _ptr(y), n, c, h, w, ph, pw, k, s, p, 0 if method == "MAX" else 1)
     return y
 
 

@@ -1,5 +1,6 @@
 // extern "C" face of the host runtime (include/rram_caffe.h).  Exceptions
 // (the reference's fatal CHECKs) become status codes + a thread-local message.
+#include <algorithm>
 #include <cstring>
 #include <sstream>
 #include <string>
@@ -200,6 +201,30 @@ int rram_net_layer_info(rram_net_t n, int i, char* name, char* type, int cap, in
     copy_str(n->net->layer_names()[i], name, cap);
     copy_str(L[i]->type(), type, cap);
     if (np) *np = (int)L[i]->blobs().size();
+  });
+}
+int rram_net_layer_contraction(rram_net_t n, int i, double* flops, int* engine) {
+  return guarded([&] {
+    NEED(n);
+    const auto& L = n->net->layers();
+    if (i < 0 || i >= (int)L.size()) throw Error("layer index out of range");
+    double f = 0.0;
+    int e = -1;
+    if (auto* c = dynamic_cast<caffe::ConvolutionLayer<float>*>(L[i].get())) {
+      rram_conv_desc d = c->desc();
+      if (rram_conv_out_shape(&d) == RRAM_OK) {
+        f = 2.0 * d.num * d.num_output * d.out_h * d.out_w * (double)(d.channels / d.group) * d.kernel_h * d.kernel_w;
+        e = rram_f32_engine_for_conv(&d);
+      }
+    } else if (auto* ip = dynamic_cast<caffe::InnerProductLayer<float>*>(L[i].get())) {
+      f = 2.0 * ip->M() * (double)ip->N() * ip->K();
+      // the workspace InnerProductLayer::Forward_gpu would hand over
+      const size_t ws = std::max(caffe::Caffe::workspace_size(),
+                                 std::min<size_t>((size_t)16 * ip->M() * ip->N() * sizeof(float), 256ull << 20));
+      e = rram_f32_engine_for_ip(ip->M(), ip->N(), ip->K(), ws);
+    }
+    if (flops) *flops = f;
+    if (engine) *engine = e;
   });
 }
 int rram_net_num_blobs(rram_net_t n, int* k) {

@@ -32,6 +32,7 @@ SIGNATURES = {
     "rram_net_clear_param_diffs": (I, [P]),
     "rram_net_num_layers": (I, [P, PI]),
     "rram_net_layer_info": (I, [P, I, C.c_char_p, C.c_char_p, I, PI]),
+    "rram_net_layer_contraction": (I, [P, I, C.POINTER(C.c_double), PI]),
     "rram_net_num_blobs": (I, [P, PI]),
     "rram_net_blob_name": (I, [P, I, C.c_char_p, I]),
     "rram_net_blob": (I, [P, C.c_char_p, PP, PP, PI, PI]),
@@ -323,6 +324,18 @@ class Net:
             name, typ, np_ = C.create_string_buffer(256), C.create_string_buffer(256), C.c_int()
             check(self._lib.rram_net_layer_info(self.h, i, name, typ, 256, C.byref(np_)), "layer_info")
             out.append((name.value.decode(), typ.value.decode(), np_.value))
+        return out
+
+    def contractions(self) -> Dict[str, tuple]:
+        """{layer name: (forward FLOPs, engine)} for the Convolution and
+        InnerProduct layers at the current shapes (rram_net_layer_contraction;
+        engine 0 = fp32 MFMA, 1 = bf16x6)."""
+        out = {}
+        for i, (name, typ, _) in enumerate(self.layers()):
+            f, e = C.c_double(), C.c_int()
+            check(self._lib.rram_net_layer_contraction(self.h, i, C.byref(f), C.byref(e)), "layer_contraction")
+            if e.value >= 0:
+                out[name] = (f.value, e.value)
         return out
 
     def blob_names(self) -> List[str]:

@@ -21,7 +21,68 @@ from __future__ import annotations
 import math
 import time
 
-MFMA_F32_PEAK_TFLOPS = 157.3
+MFMA_F32_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: fp32 MFMA dense
+MFMA_X6_PEAK_TFLOPS = 2500.0 / 6  # bf16 dense peak / the bf16x6 engine's 6 products
+PEAK_OF_ENGINE = {0: MFMA_F32_PEAK_TFLOPS, 1: MFMA_X6_PEAK_TFLOPS}
+
+
+def contraction_roofline(net, passes, lt=None, note=""):
+    """Roofline of a net's Convolution / InnerProduct forward contractions
+    (the dominant kernels): algorithmic FLOPs per forward pass from
+    rram_net_layer_contraction, times from the live hipEvent layer timers of
+    the timed region (`lt` = net.layer_times(), `passes` forwards timed); the
+    peak is each layer's engine peak (fp32 MFMA 157.3, bf16x6 416.7)."""
+    con = net.contractions()
+    flops = sum(f for f, e in con.values())
+    t_min = sum(f / (PEAK_OF_ENGINE[e] * 1e12) for f, e in con.values())
+    peak = flops / t_min / 1e12
+    out = {"bound": "mfma", "peak": round(peak, 1), "unit": "TFLOP/s", "traffic": None,
+           "algorithmic_flops_per_pass": flops,
+           "engines": {"bf16x6": sum(1 for f, e in con.values() if e == 1), "f32": sum(1 for f, e in con.values() if e == 0)},
+           "flops_share_bf16x6": round(sum(f for f, e in con.values() if e == 1) / max(flops, 1.0), 3)}
+    if lt is not None:
+        ms = sum(m for (name, typ, m, cnt) in lt if name in con) / passes
+        out.update(achieved=round(flops / (ms * 1e-3) / 1e12, 2), frac=round(flops / (ms * 1e-3) / 1e12 / peak, 4),
+                   avg_ms_per_pass=round(ms, 4), kernel="Convolution + InnerProduct forward contractions, live "
+                   "hipEvent layer timers over the timed region" + note)
+    return out
+
+
+def mc_cpu_baseline(model_fn, name, batch, cfgs, seed, budget_s=10.0):
+    """Caffe CPU mode for an MC workload (oracle/cpu_net.py, TEST
+    infrastructure): the map's injection into the faultable blobs through
+    the C oracle plus single-image forwards (per-image im2col + OpenBLAS sgemm,
+    scalar pool / LRN / ReLU loops) for ~budget_s, extrapolated to one
+    `batch`-image map; OpenBLAS on the host's physical cores."""
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "oracle"))
+    import cpu_net
+    import oracle
+    from rramsim import models
+    import os
+    ds = tuple(int(v) for v in str(models.net_options(name)["data_shape"]).split(","))
+    ocfgs = [oracle.InjectCfg(c.thr_fault, c.thr_neg, c.thr_zero, c.thr_sa1, c.stuck_scale, c.g_max, c.quant_levels,
+                              c.var_sigma, c.cell_mode, 0) for c in cfgs]
+    # physical cores and the per-GPU CPU share (OMP_NUM_THREADS): the faster is
+    # the baseline (OpenBLAS over every core of a shared box can lose on
+    # per-image GEMMs), both are reported
+    phys = oracle.physical_cores()
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    share = int(env) if env.isdigit() else 0
+    runs = {}
+    for th in sorted({phys} | ({share} if 0 < share < phys else set())):
+        runs[th] = cpu_net.mc_map_sample(model_fn(test_batch=batch), ds, batch, ocfgs, seed=seed,
+                                         budget_s=budget_s / 2, threads=th)
+    th = max(runs, key=lambda k: runs[k][0])
+    v, meta = runs[th]
+    return {"value": round(v, 3), "unit": "images/s", "cores": meta["threads"], "kind": "port",
+            "by_threads": {str(k): round(r[0], 3) for k, r in runs.items()},
+            "sample": f"1 fault map ({meta['broken']} of {meta['faultable_weights']:,} faultable cells broken by the C "
+                      f"oracle in {meta['t_inject'] * 1e3:.1f} ms) + {meta['images']} single-image TEST forwards in "
+                      f"Caffe CPU mode ({meta['t_img'] * 1e3:.2f} ms/img; sgemm = {meta['blas']} on {meta['threads']} "
+                      f"threads), extrapolated to one {batch}-image map",
+            "layer_share": meta["layer_share"]}
 
 
 def _dist_on():
@@ -29,12 +90,18 @@ def _dist_on():
     return dist.is_available() and dist.is_initialized()
 
 
-def _timed(world, dev, fn, steps, warmup):
+def _timed(world, dev, fn, steps, warmup, net=None):
+    """Warmup, then `steps` timed calls bracketed by barrier + synchronize;
+    max over ranks.  With `net`, its hipEvent timers run around the
+    Convolution / InnerProduct layers during the timed calls only."""
     import torch
     import torch.distributed as dist
     for i in range(warmup):
         fn(i)
     torch.cuda.synchronize()
+    if net is not None:
+        net.layer_times(reset=True)
+        net.set_timing(2)
     if _dist_on():
         dist.barrier()
     torch.cuda.synchronize()
@@ -43,6 +110,8 @@ def _timed(world, dev, fn, steps, warmup):
         fn(warmup + i)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    if net is not None:
+        net.set_timing(0)
     t = torch.tensor([el], dtype=torch.float64, device=dev)
     if _dist_on():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -123,10 +192,10 @@ def run_workload(args, world, rank, dev):
             gmax = float(f["data"].abs().max().item()) or 1.0
             cfgs.append(make_inject_cfg(0.01, 10, 20, 10, quant_levels=16, g_max=gmax, var_sigma=0.1,
                                         stuck_scale=gmax))
-        mc = caffe.MonteCarlo(net, cfgs, seed=args.seed, max_maps=args.steps + args.warmup + 8)
+        mc = caffe.MonteCarlo(net, cfgs, seed=args.seed, max_maps=(args.steps + args.warmup) * 10 + 8)
         maps_per_step = 10
         el = _timed(world, dev, lambda i: mc.run((rank + world * i) * maps_per_step, maps_per_step),
-                    args.steps, args.warmup)
+                    args.steps, args.warmup, net)
         st = mc.stats()
         tot = allreduce_stats(st["sums"] + [st["maps"]], dev)
         n_maps = world * args.steps * maps_per_step
@@ -135,8 +204,14 @@ def run_workload(args, world, rank, dev):
                     global_batch=batch * world, maps_per_step=maps_per_step * world, p_fault=0.01)
         res["images_per_s"] = round(n_maps * batch / el, 1)
         res["mc_mean_outputs"] = [x / max(tot[-1], 1) for x in tot[:-1]]
+        res["roofline"] = contraction_roofline(net, args.steps * maps_per_step, net.layer_times())
         mc.close()
         net.close()
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            cb = mc_cpu_baseline(models.cifar10_quick, "cifar10_quick", batch, cfgs, args.seed)
+            cb.update(value=round(cb["value"] / batch, 4), unit="maps/s",
+                      images_per_s=cb["value"])   # the metric is maps/s: one map = one `batch`-image pass
+            res["cpu_baseline"] = cb
         return res
 
     if args.workload == "lenet_mc":
@@ -181,6 +256,33 @@ def run_workload(args, world, rank, dev):
                     parallelism=f"dp{world} (RCCL all-reduce of {dp.num_params} fp32 grads"
                                 f"{', bucketed, overlapped with backward' if dp.overlap else ''})")
         res["broken_cells"] = sum(dp.solver.broken_counts())
+        # training roofline over the whole iteration: forward + weight-gradient +
+        # data-gradient contractions (the first layer computes no data gradient;
+        # the backward GEMMs run on the fp32 MFMA engine), against the step time
+        con = dp.solver.net.contractions()
+        fwd = sum(f for f, e in con.values())
+        first = next(iter(con.values()))[0] if con else 0.0
+        flops = 3 * fwd - first
+        t_min = (sum(f / (PEAK_OF_ENGINE[e] * 1e12) for f, e in con.values())
+                 + (2 * fwd - first) / (MFMA_F32_PEAK_TFLOPS * 1e12))
+        ach = flops / (el / args.steps) / 1e12
+        peak = flops / t_min / 1e12
+        res["roofline"] = {"bound": "mfma", "achieved": round(ach, 3), "peak": round(peak, 1),
+                           "unit": "TFLOP/s", "frac": round(ach / peak, 4), "traffic": None,
+                           "algorithmic_flops_per_step": flops,
+                           "kernel": "whole training iteration: forward (engine per layer) + backward dW / dX "
+                                     "contractions (fp32 MFMA) of the Convolution / InnerProduct layers over the "
+                                     "step time (includes the LRN / pool / loss / update / Fail kernels and the "
+                                     "launch gaps of a batch-100 net)"}
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            # a CPU training iteration costs more than its TEST-phase forward:
+            # the forward-only Caffe-CPU rate bounds the CPU training rate from above
+            name = args.workload.split("_train")[0] if args.workload == "lenet_train" else "cifar10_full"
+            fn = models.lenet if name == "lenet" else models.cifar10_full
+            cb = mc_cpu_baseline(fn, name, batch, [make_inject_cfg(0.0)], args.seed, budget_s=5.0)
+            cb["sample"] = ("UPPER BOUND on CPU training throughput: TEST-phase forward only, no backward / update. "
+                            + cb["sample"])
+            res["cpu_baseline"] = cb
         dp.close()
         return res
 
@@ -202,7 +304,7 @@ def run_workload(args, world, rank, dev):
         def step(i):
             for mc in mcs:                       # one map per fault rate per step
                 mc.run(rank + world * i, 1)
-        el = _timed(world, dev, step, args.steps, args.warmup)
+        el = _timed(world, dev, step, args.steps, args.warmup, net)
         sweep = []
         for p, mc in zip(rates, mcs):
             st = mc.stats()
@@ -213,8 +315,11 @@ def run_workload(args, world, rank, dev):
                     world, args, el, workload="googlenet_sweep_0.1-10pct", model="GoogLeNet (train_val TEST)",
                     global_batch=batch * world, rates=rates)
         res["sweep"] = sweep
+        res["roofline"] = contraction_roofline(net, args.steps * len(rates), net.layer_times())
         for mc in mcs:
             mc.close()
         net.close()
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = mc_cpu_baseline(models.googlenet, "googlenet", batch, cfgs_for(0.01), args.seed)
         return res
     raise ValueError(args.workload)

@@ -250,9 +250,19 @@ def test_c5_googlenet_sweep_point(rs, oracle_mod, p_fault):
     the oracle's injection and its broken count exact; over 4 maps the broken
     fraction and the -1/0/+1 split of every weight blob pass the 3.8 sigma
     binomial bound; the IP layers' outputs within 1e-4 of Σ|a·b|."""
+    _c5_sweep_point(rs, oracle_mod, p_fault, 32)
+
+
+def test_c5_googlenet_b256_sweep_point(rs, oracle_mod):
+    """C5 at the bench batch (b256, p = 2 %): the same gates on the kernels
+    and grids the googlenet_sweep workload runs (per-layer fp64 checks on the
+    first four images of the batch)."""
+    _c5_sweep_point(rs, oracle_mod, 0.02, 256)
+
+
+def _c5_sweep_point(rs, oracle_mod, p_fault, B):
     from rramsim import make_inject_cfg
     caffe, models = rs
-    B = 32
     net = caffe.Net(models.googlenet(test_batch=B), "test", models.net_options("googlenet"))
     fps = net.failure_params()
     names = [n for n, t, k in net.layers() if t == "InnerProduct"]
@@ -302,6 +312,12 @@ def test_c5_googlenet_sweep_point(rs, oracle_mod, p_fault):
     R.check_conv(N(net.blob("inception_4a/5x5"))[:4], N(net.blob("inception_4a/5x5_reduce"))[:4],
                  p["inception_4a/5x5"][0].reshape(48, 16, 5, 5), p["inception_4a/5x5"][1], 1, 2, relu=True,
                  what="inception_4a/5x5")
+    R.check_conv(N(net.blob("inception_3a/1x1"))[:4], N(net.blob("pool2/3x3_s2"))[:4],
+                 p["inception_3a/1x1"][0].reshape(64, 192, 1, 1), p["inception_3a/1x1"][1], 1, 0, relu=True,
+                 what="inception_3a/1x1")
+    R.check_conv(N(net.blob("inception_4e/3x3"))[:4], N(net.blob("inception_4e/3x3_reduce"))[:4],
+                 p["inception_4e/3x3"][0].reshape(320, 160, 3, 3), p["inception_4e/3x3"][1], 1, 1, relu=True,
+                 what="inception_4e/3x3")
     mc.close()
     net.close()
 
