@@ -215,7 +215,7 @@ struct InjectSegs {
 };
 
 constexpr int kInjChunk = 256 * 4 * 4;  // elements per block-chunk (4 float4 per lane)
-constexpr int kInjectGrid = 2048;      // default persistent grid (RRAM_INJECT_GRID overrides)
+constexpr int kInjectGrid = 2048;      // default persistent grid
 // rram_set_inject_grid: a caller-chosen grid (0: kInjectGrid), e.g. a smaller
 // one when the injection runs beside other kernels (MonteCarlo's overlap)
 std::atomic<int>& inject_grid() {
@@ -752,15 +752,8 @@ int rram_inject_rng_batched(const rram_inject_seg* segs, int nsegs, uint64_t see
   // persistent grid of kInjectGrid blocks over the 4096-weight chunks.  One
   // block per chunk (14,315 for AlexNet) measured 2x slower in the MC loop
   // (190 vs 100 us): every block ends in a same-address counter atomic, and
-  // the serialised atomics, not HBM, set the pace.  RRAM_INJECT_GRID (tuning
-  // knob) overrides the grid.
-  static const int64_t grid_env = [] {
-    const char* e = getenv("RRAM_INJECT_GRID");
-    const long v = e ? atol(e) : 0;
-    return v > 0 ? static_cast<int64_t>(v) : static_cast<int64_t>(0);
-  }();
-  const int64_t grid_cap = grid_env > 0 ? grid_env
-                           : inject_grid().load(std::memory_order_relaxed) > 0
+  // the serialised atomics, not HBM, set the pace.
+  const int64_t grid_cap = inject_grid().load(std::memory_order_relaxed) > 0
                                ? static_cast<int64_t>(inject_grid().load(std::memory_order_relaxed))
                                : static_cast<int64_t>(kInjectGrid);
   const int grid = static_cast<int>(total < grid_cap ? total : grid_cap);

@@ -1277,18 +1277,10 @@ int launch(const Params& P, int gz, hipStream_t s, bool force_big) {
     if (P.M <= 64 || P.N <= 64) return launch_cfg<2, 2, 1, 1, AM, BMODE, OM, KB>(P, gz, s);
     return launch_cfg<2, 2, 2, 2, AM, BMODE, OM, KB>(P, gz, s);
   }
-  // tuning knob: RRAM_GEMM_TILE = 64 | 96 | 128 | 192 forces BM (BN = 128), 6464 the 64x64 tile
-  static const int forced = [] {
-    const char* e = getenv("RRAM_GEMM_TILE");
-    return e ? atoi(e) : 0;
-  }();
-  if (forced == 6464) return launch_cfg<2, 2, 1, 1, AM, BMODE, OM, KB>(P, gz, s);
-  if (forced == 128256) return launch_cfg<2, 2, 2, 4, AM, BMODE, OM, KB>(P, gz, s);  // 128 x 256, 2 waves/SIMD
-  if (forced == 256128) return launch_cfg<2, 2, 4, 2, AM, BMODE, OM, KB>(P, gz, s);  // 256 x 128, 2 waves/SIMD
   // thin M (CIFAR / LeNet convolutions, M = 20..32): a 32 x 128 tile wastes no
   // MFMA rows (64 x 64 would pad half of them)
   if constexpr (KB == 32) {
-    if (P.M <= 32 && forced != 64 && forced != 96 && forced != 128 && forced != 192)
+    if (P.M <= 32)
       return launch_cfg<1, 4, 1, 1, AM, BMODE, OM, KB>(P, gz, s);
   }
   // 128 x 256 at 2 waves per SIMD (8 accumulators per wave: half the LDS and
@@ -1298,11 +1290,7 @@ int launch(const Params& P, int gz, hipStream_t s, bool force_big) {
   // conv3 (507 such tiles, one round) 0.70 -> 0.69 ms is within noise, and
   // conv4 / conv5 / conv1 (fewer tiles or M % 128 != 0) are slower, so they
   // keep the policy below.
-  static const bool wide = [] {
-    const char* e = getenv("RRAM_GEMM_WIDE");  // tuning knob: 0 disables the 128 x 256 tile
-    return !(e && atoi(e) == 0);
-  }();
-  if (KB == 16 && wide && !forced && P.M % 128 == 0 && (int64_t)(P.M / 128) * ((P.N + 255) / 256) * gz >= 1024)
+  if (KB == 16 && P.M % 128 == 0 && (int64_t)(P.M / 128) * ((P.N + 255) / 256) * gz >= 1024)
     return launch_cfg<2, 2, 2, 4, AM, BMODE, OM, KB>(P, gz, s);
   const int64_t ntn = (P.N + 127) / 128;
   const int cands[4] = {128, 192, 96, 64};  // ties keep 128 (2 blocks per CU)
@@ -1317,10 +1305,9 @@ int launch(const Params& P, int gz, hipStream_t s, bool force_big) {
       best_pad = pad;
     }
   }
-  if (KB == 16 && !forced && P.M % 128 != 0 && P.M % 64 == 0 && ntn * (P.M / 64) * gz >= 512)
+  if (KB == 16 && P.M % 128 != 0 && P.M % 64 == 0 && ntn * (P.M / 64) * gz >= 512)
     best = 64;  // e.g. M = 192: three unpadded 64-row tiles beat one 192-row tile at KB = 16
-  if (forced == 64 || forced == 96 || forced == 128 || forced == 192) best = forced;
-  else if (best == 64 && ntn * ((P.M + 63) / 64) * gz < 256)
+  if (best == 64 && ntn * ((P.M + 63) / 64) * gz < 256)
     return launch_cfg<2, 2, 1, 1, AM, BMODE, OM, KB>(P, gz, s);  // 64 x 64: twice the blocks
   switch (best) {
     case 192: return launch_cfg<2, 2, 3, 2, AM, BMODE, OM, KB>(P, gz, s);  // 192 x 128
@@ -1333,40 +1320,24 @@ int launch(const Params& P, int gz, hipStream_t s, bool force_big) {
 }
 
 template <int AM, int BMODE, int OM>
-int launch2(Params P, int gz, hipStream_t s, int nst) {
+int launch2(Params P, int gz, hipStream_t s) {
   P.tiles_m = (P.M + g2::BM - 1) / g2::BM;
   P.tiles_n = (P.N + g2::BN - 1) / g2::BN;
   P.tiles_z = gz;
   const int64_t nwg = (int64_t)P.tiles_m * P.tiles_n * gz;
   RRAM_REQUIRE(nwg < (1ll << 31), "gemm: grid too large");
-  if (nst == 2)
-    hipLaunchKernelGGL((k_gemm2<AM, BMODE, OM, 2>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, P);
-  else
-    hipLaunchKernelGGL((k_gemm2<AM, BMODE, OM, 3>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, P);
+  hipLaunchKernelGGL((k_gemm2<AM, BMODE, OM, 3>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, P);
   return launch_status("gemm2");
 }
 
-// k_gemm2 policy (tuning knob RRAM_GEMM_V2 = 0 off | 2 | 3 LDS stages, default 3):
-// 16-byte A and B (the IP layers), M padded by at most 1/8 in 128-row tiles,
-// N > 64, and operands addressable with 32-bit buffer offsets.  MI355X,
-// AlexNet b256 (scripts/gpu_g2.sh, kbench): fc6 111 -> 119 TFLOP/s, fc7 100 ->
-// 109.  The table-gather convolutions stay on k_gemm: at one wave per SIMD the
-// gather's 16 four-byte LDS-DMA issues per wave and K-tile cap it at 68 % MFMA
-// busy (conv3 109 -> 100 TFLOP/s; RRAM_GEMM_V2_CONV=1 selects it for A/B runs).
-int gemm2_stages() {
-  static const int v = [] {
-    const char* e = getenv("RRAM_GEMM_V2");
-    const int x = e ? atoi(e) : 3;
-    return x == 0 || x == 2 || x == 3 ? x : 3;
-  }();
-  return v;
-}
+// k_gemm2 policy (3 LDS stages): 16-byte A and B (the IP layers), M padded by
+// at most 1/8 in 128-row tiles, N > 64, and operands addressable with 32-bit
+// buffer offsets.  MI355X, AlexNet b256 (kbench): fc6 111 -> 119 TFLOP/s, fc7
+// 100 -> 109.  The table-gather convolutions stay on k_gemm: at one wave per
+// SIMD the gather's 16 four-byte LDS-DMA issues per wave and K-tile cap it at
+// 68 % MFMA busy (conv3 109 -> 100 TFLOP/s measured).
 bool gemm2_ok(int am, int bm, const Params& P) {
-  static const bool conv = [] {
-    const char* e = getenv("RRAM_GEMM_V2_CONV");
-    return e && atoi(e) == 1;
-  }();
-  if (gemm2_stages() == 0 || am != KCV || (bm != KCV && !(conv && bm == CONVT))) return false;
+  if (am != KCV || bm != KCV) return false;
   const int64_t mt = (P.M + g2::BM - 1) / g2::BM * g2::BM;
   if (P.N <= 64 || (mt - P.M) * 8 > mt) return false;
   auto fits = [](const View& v) { return ((int64_t)(v.rows - 1) * v.ld + v.kdim) * 4 < (1ll << 31); };
@@ -1375,24 +1346,17 @@ bool gemm2_ok(int am, int bm, const Params& P) {
   return true;
 }
 
-// K-tile depth of the implicit-GEMM convolution (tuning knob RRAM_GEMM_KB = 16 | 32)
+// K-tile depth of the implicit-GEMM convolution
 // Measured on MI355X (scripts/gpu_sweep.sh, AlexNet b256): K >= 1024 runs
 // faster with 16-deep K-tiles (half the LDS and loader registers: 3 waves per
 // SIMD instead of 2), short K (conv1, K = 363) with 32.
 int conv_kb(int K) {
-  static const int forced = [] {
-    const char* e = getenv("RRAM_GEMM_KB");
-    return e ? atoi(e) : 0;
-  }();
-  if (forced == 16 || forced == 32) return forced;
   return K >= 1024 ? 16 : 32;
 }
 
 int dispatch(int am, int bm, int om, const Params& P, int gz, hipStream_t s, bool force_big = false) {
   if (gemm2_ok(am, bm, P)) {
-    const int nst = gemm2_stages();
-    if (bm == CONVT && om == OUT_NCHW) return launch2<KCV, CONVT, OUT_NCHW>(P, gz, s, nst);
-    if (bm == KCV && om == OUT_ROWMAJOR) return launch2<KCV, KCV, OUT_ROWMAJOR>(P, gz, s, nst);
+    if (om == OUT_ROWMAJOR) return launch2<KCV, KCV, OUT_ROWMAJOR>(P, gz, s);
   }
   if (bm == CONV && om == OUT_NCHW && conv_kb(P.K) == 16) {
     if (am == KC) return launch<KC, CONV, OUT_NCHW, 16>(P, gz, s, force_big);
@@ -1535,12 +1499,7 @@ int gemm_core(int trans_a, int trans_b, int M, int N, int K, float alpha, const 
   // split-K when the 128x128 grid is far below the CU count and K is long
   const int64_t tiles = (int64_t)((N + 127) / 128) * ((M + 127) / 128);
   int split = 1;
-  // split-K target grid (A/B knob RRAM_SPLITK_TARGET, default 256 blocks)
-  static const int target = [] {
-    const char* e = getenv("RRAM_SPLITK_TARGET");
-    const int v = e ? atoi(e) : 0;
-    return v >= 64 && v <= 4096 ? v : 256;
-  }();
+  constexpr int target = 256;  // split-K target grid (blocks)
   if (ws != nullptr && tiles < target && K >= 1024) {
     split = static_cast<int>(target / (tiles > 0 ? tiles : 1));
     if (split > 16) split = 16;
@@ -1595,18 +1554,13 @@ float* pack_buffer(size_t floats, hipStream_t s) {
 
 template <int KH, int KW, int CPH, int MI, int PD>
 int launch_patch(Params P, const float* wpack, int PW, int CS, int gz, hipStream_t s) {
-  // LDS stages: 2 (two workgroups per CU, 2 waves per SIMD) unless the
-  // 192-row tile's registers need the whole SIMD; RRAM_CONV_PATCH_NST = 2 | 3
-  static const int nst_env = [] {
-    const char* e = getenv("RRAM_CONV_PATCH_NST");
-    return e ? atoi(e) : 0;
-  }();
-  // default: 2 stages whenever two workgroups' 2-stage rings fit the 160 KB LDS
+  // LDS stages: 2 (two workgroups per CU, 2 waves per SIMD) whenever two
+  // workgroups' 2-stage rings fit the 160 KB LDS, else 3
   using Sh = cp::Shape<KH, KW, CPH>;
   constexpr int a_reg = ((64 * MI * Sh::RL + 255) / 256 + 3) / 4 * 4 * 256;
   constexpr int sf = a_reg + PD * 4 * 64;
   constexpr bool two_fit = 2 * 2 * sf * 4 <= 160 * 1024;
-  const int nst = (nst_env == 2 && two_fit) || nst_env == 3 ? nst_env : (two_fit ? 2 : 3);
+  const int nst = two_fit ? 2 : 3;
   P.tiles_m = (P.M + 64 * MI - 1) / (64 * MI);
   P.tiles_n = (P.N + cp::BN - 1) / cp::BN;
   P.tiles_z = gz;
@@ -1629,13 +1583,8 @@ int launch_patch(Params P, const float* wpack, int PW, int CS, int gz, hipStream
 // k_conv_patch for a stride-1, undilated 3x3 / 5x5 convolution whose output
 // planes hold >= 128 positions.  Returns 1 when it ran, 0 when the shape is
 // not covered (the caller falls back to the implicit-im2col GEMM), < 0 on
-// error.  Tuning knob RRAM_CONV_PATCH = 0 disables it.
+// error.
 int conv_patch_fwd(const rram_conv_desc* d, const float* w, Params& P, hipStream_t s) {
-  static const bool on = [] {
-    const char* e = getenv("RRAM_CONV_PATCH");
-    return !(e && atoi(e) == 0);
-  }();
-  if (!on) return 0;
   const int KH = d->kernel_h, KW = d->kernel_w;
   if (d->stride_h != 1 || d->stride_w != 1 || d->dilation_h != 1 || d->dilation_w != 1) return 0;
   if (!((KH == 3 && KW == 3) || (KH == 5 && KW == 5))) return 0;
@@ -1746,17 +1695,17 @@ int conv_fwd_core(const rram_conv_desc* d, const float* x, const float* w, const
   const int taps = d->kernel_h * d->kernel_w;
   const bool wide = padded && taps > 31;
   int bmode = CONV;
-  if (getenv("RRAM_CONV_NO_TABLE") == nullptr && (!padded || taps <= 63) &&
+  if ((!padded || taps <= 63) &&
       (int64_t)cin_g * d->height * d->width * 4 < (1ll << 31)) {
     cv.tbl = conv_table(cv, K, padded, wide, s);
     cv.taps = padded ? taps : 0;
     if (cv.tbl) bmode = wide ? CONVT64 : CONVT;
   }
   // A: 16-byte loads when the rows are 16-byte aligned; else (K % 4 != 0) the
-  // unaligned raw-buffer form for the table gather (RRAM_CONV_NO_KCU: scalar)
+  // unaligned raw-buffer form for the table gather
   int amode = vec_ok(w, K, K, P.grp_a) ? KCV : KC;
   if (amode == KC && bmode == CONVT && (reinterpret_cast<uintptr_t>(w) & 3u) == 0 &&
-      (int64_t)g * cout_g * K * 4 < (1ll << 31) && getenv("RRAM_CONV_NO_KCU") == nullptr)
+      (int64_t)g * cout_g * K * 4 < (1ll << 31))
     amode = KCU;
   return dispatch(amode, bmode, OUT_NCHW, P, g, s);
 }

@@ -654,8 +654,7 @@ int rram_pool_fwd(const float* x, float* y, int* mask, int num, int C, int H, in
   if (total == 0) return RRAM_OK;
   RRAM_REQUIRE(x && y, "pool_fwd: NULL");
   const int planes = num * C;
-  if (method == RRAM_POOL_MAX && kh == kw && (kh == 3 || kh == 2) && H * W <= kPlaneTile &&
-      getenv("RRAM_POOL_NO_PLANES") == nullptr) {
+  if (method == RRAM_POOL_MAX && kh == kw && (kh == 3 || kh == 2) && H * W <= kPlaneTile) {
     // planes per block: fill the LDS tile, but keep >= 2048 blocks when possible
     int ppb = kPlaneTile / (H * W);
     while (ppb > 1 && (planes + ppb - 1) / ppb < 2048) --ppb;

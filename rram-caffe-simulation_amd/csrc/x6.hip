@@ -300,63 +300,24 @@ k_conv_patch_x6(Params P, const uint16_t* __restrict__ wpack, int PW, int CS) {
 // global loads: the loop is MFMA-paced.
 namespace cbx6 {
 constexpr int FRAG = 3 * 64;  // bf16x8 units per pre-split weight fragment (3 terms x 64 lanes)
-// weight prefetch distance (groups) and LDS bytes of a (KH, NB, PD) instance
-constexpr int dist(int NB) { return NB == 8 ? 2 : 3; }
-constexpr int lds_bytes(int NB, int PD) { return 2 * PD * 4096 + 4 * (dist(NB) + 1) * 3072; }
-// first patch piece of K-tile kt + 1 issued at tap s (pieces spread evenly
-// over taps 0 .. T - 2, so the last tap's weight load is younger than all)
+// first patch piece of K-tile kt + 1 staged at tap s (pieces spread evenly
+// over taps 0 .. T - 2)
 constexpr int piece_lo(int s, int PD, int T) { return s >= T - 1 ? PD : (s * PD + T - 2) / (T - 1); }
-constexpr int pieces(int s, int PD, int T, bool more) { return more ? piece_lo(s + 1, PD, T) - piece_lo(s, PD, T) : 0; }
-// memory operations issued after group q + 1's weight pieces, counted at the
-// end of tap s (q = kt T + s): the patch pieces of taps max(0, s + 1 - D) .. s
-// (those of the previous K-tile are not counted: waiting on fewer is safe)
-// and the 3-piece weight loads of groups q + 2 .. q + D that exist
-constexpr int after_a(int s, int PD, int T, int D, bool more) {
-  int n = 0;
-  for (int t = s + 1 - D < 0 ? 0 : s + 1 - D; t <= s; ++t) n += pieces(t, PD, T, more);
-  int na = more ? D - 1 : ((T - 1 - s < D ? T - 1 - s : D) - 1);
-  return n + 3 * (na > 0 ? na : 0);
-}
-// operations issued after the last patch piece of K-tile kt + 1: the weight
-// loads of the taps after it
-constexpr int after_patch(int PD, int T) {
-  int sl = 0;
-  for (int t = 0; t < T; ++t)
-    if (pieces(t, PD, T, true) > 0) sl = t;
-  return 3 * (T - 1 - sl);
-}
 }  // namespace cbx6
 
-// s_waitcnt vmcnt(n) for an n the compiler folds to a constant after unrolling
-__device__ __forceinline__ void wait_vm_n(int n) {
-  switch (n) {
-#define RRAM_W(k) \
-  case k:         \
-    g2::wait_vm<k>(); \
-    break;
-    RRAM_W(0) RRAM_W(1) RRAM_W(2) RRAM_W(3) RRAM_W(4) RRAM_W(5) RRAM_W(6) RRAM_W(7) RRAM_W(8) RRAM_W(9)
-    RRAM_W(10) RRAM_W(11) RRAM_W(12) RRAM_W(13) RRAM_W(14) RRAM_W(15) RRAM_W(16) RRAM_W(17) RRAM_W(18)
-    RRAM_W(19) RRAM_W(20) RRAM_W(21) RRAM_W(22) RRAM_W(23) RRAM_W(24)
-#undef RRAM_W
-    default:
-      g2::wait_vm<24>();  // n > 24: waiting on fewer is safe
-  }
-}
-
-// VL: the loop's global reads are compiler-visible register loads (weights
-// straight into the fragment registers one group ahead; patch pieces into
-// staging registers, written to LDS one tap later) instead of LDS-DMA, whose
-// issue cost (~100 cycles per piece among MFMAs) the weight ring paid 3 times
-// per group.
-template <int KH, int KW, int WR, int NB, int PD, bool VL>
+// The loop's global reads are compiler-visible register loads: weights
+// straight into the fragment registers one group ahead, patch pieces into
+// staging registers, written to LDS one tap later.  (An LDS-DMA weight ring
+// with hand-counted vmcnt measured slower: each DMA piece costs ~100 cycles
+// of issue among the MFMAs, and the ring paid 3 per group.)
+template <int KH, int KW, int WR, int NB, int PD>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __restrict__ xpack, int octb, int rpc,
              uint32_t xrange, int ximg, char* __restrict__ yoct, int cout8, FastDiv oct_div, FastDiv rpc_div) {
   using namespace g2;
   constexpr int T = KH * KW, WC = 4 / WR, BMc = 32 * WR, BNc = 32 * NB * WC, SFB = PD * 4 * 1024;
-  constexpr int D = cbx6::dist(NB), NSA = D + 1;
-  static_assert(cbx6::lds_bytes(NB, PD) <= 160 * 1024 && D < T, "LDS");
-  __shared__ __attribute__((aligned(16))) char smem[VL ? 2 * SFB : cbx6::lds_bytes(NB, PD)];
+  static_assert(2 * SFB <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[2 * SFB];
   const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem));
 
   const int lane = threadIdx.x & 63;
@@ -428,19 +389,6 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
     const int prow = sg == 0 ? oh - f0 : (sg == 1 ? p1 : p2) + oh;
     bb[j] = lh * octb + prow * rpc * 16 + ow * 48;
   }
-  // this wave's weight fragment stream (group q = kt T + s at byte
-  // q 3072 + t 1024), LDS-DMA'd D groups ahead into a wave-private ring of
-  // NSA slots: every global access of the loop is an LDS-DMA whose
-  // completion is counted by hand (vmcnt), so no compiler-placed vmcnt(0)
-  // waits on the patch pieces in flight
-  const int Q = KT * T;
-  const int4v arsrc = make_rsrc(
-      reinterpret_cast<const float*>(wpack + ((int64_t)((z * P.tiles_m + tm) * WR + wr) * KT) * T * cbx6::FRAG),
-      static_cast<uint32_t>(Q * 3072));
-  const uint32_t aring = lds0 + static_cast<uint32_t>(2 * SFB + wave * NSA * 3072);
-  const char* aring_p = smem + 2 * SFB + wave * NSA * 3072 + lane * 16;
-  const uint32_t lane16 = static_cast<uint32_t>(lane * 16);
-
   floatx16 acc[1][NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j)
@@ -451,18 +399,7 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
     dma_b128(xrsrc, poff[i] + static_cast<uint32_t>(kt) * 2u * PL,
              lds0 + static_cast<uint32_t>(stg * SFB + (wave * PD + i) * 1024));
   };
-  auto issue_a = [&](int q) {
-    const uint32_t sl = aring + static_cast<uint32_t>(q % NSA) * 3072u;
-#pragma unroll
-    for (int t = 0; t < 3; ++t)
-      dma_b128(arsrc, lane16 + static_cast<uint32_t>(q * 3072 + t * 1024), sl + static_cast<uint32_t>(t * 1024));
-  };
   x6::bf16x8 fa[2][3], fb[2][3];
-  auto read_a = [&](x6::bf16x8 (&f)[3], int q) {
-    const char* p = aring_p + (q % NSA) * 3072;
-#pragma unroll
-    for (int t = 0; t < 3; ++t) f[t] = *reinterpret_cast<const x6::bf16x8*>(p + 1024 * t);
-  };
   auto read_b = [&](x6::bf16x8 (&f)[3], const char* st, int s, int j) {
     const int kh = s / KW, kw = s - kh * KW;
     const char* p = st + bb[j] + kh * rpc * 16 + kw * 48;
@@ -470,7 +407,7 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
     for (int t = 0; t < 3; ++t) f[t] = *reinterpret_cast<const x6::bf16x8*>(p + 16 * t);
   };
 
-  if constexpr (VL) {
+  {
     const x6::bf16x8* ap = wpack + ((int64_t)((z * P.tiles_m + tm) * WR + wr) * KT) * T * cbx6::FRAG + lane;
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint16_t*>(xg), 0, static_cast<int>(xrange - static_cast<uint32_t>(z * (cv.C >> 3)) * PL), 0x00020000);
@@ -552,83 +489,7 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
         vtile(kt, P0{}, F_{});
       }
     }
-  } else {
-#pragma unroll
-  for (int i = 0; i < PD; ++i) issue(0, 0, i);
-#pragma unroll
-  for (int d = 0; d < D; ++d) issue_a(d);  // Q >= T > D
-  wait_vm<0>();
-  __builtin_amdgcn_s_barrier();
-  read_a(fa[0], 0);
-  read_b(fb[0], smem, 0, 0);
-
-  // one K-tile; PAR: parity of its first group's weight fragments; MORE: K-tile kt + 1 exists
-  auto ktile = [&](int kt, auto par_c, auto more_c) {
-    constexpr int PAR = decltype(par_c)::value;
-    constexpr bool MORE = decltype(more_c)::value;
-    const char* cur = smem + (kt & 1) * SFB;
-    const char* nxt = smem + ((kt + 1) & 1) * SFB;
-#pragma unroll
-    for (int s = 0; s < T; ++s) {
-      const int pa = (s + PAR) & 1;
-      const int q = kt * T + s;
-      // block 0: weights of group q + D, then the patch pieces of K-tile
-      // kt + 1 for this tap
-      if (MORE || s + D < T) issue_a(q + D);
-      if (MORE) {
-#pragma unroll
-        for (int i = cbx6::piece_lo(s, PD, T); i < cbx6::piece_lo(s + 1, PD, T); ++i) issue(kt + 1, (kt + 1) & 1, i);
-      }
-#pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        const bool last = s == T - 1 && j == NB - 1;
-        if (j == NB - 1 && (s + 1 < T || MORE)) {
-          // group q + 1's weights have landed: at most n_after(...) younger
-          // operations may still be in flight
-          const int na = cbx6::after_a(s, PD, T, D, MORE);
-          if (last && MORE) {
-            wait_vm_n(min(na, cbx6::after_patch(PD, T)));
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            __builtin_amdgcn_sched_barrier(0);
-          } else {
-            wait_vm_n(na);
-          }
-          read_a(fa[pa ^ 1], q + 1);
-        }
-        if (!last)
-          read_b(fb[(j + 1) & 1], cur, j + 1 < NB ? s : s + 1, j + 1 < NB ? j + 1 : 0);
-        else if (MORE)
-          read_b(fb[0], nxt, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);  // the reads go out ahead of this block's MFMAs
-        acc[0][j] = x6::mfma6(x6::Parts{fa[pa][0], fa[pa][1], fa[pa][2]},
-                              x6::Parts{fb[j & 1][0], fb[j & 1][1], fb[j & 1][2]}, acc[0][j]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  };
-  using T_ = std::true_type;
-  using F_ = std::false_type;
-  using P0 = std::integral_constant<int, 0>;
-  using P1 = std::integral_constant<int, 1>;
-  if constexpr (T % 2 == 0) {
-    int kt = 0;
-    for (; kt + 1 < KT; ++kt) ktile(kt, P0{}, T_{});
-    ktile(kt, P0{}, F_{});
-  } else {
-    int kt = 0;
-    for (; kt + 2 < KT; kt += 2) {
-      ktile(kt, P0{}, T_{});
-      ktile(kt + 1, P1{}, T_{});
-    }
-    if (kt + 1 < KT) {
-      ktile(kt, P0{}, T_{});
-      ktile(kt + 1, P1{}, F_{});
-    } else {
-      ktile(kt, P0{}, F_{});
-    }
   }
-  }  // VL
   conv_epilogue_nchw<1, NB>(acc, P, ep, m0 + 32 * wr, n0 + wc * 32 * NB, lr, lh);
   if (yoct != nullptr) {
     // the output's channel-octet companion (the next convolution's input,
@@ -714,223 +575,6 @@ __global__ void __launch_bounds__(256) k_conv_cb_pack_x6(const float* __restrict
 
 
 // ---------------------------------------------------------------------------
-// k_conv_wide_x6: a large-kernel, strided, unpadded convolution with few input
-// channels (AlexNet conv1: 3 x 11 x 11, stride 4, 96 filters) on the bf16x6
-// engine.  All input channels of a 256-position tile stay resident in LDS as
-// whole input rows (one contiguous block per image segment and channel,
-// copied by 16-byte LDS-DMA), so the im2col view is read from LDS with
-// immediate offsets; the pre-split weights stream through a 3-slot LDS ring,
-// one MFMA group (16 k) per slot.  Tile = 96 filters x 256 positions; wave w
-// owns all 96 rows x positions 64 w .. 64 w + 63.
-// K order: lane half h takes kernel rows 6h .. 6h + 5 (row 11 is a zero
-// weight row), item s = 8 g + j of group g is channel s / (6 KW), kernel row
-// 6h + (s / KW) % 6, column s % KW; so the two halves differ by a constant
-// 6 input rows and every B read is (channel base) + immediate.
-namespace wx6 {
-constexpr int BM = 96, BN = 256, NSLOT = 3;
-constexpr int SLOT_ROW = 112;                  // bytes per weight row of a group: [h][term][8 bf16] + pad (7 quads)
-constexpr int SLOT_B = BM * SLOT_ROW;          // 10752
-constexpr int SLOT_DMA = 3;                    // 1 KB pieces per wave per slot (12 KB >= SLOT_B)
-constexpr int SLOT_REGB = SLOT_DMA * 4 * 1024;
-template <int KH, int KW, int C>
-struct Shape {
-  static constexpr int HR = (KH + 1) / 2;      // kernel rows per lane half
-  static constexpr int S = C * HR * KW;        // items per half
-  static constexpr int G = (S + 7) / 8;        // MFMA groups
-};
-}  // namespace wx6
-
-// GA: the weight fragments come from L2 straight into registers two groups
-// ahead (wpack in fragment order, k_conv_wide_pack_ga_x6): no LDS ring, no
-// barrier in the loop (the patch is loaded once per tile); else the 3-slot
-// LDS ring with one barrier per group.
-template <int KH, int KW, int ST, int C, int PFL, bool GA>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
-k_conv_wide_x6(Params P, const uint16_t* __restrict__ wpack, int CHS) {
-  using namespace g2;
-  using Sh = wx6::Shape<KH, KW, C>;
-  constexpr int G = Sh::G, MI = 3;
-  constexpr int PATCH_B = PFL * 4;
-  constexpr int RING_B = GA ? 0 : wx6::NSLOT * wx6::SLOT_REGB;
-  static_assert(PATCH_B + RING_B <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) char smem[PATCH_B + RING_B];
-  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem));
-  const float* patch = reinterpret_cast<const float*>(smem);
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lr = lane & 31, lh = lane >> 5;
-  // XCD-grouped tile order
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, loc = bid >> 3;
-  const int q8 = nwg >> 3, r8 = nwg & 7;
-  const int tn = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
-  const int n0 = tn * wx6::BN;
-
-  const ConvGeom& cv = P.cv;
-  const int HW = cv.howo.d, OW = cv.wo_div.d, W = cv.W;
-  // image segments of positions n0 .. plast (<= 2): output rows f_s .. l_s,
-  // input rows f_s ST .. f_s ST + R_s - 1 (R_s = (l_s - f_s) ST + 2 HR)
-  const int plast = min(n0 + wx6::BN, P.N) - 1;
-  const int img0 = n0 / HW, img1 = plast / HW;
-  const int f0 = (n0 - img0 * HW) / OW;
-  const int l0 = img1 == img0 ? (plast - img0 * HW) / OW : cv.Ho - 1;
-  const int l1 = (plast - img1 * HW) / OW;
-  const int len0 = ((l0 - f0) * ST + 2 * Sh::HR) * W;
-  const int len1 = img1 == img0 ? 0 : (l1 * ST + 2 * Sh::HR) * W;
-  const int sb1 = (len0 + 255) / 256 * 256;    // LDS float offset of segment 1 in a channel block
-  const int np0 = (len0 + 255) / 256, np1 = (len1 + 255) / 256;
-  const int npc = np0 + np1;                   // 1 KB pieces per channel
-  const int4v xrsrc = make_rsrc(P.b.p, static_cast<uint32_t>(cv.in_bytes));
-  // patch DMA: piece p of channel c, spread over the waves
-  for (int q = wave; q < C * npc; q += 4) {
-    const int c = q / npc, p = q - c * npc;
-    const bool s1 = p >= np0;
-    const int pp = s1 ? p - np0 : p;
-    const int len = s1 ? len1 : len0;
-    const int64_t g0 = ((int64_t)((s1 ? img1 : img0) * C + c) * cv.H + (s1 ? 0 : f0 * ST)) * W;
-    const int e = pp * 256 + lane * 4;
-    const uint32_t off = e < len ? static_cast<uint32_t>((g0 + e) * 4) : 0x80000000u;
-    dma_b128(xrsrc, off, lds0 + static_cast<uint32_t>((c * CHS + (s1 ? sb1 : 0) + pp * 256) * 4));
-  }
-  // per-lane B bases: column j of this wave, channel c (floats)
-  int bb[2][C];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int n = min(n0 + wave * 64 + j * 32 + lr, plast);
-    const int img = n / HW, sp = n - img * HW;
-    const int oh = sp / OW, ow = sp - oh * OW;
-    const int pr = img == img0 ? (oh - f0) * ST : oh * ST;
-    const int pb = (img == img0 ? 0 : sb1) + (pr + lh * Sh::HR) * W + ow * ST;
-#pragma unroll
-    for (int c = 0; c < C; ++c) bb[j][c] = pb + c * CHS;
-  }
-  // weight ring: group g in slot g % NSLOT
-  const int4v arsrc = make_rsrc(reinterpret_cast<const float*>(wpack), static_cast<uint32_t>(G * wx6::SLOT_B));
-  auto issue_a = [&](int g) {
-    const uint32_t img = lds0 + static_cast<uint32_t>(PATCH_B + (g % wx6::NSLOT) * wx6::SLOT_REGB);
-#pragma unroll
-    for (int i = 0; i < wx6::SLOT_DMA; ++i) {
-      const int f = ((wave * wx6::SLOT_DMA + i) * 64 + lane) * 16;
-      const uint32_t off = f < wx6::SLOT_B ? static_cast<uint32_t>(g * wx6::SLOT_B + f) : 0x80000000u;
-      dma_b128(arsrc, off, img + static_cast<uint32_t>((wave * wx6::SLOT_DMA + i) * 1024));
-    }
-  };
-
-  floatx16 acc[MI][2];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-
-  x6::bf16x8 fa[MI][3];  // single-buffered weight fragments (see k_conv_patch_x6)
-  struct Fr {
-    float b[2][8];
-    x6::Parts bp[2];
-  };
-  auto read_a = [&](int g, int i) {
-    const char* p = smem + PATCH_B + (g % wx6::NSLOT) * wx6::SLOT_REGB + (i * 32 + lr) * wx6::SLOT_ROW + lh * 48;
-#pragma unroll
-    for (int t = 0; t < 3; ++t) fa[i][t] = *reinterpret_cast<const x6::bf16x8*>(p + 16 * t);
-  };
-  auto read_b = [&](Fr& F, int g) {
-#pragma unroll
-    for (int jj = 0; jj < 8; ++jj) {
-      const int sx = 8 * g + jj;
-      if (sx < Sh::S) {
-        const int c = sx / (Sh::HR * KW), r = (sx / KW) % Sh::HR, kw = sx % KW;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) F.b[j][jj] = patch[bb[j][c] + r * W + kw];
-      } else {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) F.b[j][jj] = 0.0f;
-      }
-    }
-  };
-
-  Fr F[2];
-  if constexpr (GA) {
-    // fragment (g, i, t) of this lane at ((g MI + i) 3 + t) 64 + lane (16-byte units)
-    const x6::bf16x8* ap = reinterpret_cast<const x6::bf16x8*>(wpack) + lane;
-    x6::bf16x8 fg[3][MI][3];
-    auto load_a = [&](x6::bf16x8 (&f)[MI][3], int g) {
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int t = 0; t < 3; ++t) f[i][t] = ap[((g * MI + i) * 3 + t) * 64];
-    };
-    load_a(fg[0], 0);
-    load_a(fg[1], 1);
-    wait_vm<0>();
-    __builtin_amdgcn_s_barrier();
-    read_b(F[0], 0);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) x6::split8(F[0].b[j], F[0].bp[j]);
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      Fr& fc = F[g & 1];
-      Fr& fn = F[(g + 1) & 1];
-      const bool rd = g + 1 < G;
-      if (g + 2 < G) load_a(fg[(g + 2) % 3], g + 2);
-      constexpr int NB = 2 * MI;
-#pragma unroll
-      for (int q = 0; q < NB; ++q) {
-        const int i = q >> 1, j = q & 1;
-        const auto& fa_ = fg[g % 3][i];
-        acc[i][j] = x6::mfma6(x6::Parts{fa_[0], fa_[1], fa_[2]}, fc.bp[j], acc[i][j]);
-        if (rd) {
-          if (q == 0) read_b(fn, g + 1);
-          if (q == NB - 2) x6::split8(fn.b[0], fn.bp[0]);
-          if (q == NB - 1) x6::split8(fn.b[1], fn.bp[1]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  } else {
-    issue_a(0);
-    issue_a(1);
-    wait_vm<0>();
-    __builtin_amdgcn_s_barrier();
-  #pragma unroll
-    for (int i = 0; i < MI; ++i) read_a(0, i);
-    read_b(F[0], 0);
-  #pragma unroll
-    for (int j = 0; j < 2; ++j) x6::split8(F[0].b[j], F[0].bp[j]);
-    // group g: slot of g + 1 is visible (wait + barrier; every wave is then also
-    // done with group g - 1's slot, which the DMA of group g + 2 overwrites)
-  #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      Fr& fc = F[g & 1];
-      Fr& fn = F[(g + 1) & 1];
-      const bool rd = g + 1 < G;
-      if (g > 0 && rd) {
-        wait_vm<0>();
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (g + 2 < G) issue_a(g + 2);
-      constexpr int NB = 2 * MI;
-  #pragma unroll
-      for (int q = 0; q < NB; ++q) {
-        const int i = q >> 1, j = q & 1;
-        acc[i][j] = x6::mfma6(x6::Parts{fa[i][0], fa[i][1], fa[i][2]}, fc.bp[j], acc[i][j]);
-        if (rd) {
-          if (q == 0) read_b(fn, g + 1);
-          if (j == 1) read_a(g + 1, i);
-          if (q == NB - 2) x6::split8(fn.b[0], fn.bp[0]);
-          if (q == NB - 1) x6::split8(fn.b[1], fn.bp[1]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  }
-  conv_epilogue_nchw<MI, 2>(acc, P, P.e, 0, n0 + wave * 64, lr, lh);
-}
-
-// ---------------------------------------------------------------------------
 // k_conv1_ring_x6: AlexNet conv1 (3 x 11 x 11, stride 4, 227 x 227 input, 96
 // filters) as a persistent kernel whose input is split ONCE per element and
 // whose B fragments are plain 8-byte LDS reads.
@@ -989,7 +633,7 @@ constexpr int quad_off(int qi) {
 }
 }  // namespace c1x6
 
-template <int W, int DIAG = 0>
+template <int W>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img, int tiles) {
   using namespace c1x6;
@@ -1170,7 +814,7 @@ k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img,
       constexpr int g = decltype(gc)::value;
       x6::Parts (&fc)[2] = F[g & 1];
       x6::Parts (&fn)[2] = F[(g + 1) & 1];
-      if (g + 2 < G && !(DIAG & 1)) load_a(fg[(g + 2) % 3], g + 2);
+      if (g + 2 < G) load_a(fg[(g + 2) % 3], g + 2);
       // slot refills (see the header): channel 2 of this tile at groups 1, 3, 5;
       // channel 0 / 1 of the next tile two, four and six groups after their last reader
       auto refill = [&](int u) __attribute__((always_inline)) {
@@ -1187,13 +831,11 @@ k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img,
         const auto& fa = fg[g % 3][i];
         ac[i][j] = x6::mfma6(x6::Parts{fa[0], fa[1], fa[2]}, fc[j], ac[i][j]);
         // the next group's B fragment part q under MFMA6 block q
-        if (g + 1 < G && !(DIAG & 8)) read_part(fn, g + 1, q);
-        if (!(DIAG & 4)) {
-          if (q == 1) refill(0);
-          if (q == 4) refill(1);
-        }
+        if (g + 1 < G) read_part(fn, g + 1, q);
+        if (q == 1) refill(0);
+        if (q == 4) refill(1);
         // the previous tile's outputs: groups 0 .. 11, 8 values per group
-        if (g < 12 && q == 3 && !(DIAG & 2)) store_part(ap_, g);
+        if (g < 12 && q == 3) store_part(ap_, g);
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
@@ -1233,33 +875,6 @@ k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img,
   }
 }
 
-// Weight repack for k_conv_wide_x6<GA = true>: w [M][C][KH][KW] -> fragments
-// [G][3 row blocks][3 terms][64 lanes][8 bf16]; lane (lr, h) of fragment
-// (g, i): row 32 i + lr, items 8 g + j of half h (same K order as below).
-__global__ void __launch_bounds__(256) k_conv_wide_pack_ga_x6(const float* __restrict__ w, char* __restrict__ out,
-                                                              int M, int C, int KH, int KW, int HR, int S, int units) {
-  for (int u = blockIdx.x * blockDim.x + threadIdx.x; u < units; u += gridDim.x * blockDim.x) {
-    const int lane = u & 63, i = (u >> 6) % 3, g = (u >> 6) / 3;
-    const int row = 32 * i + (lane & 31), h = lane >> 5;
-    float v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int sx = 8 * g + j;
-      v[j] = 0.0f;
-      if (sx < S && row < M) {
-        const int c = sx / (HR * KW), kh = h * HR + (sx / KW) % HR, kw = sx % KW;
-        if (kh < KH) v[j] = w[(((int64_t)row * C + c) * KH + kh) * KW + kw];
-      }
-    }
-    x6::Parts t;
-    x6::split8_safe(v, t);
-    char* f = out + (int64_t)(u >> 6) * 3072 + lane * 16;
-    *reinterpret_cast<x6::bf16x8*>(f) = t.h;
-    *reinterpret_cast<x6::bf16x8*>(f + 1024) = t.m;
-    *reinterpret_cast<x6::bf16x8*>(f + 2048) = t.l;
-  }
-}
-
 // Weight repack for k_conv1_ring_x6: w [M][3][11][11] -> fragments
 // [27 groups][3 row blocks][3 terms][64 lanes][8 bf16]; lane (lr, h) of
 // fragment (g, i): row 32 i + lr, items j of half h = quads 2 g, 2 g + 1 in
@@ -1284,28 +899,6 @@ __global__ void __launch_bounds__(256) k_conv1_pack_x6(const float* __restrict__
     *reinterpret_cast<x6::bf16x8*>(f) = t.h;
     *reinterpret_cast<x6::bf16x8*>(f + 1024) = t.m;
     *reinterpret_cast<x6::bf16x8*>(f + 2048) = t.l;
-  }
-}
-
-// Weight repack for k_conv_wide_x6: w [M][C][KH][KW] -> bf16 terms [G][96][SLOT_ROW/2]
-__global__ void __launch_bounds__(256) k_conv_wide_pack_x6(const float* __restrict__ w, uint16_t* __restrict__ out,
-                                                           int M, int C, int KH, int KW, int HR, int S, int64_t total) {
-  constexpr int RLH = wx6::SLOT_ROW / 2;
-  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    const int col = static_cast<int>(idx % RLH);
-    const int row = static_cast<int>((idx / RLH) % wx6::BM);
-    const int g = static_cast<int>(idx / ((int64_t)RLH * wx6::BM));
-    uint16_t v = 0;
-    if (col < 48 && row < M) {
-      const int h = col / 24, p = (col - h * 24) / 8, j = col & 7;
-      const int sx = 8 * g + j;
-      if (sx < S) {
-        const int c = sx / (HR * KW), kh = h * HR + (sx / KW) % HR, kw = sx % KW;
-        if (kh < KH) v = x6::split_term(w[(((int64_t)row * C + c) * KH + kh) * KW + kw], p);
-      }
-    }
-    out[idx] = v;
   }
 }
 
@@ -1606,40 +1199,18 @@ int launch_patch_x6(Params P, const uint16_t* wpack, int PW, int CS, int gz, hip
 }
 
 
-// ---- k_conv_wide_x6 (AlexNet conv1 shape family) ----
-constexpr int WIDE_PFL = 3 * 9728;  // patch floats (3 channels x the largest block pair)
-struct WidePlan {
-  int CHS;
-};
-bool conv_wide_plan(const rram_conv_desc* d, WidePlan& pl) {
-  if (d->group != 1 || d->channels != 3 || d->kernel_h != 11 || d->kernel_w != 11 || d->stride_h != 4 ||
-      d->stride_w != 4 || d->pad_h != 0 || d->pad_w != 0 || d->dilation_h != 1 || d->dilation_w != 1)
-    return false;
-  if (d->num_output > wx6::BM) return false;
-  const int HW = d->out_h * d->out_w, OW = d->out_w, N = d->num * HW;
-  if (HW < wx6::BN) return false;
-  if ((int64_t)d->num * d->channels * d->height * d->width * 4 >= (1ll << 31)) return false;
-  const int HR = 6;
-  int chs = 0;
-  for (int n0 = 0; n0 < N; n0 += wx6::BN) {
-    const int pl_ = std::min(n0 + wx6::BN, N) - 1;
-    const int i0 = n0 / HW, i1 = pl_ / HW;
-    const int f0 = (n0 - i0 * HW) / OW;
-    const int l0 = i1 == i0 ? (pl_ - i0 * HW) / OW : d->out_h - 1;
-    const int len0 = ((l0 - f0) * 4 + 2 * HR) * d->width;
-    const int len1 = i1 == i0 ? 0 : ((pl_ - i1 * HW) / OW * 4 + 2 * HR) * d->width;
-    chs = std::max(chs, (len0 + 255) / 256 * 256 + (len1 + 255) / 256 * 256);
-  }
-  pl.CHS = chs;
-  return 3 * chs <= WIDE_PFL;
+// ---- k_conv1_ring_x6 (AlexNet conv1: 3 x 227 x 227, 96 x 11 x 11, stride 4) ----
+bool conv1_ring_ok(const rram_conv_desc* d) {
+  return d->group == 1 && d->channels == 3 && d->kernel_h == 11 && d->kernel_w == 11 && d->stride_h == 4 &&
+         d->stride_w == 4 && d->pad_h == 0 && d->pad_w == 0 && d->dilation_h == 1 && d->dilation_w == 1 &&
+         d->width == 227 && d->height >= 11 && d->num_output == c1x6::BM && d->num > 0 &&
+         (int64_t)d->num * 3 * d->height * d->width * 4 < (1ll << 31);
 }
 
 int conv_wide_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const float* bias, float* y, int relu,
                      hipStream_t s, const WPack& wk) {
-  WidePlan pl;
-  if (!conv_wide_plan(d, pl)) return 0;
+  if (!conv1_ring_ok(d)) return 0;
   if ((reinterpret_cast<uintptr_t>(w) & 3u) != 0) return 0;
-  using Sh = wx6::Shape<11, 11, 3>;
   const int HW = d->out_h * d->out_w;
   Params P{};
   P.M = d->num_output;
@@ -1663,73 +1234,27 @@ int conv_wide_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, co
   P.e = make_epi(y, HW, 1.0f, 0.0f, bias, RRAM_BIAS_ROW, relu);
   P.e.cimg = (int64_t)d->num_output * HW;
   P.e.hw = make_fastdiv(HW);
-  // RRAM_WIDE_GA = 0: the LDS weight ring (A/B switch)
-  static const bool ga = [] {
-    const char* e = getenv("RRAM_WIDE_GA");
-    return !(e && atoi(e) == 0);
-  }();
-  const int64_t total = (int64_t)Sh::G * wx6::BM * (wx6::SLOT_ROW / 2);
-  const int64_t gunits = (int64_t)Sh::G * 3 * 64;  // GA: 3 KB fragments
-  const int64_t qunits = (int64_t)c1x6::G * 3 * 64;  // the ring kernel's fragments
-  // the persistent conv1 kernel (default; RRAM_WIDE_V1=1 selects the per-tile kernel for A/B)
-  static const bool v1 = [] {
-    const char* e = getenv("RRAM_WIDE_V1");
-    return e && atoi(e) == 1;
-  }();
-  const bool ring = ga && !v1 && d->width == 227 && d->height >= 11 && d->num_output == c1x6::BM;
-  const size_t wbytes = static_cast<size_t>(ring ? qunits * 48 : ga ? gunits * 48 : total * 2);
+  const int units = c1x6::G * 3 * 64;  // 3 KB fragments
+  const size_t wbytes = static_cast<size_t>(units) * 48;
   if (wk.query) {
     *wk.query = wbytes;
     return 1;
   }
-  uint16_t* wp = reinterpret_cast<uint16_t*>(wk.p ? wk.p : pack_buffer((wbytes + 3) / 4, s));
+  char* wp = static_cast<char*>(wk.p ? wk.p : pack_buffer((wbytes + 3) / 4, s));
   RRAM_REQUIRE(wp != nullptr, "conv: packed-weight buffer allocation failed");
-  if (ring) {
-    const int units1 = c1x6::G * 3 * 64;
-    if (!wk.valid) {
-      hipLaunchKernelGGL(k_conv1_pack_x6, dim3(stream_blocks(units1)), dim3(256), 0, s, w, reinterpret_cast<char*>(wp),
-                         d->num_output, units1);
-      const int rc = launch_status("conv1 weight pack x6");
-      if (rc) return rc;
-    }
-    int rc = 0;
-    const int tpi = (HW + c1x6::BN - 1) / c1x6::BN;
-    const int tiles = d->num * tpi;
-    int cus = 256;
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
-    const unsigned nwg1 = static_cast<unsigned>(std::min(tiles, cus));
-    static const int diag = [] {
-      const char* e = getenv("RRAM_C1_DIAG");
-      return e ? atoi(e) : 0;
-    }();
-    switch (diag) {
-      case 1: hipLaunchKernelGGL((k_conv1_ring_x6<227, 1>), dim3(nwg1), dim3(256), 0, s, P, wp, tpi, tiles); break;
-      case 2: hipLaunchKernelGGL((k_conv1_ring_x6<227, 2>), dim3(nwg1), dim3(256), 0, s, P, wp, tpi, tiles); break;
-      case 4: hipLaunchKernelGGL((k_conv1_ring_x6<227, 4>), dim3(nwg1), dim3(256), 0, s, P, wp, tpi, tiles); break;
-      case 8: hipLaunchKernelGGL((k_conv1_ring_x6<227, 8>), dim3(nwg1), dim3(256), 0, s, P, wp, tpi, tiles); break;
-      case 15: hipLaunchKernelGGL((k_conv1_ring_x6<227, 15>), dim3(nwg1), dim3(256), 0, s, P, wp, tpi, tiles); break;
-      default: hipLaunchKernelGGL((k_conv1_ring_x6<227>), dim3(nwg1), dim3(256), 0, s, P, wp, tpi, tiles);
-    }
-    rc = launch_status("conv1 ring x6");
-    return rc ? rc : 1;
-  }
-  int rc = 0;
   if (!wk.valid) {
-    if (ga)
-      hipLaunchKernelGGL(k_conv_wide_pack_ga_x6, dim3(stream_blocks(gunits)), dim3(256), 0, s, w,
-                         reinterpret_cast<char*>(wp), d->num_output, 3, 11, 11, Sh::HR, Sh::S, static_cast<int>(gunits));
-    else
-      hipLaunchKernelGGL(k_conv_wide_pack_x6, dim3(stream_blocks(total)), dim3(256), 0, s, w, wp, d->num_output, 3, 11,
-                         11, Sh::HR, Sh::S, total);
-    rc = launch_status("conv wide weight pack x6");
+    hipLaunchKernelGGL(k_conv1_pack_x6, dim3(stream_blocks(units)), dim3(256), 0, s, w, wp, d->num_output, units);
+    const int rc = launch_status("conv1 weight pack x6");
     if (rc) return rc;
   }
-  const unsigned nwg = static_cast<unsigned>((P.N + wx6::BN - 1) / wx6::BN);
-  if (ga)
-    hipLaunchKernelGGL((k_conv_wide_x6<11, 11, 4, 3, WIDE_PFL, true>), dim3(nwg), dim3(256), 0, s, P, wp, pl.CHS);
-  else
-    hipLaunchKernelGGL((k_conv_wide_x6<11, 11, 4, 3, WIDE_PFL, false>), dim3(nwg), dim3(256), 0, s, P, wp, pl.CHS);
-  rc = launch_status("conv wide x6");
+  const int tpi = (HW + c1x6::BN - 1) / c1x6::BN;
+  const int tiles = d->num * tpi;
+  int cus = 256;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+  const unsigned nwg = static_cast<unsigned>(std::min(tiles, cus));
+  hipLaunchKernelGGL((k_conv1_ring_x6<227>), dim3(nwg), dim3(256), 0, s, P, reinterpret_cast<const uint16_t*>(wp),
+                     tpi, tiles);
+  const int rc = launch_status("conv1 ring x6");
   return rc ? rc : 1;
 }
 
@@ -1794,22 +1319,6 @@ int pack_octets(const float* x, void* oct, int num, int C, int HWi, hipStream_t 
 }
 
 // ---- k_conv_cb_x6 (channel-octet pre-split activations) ----
-// RRAM_CB_VL = 0: the LDS-DMA weight ring (A/B switch of k_conv_cb_x6's VL)
-bool cb_vl() {
-  static const bool on = [] {
-    const char* e = getenv("RRAM_CB_VL");
-    return !(e && atoi(e) == 0);
-  }();
-  return on;
-}
-// RRAM_CONV_CB = 0 leaves these shapes to k_conv_patch_x6 (A/B switch)
-bool conv_cb_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("RRAM_CONV_CB");
-    return !(e && atoi(e) == 0);
-  }();
-  return on;
-}
 struct CbPlan {
   int WR, NB, RPC, PD, octb, tiles_m, tiles_n;
 };
@@ -1840,16 +1349,10 @@ bool conv_cb_plan(const rram_conv_desc* d, CbPlan& pl) {
   // tile (WR, NB) with the least makespan (rounds of 256 workgroups x tile
   // area); ties: taller tiles (weights fetched by one wave)
   static const int cfg[3][2] = {{4, 8}, {4, 4}, {2, 4}};
-  // RRAM_CB_CFG = "WR,NB": only that tile (A/B knob)
-  static const int force = [] {
-    const char* e = getenv("RRAM_CB_CFG");
-    int wr = 0, nb = 0;
-    return e && sscanf(e, "%d,%d", &wr, &nb) == 2 ? wr * 100 + nb : 0;
-  }();
+  // (the other tiles per layer measured slower: profiles/r02_ab_cb_cfg.txt)
   int64_t best = -1;
   for (const auto& c : cfg) {
     const int WR = c[0], NB = c[1], BM = 32 * WR, BN = 32 * NB * (4 / WR);
-    if (force != 0 && force != WR * 100 + NB) continue;
     const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
     if ((tiles_m * BM - M) * 4 > tiles_m * BM) continue;  // > 1/4 padded rows
     const int rmax = patch_rows(N, HW, OW, OH, KH, BN, 3);
@@ -1873,7 +1376,6 @@ bool conv_cb_plan(const rram_conv_desc* d, CbPlan& pl) {
 
 int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, const float* w, const float* bias,
                    float* y, void* y_oct, int relu, hipStream_t s, const WPack& wk) {
-  if (!conv_cb_enabled()) return 0;
   CbPlan pl;
   if (!conv_cb_plan(d, pl)) return 0;
   if (y_oct != nullptr && d->num_output % 8 != 0) return 0;
@@ -1943,12 +1445,7 @@ int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, c
   const uint32_t xrange = static_cast<uint32_t>(xbytes);  // whole packed input (the kernel narrows it per group)
 #define RRAM_X(kh, wr, nb, pd)                                                                                \
   if (KH == kh && pl.WR == wr && pl.NB == nb && pl.PD == pd) {                                                \
-    if (cb_vl())                                                                                             \
-      hipLaunchKernelGGL((k_conv_cb_x6<kh, kh, wr, nb, pd, true>), dim3(nwg), dim3(256), 0, s, P, wp, xp, pl.octb,  \
-                         pl.RPC, xrange, ximg, static_cast<char*>(y_oct_k), d->num_output / 8,                 \
-                         make_fastdiv(static_cast<uint32_t>(pl.octb >> 4)), make_fastdiv(static_cast<uint32_t>(pl.RPC))); \
-    else                                                                                                     \
-    hipLaunchKernelGGL((k_conv_cb_x6<kh, kh, wr, nb, pd, false>), dim3(nwg), dim3(256), 0, s, P, wp, xp, pl.octb, pl.RPC, \
+    hipLaunchKernelGGL((k_conv_cb_x6<kh, kh, wr, nb, pd>), dim3(nwg), dim3(256), 0, s, P, wp, xp, pl.octb, pl.RPC, \
                        xrange, ximg, static_cast<char*>(y_oct_k), d->num_output / 8,                          \
                        make_fastdiv(static_cast<uint32_t>(pl.octb >> 4)), make_fastdiv(static_cast<uint32_t>(pl.RPC))); \
   } else
@@ -2080,13 +1577,9 @@ bool gemm_x6_plan(int M, int N, int K, size_t ws_bytes, GemmPlan& pl) {
   }
   pl.ktc = (pl.ktiles + split - 1) / split;
   pl.split = (pl.ktiles + pl.ktc - 1) / pl.ktc;
-  // under ~half of the CUs busy: the fp32 kernel's smaller tiles fill more
-  // (RRAM_X6_GEMM_MINWG overrides the bound for A/B)
-  static const int min_wg = [] {
-    const char* e = getenv("RRAM_X6_GEMM_MINWG");
-    return e ? atoi(e) : 192;
-  }();
-  if (tiles * pl.split < min_wg) return false;
+  // under ~3/4 of the CUs busy the fp32 kernel's smaller tiles fill more
+  // (fc8 at 128 workgroups: 38 us here vs 35 on fp32, profiles/r02_ab_fc8_x6.txt)
+  if (tiles * pl.split < 192) return false;
   return (int64_t)pl.tiles_m * pl.ktiles * BMc * gx6::RLB < (1ll << 31);
 }
 
@@ -2149,11 +1642,10 @@ extern "C" {
 int rram_f32_engine_for_conv(const rram_conv_desc* d) {
   RRAM_REQUIRE(d != nullptr, "engine query: desc is NULL");
   rram::ConvPlan pl;
-  rram::WidePlan wpl;
   rram::CbPlan cpl;
   return rram::f32_engine().load() == RRAM_ENGINE_BF16X6 &&
-                 (rram::conv_x6_plan(d, pl) || rram::conv_wide_plan(d, wpl) ||
-                  (rram::conv_cb_enabled() && rram::conv_cb_plan(d, cpl)))
+                 (rram::conv_x6_plan(d, pl) || rram::conv1_ring_ok(d) ||
+                  rram::conv_cb_plan(d, cpl))
              ? RRAM_ENGINE_BF16X6
              : RRAM_ENGINE_F32;
 }
@@ -2161,8 +1653,7 @@ int rram_f32_engine_for_conv(const rram_conv_desc* d) {
 int rram_conv_input_octets(const rram_conv_desc* d) {
   RRAM_REQUIRE(d != nullptr, "octet query: desc is NULL");
   rram::CbPlan cpl;
-  return rram::f32_engine().load() == RRAM_ENGINE_BF16X6 && rram::conv_cb_enabled() && rram::conv_cb_plan(d, cpl) ? 1
-                                                                                                                  : 0;
+  return rram::f32_engine().load() == RRAM_ENGINE_BF16X6 && rram::conv_cb_plan(d, cpl) ? 1 : 0;
 }
 
 int rram_pack_octets(const float* x, void* oct, int num, int channels, int height, int width, rram_stream_t s) {

@@ -83,14 +83,15 @@ def test_pool_fwd_bwd_vs_autograd(device, method, k, s, p):
 @pytest.mark.parametrize("shape,k,s,p", [((8, 64, 28, 28), 3, 1, 1), ((4, 48, 27, 27), 3, 2, 0),
                                          ((3, 7, 64, 64), 2, 2, 0), ((2, 9, 7, 7), 3, 2, 1)])
 def test_max_pool_plane_kernel_equals_direct(device, shape, k, s, p):
-    """LDS-plane max pool (several planes per block) == the direct kernel, values
-    and argmax mask, bit for bit."""
-    import os
+    """The LDS-plane max pool (several planes per block; 64 x 64 planes take
+    the direct kernel) against MaxPoolForward restated (pooling_layer.cu:11-47:
+    window clipped to the image, -FLT_MAX start, strict ">" in row-major
+    order): values and argmax mask, bit for bit."""
     import torch
     from rramsim import ops
     torch.manual_seed(4)
     x = torch.randn(*shape, device=device)
-    x[0, 0, :3, :3] = 1.0                            # ties: first index wins in both
+    x[0, 0, :3, :3] = 1.0                            # ties: the first index wins
     N, C, H, W = shape
     PH = -(-(H + 2 * p - k) // s) + 1
     PW = -(-(W + 2 * p - k) // s) + 1
@@ -99,20 +100,24 @@ def test_max_pool_plane_kernel_equals_direct(device, shape, k, s, p):
     if (PW - 1) * s >= W + p:
         PW -= 1
     geom = (N, C, H, W, PH, PW, k, k, s, s, p, p)
-    outs = []
-    for direct in (False, True):
-        if direct:
-            os.environ["RRAM_POOL_NO_PLANES"] = "1"
-        try:
-            y = torch.full((N, C, PH, PW), float("nan"), device=device)
-            m = torch.full((N, C, PH, PW), -7, dtype=torch.int32, device=device)
-            ops.pool_fwd(x, y, m, geom, 0)
-            torch.cuda.synchronize()
-            outs.append((y, m))
-        finally:
-            os.environ.pop("RRAM_POOL_NO_PLANES", None)
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
-    torch.testing.assert_close(outs[0][0], _caffe_pool_ref(x, k, s, p, "MAX"), rtol=0, atol=0)
+    y = torch.full((N, C, PH, PW), float("nan"), device=device)
+    m = torch.full((N, C, PH, PW), -7, dtype=torch.int32, device=device)
+    ops.pool_fwd(x, y, m, geom, 0)
+    torch.cuda.synchronize()
+    xs = x.cpu().numpy()
+    ry = np.empty((N, C, PH, PW), np.float32)
+    rm = np.empty((N, C, PH, PW), np.int32)
+    for a in range(PH):
+        for b in range(PW):
+            hs, ws = a * s - p, b * s - p
+            he, we = min(hs + k, H), min(ws + k, W)
+            hs, ws = max(hs, 0), max(ws, 0)
+            win = xs[:, :, hs:he, ws:we].reshape(N, C, -1)
+            i = win.argmax(axis=2)                    # first maximum in row-major order
+            ry[:, :, a, b] = np.take_along_axis(win, i[..., None], 2)[..., 0]
+            rm[:, :, a, b] = (hs + i // (we - ws)) * W + ws + i % (we - ws)
+    np.testing.assert_array_equal(y.cpu().numpy(), ry)
+    np.testing.assert_array_equal(m.cpu().numpy(), rm)
 
 
 def _lrn_across_ref(x, size, alpha, beta, k):
@@ -150,11 +155,14 @@ def test_lrn_across_fwd_bwd_vs_autograd(device, size):
 
 @pytest.mark.parametrize("size,k,s,p,C,H", [(5, 3, 2, 0, 13, 15), (5, 3, 2, 0, 96, 55), (3, 3, 2, 1, 7, 12),
                                              (5, 2, 2, 0, 9, 10), (3, 3, 1, 0, 6, 8), (5, 3, 2, 0, 256, 27),
-                                             (5, 2, 1, 1, 5, 21), (3, 3, 3, 2, 4, 30)])
+                                             (5, 2, 1, 1, 5, 21), (3, 3, 3, 2, 4, 30), (5, 3, 2, 1, 6, 33),
+                                             (3, 3, 2, 0, 10, 64), (5, 3, 2, 0, 8, 70)])
 def test_lrn_maxpool_fused_equals_unfused(device, size, k, s, p, C, H):
     """rram_lrn_maxpool_fwd == rram_lrn_fwd then rram_pool_fwd, bit for bit
     (same LRN arithmetic; window edges of the ceil rule), and the torch fp32
-    reference within the LRN tolerance."""
+    reference within the LRN tolerance.  3 x 3 / stride 2 windows over images
+    up to 64 wide take the register kernel (two segments per wave up to 32
+    wide), the rest and W = 69 the LDS band kernel."""
     import torch
     from rramsim import ops
     torch.manual_seed(9)
