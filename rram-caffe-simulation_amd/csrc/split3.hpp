@@ -15,25 +15,8 @@ typedef float float2v __attribute__((ext_vector_type(2)));
 struct Parts {
   bf16x8 h, m, l;
 };
-// exact three-term split of 8 floats (round to nearest even at each step)
-__device__ __forceinline__ void split8(const float (&x)[8], Parts& r) {
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const float2v v = {x[2 * p], x[2 * p + 1]};
-    const bf16x2 h = __builtin_convertvector(v, bf16x2);
-    const float2v r1 = v - __builtin_convertvector(h, float2v);
-    const bf16x2 m = __builtin_convertvector(r1, bf16x2);
-    const float2v r2 = r1 - __builtin_convertvector(m, float2v);
-    const bf16x2 l = __builtin_convertvector(r2, bf16x2);
-    r.h[2 * p] = h[0];
-    r.h[2 * p + 1] = h[1];
-    r.m[2 * p] = m[0];
-    r.m[2 * p + 1] = m[1];
-    r.l[2 * p] = l[0];
-    r.l[2 * p + 1] = l[1];
-  }
-}
-// The split above is exact for every finite |x| up to the largest bf16
+// The plain split (each term = bf16 round-to-nearest-even of the remainder)
+// is exact for every finite |x| up to the largest bf16
 // (BF16_MAX = 0x1.fep127); past it the high term rounds to Inf, and an Inf
 // operand gives Inf - Inf = NaN in the middle term where the fp32 product the
 // reference forms is +-Inf.  The safe form clamps each term's input to
@@ -43,9 +26,9 @@ __device__ __forceinline__ void split8(const float (&x)[8], Parts& r) {
 //   x = +-Inf                  (+-BF16_MAX, +-BF16_MAX, +-Inf): every product
 //                              with a nonzero operand is +-Inf, with 0 NaN, as in fp32;
 //   NaN                        NaN reaches the low term.
-// The pack kernels (one split per element per call) use it; the in-loop
-// splits of k_conv_patch_x6 and k_gemm_x6 use split8 (their operands: see
-// rram_kernels.h, bf16x6 engine).
+// Every split of the engine uses it (the pack kernels, the conv1 staging and
+// the in-loop splits of k_conv_patch_x6 / k_gemm_x6), so the engine's
+// products of non-finite or > BF16_MAX operands follow fp32's.
 constexpr float kBf16Max = 0x1.fep127f;
 __device__ __forceinline__ float2v clamp_bf16(float2v v) {
   return float2v{__builtin_amdgcn_fmed3f(v[0], -kBf16Max, kBf16Max), __builtin_amdgcn_fmed3f(v[1], -kBf16Max, kBf16Max)};

@@ -206,7 +206,7 @@ k_conv_patch_x6(Params P, const uint16_t* __restrict__ wpack, int PW, int CS) {
   for (int i = 0; i < MI; ++i) read_a(smem, 0, i);
   read_b(F[0], smem, 0);
 #pragma unroll
-  for (int j = 0; j < 2; ++j) x6::split8(F[0].b[j], F[0].bp[j]);
+  for (int j = 0; j < 2; ++j) x6::split8_safe(F[0].b[j], F[0].bp[j]);
 
   // one K-tile; PAR: parity of its first group's fragments; MORE: tile t + 1 exists
   auto tile = [&](int t, auto par_c, auto more_c) {
@@ -239,8 +239,8 @@ k_conv_patch_x6(Params P, const uint16_t* __restrict__ wpack, int PW, int CS) {
         if (rd) {
           if (q == 0) read_b(fn, src, gn);
           if (j == 1) read_a(src, gn, i);
-          if (q == NB - 3) x6::split8(fn.b[0], fn.bp[0]);
-          if (q == NB - 1) x6::split8(fn.b[1], fn.bp[1]);
+          if (q == NB - 3) x6::split8_safe(fn.b[0], fn.bp[0]);
+          if (q == NB - 1) x6::split8_safe(fn.b[1], fn.bp[1]);
         }
         // DMA of tile t + 1 spread over the blocks of groups 0 .. G8-2
         if (!last && MORE) {
@@ -527,6 +527,132 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
       }
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// k_conv_pw_x6: 1 x 1, stride-1, unpadded convolution (GoogLeNet's inception
+// reductions / projections) on the bf16x6 engine: per image a plain GEMM
+// Y[co][p] = W[co][ci] X[ci][p] over the channel-octet companion of X
+// ([n][C/8][HW][3][8] bf16, the pre-split operand form the channel-octet
+// kernel reads) and pre-split weight fragments (k_conv_cb_pack_x6 with one
+// tap; cached across calls by rram_conv2d_fwd_cached).
+// Tile 128 rows x 128 positions (positions run across image boundaries);
+// wave w owns rows 32 w .. + 31 and all 128 positions (4 column blocks), so
+// a B fragment read from LDS feeds one wave and each weight fragment 4
+// blocks.  K runs in groups of 16 channels (lane half h = octet 2 g + h);
+// GPS groups form a stage: the stage's octet planes (128 positions x 48 B x
+// 2 octets per group) are loaded by all threads into registers while the
+// previous stage computes and written to the other LDS buffer before the
+// one barrier per stage.  B reads: ds_read_b128 at a 48-byte lane stride,
+// 16 lanes on 16 disjoint bank quads (3 n mod 16 as in k_conv_cb_x6).
+// Weights come from L2 straight into registers one group ahead.
+namespace pwx6 {
+constexpr int BM = 128, BN = 128, NB = 4, GPS = 3;
+constexpr int GB = BN * 96;                 // LDS bytes per group (2 octets x 128 positions x 48 B)
+constexpr int SB = GPS * GB;                // bytes per stage (36 KB: two workgroups per CU)
+constexpr int CPT = GPS * GB / 16 / 256;    // 16-byte chunks per thread per stage (9)
+static_assert(GPS * GB % (16 * 256) == 0, "chunks");
+}  // namespace pwx6
+
+__global__ void __launch_bounds__(256, 2)
+k_conv_pw_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __restrict__ xoct, uint32_t xbytes,
+             int NG) {
+  using namespace pwx6;
+  __shared__ __attribute__((aligned(16))) char smem[2 * SB];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lr = lane & 31, lh = lane >> 5;
+  // XCD-grouped tile order (as k_conv_cb_x6)
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, loc = bid >> 3;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int tid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const int tm = __builtin_amdgcn_readfirstlane(tid % P.tiles_m);
+  const int tn = __builtin_amdgcn_readfirstlane(tid / P.tiles_m);
+  const int n0 = tn * BN, m0 = tm * BM;
+  const int HW = P.cv.howo.d;
+  const uint32_t PL = static_cast<uint32_t>(HW) * 48u;  // bytes per octet plane of one image
+  const uint32_t img_b = static_cast<uint32_t>(P.cv.C >> 3) * PL;
+  // this thread's staging chunks: chunk c of a stage = (group slot gs, octet h, position pn, term t)
+  uint32_t soff[CPT];  // global byte offset for stage 0 (group g adds 2 g PL)
+  uint32_t loff[CPT];  // LDS byte offset within a stage
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    const int c = threadIdx.x + k * 256;
+    const int gs = c / (BN * 6), rem = c - gs * (BN * 6);
+    const int h = rem / (BN * 3), r2 = rem - h * (BN * 3);
+    const int pn = r2 / 3, t = r2 - pn * 3;
+    const int n = n0 + pn;
+    const uint32_t img = static_cast<uint32_t>(fdiv(static_cast<uint32_t>(min(n, P.N - 1)), P.cv.howo));
+    const uint32_t sp = static_cast<uint32_t>(min(n, P.N - 1)) - img * static_cast<uint32_t>(HW);
+    soff[k] = n < P.N ? img * img_b + static_cast<uint32_t>(2 * gs + h) * PL + sp * 48u + static_cast<uint32_t>(t) * 16u
+                      : 0x80000000u;
+    loff[k] = static_cast<uint32_t>((gs * 2 + h) * BN * 48 + pn * 48 + t * 16);
+  }
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(xoct), 0, static_cast<int>(xbytes), 0x00020000);
+  typedef int int4x __attribute__((ext_vector_type(4)));
+  int4x stg[CPT];
+  // groups past NG load from past the range (zeros) into slots no MFMA reads
+  auto load_stage = [&](int st) __attribute__((always_inline)) {
+    const uint32_t goff = static_cast<uint32_t>(st * GPS) * 2u * PL;
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      const int gs = (threadIdx.x + k * 256) / (BN * 6);
+      const bool ok = st * GPS + gs < NG && soff[k] != 0x80000000u;
+      stg[k] = __builtin_bit_cast(int4x, __builtin_amdgcn_raw_buffer_load_b128(
+                                             xr, static_cast<int>(ok ? soff[k] + goff : 0x80000000u), 0, 0));
+    }
+  };
+  auto store_stage = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) *reinterpret_cast<int4x*>(smem + buf * SB + loff[k]) = stg[k];
+  };
+  // weight fragments of this wave's row block: group g at ap[g * FRAG + t * 64]
+  const x6::bf16x8* ap = wpack + ((int64_t)(tm * 4 + wave) * NG) * cbx6::FRAG + lane;
+  auto load_a = [&](x6::bf16x8 (&f)[3], int g) {
+#pragma unroll
+    for (int t = 0; t < 3; ++t) f[t] = ap[g * cbx6::FRAG + t * 64];
+  };
+  floatx16 acc[1][NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[0][j][r] = 0.0f;
+  const int nst = (NG + GPS - 1) / GPS;
+  x6::bf16x8 fa[2][3];
+  load_stage(0);
+  load_a(fa[0], 0);
+  store_stage(0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int st = 0; st < nst; ++st) {
+    const char* cur = smem + (st & 1) * SB + lh * BN * 48 + lr * 48;
+    const bool more = st + 1 < nst;
+    if (more) load_stage(st + 1);
+#pragma unroll
+    for (int gs = 0; gs < GPS; ++gs) {
+      const int g = st * GPS + gs;
+      if (g >= NG) break;
+      const x6::bf16x8 (&fc)[3] = fa[gs & 1];
+      if (g + 1 < NG) load_a(fa[(gs + 1) & 1], g + 1);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const char* p = cur + gs * 2 * BN * 48 + j * 32 * 48;
+        x6::Parts b;
+        b.h = *reinterpret_cast<const x6::bf16x8*>(p);
+        b.m = *reinterpret_cast<const x6::bf16x8*>(p + 16);
+        b.l = *reinterpret_cast<const x6::bf16x8*>(p + 32);
+        acc[0][j] = x6::mfma6(x6::Parts{fc[0], fc[1], fc[2]}, b, acc[0][j]);
+      }
+    }
+    if (more) {
+      store_stage((st + 1) & 1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+  conv_epilogue_nchw<1, NB>(acc, P, P.e, m0 + 32 * wave, n0, lr, lh);
 }
 
 // x [img][C][H][W] fp32 -> bf16 terms [img][C/8][H][W][3][8] (k_conv_cb_x6's
@@ -1080,7 +1206,7 @@ k_gemm_x6(Params P, const uint16_t* __restrict__ apack, int ktiles_all, int ktc)
   for (int i = 0; i < MI; ++i) read_a(a_st(0), 0, i);
   read_b(F[0], b_st(0), 0);
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) x6::split8(F[0].b[j], F[0].bp[j]);
+  for (int j = 0; j < NJ; ++j) x6::split8_safe(F[0].b[j], F[0].bp[j]);
 
   auto tile = [&](int t, auto more_c) {
     constexpr bool MORE = decltype(more_c)::value;
@@ -1113,7 +1239,7 @@ k_gemm_x6(Params P, const uint16_t* __restrict__ apack, int ktiles_all, int ktc)
           if (j == NJ - 1) read_a(asrc, gn, i);
 #pragma unroll
           for (int jj = 0; jj < NJ; ++jj)
-            if (q == NB - NJ + jj) x6::split8(fn.b[jj], fn.bp[jj]);
+            if (q == NB - NJ + jj) x6::split8_safe(fn.b[jj], fn.bp[jj]);
         }
         if (!last && MORE) {  // A of t + 1, then B of t + 2, spread over the group's blocks
 #pragma unroll
@@ -1456,6 +1582,69 @@ int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, c
   return rc ? rc : 1;
 }
 
+// ---- k_conv_pw_x6 (1 x 1 convolutions) ----
+bool conv_pw_ok(const rram_conv_desc* d) {
+  if (d->kernel_h != 1 || d->kernel_w != 1 || d->stride_h != 1 || d->stride_w != 1 || d->pad_h != 0 ||
+      d->pad_w != 0 || d->group != 1 || d->channels % 16 != 0)
+    return false;
+  const int64_t N = (int64_t)d->num * d->height * d->width;
+  const int64_t tiles = ((d->num_output + pwx6::BM - 1) / pwx6::BM) * ((N + pwx6::BN - 1) / pwx6::BN);
+  // > 1/4 padded rows, or under half of the 512 two-per-CU slots: the fp32
+  // kernel's smaller tiles do better
+  const int mt = (d->num_output + pwx6::BM - 1) / pwx6::BM * pwx6::BM;
+  if ((mt - d->num_output) * 4 > mt || tiles < 256) return false;
+  return N < (1ll << 31) && N * d->channels * 6 < (1ll << 31);
+}
+
+int conv_pw_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, const float* w, const float* bias,
+                   float* y, int relu, hipStream_t s, const WPack& wk) {
+  if (!conv_pw_ok(d)) return 0;
+  const int C = d->channels, M = d->num_output, HW = d->height * d->width, NG = C / 16;
+  const int tiles_m = (M + pwx6::BM - 1) / pwx6::BM;
+  const int64_t wfrags = (int64_t)tiles_m * 4 * NG;  // [row block][group], one tap
+  const size_t wbytes = static_cast<size_t>(wfrags * 3072);
+  if (wk.query) {
+    *wk.query = wbytes;
+    return 1;
+  }
+  const int64_t xbytes = (int64_t)d->num * C * HW * 6;
+  const int64_t xb_al = x_oct != nullptr ? 0 : (xbytes + 255) / 256 * 256;
+  const int64_t scratch = xb_al + (wk.p ? 0 : (int64_t)wbytes);
+  char* buf = scratch > 0 ? reinterpret_cast<char*>(pack_buffer(static_cast<size_t>(scratch / 4), s)) : nullptr;
+  RRAM_REQUIRE(scratch == 0 || buf != nullptr, "conv: packed-operand buffer allocation failed");
+  char* wbuf = wk.p ? static_cast<char*>(wk.p) : buf + xb_al;
+  int rc = 0;
+  if (x_oct == nullptr) {
+    rc = pack_octets(x, buf, d->num, C, HW, s);
+    if (rc) return rc;
+  }
+  if (!wk.valid) {
+    const int wunits = static_cast<int>(wfrags * 64);
+    hipLaunchKernelGGL(k_conv_cb_pack_x6, dim3(stream_blocks(wunits)), dim3(256), 0, s, w, wbuf, M, C, 1,
+                       tiles_m * 4, wunits);
+    rc = launch_status("conv weight pack x6 (1x1)");
+    if (rc) return rc;
+  }
+  Params P{};
+  P.M = M;
+  P.N = d->num * HW;
+  P.K = C;
+  P.split = 1;
+  P.cv.C = C;
+  P.cv.howo = make_fastdiv(HW);
+  P.e = make_epi(y, HW, 1.0f, 0.0f, bias, RRAM_BIAS_ROW, relu);
+  P.e.cimg = (int64_t)M * HW;
+  P.e.hw = make_fastdiv(HW);
+  P.tiles_m = tiles_m;
+  P.tiles_n = (P.N + pwx6::BN - 1) / pwx6::BN;
+  const unsigned nwg = static_cast<unsigned>((int64_t)P.tiles_m * P.tiles_n);
+  const auto* xp = reinterpret_cast<const uint16_t*>(x_oct != nullptr ? x_oct : buf);
+  hipLaunchKernelGGL(k_conv_pw_x6, dim3(nwg), dim3(256), 0, s, P, reinterpret_cast<const x6::bf16x8*>(wbuf), xp,
+                     static_cast<uint32_t>(xbytes), NG);
+  rc = launch_status("conv pw x6");
+  return rc ? rc : 1;
+}
+
 int conv_patch_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const float* bias, float* y, int relu,
                       hipStream_t s, const WPack& wk);
 // The bf16x6 convolution forward.  x_oct: NULL or the octet companion of x
@@ -1472,6 +1661,7 @@ int conv_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, cons
     if (rc != 0) return rc;
   }
   int rc = conv_wide_x6_fwd(d, x, w, bias, y, relu, s, wk);
+  if (rc == 0) rc = conv_pw_x6_fwd(d, x, x_oct, w, bias, y, relu, s, wk);
   if (rc == 0) rc = conv_patch_x6_fwd(d, x, w, bias, y, relu, s, wk);
   if (wk.query) return rc;
   if (rc > 0 && y_oct != nullptr) {
@@ -1644,7 +1834,7 @@ int rram_f32_engine_for_conv(const rram_conv_desc* d) {
   rram::ConvPlan pl;
   rram::CbPlan cpl;
   return rram::f32_engine().load() == RRAM_ENGINE_BF16X6 &&
-                 (rram::conv_x6_plan(d, pl) || rram::conv1_ring_ok(d) ||
+                 (rram::conv_x6_plan(d, pl) || rram::conv1_ring_ok(d) || rram::conv_pw_ok(d) ||
                   rram::conv_cb_plan(d, cpl))
              ? RRAM_ENGINE_BF16X6
              : RRAM_ENGINE_F32;
@@ -1653,7 +1843,8 @@ int rram_f32_engine_for_conv(const rram_conv_desc* d) {
 int rram_conv_input_octets(const rram_conv_desc* d) {
   RRAM_REQUIRE(d != nullptr, "octet query: desc is NULL");
   rram::CbPlan cpl;
-  return rram::f32_engine().load() == RRAM_ENGINE_BF16X6 && rram::conv_cb_plan(d, cpl) ? 1 : 0;
+  return rram::f32_engine().load() == RRAM_ENGINE_BF16X6 && (rram::conv_cb_plan(d, cpl) || rram::conv_pw_ok(d)) ? 1
+                                                                                                               : 0;
 }
 
 int rram_pack_octets(const float* x, void* oct, int num, int channels, int height, int width, rram_stream_t s) {

@@ -221,7 +221,20 @@ void ConvolutionLayer<Dtype>::Forward_gpu(const std::vector<Blob<Dtype>*>& botto
                                           const std::vector<Blob<Dtype>*>& top) {
   CAFFE_CHECK(bottom[0] != top[0], this->name() << ": in-place convolution is not allowed");
   const int shp[4] = {desc_.num, desc_.channels, desc_.height, desc_.width};
-  const void* xo = want_in_oct_ ? bottom[0]->data()->valid_octets(shp) : nullptr;
+  const void* xo = nullptr;
+  if (want_in_oct_) {
+    // the input's companion: written by its producer, else packed here into
+    // the blob's own companion so the other consumers of the same blob (the
+    // inception branches) reuse it instead of each packing a scratch copy
+    SyncedMemory* xm = bottom[0]->data().get();
+    xo = xm->valid_octets(shp);
+    if (xo == nullptr) {
+      void* buf = xm->octets(static_cast<size_t>(bottom[0]->count()) * 6);
+      RRAM_CALL(rram_pack_octets(bottom[0]->gpu_data(), buf, shp[0], shp[1], shp[2], shp[3], Caffe::stream()));
+      xm->set_octets_valid(shp);
+      xo = buf;
+    }
+  }
   float* y = top[0]->mutable_gpu_data();  // invalidates top's companion
   void* yo = octets_for(top[0], kOctConv);
   const float* bias = bias_term_ ? this->blobs_[1]->gpu_data() : nullptr;

@@ -58,4 +58,85 @@ if cnt[("gemm", "FETCH_SIZE")] and cnt[("gemm", "WRITE_SIZE")]:
                    "dispatches_per_step": cnt[("gemm", "FETCH_SIZE")] / forwards,
                    "algorithmic_bytes_per_step": ALG_BYTES,
                    "ratio_to_algorithmic": (fb + wb) / ALG_BYTES}
+
+# ---- per-kernel table: measured vs algorithmic bytes per step ----
+# algorithmic bytes of each AlexNet b256 kernel in the operand form the engine
+# reads (the bf16x6 kernels read pre-split octets: 6 B per element; fp32
+# tensors 4 B), each tensor once; split-K partials and the packs' own outputs
+# count as the bytes they must move
+MB = 1e6
+A1, Y1 = 3*227*227*B*4, 96*55*55*B*4
+P1O, P1Y = 96*27*27*B*6, 96*27*27*B*4
+Y2 = 256*27*27*B*4
+P2O, P2Y = 256*13*13*B*6, 256*13*13*B*4
+Y3 = Y4 = 384*13*13*B*4
+O4 = 384*13*13*B*6
+Y5 = 256*13*13*B*4
+ALG = {  # class: (algorithmic bytes per step, description)
+    "conv1 k_conv1_ring_x6": (A1 + 96*363*4 + Y1, "x fp32 + w + y"),
+    "norm1+pool1 (LRN + max pool, octets)": (Y1 + P1Y + P1O, "x + y + y octets"),
+    "conv2 k_conv_cb_x6<5,5,...>": (P1O + 256*48*25*4 + Y2, "x octets + w + y"),
+    "norm2+pool2 (LRN + max pool, octets)": (Y2 + P2Y + P2O, "x + y + y octets"),
+    "conv3 k_conv_cb_x6<3,3,4,8,...>": (P2O + 384*256*9*4 + Y3, "x octets + w + y"),
+    "conv4/conv5 input packs k_pack_octets_x6": (2 * (Y3 + O4), "2 x (read fp32, write octets)"),
+    "conv4 k_conv_cb_x6<3,3,2,4,...>": (O4 + 384*192*9*4 + Y4, "x octets + w + y"),
+    "conv5 k_conv_cb_x6<3,3,4,4,...>": (O4 + 256*192*9*4 + Y5, "x octets + w + y"),
+    "fc6/fc7 k_gemm_x6 + k_pack_rows_x6": ((9216 + 4096)*B*(4 + 6 + 6) + (4096*9216 + 4096*4096)*4 + 2*4096*B*4,
+                                            "x read + slabs written/read, w, y"),
+    "fc8 k_gemm2": (4096*B*4 + 1000*4096*4 + 1000*B*4, "x + w + y"),
+    "split-K reductions": (0.0, "partials (no algorithmic counterpart)"),
+    "injection k_inject_batched": (8.0 * 58631144, "read clean + write faulted"),
+}
+
+
+def classify(name):
+    if "k_inject_batched" in name:
+        return "injection k_inject_batched"
+    if "k_conv1_ring_x6" in name:
+        return "conv1 k_conv1_ring_x6"
+    if "lrn_maxpool" in name:
+        return None  # split below by grid
+    if "k_conv_cb_x6ILi5ELi5" in name or "k_conv_cb_x6<5, 5" in name:
+        return "conv2 k_conv_cb_x6<5,5,...>"
+    if "k_conv_cb_x6ILi3ELi3ELi4ELi8" in name:
+        return "conv3 k_conv_cb_x6<3,3,4,8,...>"
+    if "k_conv_cb_x6ILi3ELi3ELi2ELi4" in name:
+        return "conv4 k_conv_cb_x6<3,3,2,4,...>"
+    if "k_conv_cb_x6ILi3ELi3ELi4ELi4" in name:
+        return "conv5 k_conv_cb_x6<3,3,4,4,...>"
+    if "k_pack_octets_x6" in name:
+        return "conv4/conv5 input packs k_pack_octets_x6"
+    if "k_gemm_x6" in name or "k_pack_rows_x6" in name:
+        return "fc6/fc7 k_gemm_x6 + k_pack_rows_x6"
+    if "k_gemm2" in name:
+        return "fc8 k_gemm2"
+    if "k_splitk_reduce" in name:
+        return "split-K reductions"
+    return "other"
+
+
+per = defaultdict(float)
+lrn_grids = {}
+for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
+    for r in csv.DictReader(open(f)):
+        name, c = r["Kernel_Name"], r["Counter_Name"]
+        if c not in ("FETCH_SIZE", "WRITE_SIZE"):
+            continue
+        k = classify(name)
+        if k is None:
+            lrn_grids.setdefault(int(r["Grid_Size"]), []).append((c, float(r["Counter_Value"])))
+            continue
+        per[k] += (2 if c == "FETCH_SIZE" else 1) * KIB * float(r["Counter_Value"])
+# the two LRN + pool launches: the larger grid is norm1 / pool1 (96 x 55 x 55 input)
+for i, (gsz, vals) in enumerate(sorted(lrn_grids.items(), reverse=True)):
+    k = "norm1+pool1 (LRN + max pool, octets)" if i == 0 else "norm2+pool2 (LRN + max pool, octets)"
+    per[k] += sum((2 if c == "FETCH_SIZE" else 1) * KIB * v for c, v in vals)
+table = {}
+for k, (alg, what) in ALG.items():
+    meas = per.get(k, 0.0) / forwards
+    table[k] = {"measured_MB_per_step": round(meas / MB, 1), "algorithmic_MB_per_step": round(alg / MB, 1),
+                "ratio": round(meas / alg, 3) if alg else None, "algorithmic": what}
+if per.get("other"):
+    table["other"] = {"measured_MB_per_step": round(per["other"] / forwards / MB, 1)}
+out["per_kernel"] = table
 print(json.dumps(out, indent=1))

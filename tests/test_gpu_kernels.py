@@ -492,11 +492,16 @@ def test_conv_patch_shapes_vs_fp64(device, cs, conv_engine):
 
 # AlexNet conv2 / conv3 / conv4 / conv5 at 4 images (Caffe-filler-like weight scale)
 ENGINE_CASES = [
-    dict(x=(2, 3, 227, 227), cout=96, k=11, p=0, g=1, s=4),    # conv1 (k_conv_wide_x6)
+    dict(x=(2, 3, 227, 227), cout=96, k=11, p=0, g=1, s=4),    # conv1 (k_conv1_ring_x6)
     dict(x=(4, 96, 27, 27), cout=256, k=5, p=2, g=2),
     dict(x=(4, 256, 13, 13), cout=384, k=3, p=1, g=1),
     dict(x=(4, 384, 13, 13), cout=384, k=3, p=1, g=2),
     dict(x=(4, 384, 13, 13), cout=256, k=3, p=1, g=2),
+    # GoogLeNet 1x1 reductions / projections on the pointwise kernel (k_conv_pw_x6)
+    dict(x=(32, 256, 28, 28), cout=128, k=1, p=0, g=1),
+    dict(x=(128, 480, 14, 14), cout=192, k=1, p=0, g=1),
+    dict(x=(256, 832, 7, 7), cout=384, k=1, p=0, g=1),
+    dict(x=(64, 528, 14, 14), cout=160, k=1, p=0, g=1),
 ]
 
 
