@@ -22,7 +22,7 @@ namespace {
 // a*b is accumulated in fp32 as the six terms
 //   al*bh + ah*bl + am*bm + am*bh + ah*bm + ah*bh
 // (v_mfma_f32_32x32x16_bf16: a product of two bf16 is exact in fp32).  The
-// dropped terms am*bl, al*bm, al*bl are below 2^-25 |a*b| with independent
+// dropped terms am*bl, al*bm, al*bl are at most 2^-24, 2^-24, 2^-32 |a*b| with independent
 // signs, under the fp32 rounding of the accumulation itself, so the result
 // carries fp32 accuracy (tests compare it with a float64 evaluation at the
 // same bound as the fp32-MFMA kernels) while a 32x32x16 bf16 MFMA does the
@@ -536,10 +536,10 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
 // ([n][C/8][HW][3][8] bf16, the pre-split operand form the channel-octet
 // kernel reads) and pre-split weight fragments (k_conv_cb_pack_x6 with one
 // tap; cached across calls by rram_conv2d_fwd_cached).
-// Tile 128 rows x 128 positions (positions run across image boundaries);
-// wave w owns rows 32 w .. + 31 and all 128 positions (4 column blocks), so
-// a B fragment read from LDS feeds one wave and each weight fragment 4
-// blocks.  K runs in groups of 16 channels (lane half h = octet 2 g + h);
+// Tile 32 WR rows x 128 (4 / WR) positions (positions run across image
+// boundaries): WR = 4 (128 x 128, two workgroups per CU) or WR = 2 (64 x 256
+// for the 48..64-row reductions); wave w owns rows 32 (w % WR) .. + 31 and
+// 128 positions (4 column blocks), so each weight fragment feeds 4 blocks.  K runs in groups of 16 channels (lane half h = octet 2 g + h);
 // GPS groups form a stage: the stage's octet planes (128 positions x 48 B x
 // 2 octets per group) are loaded by all threads into registers while the
 // previous stage computes and written to the other LDS buffer before the
@@ -547,21 +547,29 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
 // 16 lanes on 16 disjoint bank quads (3 n mod 16 as in k_conv_cb_x6).
 // Weights come from L2 straight into registers one group ahead.
 namespace pwx6 {
-constexpr int BM = 128, BN = 128, NB = 4, GPS = 3;
-constexpr int GB = BN * 96;                 // LDS bytes per group (2 octets x 128 positions x 48 B)
-constexpr int SB = GPS * GB;                // bytes per stage (36 KB: two workgroups per CU)
-constexpr int CPT = GPS * GB / 16 / 256;    // 16-byte chunks per thread per stage (9)
-static_assert(GPS * GB % (16 * 256) == 0, "chunks");
+constexpr int NB = 4, GPS = 3;
+template <int WR>
+struct Tile {
+  static constexpr int BM = 32 * WR, BN = 128 * (4 / WR);
+  static constexpr int GB = BN * 96;               // LDS bytes per group (2 octets x BN positions x 48 B)
+  static constexpr int SB = GPS * GB;              // bytes per stage (WR = 4: 36 KB, two workgroups per CU)
+  static constexpr int CPT = GPS * GB / 16 / 256;  // 16-byte chunks per thread per stage
+  static_assert(GPS * GB % (16 * 256) == 0, "chunks");
+};
 }  // namespace pwx6
 
-__global__ void __launch_bounds__(256, 2)
+template <int WR>
+__global__ void __launch_bounds__(256, WR == 4 ? 2 : 1)
 k_conv_pw_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __restrict__ xoct, uint32_t xbytes,
              int NG) {
   using namespace pwx6;
+  using Tl = Tile<WR>;
+  constexpr int BM = Tl::BM, BN = Tl::BN, SB = Tl::SB, CPT = Tl::CPT;
   __shared__ __attribute__((aligned(16))) char smem[2 * SB];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lr = lane & 31, lh = lane >> 5;
+  const int wr = wave % WR, wc = wave / WR;
   // XCD-grouped tile order (as k_conv_cb_x6)
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, loc = bid >> 3;
@@ -609,7 +617,7 @@ k_conv_pw_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
     for (int k = 0; k < CPT; ++k) *reinterpret_cast<int4x*>(smem + buf * SB + loff[k]) = stg[k];
   };
   // weight fragments of this wave's row block: group g at ap[g * FRAG + t * 64]
-  const x6::bf16x8* ap = wpack + ((int64_t)(tm * 4 + wave) * NG) * cbx6::FRAG + lane;
+  const x6::bf16x8* ap = wpack + ((int64_t)(tm * WR + wr) * NG) * cbx6::FRAG + lane;
   auto load_a = [&](x6::bf16x8 (&f)[3], int g) {
 #pragma unroll
     for (int t = 0; t < 3; ++t) f[t] = ap[g * cbx6::FRAG + t * 64];
@@ -627,7 +635,7 @@ k_conv_pw_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   for (int st = 0; st < nst; ++st) {
-    const char* cur = smem + (st & 1) * SB + lh * BN * 48 + lr * 48;
+    const char* cur = smem + (st & 1) * SB + lh * BN * 48 + (wc * 128 + lr) * 48;
     const bool more = st + 1 < nst;
     if (more) load_stage(st + 1);
 #pragma unroll
@@ -652,7 +660,7 @@ k_conv_pw_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
       __builtin_amdgcn_s_barrier();
     }
   }
-  conv_epilogue_nchw<1, NB>(acc, P, P.e, m0 + 32 * wave, n0, lr, lh);
+  conv_epilogue_nchw<1, NB>(acc, P, P.e, m0 + 32 * wr, n0 + wc * 128, lr, lh);
 }
 
 // x [img][C][H][W] fp32 -> bf16 terms [img][C/8][H][W][3][8] (k_conv_cb_x6's
@@ -1583,25 +1591,33 @@ int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, c
 }
 
 // ---- k_conv_pw_x6 (1 x 1 convolutions) ----
-bool conv_pw_ok(const rram_conv_desc* d) {
+// tile rows WR 32: the less padded of 128 / 64 (ties 128); 0 = not covered
+// (> 1/4 padded rows, or a grid under ~3/4 of the workgroup slots, where the
+// fp32 kernel's smaller tiles do better)
+int conv_pw_wr(const rram_conv_desc* d) {
   if (d->kernel_h != 1 || d->kernel_w != 1 || d->stride_h != 1 || d->stride_w != 1 || d->pad_h != 0 ||
       d->pad_w != 0 || d->group != 1 || d->channels % 16 != 0)
-    return false;
+    return 0;
   const int64_t N = (int64_t)d->num * d->height * d->width;
-  const int64_t tiles = ((d->num_output + pwx6::BM - 1) / pwx6::BM) * ((N + pwx6::BN - 1) / pwx6::BN);
-  // > 1/4 padded rows, or under half of the 512 two-per-CU slots: the fp32
-  // kernel's smaller tiles do better
-  const int mt = (d->num_output + pwx6::BM - 1) / pwx6::BM * pwx6::BM;
-  if ((mt - d->num_output) * 4 > mt || tiles < 256) return false;
-  return N < (1ll << 31) && N * d->channels * 6 < (1ll << 31);
+  if (N >= (1ll << 31) || N * d->channels * 6 >= (1ll << 31)) return 0;
+  const int M = d->num_output;
+  const int m128 = (M + 127) / 128 * 128, m64 = (M + 63) / 64 * 64;
+  const int wr = (m64 - M) < (m128 - M) ? 2 : 4;
+  const int bm = 32 * wr, bn = 128 * (4 / wr), mt = wr == 2 ? m64 : m128;
+  if ((mt - M) * 4 > mt) return 0;
+  const int64_t tiles = (int64_t)(mt / bm) * ((N + bn - 1) / bn);
+  return tiles >= (wr == 4 ? 384 : 192) ? wr : 0;
 }
+bool conv_pw_ok(const rram_conv_desc* d) { return conv_pw_wr(d) != 0; }
 
 int conv_pw_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, const float* w, const float* bias,
                    float* y, int relu, hipStream_t s, const WPack& wk) {
-  if (!conv_pw_ok(d)) return 0;
+  const int WR = conv_pw_wr(d);
+  if (WR == 0) return 0;
   const int C = d->channels, M = d->num_output, HW = d->height * d->width, NG = C / 16;
-  const int tiles_m = (M + pwx6::BM - 1) / pwx6::BM;
-  const int64_t wfrags = (int64_t)tiles_m * 4 * NG;  // [row block][group], one tap
+  const int BM = 32 * WR, BN = 128 * (4 / WR);
+  const int tiles_m = (M + BM - 1) / BM;
+  const int64_t wfrags = (int64_t)tiles_m * WR * NG;  // [row block][group], one tap
   const size_t wbytes = static_cast<size_t>(wfrags * 3072);
   if (wk.query) {
     *wk.query = wbytes;
@@ -1621,7 +1637,7 @@ int conv_pw_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, c
   if (!wk.valid) {
     const int wunits = static_cast<int>(wfrags * 64);
     hipLaunchKernelGGL(k_conv_cb_pack_x6, dim3(stream_blocks(wunits)), dim3(256), 0, s, w, wbuf, M, C, 1,
-                       tiles_m * 4, wunits);
+                       tiles_m * WR, wunits);
     rc = launch_status("conv weight pack x6 (1x1)");
     if (rc) return rc;
   }
@@ -1636,11 +1652,14 @@ int conv_pw_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, c
   P.e.cimg = (int64_t)M * HW;
   P.e.hw = make_fastdiv(HW);
   P.tiles_m = tiles_m;
-  P.tiles_n = (P.N + pwx6::BN - 1) / pwx6::BN;
+  P.tiles_n = (P.N + BN - 1) / BN;
   const unsigned nwg = static_cast<unsigned>((int64_t)P.tiles_m * P.tiles_n);
   const auto* xp = reinterpret_cast<const uint16_t*>(x_oct != nullptr ? x_oct : buf);
-  hipLaunchKernelGGL(k_conv_pw_x6, dim3(nwg), dim3(256), 0, s, P, reinterpret_cast<const x6::bf16x8*>(wbuf), xp,
-                     static_cast<uint32_t>(xbytes), NG);
+  const auto* wpp = reinterpret_cast<const x6::bf16x8*>(wbuf);
+  if (WR == 4)
+    hipLaunchKernelGGL(k_conv_pw_x6<4>, dim3(nwg), dim3(256), 0, s, P, wpp, xp, static_cast<uint32_t>(xbytes), NG);
+  else
+    hipLaunchKernelGGL(k_conv_pw_x6<2>, dim3(nwg), dim3(256), 0, s, P, wpp, xp, static_cast<uint32_t>(xbytes), NG);
   rc = launch_status("conv pw x6");
   return rc ? rc : 1;
 }

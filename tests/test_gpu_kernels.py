@@ -502,6 +502,8 @@ ENGINE_CASES = [
     dict(x=(128, 480, 14, 14), cout=192, k=1, p=0, g=1),
     dict(x=(256, 832, 7, 7), cout=384, k=1, p=0, g=1),
     dict(x=(64, 528, 14, 14), cout=160, k=1, p=0, g=1),
+    dict(x=(64, 192, 28, 28), cout=64, k=1, p=0, g=1),       # 64 x 256 tiles
+    dict(x=(256, 512, 14, 14), cout=48, k=1, p=0, g=1),
 ]
 
 
