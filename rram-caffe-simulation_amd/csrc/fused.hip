@@ -191,136 +191,6 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// LRN ACROSS_CHANNELS followed by 3 x 3 / stride 2 MAX pooling, in registers.
-//
-// A segment of SW lanes (SW = 32 or 64 >= W: two segments per wave when the
-// image is at most 32 wide) owns one image x a band of P pooled rows x a chunk
-// of CC channels; lane l holds input column l of the band's NR = 2 (P - 1) + 3
-// input rows.  Walking the chunk's channels, each lane keeps the SIZE
-// channels around the current one in a register ring (the entering channel
-// loaded two channels ahead), forms the LRN value of its NR pixels with the
-// unfused kernel's arithmetic (lrn_sq_add over the window in channel order,
-// lrn_scale, lrn_out: bit for bit k_lrn_fwd_slide's), takes the max over each
-// pooled row's 3 input rows in registers, and the max over the 3 columns by
-// lane shuffles (ds_bpermute within the segment); pooled column pw is written
-// by lane pw.  No LDS, no barrier: the k_lrn_maxpool_band structure (LDS
-// plane + a barrier per 2-4 channels) left AlexNet's norm1 / norm2 at 3.5 /
-// 2.9 TB/s.  The max is taken column-wise, then across columns; with the
-// -FLT_MAX start and strict ">" of MaxPoolForward (pooling_layer.cu:11-47)
-// that is the same maximum as its row-major walk (only the order in which
-// equal values are met differs, which cannot change the value).
-// OCT: also writes y's channel-octet companion (x6.hip k_pack_octets_x6
-// layout) from the 8 pooled channels held in registers.
-template <int SIZE, int SW, int P, bool OCT>
-__global__ void __launch_bounds__(256)
-    k_lrn_maxpool_rows(const float* __restrict__ x, float* __restrict__ y, char* __restrict__ yo, int C, int H, int W,
-                       int PH, int PW, int ph, int pw, int bands, int CC, int nchunks, int items,
-                       float alpha_over_size, float beta, float k) {
-  constexpr int K = 3, S = 2, PRE = (SIZE - 1) / 2, POST = SIZE - 1 - PRE;
-  constexpr int NR = (P - 1) * S + K;
-  constexpr int SEG = 64 / SW;
-  const int lane = threadIdx.x & 63;
-  const int sl = lane % SW;
-  const int item = (blockIdx.x * 4 + (threadIdx.x >> 6)) * SEG + lane / SW;
-  if (item >= items) return;  // a whole segment: its shuffles read only its own lanes
-  const int band = item % bands, rest = item / bands;
-  const int chunk = rest % nchunks, n = rest / nchunks;
-  const int p0 = band * P, np = min(P, PH - p0);
-  const int r0 = p0 * S - ph;
-  const int cb = chunk * CC, ce = min(C, cb + CC);
-  const bool colok = sl < W;
-  uint32_t rowok = 0;
-#pragma unroll
-  for (int i = 0; i < NR; ++i) rowok |= static_cast<uint32_t>(r0 + i >= 0 && r0 + i < H) << i;
-  const int64_t HW = (int64_t)H * W;
-  const float* xn = x + (int64_t)n * C * HW + (int64_t)r0 * W + sl;
-  auto ld = [&](int c, int i) -> float {
-    return (c >= 0 && c < C && colok && ((rowok >> i) & 1u)) ? xn[(int64_t)c * HW + (int64_t)i * W] : 0.0f;
-  };
-  float win[SIZE][NR];
-#pragma unroll
-  for (int j = 0; j < SIZE; ++j)
-#pragma unroll
-    for (int i = 0; i < NR; ++i) win[j][i] = ld(cb - PRE + j, i);
-  float sa[NR], sb[NR];  // entering channels, alternating by step parity
-#pragma unroll
-  for (int i = 0; i < NR; ++i) sa[i] = ld(cb + POST + 1, i);
-  const int64_t PHW = (int64_t)PH * PW;
-  float* yn = y + (int64_t)n * C * PHW + (int64_t)p0 * PW + sl;
-  const bool store = sl < PW;
-  // source lane of pooled column sl's tap b (outside the image: masked)
-  int src[K];
-  bool srcok[K];
-#pragma unroll
-  for (int b = 0; b < K; ++b) {
-    src[b] = sl * S - pw + b;
-    srcok[b] = src[b] >= 0 && src[b] < W;
-  }
-  float oc[OCT ? 8 : 1][P];
-  // one channel: LRN, vertical then horizontal max, store; shift the ring
-  // (stin enters it) after issuing the loads of channel c + POST + 2 into stld
-  auto step = [&](int c, int d, float (&stin)[NR], float (&stld)[NR]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < NR; ++i) stld[i] = ld(c + POST + 2, i);
-    float m[P];
-#pragma unroll
-    for (int q = 0; q < P; ++q) m[q] = -FLT_MAX;
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      float acc = 0.0f;
-#pragma unroll
-      for (int j = 0; j < SIZE; ++j) acc = lrn_sq_add(acc, win[j][i]);
-      const float v = lrn_out(win[PRE][i], lrn_scale(acc, alpha_over_size, k), beta);
-      const bool ok = colok && ((rowok >> i) & 1u);
-#pragma unroll
-      for (int q = 0; q < P; ++q)
-        if (i >= q * S && i < q * S + K && ok && v > m[q]) m[q] = v;
-    }
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-      float o = -FLT_MAX;
-#pragma unroll
-      for (int b = 0; b < K; ++b) {
-        const float t = __shfl(m[q], src[b], SW);
-        if (srcok[b] && t > o) o = t;
-      }
-      if (store && q < np) yn[(int64_t)c * PHW + q * PW] = o;
-      if (OCT) oc[d & (OCT ? 7 : 0)][q] = o;
-    }
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-#pragma unroll
-      for (int j = 0; j < SIZE - 1; ++j) win[j][i] = win[j + 1][i];
-      win[SIZE - 1][i] = stin[i];
-    }
-  };
-  if (!OCT) {
-    for (int c = cb; c < ce; c += 2) {
-      step(c, 0, sa, sb);
-      if (c + 1 < ce) step(c + 1, 1, sb, sa);
-    }
-    return;
-  }
-  char* yon = yo + (int64_t)n * (C / 8) * PHW * 48;
-  for (int c0 = cb; c0 < ce; c0 += 8) {
-#pragma unroll
-    for (int d = 0; d < 8; d += 2) {
-      step(c0 + d, d, sa, sb);
-      step(c0 + d + 1, d + 1, sb, sa);
-    }
-    if (store) {
-#pragma unroll
-      for (int q = 0; q < P; ++q) {
-        if (q >= np) break;
-        float v[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = oc[e][q];
-        x6::store_terms8(v, yon + ((int64_t)(c0 / 8) * PHW + (int64_t)(p0 + q) * PW + sl) * 48);
-      }
-    }
-  }
-}
-
 }  // namespace
 }  // namespace rram
 
@@ -349,49 +219,6 @@ int rram_lrn_maxpool_fwd_octets(const float* x, float* y, void* y_oct, int num, 
                "lrn_maxpool_fwd: more than 2^31 elements is not supported");
   if (num == 0) return RRAM_OK;
   RRAM_REQUIRE(x && y, "lrn_maxpool_fwd: NULL");
-  char* yo = static_cast<char*>(y_oct);
-  const float aos = alpha / size;
-  // 3 x 3 / stride 2 windows over images at most 64 wide: the register kernel
-  if (kernel == 3 && sh == 2 && sw == 2 && W <= 64 && PW <= 64) {
-    const int SWd = W <= 32 ? 32 : 64;
-    const int P = SWd == 32 ? 5 : 4;
-    const int bands = (PH + P - 1) / P;
-    const int64_t per = (int64_t)num * bands;  // segments per channel chunk
-    const int step = y_oct ? 8 : 2;
-    // channel chunks: as few as give >= 4096 segments (each re-reads the
-    // SIZE - 1 halo channels), equal sizes in multiples of `step`
-    const int64_t want = (4096 + per - 1) / per;
-    const int64_t most = (C + step - 1) / step;
-    const int chunks0 = static_cast<int>(want < 1 ? 1 : (want > most ? most : want));
-    const int cc = ((C + chunks0 - 1) / chunks0 + step - 1) / step * step;
-    const int nchunks = (C + cc - 1) / cc;
-    RRAM_REQUIRE(per * nchunks < (1ll << 31), "lrn_maxpool_fwd: grid too large");
-    const int items = static_cast<int>(per * nchunks);
-    const int segs_per_block = 4 * (64 / SWd);
-    const dim3 grid(static_cast<unsigned>((items + segs_per_block - 1) / segs_per_block));
-#define RRAM_LR(S_, SW_, P_)                                                                                    \
-  if (yo)                                                                                                       \
-    hipLaunchKernelGGL((k_lrn_maxpool_rows<S_, SW_, P_, true>), grid, dim3(kThreads), 0, as_stream(s), x, y, yo, C, \
-                       H, W, PH, PW, ph, pw, bands, cc, nchunks, items, aos, beta, k);                          \
-  else                                                                                                          \
-    hipLaunchKernelGGL((k_lrn_maxpool_rows<S_, SW_, P_, false>), grid, dim3(kThreads), 0, as_stream(s), x, y, yo, \
-                       C, H, W, PH, PW, ph, pw, bands, cc, nchunks, items, aos, beta, k);
-    if (size == 5) {
-      if (SWd == 32) {
-        RRAM_LR(5, 32, 5)
-      } else {
-        RRAM_LR(5, 64, 4)
-      }
-    } else {
-      if (SWd == 32) {
-        RRAM_LR(3, 32, 5)
-      } else {
-        RRAM_LR(3, 64, 4)
-      }
-    }
-#undef RRAM_LR
-    return launch_status("lrn_maxpool_fwd (rows)");
-  }
   // band height: input rows of RB pooled rows must fit the block's pixel
   // budget and RB * PW outputs its threads
   auto fits = [&](int rb) {
@@ -413,6 +240,8 @@ int rram_lrn_maxpool_fwd_octets(const float* x, float* y, void* y_oct, int num, 
   const int chunks = static_cast<int>(want < 1 ? 1 : (want > most ? most : want));
   const int cc = ((C + chunks - 1) / chunks + step - 1) / step * step;
   const dim3 grid(static_cast<unsigned>(bands), static_cast<unsigned>(num), static_cast<unsigned>((C + cc - 1) / cc));
+  const float aos = alpha / size;
+  char* yo = static_cast<char*>(y_oct);
 #define RRAM_LP2(K_, S_, G_)                                                                                  \
   if (yo)                                                                                                     \
     hipLaunchKernelGGL((k_lrn_maxpool_band<K_, S_, G_, true>), grid, dim3(kThreads), 0, as_stream(s), x, y, yo, \

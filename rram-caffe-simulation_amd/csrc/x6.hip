@@ -628,7 +628,7 @@ k_conv_pw_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[0][j][r] = 0.0f;
   const int nst = (NG + GPS - 1) / GPS;
-  x6::bf16x8 fa[2][3];
+  x6::bf16x8 fa[GPS][3];  // group g of a stage in fa[g % GPS]: the next stage's first lands in fa[0]
   load_stage(0);
   load_a(fa[0], 0);
   store_stage(0);
@@ -642,8 +642,8 @@ k_conv_pw_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
     for (int gs = 0; gs < GPS; ++gs) {
       const int g = st * GPS + gs;
       if (g >= NG) break;
-      const x6::bf16x8 (&fc)[3] = fa[gs & 1];
-      if (g + 1 < NG) load_a(fa[(gs + 1) & 1], g + 1);
+      const x6::bf16x8 (&fc)[3] = fa[gs];
+      if (g + 1 < NG) load_a(fa[(gs + 1) % GPS], g + 1);
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         const char* p = cur + gs * 2 * BN * 48 + j * 32 * 48;
@@ -919,11 +919,21 @@ k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img,
     // two ds_read_b64 at compile-time offsets, issued one group ahead
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    // the padded K items (kernel column 11, and kernel row 11 in lane half 1)
+    // carry zero weights but read real input elements; their B values are
+    // zeroed too, so a non-finite input outside the 11 x 11 window never
+    // meets a zero weight (0 * Inf = NaN where fp32 has no such product)
+    const uint32_t row11_keep = lh ? 0u : 0xFFFFFFFFu;
+    auto mask_quad = [&](u32x2 v, int qi) __attribute__((always_inline)) {
+      if (qi % KQ == KQ - 1) v[1] &= 0x0000FFFFu;               // column 11: element 3 of the last quad
+      if ((qi / KQ) % HR == HR - 1) v = v & u32x2{row11_keep, row11_keep};  // row 11 (half 1)
+      return v;
+    };
     auto read_part = [&](x6::Parts (&F)[2], int g, int part) __attribute__((always_inline)) {
       const int j = part / 3, tt = part % 3;
       const char* b = smem + lb[j] + tt * TERMB;
-      const u32x2 lo = *reinterpret_cast<const u32x2*>(b + quad_off(2 * g));
-      const u32x2 hi = *reinterpret_cast<const u32x2*>(b + quad_off(2 * g + 1));
+      const u32x2 lo = mask_quad(*reinterpret_cast<const u32x2*>(b + quad_off(2 * g)), 2 * g);
+      const u32x2 hi = mask_quad(*reinterpret_cast<const u32x2*>(b + quad_off(2 * g + 1)), 2 * g + 1);
       const x6::bf16x8 v = __builtin_bit_cast(x6::bf16x8, u32x4{lo[0], lo[1], hi[0], hi[1]});
       if (tt == 0) F[j].h = v;
       else if (tt == 1) F[j].m = v;
@@ -1592,8 +1602,8 @@ int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, c
 
 // ---- k_conv_pw_x6 (1 x 1 convolutions) ----
 // tile rows WR 32: the less padded of 128 / 64 (ties 128); 0 = not covered
-// (> 1/4 padded rows, or a grid under ~3/4 of the workgroup slots, where the
-// fp32 kernel's smaller tiles do better)
+// (> 1/4 padded rows, or a grid under one workgroup per CU (128 x 128) / half
+// of the CUs (64 x 256), where the fp32 kernel's smaller tiles fill more)
 int conv_pw_wr(const rram_conv_desc* d) {
   if (d->kernel_h != 1 || d->kernel_w != 1 || d->stride_h != 1 || d->stride_w != 1 || d->pad_h != 0 ||
       d->pad_w != 0 || d->group != 1 || d->channels % 16 != 0)
@@ -1606,7 +1616,7 @@ int conv_pw_wr(const rram_conv_desc* d) {
   const int bm = 32 * wr, bn = 128 * (4 / wr), mt = wr == 2 ? m64 : m128;
   if ((mt - M) * 4 > mt) return 0;
   const int64_t tiles = (int64_t)(mt / bm) * ((N + bn - 1) / bn);
-  return tiles >= (wr == 4 ? 384 : 192) ? wr : 0;
+  return tiles >= (wr == 4 ? 256 : 128) ? wr : 0;
 }
 bool conv_pw_ok(const rram_conv_desc* d) { return conv_pw_wr(d) != 0; }
 

@@ -160,9 +160,7 @@ def test_lrn_across_fwd_bwd_vs_autograd(device, size):
 def test_lrn_maxpool_fused_equals_unfused(device, size, k, s, p, C, H):
     """rram_lrn_maxpool_fwd == rram_lrn_fwd then rram_pool_fwd, bit for bit
     (same LRN arithmetic; window edges of the ceil rule), and the torch fp32
-    reference within the LRN tolerance.  3 x 3 / stride 2 windows over images
-    up to 64 wide take the register kernel (two segments per wave up to 32
-    wide), the rest and W = 69 the LDS band kernel."""
+    reference within the LRN tolerance."""
     import torch
     from rramsim import ops
     torch.manual_seed(9)

@@ -30,7 +30,7 @@ CASES = [
     dict(x=(2, 96, 27, 27), cout=256, k=5, s=1, p=2, g=2),    # conv2: channel-octet kernel
     dict(x=(2, 256, 13, 13), cout=384, k=3, s=1, p=1, g=1),   # conv3: channel-octet kernel
     dict(x=(2, 24, 20, 20), cout=96, k=3, s=1, p=1, g=1),     # Cin % 16 != 0: patch kernel
-    dict(x=(32, 256, 28, 28), cout=128, k=1, s=1, p=0, g=1),  # 1x1: pointwise kernel, 128 x 128 tiles
+    dict(x=(64, 256, 28, 28), cout=128, k=1, s=1, p=0, g=1),  # 1x1: pointwise kernel, 128 x 128 tiles
     dict(x=(64, 192, 28, 28), cout=64, k=1, s=1, p=0, g=1),   # 1x1: 64 x 256 tiles
 ]
 

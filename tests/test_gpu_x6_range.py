@@ -1,7 +1,10 @@
 """The bf16x6 engine at the ends of the fp32 range (include/rram_kernels.h,
 DESIGN §4.1 "Range").  Every split clamps each term's input to +-BF16_MAX, so
 operands above the largest bf16 and +-Inf give the products fp32 gives (+-Inf,
-Inf * 0 = NaN); operands down to 2^-110 split exactly.  Checked on every
+Inf * 0 = NaN; the conv1 kernel's padded K items read zeroed B values, so no
+0 * Inf product exists that fp32 does not form); operands down to 2^-110
+split exactly (below it the low terms fall under the normal range: the
+engine's documented limit, measured by scripts/x6_range_probe.py).  Checked on every
 kernel of the engine — the channel-octet convolution, the persistent conv1
 kernel, the patch kernel, the pointwise kernel and the InnerProduct GEMM —
 against a CPU float32 evaluation (NaN / +Inf / -Inf positions) and a float64
@@ -15,7 +18,7 @@ CONVS = {
     "octet": ((2, 256, 13, 13), 384, 3, 1, 1),
     "conv1": ((2, 3, 227, 227), 96, 11, 4, 0),
     "patch": ((2, 24, 20, 20), 96, 3, 1, 1),
-    "pointwise": ((32, 256, 28, 28), 128, 1, 1, 0),
+    "pointwise": ((64, 256, 28, 28), 128, 1, 1, 0),
     "pointwise64": ((64, 192, 28, 28), 64, 1, 1, 0),
 }
 
