@@ -529,140 +529,6 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
   }
 }
 
-// ---------------------------------------------------------------------------
-// k_conv_pw_x6: 1 x 1, stride-1, unpadded convolution (GoogLeNet's inception
-// reductions / projections) on the bf16x6 engine: per image a plain GEMM
-// Y[co][p] = W[co][ci] X[ci][p] over the channel-octet companion of X
-// ([n][C/8][HW][3][8] bf16, the pre-split operand form the channel-octet
-// kernel reads) and pre-split weight fragments (k_conv_cb_pack_x6 with one
-// tap; cached across calls by rram_conv2d_fwd_cached).
-// Tile 32 WR rows x 128 (4 / WR) positions (positions run across image
-// boundaries): WR = 4 (128 x 128, two workgroups per CU) or WR = 2 (64 x 256
-// for the 48..64-row reductions); wave w owns rows 32 (w % WR) .. + 31 and
-// 128 positions (4 column blocks), so each weight fragment feeds 4 blocks.  K runs in groups of 16 channels (lane half h = octet 2 g + h);
-// GPS groups form a stage: the stage's octet planes (128 positions x 48 B x
-// 2 octets per group) are loaded by all threads into registers while the
-// previous stage computes and written to the other LDS buffer before the
-// one barrier per stage.  B reads: ds_read_b128 at a 48-byte lane stride,
-// 16 lanes on 16 disjoint bank quads (3 n mod 16 as in k_conv_cb_x6).
-// Weights come from L2 straight into registers one group ahead.
-namespace pwx6 {
-constexpr int NB = 4, GPS = 3;
-template <int WR>
-struct Tile {
-  static constexpr int BM = 32 * WR, BN = 128 * (4 / WR);
-  static constexpr int GB = BN * 96;               // LDS bytes per group (2 octets x BN positions x 48 B)
-  static constexpr int SB = GPS * GB;              // bytes per stage (WR = 4: 36 KB, two workgroups per CU)
-  static constexpr int CPT = GPS * GB / 16 / 256;  // 16-byte chunks per thread per stage
-  static_assert(GPS * GB % (16 * 256) == 0, "chunks");
-};
-}  // namespace pwx6
-
-template <int WR>
-__global__ void __launch_bounds__(256, WR == 4 ? 2 : 1)
-k_conv_pw_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __restrict__ xoct, uint32_t xbytes,
-             int NG) {
-  using namespace pwx6;
-  using Tl = Tile<WR>;
-  constexpr int BM = Tl::BM, BN = Tl::BN, SB = Tl::SB, CPT = Tl::CPT;
-  __shared__ __attribute__((aligned(16))) char smem[2 * SB];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lr = lane & 31, lh = lane >> 5;
-  const int wr = wave % WR, wc = wave / WR;
-  // XCD-grouped tile order (as k_conv_cb_x6)
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, loc = bid >> 3;
-  const int q8 = nwg >> 3, r8 = nwg & 7;
-  const int tid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
-  const int tm = __builtin_amdgcn_readfirstlane(tid % P.tiles_m);
-  const int tn = __builtin_amdgcn_readfirstlane(tid / P.tiles_m);
-  const int n0 = tn * BN, m0 = tm * BM;
-  const int HW = P.cv.howo.d;
-  const uint32_t PL = static_cast<uint32_t>(HW) * 48u;  // bytes per octet plane of one image
-  const uint32_t img_b = static_cast<uint32_t>(P.cv.C >> 3) * PL;
-  // this thread's staging chunks: chunk c of a stage = (group slot gs, octet h, position pn, term t)
-  uint32_t soff[CPT];  // global byte offset for stage 0 (group g adds 2 g PL)
-  uint32_t loff[CPT];  // LDS byte offset within a stage
-#pragma unroll
-  for (int k = 0; k < CPT; ++k) {
-    const int c = threadIdx.x + k * 256;
-    const int gs = c / (BN * 6), rem = c - gs * (BN * 6);
-    const int h = rem / (BN * 3), r2 = rem - h * (BN * 3);
-    const int pn = r2 / 3, t = r2 - pn * 3;
-    const int n = n0 + pn;
-    const uint32_t img = static_cast<uint32_t>(fdiv(static_cast<uint32_t>(min(n, P.N - 1)), P.cv.howo));
-    const uint32_t sp = static_cast<uint32_t>(min(n, P.N - 1)) - img * static_cast<uint32_t>(HW);
-    soff[k] = n < P.N ? img * img_b + static_cast<uint32_t>(2 * gs + h) * PL + sp * 48u + static_cast<uint32_t>(t) * 16u
-                      : 0x80000000u;
-    loff[k] = static_cast<uint32_t>((gs * 2 + h) * BN * 48 + pn * 48 + t * 16);
-  }
-  const __amdgpu_buffer_rsrc_t xr =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(xoct), 0, static_cast<int>(xbytes), 0x00020000);
-  typedef int int4x __attribute__((ext_vector_type(4)));
-  int4x stg[CPT];
-  // groups past NG load from past the range (zeros) into slots no MFMA reads
-  auto load_stage = [&](int st) __attribute__((always_inline)) {
-    const uint32_t goff = static_cast<uint32_t>(st * GPS) * 2u * PL;
-#pragma unroll
-    for (int k = 0; k < CPT; ++k) {
-      const int gs = (threadIdx.x + k * 256) / (BN * 6);
-      const bool ok = st * GPS + gs < NG && soff[k] != 0x80000000u;
-      stg[k] = __builtin_bit_cast(int4x, __builtin_amdgcn_raw_buffer_load_b128(
-                                             xr, static_cast<int>(ok ? soff[k] + goff : 0x80000000u), 0, 0));
-    }
-  };
-  auto store_stage = [&](int buf) __attribute__((always_inline)) {
-#pragma unroll
-    for (int k = 0; k < CPT; ++k) *reinterpret_cast<int4x*>(smem + buf * SB + loff[k]) = stg[k];
-  };
-  // weight fragments of this wave's row block: group g at ap[g * FRAG + t * 64]
-  const x6::bf16x8* ap = wpack + ((int64_t)(tm * WR + wr) * NG) * cbx6::FRAG + lane;
-  auto load_a = [&](x6::bf16x8 (&f)[3], int g) {
-#pragma unroll
-    for (int t = 0; t < 3; ++t) f[t] = ap[g * cbx6::FRAG + t * 64];
-  };
-  floatx16 acc[1][NB];
-#pragma unroll
-  for (int j = 0; j < NB; ++j)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[0][j][r] = 0.0f;
-  const int nst = (NG + GPS - 1) / GPS;
-  x6::bf16x8 fa[GPS][3];  // group g of a stage in fa[g % GPS]: the next stage's first lands in fa[0]
-  load_stage(0);
-  load_a(fa[0], 0);
-  store_stage(0);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  for (int st = 0; st < nst; ++st) {
-    const char* cur = smem + (st & 1) * SB + lh * BN * 48 + (wc * 128 + lr) * 48;
-    const bool more = st + 1 < nst;
-    if (more) load_stage(st + 1);
-#pragma unroll
-    for (int gs = 0; gs < GPS; ++gs) {
-      const int g = st * GPS + gs;
-      if (g >= NG) break;
-      const x6::bf16x8 (&fc)[3] = fa[gs];
-      if (g + 1 < NG) load_a(fa[(gs + 1) % GPS], g + 1);
-#pragma unroll
-      for (int j = 0; j < NB; ++j) {
-        const char* p = cur + gs * 2 * BN * 48 + j * 32 * 48;
-        x6::Parts b;
-        b.h = *reinterpret_cast<const x6::bf16x8*>(p);
-        b.m = *reinterpret_cast<const x6::bf16x8*>(p + 16);
-        b.l = *reinterpret_cast<const x6::bf16x8*>(p + 32);
-        acc[0][j] = x6::mfma6(x6::Parts{fc[0], fc[1], fc[2]}, b, acc[0][j]);
-      }
-    }
-    if (more) {
-      store_stage((st + 1) & 1);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
-  }
-  conv_epilogue_nchw<1, NB>(acc, P, P.e, m0 + 32 * wr, n0 + wc * 128, lr, lh);
-}
-
 // x [img][C][H][W] fp32 -> bf16 terms [img][C/8][H][W][3][8] (k_conv_cb_x6's
 // input).  One thread per (image, octet, position): 8 strided loads (coalesced
 // across the threads), 48 bytes out.
@@ -1600,80 +1466,6 @@ int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, c
   return rc ? rc : 1;
 }
 
-// ---- k_conv_pw_x6 (1 x 1 convolutions) ----
-// tile rows WR 32: the less padded of 128 / 64 (ties 128); 0 = not covered
-// (> 1/4 padded rows, or a grid under one workgroup per CU (128 x 128) / half
-// of the CUs (64 x 256), where the fp32 kernel's smaller tiles fill more)
-int conv_pw_wr(const rram_conv_desc* d) {
-  if (d->kernel_h != 1 || d->kernel_w != 1 || d->stride_h != 1 || d->stride_w != 1 || d->pad_h != 0 ||
-      d->pad_w != 0 || d->group != 1 || d->channels % 16 != 0)
-    return 0;
-  const int64_t N = (int64_t)d->num * d->height * d->width;
-  if (N >= (1ll << 31) || N * d->channels * 6 >= (1ll << 31)) return 0;
-  const int M = d->num_output;
-  const int m128 = (M + 127) / 128 * 128, m64 = (M + 63) / 64 * 64;
-  const int wr = (m64 - M) < (m128 - M) ? 2 : 4;
-  const int bm = 32 * wr, bn = 128 * (4 / wr), mt = wr == 2 ? m64 : m128;
-  if ((mt - M) * 4 > mt) return 0;
-  const int64_t tiles = (int64_t)(mt / bm) * ((N + bn - 1) / bn);
-  return tiles >= (wr == 4 ? 256 : 128) ? wr : 0;
-}
-bool conv_pw_ok(const rram_conv_desc* d) { return conv_pw_wr(d) != 0; }
-
-int conv_pw_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, const float* w, const float* bias,
-                   float* y, int relu, hipStream_t s, const WPack& wk) {
-  const int WR = conv_pw_wr(d);
-  if (WR == 0) return 0;
-  const int C = d->channels, M = d->num_output, HW = d->height * d->width, NG = C / 16;
-  const int BM = 32 * WR, BN = 128 * (4 / WR);
-  const int tiles_m = (M + BM - 1) / BM;
-  const int64_t wfrags = (int64_t)tiles_m * WR * NG;  // [row block][group], one tap
-  const size_t wbytes = static_cast<size_t>(wfrags * 3072);
-  if (wk.query) {
-    *wk.query = wbytes;
-    return 1;
-  }
-  const int64_t xbytes = (int64_t)d->num * C * HW * 6;
-  const int64_t xb_al = x_oct != nullptr ? 0 : (xbytes + 255) / 256 * 256;
-  const int64_t scratch = xb_al + (wk.p ? 0 : (int64_t)wbytes);
-  char* buf = scratch > 0 ? reinterpret_cast<char*>(pack_buffer(static_cast<size_t>(scratch / 4), s)) : nullptr;
-  RRAM_REQUIRE(scratch == 0 || buf != nullptr, "conv: packed-operand buffer allocation failed");
-  char* wbuf = wk.p ? static_cast<char*>(wk.p) : buf + xb_al;
-  int rc = 0;
-  if (x_oct == nullptr) {
-    rc = pack_octets(x, buf, d->num, C, HW, s);
-    if (rc) return rc;
-  }
-  if (!wk.valid) {
-    const int wunits = static_cast<int>(wfrags * 64);
-    hipLaunchKernelGGL(k_conv_cb_pack_x6, dim3(stream_blocks(wunits)), dim3(256), 0, s, w, wbuf, M, C, 1,
-                       tiles_m * WR, wunits);
-    rc = launch_status("conv weight pack x6 (1x1)");
-    if (rc) return rc;
-  }
-  Params P{};
-  P.M = M;
-  P.N = d->num * HW;
-  P.K = C;
-  P.split = 1;
-  P.cv.C = C;
-  P.cv.howo = make_fastdiv(HW);
-  P.e = make_epi(y, HW, 1.0f, 0.0f, bias, RRAM_BIAS_ROW, relu);
-  P.e.cimg = (int64_t)M * HW;
-  P.e.hw = make_fastdiv(HW);
-  P.tiles_m = tiles_m;
-  P.tiles_n = (P.N + BN - 1) / BN;
-  const unsigned nwg = static_cast<unsigned>((int64_t)P.tiles_m * P.tiles_n);
-  const auto* xp = reinterpret_cast<const uint16_t*>(x_oct != nullptr ? x_oct : buf);
-  const auto* wpp = reinterpret_cast<const x6::bf16x8*>(wbuf);
-  if (WR == 4)
-    hipLaunchKernelGGL(k_conv_pw_x6<4>, dim3(nwg), dim3(256), 0, s, P, wpp, xp, static_cast<uint32_t>(xbytes), NG);
-  else
-    hipLaunchKernelGGL(k_conv_pw_x6<2>, dim3(nwg), dim3(256), 0, s, P, wpp, xp, static_cast<uint32_t>(xbytes), NG);
-  rc = launch_status("conv pw x6");
-  return rc ? rc : 1;
-}
-
 int conv_patch_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const float* bias, float* y, int relu,
                       hipStream_t s, const WPack& wk);
 // The bf16x6 convolution forward.  x_oct: NULL or the octet companion of x
@@ -1690,7 +1482,6 @@ int conv_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, cons
     if (rc != 0) return rc;
   }
   int rc = conv_wide_x6_fwd(d, x, w, bias, y, relu, s, wk);
-  if (rc == 0) rc = conv_pw_x6_fwd(d, x, x_oct, w, bias, y, relu, s, wk);
   if (rc == 0) rc = conv_patch_x6_fwd(d, x, w, bias, y, relu, s, wk);
   if (wk.query) return rc;
   if (rc > 0 && y_oct != nullptr) {
@@ -1863,7 +1654,7 @@ int rram_f32_engine_for_conv(const rram_conv_desc* d) {
   rram::ConvPlan pl;
   rram::CbPlan cpl;
   return rram::f32_engine().load() == RRAM_ENGINE_BF16X6 &&
-                 (rram::conv_x6_plan(d, pl) || rram::conv1_ring_ok(d) || rram::conv_pw_ok(d) ||
+                 (rram::conv_x6_plan(d, pl) || rram::conv1_ring_ok(d) ||
                   rram::conv_cb_plan(d, cpl))
              ? RRAM_ENGINE_BF16X6
              : RRAM_ENGINE_F32;
@@ -1872,8 +1663,7 @@ int rram_f32_engine_for_conv(const rram_conv_desc* d) {
 int rram_conv_input_octets(const rram_conv_desc* d) {
   RRAM_REQUIRE(d != nullptr, "octet query: desc is NULL");
   rram::CbPlan cpl;
-  return rram::f32_engine().load() == RRAM_ENGINE_BF16X6 && (rram::conv_cb_plan(d, cpl) || rram::conv_pw_ok(d)) ? 1
-                                                                                                               : 0;
+  return rram::f32_engine().load() == RRAM_ENGINE_BF16X6 && rram::conv_cb_plan(d, cpl) ? 1 : 0;
 }
 
 int rram_pack_octets(const float* x, void* oct, int num, int channels, int height, int width, rram_stream_t s) {

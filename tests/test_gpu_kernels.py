@@ -497,13 +497,6 @@ ENGINE_CASES = [
     dict(x=(4, 256, 13, 13), cout=384, k=3, p=1, g=1),
     dict(x=(4, 384, 13, 13), cout=384, k=3, p=1, g=2),
     dict(x=(4, 384, 13, 13), cout=256, k=3, p=1, g=2),
-    # GoogLeNet 1x1 reductions / projections on the pointwise kernel (k_conv_pw_x6)
-    dict(x=(64, 256, 28, 28), cout=128, k=1, p=0, g=1),
-    dict(x=(128, 480, 14, 14), cout=192, k=1, p=0, g=1),
-    dict(x=(256, 832, 7, 7), cout=384, k=1, p=0, g=1),
-    dict(x=(64, 528, 14, 14), cout=160, k=1, p=0, g=1),
-    dict(x=(64, 192, 28, 28), cout=64, k=1, p=0, g=1),       # 64 x 256 tiles
-    dict(x=(256, 512, 14, 14), cout=48, k=1, p=0, g=1),
 ]
 
 
