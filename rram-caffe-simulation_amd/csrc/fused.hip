@@ -40,7 +40,11 @@ constexpr int kLrnBlocks = 4096;
 // pre-split input, x6.hip k_pack_octets_x6 layout [num][C/8][PH][PW][3][8]
 // bf16): the pooled values of 8 channels are gathered in an LDS plane and
 // split by the band's output threads (C % 8 == 0 and CC % 8 == 0; G divides 8).
-template <int K, int SIZE, int G, bool OCT>
+// WT > 0: the plane width W is WT (AlexNet's 55 / 27), so a window that lies
+// wholly inside the image reads its K x K taps at immediate LDS offsets with
+// no per-tap mask (3 instructions a tap instead of ~6; every AlexNet window
+// is such, the ceil rule clips none); WT = 0: any W.
+template <int K, int SIZE, int G, bool OCT, int WT = 0>
 __global__ void __launch_bounds__(256)
     k_lrn_maxpool_band(const float* __restrict__ x, float* __restrict__ y, char* __restrict__ yo, int C, int H, int W,
                        int PH, int PW, int sh, int sw, int ph, int pw, int RB, int CC, float alpha_over_size,
@@ -68,7 +72,15 @@ __global__ void __launch_bounds__(256)
     pix[q] = threadIdx.x + q * 256;
     own[q] = pix[q] < NP;
   }
-  auto ld = [&](int q, int cc) { return (cc >= 0 && cc < C && own[q]) ? xb[(int64_t)cc * HW + pix[q]] : 0.0f; };
+  // buffer loads with 32-bit offsets from the band's first row (one image is
+  // < 2 GiB: host check); a channel outside [0, C) or a pixel outside the band
+  // reads past the range, i.e. zero
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(xb), 0, static_cast<int>(((int64_t)C * HW - (int64_t)h0 * W) * 4), 0x00020000);
+  auto ld = [&](int q, int cc) {
+    const uint32_t off = (cc >= 0 && cc < C && own[q]) ? static_cast<uint32_t>((cc * HW + pix[q]) * 4) : 0x80000000u;
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xrs, static_cast<int>(off), 0, 0));
+  };
   // win[q][j] = x at channel (c0 - PRE + j) of pixel q, zero outside [0, C).
   // The entering channels of group g + 2 are loaded at the top of group g
   // into one of two staging arrays (st0 / st1, alternating by group parity so
@@ -143,14 +155,24 @@ __global__ void __launch_bounds__(256)
       if (d < nd) {
         const float* yl = yb[d] + it_l[i];
         float mv = -FLT_MAX;
+        if (WT > 0 && it_ok[i] == (1u << (K * K)) - 1u) {
 #pragma unroll
-        for (int a = 0; a < K; ++a)
+          for (int a = 0; a < K; ++a)
 #pragma unroll
-          for (int b = 0; b < K; ++b) {
-            const bool ok = (it_ok[i] >> (a * K + b)) & 1u;
-            const float v = yl[ok ? a * W + b : -it_l[i]];  // masked taps read element 0
-            if (ok && v > mv) mv = v;
-          }
+            for (int b = 0; b < K; ++b) {
+              const float v = yl[a * WT + b];
+              mv = v > mv ? v : mv;
+            }
+        } else {
+#pragma unroll
+          for (int a = 0; a < K; ++a)
+#pragma unroll
+            for (int b = 0; b < K; ++b) {
+              const bool ok = (it_ok[i] >> (a * K + b)) & 1u;
+              const float v = yl[ok ? a * W + b : -it_l[i]];  // masked taps read element 0
+              if (ok && v > mv) mv = v;
+            }
+        }
         yn[(int64_t)(c0 + d) * PHW + it_out[i]] = mv;
         if (OCT) obuf[(c0 + d) & 7][it_out[i] - pr0 * PW] = mv;
       }
@@ -217,6 +239,7 @@ int rram_lrn_maxpool_fwd_octets(const float* x, float* y, void* y_oct, int num, 
   RRAM_REQUIRE(ph < kernel && pw < kernel, "lrn_maxpool_fwd: pad must be < kernel");
   RRAM_REQUIRE((int64_t)num * C * H * W < 2147483647ll && (int64_t)num * C * PH * PW < 2147483647ll,
                "lrn_maxpool_fwd: more than 2^31 elements is not supported");
+  RRAM_REQUIRE((int64_t)C * H * W * 4 < 2147483647ll, "lrn_maxpool_fwd: one image must be < 2 GiB");
   if (num == 0) return RRAM_OK;
   RRAM_REQUIRE(x && y, "lrn_maxpool_fwd: NULL");
   // band height: input rows of RB pooled rows must fit the block's pixel
@@ -242,13 +265,21 @@ int rram_lrn_maxpool_fwd_octets(const float* x, float* y, void* y_oct, int num, 
   const dim3 grid(static_cast<unsigned>(bands), static_cast<unsigned>(num), static_cast<unsigned>((C + cc - 1) / cc));
   const float aos = alpha / size;
   char* yo = static_cast<char*>(y_oct);
-#define RRAM_LP2(K_, S_, G_)                                                                                  \
+#define RRAM_LP3(K_, S_, G_, WT_)                                                                             \
   if (yo)                                                                                                     \
-    hipLaunchKernelGGL((k_lrn_maxpool_band<K_, S_, G_, true>), grid, dim3(kThreads), 0, as_stream(s), x, y, yo, \
-                       C, H, W, PH, PW, sh, sw, ph, pw, rb, cc, aos, beta, k);                                \
+    hipLaunchKernelGGL((k_lrn_maxpool_band<K_, S_, G_, true, WT_>), grid, dim3(kThreads), 0, as_stream(s), x, y, \
+                       yo, C, H, W, PH, PW, sh, sw, ph, pw, rb, cc, aos, beta, k);                            \
   else                                                                                                        \
-    hipLaunchKernelGGL((k_lrn_maxpool_band<K_, S_, G_, false>), grid, dim3(kThreads), 0, as_stream(s), x, y,    \
-                       yo, C, H, W, PH, PW, sh, sw, ph, pw, rb, cc, aos, beta, k);
+    hipLaunchKernelGGL((k_lrn_maxpool_band<K_, S_, G_, false, WT_>), grid, dim3(kThreads), 0, as_stream(s), x, \
+                       y, yo, C, H, W, PH, PW, sh, sw, ph, pw, rb, cc, aos, beta, k);
+#define RRAM_LP2(K_, S_, G_)                               \
+  if (K_ == 3 && S_ == 5 && W == 55) {                     \
+    RRAM_LP3(K_, S_, G_, (K_ == 3 && S_ == 5 ? 55 : 0))    \
+  } else if (K_ == 3 && S_ == 5 && W == 27) {              \
+    RRAM_LP3(K_, S_, G_, (K_ == 3 && S_ == 5 ? 27 : 0))    \
+  } else {                                                 \
+    RRAM_LP3(K_, S_, G_, 0)                                \
+  }
 #define RRAM_LP(K_, S_)          \
   if (kernel == K_ && size == S_) { \
     if (gsel == 2) {             \
@@ -261,6 +292,7 @@ int rram_lrn_maxpool_fwd_octets(const float* x, float* y, void* y_oct, int num, 
   else RRAM_LP(3, 3) else RRAM_LP(2, 5) else RRAM_LP(2, 3)
 #undef RRAM_LP
 #undef RRAM_LP2
+#undef RRAM_LP3
   return launch_status("lrn_maxpool_fwd");
 }
 

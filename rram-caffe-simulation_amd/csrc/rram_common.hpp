@@ -108,9 +108,14 @@ __device__ __forceinline__ float lrn_sq_add(float acc, float v) { return fmaf(v,
 __device__ __forceinline__ float lrn_scale(float acc, float alpha_over_size, float k) {
   return fmaf(acc, alpha_over_size, k);
 }
-// x * scale^-beta via v_log_f32 / v_exp_f32 (scale >= k > 0)
+// x * scale^-beta via the raw v_log_f32 / v_exp_f32 (scale >= k > 0).  The
+// libm-style log2f / exp2f wrap each in denormal range scaling (two
+// v_ldexp + compares + selects per call); neither applies here: scale >= k
+// is normal for any LRN k >= 2^-126, and scale^-beta >= FLT_MAX^-beta is
+// normal for beta < 1 (Caffe's 0.75), with exp2 of a tinier argument
+// flushing to 0 as powf's would round to a denormal.
 __device__ __forceinline__ float lrn_out(float x, float scale, float beta) {
-  return x * exp2f(-beta * log2f(scale));
+  return x * __builtin_amdgcn_exp2f(-beta * __builtin_amdgcn_logf(scale));
 }
 
 // 32-bit word -> uniform in (0, 1] (never 0: safe for log) and [0, 1).

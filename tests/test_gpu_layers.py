@@ -181,6 +181,32 @@ def test_lrn_maxpool_fused_equals_unfused(device, size, k, s, p, C, H):
                                rtol=2e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("C,H", [(96, 55), (256, 27)])
+def test_lrn_maxpool_fused_equals_unfused_alexnet_planes(device, C, H):
+    """AlexNet's square 55 x 55 / 27 x 27 planes take the band kernel's
+    compile-time-width path (immediate-offset pooling taps): bit for bit the
+    unfused LRN + max pool, with and without the octet companion."""
+    import torch
+    from rramsim import ops
+    torch.manual_seed(11)
+    N, W = 3, H
+    x = 4 * torch.randn(N, C, H, W, device=device)
+    alpha, beta, kk = 1e-2, 0.75, 1.5
+    lrn = torch.empty_like(x)
+    ops.lrn_fwd(x, lrn, None, N, C, H, W, 5, alpha, beta, kk)
+    PH = PW = (H - 3 + 1) // 2 + 1
+    geom = (N, C, H, W, PH, PW, 3, 3, 2, 2, 0, 0)
+    unfused = torch.empty((N, C, PH, PW), device=device)
+    ops.pool_fwd(lrn, unfused, None, geom, 0)
+    fused = torch.full_like(unfused, float("nan"))
+    ops.lrn_maxpool_fwd(x, fused, N, C, H, W, PH, PW, 3, 2, 0, 5, alpha, beta, kk)
+    fo = torch.full_like(unfused, float("nan"))
+    yo = torch.zeros(unfused.numel() * 6, dtype=torch.uint8, device=device)
+    ops.lrn_maxpool_fwd_octets(x, fo, yo, N, C, H, W, PH, PW, 3, 2, 0, 5, alpha, beta, kk)
+    torch.cuda.synchronize()
+    assert torch.equal(fused, unfused) and torch.equal(fo, unfused)
+
+
 def test_lrn_maxpool_fusion_in_alexnet_test_net(device):
     """Net folds norm1/norm2 into pool1/pool2 in the TEST phase; the net outputs
     are bit-identical to the unfused net."""
