@@ -524,6 +524,69 @@ __global__ void __launch_bounds__(256) k_accuracy(const float* __restrict__ x, c
     if (N) atomicAdd(count, static_cast<float>(N));
   }
 }
+// Single-launch form for the large heads (AlexNet / GoogLeNet: 256 x 1000):
+// k_accuracy's per-block counts go to a per-block slot instead of atomics on
+// zeroed outputs; the last block to finish (a device-scope ticket) sums the
+// slots in block order and writes correct / count / ratio, then re-arms the
+// ticket — no memsets, no second launch.  Launches on one stream are ordered;
+// the slots are a single per-device set, so concurrent accuracy launches on
+// different streams are not supported (the host runs them on its one stream).
+constexpr int kAccFusedBlocks = 4096;
+__device__ int g_acc_part[2 * kAccFusedBlocks];
+__device__ unsigned g_acc_ticket;
+__global__ void __launch_bounds__(256) k_accuracy_fused(const float* __restrict__ x, const float* __restrict__ label,
+                                                        float* correct, float* count, float* ratio, int outer, int C,
+                                                        int inner, int top_k, int ignore) {
+  __shared__ int sa[4], sc[4];
+  __shared__ bool last;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t cols = (int64_t)outer * inner;
+  const int64_t col = (int64_t)blockIdx.x * 4 + wave;
+  int hit = 0, cnt = 0;
+  if (col < cols) {
+    const int64_t o = col / inner, q = col - o * inner;
+    const int lv = static_cast<int>(label[col]);
+    if (!(ignore >= 0 && lv == ignore)) {
+      const float* xs = x + o * C * inner + q;
+      const float v = xs[(int64_t)lv * inner];
+      int rank = 0;  // #classes ahead of the label in Caffe's (value, index) descending order
+      for (int c = lane; c < C; c += 64) {
+        const float u = xs[(int64_t)c * inner];
+        rank += (u > v) || (u == v && c > lv);
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) rank += __shfl_xor(rank, off, 64);
+      hit = rank < top_k;
+      cnt = 1;
+    }
+  }
+  if (lane == 0) {
+    sa[wave] = hit;
+    sc[wave] = cnt;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    g_acc_part[2 * blockIdx.x] = sa[0] + sa[1] + sa[2] + sa[3];
+    g_acc_part[2 * blockIdx.x + 1] = sc[0] + sc[1] + sc[2] + sc[3];
+    __threadfence();
+    last = atomicAdd(&g_acc_ticket, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  if (threadIdx.x == 0) {
+    // integer sums: exact in any order (< 2^24, host check), written as floats
+    int A = 0, N = 0;
+    for (unsigned b = 0; b < gridDim.x; ++b) {
+      A += __hip_atomic_load(&g_acc_part[2 * b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      N += __hip_atomic_load(&g_acc_part[2 * b + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *correct = static_cast<float>(A);
+    *count = static_cast<float>(N);
+    if (ratio) *ratio = static_cast<float>(A) / static_cast<float>(N > 0 ? N : 1);
+    g_acc_ticket = 0u;
+  }
+}
 // Single-launch form for small heads (columns x classes <= kAccSmall, classes
 // <= 64: the configs' TEST batches of CIFAR / LeNet): one block, a thread per
 // column looping over the classes (independent loads, so one memory latency),
@@ -804,6 +867,11 @@ int rram_accuracy(const float* x, const float* label, float* correct, float* cou
   if (cols * C <= kAccSmall && C <= 64) {
     hipLaunchKernelGGL(k_accuracy_small, dim3(1), dim3(1024), 0, as_stream(s), x, label, correct, count, ratio,
                        outer, C, inner, top_k, ignore);
+    return launch_status("accuracy");
+  }
+  if (cols > 0 && (cols + 3) / 4 <= kAccFusedBlocks) {
+    hipLaunchKernelGGL(k_accuracy_fused, dim3(static_cast<unsigned>((cols + 3) / 4)), dim3(256), 0, as_stream(s), x,
+                       label, correct, count, ratio, outer, C, inner, top_k, ignore);
     return launch_status("accuracy");
   }
   RRAM_HIP_RET(hipMemsetAsync(correct, 0, sizeof(float), as_stream(s)));

@@ -632,16 +632,21 @@ def test_im2col_col2im_vs_oracle(device, oracle_mod):
 
 
 # ---------------------------------------------------------- support layers
-@pytest.mark.parametrize("outer,C,inner,ignore", [(100, 10, 1, -1), (7, 10, 5, 3), (64, 64, 1, -1), (1, 2, 1, -1)])
+@pytest.mark.parametrize("outer,C,inner,ignore", [(100, 10, 1, -1), (7, 10, 5, 3), (64, 64, 1, -1), (1, 2, 1, -1),
+                                                  (256, 1000, 1, -1), (50, 1000, 1, 7), (3, 100, 50, -1),
+                                                  (20000, 100, 1, -1)])
 def test_accuracy_small_head_single_launch(device, oracle_mod, outer, C, inner, ignore):
-    """The one-block accuracy (classes <= 64) == the oracle, with ties, an ignore
-    label, spatial positions, and the ratio output (top-1 and top-3)."""
+    """Accuracy == the restated AccuracyLayer, with ties, an ignore label,
+    spatial positions, and the ratio output (top-1 and top-3), twice per case:
+    the one-block kernel (classes <= 64), the single-launch multi-block kernel
+    (per-block slots + last-block sum; its ticket re-arms itself, so the
+    second call must agree), and past 4096 blocks the atomics + ratio form."""
     import torch
     from rramsim import ops
     rng = np.random.default_rng(outer + C)
     x = rng.integers(-3, 4, (outer, C, inner)).astype(np.float32)   # many exact ties
     label = rng.integers(0, C, (outer, inner)).astype(np.float32)
-    for k in (1, 3):
+    for k in (1, 3, 1):
         if k > C:
             continue
         cor, cnt, ratio = (torch.full((1,), -5.0, device=device) for _ in range(3))
