@@ -12,8 +12,11 @@ data-path collective); one RCCL all-reduce of the statistics closes the job.
 
 Prints ONE JSON line (rank 0):
   value = images classified under faults per second, summed over ranks
-  roofline = the conv/IP contractions (dominant kernels) vs the peak of the
-             engine each runs on (fp32 MFMA, or the bf16x6 split: bf16 peak / 6)
+  roofline = the dominant kernel (conv2, k_conv_cb_x6 5x5) vs the peak of
+             its engine (bf16x6 split: bf16 dense peak / 6), hipEvents around
+             its layer in the timed region; `contractions` = all conv / IP
+             layers vs their engines' peaks, timed over K further maps after
+             the timed region (events around 8 layers cost ~1 % of a step)
   roofline_inject = the injection kernel vs HBM peak
   cpu_baseline = Caffe CPU mode restated in C (oracle/caffe_cpu.c: per-image
                  im2col + cblas_sgemm, Fail_cpu) over one full map, rank 0 at N=1.
@@ -39,6 +42,11 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: bf16 dense MFMA (no spars
 # fp32 product: its roofline is the bf16 dense peak / 6 in fp32 FLOPs
 MFMA_X6_PEAK_TFLOPS = MFMA_BF16_PEAK_TFLOPS / 6.0
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
+# the dominant kernel of the step: conv2's k_conv_cb_x6<5,5,...> (22 % of GPU
+# time, profiles/r03_*_kernel_stats.csv); the only layer timed inside the
+# timed region, so the stream carries two markers per map for it
+DOMINANT_LAYER = "conv2"
+DOMINANT_PMC_CLASS = "conv2 k_conv_cb_x6<5,5,...>"
 
 
 def alexnet_gemm_table(batch):
@@ -121,6 +129,8 @@ def main():
     ap.add_argument("--seed", type=int, default=1701)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-layers", action="store_true", help="print the per-layer table to stderr")
+    ap.add_argument("--layer-events", choices=["dominant", "none"], default="dominant",
+                    help="hipEvents in the timed region: around the dominant kernel's layer (roofline) or none")
     ap.add_argument("--workload", default="alexnet_mc",
                     choices=["alexnet_mc", "cifar10_quick_mc", "cifar10_full_train", "googlenet_sweep", "lenet_train",
                              "lenet_mc"],
@@ -163,7 +173,7 @@ def main():
 
     net = caffe.Net(models.alexnet(test_batch=args.batch), "test", models.net_options("alexnet"))
     cfg = make_inject_cfg(args.p_fault)             # reference stuck-at semantics, neg/zero/pos 10/20/10
-    mc = caffe.MonteCarlo(net, cfg, seed=args.seed, max_maps=args.steps + args.warmup + 8)
+    mc = caffe.MonteCarlo(net, cfg, seed=args.seed, max_maps=2 * args.steps + args.warmup + 8)
 
     def step(i):
         mc.run(rank + world * i, 1)                 # map m on rank m mod N
@@ -174,7 +184,12 @@ def main():
     mc.reset()
     net.layer_times(reset=True)
     mc.inject_times(reset=True)
-    net.set_timing(1 if args.profile_layers else 2)   # events only around conv / IP unless profiling
+    if args.profile_layers:
+        net.set_timing(1)
+    elif args.layer_events == "dominant":
+        net.set_timing_layer(DOMINANT_LAYER)
+    else:
+        net.set_timing(0)
     mc.set_timing(True)
 
     stats = torch.zeros(8, dtype=torch.float64, device=dev)
@@ -199,20 +214,31 @@ def main():
     torch.cuda.synchronize()
     elapsed = float(t.item())
 
-    # ---- roofline from the live hipEvent layer timings of the timed region
-    lt = net.layer_times()
+    # ---- roofline of the dominant kernel: live hipEvents of the timed region
+    lt_timed = net.layer_times(reset=True)
+    # ---- contraction table: K further maps, untimed for `value`, with events
+    # around every conv / IP layer (each rank on its own maps, no collective)
+    if not args.profile_layers:
+        net.set_timing(2)
+        for i in range(args.steps):
+            step(args.warmup + args.steps + i)
+        torch.cuda.synchronize()
+        net.set_timing(False)
+        lt = net.layer_times()
+    else:
+        lt = lt_timed
     flops = alexnet_gemm_table(args.batch)
     engines = alexnet_engines(args.batch)
     gemm_ms = sum(ms for (name, typ, ms, cnt) in lt if name in flops) / args.steps
     gemm_flops = sum(flops.values())
-    achieved_tf = gemm_flops / (gemm_ms * 1e-3) / 1e12
+    achieved_tf = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0
     # the roofline of the mixed-engine layer set: each layer's FLOPs at its
     # engine's peak; effective peak = total FLOPs / that minimum time
     peak_of = {"f32": MFMA_F32_PEAK_TFLOPS, "bf16x6": MFMA_X6_PEAK_TFLOPS}
     t_min = sum(f / (peak_of[engines[n]] * 1e12) for n, f in flops.items())
     peak_tf = gemm_flops / t_min / 1e12
     layers = {name: {"engine": engines[name], "ms": round(ms / args.steps, 4),
-                     "tflops": round(flops[name] / (ms / args.steps * 1e-3) / 1e12, 1)}
+                     "tflops": round(flops[name] / (ms / args.steps * 1e-3) / 1e12, 1) if ms > 0 else None}
               for (name, typ, ms, cnt) in lt if name in flops}
     inj_ms, inj_n, inj_w = mc.inject_times()
     inj_ms_per = inj_ms / max(inj_n, 1)
@@ -222,6 +248,10 @@ def main():
             print(f"{name:>12s} {typ:>16s} {ms / max(cnt, 1):9.3f} ms", file=sys.stderr)
 
     traffic = load_traffic()
+    dom_ms = {name: ms for (name, typ, ms, cnt) in lt_timed}.get(DOMINANT_LAYER, 0.0) / args.steps
+    dom_tf = flops[DOMINANT_LAYER] / (dom_ms * 1e-3) / 1e12 if dom_ms > 0 else 0.0
+    dom_peak = peak_of[engines[DOMINANT_LAYER]]
+    dom_pmc = traffic.get("per_kernel", {}).get(DOMINANT_PMC_CLASS, {})
     n_images = world * args.steps * args.batch
     value = n_images / elapsed
     out_names = [k for k in net.outputs().keys()]
@@ -247,14 +277,27 @@ def main():
                                    if distributed else "mc-maps x1 (single process, no collective)"),
                    "f32_engine": "bf16x6 (exact 3-term bf16 split, 6 products, fp32 accumulation)"
                    if "bf16x6" in engines.values() else "f32 MFMA"},
-        "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 2), "peak": round(peak_tf, 1),
-                     "unit": "TFLOP/s", "frac": round(achieved_tf / peak_tf, 4),
-                     "traffic": traffic.get("gemm", {}).get("bytes_per_step"),
-                     "kernel": "conv1-5 + fc6-8 forward contractions per step; peak = each layer's engine peak "
-                               "(f32: v_mfma_f32_32x32x2_f32 157.3; bf16x6: bf16 dense 2500 / 6 products = 416.7)",
-                     "frac_of_f32_mfma_peak": round(achieved_tf / MFMA_F32_PEAK_TFLOPS, 4),
-                     "algorithmic_flops_per_step": gemm_flops, "avg_ms_per_step": round(gemm_ms, 4),
-                     "layers": layers},
+        "roofline": {"bound": "mfma", "achieved": round(dom_tf, 2), "peak": round(dom_peak, 1), "unit": "TFLOP/s",
+                     "frac": round(dom_tf / dom_peak, 4),
+                     "traffic": (dom_pmc["measured_MB_per_step"] * 1e6 if dom_pmc.get("measured_MB_per_step")
+                                 else None),
+                     "kernel": f"k_conv_cb_x6<5,5,4,8,15> = AlexNet {DOMINANT_LAYER} ({engines[DOMINANT_LAYER]} engine, "
+                               "one launch per map), hipEvents around its layer over the timed region; peak = "
+                               "bf16 dense 2500 / 6 products = 416.7 (f32 engine: v_mfma_f32_32x32x2_f32 157.3)",
+                     "algorithmic_flops_per_launch": flops[DOMINANT_LAYER],
+                     "algorithmic_bytes_per_launch": (dom_pmc["algorithmic_MB_per_step"] * 1e6
+                                                      if dom_pmc.get("algorithmic_MB_per_step") else None),
+                     "avg_us_per_launch": round(dom_ms * 1e3, 2),
+                     "contractions": {
+                         "achieved": round(achieved_tf, 2), "peak": round(peak_tf, 1), "unit": "TFLOP/s",
+                         "frac": round(achieved_tf / peak_tf, 4) if peak_tf else None,
+                         "frac_of_f32_mfma_peak": round(achieved_tf / MFMA_F32_PEAK_TFLOPS, 4),
+                         "traffic": traffic.get("gemm", {}).get("bytes_per_step"),
+                         "algorithmic_flops_per_step": gemm_flops, "avg_ms_per_step": round(gemm_ms, 4),
+                         "layers": layers,
+                         "note": ("conv1-5 + fc6-8 forward, each layer at its engine's peak; hipEvents around every "
+                                  "conv / IP layer over K further maps after the timed region"
+                                  if not args.profile_layers else "every layer timed inside the timed region")}},
         "roofline_inject": {"bound": "hbm", "achieved": round(inj_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                             "frac": round(inj_gbps / HBM_PEAK_GBPS, 4),
                             "traffic": traffic.get("inject", {}).get("bytes_per_launch"),

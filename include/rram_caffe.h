@@ -106,6 +106,9 @@ int rram_net_alias_flat_params(rram_net_t net, float* data, float* diff);
  * layer_times synchronises and returns total ms and launch count per layer
  * since the last reset. */
 int rram_net_set_timing(rram_net_t net, int enable);
+/* Events around one layer only (index into the net's layers): the live
+ * timing of a single kernel with the fewest markers in the stream. */
+int rram_net_set_timing_layer(rram_net_t net, int layer);
 int rram_net_layer_times(rram_net_t net, double* ms, long* counts, int cap, int* n, int reset);
 /* Host-only structural view (no device): phase filter + split insertion;
  * writes "name\ttype\tbottoms\ttops\n" lines into out (cap bytes);

@@ -2,8 +2,11 @@
 // the arithmetic of the layers it merges: every intermediate value is the one
 // the unfused kernels produce, only its round trip through HBM disappears.
 #include <float.h>
+#include <limits.h>
 #include <math.h>
 #include <stdlib.h>
+
+#include <type_traits>
 
 #include "rram_common.hpp"
 #include "split3.hpp"
@@ -33,9 +36,10 @@ namespace {
 constexpr int kBandPix = 512;  // input pixels per band (PPT = 2 per thread)
 // target grid of the LRN + pool band kernel: several block waves of 256 CUs
 constexpr int kLrnBlocks = 4096;
+constexpr int kLrnG = 2;
 
-// G channels per barrier; the loads run one group ahead.  Measured on MI355X
-// (AlexNet b256): G = 2 for norm1 (55 x 55 planes), G = 4 for norm2 (27 x 27).
+// G channels per barrier (kLrnG = 2: measured on MI355X for both AlexNet
+// planes once the loads run 8 channels ahead; G = 4 spilled SGPRs).
 // OCT: also write y's channel-octet companion yo (the next convolution's
 // pre-split input, x6.hip k_pack_octets_x6 layout [num][C/8][PH][PW][3][8]
 // bf16): the pooled values of 8 channels are gathered in an LDS plane and
@@ -44,69 +48,87 @@ constexpr int kLrnBlocks = 4096;
 // wholly inside the image reads its K x K taps at immediate LDS offsets with
 // no per-tap mask (3 instructions a tap instead of ~6; every AlexNet window
 // is such, the ceil rule clips none); WT = 0: any W.
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 template <int K, int SIZE, int G, bool OCT, int WT = 0>
 __global__ void __launch_bounds__(256)
     k_lrn_maxpool_band(const float* __restrict__ x, float* __restrict__ y, char* __restrict__ yo, int C, int H, int W,
-                       int PH, int PW, int sh, int sw, int ph, int pw, int RB, int CC, float alpha_over_size,
-                       float beta, float k) {
+                       int PH, int PW, int sh, int sw, int ph, int pw, int RB, int CC, int bands, int chunks,
+                       float alpha_over_size, float beta, float k) {
   static_assert(!OCT || (8 % (2 * G) == 0), "the octet walk needs G in {2, 4}");
+  static_assert(kBandPix == 2 * 256, "two pixels per thread: the packed LRN pair");
   constexpr int PRE = (SIZE - 1) / 2;
   constexpr int D = G;
-  constexpr int PPT = kBandPix / 256;
   __shared__ float ybuf[2][D][kBandPix];
   __shared__ float obuf[OCT ? 8 : 1][OCT ? 256 : 1];
-  const int n = blockIdx.y;
-  const int cb = blockIdx.z * CC;
+  // XCD-aware tile order: consecutive workgroups go to the 8 XCDs in turn, so
+  // workgroup L runs on XCD L % 8 as that XCD's (L / 8)-th; each XCD gets a
+  // contiguous range of tiles in (image, chunk, band) order, band fastest.
+  // Tiles that read the same input rows (adjacent bands share a row, adjacent
+  // chunks share the LRN halo channels) then run on one XCD close in time, and
+  // the second read can hit that XCD's L2 instead of going to HBM.
+  const int total = bands * chunks * static_cast<int>(gridDim.y);  // gridDim.y = images
+  const int L = blockIdx.x + static_cast<int>(gridDim.x) * blockIdx.y;
+  const int xq = total / 8, xr = total % 8, xcd = L % 8, xk = L / 8;
+  const int tile = xcd < xr ? xcd * (xq + 1) + xk : xr * (xq + 1) + (xcd - xr) * xq + xk;
+  const int band = tile % bands, rest = tile / bands;
+  const int n = rest / chunks;
+  const int cb = (rest - n * chunks) * CC;
   const int ce = min(C, cb + CC);
-  const int pr0 = blockIdx.x * RB;
+  const int pr0 = band * RB;
   const int pr1 = min(PH, pr0 + RB);
   const int h0 = max(0, pr0 * sh - ph);
   const int h1 = min(H, (pr1 - 1) * sh - ph + K);  // exclusive
   const int NP = (h1 - h0) * W;
   const int HW = H * W;
-  const float* xb = x + (int64_t)n * C * HW + (int64_t)h0 * W;
-  int pix[PPT];
-  bool own[PPT];
-#pragma unroll
-  for (int q = 0; q < PPT; ++q) {
-    pix[q] = threadIdx.x + q * 256;
-    own[q] = pix[q] < NP;
-  }
-  // buffer loads with 32-bit offsets from the band's first row (one image is
-  // < 2 GiB: host check); a channel outside [0, C) or a pixel outside the band
-  // reads past the range, i.e. zero
-  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(xb), 0, static_cast<int>(((int64_t)C * HW - (int64_t)h0 * W) * 4), 0x00020000);
-  auto ld = [&](int q, int cc) {
-    const uint32_t off = (cc >= 0 && cc < C && own[q]) ? static_cast<uint32_t>((cc * HW + pix[q]) * 4) : 0x80000000u;
-    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xrs, static_cast<int>(off), 0, 0));
+  // the thread's two pixels of the band: threadIdx.x and threadIdx.x + 256
+  const int pix0 = threadIdx.x, pix1 = threadIdx.x + 256;
+  const bool own0 = pix0 < NP, own1 = pix1 < NP;
+  // channel cc's band is read through a buffer resource of its own (base and
+  // range are uniform: scalar work), so a load is one instruction at a lane
+  // offset fixed for the whole walk; a pixel outside the band reads at 2^31,
+  // a channel outside [0, C) through an empty range: zero either way
+  const char* xband = reinterpret_cast<const char*>(x + (int64_t)n * C * HW + (int64_t)h0 * W);
+  const int vo0 = own0 ? pix0 * 4 : INT_MIN, vo1 = own1 ? pix1 * 4 : INT_MIN;
+  auto ld = [&](int cc) {
+    const bool in = cc >= 0 && cc < C;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<char*>(xband) + (in ? (int64_t)cc * HW * 4 : 0), 0, in ? NP * 4 : 0, 0x00020000);
+    return f32x2{__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo0, 0, 0)),
+                 __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo1, 0, 0))};
   };
-  // win[q][j] = x at channel (c0 - PRE + j) of pixel q, zero outside [0, C).
-  // The entering channels of group g + 2 are loaded at the top of group g
-  // into one of two staging arrays (st0 / st1, alternating by group parity so
-  // the registers are named statically) and moved into the ring at the bottom
-  // of group g + 1: two groups of loads stay in flight across the LDS / pool
-  // work, instead of one group whose loads the ring shift waits for.
-  float win[PPT][SIZE + D];
-  float st0[D][PPT], st1[D][PPT];
+  // win[j] = both pixels at channel (c0 - PRE + j), zero outside [0, C).
+  // NS staging arrays rotate by group (st[g % NS], so the registers are named
+  // statically): the entering channels of group g + NS are loaded at the top
+  // of group g and moved into the ring at the bottom of group g + NS - 1, so
+  // NS groups of loads (NS * D channels) stay in flight across the LDS / pool
+  // work.  With octets NS = 8 / D (the octet's groups, 8 channels ahead),
+  // else 2.
+  constexpr int NS = OCT ? 8 / D : 2;
+  f32x2 win[SIZE + D];
+  f32x2 st[NS][D];
 #pragma unroll
-  for (int q = 0; q < PPT; ++q)
+  for (int j = 0; j < SIZE + D; ++j) win[j] = ld(cb + j - PRE);
 #pragma unroll
-    for (int j = 0; j < SIZE + D; ++j) win[q][j] = ld(q, cb + j - PRE);
+  for (int j = 1; j < NS; ++j)  // the entering channels of groups 1 .. NS - 1
 #pragma unroll
-  for (int d = 0; d < D; ++d)
-#pragma unroll
-    for (int q = 0; q < PPT; ++q) st1[d][q] = ld(q, cb + SIZE + D - PRE + d);  // group 1's entering channels
+    for (int d = 0; d < D; ++d) st[j][d] = ld(cb - PRE + SIZE + j * D + d);
   const int NO = (pr1 - pr0) * PW;  // pooled outputs of the band per channel
-  const int64_t PHW = (int64_t)PH * PW;
-  float* yn = y + (int64_t)n * C * PHW;
+  const int PHW = PH * PW;
+  // y of image n through a buffer resource too (one image < 2 GiB: host check)
+  const __amdgpu_buffer_rsrc_t yrs =
+      __builtin_amdgcn_make_buffer_rsrc(y + (int64_t)n * C * PHW, 0, C * PHW * 4, 0x00020000);
   // pooling items of a group: (channel d, output o), consecutive outputs of
   // one channel on consecutive lanes (coalesced stores); each thread's items
   // and their windows are fixed for the whole channel walk, so they are
   // decoded once here: LDS base of the window, tap validity (the window
-  // clipped to the image), output offset
+  // clipped to the image), output byte offset from the group's first channel
   constexpr int MAXI = D;  // D * NO <= D * 256 items
-  int it_d[MAXI], it_l[MAXI], it_out[MAXI];
+  int it_d[MAXI], it_l[MAXI], it_out[MAXI], it_vo[MAXI];
   uint32_t it_ok[MAXI];
 #pragma unroll
   for (int i = 0; i < MAXI; ++i) {
@@ -125,25 +147,24 @@ __global__ void __launch_bounds__(256)
     it_d[i] = it < D * NO ? d : D;  // D = no item
     it_l[i] = (hr - h0) * W + wr;
     it_out[i] = (pr0 + prl) * PW + pwi;
+    it_vo[i] = (d * PHW + it_out[i]) * 4;
     it_ok[i] = ok;
   }
-  // one channel group: c0 = its first channel, yb = its LDS plane buffer
-  auto group = [&](int c0, float (*yb)[kBandPix], float (&load_into)[D][PPT], const float (&fill_from)[D][PPT]) {
+  // one channel group: c0 = its first channel, yb = its LDS plane buffer,
+  // gi = its place in the staging rotation (g % NS)
+  auto group = [&](int c0, float (*yb)[kBandPix], auto gi) {
+    constexpr int GI = decltype(gi)::value;
+    f32x2(&load_into)[D] = st[GI];
+    const f32x2(&fill_from)[D] = st[(GI + 1) % NS];
 #pragma unroll
-    for (int d = 0; d < D; ++d)
-#pragma unroll
-      for (int q = 0; q < PPT; ++q) load_into[d][q] = ld(q, c0 - PRE + SIZE + 2 * D + d);
+    for (int d = 0; d < D; ++d) load_into[d] = ld(c0 - PRE + SIZE + NS * D + d);
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-#pragma unroll
-      for (int q = 0; q < PPT; ++q) {
-        // the helpers k_lrn_fwd_slide uses, in the same order
-        float acc = 0.0f;
-#pragma unroll
-        for (int j = 0; j < SIZE; ++j) acc = lrn_sq_add(acc, win[q][d + j]);
-        const float v = lrn_out(win[q][d + PRE], lrn_scale(acc, alpha_over_size, k), beta);
-        if (own[q]) yb[d][pix[q]] = v;
-      }
+      // lrn_sq_add / lrn_scale / lrn_out (the unfused kernels' arithmetic) on
+      // both pixels at once
+      const f32x2 v = lrn_value2<SIZE>(win + d, alpha_over_size, beta, k);
+      if (own0) yb[d][pix0] = v.x;
+      if (own1) yb[d][pix1] = v.y;
     }
     __syncthreads();
     // pool the group's D channels (MaxPoolForward: -FLT_MAX start, strict ">"
@@ -156,13 +177,23 @@ __global__ void __launch_bounds__(256)
         const float* yl = yb[d] + it_l[i];
         float mv = -FLT_MAX;
         if (WT > 0 && it_ok[i] == (1u << (K * K)) - 1u) {
+          float t[K * K];
 #pragma unroll
           for (int a = 0; a < K; ++a)
 #pragma unroll
-            for (int b = 0; b < K; ++b) {
-              const float v = yl[a * WT + b];
-              mv = v > mv ? v : mv;
-            }
+            for (int b = 0; b < K; ++b) t[a * K + b] = yl[a * WT + b];
+          // v_max3 over the taps: the strict-">" walk's value whenever the
+          // maximum is not zero (a quiet NaN loses to any number in both; the
+          // plane holds products, never a signalling NaN); for a zero maximum
+          // the walk keeps the FIRST zero's sign where v_max takes +0 over
+          // -0, so such a window is walked again in order
+#pragma unroll
+          for (int j = 0; j < K * K; j += 2) mv = max3f(mv, t[j], t[j + 1 < K * K ? j + 1 : j]);
+          if (mv == 0.0f) {
+            mv = -FLT_MAX;
+#pragma unroll
+            for (int j = 0; j < K * K; ++j) mv = t[j] > mv ? t[j] : mv;
+          }
         } else {
 #pragma unroll
           for (int a = 0; a < K; ++a)
@@ -173,32 +204,32 @@ __global__ void __launch_bounds__(256)
               if (ok && v > mv) mv = v;
             }
         }
-        yn[(int64_t)(c0 + d) * PHW + it_out[i]] = mv;
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, mv), yrs, it_vo[i], c0 * PHW * 4, 0);
         if (OCT) obuf[(c0 + d) & 7][it_out[i] - pr0 * PW] = mv;
       }
     }
 #pragma unroll
-    for (int q = 0; q < PPT; ++q) {
+    for (int j = 0; j < SIZE; ++j) win[j] = win[j + D];
 #pragma unroll
-      for (int j = 0; j < SIZE; ++j) win[q][j] = win[q][j + D];
-#pragma unroll
-      for (int d = 0; d < D; ++d) win[q][SIZE + d] = fill_from[d][q];
-    }
+    for (int d = 0; d < D; ++d) win[SIZE + d] = fill_from[d];
   };
+  using G0 = std::integral_constant<int, 0>;
+  using G1 = std::integral_constant<int, 1>;
   if (!OCT) {
     for (int c0 = cb; c0 < ce; c0 += 2 * D) {
-      group(c0, ybuf[0], st0, st1);
-      if (c0 + D < ce) group(c0 + D, ybuf[1], st1, st0);
+      group(c0, ybuf[0], G0{});
+      if (c0 + D < ce) group(c0 + D, ybuf[1], G1{});
     }
     return;
   }
   // OCT: 8 channels per step (an even number of groups), then the octet
   char* yon = yo + (int64_t)n * (C / 8) * PHW * 48;
   for (int c0 = cb; c0 < ce; c0 += 8) {
-#pragma unroll
-    for (int g = 0; g < 8; g += 2 * D) {
-      group(c0 + g, ybuf[0], st0, st1);
-      group(c0 + g + D, ybuf[1], st1, st0);
+    group(c0, ybuf[0], G0{});
+    group(c0 + D, ybuf[1], G1{});
+    if constexpr (NS == 4) {  // D == 2 with octets
+      group(c0 + 4, ybuf[0], std::integral_constant<int, 2>{});
+      group(c0 + 6, ybuf[1], std::integral_constant<int, 3>{});
     }
     __syncthreads();  // obuf complete (the next group's barrier orders its rewrite)
     const int o = threadIdx.x;
@@ -239,7 +270,8 @@ int rram_lrn_maxpool_fwd_octets(const float* x, float* y, void* y_oct, int num, 
   RRAM_REQUIRE(ph < kernel && pw < kernel, "lrn_maxpool_fwd: pad must be < kernel");
   RRAM_REQUIRE((int64_t)num * C * H * W < 2147483647ll && (int64_t)num * C * PH * PW < 2147483647ll,
                "lrn_maxpool_fwd: more than 2^31 elements is not supported");
-  RRAM_REQUIRE((int64_t)C * H * W * 4 < 2147483647ll, "lrn_maxpool_fwd: one image must be < 2 GiB");
+  RRAM_REQUIRE((int64_t)C * H * W * 4 < 2147483647ll && (int64_t)C * PH * PW * 4 < 2147483647ll,
+               "lrn_maxpool_fwd: one image must be < 2 GiB");
   if (num == 0) return RRAM_OK;
   RRAM_REQUIRE(x && y, "lrn_maxpool_fwd: NULL");
   // band height: input rows of RB pooled rows must fit the block's pixel
@@ -251,47 +283,42 @@ int rram_lrn_maxpool_fwd_octets(const float* x, float* y, void* y_oct, int num, 
   RRAM_REQUIRE(fits(1), "lrn_maxpool_fwd: a pooled row needs more than %d input pixels", kBandPix);
   int rb = 1;
   while (rb < PH && fits(rb + 1)) ++rb;
-  // channels per barrier: measured G = 2 for 55 x 55 planes, 4 for 27 x 27
-  const int gsel = H * W >= 1024 ? 2 : 4;
   // channel chunks: as few as give >= kLrnBlocks blocks (each chunk re-reads
   // SIZE - 1 halo channels), equal sizes in multiples of 8 (2 * G without octets)
-  const int step = y_oct ? 8 : 2 * gsel;
-  const int64_t bands = (PH + rb - 1) / rb;
+  const int step = y_oct ? 8 : 2 * kLrnG;
+  const int bands = (PH + rb - 1) / rb;
   const int64_t tiles = (int64_t)num * bands;  // > 0
   const int64_t want = ((int64_t)kLrnBlocks + tiles - 1) / tiles;
   const int64_t most = (C + step - 1) / step;
   const int chunks = static_cast<int>(want < 1 ? 1 : (want > most ? most : want));
   const int cc = ((C + chunks - 1) / chunks + step - 1) / step * step;
-  const dim3 grid(static_cast<unsigned>(bands), static_cast<unsigned>(num), static_cast<unsigned>((C + cc - 1) / cc));
+  const int nchunks = (C + cc - 1) / cc;
+  RRAM_REQUIRE((int64_t)bands * nchunks * num < 2147483647ll && num < 65536, "lrn_maxpool_fwd: grid too large");
+  // (bands x chunks, images): the kernel maps the linear workgroup id to an
+  // XCD-local tile order itself
+  const dim3 grid(static_cast<unsigned>(bands * nchunks), static_cast<unsigned>(num));
   const float aos = alpha / size;
   char* yo = static_cast<char*>(y_oct);
-#define RRAM_LP3(K_, S_, G_, WT_)                                                                             \
-  if (yo)                                                                                                     \
-    hipLaunchKernelGGL((k_lrn_maxpool_band<K_, S_, G_, true, WT_>), grid, dim3(kThreads), 0, as_stream(s), x, y, \
-                       yo, C, H, W, PH, PW, sh, sw, ph, pw, rb, cc, aos, beta, k);                            \
-  else                                                                                                        \
-    hipLaunchKernelGGL((k_lrn_maxpool_band<K_, S_, G_, false, WT_>), grid, dim3(kThreads), 0, as_stream(s), x, \
-                       y, yo, C, H, W, PH, PW, sh, sw, ph, pw, rb, cc, aos, beta, k);
-#define RRAM_LP2(K_, S_, G_)                               \
-  if (K_ == 3 && S_ == 5 && W == 55) {                     \
-    RRAM_LP3(K_, S_, G_, (K_ == 3 && S_ == 5 ? 55 : 0))    \
-  } else if (K_ == 3 && S_ == 5 && W == 27) {              \
-    RRAM_LP3(K_, S_, G_, (K_ == 3 && S_ == 5 ? 27 : 0))    \
-  } else {                                                 \
-    RRAM_LP3(K_, S_, G_, 0)                                \
-  }
-#define RRAM_LP(K_, S_)          \
-  if (kernel == K_ && size == S_) { \
-    if (gsel == 2) {             \
-      RRAM_LP2(K_, S_, 2)        \
-    } else {                     \
-      RRAM_LP2(K_, S_, 4)        \
-    }                            \
+#define RRAM_LP3(K_, S_, WT_)                                                                                      \
+  if (yo)                                                                                                          \
+    hipLaunchKernelGGL((k_lrn_maxpool_band<K_, S_, kLrnG, true, WT_>), grid, dim3(kThreads), 0, as_stream(s), x, y, \
+                       yo, C, H, W, PH, PW, sh, sw, ph, pw, rb, cc, bands, nchunks, aos, beta, k);                 \
+  else                                                                                                             \
+    hipLaunchKernelGGL((k_lrn_maxpool_band<K_, S_, kLrnG, false, WT_>), grid, dim3(kThreads), 0, as_stream(s), x,  \
+                       y, yo, C, H, W, PH, PW, sh, sw, ph, pw, rb, cc, bands, nchunks, aos, beta, k);
+#define RRAM_LP(K_, S_)                                  \
+  if (kernel == K_ && size == S_) {                      \
+    if (K_ == 3 && S_ == 5 && W == 55) {                 \
+      RRAM_LP3(K_, S_, (K_ == 3 && S_ == 5 ? 55 : 0))    \
+    } else if (K_ == 3 && S_ == 5 && W == 27) {          \
+      RRAM_LP3(K_, S_, (K_ == 3 && S_ == 5 ? 27 : 0))    \
+    } else {                                             \
+      RRAM_LP3(K_, S_, 0)                                \
+    }                                                    \
   }
   RRAM_LP(3, 5)
   else RRAM_LP(3, 3) else RRAM_LP(2, 5) else RRAM_LP(2, 3)
 #undef RRAM_LP
-#undef RRAM_LP2
 #undef RRAM_LP3
   return launch_status("lrn_maxpool_fwd");
 }

@@ -574,13 +574,28 @@ __global__ void __launch_bounds__(256) k_accuracy_fused(const float* __restrict_
   __syncthreads();
   if (!last) return;
   __threadfence();
+  // integer sums: exact in any order (< 2^24, host check), written as floats;
+  // the slots are read by all 256 threads at once (one memory latency, not
+  // one per block) and reduced through the waves
+  int A = 0, N = 0;
+  for (unsigned b = threadIdx.x; b < gridDim.x; b += 256) {
+    A += __hip_atomic_load(&g_acc_part[2 * b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    N += __hip_atomic_load(&g_acc_part[2 * b + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    A += __shfl_xor(A, off, 64);
+    N += __shfl_xor(N, off, 64);
+  }
+  __syncthreads();  // every wave is past its reads of sa / sc
+  if (lane == 0) {
+    sa[wave] = A;
+    sc[wave] = N;
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
-    // integer sums: exact in any order (< 2^24, host check), written as floats
-    int A = 0, N = 0;
-    for (unsigned b = 0; b < gridDim.x; ++b) {
-      A += __hip_atomic_load(&g_acc_part[2 * b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      N += __hip_atomic_load(&g_acc_part[2 * b + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    A = sa[0] + sa[1] + sa[2] + sa[3];
+    N = sc[0] + sc[1] + sc[2] + sc[3];
     *correct = static_cast<float>(A);
     *count = static_cast<float>(N);
     if (ratio) *ratio = static_cast<float>(A) / static_cast<float>(N > 0 ? N : 1);

@@ -117,6 +117,20 @@ __device__ __forceinline__ float lrn_scale(float acc, float alpha_over_size, flo
 __device__ __forceinline__ float lrn_out(float x, float scale, float beta) {
   return x * __builtin_amdgcn_exp2f(-beta * __builtin_amdgcn_logf(scale));
 }
+// The same three steps on two pixels at once: v_pk_fma_f32 / v_pk_mul_f32 are
+// two IEEE fmas / multiplies per instruction (half the issue of two scalar
+// ones), so each component is the scalar helpers' value bit for bit.
+// win[j] = the SIZE channels' values of the two pixels in channel order.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+template <int SIZE>
+__device__ __forceinline__ f32x2 lrn_value2(const f32x2* win, float alpha_over_size, float beta, float k) {
+  f32x2 acc = {0.0f, 0.0f};
+#pragma unroll
+  for (int j = 0; j < SIZE; ++j) acc = __builtin_elementwise_fma(win[j], win[j], acc);
+  const f32x2 sc = __builtin_elementwise_fma(acc, f32x2{alpha_over_size, alpha_over_size}, f32x2{k, k});
+  const f32x2 e = f32x2{-beta, -beta} * f32x2{__builtin_amdgcn_logf(sc.x), __builtin_amdgcn_logf(sc.y)};
+  return win[(SIZE - 1) / 2] * f32x2{__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
+}
 
 // 32-bit word -> uniform in (0, 1] (never 0: safe for log) and [0, 1).
 __host__ __device__ __forceinline__ float u01_open0(uint32_t r) {

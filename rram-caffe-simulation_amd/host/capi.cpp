@@ -343,6 +343,14 @@ int rram_net_set_timing(rram_net_t n, int enable) {
     n->net->set_timing(enable == 2 ? 2 : (enable != 0 ? 1 : 0));
   });
 }
+int rram_net_set_timing_layer(rram_net_t n, int layer) {
+  return guarded([&] {
+    NEED(n);
+    if (layer < 0 || layer >= static_cast<int>(n->net->layers().size()))
+      throw Error("set_timing_layer: layer index out of range");
+    n->net->set_timing_layer(layer);
+  });
+}
 int rram_net_layer_times(rram_net_t n, double* ms, long* counts, int cap, int* k, int reset) {
   return guarded([&] {
     NEED(n);

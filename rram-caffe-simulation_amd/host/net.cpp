@@ -333,7 +333,8 @@ std::string DescribeNet(const Msg& in_param, Phase phase) {
 template <typename Dtype>
 Dtype Net<Dtype>::ForwardFromTo(int start, int end, bool compute_loss) {
   for (int i = start; i <= end; ++i) {
-    const bool timed = timing_ == 1 || (timing_ == 2 && !layers_[i]->blobs().empty());
+    const bool timed = timing_ == 1 || (timing_ == 2 && !layers_[i]->blobs().empty()) ||
+                       (timing_ == 3 && i == timed_layer_);
     if (timed) timer_.start(i);
     layers_[i]->Forward(bottom_vecs_[i], top_vecs_[i]);
     if (timed) timer_.stop(i);

@@ -88,6 +88,12 @@ class Net {
   // per-layer forward timing with hipEvents (`caffe time`, tools/caffe.cpp:334-421):
   // 0 off, 1 every layer, 2 only layers that own parameters (conv / IP)
   void set_timing(int mode) { timing_ = mode; }
+  // events around layer i only (mode 3): one kernel's live timing at the
+  // least event overhead
+  void set_timing_layer(int i) {
+    timing_ = 3;
+    timed_layer_ = i;
+  }
   // convolution layers keep their packed weights between forwards while the
   // weights are unchanged (ConvolutionLayer::cache_wpack); off drops every pack
   void set_weight_pack_cache(bool on);
@@ -95,6 +101,7 @@ class Net {
 
  private:
   int timing_ = 0;
+  int timed_layer_ = -1;
   EventTimer timer_;
   Dtype* flat_diff_ = nullptr;  // set by alias_flat_params
   void AppendParam(int layer_id, int param_id, const Msg& layer_param);

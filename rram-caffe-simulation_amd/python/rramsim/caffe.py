@@ -46,6 +46,7 @@ SIGNATURES = {
     "rram_net_flat_param_count": (I, [P, PI64]),
     "rram_net_alias_flat_params": (I, [P, P, P]),
     "rram_net_set_timing": (I, [P, I]),
+    "rram_net_set_timing_layer": (I, [P, I]),
     "rram_net_layer_times": (I, [P, C.POINTER(C.c_double), C.POINTER(C.c_long), I, PI, I]),
     "rram_net_describe": (I, [C.c_char_p, I, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "rram_mc_set_timing": (I, [P, I]),
@@ -393,6 +394,13 @@ class Net:
     def set_timing(self, mode):
         """False/0 off, True/1 every layer, 2 only parameter layers (conv / IP)."""
         check(self._lib.rram_net_set_timing(self.h, int(mode)), "set_timing")
+
+    def set_timing_layer(self, name):
+        """hipEvents around the named layer only."""
+        idx = [i for i, (nm, _, _) in enumerate(self.layers()) if nm == name]
+        if not idx:
+            raise KeyError(name)
+        check(self._lib.rram_net_set_timing_layer(self.h, idx[0]), "set_timing_layer")
 
     def layer_times(self, reset=False):
         """[(layer name, type, total ms, launches)] since the last reset."""

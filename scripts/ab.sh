@@ -17,7 +17,7 @@ for r in $(seq 1 ${REPS:-2}); do
     python3 - "$O/v${i}_r$r.json" "$v" <<'PY'
 import json, sys
 d = json.load(open(sys.argv[1]))
-L = d["roofline"]["layers"]
+L = d["roofline"]["contractions"]["layers"]
 print(f"[{sys.argv[2]}] {d['value']:.0f} img/s  {d['ms_per_step']:.3f} ms/step  inject {d['roofline_inject']['avg_us_per_launch']:.0f} us  "
       + " ".join(f"{k} {v['ms']:.3f}" for k, v in L.items()), flush=True)
 PY

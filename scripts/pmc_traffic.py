@@ -18,7 +18,7 @@ import sys
 from collections import defaultdict
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
-forwards = int(sys.argv[2]) if len(sys.argv) > 2 else 4   # 1 warmup + 3 timed steps
+forwards = int(sys.argv[2]) if len(sys.argv) > 2 else 7   # 1 warmup + 3 timed + 3 contraction-table steps
 tot = defaultdict(float)       # (kernel class, counter) -> sum over dispatches
 cnt = defaultdict(int)         # (kernel class, counter) -> dispatches
 for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):

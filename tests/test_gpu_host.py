@@ -272,6 +272,13 @@ def test_layer_timing_and_flat_params(rs):
     net.forward()
     lt = net.layer_times(reset=True)
     assert all(c == 2 for _, _, _, c in lt) and sum(ms for _, _, ms, _ in lt) > 0
+    net.set_timing_layer("conv2")                      # one layer's events only (bench.py's timed region)
+    net.forward()
+    lt = net.layer_times(reset=True)
+    assert [(n, c) for n, _, ms, c in lt if c] == [("conv2", 1)] and [ms for n, _, ms, _ in lt if n == "conv2"][0] > 0
+    with pytest.raises(KeyError):
+        net.set_timing_layer("no_such_layer")
+    net.set_timing(False)
     n = net.flat_param_count()
     data = torch.empty(n, device="cuda")
     diff = torch.empty(n, device="cuda")

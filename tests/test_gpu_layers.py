@@ -207,6 +207,47 @@ def test_lrn_maxpool_fused_equals_unfused_alexnet_planes(device, C, H):
     assert torch.equal(fused, unfused) and torch.equal(fo, unfused)
 
 
+@pytest.mark.parametrize("C,H,W", [(96, 55, 55), (256, 27, 27), (32, 20, 23)])
+def test_lrn_maxpool_special_values_bitwise(device, C, H, W):
+    """Signed zeros (Caffe's ReLU writes -0 for negative inputs), +-Inf, NaN
+    and exact ties: the fused kernel's v_max3 windows (and their in-order
+    re-walk when the maximum is zero) give the unfused strict-">" pooling's
+    bits, sign of zero and NaN payload positions included."""
+    import torch
+    from rramsim import ops
+    g = torch.Generator().manual_seed(23)
+    N = 2
+    x = 4 * torch.randn(N, C, H, W, generator=g)
+    r = torch.rand(N, C, H, W, generator=g)
+    x = torch.where(x < 0, x * 0.0, x)                       # ReLU's -0
+    x = torch.where(r < 0.05, torch.zeros_like(x), x)        # +0 among the -0
+    x[:, 3] = -0.0                                           # whole planes of zeros
+    x[:, 4] = 0.0
+    x[:, 5] = torch.where(r[:, 5] < 0.5, -0.0, 0.0)
+    x.view(-1)[::4099] = float("inf")
+    x.view(-1)[7::5003] = -float("inf")
+    x.view(-1)[11::6007] = float("nan")
+    x[:, 6] = 2.5                                            # exact ties everywhere
+    x = x.to(device)
+    alpha, beta, kk = 1e-4, 0.75, 1.0
+    lrn = torch.empty_like(x)
+    ops.lrn_fwd(x, lrn, None, N, C, H, W, 5, alpha, beta, kk)
+    PH, PW = -(-(H - 3) // 2) + 1, -(-(W - 3) // 2) + 1
+    unfused = torch.empty((N, C, PH, PW), device=device)
+    ops.pool_fwd(lrn, unfused, None, (N, C, H, W, PH, PW, 3, 3, 2, 2, 0, 0), 0)
+    fused = torch.full_like(unfused, 7.0)
+    ops.lrn_maxpool_fwd(x, fused, N, C, H, W, PH, PW, 3, 2, 0, 5, alpha, beta, kk)
+    fo = torch.full_like(unfused, 7.0)
+    yo = torch.zeros(unfused.numel() * 6, dtype=torch.uint8, device=device)
+    ops.lrn_maxpool_fwd_octets(x, fo, yo, N, C, H, W, PH, PW, 3, 2, 0, 5, alpha, beta, kk)
+    torch.cuda.synchronize()
+    ub = unfused.cpu().view(torch.int32)
+    assert bool(torch.isnan(lrn).any()), "no NaN in the LRN planes"  # Inf inputs: Inf * Inf^-beta
+    assert bool((ub == -2**31).any()), "no -0 maximum in the case"
+    assert torch.equal(fused.cpu().view(torch.int32), ub)
+    assert torch.equal(fo.cpu().view(torch.int32), ub)
+
+
 def test_lrn_maxpool_fusion_in_alexnet_test_net(device):
     """Net folds norm1/norm2 into pool1/pool2 in the TEST phase; the net outputs
     are bit-identical to the unfused net."""
