@@ -310,8 +310,8 @@ constexpr int piece_lo(int s, int PD, int T) { return s >= T - 1 ? PD : (s * PD 
 // staging registers, written to LDS one tap later.  (An LDS-DMA weight ring
 // with hand-counted vmcnt measured slower: each DMA piece costs ~100 cycles
 // of issue among the MFMAs, and the ring paid 3 per group.)
-template <int KH, int KW, int WR, int NB, int PD>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+template <int KH, int KW, int WR, int NB, int PD, int OCC>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __restrict__ xpack, int octb, int rpc,
              uint32_t xrange, int ximg, char* __restrict__ yoct, int cout8, FastDiv oct_div, FastDiv rpc_div) {
   using namespace g2;
@@ -1330,15 +1330,16 @@ int pack_octets(const float* x, void* oct, int num, int C, int HWi, hipStream_t 
 
 // ---- k_conv_cb_x6 (channel-octet pre-split activations) ----
 struct CbPlan {
-  int WR, NB, RPC, PD, octb, tiles_m, tiles_n;
+  int WR, NB, RPC, PD, octb, tiles_m, tiles_n, OCC;
 };
-// instantiated (KH, WR, NB, PD) combinations
-#define RRAM_CB_LIST(X)                                                                                      \
-  X(5, 4, 8, 15) X(5, 4, 4, 12) X(5, 4, 4, 14) X(5, 2, 4, 14) X(3, 4, 8, 12) X(3, 4, 8, 15) X(3, 4, 4, 8) \
-  X(3, 4, 4, 12) X(3, 2, 4, 12) X(3, 2, 4, 14)
-bool cb_instantiated(int KH, int WR, int NB, int PD) {
-#define RRAM_X(kh, wr, nb, pd) \
-  if (KH == kh && WR == wr && NB == nb && PD == pd) return true;
+// instantiated (KH, WR, NB, PD, OCC) combinations; OCC = workgroups per CU
+#define RRAM_CB_LIST(X)                                                                              \
+  X(5, 4, 8, 15, 1) X(5, 4, 4, 12, 1) X(5, 4, 4, 14, 1) X(5, 2, 4, 14, 1) X(3, 4, 8, 12, 1)          \
+  X(3, 4, 8, 15, 1) X(3, 4, 4, 8, 1) X(3, 4, 4, 12, 1) X(3, 2, 4, 12, 1) X(3, 2, 4, 14, 1)          \
+  X(5, 4, 4, 8, 2) X(3, 4, 4, 8, 2)
+bool cb_instantiated(int KH, int WR, int NB, int PD, int OCC = 1) {
+#define RRAM_X(kh, wr, nb, pd, occ) \
+  if (KH == kh && WR == wr && NB == nb && PD == pd && OCC == occ) return true;
   RRAM_CB_LIST(RRAM_X)
 #undef RRAM_X
   return false;
@@ -1378,9 +1379,14 @@ bool conv_cb_plan(const rram_conv_desc* d, CbPlan& pl) {
     const int64_t cost = (nwg + 255) / 256 * BM * BN;
     if (best < 0 || cost < best) {
       best = cost;
-      pl = CbPlan{WR, NB, RPC, PD, octb, tiles_m, tiles_n};
+      pl = CbPlan{WR, NB, RPC, PD, octb, tiles_m, tiles_n, 1};
     }
   }
+  // a 128 x 128 tile whose patch fits 8 pieces per wave runs two workgroups
+  // per CU (64 KB LDS, <= 256 registers each): one's prologue / epilogue then
+  // overlaps the other's MFMAs (AlexNet conv5 215 -> 204 us per layer; forced
+  // on conv4's 192-row groups it lost to the 64 x 256 tile, 279 -> 335)
+  if (best > 0 && pl.WR == 4 && pl.NB == 4 && pl.PD == 8 && cb_instantiated(KH, 4, 4, 8, 2)) pl.OCC = 2;
   return best > 0;
 }
 
@@ -1453,9 +1459,10 @@ int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, c
   const int ximg = d->channels / 8 * HWi * 48;
   const unsigned nwg = static_cast<unsigned>((int64_t)G * pl.tiles_m * pl.tiles_n);
   const uint32_t xrange = static_cast<uint32_t>(xbytes);  // whole packed input (the kernel narrows it per group)
-#define RRAM_X(kh, wr, nb, pd)                                                                                \
-  if (KH == kh && pl.WR == wr && pl.NB == nb && pl.PD == pd) {                                                \
-    hipLaunchKernelGGL((k_conv_cb_x6<kh, kh, wr, nb, pd>), dim3(nwg), dim3(256), 0, s, P, wp, xp, pl.octb, pl.RPC, \
+#define RRAM_X(kh, wr, nb, pd, occ)                                                                           \
+  if (KH == kh && pl.WR == wr && pl.NB == nb && pl.PD == pd && pl.OCC == occ) {                               \
+    hipLaunchKernelGGL((k_conv_cb_x6<kh, kh, wr, nb, pd, occ>), dim3(nwg), dim3(256), 0, s, P, wp, xp, pl.octb,   \
+                       pl.RPC,                                                                                 \
                        xrange, ximg, static_cast<char*>(y_oct_k), d->num_output / 8,                          \
                        make_fastdiv(static_cast<uint32_t>(pl.octb >> 4)), make_fastdiv(static_cast<uint32_t>(pl.RPC))); \
   } else
