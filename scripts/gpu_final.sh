@@ -10,9 +10,9 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
 tail -3 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
 tail -1 $O/smoke.log
-timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || exit $?
+timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || exit $?
 cut -c1-300 $O/bench.json
-( cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/$O/prof -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline > $R/$O/prof_bench.json 2> $R/$O/prof.err ) || exit $?
+( cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/$O/prof -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $R/$O/prof_bench.json 2> $R/$O/prof.err ) || exit $?
 timeout -k 10 900 ./scripts/pmc.sh gpurun_out/pmc > $O/pmc.log 2>&1 || { tail $O/pmc.log; exit 1; }
 python3 scripts/pmc_traffic.py gpurun_out/pmc > $O/pmc_traffic.json && python3 scripts/pmc_summary.py gpurun_out/pmc > $O/pmc_summary.txt
 for w in cifar10_quick_mc cifar10_full_train googlenet_sweep lenet_mc lenet_train; do
