@@ -223,7 +223,7 @@ __device__ __forceinline__ void gemm_epilogue(floatx16 (&acc)[MI][NI], const Par
 // acc is left holding the stored values before the ReLU.
 template <int MI, int NI>
 __device__ __forceinline__ void conv_epilogue_nchw(floatx16 (&acc)[MI][NI], const Params& P, const Epi& ep,
-                                                   int mwave, int nwave, int lr, int lh) {
+                                                   int mwave, int nwave, int lr, int lh, int nlim = 0x7FFFFFFF) {
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(ep.C, 0, 0x7FFFFFFF, 0x00020000);
   const int HWo = static_cast<int>(ep.hw.d);
   const int mw = mwave + 4 * lh;  // this lane's first row
@@ -242,7 +242,7 @@ __device__ __forceinline__ void conv_epilogue_nchw(floatx16 (&acc)[MI][NI], cons
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
     const int n = nwave + j * 32 + lr;
-    if (n >= P.N) continue;
+    if (n >= P.N || n >= nlim) continue;  // nlim: a tile's last column + 1 (per-image tiles)
     const float cb = *(col_bias ? ep.bias + n : g_zero4);
     const uint32_t im = fdiv(static_cast<uint32_t>(n), ep.hw);
     const uint32_t sp = static_cast<uint32_t>(n) - im * ep.hw.d;

@@ -313,7 +313,8 @@ constexpr int piece_lo(int s, int PD, int T) { return s >= T - 1 ? PD : (s * PD 
 template <int KH, int KW, int WR, int NB, int PD, int OCC>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __restrict__ xpack, int octb, int rpc,
-             uint32_t xrange, int ximg, char* __restrict__ yoct, int cout8, FastDiv oct_div, FastDiv rpc_div) {
+             uint32_t xrange, int ximg, char* __restrict__ yoct, int cout8, FastDiv oct_div, FastDiv rpc_div,
+             int tpi) {
   using namespace g2;
   constexpr int T = KH * KW, WC = 4 / WR, BMc = 32 * WR, BNc = 32 * NB * WC, SFB = PD * 4 * 1024;
   static_assert(2 * SFB <= 160 * 1024, "LDS");
@@ -333,10 +334,16 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
   const int tm = __builtin_amdgcn_readfirstlane(tid % P.tiles_m);
   const int tn = __builtin_amdgcn_readfirstlane((tid / P.tiles_m) % P.tiles_n);
   const int z = __builtin_amdgcn_readfirstlane(tid / (P.tiles_m * P.tiles_n));
-  const int n0 = tn * BNc, m0 = tm * BMc;
+  const int m0 = tm * BMc;
 
   const ConvGeom& cv = P.cv;
   const int HW = cv.howo.d, OW = cv.wo_div.d;
+  // tpi > 0: per-image tiles (tpi of them per image, the last one short), so
+  // no tile spans two images and the patch carries one halo (the 5 x 5 patch
+  // then fits the LDS of two workgroups per CU); tpi = 0: tiles of BNc
+  // consecutive positions across images
+  const int timg = tpi > 0 ? tn / tpi : 0;
+  const int n0 = tpi > 0 ? timg * HW + (tn - timg * tpi) * BNc : tn * BNc;
   const int KT = cv.C >> 4;                      // K-tiles of 16 channels (>= 1, host)
   const uint32_t PL = static_cast<uint32_t>(cv.H * cv.W * 48);  // bytes per octet plane of the packed input
   Epi ep = P.e;
@@ -350,7 +357,7 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
 
   // patch: positions n0 .. plast cover images img0 .. img0 + nseg - 1 (<= 3);
   // segment s holds output rows f_s .. l_s of its image plus the KH - 1 halo
-  const int plast = min(n0 + BNc, P.N) - 1;
+  const int plast = min(n0 + BNc, tpi > 0 ? (timg + 1) * HW : P.N) - 1;
   const int img0 = n0 / HW, nseg = plast / HW - img0 + 1;
   const int f0 = (n0 - img0 * HW) / OW;
   auto seg_last = [&](int s) { return s == nseg - 1 ? (plast - (img0 + s) * HW) / OW : cv.Ho - 1; };
@@ -490,7 +497,7 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
       }
     }
   }
-  conv_epilogue_nchw<1, NB>(acc, P, ep, m0 + 32 * wr, n0 + wc * 32 * NB, lr, lh);
+  conv_epilogue_nchw<1, NB>(acc, P, ep, m0 + 32 * wr, n0 + wc * 32 * NB, lr, lh, plast + 1);
   if (yoct != nullptr) {
     // the output's channel-octet companion (the next convolution's input,
     // k_pack_octets_x6 layout): the split of the stored values (bias and
@@ -509,7 +516,7 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
       float rcv[8];
 #pragma unroll
       for (int r = 0; r < 8; ++r) rcv[r] = __shfl_xor(lh ? o[r] : o[8 + r], 32);
-      if (n >= P.N) continue;
+      if (n > plast) continue;
       const uint32_t im = fdiv(static_cast<uint32_t>(n), ep.hw);
       const int sp = n - static_cast<int>(im) * HW;
 #pragma unroll
@@ -1330,7 +1337,7 @@ int pack_octets(const float* x, void* oct, int num, int C, int HWi, hipStream_t 
 
 // ---- k_conv_cb_x6 (channel-octet pre-split activations) ----
 struct CbPlan {
-  int WR, NB, RPC, PD, octb, tiles_m, tiles_n, OCC;
+  int WR, NB, RPC, PD, octb, tiles_m, tiles_n, OCC, tpi;
 };
 // instantiated (KH, WR, NB, PD, OCC) combinations; OCC = workgroups per CU
 #define RRAM_CB_LIST(X)                                                                              \
@@ -1379,7 +1386,7 @@ bool conv_cb_plan(const rram_conv_desc* d, CbPlan& pl) {
     const int64_t cost = (nwg + 255) / 256 * BM * BN;
     if (best < 0 || cost < best) {
       best = cost;
-      pl = CbPlan{WR, NB, RPC, PD, octb, tiles_m, tiles_n, 1};
+      pl = CbPlan{WR, NB, RPC, PD, octb, tiles_m, tiles_n, 1, 0};
     }
   }
   // a 128 x 128 tile whose patch fits 8 pieces per wave runs two workgroups
@@ -1387,6 +1394,25 @@ bool conv_cb_plan(const rram_conv_desc* d, CbPlan& pl) {
   // overlaps the other's MFMAs (AlexNet conv5 215 -> 204 us per layer; forced
   // on conv4's 192-row groups it lost to the 64 x 256 tile, 279 -> 335)
   if (best > 0 && pl.WR == 4 && pl.NB == 4 && pl.PD == 8 && cb_instantiated(KH, 4, 4, 8, 2)) pl.OCC = 2;
+  // a layer whose 128 x 128 contiguous tiles need more than 8 pieces (tiles
+  // spanning two images carry two halos: AlexNet conv2's 5 x 5) takes
+  // per-image tiles at two workgroups per CU when their patch fits 8 pieces
+  // and their makespan (rounds of 512 half-CU tiles) is no worse
+  if (best > 0 && pl.OCC == 1 && cb_instantiated(KH, 4, 4, 8, 2)) {
+    const int BM = 128, BN = 128;
+    const int tiles_m = (M + BM - 1) / BM, tpi = (HW + BN - 1) / BN;
+    int rmax = 0;
+    for (int t = 0; t < tpi; ++t) {
+      const int f = t * BN / OW, l = (std::min((t + 1) * BN, HW) - 1) / OW;
+      rmax = std::max(rmax, l - f + KH);
+    }
+    const int octb = rmax * RPC * 16;
+    const int need = (2 * octb / 16 + 255) / 256;
+    const int64_t nwg = (int64_t)G * tiles_m * tpi * d->num;
+    const int64_t cost = (nwg + 511) / 512 * 2 * BM * BN;
+    if ((tiles_m * BM - M) * 4 <= tiles_m * BM && need <= 8 && nwg < (1ll << 31) && cost <= best)
+      pl = CbPlan{4, 4, RPC, 8, octb, tiles_m, static_cast<int>(tpi * d->num), 2, tpi};
+  }
   return best > 0;
 }
 
@@ -1464,7 +1490,8 @@ int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, c
     hipLaunchKernelGGL((k_conv_cb_x6<kh, kh, wr, nb, pd, occ>), dim3(nwg), dim3(256), 0, s, P, wp, xp, pl.octb,   \
                        pl.RPC,                                                                                 \
                        xrange, ximg, static_cast<char*>(y_oct_k), d->num_output / 8,                          \
-                       make_fastdiv(static_cast<uint32_t>(pl.octb >> 4)), make_fastdiv(static_cast<uint32_t>(pl.RPC))); \
+                       make_fastdiv(static_cast<uint32_t>(pl.octb >> 4)), make_fastdiv(static_cast<uint32_t>(pl.RPC)), \
+                       pl.tpi);                                                                                \
   } else
   RRAM_CB_LIST(RRAM_X) { return 0; }
 #undef RRAM_X
