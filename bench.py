@@ -281,7 +281,8 @@ def main():
                      "frac": round(dom_tf / dom_peak, 4),
                      "traffic": (dom_pmc["measured_MB_per_step"] * 1e6 if dom_pmc.get("measured_MB_per_step")
                                  else None),
-                     "kernel": f"k_conv_cb_x6<5,5,4,8,15> = AlexNet {DOMINANT_LAYER} ({engines[DOMINANT_LAYER]} engine, "
+                     "kernel": f"k_conv_cb_x6 5x5 (128 x 128 per-image tiles, two workgroups per CU) = AlexNet "
+                               f"{DOMINANT_LAYER} ({engines[DOMINANT_LAYER]} engine, "
                                "one launch per map), hipEvents around its layer over the timed region; peak = "
                                "bf16 dense 2500 / 6 products = 416.7 (f32 engine: v_mfma_f32_32x32x2_f32 157.3)",
                      "algorithmic_flops_per_launch": flops[DOMINANT_LAYER],
