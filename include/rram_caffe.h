@@ -223,6 +223,14 @@ int rram_mc_stats(rram_mc_t mc, double* sums, int sums_cap, int* n_outputs, unsi
 /* hipEvent timing of the injection launches; inject_times synchronises and
  * returns total ms / launches since the last reset, and the faultable weight count. */
 int rram_mc_set_timing(rram_mc_t mc, int enable);
+/* Opt-in prefix reuse (a different workload from the reference's per-map
+ * full forward): with only InnerProduct blobs faulted, the layers before the
+ * first faultable one give the same bits for every map of a fixed input
+ * batch, so they run once and later maps start at the first faultable layer.
+ * RRAM_EINVAL when a source layer advances between forwards (HDF5Data) or a
+ * later layer writes a prefix blob in place.  Re-enable after changing the
+ * input batch or a prefix weight (the prefix is recomputed on the next map). */
+int rram_mc_set_reuse_prefix(rram_mc_t mc, int enable);
 int rram_mc_inject_times(rram_mc_t mc, double* ms, long* launches, int64_t* weights, int reset);
 
 #ifdef __cplusplus

@@ -703,6 +703,12 @@ int rram_mc_restore_clean(rram_mc_t m) {
     m->mc->RestoreClean();
   });
 }
+int rram_mc_set_reuse_prefix(rram_mc_t m, int enable) {
+  return guarded([&] {
+    NEED(m);
+    m->mc->set_reuse_prefix(enable != 0);
+  });
+}
 int rram_mc_set_timing(rram_mc_t m, int enable) {
   return guarded([&] {
     NEED(m);

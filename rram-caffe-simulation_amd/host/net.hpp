@@ -52,6 +52,7 @@ class Net {
   const std::string& name() const { return name_; }
   Phase phase() const { return phase_; }
   const std::vector<std::shared_ptr<Layer<Dtype>>>& layers() const { return layers_; }
+  const std::vector<std::vector<Blob<Dtype>*>>& top_vecs() const { return top_vecs_; }
   const std::vector<std::string>& layer_names() const { return layer_names_; }
   const std::vector<std::shared_ptr<Blob<Dtype>>>& blobs() const { return blobs_; }
   const std::vector<std::string>& blob_names() const { return blob_names_; }

@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
+#include <set>
 #include <sstream>
 
 namespace caffe {
@@ -659,6 +660,26 @@ void MonteCarlo<Dtype>::RestoreClean() {
 }
 
 template <typename Dtype>
+void MonteCarlo<Dtype>::set_reuse_prefix(bool on) {
+  if (on) {
+    const auto& L = net_->layers();
+    const auto& tops = net_->top_vecs();
+    std::set<const Blob<Dtype>*> prefix_blobs;
+    for (int i = 0; i < first_fault_layer_; ++i) {
+      CAFFE_CHECK(std::string(L[i]->type()) != "HDF5Data",
+                  "MonteCarlo prefix reuse: layer " << net_->layer_names()[i] << " (HDF5Data) advances between forwards");
+      for (auto* b : tops[i]) prefix_blobs.insert(b);
+    }
+    for (size_t i = first_fault_layer_; i < L.size(); ++i)
+      for (auto* b : tops[i])
+        CAFFE_CHECK(!prefix_blobs.count(b), "MonteCarlo prefix reuse: layer " << net_->layer_names()[i]
+                                                << " writes a blob of the layers before the first faultable one");
+  }
+  reuse_prefix_ = on;
+  prefix_done_ = false;  // (re-)enabling recomputes the prefix on the next map
+}
+
+template <typename Dtype>
 void MonteCarlo<Dtype>::Run(uint32_t map_begin, uint32_t map_count) {
   std::vector<rram_inject_seg> segs(params_.size());
   for (size_t i = 0; i < params_.size(); ++i)
@@ -673,7 +694,9 @@ void MonteCarlo<Dtype>::Run(uint32_t map_begin, uint32_t map_count) {
     if (m != map_begin)
       for (auto* p : params_) (void)p->mutable_gpu_data();
     hipStream_t is = Caffe::hip_stream();
-    if (overlap_) {
+    const bool skip_prefix = reuse_prefix_ && prefix_done_ && first_fault_layer_ > 0;
+    const bool overlap = overlap_ && !skip_prefix;
+    if (overlap) {
       HIP_CALL(hipEventRecord(ev_free_, Caffe::hip_stream()));  // previous map's forward is done with the weights
       HIP_CALL(hipStreamWaitEvent(side_, ev_free_, 0));
       is = side_;
@@ -684,14 +707,17 @@ void MonteCarlo<Dtype>::Run(uint32_t map_begin, uint32_t map_count) {
       RRAM_CALL(rram_inject_rng_batched(segs.data() + s, k, seed_, m, d_broken_ + s, is));
     }
     if (timing_) timer_.stop(0, is);
-    if (overlap_) {
+    if (overlap) {
       HIP_CALL(hipEventRecord(ev_injected_, side_));
       net_->ForwardFromTo(0, first_fault_layer_ - 1, false);  // the layers before the first faultable one run under the injection
       HIP_CALL(hipStreamWaitEvent(Caffe::hip_stream(), ev_injected_, 0));
       net_->ForwardFromTo(first_fault_layer_, L - 1, false);
+    } else if (skip_prefix) {
+      net_->ForwardFromTo(first_fault_layer_, L - 1, false);  // the prefix's blobs hold the first map's bits
     } else {
       net_->Forward(false);
     }
+    if (reuse_prefix_) prefix_done_ = true;
     for (size_t k0 = 0; k0 < no; k0 += RRAM_MC_MAX_OUTPUTS) {
       rram_mc_outputs mo{};
       mo.n = static_cast<int>(std::min<size_t>(RRAM_MC_MAX_OUTPUTS, no - k0));

@@ -257,6 +257,15 @@ class MonteCarlo {
   void RestoreClean();
   // hipEvent timing of the injection launches (key 0)
   void set_timing(bool on) { timing_ = on; }
+  // Prefix reuse (opt-in; a different workload from the reference's, which
+  // runs every map's whole forward): under reference semantics only the
+  // InnerProduct blobs are faulted, so the layers before the first faultable
+  // one compute the same bits for every map of a fixed input batch.  On, the
+  // next map runs them once and the following maps start at the first
+  // faultable layer.  Refused when a source layer advances between forwards
+  // (HDF5Data) or a later layer writes a prefix blob in place; the caller
+  // re-enables it after changing the input batch or a prefix weight.
+  void set_reuse_prefix(bool on);
   EventTimer& timer() { return timer_; }
   int64_t fault_weights() const {
     int64_t n = 0;
@@ -266,6 +275,7 @@ class MonteCarlo {
 
  private:
   bool timing_ = false;
+  bool reuse_prefix_ = false, prefix_done_ = false;
   EventTimer timer_;
   std::shared_ptr<Net<Dtype>> net_;
   std::vector<rram_inject_cfg> cfgs_;

@@ -50,6 +50,7 @@ SIGNATURES = {
     "rram_net_layer_times": (I, [P, C.POINTER(C.c_double), C.POINTER(C.c_long), I, PI, I]),
     "rram_net_describe": (I, [C.c_char_p, I, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "rram_mc_set_timing": (I, [P, I]),
+    "rram_mc_set_reuse_prefix": (I, [P, I]),
     "rram_mc_inject_times": (I, [P, C.POINTER(C.c_double), C.POINTER(C.c_long), PI64, I]),
     "rram_solver_create": (I, [C.c_char_p, C.c_char_p, C.c_char_p, PP]),
     "rram_solver_destroy": (I, [P]),
@@ -591,6 +592,11 @@ class MonteCarlo:
 
     def set_timing(self, on: bool):
         check(self._lib.rram_mc_set_timing(self.h, int(on)), "mc_set_timing")
+
+    def set_reuse_prefix(self, on: bool):
+        """Opt-in: run the layers before the first faultable one once for a
+        fixed input batch (include/rram_caffe.h rram_mc_set_reuse_prefix)."""
+        check(self._lib.rram_mc_set_reuse_prefix(self.h, int(on)), "mc_set_reuse_prefix")
 
     def inject_times(self, reset=False):
         """(total ms, launches, faultable weights) of the injection launches."""

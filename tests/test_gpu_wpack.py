@@ -141,3 +141,32 @@ def test_mc_overlapped_injection_equals_serial(device, monkeypatch):
         net.close()
     assert res[0][0] == res[1][0] and res[0][1] == res[1][1]
     np.testing.assert_array_equal(res[0][2], res[1][2])
+
+
+@pytest.mark.parametrize("conv_faults", [False, True])
+def test_mc_prefix_reuse_bit_identical(device, conv_faults):
+    """MonteCarlo prefix reuse (include/rram_caffe.h rram_mc_set_reuse_prefix,
+    an opt-in workload): maps that start at the first faultable layer give the
+    full forward's per-map accuracy / loss, broken-cell counts and final logits
+    bit for bit; with the conv-fault extension the prefix is the data layer
+    alone and the option changes nothing."""
+    from rramsim import caffe, make_inject_cfg, models
+    caffe.set_stream_from_torch()
+    res = []
+    for reuse in (False, True):
+        caffe.set_random_seed(17)
+        opts = models.net_options("alexnet")
+        if conv_faults:
+            opts["fault_layers"] = "InnerProduct,Convolution"
+        net = caffe.Net(models.alexnet(test_batch=16), "test", opts)
+        mc = caffe.MonteCarlo(net, make_inject_cfg(0.03), seed=9, max_maps=8)
+        if reuse:
+            mc.set_reuse_prefix(True)
+        mc.run(0, 4)
+        st = mc.stats()
+        res.append((st["per_map"], st["broken"], N(net.blob("fc8")), N(net.blob("pool5"))))
+        mc.close()
+        net.close()
+    assert res[0][0] == res[1][0] and res[0][1] == res[1][1]
+    np.testing.assert_array_equal(res[0][2], res[1][2])
+    np.testing.assert_array_equal(res[0][3], res[1][3])
