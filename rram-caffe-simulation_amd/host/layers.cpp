@@ -190,16 +190,18 @@ void ConvolutionLayer<Dtype>::Reshape(const std::vector<Blob<Dtype>*>& bottom,
 
 // the octet companion a producer writes next to top (nullptr: not wanted).
 // RRAM_OCTETS selects the producers: 0 none (every convolution packs its
-// input), 1 all, 2 (default) the fused LRN + max pool only.  Measured on
-// MI355X (AlexNet b256, per-layer hipEvents, profiles/r02_ab_octets.txt): the
-// companion write costs the producer pool1 +35 us / saves conv2 39 us, pool2
-// +13 / conv3 -35, conv3's epilogue +40 / conv4 -35, conv4's +40 / conv5 -32,
-// so only the pooling producers pay off.
+// input), 1 (default) all, 2 the fused LRN + max pool only.  Measured on
+// MI355X (AlexNet b256, per-layer hipEvents): round 2 (profiles/
+// r02_ab_octets.txt) the epilogue companions lost (conv3's epilogue +40 us /
+// conv4 -35, conv4's +40 / conv5 -32); round 3, with conv5 at two workgroups
+// per CU and per-image conv2 tiles, all producers win by 8 us per map
+// (conv3 +30, conv4 +3, conv5 -41: 112.7-113.3k vs 112.1-113.1k images/s,
+// profiles/r03_ab_octets.txt).
 enum OctetProducer { kOctConv = 1, kOctPool = 2 };
 bool octets_enabled(int producer) {
   static const int mode = [] {
     const char* e = std::getenv("RRAM_OCTETS");
-    return e ? std::atoi(e) : 2;
+    return e ? std::atoi(e) : 1;
   }();
   return mode == 1 || (mode == 2 && producer == kOctPool);
 }

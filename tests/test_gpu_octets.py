@@ -138,26 +138,28 @@ def test_lrn_maxpool_octets_bit_identical(device):
         np.testing.assert_array_equal(_as_u16(yo, (n, c, ph, pw)), octets_ref(ref))
 
 
-def test_alexnet_forward_with_companions_bit_identical(device):
-    """A whole AlexNet TEST forward, where pool1 / pool2 / conv3 / conv4 hand
-    their companions to conv2-5 (RRAM_OCTETS=1, read once per process, so it
-    runs in a child): every convolution's output equals a plain
-    rram_conv2d_fwd of the net's own bottom blob bit for bit."""
+def test_alexnet_forward_pool_companions_only_bit_identical(device):
+    """A whole AlexNet TEST forward where only pool1 / pool2 hand their
+    companions to conv2 / conv3 and conv4 / conv5 pack their inputs
+    (RRAM_OCTETS=2, read once per process, so it runs in a child): every
+    convolution's output equals a plain rram_conv2d_fwd of the net's own
+    bottom blob bit for bit."""
     import os
     import subprocess
     import sys
-    if os.environ.get("RRAM_OCTETS") == "1":
+    if os.environ.get("RRAM_OCTETS") == "2":
         _alexnet_check(device)
         return
-    env = dict(os.environ, RRAM_OCTETS="1")
+    env = dict(os.environ, RRAM_OCTETS="2")
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-p", "no:cacheprovider", "-m", "gpu",
-                        __file__ + "::test_alexnet_forward_with_companions_bit_identical"],
+                        __file__ + "::test_alexnet_forward_pool_companions_only_bit_identical"],
                        env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
 
 
 def test_alexnet_forward_bit_identical(device):
-    """The same check with the default (each convolution packs its input)."""
+    """The same check with the default (RRAM_OCTETS=1: pool1 / pool2 / conv3 /
+    conv4 all hand their companions to conv2-5)."""
     _alexnet_check(device)
 
 
