@@ -312,6 +312,11 @@ int rram_conv2d_fwd_cached(const rram_conv_desc* d, const float* x, const void* 
                            rram_stream_t stream);
 /* 1 when rram_conv2d_fwd_octets would read an x_oct for this shape now. */
 int rram_conv_input_octets(const rram_conv_desc* d);
+/* Host-side plan of the channel-octet kernel for d (no device work):
+ * plan[0..4] = tile rows, tile columns, workgroups per CU, tiles per image
+ * (0 = tiles run across images), LDS patch pieces per wave.  Returns 1 with
+ * the plan filled, 0 when the octet kernel does not take d. */
+int rram_conv_octet_plan(const rram_conv_desc* d, int* plan);
 /* oct = the octet companion of x (channels % 8 == 0). */
 int rram_pack_octets(const float* x, void* oct, int num, int channels, int height, int width,
                      rram_stream_t stream);

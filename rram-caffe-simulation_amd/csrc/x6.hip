@@ -1694,6 +1694,18 @@ int rram_f32_engine_for_conv(const rram_conv_desc* d) {
              : RRAM_ENGINE_F32;
 }
 
+int rram_conv_octet_plan(const rram_conv_desc* d, int* plan) {
+  RRAM_REQUIRE(d != nullptr && plan != nullptr, "octet plan query: NULL");
+  rram::CbPlan cpl;
+  if (!rram::conv_cb_plan(d, cpl)) return 0;
+  plan[0] = 32 * cpl.WR;
+  plan[1] = 32 * cpl.NB * (4 / cpl.WR);
+  plan[2] = cpl.OCC;
+  plan[3] = cpl.tpi;
+  plan[4] = cpl.PD;
+  return 1;
+}
+
 int rram_conv_input_octets(const rram_conv_desc* d) {
   RRAM_REQUIRE(d != nullptr, "octet query: desc is NULL");
   rram::CbPlan cpl;

@@ -100,6 +100,7 @@ SIGNATURES = {
     "rram_conv2d_fwd": (I, [P, P, P, P, P, I, P]),
     "rram_conv2d_fwd_octets": (I, [P, P, P, P, P, P, P, I, P]),
     "rram_conv_input_octets": (I, [P]),
+    "rram_conv_octet_plan": (I, [P, P]),
     "rram_conv_weight_pack_bytes": (SZ, [P]),
     "rram_conv2d_fwd_cached": (I, [P, P, P, P, P, I, P, P, P, I, P]),
     "rram_pack_octets": (I, [P, P, I, I, I, I, P]),

@@ -213,6 +213,15 @@ def conv_input_octets(d):
     return _lib().rram_conv_input_octets(C.byref(d))
 
 
+def conv_octet_plan(d):
+    """The channel-octet kernel's host plan for d: dict(rows, cols, per_cu,
+    tiles_per_image, pieces), or None when that kernel does not take d."""
+    plan = (C.c_int * 5)()
+    if not _lib().rram_conv_octet_plan(C.byref(d), plan):
+        return None
+    return dict(rows=plan[0], cols=plan[1], per_cu=plan[2], tiles_per_image=plan[3], pieces=plan[4])
+
+
 def pack_octets(x, oct_, n, c, h, w):
     K.check(_lib().rram_pack_octets(_p(x), _p(oct_), n, c, h, w, _stream()), "pack_octets")
 
