@@ -131,6 +131,13 @@ for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
 for i, (gsz, vals) in enumerate(sorted(lrn_grids.items(), reverse=True)):
     k = "norm1+pool1 (LRN + max pool, octets)" if i == 0 else "norm2+pool2 (LRN + max pool, octets)"
     per[k] += sum((2 if c == "FETCH_SIZE" else 1) * KIB * v for c, v in vals)
+# octet companions from the convolution epilogues (RRAM_OCTETS=1, the default
+# since round 3): conv3 / conv4 write their outputs' companions and no input
+# pack runs, so those bytes move from the pack row to the producers' rows
+if per.get("conv4/conv5 input packs k_pack_octets_x6", 0.0) == 0.0:
+    ALG["conv3 k_conv_cb_x6<3,3,4,8,...>"] = (P2O + 384*256*9*4 + Y3 + O4, "x octets + w + y + y octets")
+    ALG["conv4 k_conv_cb_x6<3,3,2,4,...>"] = (O4 + 384*192*9*4 + Y4 + O4, "x octets + w + y + y octets")
+    ALG["conv4/conv5 input packs k_pack_octets_x6"] = (0.0, "none run (companions from the conv3 / conv4 epilogues)")
 table = {}
 for k, (alg, what) in ALG.items():
     meas = per.get(k, 0.0) / forwards
