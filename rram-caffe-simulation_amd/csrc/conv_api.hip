@@ -316,6 +316,20 @@ int rram_col2im(const float* col, int C, int H, int W, int kh, int kw, int ph, i
 int rram_ip_fwd(const float* x, const float* w, const float* bias, float* y, int M, int N, int K,
                 int transpose, int relu, void* ws, size_t ws_bytes, rram_stream_t s) {
   // top = bottom * W^T (W [N][K]) or bottom * W (W [K][N], transpose)
+  if (M == 1 && !transpose) {
+    // one row: the reference's GPU path is caffe_gpu_gemv(NoTrans, N, K, W, x)
+    // then caffe_gpu_axpy(N, 1, bias, top) (inner_product_layer.cu:15-20).
+    // (With transpose it still calls gemv(NoTrans) on the [K][N] weights,
+    // i.e. reads them as [N][K]; its CPU path, inner_product_layer.cpp:83-96,
+    // does the transposed product, which this build follows: Appendix Q15.)
+    int rc = gemv_core(0, N, K, 1.0f, w, x, 0.0f, y, as_stream(s));
+    if (rc) return rc;
+    if (bias) {
+      rc = rram_bias_add(y, bias, 1, N, 1, s);
+      if (rc) return rc;
+    }
+    return relu ? rram_relu_fwd(y, y, N, 0.0f, s) : RRAM_OK;
+  }
   if (transpose)
     return gemm_core(0, 0, M, N, K, 1.0f, x, K, w, N, 0.0f, y, N, bias, RRAM_BIAS_COL, relu, ws,
                      ws_bytes, as_stream(s));

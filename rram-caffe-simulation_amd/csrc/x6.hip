@@ -36,13 +36,19 @@ namespace {
 // of 8; MFMA group g takes steps 8g .. 8g+7 of both halves (lane half h holds
 // k = 8h + j of the 32x32x16 operand).  Padded steps have zero weights and
 // read no activations.
+// RRAM_X6_DROP = k (1..5) leaves out the k-th product below.  Guard
+// validation only (profiles/r04_fp32_guard.txt: a build with a term dropped
+// must fail tests/test_gpu_fp32_guard.py); the product build has it 0.
+#ifndef RRAM_X6_DROP
+#define RRAM_X6_DROP 0
+#endif
 namespace x6 {
 __device__ __forceinline__ floatx16 mfma6(const Parts& a, const Parts& b, floatx16 c) {
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.l, b.h, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.l, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, b.m, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, b.h, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.m, c, 0, 0, 0);
+  if (RRAM_X6_DROP != 1) c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.l, b.h, c, 0, 0, 0);
+  if (RRAM_X6_DROP != 2) c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.l, c, 0, 0, 0);
+  if (RRAM_X6_DROP != 3) c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, b.m, c, 0, 0, 0);
+  if (RRAM_X6_DROP != 4) c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, b.h, c, 0, 0, 0);
+  if (RRAM_X6_DROP != 5) c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.m, c, 0, 0, 0);
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.h, c, 0, 0, 0);
 }
 template <int KH, int KW, int CPH>

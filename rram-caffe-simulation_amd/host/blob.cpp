@@ -61,7 +61,7 @@ void* SyncedMemory::octets(size_t bytes) {
   return oct_ptr_;
 }
 const void* SyncedMemory::valid_octets(const int (&shape)[4]) const {
-  if (!oct_valid_) return nullptr;
+  if (!oct_valid_ || exposed_) return nullptr;
   for (int i = 0; i < 4; ++i)
     if (shape[i] != oct_shape_[i]) return nullptr;
   return oct_ptr_;

@@ -35,7 +35,10 @@ class SyncedMemory {
   // Channel-octet companion (rram_conv2d_fwd_octets): a device buffer with the
   // pre-split bf16x3 form of this memory's NCHW contents.  It is valid only
   // while the data is unchanged since a producer wrote both (every mutable_* /
-  // set_* access invalidates it) and only for the shape it was written for.
+  // set_* access invalidates it), only for the shape it was written for, and
+  // never once the C-ABI handed the data pointer out (expose(): the caller may
+  // write a new batch through it with no mutable access, e.g. into an Input
+  // blob, so a companion packed from the old batch must not be read).
   void* octets(size_t bytes);  // the buffer, grown to `bytes`
   const void* valid_octets(const int (&shape)[4]) const;
   void set_octets_valid(const int (&shape)[4]);
@@ -47,8 +50,10 @@ class SyncedMemory {
   void* wpack(size_t bytes);  // the buffer, grown to `bytes`
   bool wpack_valid(uint64_t key) const { return wp_valid_ && !exposed_ && wp_key_ == key; }
   // the C-ABI handed this memory's device pointer to a caller, who may write
-  // through it at any time without a mutable access: no pack is trusted after
+  // through it at any time without a mutable access: no pack or octet
+  // companion is trusted after
   void expose() { exposed_ = true; }
+  bool exposed() const { return exposed_; }
   void set_wpack_valid(uint64_t key) {
     wp_key_ = key;
     wp_valid_ = wp_ptr_ != nullptr;

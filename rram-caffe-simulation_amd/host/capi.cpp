@@ -247,7 +247,10 @@ int rram_net_blob(rram_net_t n, const char* name, float** data, float** diff, in
     NEED(name);
     auto b = n->net->blob_by_name(name);
     if (!b) throw Error(std::string("Unknown blob name ") + name);
-    if (data) *data = b->mutable_gpu_data();
+    if (data) {
+      *data = b->mutable_gpu_data();
+      b->data()->expose();  // the caller may write a new batch through it unseen
+    }
     if (diff) *diff = b->mutable_gpu_diff();
     if (naxes) *naxes = b->num_axes();
     if (shape)
@@ -334,6 +337,9 @@ int rram_net_alias_flat_params(rram_net_t n, float* data, float* diff) {
     NEED(data);
     NEED(diff);
     n->net->alias_flat_params(data, diff);
+    // the flat buffer is the caller's: writes through it (a broadcast, a
+    // torch copy_) bypass every mutable access, so no weight pack is trusted
+    for (auto* p : n->net->learnable_params()) p->data()->expose();
   });
 }
 

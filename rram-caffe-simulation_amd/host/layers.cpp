@@ -245,9 +245,14 @@ void ConvolutionLayer<Dtype>::Forward_gpu(const std::vector<Blob<Dtype>*>& botto
     // the pack is valid for this layer's shape and engine until the weights'
     // next mutable access (the MC driver's injection, a solver update, ...)
     SyncedMemory* wm = this->blobs_[0]->data().get();
-    const rram_conv_desc& d = desc_;
-    const uint64_t key = (((((uint64_t)d.num * 131 + d.channels) * 131 + d.height) * 131 + d.width) * 131 +
-                          d.num_output) * 131 + (uint64_t)d.group * 8 + (uint64_t)rram_get_f32_engine();
+    // key: every field of the descriptor (the pack layout follows the tile
+    // plan, which depends on kernel / stride / pad / dilation and the output
+    // shape) plus the engine, so two convolutions sharing one weight blob
+    // never read each other's pack
+    const int* f = reinterpret_cast<const int*>(&desc_);
+    uint64_t key = 1469598103934665603ull;
+    for (size_t i = 0; i < sizeof(rram_conv_desc) / sizeof(int); ++i) key = (key ^ (uint32_t)f[i]) * 1099511628211ull;
+    key = (key ^ (uint64_t)rram_get_f32_engine()) * 1099511628211ull;
     const float* w = this->blobs_[0]->gpu_data();
     void* wp = wm->wpack(wpb);
     RRAM_CALL(rram_conv2d_fwd_cached(&desc_, bottom[0]->gpu_data(), xo, w, wp, wm->wpack_valid(key) ? 1 : 0, bias, y,

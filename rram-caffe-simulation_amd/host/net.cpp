@@ -164,7 +164,7 @@ Net<Dtype>::Net(const Msg& in_param, Phase phase, const Msg& options) : phase_(p
       lp.set("rram_num_classes", options.str("num_classes", "10"));
       lp.set("rram_data_seed", options.str("data_seed", "0"));
     }
-    if (type == "HDF5Data") {  // data-parallel row split (HDF5DataLayer::Skip)
+    if (type == "HDF5Data") {  // opt-in data-parallel row split (Caffe 1.0's Skip; not the reference's)
       lp.set("rram_solver_rank", options.str("solver_rank", "0"));
       lp.set("rram_solver_count", options.str("solver_count", "1"));
     }
@@ -272,6 +272,19 @@ Net<Dtype>::Net(const Msg& in_param, Phase phase, const Msg& options) : phase_(p
         prev->folded_into_next = true;
     }
     ++lid;
+  }
+  // force_backward (net.cpp:249-265): every layer runs backward and every
+  // bottom its layer allows gets a diff, every param propagates
+  if (param.boolean("force_backward", false)) {
+    for (size_t l = 0; l < layers_.size(); ++l) {
+      layer_need_backward_[l] = true;
+      for (size_t j = 0; j < bottom_need_backward_[l].size(); ++j) {
+        const bool nb = bottom_need_backward_[l][j] || layers_[l]->AllowForceBackward(static_cast<int>(j));
+        bottom_need_backward_[l][j] = nb;
+        blob_need_backward_[bottom_id_vecs_[l][j]] = blob_need_backward_[bottom_id_vecs_[l][j]] || nb;
+      }
+      for (size_t p = 0; p < layers_[l]->blobs().size(); ++p) layers_[l]->set_param_propagate_down(static_cast<int>(p), true);
+    }
   }
   for (auto& n : available) {
     const int id = blob_names_index_[n];

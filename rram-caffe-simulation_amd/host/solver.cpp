@@ -664,16 +664,23 @@ void MonteCarlo<Dtype>::set_reuse_prefix(bool on) {
   if (on) {
     const auto& L = net_->layers();
     const auto& tops = net_->top_vecs();
-    std::set<const Blob<Dtype>*> prefix_blobs;
+    // compare the memory, not the Blob: Split, single-input Concat and
+    // single-top Slice tops share their bottom's SyncedMemory (ShareData)
+    std::set<const SyncedMemory*> prefix_mem;
     for (int i = 0; i < first_fault_layer_; ++i) {
       CAFFE_CHECK(std::string(L[i]->type()) != "HDF5Data",
                   "MonteCarlo prefix reuse: layer " << net_->layer_names()[i] << " (HDF5Data) advances between forwards");
-      for (auto* b : tops[i]) prefix_blobs.insert(b);
+      for (auto* b : tops[i]) prefix_mem.insert(b->data().get());
     }
-    for (size_t i = first_fault_layer_; i < L.size(); ++i)
+    for (size_t i = first_fault_layer_; i < L.size(); ++i) {
+      // Split / Concat / Slice tops that share a prefix blob's memory are
+      // views of it, not writes (they write only into memory of their own)
+      const std::string t = L[i]->type();
+      if (t == "Split" || t == "Concat" || t == "Slice") continue;
       for (auto* b : tops[i])
-        CAFFE_CHECK(!prefix_blobs.count(b), "MonteCarlo prefix reuse: layer " << net_->layer_names()[i]
+        CAFFE_CHECK(!prefix_mem.count(b->data().get()), "MonteCarlo prefix reuse: layer " << net_->layer_names()[i]
                                                 << " writes a blob of the layers before the first faultable one");
+    }
   }
   reuse_prefix_ = on;
   prefix_done_ = false;  // (re-)enabling recomputes the prefix on the next map

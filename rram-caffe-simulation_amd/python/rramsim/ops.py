@@ -146,6 +146,11 @@ def gemm_ex(trans_a, trans_b, M, N, K_, alpha, A, lda, B, ldb, beta, Cm, ldc, bi
                                     ws, wsb, _stream()), "gemm_ex")
 
 
+def gemv(trans_a, M, N, alpha, A, x, beta, y):
+    """y = alpha * op(A) x + beta * y, A [M][N] row-major (caffe_gpu_gemv)."""
+    K.check(_lib().rram_gemv_f32(int(trans_a), M, N, alpha, _p(A), _p(x), beta, _p(y), _stream()), "gemv")
+
+
 def conv_desc(x_shape, num_output, kernel, stride=1, pad=0, dilation=1, group=1):
     kh, kw = (kernel, kernel) if isinstance(kernel, int) else kernel
     sh, sw = (stride, stride) if isinstance(stride, int) else stride

@@ -85,7 +85,7 @@ class DataParallelSolver:
     """Fault-aware data-parallel SGD (C4) on top of caffe.Solver."""
 
     def __init__(self, solver_prototxt: str, net_prototxt: str, options: Optional[Dict] = None, seed: int = 1701,
-                 group=None, log=None, overlap: bool = False, bucket_mb: float = 4.0):
+                 group=None, log=None, overlap: bool = False, bucket_mb: float = 4.0, shard_hdf5: bool = False):
         import torch
         import torch.distributed as dist
 
@@ -98,8 +98,14 @@ class DataParallelSolver:
         caffe.set_random_seed(seed)            # identical weights and fault maps on every rank
         opts = dict(options or {})
         opts["data_seed"] = self.rank           # a different synthetic data shard per rank
-        opts["solver_rank"] = self.rank         # HDF5Data row split (HDF5DataLayer::Skip)
-        opts["solver_count"] = self.world
+        # HDF5Data: by default every rank reads every row from row 0, as each
+        # P2PSync worker's own data layer does in the reference (parallel.cpp:
+        # 201-284; its hdf5_data_layer.cpp:128-157 has no Skip).  shard_hdf5
+        # opts into Caffe 1.0's HDF5DataLayer::Skip row split instead (rank r
+        # reads rows r, r + N, ...): a deliberate divergence, off by default.
+        if shard_hdf5:
+            opts["solver_rank"] = self.rank
+            opts["solver_count"] = self.world
         self.solver = caffe.Solver(solver_prototxt, net_prototxt, opts, log=log if self.rank == 0 else None)
         net = self.solver.net
         n = net.flat_param_count()

@@ -96,3 +96,23 @@ def maxpool64(x, k, s):
         for b_ in range(PW):
             out[:, :, a, b_] = x[:, :, a * s:min(a * s + k, H), b_ * s:min(b_ * s + k, W)].max(axis=(2, 3))
     return out
+
+
+# fp32-level guard of the bf16x6 engine (tests/test_gpu_fp32_guard.py): per
+# layer, errors in units of Σ|a·b| (max, mean) of the bf16x6 kernel and of the
+# fp32-MFMA kernel on the same data.  The 1e-4 gate above would pass a kernel
+# that had lost fp32 accuracy; these bounds do not (tests/test_x6_guard_emulation.py).
+X6_GUARD_MAX = 1e-6
+X6_GUARD_RATIO = 2.0
+
+
+def x6_guard_failures(x6, f32):
+    """x6, f32 = (max, mean) error / Σ|a·b|; the list of violated bounds."""
+    bad = []
+    if not x6[0] <= X6_GUARD_MAX:
+        bad.append(f"max {x6[0]:.3e} > {X6_GUARD_MAX}")
+    if not x6[0] <= X6_GUARD_RATIO * f32[0]:
+        bad.append(f"max {x6[0]:.3e} > {X6_GUARD_RATIO} x fp32 MFMA max {f32[0]:.3e}")
+    if not x6[1] <= X6_GUARD_RATIO * f32[1]:
+        bad.append(f"mean {x6[1]:.3e} > {X6_GUARD_RATIO} x fp32 MFMA mean {f32[1]:.3e}")
+    return bad

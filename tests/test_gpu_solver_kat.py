@@ -260,7 +260,7 @@ def _free_port():
     return p
 
 
-def _dp_worker(rank, world, port, backend, list_file, cases, q):
+def _dp_worker(rank, world, port, backend, list_file, cases, q, shard=False):
     import sys
     sys.path.insert(0, str(ROOT / "rram-caffe-simulation_amd" / "python"))
     import torch
@@ -275,7 +275,8 @@ def _dp_worker(rank, world, port, backend, list_file, cases, q):
     from rramsim.parallel import DataParallelSolver
     out = []
     for lr, wd, mom, iters in cases:
-        dp = DataParallelSolver(solver_proto(lr, wd, mom, iters), net_proto(list_file, NUM), seed=1701)
+        dp = DataParallelSolver(solver_proto(lr, wd, mom, iters), net_proto(list_file, NUM), seed=1701,
+                                shard_hdf5=shard)
         dp.step(iters)
         torch.cuda.synchronize()
         ps = dp.solver.net.params()
@@ -288,12 +289,13 @@ def _dp_worker(rank, world, port, backend, list_file, cases, q):
     dist.destroy_process_group()
 
 
-def _run_dp(world, backend, list_file, cases):
+def _run_dp(world, backend, list_file, cases, shard=False):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_dp_worker, args=(r, world, port, backend, list_file, cases, q)) for r in range(world)]
+    ps = [ctx.Process(target=_dp_worker, args=(r, world, port, backend, list_file, cases, q, shard))
+          for r in range(world)]
     for p in ps:
         p.start()
     res = sorted((q.get(timeout=300) for _ in ps), key=lambda t: t[0])
@@ -316,14 +318,34 @@ def _multi_device_expected(tmp_path, cases, devices):
 
 
 def test_least_squares_update_two_ranks(device, tmp_path):
-    """devices = 2 (:465-487): one process at batch 8 for K iterations, the
-    analytic (K+1)th update, then 2 data-parallel ranks at batch 4 each for
-    K+1 iterations (rank r reads rows r, r+2, ... as HDF5DataLayer::Skip, the
-    gradient all-reduce averages them) must land on it — for every K of the
-    "everything" case, and the ranks stay bitwise identical."""
+    """devices = 2 with this fork's data semantics: under its P2PSync every
+    worker's HDF5Data layer reads its own stream from row 0 (parallel.cpp:
+    201-284; hdf5_data_layer.cpp:128-157 has no Skip), so 2 ranks at batch 4
+    see the same 4 rows and their averaged gradient is the single-device
+    gradient of those rows: 2 data-parallel ranks for K+1 iterations must land
+    on the analytic (K+1)th update of one process at batch 4 — for every K of
+    the "everything" case, and the ranks stay bitwise identical.  (The
+    reference test's own num = kNum x devices comparison, :465-487, needs
+    constant data under these semantics; the row split that makes it hold on
+    solver_data.h5 is Caffe 1.0's Skip, the opt-in case below.)"""
+    cases = [(0.01, 0.5, 0.5, k + 1) for k in range(3)]
+    exp = _multi_device_expected(tmp_path, cases, 1)
+    res = _run_dp(2, "gloo", _list_file(tmp_path), cases)
+    for (ep, eu), (p0, h0, n0), (p1, h1, n1) in zip(exp, res[0][1], res[1][1]):
+        _near(ep, p0.astype(np.float64))
+        _near(eu, h0.astype(np.float64))
+        assert np.array_equal(p0.view(np.uint32), p1.view(np.uint32))
+        assert n0 == n1 > 0
+
+
+def test_least_squares_update_two_ranks_row_split(device, tmp_path):
+    """devices = 2 (:465-487) with the opt-in row split (DataParallelSolver
+    shard_hdf5=True, Caffe 1.0's HDF5DataLayer::Skip: rank r reads rows r,
+    r+2, ...): one process at batch 8 for K iterations, the analytic (K+1)th
+    update, then 2 ranks at batch 4 each for K+1 iterations must land on it."""
     cases = [(0.01, 0.5, 0.5, k + 1) for k in range(3)]
     exp = _multi_device_expected(tmp_path, cases, 2)
-    res = _run_dp(2, "gloo", _list_file(tmp_path), cases)
+    res = _run_dp(2, "gloo", _list_file(tmp_path), cases, shard=True)
     for (ep, eu), (p0, h0, n0), (p1, h1, n1) in zip(exp, res[0][1], res[1][1]):
         _near(ep, p0.astype(np.float64))
         _near(eu, h0.astype(np.float64))

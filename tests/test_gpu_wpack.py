@@ -170,3 +170,68 @@ def test_mc_prefix_reuse_bit_identical(device, conv_faults):
     assert res[0][0] == res[1][0] and res[0][1] == res[1][1]
     np.testing.assert_array_equal(res[0][2], res[1][2])
     np.testing.assert_array_equal(res[0][3], res[1][3])
+
+
+def test_net_input_octet_companion_not_stale(device):
+    """A convolution reading a net input packs the input's octet companion
+    itself.  The Input blob's data pointer was handed out (rram_net_blob), so
+    a caller can write the next batch through it with no mutable access: the
+    second forward must convolve the new batch, not the companion of the old
+    one (SyncedMemory::valid_octets refuses exposed memory)."""
+    import torch
+    from rramsim import caffe, ops
+    shape, cout = (2, 32, 13, 13), 96
+    d = ops.conv_desc(shape, cout, 3, 1, 1, 1, 1)
+    assert ops.conv_input_octets(d) == 1                 # this convolution reads the companion
+    txt = ('layer { name: "x" type: "Input" top: "x" input_param { shape { dim: 2 dim: 32 dim: 13 dim: 13 } } }\n'
+           'layer { name: "conv" type: "Convolution" bottom: "x" top: "y" convolution_param { num_output: 96 '
+           'kernel_size: 3 pad: 1 weight_filler { type: "gaussian" std: 0.1 } bias_filler { type: "constant" value: 0.5 } } }\n')
+    caffe.set_stream_from_torch()
+    net = caffe.Net(txt, "test")
+    xb = net.blob("x")                                    # kept across both batches
+    p = net.params()
+    w, b = p[0]["data"].view(cout, 32, 3, 3), p[1]["data"]
+    rng = np.random.default_rng(3)
+    for batch in range(3):
+        x = torch.from_numpy(rng.standard_normal(shape).astype(np.float32)).to(device)
+        xb.copy_(x)
+        net.forward()
+        ref = torch.empty((2, cout, 13, 13), device=device)
+        ops.conv2d_fwd(d, x, w, b, ref)
+        np.testing.assert_array_equal(N(net.blob("y")), N(ref), err_msg=f"batch {batch}")
+    net.close()
+
+
+def test_shared_weights_different_geometry_under_mc(device):
+    """Two convolutions share one weight blob (param names) but differ in pad,
+    so their packed weights follow different tile plans; with the packs kept
+    across MC maps (SyncedMemory::wpack), each must keep its own key (the
+    whole descriptor) and both outputs equal plain forwards."""
+    from rramsim import caffe, make_inject_cfg, ops
+    txt = ('layer { name: "x" type: "DummyData" top: "x" dummy_data_param { shape { dim: 4 dim: 32 dim: 15 dim: 15 } '
+           'data_filler { type: "gaussian" std: 1 } } }\n'
+           'layer { name: "ca" type: "Convolution" bottom: "x" top: "ya" param { name: "w" } param { name: "b" } '
+           'convolution_param { num_output: 64 kernel_size: 3 pad: 1 weight_filler { type: "gaussian" std: 0.1 } '
+           'bias_filler { type: "constant" value: 0.1 } } }\n'
+           'layer { name: "cb" type: "Convolution" bottom: "x" top: "yb" param { name: "w" } param { name: "b" } '
+           'convolution_param { num_output: 64 kernel_size: 3 pad: 0 weight_filler { type: "gaussian" std: 0.1 } '
+           'bias_filler { type: "constant" value: 0.1 } } }\n'
+           'layer { name: "fc" type: "InnerProduct" bottom: "yb" top: "fc" inner_product_param { num_output: 10 '
+           'weight_filler { type: "gaussian" std: 0.01 } } }\n')
+    caffe.set_stream_from_torch()
+    caffe.set_random_seed(21)
+    net = caffe.Net(txt, "test")
+    mc = caffe.MonteCarlo(net, make_inject_cfg(0.05), seed=2, max_maps=4)
+    for m in range(3):
+        mc.run(m, 1)
+    import torch
+    ps = net.params()
+    w, b = ps[0]["data"].view(64, 32, 3, 3), ps[1]["data"]
+    x = net.blob("x").contiguous()
+    for name, pad in (("ya", 1), ("yb", 0)):
+        d = ops.conv_desc((4, 32, 15, 15), 64, 3, 1, pad, 1, 1)
+        y = torch.empty((4, 64, d.out_h, d.out_w), device=device)
+        ops.conv2d_fwd(d, x, w, b, y)
+        np.testing.assert_array_equal(N(net.blob(name)).reshape(N(y).shape), N(y), err_msg=name)
+    mc.close()
+    net.close()
