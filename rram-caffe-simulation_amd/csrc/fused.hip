@@ -44,10 +44,16 @@ constexpr int kLrnG = 2;
 // pre-split input, x6.hip k_pack_octets_x6 layout [num][C/8][PH][PW][3][8]
 // bf16): the pooled values of 8 channels are gathered in an LDS plane and
 // split by the band's output threads (C % 8 == 0 and CC % 8 == 0; G divides 8).
-// WT > 0: the plane width W is WT (AlexNet's 55 / 27), so a window that lies
-// wholly inside the image reads its K x K taps at immediate LDS offsets with
-// no per-tap mask (3 instructions a tap instead of ~6; every AlexNet window
-// is such, the ceil rule clips none); WT = 0: any W.
+// WT > 0: the plane width W is WT (AlexNet's 55 / 27) and the window stride
+// is 2 with no column padding (host check), so a window that lies wholly
+// inside the image reads its K x K taps at immediate LDS offsets with no
+// per-tap mask (every AlexNet window is such, the ceil rule clips none), and
+// each plane row is stored de-interleaved, even input columns then odd ones
+// (column c at (c & 1) * HWC + (c >> 1)): the taps of consecutive pooled
+// outputs (input columns 2 o + b) then sit on consecutive words, where the
+// plain row had consecutive lanes two words apart (2-way LDS bank conflicts
+// on every tap: 46-48 % of the LDS-active cycles in round 3).  WT = 0: any W,
+// plain rows.
 __device__ __forceinline__ float max3f(float a, float b, float c) {
   float r;
   asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
@@ -88,18 +94,31 @@ __global__ void __launch_bounds__(256)
   // the thread's two pixels of the band: threadIdx.x and threadIdx.x + 256
   const int pix0 = threadIdx.x, pix1 = threadIdx.x + 256;
   const bool own0 = pix0 < NP, own1 = pix1 < NP;
-  // channel cc's band is read through a buffer resource of its own (base and
-  // range are uniform: scalar work), so a load is one instruction at a lane
-  // offset fixed for the whole walk; a pixel outside the band reads at 2^31,
-  // a channel outside [0, C) through an empty range: zero either way
-  const char* xband = reinterpret_cast<const char*>(x + (int64_t)n * C * HW + (int64_t)h0 * W);
-  const int vo0 = own0 ? pix0 * 4 : INT_MIN, vo1 = own1 ? pix1 * 4 : INT_MIN;
+  // LDS slots of the two pixels (WT: de-interleaved rows)
+  constexpr int HWC = (WT + 1) / 2;
+  auto slot = [&](int pix) {
+    if constexpr (WT > 0) {
+      const int r = pix / WT, c = pix - r * WT;
+      return r * WT + (c & 1) * HWC + (c >> 1);
+    } else {
+      return pix;
+    }
+  };
+  const int sl0 = slot(pix0), sl1 = slot(pix1);
+  // one buffer resource over image n (range C H W floats) and a lane offset
+  // per channel: channel cc at (h0 W + pix + cc H W) * 4, one VALU add per
+  // pixel (a resource per channel cost ~10 scalar instructions a load: SALU
+  // above VALU in round 3).  A pixel outside the band starts at 2^31 and a
+  // channel outside [0, C) lands past the range (cc < 0 wraps above 2^31):
+  // zero either way
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x + (int64_t)n * C * HW), 0, C * HW * 4, 0x00020000);
+  const uint32_t vo0 = own0 ? static_cast<uint32_t>(h0 * W + pix0) * 4u : 0x80000000u;
+  const uint32_t vo1 = own1 ? static_cast<uint32_t>(h0 * W + pix1) * 4u : 0x80000000u;
   auto ld = [&](int cc) {
-    const bool in = cc >= 0 && cc < C;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<char*>(xband) + (in ? (int64_t)cc * HW * 4 : 0), 0, in ? NP * 4 : 0, 0x00020000);
-    return f32x2{__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo0, 0, 0)),
-                 __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo1, 0, 0))};
+    const uint32_t co = static_cast<uint32_t>(cc) * static_cast<uint32_t>(HW * 4);  // mod 2^32
+    return f32x2{__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xrs, static_cast<int>(vo0 + co), 0, 0)),
+                 __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xrs, static_cast<int>(vo1 + co), 0, 0))};
   };
   // win[j] = both pixels at channel (c0 - PRE + j), zero outside [0, C).
   // NS staging arrays rotate by group (st[g % NS], so the registers are named
@@ -145,7 +164,7 @@ __global__ void __launch_bounds__(256)
                                     static_cast<unsigned>(wr + b) < static_cast<unsigned>(W))
               << (a * K + b);
     it_d[i] = it < D * NO ? d : D;  // D = no item
-    it_l[i] = (hr - h0) * W + wr;
+    it_l[i] = (hr - h0) * W + (WT > 0 ? (wr >> 1) : wr);  // WT: wr is even (stride 2, no column pad)
     it_out[i] = (pr0 + prl) * PW + pwi;
     it_vo[i] = (d * PHW + it_out[i]) * 4;
     it_ok[i] = ok;
@@ -163,8 +182,8 @@ __global__ void __launch_bounds__(256)
       // lrn_sq_add / lrn_scale / lrn_out (the unfused kernels' arithmetic) on
       // both pixels at once
       const f32x2 v = lrn_value2<SIZE>(win + d, alpha_over_size, beta, k);
-      if (own0) yb[d][pix0] = v.x;
-      if (own1) yb[d][pix1] = v.y;
+      if (own0) yb[d][sl0] = v.x;
+      if (own1) yb[d][sl1] = v.y;
     }
     __syncthreads();
     // pool the group's D channels (MaxPoolForward: -FLT_MAX start, strict ">"
@@ -181,7 +200,7 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
           for (int a = 0; a < K; ++a)
 #pragma unroll
-            for (int b = 0; b < K; ++b) t[a * K + b] = yl[a * WT + b];
+            for (int b = 0; b < K; ++b) t[a * K + b] = yl[a * WT + (b & 1) * HWC + (b >> 1)];
           // v_max3 over the taps: the strict-">" walk's value whenever the
           // maximum is not zero (a quiet NaN loses to any number in both; the
           // plane holds products, never a signalling NaN); for a zero maximum
@@ -200,7 +219,8 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
             for (int b = 0; b < K; ++b) {
               const bool ok = (it_ok[i] >> (a * K + b)) & 1u;
-              const float v = yl[ok ? a * W + b : -it_l[i]];  // masked taps read element 0
+              const int tap = WT > 0 ? a * WT + (b & 1) * HWC + (b >> 1) : a * W + b;
+              const float v = yl[ok ? tap : -it_l[i]];  // masked taps read element 0
               if (ok && v > mv) mv = v;
             }
         }
@@ -306,11 +326,12 @@ int rram_lrn_maxpool_fwd_octets(const float* x, float* y, void* y_oct, int num, 
   else                                                                                                             \
     hipLaunchKernelGGL((k_lrn_maxpool_band<K_, S_, kLrnG, false, WT_>), grid, dim3(kThreads), 0, as_stream(s), x,  \
                        y, yo, C, H, W, PH, PW, sh, sw, ph, pw, rb, cc, bands, nchunks, aos, beta, k);
+  const bool wt_ok = sw == 2 && pw == 0;  // the WT plane rows are de-interleaved by a window stride of 2
 #define RRAM_LP(K_, S_)                                  \
   if (kernel == K_ && size == S_) {                      \
-    if (K_ == 3 && S_ == 5 && W == 55) {                 \
+    if (K_ == 3 && S_ == 5 && W == 55 && wt_ok) {        \
       RRAM_LP3(K_, S_, (K_ == 3 && S_ == 5 ? 55 : 0))    \
-    } else if (K_ == 3 && S_ == 5 && W == 27) {          \
+    } else if (K_ == 3 && S_ == 5 && W == 27 && wt_ok) { \
       RRAM_LP3(K_, S_, (K_ == 3 && S_ == 5 ? 27 : 0))    \
     } else {                                             \
       RRAM_LP3(K_, S_, 0)                                \

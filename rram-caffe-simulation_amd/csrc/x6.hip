@@ -542,6 +542,363 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
   }
 }
 
+// ---------------------------------------------------------------------------
+// k_conv_cb16_x6: k_conv_cb_x6 on v_mfma_f32_16x16x32_bf16.  Same input
+// octet companion, patch ring, DMA / staging schedule and tile order; the
+// matrix-core shape differs.  MI355X_MICROARCH.md (DVFS give-back, item 7):
+// at equal cycles per FLOP a 16x16x32 loop on random data holds a higher
+// clock than a 32x32x16 one (1.12-1.15x the FLOP/s, LDS-fed).
+// K order: a K-tile is still 16 channels (two octets) x all T taps; MFMA
+// group p pairs taps 2p and 2p + 1: lane group g = lane >> 4 of the operands
+// holds octet g & 1 at tap 2p + (g >> 1).  With T odd the last group's upper
+// half (tap T) is padding: zero weights (pack) and B zeroed after the read, so
+// a non-finite input never meets a zero weight.  Wave tile = 32 rows (two
+// 16-row blocks) x 32 NB columns (2 NB 16-column blocks), the accumulators
+// the same 64 floats per lane as the 32x32 form.
+namespace cb16 {
+constexpr int FRAG = 3 * 64;  // bf16x8 units per fragment (3 terms x 64 lanes): 16 rows x 32 k
+}  // namespace cb16
+namespace x6 {
+__device__ __forceinline__ floatx4 mfma6_16(const Parts& a, const Parts& b, floatx4 c) {
+  if (RRAM_X6_DROP != 1) c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.l, b.h, c, 0, 0, 0);
+  if (RRAM_X6_DROP != 2) c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.l, c, 0, 0, 0);
+  if (RRAM_X6_DROP != 3) c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.m, b.m, c, 0, 0, 0);
+  if (RRAM_X6_DROP != 4) c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.m, b.h, c, 0, 0, 0);
+  if (RRAM_X6_DROP != 5) c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.m, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.h, b.h, c, 0, 0, 0);
+}
+}  // namespace x6
+
+// Epilogue of MI x NJ 16x16 accumulator blocks (v_mfma_f32_16x16x32 layout:
+// col = lane & 15, row = 4 (lane >> 4) + r): conv_epilogue_nchw's arithmetic
+// and raw buffer stores, the lane's row group folded into its base address.
+// acc is left holding the stored values before the ReLU.
+template <int MI, int NJ>
+__device__ __forceinline__ void conv_epilogue_nchw16(floatx4 (&acc)[MI][NJ], const Params& P, const Epi& ep, int mwave,
+                                                     int nwave, int c16, int g, int nlim) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(ep.C, 0, 0x7FFFFFFF, 0x00020000);
+  const int HWo = static_cast<int>(ep.hw.d);
+  const int mw = mwave + 4 * g;
+  const bool rows_full = mwave + MI * 16 <= P.M;
+  const bool row_bias = ep.bias_mode == RRAM_BIAS_ROW, col_bias = ep.bias_mode == RRAM_BIAS_COL;
+  const bool relu = ep.relu != 0;
+  const float alpha = ep.alpha;
+  float bz[MI][4];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = mw + 16 * i + r;
+      bz[i][r] = *((row_bias && m < P.M) ? ep.bias + m : g_zero4);
+    }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int n = nwave + 16 * j + c16;
+    if (n >= P.N || n >= nlim) continue;
+    const float cb = *(col_bias ? ep.bias + n : g_zero4);
+    const uint32_t im = fdiv(static_cast<uint32_t>(n), ep.hw);
+    const uint32_t sp = static_cast<uint32_t>(n) - im * ep.hw.d;
+    const uint32_t base = static_cast<uint32_t>((im * ep.cimg + sp + static_cast<int64_t>(mw) * HWo) * 4);
+    float ov[MI][4];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float o = (alpha * acc[i][j][r] + bz[i][r]) + cb;
+        acc[i][j][r] = o;
+        ov[i][r] = relu ? fmaxf(o, 0.0f) : o;
+      }
+    if (rows_full) {  // uniform: no per-store exec masking
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, ov[i][r]), rs, static_cast<int>(base),
+                                                (16 * i + r) * HWo * 4, 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (mw + 16 * i + r < P.M)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, ov[i][r]), rs, static_cast<int>(base),
+                                                  (16 * i + r) * HWo * 4, 0);
+    }
+  }
+}
+
+template <int KH, int KW, int WR, int NB, int PD, int OCC>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
+k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __restrict__ xpack, int octb, int rpc,
+               uint32_t xrange, int ximg, char* __restrict__ yoct, int cout8, FastDiv oct_div, FastDiv rpc_div,
+               int tpi) {
+  using namespace g2;
+  constexpr int T = KH * KW, PP = (T + 1) / 2, WC = 4 / WR, BMc = 32 * WR, BNc = 32 * NB * WC, SFB = PD * 4 * 1024;
+  constexpr int MI = 2, NJ = 2 * NB;
+  static_assert(2 * SFB <= 160 * 1024, "LDS");
+  static_assert(PP >= 2, "pair groups");
+  __shared__ __attribute__((aligned(16))) char smem[2 * SFB];
+  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem));
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c16 = lane & 15, g = lane >> 4, up = g >> 1;
+  const int wr = wave % WR, wc = wave / WR;
+
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, loc = bid >> 3;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int tid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const int tm = __builtin_amdgcn_readfirstlane(tid % P.tiles_m);
+  const int tn = __builtin_amdgcn_readfirstlane((tid / P.tiles_m) % P.tiles_n);
+  const int z = __builtin_amdgcn_readfirstlane(tid / (P.tiles_m * P.tiles_n));
+  const int m0 = tm * BMc;
+
+  const ConvGeom& cv = P.cv;
+  const int HW = cv.howo.d, OW = cv.wo_div.d;
+  const int timg = tpi > 0 ? tn / tpi : 0;
+  const int n0 = tpi > 0 ? timg * HW + (tn - timg * tpi) * BNc : tn * BNc;
+  const int KT = cv.C >> 4;
+  const uint32_t PL = static_cast<uint32_t>(cv.H * cv.W * 48);
+  Epi ep = P.e;
+  if (z > 0) {
+    ep.C += z * P.grp_c;
+    if (ep.bias) ep.bias += z * P.grp_bias;
+  }
+  const uint16_t* xg = xpack + (int64_t)z * (cv.C >> 3) * (PL >> 1);
+  const int4v xrsrc = make_rsrc(reinterpret_cast<const float*>(xg), xrange - static_cast<uint32_t>(z * (cv.C >> 3)) * PL);
+
+  const int plast = min(n0 + BNc, tpi > 0 ? (timg + 1) * HW : P.N) - 1;
+  const int img0 = n0 / HW, nseg = plast / HW - img0 + 1;
+  const int f0 = (n0 - img0 * HW) / OW;
+  auto seg_last = [&](int s) { return s == nseg - 1 ? (plast - (img0 + s) * HW) / OW : cv.Ho - 1; };
+  const int p1 = seg_last(0) - f0 + KH;
+  const int p2 = p1 + (nseg > 1 ? seg_last(1) + KH : 0);
+  const int R = p2 + (nseg > 2 ? seg_last(2) + KH : 0);
+  const int PW = cv.W + 2 * cv.pw;
+  uint32_t poff[PD];
+#pragma unroll
+  for (int i = 0; i < PD; ++i) {
+    const int c = (wave * PD + i) * 64 + lane;
+    const int h = static_cast<int>(fdiv(static_cast<uint32_t>(c), oct_div)), rem = c - h * (octb >> 4);
+    const int prow = static_cast<int>(fdiv(static_cast<uint32_t>(rem), rpc_div)), pc = rem - prow * rpc;
+    const int pcol = pc / 3, t = pc - pcol * 3;
+    uint32_t off = 0x80000000u;
+    if (h < 2 && prow < R && pcol < PW) {
+      const int sg = prow >= p2 ? 2 : prow >= p1 ? 1 : 0;
+      const int y = (sg == 0 ? f0 + prow : prow - (sg == 1 ? p1 : p2)) - cv.ph;
+      const int x = pcol - cv.pw;
+      if (y >= 0 && y < cv.H && x >= 0 && x < cv.W)
+        off = static_cast<uint32_t>(img0 + sg) * static_cast<uint32_t>(ximg) + static_cast<uint32_t>(h) * PL +
+              static_cast<uint32_t>((y * cv.W + x) * 48 + t * 16);
+    }
+    poff[i] = off;
+  }
+  // B fragment bases (bytes into a stage) of this lane's column in block j,
+  // at tap 0 of its octet (g & 1)
+  int bb[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int n = min(n0 + wc * 32 * NB + 16 * j + c16, plast);
+    const int img = static_cast<int>(fdiv(static_cast<uint32_t>(n), cv.howo)), sp = n - img * HW;
+    const int oh = static_cast<int>(fdiv(static_cast<uint32_t>(sp), cv.wo_div)), ow = sp - oh * OW;
+    const int sg = img - img0;
+    const int prow = sg == 0 ? oh - f0 : (sg == 1 ? p1 : p2) + oh;
+    bb[j] = (g & 1) * octb + prow * rpc * 16 + ow * 48;
+  }
+  floatx4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[i][j][r] = 0.0f;
+
+  auto issue = [&](int kt, int stg, int i) {
+    dma_b128(xrsrc, poff[i] + static_cast<uint32_t>(kt) * 2u * PL,
+             lds0 + static_cast<uint32_t>(stg * SFB + (wave * PD + i) * 1024));
+  };
+  // the lane's byte offset of pair group p: tap 2p (lower half) or 2p + 1
+  // (upper half; tap 2p again for the padded half of the last group)
+  const int rowb = rpc * 16;
+  // (opaque to the compiler: hoisted out of the K-tile loop, the NJ x PP
+  // sums bb[j] + tap_off(p) would each hold a register)
+  auto tap_off = [&](int p) {
+    const int s0 = 2 * p, s1 = 2 * p + 1;
+    const int o0 = (s0 / KW) * rowb + (s0 % KW) * 48;
+    const int d = s1 < T ? ((s1 / KW) - (s0 / KW)) * rowb + ((s1 % KW) - (s0 % KW)) * 48 : 0;
+    int o = o0 + (up ? d : 0);
+    asm volatile("" : "+v"(o));
+    return o;
+  };
+  x6::bf16x8 fa[2][MI][3], fb[2][3];
+  auto read_b = [&](x6::bf16x8 (&f)[3], const char* st, int to, int p, int j) {
+    const char* q = st + bb[j] + to;
+#pragma unroll
+    for (int t = 0; t < 3; ++t) f[t] = *reinterpret_cast<const x6::bf16x8*>(q + 16 * t);
+    if (2 * p + 1 >= T) {  // padded upper half: zero B (its weights are zero too)
+#pragma unroll
+      for (int t = 0; t < 3; ++t) f[t] = up ? x6::bf16x8{} : f[t];
+    }
+  };
+
+  {
+    const x6::bf16x8* ap = wpack + ((int64_t)((z * P.tiles_m + tm) * WR + wr) * KT) * PP * MI * cb16::FRAG + lane;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint16_t*>(xg), 0, static_cast<int>(xrange - static_cast<uint32_t>(z * (cv.C >> 3)) * PL), 0x00020000);
+    auto load_a = [&](x6::bf16x8 (&f)[MI][3], int q) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int t = 0; t < 3; ++t) f[i][t] = ap[(q * MI + i) * cb16::FRAG + t * 64];
+    };
+    constexpr int PMAX = (PD + PP - 2) / (PP - 1);  // patch pieces per group
+    typedef int int4x __attribute__((ext_vector_type(4)));
+    int4x stg[2][PMAX];
+#pragma unroll
+    for (int i = 0; i < PD; ++i) issue(0, 0, i);
+    load_a(fa[0], 0);
+    wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    read_b(fb[0], smem, tap_off(0), 0, 0);
+    auto vtile = [&](int kt, auto par_c, auto more_c) {
+      constexpr int PAR = decltype(par_c)::value;
+      constexpr bool MORE = decltype(more_c)::value;
+      const char* cur = smem + (kt & 1) * SFB;
+      const char* nxt = smem + ((kt + 1) & 1) * SFB;
+      char* nst = smem + ((kt + 1) & 1) * SFB + wave * PD * 1024 + lane * 16;
+#pragma unroll
+      for (int p = 0; p < PP; ++p) {
+        const int pa = (p + PAR) & 1;
+        const int q = kt * PP + p;
+        const int to = tap_off(p), to1 = p + 1 < PP ? tap_off(p + 1) : tap_off(0);
+        if (MORE) {
+          if (p > 0) {
+#pragma unroll
+            for (int i = cbx6::piece_lo(p - 1, PD, PP); i < cbx6::piece_lo(p, PD, PP); ++i)
+              *reinterpret_cast<int4x*>(nst + i * 1024) = stg[(p - 1) & 1][i - cbx6::piece_lo(p - 1, PD, PP)];
+          }
+#pragma unroll
+          for (int i = cbx6::piece_lo(p, PD, PP); i < cbx6::piece_lo(p + 1, PD, PP); ++i)
+            stg[p & 1][i - cbx6::piece_lo(p, PD, PP)] = __builtin_bit_cast(
+                int4x, __builtin_amdgcn_raw_buffer_load_b128(
+                           xr, static_cast<int>(poff[i] + static_cast<uint32_t>(kt + 1) * 2u * PL), 0, 0));
+        }
+        if (p + 1 < PP || MORE) load_a(fa[pa ^ 1], q + 1);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const bool last = p == PP - 1 && j == NJ - 1;
+          if (last && MORE) {  // the next stage is complete
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          if (!last) {
+            if (j + 1 < NJ)
+              read_b(fb[(j + 1) & 1], cur, to, p, j + 1);
+            else
+              read_b(fb[(j + 1) & 1], cur, to1, p + 1, 0);
+          } else if (MORE) {
+            read_b(fb[0], nxt, to1, 0, 0);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+            acc[i][j] = x6::mfma6_16(x6::Parts{fa[pa][i][0], fa[pa][i][1], fa[pa][i][2]},
+                                     x6::Parts{fb[j & 1][0], fb[j & 1][1], fb[j & 1][2]}, acc[i][j]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    };
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    using P0 = std::integral_constant<int, 0>;
+    using P1 = std::integral_constant<int, 1>;
+    if constexpr (PP % 2 == 0) {
+      int kt = 0;
+      for (; kt + 1 < KT; ++kt) vtile(kt, P0{}, T_{});
+      vtile(kt, P0{}, F_{});
+    } else {
+      int kt = 0;
+      for (; kt + 2 < KT; kt += 2) {
+        vtile(kt, P0{}, T_{});
+        vtile(kt + 1, P1{}, T_{});
+      }
+      if (kt + 1 < KT) {
+        vtile(kt, P0{}, T_{});
+        vtile(kt + 1, P1{}, F_{});
+      } else {
+        vtile(kt, P0{}, F_{});
+      }
+    }
+  }
+  const int mwave = m0 + 32 * wr, nwave = n0 + wc * 32 * NB;
+  conv_epilogue_nchw16<MI, NJ>(acc, P, ep, mwave, nwave, c16, g, plast + 1);
+  if (yoct != nullptr) {
+    // the output's octet companion: lane group g holds rows 4 g .. 4 g + 3 of
+    // both 16-row blocks; lanes g, g ^ 1 (lane ^ 16) trade one block so that
+    // an even g stores octet g / 2 of block 0 and an odd g octet (g - 1) / 2
+    // of block 1, each whole (8 consecutive rows).
+    const bool relu = ep.relu != 0;
+    const bool ev = (g & 1) == 0;
+    const int orow = mwave + 16 * (g & 1) + 8 * (g >> 1);  // first row of the lane's octet
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int n = nwave + 16 * j + c16;
+      float o0[4], o1[4], rcv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        o0[r] = relu ? fmaxf(acc[0][j][r], 0.0f) : acc[0][j][r];
+        o1[r] = relu ? fmaxf(acc[1][j][r], 0.0f) : acc[1][j][r];
+        rcv[r] = __shfl_xor(ev ? o1[r] : o0[r], 16);
+      }
+      if (n > plast || orow >= P.M) continue;
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = ev ? o0[r] : rcv[r];
+        v[4 + r] = ev ? rcv[r] : o1[r];
+      }
+      const uint32_t im = fdiv(static_cast<uint32_t>(n), ep.hw);
+      const int sp = n - static_cast<int>(im) * HW;
+      const int oct = (z * P.M + orow) / 8;
+      x6::store_terms8(v, yoct + (((int64_t)im * cout8 + oct) * HW + sp) * 48);
+    }
+  }
+}
+
+// w [G*M][Cg][T] -> k_conv_cb16_x6 fragments [G][rblocks][Cg/16][PP][2][term][64 lanes][8]:
+// lane l of fragment (kt, p, i) holds row 32 rb + 16 i + (l & 15), channels
+// 16 kt + 8 ((l >> 4) & 1) .. + 7 at tap 2 p + (l >> 5) (zero at tap T).
+__global__ void __launch_bounds__(256) k_conv_cb16_pack_x6(const float* __restrict__ w, char* __restrict__ out, int M,
+                                                           int Cg, int T, int rblocks, int units) {
+  const int KT = Cg >> 4, PP = (T + 1) / 2;
+  for (int u = blockIdx.x * blockDim.x + threadIdx.x; u < units; u += gridDim.x * blockDim.x) {
+    const int lane = u & 63;
+    int r = u >> 6;
+    const int i = r & 1;
+    r >>= 1;
+    const int p = r % PP;
+    r /= PP;
+    const int kt = r % KT;
+    r /= KT;
+    const int rb = r % rblocks;
+    const int gz = r / rblocks;
+    const int m = rb * 32 + 16 * i + (lane & 15), c0 = kt * 16 + ((lane >> 4) & 1) * 8, s = 2 * p + (lane >> 5);
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      v[e] = (m < M && s < T) ? w[((int64_t)gz * M + m) * Cg * T + (int64_t)(c0 + e) * T + s] : 0.0f;
+    x6::Parts t;
+    x6::split8_safe(v, t);
+    char* f = out + (int64_t)(u >> 6) * 3072 + lane * 16;
+    *reinterpret_cast<x6::bf16x8*>(f) = t.h;
+    *reinterpret_cast<x6::bf16x8*>(f + 1024) = t.m;
+    *reinterpret_cast<x6::bf16x8*>(f + 2048) = t.l;
+  }
+}
+
 // x [img][C][H][W] fp32 -> bf16 terms [img][C/8][H][W][3][8] (k_conv_cb_x6's
 // input).  One thread per (image, octet, position): 8 strided loads (coalesced
 // across the threads), 48 bytes out.
@@ -1422,10 +1779,31 @@ bool conv_cb_plan(const rram_conv_desc* d, CbPlan& pl) {
   return best > 0;
 }
 
+// k_conv_cb16_x6 instantiations (KH, WR, NB, PD, OCC): the 16x16x32 form of
+// the octet kernel for a plan of the same tile
+#define RRAM_CB16_LIST(X) \
+  X(5, 4, 4, 8, 2) X(3, 4, 4, 8, 2) X(3, 4, 8, 12, 1) X(3, 4, 8, 15, 1) X(3, 2, 4, 12, 1) X(3, 2, 4, 14, 1)
+bool cb16_instantiated(int KH, int WR, int NB, int PD, int OCC) {
+#define RRAM_X(kh, wr, nb, pd, occ) \
+  if (KH == kh && WR == wr && NB == nb && PD == pd && OCC == occ) return true;
+  RRAM_CB16_LIST(RRAM_X)
+#undef RRAM_X
+  return false;
+}
+// RRAM_CB16: which octet-kernel plans run on 16x16x32 (bit 0: 5x5, bit 1: 3x3)
+bool cb16_for(int KH) {
+  static const int mode = [] {
+    const char* e = getenv("RRAM_CB16");
+    return e ? atoi(e) : 0;
+  }();
+  return (mode & (KH == 5 ? 1 : 2)) != 0;
+}
+
 int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, const float* w, const float* bias,
                    float* y, void* y_oct, int relu, hipStream_t s, const WPack& wk) {
   CbPlan pl;
   if (!conv_cb_plan(d, pl)) return 0;
+  const bool use16 = cb16_for(d->kernel_h) && cb16_instantiated(d->kernel_h, pl.WR, pl.NB, pl.PD, pl.OCC);
   if (y_oct != nullptr && d->num_output % 8 != 0) return 0;
   const int KH = d->kernel_h, KW = d->kernel_w, T = KH * KW;
   const int G = d->group, Cg = d->channels / G, M = d->num_output / G;
@@ -1464,7 +1842,7 @@ int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, c
   // input's octet companion), then the weight fragments
   const int64_t xbytes = (int64_t)d->num * d->channels * HWi * 6;
   const int rblocks = pl.tiles_m * pl.WR;
-  const int64_t wfrags = (int64_t)G * rblocks * (Cg / 16) * T;
+  const int64_t wfrags = use16 ? (int64_t)G * rblocks * (Cg / 16) * ((T + 1) / 2) * 2 : (int64_t)G * rblocks * (Cg / 16) * T;
   if (wk.query) {
     *wk.query = static_cast<size_t>(wfrags * 3072);
     return 1;
@@ -1481,8 +1859,12 @@ int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, c
   }
   if (!wk.valid) {
     const int wunits = static_cast<int>(wfrags * 64);
-    hipLaunchKernelGGL(k_conv_cb_pack_x6, dim3(stream_blocks(wunits)), dim3(256), 0, s, w, wbuf, M, Cg, T,
-                       rblocks, wunits);
+    if (use16)
+      hipLaunchKernelGGL(k_conv_cb16_pack_x6, dim3(stream_blocks(wunits)), dim3(256), 0, s, w, wbuf, M, Cg, T,
+                         rblocks, wunits);
+    else
+      hipLaunchKernelGGL(k_conv_cb_pack_x6, dim3(stream_blocks(wunits)), dim3(256), 0, s, w, wbuf, M, Cg, T,
+                         rblocks, wunits);
     rc = launch_status("conv weight pack x6 (octets)");
     if (rc) return rc;
   }
@@ -1491,6 +1873,20 @@ int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, c
   const int ximg = d->channels / 8 * HWi * 48;
   const unsigned nwg = static_cast<unsigned>((int64_t)G * pl.tiles_m * pl.tiles_n);
   const uint32_t xrange = static_cast<uint32_t>(xbytes);  // whole packed input (the kernel narrows it per group)
+  if (use16) {
+#define RRAM_X(kh, wr, nb, pd, occ)                                                                             \
+  if (KH == kh && pl.WR == wr && pl.NB == nb && pl.PD == pd && pl.OCC == occ) {                                 \
+    hipLaunchKernelGGL((k_conv_cb16_x6<kh, kh, wr, nb, pd, occ>), dim3(nwg), dim3(256), 0, s, P, wp, xp, pl.octb, \
+                       pl.RPC, xrange, ximg, static_cast<char*>(y_oct_k), d->num_output / 8,                    \
+                       make_fastdiv(static_cast<uint32_t>(pl.octb >> 4)), make_fastdiv(static_cast<uint32_t>(pl.RPC)), \
+                       pl.tpi);                                                                                  \
+  } else
+    RRAM_CB16_LIST(RRAM_X) { return 0; }
+#undef RRAM_X
+    rc = launch_status("conv cb16 x6");
+    if (rc == 0 && y_oct != nullptr && y_oct_k == nullptr) rc = pack_octets(y, y_oct, d->num, d->num_output, HW, s);
+    return rc ? rc : 1;
+  }
 #define RRAM_X(kh, wr, nb, pd, occ)                                                                           \
   if (KH == kh && pl.WR == wr && pl.NB == nb && pl.PD == pd && pl.OCC == occ) {                               \
     hipLaunchKernelGGL((k_conv_cb_x6<kh, kh, wr, nb, pd, occ>), dim3(nwg), dim3(256), 0, s, P, wp, xp, pl.octb,   \
