@@ -310,6 +310,17 @@ size_t rram_conv_weight_pack_bytes(const rram_conv_desc* d);
 int rram_conv2d_fwd_cached(const rram_conv_desc* d, const float* x, const void* x_oct, const float* w,
                            void* w_pack, int w_pack_valid, const float* bias, float* y, void* y_oct, int relu,
                            rram_stream_t stream);
+/* rram_conv2d_fwd_cached writing y inside a larger NCHW tensor: image n's
+ * output starts at y + n * y_image_stride (>= num_output * out_h * out_w
+ * floats), e.g. y = top + offset * out_h * out_w and y_image_stride =
+ * C_top * out_h * out_w for a Concat top along channels.  The TEST-phase
+ * Concat fold writes each inception branch straight into its slice of the
+ * Concat top, replacing the copy of concat_layer.cu:6-48 (Forward_gpu) for
+ * those bottoms.  No output octets; w_pack as in rram_conv2d_fwd_cached.
+ * Every value is bit-identical to rram_conv2d_fwd_cached's. */
+int rram_conv2d_fwd_strided(const rram_conv_desc* d, const float* x, const void* x_oct, const float* w,
+                            void* w_pack, int w_pack_valid, const float* bias, float* y, int64_t y_image_stride,
+                            int relu, rram_stream_t stream);
 /* 1 when rram_conv2d_fwd_octets would read an x_oct for this shape now. */
 int rram_conv_input_octets(const rram_conv_desc* d);
 /* Host-side plan of the channel-octet kernel for d (no device work):

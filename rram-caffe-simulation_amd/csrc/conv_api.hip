@@ -10,7 +10,7 @@ int gemm_core(int trans_a, int trans_b, int M, int N, int K, float alpha, const 
               const float* B, int ldb, float beta, float* C, int ldc, const float* bias,
               int bias_mode, int relu, void* ws, size_t ws_bytes, hipStream_t s);
 int conv_fwd_core(const rram_conv_desc* d, const float* x, const float* w, const float* bias,
-                  float* y, int relu, hipStream_t s);
+                  float* y, int relu, hipStream_t s, int64_t y_img = 0);
 int conv_bwd_weight_core(const rram_conv_desc* d, int nimg, const float* dy, const float* col,
                          int64_t ldcol, float* dw, void* part, size_t part_bytes, hipStream_t s);
 int bwd_weight_split(int M, int N, int64_t K);
@@ -208,6 +208,37 @@ int rram_conv2d_fwd_cached(const rram_conv_desc* d_in, const float* x, const voi
   if (rc < 0) return rc;
   RRAM_REQUIRE(rc > 0, "conv2d_fwd_cached: the packed-weight engine did not run (w misaligned?)");
   return RRAM_OK;
+}
+
+int rram_conv2d_fwd_strided(const rram_conv_desc* d_in, const float* x, const void* x_oct, const float* w,
+                            void* w_pack, int w_pack_valid, const float* bias, float* y, int64_t y_image_stride,
+                            int relu, rram_stream_t s) {
+  RRAM_REQUIRE(w_pack != nullptr || !w_pack_valid, "conv2d_fwd_strided: w_pack_valid without a w_pack buffer");
+  rram_conv_desc d = *d_in;
+  int rc = rram_conv_out_shape(&d);
+  if (rc) return rc;
+  if (d.num == 0) return RRAM_OK;
+  RRAM_REQUIRE(x && w && y, "conv2d_fwd_strided: NULL pointer");
+  const int64_t dense = (int64_t)d.num_output * d.out_h * d.out_w;
+  RRAM_REQUIRE(y_image_stride >= dense, "conv2d_fwd_strided: image stride %lld < num_output * Ho * Wo = %lld",
+               (long long)y_image_stride, (long long)dense);
+  RRAM_REQUIRE(((int64_t)d.num - 1) * y_image_stride + dense < (1ll << 31) &&
+                   (int64_t)d.num * d.out_h * d.out_w < (1ll << 31),
+               "conv2d_fwd_strided: output span >= 2^31 floats");
+  RRAM_REQUIRE(x_oct == nullptr || d.channels % 8 == 0, "conv2d_fwd_strided: input octets need channels %% 8 == 0");
+  WPack wk;
+  wk.y_img = y_image_stride;
+  if (w_pack != nullptr) {
+    RRAM_REQUIRE(rram_conv_weight_pack_bytes(&d) > 0, "conv2d_fwd_strided: this shape's engine takes no weight pack");
+    RRAM_REQUIRE((reinterpret_cast<uintptr_t>(w_pack) & 15u) == 0, "conv2d_fwd_strided: w_pack must be 16-byte aligned");
+    wk.p = w_pack;
+    wk.valid = w_pack_valid != 0;
+  }
+  rc = conv_x6_fwd(&d, x, x_oct, w, bias, y, nullptr, relu, as_stream(s), wk);
+  if (rc < 0) return rc;
+  if (rc > 0) return RRAM_OK;
+  RRAM_REQUIRE(w_pack == nullptr, "conv2d_fwd_strided: the packed-weight engine did not run (w misaligned?)");
+  return conv_fwd_core(&d, x, w, bias, y, relu, as_stream(s), y_image_stride);
 }
 
 namespace {

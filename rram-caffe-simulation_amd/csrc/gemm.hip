@@ -1641,9 +1641,11 @@ int conv_patch_fwd(const rram_conv_desc* d, const float* w, Params& P, hipStream
 }
 
 int conv_fwd_core(const rram_conv_desc* d, const float* x, const float* w, const float* bias,
-                  float* y, int relu, hipStream_t s) {
+                  float* y, int relu, hipStream_t s, int64_t y_img) {
   {
-    const int rc = conv_x6_fwd(d, x, nullptr, w, bias, y, nullptr, relu, s);  // x6.hip
+    WPack wk;
+    wk.y_img = y_img;
+    const int rc = conv_x6_fwd(d, x, nullptr, w, bias, y, nullptr, relu, s, wk);  // x6.hip
     if (rc != 0) return rc < 0 ? rc : RRAM_OK;
   }
   const int g = d->group;
@@ -1680,7 +1682,7 @@ int conv_fwd_core(const rram_conv_desc* d, const float* x, const float* w, const
   RRAM_REQUIRE((int64_t)d->num * cv.chw * 4 < (1ll << 31), "conv2d_fwd: input must be < 2 GiB (32-bit buffer offsets)");
   cv.in_bytes = static_cast<int>((int64_t)d->num * cv.chw * 4);
   P.e = make_epi(y, HoWo, 1.0f, 0.0f, bias, RRAM_BIAS_ROW, relu);
-  P.e.cimg = (int64_t)d->num_output * HoWo;
+  P.e.cimg = y_img > 0 ? y_img : (int64_t)d->num_output * HoWo;
   P.e.hw = make_fastdiv(HoWo);
   P.grp_a = (int64_t)cout_g * K;
   P.grp_b = (int64_t)cin_g * d->height * d->width;

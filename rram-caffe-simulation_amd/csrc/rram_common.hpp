@@ -140,14 +140,18 @@ __host__ __device__ __forceinline__ float u01(uint32_t r) {
   return static_cast<float>(r >> 8) * (1.0f / 16777216.0f);
 }
 
-// Packed-weight companion of a convolution (rram_conv2d_fwd_cached): the
-// bf16x6 engine's pre-split fragment form of w in a caller-owned buffer that
-// outlives the call, so weights that do not change between calls (Monte-Carlo
-// inference: only the faultable blobs are rewritten) are split once.
+// Call options of the bf16x6 convolution forward.  The packed-weight
+// companion (rram_conv2d_fwd_cached): the engine's pre-split fragment form of
+// w in a caller-owned buffer that outlives the call, so weights that do not
+// change between calls (Monte-Carlo inference: only the faultable blobs are
+// rewritten) are split once.  y_img: the output's image stride in floats
+// (rram_conv2d_fwd_strided: y inside a larger NCHW tensor, e.g. a Concat top
+// at a channel offset); 0 = dense (num_output * Ho * Wo).
 struct WPack {
   void* p = nullptr;         // caller's buffer (nullptr: the per-stream scratch buffer)
   bool valid = false;        // p already holds this shape's pack of w: launch no pack kernel
   size_t* query = nullptr;   // set: report the pack bytes of the engine that would run, launch nothing
+  int64_t y_img = 0;
 };
 int conv_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, const float* w, const float* bias,
                 float* y, void* y_oct, int relu, hipStream_t s, const WPack& wk = WPack{});

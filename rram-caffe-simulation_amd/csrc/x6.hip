@@ -548,13 +548,20 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
 // matrix-core shape differs.  MI355X_MICROARCH.md (DVFS give-back, item 7):
 // at equal cycles per FLOP a 16x16x32 loop on random data holds a higher
 // clock than a 32x32x16 one (1.12-1.15x the FLOP/s, LDS-fed).
-// K order: a K-tile is still 16 channels (two octets) x all T taps; MFMA
-// group p pairs taps 2p and 2p + 1: lane group g = lane >> 4 of the operands
-// holds octet g & 1 at tap 2p + (g >> 1).  With T odd the last group's upper
-// half (tap T) is padding: zero weights (pack) and B zeroed after the read, so
-// a non-finite input never meets a zero weight.  Wave tile = 32 rows (two
-// 16-row blocks) x 32 NB columns (2 NB 16-column blocks), the accumulators
-// the same 64 floats per lane as the 32x32 form.
+// K order: a K-tile is still 16 channels (two octets) x all T taps; an MFMA
+// group's lane group g = lane >> 4 of the operands holds octet g & 1 at one
+// tap (lower half g < 2, upper half g >= 2): taps 2p, 2p + 1 of one K-tile,
+// or tap T - 1 of two consecutive K-tiles (the cross group, see the loop).
+// Wave tile = 32 rows (two 16-row blocks) x 32 NB columns (2 NB 16-column
+// blocks), the accumulators the same 64 floats per lane as the 32x32 form.
+// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
 namespace cb16 {
 constexpr int FRAG = 3 * 64;  // bf16x8 units per fragment (3 terms x 64 lanes): 16 rows x 32 k
 }  // namespace cb16
@@ -719,32 +726,43 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
     dma_b128(xrsrc, poff[i] + static_cast<uint32_t>(kt) * 2u * PL,
              lds0 + static_cast<uint32_t>(stg * SFB + (wave * PD + i) * 1024));
   };
-  // the lane's byte offset of pair group p: tap 2p (lower half) or 2p + 1
-  // (upper half; tap 2p again for the padded half of the last group)
+  // K order (T odd: 3x3, 5x5): K-tiles alternate even / odd.  An even K-tile
+  // runs H = T / 2 pair groups (taps 2p, 2p + 1: lower / upper half) and
+  // leaves tap T - 1; the odd K-tile after it starts with the cross group
+  // (lower half: the even K-tile's tap T - 1 from the stage before, upper
+  // half: its own tap T - 1), then its H pairs.  So no MFMA group is padded,
+  // except a last even K-tile's tap T - 1 (odd KT): its upper half is zero
+  // weights (pack) and zero B, so a non-finite input never meets a zero
+  // weight.  The cross group reads the stage the odd K-tile's refill writes
+  // next: a barrier after it (odd K-tiles only) orders the refill behind it.
+  constexpr int H = T / 2;
+  static_assert(T % 2 == 1, "odd tap counts (3x3, 5x5)");
   const int rowb = rpc * 16;
-  // (opaque to the compiler: hoisted out of the K-tile loop, the NJ x PP
-  // sums bb[j] + tap_off(p) would each hold a register)
-  auto tap_off = [&](int p) {
-    const int s0 = 2 * p, s1 = 2 * p + 1;
-    const int o0 = (s0 / KW) * rowb + (s0 % KW) * 48;
-    const int d = s1 < T ? ((s1 / KW) - (s0 / KW)) * rowb + ((s1 % KW) - (s0 % KW)) * 48 : 0;
-    int o = o0 + (up ? d : 0);
+  auto toff = [&](int s) { return (s / KW) * rowb + (s % KW) * 48; };  // uniform
+  // (opaque to the compiler: hoisted out of the K-tile loop, the NJ x H sums
+  // bb[j] + pair_off(s0) would each hold a register)
+  auto pair_off = [&](int s0) {
+    int o = toff(s0) + (up ? toff(s0 + 1) - toff(s0) : 0);
     asm volatile("" : "+v"(o));
     return o;
   };
   x6::bf16x8 fa[2][MI][3], fb[2][3];
-  auto read_b = [&](x6::bf16x8 (&f)[3], const char* st, int to, int p, int j) {
+  // group kinds: 0 pair (s0, s0 + 1), 1 cross (tap T - 1 of two K-tiles), 2 padded (tap T - 1, upper zero)
+  auto read_b = [&](x6::bf16x8 (&f)[3], const char* lo, const char* hi, int kind, int s0, int j) {
+    const char* st = kind == 1 ? (up ? hi : lo) : lo;
+    const int to = kind == 0 ? pair_off(s0) : toff(T - 1);
     const char* q = st + bb[j] + to;
 #pragma unroll
     for (int t = 0; t < 3; ++t) f[t] = *reinterpret_cast<const x6::bf16x8*>(q + 16 * t);
-    if (2 * p + 1 >= T) {  // padded upper half: zero B (its weights are zero too)
+    if (kind == 2) {
 #pragma unroll
       for (int t = 0; t < 3; ++t) f[t] = up ? x6::bf16x8{} : f[t];
     }
   };
 
   {
-    const x6::bf16x8* ap = wpack + ((int64_t)((z * P.tiles_m + tm) * WR + wr) * KT) * PP * MI * cb16::FRAG + lane;
+    const int NQ = (KT * T + 1) / 2;  // MFMA groups of the whole K
+    const x6::bf16x8* ap = wpack + ((int64_t)((z * P.tiles_m + tm) * WR + wr) * NQ) * MI * cb16::FRAG + lane;
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint16_t*>(xg), 0, static_cast<int>(xrange - static_cast<uint32_t>(z * (cv.C >> 3)) * PL), 0x00020000);
     auto load_a = [&](x6::bf16x8 (&f)[MI][3], int q) {
@@ -753,7 +771,8 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
 #pragma unroll
         for (int t = 0; t < 3; ++t) f[i][t] = ap[(q * MI + i) * cb16::FRAG + t * 64];
     };
-    constexpr int PMAX = (PD + PP - 2) / (PP - 1);  // patch pieces per group
+    constexpr int PMAX = (PD + H - 2) / (H - 1);  // patch pieces per group (the shortest K-tile spreads them over H - 1 groups)
+    static_assert(H >= 2, "pair groups");
     typedef int int4x __attribute__((ext_vector_type(4)));
     int4x stg[2][PMAX];
 #pragma unroll
@@ -761,46 +780,60 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
     load_a(fa[0], 0);
     wait_vm<0>();
     __builtin_amdgcn_s_barrier();
-    read_b(fb[0], smem, tap_off(0), 0, 0);
-    auto vtile = [&](int kt, auto par_c, auto more_c) {
-      constexpr int PAR = decltype(par_c)::value;
-      constexpr bool MORE = decltype(more_c)::value;
+    // the first K-tile is even: pair (0, 1), or the padded group when T == 1 ... (T >= 9 here)
+    read_b(fb[0], smem, smem, 0, 0, 0);
+    // K-tile kt of kind ODD (0 even, 1 odd); q0 = its first global group;
+    // MORE: a next K-tile exists; PADT: the padded group ends it (last even K-tile)
+    auto ktile = [&](int kt, int q0, auto odd_c, auto more_c, auto padt_c) {
+      constexpr bool ODD = decltype(odd_c)::value, MORE = decltype(more_c)::value, PADT = decltype(padt_c)::value;
+      constexpr int NG = ODD ? H + 1 : H + (PADT ? 1 : 0);
+      constexpr int PAR = ODD ? (H & 1) : 0;  // A parity: an (even, odd) pair of K-tiles runs 2 H + 1 groups
       const char* cur = smem + (kt & 1) * SFB;
-      const char* nxt = smem + ((kt + 1) & 1) * SFB;
+      const char* oth = smem + ((kt + 1) & 1) * SFB;  // the stage before = the stage refilled next
       char* nst = smem + ((kt + 1) & 1) * SFB + wave * PD * 1024 + lane * 16;
-#pragma unroll
-      for (int p = 0; p < PP; ++p) {
-        const int pa = (p + PAR) & 1;
-        const int q = kt * PP + p;
-        const int to = tap_off(p), to1 = p + 1 < PP ? tap_off(p + 1) : tap_off(0);
+      static_for<0, NG>([&](auto gc) {
+        constexpr int gi = decltype(gc)::value;
+        constexpr int KIND = ODD ? (gi == 0 ? 1 : 0) : (gi < H ? 0 : 2);
+        constexpr int S0 = ODD ? 2 * (gi - 1) : 2 * gi;
+        constexpr int pa = (gi + PAR) & 1;
+        // the group after this one (same K-tile)
+        constexpr int NKIND = ODD ? 0 : (gi + 1 < H ? 0 : 2);
+        constexpr int NS0 = ODD ? 2 * gi : 2 * (gi + 1);
+        const int q = q0 + gi;
         if (MORE) {
-          if (p > 0) {
+          if (gi > 0) {
 #pragma unroll
-            for (int i = cbx6::piece_lo(p - 1, PD, PP); i < cbx6::piece_lo(p, PD, PP); ++i)
-              *reinterpret_cast<int4x*>(nst + i * 1024) = stg[(p - 1) & 1][i - cbx6::piece_lo(p - 1, PD, PP)];
+            for (int i = cbx6::piece_lo(gi - 1, PD, NG); i < cbx6::piece_lo(gi, PD, NG); ++i)
+              *reinterpret_cast<int4x*>(nst + i * 1024) = stg[(gi - 1) & 1][i - cbx6::piece_lo(gi - 1, PD, NG)];
           }
 #pragma unroll
-          for (int i = cbx6::piece_lo(p, PD, PP); i < cbx6::piece_lo(p + 1, PD, PP); ++i)
-            stg[p & 1][i - cbx6::piece_lo(p, PD, PP)] = __builtin_bit_cast(
+          for (int i = cbx6::piece_lo(gi, PD, NG); i < cbx6::piece_lo(gi + 1, PD, NG); ++i)
+            stg[gi & 1][i - cbx6::piece_lo(gi, PD, NG)] = __builtin_bit_cast(
                 int4x, __builtin_amdgcn_raw_buffer_load_b128(
                            xr, static_cast<int>(poff[i] + static_cast<uint32_t>(kt + 1) * 2u * PL), 0, 0));
         }
-        if (p + 1 < PP || MORE) load_a(fa[pa ^ 1], q + 1);
+        if (gi + 1 < NG || MORE) load_a(fa[pa ^ 1], q + 1);
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
-          const bool last = p == PP - 1 && j == NJ - 1;
+          const bool last = gi == NG - 1 && j == NJ - 1;
           if (last && MORE) {  // the next stage is complete
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
           }
           if (!last) {
-            if (j + 1 < NJ)
-              read_b(fb[(j + 1) & 1], cur, to, p, j + 1);
+            if (j + 1 < NJ)  // (the cross group: lower half from the stage before)
+              read_b(fb[(j + 1) & 1], KIND == 1 ? oth : cur, cur, KIND, S0, j + 1);
             else
-              read_b(fb[(j + 1) & 1], cur, to1, p + 1, 0);
+              read_b(fb[(j + 1) & 1], cur, cur, NKIND, NS0, 0);
           } else if (MORE) {
-            read_b(fb[0], nxt, to1, 0, 0);
+            // the next K-tile's first group: after an even K-tile the cross
+            // group (lower half here, upper half in the new stage), after an
+            // odd one the pair (0, 1) of the new stage
+            if (ODD)
+              read_b(fb[0], oth, oth, 0, 0, 0);
+            else
+              read_b(fb[0], cur, oth, 1, 0, 0);
           }
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -809,28 +842,32 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
                                      x6::Parts{fb[j & 1][0], fb[j & 1][1], fb[j & 1][2]}, acc[i][j]);
           __builtin_amdgcn_sched_barrier(0);
         }
-      }
+        if (ODD && gi == 0 && MORE) {  // every wave is past the cross group: the refill may overwrite `oth`
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      });
     };
     using T_ = std::true_type;
     using F_ = std::false_type;
-    using P0 = std::integral_constant<int, 0>;
-    using P1 = std::integral_constant<int, 1>;
-    if constexpr (PP % 2 == 0) {
-      int kt = 0;
-      for (; kt + 1 < KT; ++kt) vtile(kt, P0{}, T_{});
-      vtile(kt, P0{}, F_{});
+    int kt = 0;
+    for (; kt + 2 < KT; kt += 2) {
+      const int q0 = (kt / 2) * (2 * H + 1);
+      ktile(kt, q0, F_{}, T_{}, F_{});
+      ktile(kt + 1, q0 + H, T_{}, T_{}, F_{});
+      // the pair ran 2 H + 1 groups: the next A sits in fa[1]
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int t = 0; t < 3; ++t) fa[0][i][t] = fa[1][i][t];
+    }
+    const int q0 = (kt / 2) * (2 * H + 1);
+    if (kt + 1 < KT) {
+      ktile(kt, q0, F_{}, T_{}, F_{});
+      ktile(kt + 1, q0 + H, T_{}, F_{}, F_{});
     } else {
-      int kt = 0;
-      for (; kt + 2 < KT; kt += 2) {
-        vtile(kt, P0{}, T_{});
-        vtile(kt + 1, P1{}, T_{});
-      }
-      if (kt + 1 < KT) {
-        vtile(kt, P0{}, T_{});
-        vtile(kt + 1, P1{}, F_{});
-      } else {
-        vtile(kt, P0{}, F_{});
-      }
+      ktile(kt, q0, F_{}, F_{}, T_{});
     }
   }
   const int mwave = m0 + 32 * wr, nwave = n0 + wc * 32 * NB;
@@ -868,28 +905,42 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
   }
 }
 
-// w [G*M][Cg][T] -> k_conv_cb16_x6 fragments [G][rblocks][Cg/16][PP][2][term][64 lanes][8]:
-// lane l of fragment (kt, p, i) holds row 32 rb + 16 i + (l & 15), channels
-// 16 kt + 8 ((l >> 4) & 1) .. + 7 at tap 2 p + (l >> 5) (zero at tap T).
+// w [G*M][Cg][T] -> k_conv_cb16_x6 fragments [G][rblocks][NQ][2][term][64 lanes][8],
+// NQ = ceil(KT T / 2) groups in the kernel's K order: per (even, odd) pair
+// of K-tiles, H = T / 2 pairs of the even one, the cross group, H pairs of
+// the odd one (an odd KT ends with the padded group).  Lane l of fragment
+// (q, i) holds row 32 rb + 16 i + (l & 15), channel octet (l >> 4) & 1 of its
+// half's K-tile at its half's tap (l >> 5: upper half); zero on padding.
 __global__ void __launch_bounds__(256) k_conv_cb16_pack_x6(const float* __restrict__ w, char* __restrict__ out, int M,
                                                            int Cg, int T, int rblocks, int units) {
-  const int KT = Cg >> 4, PP = (T + 1) / 2;
+  const int KT = Cg >> 4, H = T / 2, NQ = (KT * T + 1) / 2;
   for (int u = blockIdx.x * blockDim.x + threadIdx.x; u < units; u += gridDim.x * blockDim.x) {
-    const int lane = u & 63;
+    const int lane = u & 63, up = lane >> 5;
     int r = u >> 6;
     const int i = r & 1;
     r >>= 1;
-    const int p = r % PP;
-    r /= PP;
-    const int kt = r % KT;
-    r /= KT;
+    const int q = r % NQ;
+    r /= NQ;
     const int rb = r % rblocks;
     const int gz = r / rblocks;
-    const int m = rb * 32 + 16 * i + (lane & 15), c0 = kt * 16 + ((lane >> 4) & 1) * 8, s = 2 * p + (lane >> 5);
+    // (K-tile, tap) of this lane's half in group q
+    const int a = q / (2 * H + 1), gq = q - a * (2 * H + 1);
+    int kt, s;
+    if (gq < H) {                   // pair of the even K-tile 2a
+      kt = 2 * a;
+      s = 2 * gq + up;
+    } else if (gq == H) {           // cross group (or the padded one at an odd KT's end)
+      kt = 2 * a + up;
+      s = T - 1;
+    } else {                        // pair of the odd K-tile 2a + 1
+      kt = 2 * a + 1;
+      s = 2 * (gq - H - 1) + up;
+    }
+    const int m = rb * 32 + 16 * i + (lane & 15), c0 = kt * 16 + ((lane >> 4) & 1) * 8;
+    const bool ok = m < M && kt < KT;
     float v[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e)
-      v[e] = (m < M && s < T) ? w[((int64_t)gz * M + m) * Cg * T + (int64_t)(c0 + e) * T + s] : 0.0f;
+    for (int e = 0; e < 8; ++e) v[e] = ok ? w[((int64_t)gz * M + m) * Cg * T + (int64_t)(c0 + e) * T + s] : 0.0f;
     x6::Parts t;
     x6::split8_safe(v, t);
     char* f = out + (int64_t)(u >> 6) * 3072 + lane * 16;
@@ -970,14 +1021,6 @@ __global__ void __launch_bounds__(256) k_conv_cb_pack_x6(const float* __restrict
 // slot 2 at the start of the tile it serves (read from group 18 on); three
 // barriers per tile.  The weight fragments come from L2 into registers two
 // groups ahead (fragment order, k_conv1_pack_x6).
-// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
-template <int B, int E, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (B < E) {
-    f(std::integral_constant<int, B>{});
-    static_for<B + 1, E>(f);
-  }
-}
 namespace c1x6 {
 constexpr int BM = 96, BN = 256;
 constexpr int HR = 6, KQ = 3, C = 3, QH = C * HR * KQ, G = QH / 2;  // 54 quads per half, 27 groups
@@ -1612,7 +1655,7 @@ int conv_wide_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, co
   cv.chw = (int64_t)3 * d->height * d->width;
   cv.in_bytes = static_cast<int>((int64_t)d->num * cv.chw * 4);
   P.e = make_epi(y, HW, 1.0f, 0.0f, bias, RRAM_BIAS_ROW, relu);
-  P.e.cimg = (int64_t)d->num_output * HW;
+  P.e.cimg = wk.y_img > 0 ? wk.y_img : (int64_t)d->num_output * HW;
   P.e.hw = make_fastdiv(HW);
   const int units = c1x6::G * 3 * 64;  // 3 KB fragments
   const size_t wbytes = static_cast<size_t>(units) * 48;
@@ -1790,20 +1833,27 @@ bool cb16_instantiated(int KH, int WR, int NB, int PD, int OCC) {
 #undef RRAM_X
   return false;
 }
-// RRAM_CB16: which octet-kernel plans run on 16x16x32 (bit 0: 5x5, bit 1: 3x3)
-bool cb16_for(int KH) {
+// Which octet-kernel plans run on 16x16x32: bit 0 the 5x5 plans, bit 1 the
+// 3x3 plans at one workgroup per CU, bit 2 the 3x3 plans at two.  Default 5
+// (RRAM_CB16 overrides it for A/Bs).  Measured on MI355X (AlexNet b256,
+// profiles/r04_ab_cb16.txt): the 16x16x32 loop holds a 6-13 % higher clock;
+// conv2 (5x5, two workgroups per CU) 0.482 -> 0.457-0.461 ms, conv5 (3x3, two
+// per CU) 0.170 -> 0.166; conv3 / conv4 (one per CU) lose MFMA-busy (0.64 ->
+// 0.59, 0.54 -> 0.51) faster than they gain clock (0.340 -> 0.350, 0.287 ->
+// 0.300), so they stay on 32x32x16.
+bool cb16_for(int KH, int OCC) {
   static const int mode = [] {
     const char* e = getenv("RRAM_CB16");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 5;
   }();
-  return (mode & (KH == 5 ? 1 : 2)) != 0;
+  return (mode & (KH == 5 ? 1 : OCC == 1 ? 2 : 4)) != 0;
 }
 
 int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, const float* w, const float* bias,
                    float* y, void* y_oct, int relu, hipStream_t s, const WPack& wk) {
   CbPlan pl;
   if (!conv_cb_plan(d, pl)) return 0;
-  const bool use16 = cb16_for(d->kernel_h) && cb16_instantiated(d->kernel_h, pl.WR, pl.NB, pl.PD, pl.OCC);
+  const bool use16 = cb16_for(d->kernel_h, pl.OCC) && cb16_instantiated(d->kernel_h, pl.WR, pl.NB, pl.PD, pl.OCC);
   if (y_oct != nullptr && d->num_output % 8 != 0) return 0;
   const int KH = d->kernel_h, KW = d->kernel_w, T = KH * KW;
   const int G = d->group, Cg = d->channels / G, M = d->num_output / G;
@@ -1831,7 +1881,7 @@ int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, c
   cv.howo = make_fastdiv(HW);
   cv.wo_div = make_fastdiv(d->out_w);
   P.e = make_epi(y, HW, 1.0f, 0.0f, bias, RRAM_BIAS_ROW, relu);
-  P.e.cimg = (int64_t)d->num_output * HW;
+  P.e.cimg = wk.y_img > 0 ? wk.y_img : (int64_t)d->num_output * HW;
   P.e.hw = make_fastdiv(HW);
   P.grp_c = (int64_t)M * HW;
   P.grp_bias = M;
@@ -1842,7 +1892,8 @@ int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, c
   // input's octet companion), then the weight fragments
   const int64_t xbytes = (int64_t)d->num * d->channels * HWi * 6;
   const int rblocks = pl.tiles_m * pl.WR;
-  const int64_t wfrags = use16 ? (int64_t)G * rblocks * (Cg / 16) * ((T + 1) / 2) * 2 : (int64_t)G * rblocks * (Cg / 16) * T;
+  const int64_t wfrags =
+      use16 ? (int64_t)G * rblocks * (((Cg / 16) * T + 1) / 2) * 2 : (int64_t)G * rblocks * (Cg / 16) * T;
   if (wk.query) {
     *wk.query = static_cast<size_t>(wfrags * 3072);
     return 1;
@@ -1957,7 +2008,7 @@ int conv_patch_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, c
   cv.chw = (int64_t)d->channels * d->height * d->width;
   cv.in_bytes = static_cast<int>((int64_t)d->num * cv.chw * 4);
   P.e = make_epi(y, HW, 1.0f, 0.0f, bias, RRAM_BIAS_ROW, relu);
-  P.e.cimg = (int64_t)d->num_output * HW;
+  P.e.cimg = wk.y_img > 0 ? wk.y_img : (int64_t)d->num_output * HW;
   P.e.hw = make_fastdiv(HW);
   P.grp_b = (int64_t)Cg * d->height * d->width;
   P.grp_c = (int64_t)M * HW;

@@ -91,6 +91,13 @@ class Layer {
     return false;
   }
   bool folded_into_next = false;
+  // TEST-phase Concat fold (Net::Net): a producer whose top only feeds a
+  // channel Concat writes its output straight into the Concat top at a
+  // channel offset (write_into_concat: true when it can), and the Concat then
+  // skips that bottom's copy (skip_concat_bottom).  The producer's own top is
+  // then never materialised (like a folded LRN's).
+  virtual bool write_into_concat(Blob<Dtype>* /*concat_top*/, int /*channel_offset*/) { return false; }
+  virtual void skip_concat_bottom(int /*bottom_index*/) {}
 
  protected:
   virtual void Forward_gpu(const std::vector<Blob<Dtype>*>& bottom,

@@ -237,10 +237,37 @@ void ConvolutionLayer<Dtype>::Forward_gpu(const std::vector<Blob<Dtype>*>& botto
       xo = buf;
     }
   }
-  float* y = top[0]->mutable_gpu_data();  // invalidates top's companion
-  void* yo = octets_for(top[0], kOctConv);
   const float* bias = bias_term_ ? this->blobs_[1]->gpu_data() : nullptr;
   const size_t wpb = cache_wpack ? rram_conv_weight_pack_bytes(&desc_) : 0;
+  if (concat_top_ != nullptr) {
+    // TEST-phase Concat fold: straight into the Concat top's channel slice
+    // (replaces concat_layer.cu's copy of this bottom); top[0] stays unwritten
+    const int64_t hw = (int64_t)desc_.out_h * desc_.out_w;
+    CAFFE_CHECK(concat_top_->num_axes() == 4 && concat_top_->shape(0) == desc_.num &&
+                    concat_top_->count(2) == hw && concat_off_ + desc_.num_output <= concat_top_->shape(1),
+                this->name() << ": folded Concat top " << concat_top_->shape_string() << " does not fit");
+    float* yc = concat_top_->mutable_gpu_data() + concat_off_ * hw;
+    void* wp = nullptr;
+    int wvalid = 0;
+    uint64_t key = 0;
+    SyncedMemory* wm = this->blobs_[0]->data().get();
+    if (wpb > 0) {
+      const int* f = reinterpret_cast<const int*>(&desc_);
+      key = 1469598103934665603ull;
+      for (size_t i = 0; i < sizeof(rram_conv_desc) / sizeof(int); ++i) key = (key ^ (uint32_t)f[i]) * 1099511628211ull;
+      key = (key ^ (uint64_t)rram_get_f32_engine()) * 1099511628211ull;
+      (void)this->blobs_[0]->gpu_data();
+      wp = wm->wpack(wpb);
+      wvalid = wm->wpack_valid(key) ? 1 : 0;
+    }
+    RRAM_CALL(rram_conv2d_fwd_strided(&desc_, bottom[0]->gpu_data(), xo, this->blobs_[0]->gpu_data(), wp, wvalid,
+                                      bias, yc, (int64_t)concat_top_->shape(1) * hw, fused_relu ? 1 : 0,
+                                      Caffe::stream()));
+    if (wpb > 0) wm->set_wpack_valid(key);
+    return;
+  }
+  float* y = top[0]->mutable_gpu_data();  // invalidates top's companion
+  void* yo = octets_for(top[0], kOctConv);
   if (wpb > 0) {
     // the pack is valid for this layer's shape and engine until the weights'
     // next mutable access (the MC driver's injection, a solver update, ...)
@@ -738,12 +765,24 @@ class ConcatLayer : public Layer<Dtype> {
     const int inner = (int)top[0]->count(axis_ + 1), outer = (int)top[0]->count(0, axis_);
     const int dci = top[0]->shape(axis_) * inner;
     int off = 0;
-    for (auto* b : bottom) {
-      const int sci = b->shape(axis_) * inner;
-      RRAM_CALL(rram_concat_copy(b->gpu_data(), top[0]->mutable_gpu_data(), outer, sci, dci, off, 0, Caffe::stream()));
+    for (size_t i = 0; i < bottom.size(); ++i) {
+      const int sci = bottom[i]->shape(axis_) * inner;
+      // a folded bottom's producer already wrote its slice (Net: TEST-phase Concat fold)
+      if (!(i < skip_.size() && skip_[i]))
+        RRAM_CALL(rram_concat_copy(bottom[i]->gpu_data(), top[0]->mutable_gpu_data(), outer, sci, dci, off, 0,
+                                   Caffe::stream()));
       off += sci;
     }
   }
+ public:
+  void skip_concat_bottom(int i) override {
+    if ((int)skip_.size() <= i) skip_.resize(i + 1, false);
+    skip_[i] = true;
+  }
+  int axis() const { return axis_; }
+
+ protected:
+  std::vector<bool> skip_;
   void Backward_gpu(const std::vector<Blob<Dtype>*>& top, const std::vector<bool>& pd,
                     const std::vector<Blob<Dtype>*>& bottom) override {
     if (bottom.size() == 1) return;

@@ -26,6 +26,11 @@ class ConvolutionLayer : public Layer<Dtype> {
   // unchanged; set by Net::set_weight_pack_cache for the Monte-Carlo driver
   bool cache_wpack = false;
   const rram_conv_desc& desc() const { return desc_; }
+  bool write_into_concat(Blob<Dtype>* concat_top, int channel_offset) override {
+    concat_top_ = concat_top;
+    concat_off_ = channel_offset;
+    return true;
+  }
 
  protected:
   void Forward_gpu(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override;
@@ -36,6 +41,8 @@ class ConvolutionLayer : public Layer<Dtype> {
   // the forward reads its input's channel-octet companion (cached per input shape / engine)
   bool want_in_oct_ = false;
   int oct_key_[4] = {-1, -1, -1, -1};
+  Blob<Dtype>* concat_top_ = nullptr;  // write_into_concat: the output goes to this top at channel concat_off_
+  int concat_off_ = 0;
 };
 
 // ★ InnerProduct (inner_product_layer.cpp:9-141, .cu:9-75).

@@ -134,6 +134,15 @@ static Msg InputsToLayer(const Msg& param) {
   return out;
 }
 
+namespace {
+// concat_param.axis (or its V1 spelling concat_dim), as ConcatLayer reads it
+int canon_axis_of(const Msg& lp) {
+  const Msg& cp = lp.sub_or_empty("concat_param");
+  const int a = (int)cp.integer("axis", cp.integer("concat_dim", 1));
+  return a < 0 ? a + 4 : a;
+}
+}  // namespace
+
 template <typename Dtype>
 Net<Dtype>::Net(const Msg& in_param, Phase phase, const Msg& options) : phase_(phase) {
   Msg param = InsertSplits(FilterNet(InputsToLayer(in_param), phase));
@@ -146,6 +155,7 @@ Net<Dtype>::Net(const Msg& in_param, Phase phase, const Msg& options) : phase_(p
   }
   const bool fuse_relu = options.boolean("fuse_relu", true);
   const bool fuse_lrn_pool = options.boolean("fuse_lrn_pool", true);
+  const bool fuse_concat = options.boolean("fuse_concat", true);
   std::vector<int> data_shape;
   {
     std::string ds = options.str("data_shape", "");
@@ -284,6 +294,43 @@ Net<Dtype>::Net(const Msg& in_param, Phase phase, const Msg& options) : phase_(p
         blob_need_backward_[bottom_id_vecs_[l][j]] = blob_need_backward_[bottom_id_vecs_[l][j]] || nb;
       }
       for (size_t p = 0; p < layers_[l]->blobs().size(); ++p) layers_[l]->set_param_propagate_down(static_cast<int>(p), true);
+    }
+  }
+  // TEST phase: a channel Concat whose bottom is written only by a
+  // Convolution (plus its folded in-place ReLU) and read only by the Concat
+  // gets that slice written by the Convolution itself (rram_conv2d_fwd_strided)
+  // and skips its copy; the bottom blob is then never materialised
+  if (fuse_concat && phase == TEST) {
+    const int L = static_cast<int>(layers_.size());
+    for (int l = 0; l < L; ++l) {
+      if (std::string(layers_[l]->type()) != "Concat" || bottom_vecs_[l].size() < 2 || top_vecs_[l].size() != 1)
+        continue;
+      Blob<Dtype>* ct = top_vecs_[l][0];
+      if (ct->num_axes() != 4 || canon_axis_of(layers_[l]->layer_param()) != 1) continue;
+      int off = 0;
+      for (size_t j = 0; j < bottom_vecs_[l].size(); ++j) {
+        const int b = bottom_id_vecs_[l][j];
+        const int chans = bottom_vecs_[l][j]->shape(1);
+        int writer = -1;
+        bool ok = true;
+        for (int k = 0; k < L && ok; ++k) {
+          const bool reads = std::count(bottom_id_vecs_[k].begin(), bottom_id_vecs_[k].end(), b) > 0;
+          const bool writes = std::count(top_id_vecs_[k].begin(), top_id_vecs_[k].end(), b) > 0;
+          if (!reads && !writes) continue;
+          if (k == l && !writes) continue;                       // the Concat itself
+          auto* relu = dynamic_cast<ReLULayer<Dtype>*>(layers_[k].get());
+          if (relu && relu->folded) continue;                    // applied in the producer's epilogue
+          if (writes && !reads && writer < 0 && dynamic_cast<ConvolutionLayer<Dtype>*>(layers_[k].get())) {
+            writer = k;
+            continue;
+          }
+          ok = false;                                            // another reader or writer
+        }
+        if (ok && writer >= 0 && j < bottom_need_backward_[l].size() &&
+            layers_[writer]->write_into_concat(ct, off))
+          layers_[l]->skip_concat_bottom(static_cast<int>(j));
+        off += chans;
+      }
     }
   }
   for (auto& n : available) {

@@ -103,6 +103,7 @@ SIGNATURES = {
     "rram_conv_octet_plan": (I, [P, P]),
     "rram_conv_weight_pack_bytes": (SZ, [P]),
     "rram_conv2d_fwd_cached": (I, [P, P, P, P, P, I, P, P, P, I, P]),
+    "rram_conv2d_fwd_strided": (I, [P, P, P, P, P, I, P, P, C.c_int64, I, P]),
     "rram_pack_octets": (I, [P, P, I, I, I, I, P]),
     "rram_conv2d_bwd_workspace": (SZ, [P, I]),
     "rram_conv2d_bwd": (I, [P, P, P, P, P, P, P, P, SZ, P]),

@@ -213,6 +213,14 @@ def conv2d_fwd_cached(d, x, x_oct, w, w_pack, w_pack_valid, bias, y, y_oct=None,
                                           _p(bias), _p(y), _p(y_oct), int(relu), _stream()), "conv2d_fwd_cached")
 
 
+def conv2d_fwd_strided(d, x, w, bias, y, y_image_stride, relu=False, x_oct=None, w_pack=None, w_pack_valid=False):
+    """rram_conv2d_fwd_strided: image n's output at y + n * y_image_stride
+    floats (y may be a channel-offset view into a larger NCHW tensor)."""
+    K.check(_lib().rram_conv2d_fwd_strided(C.byref(d), _p(x), _p(x_oct), _p(w), _p(w_pack), int(bool(w_pack_valid)),
+                                           _p(bias), C.c_void_p(y.data_ptr()), int(y_image_stride), int(relu),
+                                           _stream()), "conv2d_fwd_strided")
+
+
 def conv_input_octets(d):
     """1 when rram_conv2d_fwd_octets would read an input companion for d now."""
     return _lib().rram_conv_input_octets(C.byref(d))

@@ -19,6 +19,7 @@ barrier + synchronize, max over ranks, whole-job throughput.
 from __future__ import annotations
 
 import math
+import os
 import time
 
 MFMA_F32_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: fp32 MFMA dense
@@ -288,7 +289,9 @@ def run_workload(args, world, rank, dev):
 
     if args.workload == "googlenet_sweep":
         batch = args.batch
-        net = caffe.Net(models.googlenet(test_batch=batch), "test", models.net_options("googlenet"))
+        # RRAM_FUSE_CONCAT=0: the unfolded net (A/B of the TEST-phase Concat fold)
+        fold = os.environ.get("RRAM_FUSE_CONCAT", "1") != "0"
+        net = caffe.Net(models.googlenet(test_batch=batch), "test", models.net_options("googlenet", fuse_concat=fold))
         rates = [0.001, 0.002, 0.005, 0.01, 0.02, 0.05, 0.10]
         nblobs = len(net.failure_params())
         # per-layer SA ratios: classifier weights lean SA0 (zero), aux-heads lean SA1 (+-1)

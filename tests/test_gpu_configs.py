@@ -306,16 +306,18 @@ def _c5_sweep_point(rs, oracle_mod, p_fault, B):
                          ("loss2/fc", "loss2/conv", True), ("loss2/classifier", "loss2/fc", False),
                          ("loss3/classifier", "pool5/7x7_s1", False)):
         R.check_ip(N(net.blob(k)), N(net.blob(bot)), p[k][0], p[k][1], relu=relu, what=k)
-    # and two convolutions of the trunk on the same forward
+    # and convolutions of the trunk on the same forward; the inception
+    # branches are read from their slices of the Concat top, which the
+    # TEST-phase Concat fold has them write directly (rram_conv2d_fwd_strided)
     R.check_conv(N(net.blob("conv1/7x7_s2"))[:4], N(net.blob("data"))[:4], p["conv1/7x7_s2"][0].reshape(64, 3, 7, 7),
                  p["conv1/7x7_s2"][1], 2, 3, relu=True, what="conv1/7x7_s2")
-    R.check_conv(N(net.blob("inception_4a/5x5"))[:4], N(net.blob("inception_4a/5x5_reduce"))[:4],
+    R.check_conv(N(net.blob("inception_4a/output"))[:4, 400:448], N(net.blob("inception_4a/5x5_reduce"))[:4],
                  p["inception_4a/5x5"][0].reshape(48, 16, 5, 5), p["inception_4a/5x5"][1], 1, 2, relu=True,
                  what="inception_4a/5x5")
-    R.check_conv(N(net.blob("inception_3a/1x1"))[:4], N(net.blob("pool2/3x3_s2"))[:4],
+    R.check_conv(N(net.blob("inception_3a/output"))[:4, 0:64], N(net.blob("pool2/3x3_s2"))[:4],
                  p["inception_3a/1x1"][0].reshape(64, 192, 1, 1), p["inception_3a/1x1"][1], 1, 0, relu=True,
                  what="inception_3a/1x1")
-    R.check_conv(N(net.blob("inception_4e/3x3"))[:4], N(net.blob("inception_4e/3x3_reduce"))[:4],
+    R.check_conv(N(net.blob("inception_4e/output"))[:4, 256:576], N(net.blob("inception_4e/3x3_reduce"))[:4],
                  p["inception_4e/3x3"][0].reshape(320, 160, 3, 3), p["inception_4e/3x3"][1], 1, 1, relu=True,
                  what="inception_4e/3x3")
     mc.close()
@@ -373,7 +375,7 @@ def test_c5_conv_fault_extension(rs, oracle_mod):
         R.check_conv(N(net.blob("conv1/7x7_s2"))[:4], N(net.blob("data"))[:4],
                      pl["conv1/7x7_s2"][0].reshape(64, 3, 7, 7), pl["conv1/7x7_s2"][1], 2, 3, relu=True,
                      what=f"conv1/7x7_s2 map {m}")
-        R.check_conv(N(net.blob("inception_4a/5x5"))[:4], N(net.blob("inception_4a/5x5_reduce"))[:4],
+        R.check_conv(N(net.blob("inception_4a/output"))[:4, 400:448], N(net.blob("inception_4a/5x5_reduce"))[:4],
                      pl["inception_4a/5x5"][0].reshape(48, 16, 5, 5), pl["inception_4a/5x5"][1], 1, 2, relu=True,
                      what=f"inception_4a/5x5 map {m}")
     checked = 0

@@ -352,3 +352,54 @@ def test_concat_fwd_bwd(device):
     ops.concat_copy(da, dst, 3, 4 * 5, 10 * 5, 0, backward=True)
     ops.concat_copy(db, dst, 3, 6 * 5, 10 * 5, 4 * 5, backward=True)
     assert torch.equal(da, a) and torch.equal(db, b)
+
+
+@pytest.mark.parametrize("xs,cout,k,s,p,g", [
+    ((3, 64, 14, 14), 48, 1, 1, 0, 1),       # 1x1 (fp32 MFMA GEMM)
+    ((3, 96, 14, 14), 208, 3, 1, 1, 1),      # 3x3, channel-octet kernel
+    ((3, 16, 14, 14), 48, 5, 1, 2, 1),       # 5x5, channel-octet kernel (one K-tile)
+    ((3, 24, 14, 14), 64, 3, 1, 1, 1),       # Cin % 16 != 0: patch kernel
+    ((2, 3, 64, 64), 64, 7, 2, 3, 1),        # 7x7 stride 2 (GoogLeNet conv1, 64-bit tap mask)
+    ((2, 3, 227, 227), 96, 11, 4, 0, 1),     # AlexNet conv1 (persistent ring kernel)
+    ((2, 64, 13, 13), 128, 3, 1, 1, 2),      # groups
+])
+def test_conv_fwd_strided_equals_dense(device, xs, cout, k, s, p, g):
+    """rram_conv2d_fwd_strided (the TEST-phase Concat fold's write): the
+    output lands in a channel slice of a wider NCHW tensor, bit-identical to
+    rram_conv2d_fwd, and nothing outside the slice is touched."""
+    import torch
+    from rramsim import ops
+    rng = np.random.default_rng(31)
+    x = torch.from_numpy(rng.standard_normal(xs).astype(np.float32)).to(device)
+    w = torch.from_numpy((rng.standard_normal((cout, xs[1] // g, k, k)) * 0.05).astype(np.float32)).to(device)
+    b = torch.from_numpy(rng.standard_normal(cout).astype(np.float32)).to(device)
+    d = ops.conv_desc(xs, cout, k, s, p, 1, g)
+    ref = torch.empty((xs[0], cout, d.out_h, d.out_w), device=device)
+    ops.conv2d_fwd(d, x, w, b, ref, relu=True)
+    ctot, off = cout + 40, 24
+    big = torch.full((xs[0], ctot, d.out_h, d.out_w), float("nan"), device=device)
+    ops.conv2d_fwd_strided(d, x, w, b, big[:, off:], ctot * d.out_h * d.out_w, relu=True)
+    torch.cuda.synchronize()
+    assert torch.equal(big[:, off:off + cout], ref)
+    assert torch.isnan(big[:, :off]).all() and torch.isnan(big[:, off + cout:]).all()
+
+
+def test_concat_fold_in_googlenet_test_net(device):
+    """Net folds the inception branch convolutions into their Concat tops in
+    the TEST phase (each writes its channel slice; the Concat copies nothing):
+    every Concat top and the net outputs are bit-identical to the unfolded net."""
+    import torch
+    from rramsim import caffe, models
+    caffe.set_stream_from_torch()
+    outs = []
+    for fuse in (False, True):
+        caffe.set_random_seed(1701)
+        net = caffe.Net(models.googlenet(test_batch=4), "test", models.net_options("googlenet", fuse_concat=fuse))
+        net.forward()
+        torch.cuda.synchronize()
+        names = [n for n in net.blob_names() if n.endswith("/output")] + ["loss3/classifier", "loss1/classifier"]
+        outs.append({n: net.blob(n).detach().cpu().clone() for n in names})
+        net.close()
+    assert len(outs[0]) == 11
+    for n in outs[0]:
+        assert torch.equal(outs[0][n], outs[1][n]), n
