@@ -231,6 +231,15 @@ int rram_mc_set_timing(rram_mc_t mc, int enable);
  * later layer writes a prefix blob in place.  Re-enable after changing the
  * input batch or a prefix weight (the prefix is recomputed on the next map). */
 int rram_mc_set_reuse_prefix(rram_mc_t mc, int enable);
+/* hipGraph replay of the maps (opt-in, for launch-bound small nets; no
+ * reference counterpart): one map (injection + forward + statistics) is
+ * captured after one eager map and replayed per map, the map id and the
+ * per-map row advancing in device memory.  Bit-identical to the eager maps;
+ * the eager path runs while timing, injection overlap or prefix reuse is on.
+ * RRAM_EINVAL for nets whose source layers advance between forwards
+ * (HDF5Data).  rram_mc_graph_active: 1 once a graph has been captured. */
+int rram_mc_set_graph(rram_mc_t mc, int enable);
+int rram_mc_graph_active(rram_mc_t mc, int* active);
 int rram_mc_inject_times(rram_mc_t mc, double* ms, long* launches, int64_t* weights, int reset);
 
 #ifdef __cplusplus

@@ -149,6 +149,13 @@ int rram_set_inject_grid(int blocks);
 int rram_inject_rng_batched(const rram_inject_seg* segs, int nsegs,
                             uint64_t seed, uint32_t map_id,
                             unsigned long long* counters, rram_stream_t stream);
+/* The same with the map id read from device memory at run time (a captured
+ * hipGraph of one Monte-Carlo map replays over consecutive maps; see
+ * rram_mc_accumulate_dev).  Bit-identical to rram_inject_rng_batched with
+ * map_id = *map_id_dev. */
+int rram_inject_rng_batched_dev(const rram_inject_seg* segs, int nsegs, uint64_t seed,
+                                const uint32_t* map_id_dev, unsigned long long* counters,
+                                rram_stream_t stream);
 
 /* Monte-Carlo statistics of one map in one launch (the MC analogue of
  * Solver::Test's score accumulation, src/caffe/solver.cpp:410-430):
@@ -159,6 +166,12 @@ typedef struct {
   int n;
 } rram_mc_outputs;
 int rram_mc_accumulate(const rram_mc_outputs* outs, float* sums, float* per_map_row, rram_stream_t stream);
+/* rram_mc_accumulate with the per-map row from device memory: row = *row_dev,
+ * per_map[row * row_stride + k] = p[k][0] when row < max_rows (per_map
+ * nullable); advance != 0 then increments *row_dev and *map_id_dev (nullable)
+ * on the device, after every lane read them. */
+int rram_mc_accumulate_dev(const rram_mc_outputs* outs, float* sums, float* per_map, int64_t row_stride,
+                           int max_rows, int* row_dev, uint32_t* map_id_dev, int advance, rram_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * Strategy / solver elementwise

@@ -345,9 +345,13 @@ __device__ __forceinline__ float inject1(float w, int64_t i, uint64_t seed, uint
 // FAST: every segment is plain stuck-at (mode 0), so the quantisation /
 // variation / pair paths are compiled out and the kernel's register budget is
 // that of the Philox + stuck-value path alone (higher occupancy).
+// map_dev (nullable): the map id read from device memory (a replayed hipGraph
+// advances it on the device, rram_mc_accumulate_dev), else map_arg
 template <bool FAST>
 __global__ void __launch_bounds__(256)
-    k_inject_batched(InjectSegs segs, uint64_t seed, uint32_t map_id, unsigned long long* counters) {
+    k_inject_batched(InjectSegs segs, uint64_t seed, uint32_t map_arg, const uint32_t* __restrict__ map_dev,
+                     unsigned long long* counters) {
+  const uint32_t map_id = map_dev != nullptr ? *map_dev : map_arg;
   // each block owns a contiguous run of chunks, so it crosses at most a few
   // segment boundaries and flushes its broken-cell count (one atomic per
   // segment visited) about once: ~grid + nsegs atomics per launch
@@ -402,6 +406,25 @@ __global__ void k_mc_accumulate(rram_mc_outputs o, float* __restrict__ sums, flo
     const float v = o.p[k][0];
     sums[k] += v;
     if (per_map) per_map[k] = v;
+  }
+}
+// The same with the per-map row from device memory: row = *row_dev; the row
+// is written when row < max_rows; advance != 0: then row_dev += 1 and
+// map_dev (nullable) += 1, so a replayed graph of one map walks the maps.
+__global__ void k_mc_accumulate_dev(rram_mc_outputs o, float* __restrict__ sums, float* __restrict__ per_map,
+                                    int64_t row_stride, int max_rows, int* __restrict__ row_dev,
+                                    uint32_t* __restrict__ map_dev, int advance) {
+  const int k = threadIdx.x;
+  const int row = *row_dev;
+  if (k < o.n) {
+    const float v = o.p[k][0];
+    sums[k] += v;
+    if (per_map != nullptr && row < max_rows) per_map[(int64_t)row * row_stride + k] = v;
+  }
+  __syncthreads();  // every lane has read row before it moves
+  if (advance && k == 0) {
+    *row_dev = row + 1;
+    if (map_dev != nullptr) *map_dev = *map_dev + 1u;
   }
 }
 
@@ -730,8 +753,29 @@ int rram_set_inject_grid(int blocks) {
   return rram::inject_grid().exchange(blocks);
 }
 
+namespace rram {
+namespace {
+int inject_batched_core(const rram_inject_seg* segs, int nsegs, uint64_t seed, uint32_t map_id,
+                        const uint32_t* map_dev, unsigned long long* counters, rram_stream_t s);
+}
+}  // namespace rram
+
 int rram_inject_rng_batched(const rram_inject_seg* segs, int nsegs, uint64_t seed,
                             uint32_t map_id, unsigned long long* counters, rram_stream_t s) {
+  return rram::inject_batched_core(segs, nsegs, seed, map_id, nullptr, counters, s);
+}
+
+int rram_inject_rng_batched_dev(const rram_inject_seg* segs, int nsegs, uint64_t seed, const uint32_t* map_id_dev,
+                                unsigned long long* counters, rram_stream_t s) {
+  RRAM_REQUIRE(map_id_dev != nullptr, "inject_dev: map_id_dev is NULL");
+  return rram::inject_batched_core(segs, nsegs, seed, 0, map_id_dev, counters, s);
+}
+}  // extern "C"
+
+namespace rram {
+namespace {
+int inject_batched_core(const rram_inject_seg* segs, int nsegs, uint64_t seed, uint32_t map_id,
+                        const uint32_t* map_dev, unsigned long long* counters, rram_stream_t s) {
   RRAM_REQUIRE(nsegs >= 0 && nsegs <= RRAM_MAX_SEGS, "inject: nsegs out of range");
   if (nsegs == 0) return RRAM_OK;
   RRAM_REQUIRE(segs, "inject: segs is NULL");
@@ -761,12 +805,16 @@ int rram_inject_rng_batched(const rram_inject_seg* segs, int nsegs, uint64_t see
   for (int i = 0; i < nsegs; ++i) fast = fast && is.s[i].mode == 0;
   if (fast)
     hipLaunchKernelGGL(k_inject_batched<true>, dim3(grid), dim3(kThreads), 0, as_stream(s), is, seed,
-                       map_id, counters);
+                       map_id, map_dev, counters);
   else
     hipLaunchKernelGGL(k_inject_batched<false>, dim3(grid), dim3(kThreads), 0, as_stream(s), is, seed,
-                       map_id, counters);
+                       map_id, map_dev, counters);
   return launch_status("inject_rng");
 }
+}  // namespace
+}  // namespace rram
+
+extern "C" {
 
 int rram_inject_rng(const float* w_clean, float* w_out, int64_t n, const rram_inject_cfg* cfg,
                     uint64_t seed, uint32_t map_id, uint32_t layer_id,
@@ -786,6 +834,16 @@ int rram_mc_accumulate(const rram_mc_outputs* outs, float* sums, float* per_map_
   if (outs->n == 0) return RRAM_OK;
   hipLaunchKernelGGL(k_mc_accumulate, dim3(1), dim3(64), 0, as_stream(s), *outs, sums, per_map_row);
   return launch_status("mc_accumulate");
+}
+
+int rram_mc_accumulate_dev(const rram_mc_outputs* outs, float* sums, float* per_map, int64_t row_stride,
+                           int max_rows, int* row_dev, uint32_t* map_id_dev, int advance, rram_stream_t s) {
+  RRAM_REQUIRE(outs && sums && row_dev && outs->n >= 0 && outs->n <= RRAM_MC_MAX_OUTPUTS && max_rows >= 0 &&
+                   row_stride >= outs->n,
+               "mc_accumulate_dev: bad arguments");
+  hipLaunchKernelGGL(k_mc_accumulate_dev, dim3(1), dim3(64), 0, as_stream(s), *outs, sums, per_map, row_stride,
+                     max_rows, row_dev, map_id_dev, advance);
+  return launch_status("mc_accumulate_dev");
 }
 
 int rram_threshold_strategy(float* dw, int64_t n, float thr, unsigned long long* cleared,

@@ -715,6 +715,19 @@ int rram_mc_set_reuse_prefix(rram_mc_t m, int enable) {
     m->mc->set_reuse_prefix(enable != 0);
   });
 }
+int rram_mc_set_graph(rram_mc_t m, int enable) {
+  return guarded([&] {
+    NEED(m);
+    m->mc->set_graph(enable != 0);
+  });
+}
+int rram_mc_graph_active(rram_mc_t m, int* active) {
+  return guarded([&] {
+    NEED(m);
+    NEED(active);
+    *active = m->mc->graph_active() ? 1 : 0;
+  });
+}
 int rram_mc_set_timing(rram_mc_t m, int enable) {
   return guarded([&] {
     NEED(m);

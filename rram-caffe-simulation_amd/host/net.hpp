@@ -89,6 +89,7 @@ class Net {
   // per-layer forward timing with hipEvents (`caffe time`, tools/caffe.cpp:334-421):
   // 0 off, 1 every layer, 2 only layers that own parameters (conv / IP)
   void set_timing(int mode) { timing_ = mode; }
+  bool timing_on() const { return timing_ != 0; }
   // events around layer i only (mode 3): one kernel's live timing at the
   // least event overhead
   void set_timing_layer(int i) {

@@ -633,6 +633,8 @@ MonteCarlo<Dtype>::~MonteCarlo() {
     Caffe::synchronize();
   } catch (...) {
   }
+  drop_graph();
+  if (d_state_) (void)hipFree(d_state_);
   for (auto* c : clean_) (void)hipFree(c);
   if (side_) {
     (void)hipStreamSynchronize(side_);
@@ -648,6 +650,7 @@ MonteCarlo<Dtype>::~MonteCarlo() {
 template <typename Dtype>
 void MonteCarlo<Dtype>::Reset() {
   maps_run_ = 0;
+  if (d_state_) HIP_CALL(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_state_ + 1), 0, 1, Caffe::hip_stream()));
   HIP_CALL(hipMemsetAsync(d_sums_, 0, std::max<size_t>(outs_.size(), 1) * sizeof(Dtype), Caffe::hip_stream()));
   HIP_CALL(hipMemsetAsync(d_broken_, 0, params_.size() * sizeof(unsigned long long), Caffe::hip_stream()));
 }
@@ -687,7 +690,130 @@ void MonteCarlo<Dtype>::set_reuse_prefix(bool on) {
 }
 
 template <typename Dtype>
+void MonteCarlo<Dtype>::drop_graph() {
+  if (gexec_) (void)hipGraphExecDestroy(gexec_);
+  if (graph_g_) (void)hipGraphDestroy(graph_g_);
+  gexec_ = nullptr;
+  graph_g_ = nullptr;
+  graph_warm_ = false;
+  graph_ptrs_.clear();
+}
+
+template <typename Dtype>
+void MonteCarlo<Dtype>::set_graph(bool on) {
+  if (on) {
+    for (const auto& l : net_->layers())
+      CAFFE_CHECK(std::string(l->type()) != "HDF5Data",
+                  "MonteCarlo graph replay: " << l->name() << " (HDF5Data) advances between forwards");
+    if (!d_state_) {
+      HIP_CALL(hipMalloc(reinterpret_cast<void**>(&d_state_), 2 * sizeof(uint32_t)));
+      HIP_CALL(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_state_), 0, 1, Caffe::hip_stream()));
+      HIP_CALL(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_state_ + 1), maps_run_, 1, Caffe::hip_stream()));
+    }
+  } else {
+    drop_graph();
+  }
+  graph_ = on;
+}
+
+// the device pointers a captured map depends on: every blob's and
+// parameter's data and diff (a reshape or a set_gpu_data moves them), the
+// clean copies and the statistics buffers
+template <typename Dtype>
+std::vector<const void*> MonteCarlo<Dtype>::graph_key() const {
+  std::vector<const void*> k;
+  for (const auto& b : net_->blobs()) k.push_back(b->data()->gpu_data());
+  for (auto* p : net_->learnable_params()) {
+    k.push_back(p->data()->gpu_data());
+    k.push_back(static_cast<const void*>(p));
+  }
+  for (auto* c : clean_) k.push_back(c);
+  k.push_back(d_sums_);
+  k.push_back(d_per_map_);
+  k.push_back(d_broken_);
+  k.push_back(Caffe::hip_stream());
+  return k;
+}
+
+// One map on the working stream: injection (map id m, or from d_state_[0]),
+// the whole forward, the statistics (row maps_run_, or d_state_[1], which
+// then advances together with the map id).
+template <typename Dtype>
+void MonteCarlo<Dtype>::map_body(bool dev_state, uint32_t m) {
+  std::vector<rram_inject_seg> segs(params_.size());
+  for (size_t i = 0; i < params_.size(); ++i)
+    segs[i] = rram_inject_seg{clean_[i], params_[i]->mutable_gpu_data(), params_[i]->count(), (uint32_t)i, 0, cfgs_[i]};
+  for (size_t s = 0; s < segs.size(); s += RRAM_MAX_SEGS) {
+    const int k = static_cast<int>(std::min<size_t>(RRAM_MAX_SEGS, segs.size() - s));
+    if (dev_state)
+      RRAM_CALL(rram_inject_rng_batched_dev(segs.data() + s, k, seed_, d_state_, d_broken_ + s, Caffe::stream()));
+    else
+      RRAM_CALL(rram_inject_rng_batched(segs.data() + s, k, seed_, m, d_broken_ + s, Caffe::stream()));
+  }
+  net_->Forward(false);
+  const size_t no = outs_.size();
+  if (no == 0 && dev_state) {  // still advance the map id and the row
+    rram_mc_outputs mo{};
+    RRAM_CALL(rram_mc_accumulate_dev(&mo, d_sums_, nullptr, 1, 0, reinterpret_cast<int*>(d_state_ + 1), d_state_, 1,
+                                     Caffe::stream()));
+  }
+  for (size_t k0 = 0; k0 < no; k0 += RRAM_MC_MAX_OUTPUTS) {
+    rram_mc_outputs mo{};
+    mo.n = static_cast<int>(std::min<size_t>(RRAM_MC_MAX_OUTPUTS, no - k0));
+    for (int k = 0; k < mo.n; ++k) mo.p[k] = outs_[k0 + k]->gpu_data();
+    if (dev_state)
+      RRAM_CALL(rram_mc_accumulate_dev(&mo, d_sums_ + k0, d_per_map_ + k0, static_cast<int64_t>(no), max_maps_,
+                                       reinterpret_cast<int*>(d_state_ + 1), d_state_,
+                                       k0 + RRAM_MC_MAX_OUTPUTS >= no ? 1 : 0, Caffe::stream()));
+    else
+      RRAM_CALL(rram_mc_accumulate(&mo, d_sums_ + k0,
+                                   maps_run_ < max_maps_ ? d_per_map_ + (size_t)maps_run_ * no + k0 : nullptr,
+                                   Caffe::stream()));
+  }
+}
+
+template <typename Dtype>
 void MonteCarlo<Dtype>::Run(uint32_t map_begin, uint32_t map_count) {
+  if (graph_ && !overlap_ && !reuse_prefix_ && !timing_ && !net_->timing_on() && map_count > 0) {
+    hipStream_t st = Caffe::hip_stream();
+    HIP_CALL(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_state_), static_cast<int>(map_begin), 1, st));
+    if (gexec_ && graph_key() != graph_ptrs_) drop_graph();
+    for (uint32_t m = map_begin; m < map_begin + map_count; ++m) {
+      if (!gexec_) {
+        if (!graph_warm_) {
+          // eager first (every workspace and pack buffer gets allocated), on
+          // the device-state path the graph will replay
+          map_body(true, m);
+          graph_warm_ = true;
+          ++maps_run_;
+          continue;
+        }
+        // every cache the forward keeps across calls (octet companions,
+        // packed weights) is dropped, so the captured map recomputes what it
+        // reads and stays exact whatever the host-side cache state is later
+        for (const auto& b : net_->blobs()) (void)b->mutable_gpu_data();
+        for (auto* p : net_->learnable_params()) (void)p->mutable_gpu_data();
+        HIP_CALL(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+        try {
+          map_body(true, m);
+        } catch (...) {
+          hipGraph_t g = nullptr;
+          (void)hipStreamEndCapture(st, &g);
+          if (g) (void)hipGraphDestroy(g);
+          throw;
+        }
+        HIP_CALL(hipStreamEndCapture(st, &graph_g_));
+        HIP_CALL(hipGraphInstantiate(&gexec_, graph_g_, nullptr, nullptr, 0));
+        graph_ptrs_ = graph_key();
+      }
+      HIP_CALL(hipGraphLaunch(gexec_, st));
+      ++maps_run_;
+    }
+    return;
+  }
+  if (d_state_)  // keep the device-side row in step with the eager maps
+    HIP_CALL(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_state_ + 1), maps_run_ + static_cast<int>(map_count),
+                               1, Caffe::hip_stream()));
   std::vector<rram_inject_seg> segs(params_.size());
   for (size_t i = 0; i < params_.size(); ++i)
     segs[i] = rram_inject_seg{clean_[i], params_[i]->mutable_gpu_data(), params_[i]->count(), (uint32_t)i, 0, cfgs_[i]};

@@ -266,6 +266,14 @@ class MonteCarlo {
   // (HDF5Data) or a later layer writes a prefix blob in place; the caller
   // re-enables it after changing the input batch or a prefix weight.
   void set_reuse_prefix(bool on);
+  // hipGraph replay (opt-in; for launch-bound small nets): one map (injection
+  // + forward + statistics) is captured once and replayed per map, the map
+  // id and the per-map row advancing in device memory (rram_inject_rng_batched_dev,
+  // rram_mc_accumulate_dev).  Bit-identical to the eager maps.  Falls back to
+  // the eager path while timing, injection overlap or prefix reuse is on, and
+  // refuses nets whose source layers advance between forwards (HDF5Data).
+  void set_graph(bool on);
+  bool graph_active() const { return gexec_ != nullptr; }
   EventTimer& timer() { return timer_; }
   int64_t fault_weights() const {
     int64_t n = 0;
@@ -296,6 +304,15 @@ class MonteCarlo {
   Dtype* d_sums_ = nullptr;       // [n_outputs]
   Dtype* d_per_map_ = nullptr;    // [max_maps][n_outputs]
   unsigned long long* d_broken_ = nullptr;
+  // graph replay: d_state_ = {map id, per-map row} on the device
+  bool graph_ = false, graph_warm_ = false;
+  uint32_t* d_state_ = nullptr;
+  hipGraph_t graph_g_ = nullptr;
+  hipGraphExec_t gexec_ = nullptr;
+  std::vector<const void*> graph_ptrs_;  // the device pointers the graph was captured with
+  void map_body(bool dev_state, uint32_t m);  // one map's launches on the working stream
+  std::vector<const void*> graph_key() const;
+  void drop_graph();
 };
 
 }  // namespace caffe

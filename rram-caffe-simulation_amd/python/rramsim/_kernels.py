@@ -104,6 +104,8 @@ SIGNATURES = {
     "rram_conv_weight_pack_bytes": (SZ, [P]),
     "rram_conv2d_fwd_cached": (I, [P, P, P, P, P, I, P, P, P, I, P]),
     "rram_conv2d_fwd_strided": (I, [P, P, P, P, P, I, P, P, C.c_int64, I, P]),
+    "rram_inject_rng_batched_dev": (I, [P, I, C.c_uint64, P, P, P]),
+    "rram_mc_accumulate_dev": (I, [P, P, P, C.c_int64, I, P, P, I, P]),
     "rram_pack_octets": (I, [P, P, I, I, I, I, P]),
     "rram_conv2d_bwd_workspace": (SZ, [P, I]),
     "rram_conv2d_bwd": (I, [P, P, P, P, P, P, P, P, SZ, P]),

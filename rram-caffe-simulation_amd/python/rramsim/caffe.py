@@ -51,6 +51,8 @@ SIGNATURES = {
     "rram_net_describe": (I, [C.c_char_p, I, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "rram_mc_set_timing": (I, [P, I]),
     "rram_mc_set_reuse_prefix": (I, [P, I]),
+    "rram_mc_set_graph": (I, [P, I]),
+    "rram_mc_graph_active": (I, [P, PI]),
     "rram_mc_inject_times": (I, [P, C.POINTER(C.c_double), C.POINTER(C.c_long), PI64, I]),
     "rram_solver_create": (I, [C.c_char_p, C.c_char_p, C.c_char_p, PP]),
     "rram_solver_destroy": (I, [P]),
@@ -597,6 +599,15 @@ class MonteCarlo:
         """Opt-in: run the layers before the first faultable one once for a
         fixed input batch (include/rram_caffe.h rram_mc_set_reuse_prefix)."""
         check(self._lib.rram_mc_set_reuse_prefix(self.h, int(on)), "mc_set_reuse_prefix")
+
+    def set_graph(self, on: bool):
+        """Opt-in hipGraph replay of the maps (include/rram_caffe.h rram_mc_set_graph)."""
+        check(self._lib.rram_mc_set_graph(self.h, int(on)), "mc_set_graph")
+
+    def graph_active(self) -> bool:
+        a = C.c_int()
+        check(self._lib.rram_mc_graph_active(self.h, C.byref(a)), "mc_graph_active")
+        return bool(a.value)
 
     def inject_times(self, reset=False):
         """(total ms, launches, faultable weights) of the injection launches."""

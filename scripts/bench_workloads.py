@@ -177,6 +177,11 @@ def lenet_cpu_baseline(batch, p_fault, seed, budget_s=10.0):
                       f"extrapolated to one {batch}-image map"}
 
 
+def _graph_on():
+    """MonteCarlo hipGraph replay for the launch-bound MC workloads (RRAM_MC_GRAPH=0: eager, for A/Bs)."""
+    return os.environ.get("RRAM_MC_GRAPH", "1") != "0"
+
+
 def run_workload(args, world, rank, dev):
     import torch
     import torch.distributed as dist
@@ -194,16 +199,27 @@ def run_workload(args, world, rank, dev):
             cfgs.append(make_inject_cfg(0.01, 10, 20, 10, quant_levels=16, g_max=gmax, var_sigma=0.1,
                                         stuck_scale=gmax))
         mc = caffe.MonteCarlo(net, cfgs, seed=args.seed, max_maps=(args.steps + args.warmup) * 10 + 8)
+        mc.set_graph(_graph_on())         # launch-bound: replay each map as one hipGraph
         maps_per_step = 10
         el = _timed(world, dev, lambda i: mc.run((rank + world * i) * maps_per_step, maps_per_step),
-                    args.steps, args.warmup, net)
+                    args.steps, args.warmup)
         st = mc.stats()
+        graph = mc.graph_active()
+        # the contraction table: events around every conv / IP layer over K
+        # further maps after the timed region (the maps run eager while timed)
+        net.layer_times(reset=True)
+        net.set_timing(2)
+        for i in range(args.steps):
+            mc.run((rank + world * (args.warmup + args.steps + i)) * maps_per_step, maps_per_step)
+        torch.cuda.synchronize()
+        net.set_timing(0)
         tot = allreduce_stats(st["sums"] + [st["maps"]], dev)
         n_maps = world * args.steps * maps_per_step
         res = _base("Monte Carlo fault maps/sec, CIFAR-10 quick (quantised + lognormal)", "maps/s", n_maps / el,
                     world, args, el, workload="cifar10_quick_mc_quant16_lognormal0.1", model="CIFAR10_quick",
                     global_batch=batch * world, maps_per_step=maps_per_step * world, p_fault=0.01)
         res["images_per_s"] = round(n_maps * batch / el, 1)
+        res["hipgraph"] = graph
         res["mc_mean_outputs"] = [x / max(tot[-1], 1) for x in tot[:-1]]
         res["roofline"] = contraction_roofline(net, args.steps * maps_per_step, net.layer_times())
         mc.close()
@@ -220,6 +236,7 @@ def run_workload(args, world, rank, dev):
         net = caffe.Net(models.lenet(test_batch=batch), "test", models.net_options("lenet"))
         mc = caffe.MonteCarlo(net, make_inject_cfg(args.p_fault), seed=args.seed,
                               max_maps=(args.steps + args.warmup) * 10 + 8)
+        mc.set_graph(_graph_on())
         maps_per_step = 10
         el = _timed(world, dev, lambda i: mc.run((rank + world * i) * maps_per_step, maps_per_step),
                     args.steps, args.warmup)
@@ -230,6 +247,7 @@ def run_workload(args, world, rank, dev):
                     workload="lenet_mc_stuckat", model="LeNet (lenet_train_test TEST)", global_batch=batch * world,
                     maps_per_step=maps_per_step * world, p_fault=args.p_fault)
         res["mc_mean_outputs"] = [x / max(tot[-1], 1) for x in tot[:-1]]
+        res["hipgraph"] = mc.graph_active()
         mc.close()
         net.close()
         if rank == 0 and world == 1 and not args.no_cpu_baseline:

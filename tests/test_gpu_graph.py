@@ -1,0 +1,79 @@
+"""hipGraph replay of Monte-Carlo maps (include/rram_caffe.h rram_mc_set_graph;
+no reference counterpart: the reference runs one map per process,
+SURVEY.md §3.3).  One map (injection + forward + statistics) is captured
+after one eager map and replayed, the map id and the per-map row advancing
+in device memory.  Gate: bit-identity with the eager maps — per-map
+accuracy / loss, broken-cell counts, the last map's weights and logits —
+over consecutive and strided map ids (the bench's map m on rank m mod N),
+and with the conv-fault extension, whose injections rewrite the conv
+weights every map (the captured map repacks them)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def N(t):
+    import torch
+    torch.cuda.synchronize()
+    return t.detach().cpu().numpy().copy()
+
+
+def _run(model, graph, calls, opts_extra=None, cfg_kw=None):
+    from rramsim import caffe, make_inject_cfg, models
+    caffe.set_stream_from_torch()
+    caffe.set_random_seed(1701)
+    name = "cifar10_quick" if model == "cifar" else "lenet"
+    build = models.cifar10_quick if model == "cifar" else models.lenet
+    opts = models.net_options(name, **(opts_extra or {}))
+    net = caffe.Net(build(test_batch=50), "test", opts)
+    mc = caffe.MonteCarlo(net, make_inject_cfg(0.05, **(cfg_kw or {})), seed=77, max_maps=64)
+    mc.set_graph(graph)
+    for begin, count in calls:
+        mc.run(begin, count)
+    st = mc.stats()
+    fps = [N(f["data"]) for f in net.failure_params()]
+    outs = {k: N(v) for k, v in net.outputs().items()}
+    active = mc.graph_active()
+    mc.close()
+    net.close()
+    return st, fps, outs, active
+
+
+@pytest.mark.parametrize("model", ["lenet", "cifar"])
+@pytest.mark.parametrize("calls", [[(0, 6)], [(0, 1), (2, 1), (4, 1), (6, 1)], [(3, 2), (10, 3)]],
+                         ids=["consecutive", "strided", "two_runs"])
+def test_graph_maps_equal_eager(device, model, calls):
+    ref = _run(model, False, calls)
+    got = _run(model, True, calls)
+    assert got[3] and not ref[3]                      # the graph ran
+    assert got[0]["per_map"] == ref[0]["per_map"]
+    assert got[0]["broken"] == ref[0]["broken"] and got[0]["sums"] == ref[0]["sums"]
+    assert got[0]["maps"] == ref[0]["maps"]
+    for a, b in zip(got[1], ref[1]):
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    for k in ref[2]:
+        assert np.array_equal(got[2][k], ref[2][k]), k
+
+
+def test_graph_conv_fault_extension_equals_eager(device):
+    calls = [(0, 4)]
+    kw = dict(opts_extra=dict(fault_layers="InnerProduct,Convolution"))
+    ref = _run("cifar", False, calls, **kw)
+    got = _run("cifar", True, calls, **kw)
+    assert got[3]
+    assert got[0]["per_map"] == ref[0]["per_map"] and got[0]["broken"] == ref[0]["broken"]
+    for k in ref[2]:
+        assert np.array_equal(got[2][k], ref[2][k]), k
+
+
+def test_graph_quantised_lognormal_equals_eager(device):
+    """C2's injection modes (quantisation + lognormal variation)."""
+    calls = [(0, 5)]
+    kw = dict(cfg_kw=dict(quant_levels=16, g_max=0.5, var_sigma=0.1))
+    ref = _run("cifar", False, calls, **kw)
+    got = _run("cifar", True, calls, **kw)
+    assert got[3]
+    assert got[0]["per_map"] == ref[0]["per_map"] and got[0]["broken"] == ref[0]["broken"]
+    for a, b in zip(got[1], ref[1]):
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
