@@ -123,6 +123,15 @@ int rram_solver_create(const char* solver_prototxt, const char* net_prototxt, co
                        rram_solver_t* out);
 int rram_solver_destroy(rram_solver_t s);
 int rram_solver_step(rram_solver_t s, int iters);
+/* hipGraph replay of the training iteration (opt-in, for launch-bound small
+ * nets; no reference counterpart): clear + forward + backward and the fused
+ * update / threshold / Fail tail are each captured once and replayed, the
+ * on_gradients_ready hook (data-parallel all-reduce) running between them.
+ * Iterations that display, test, snapshot or average the loss run eager;
+ * a moving learning rate keeps the eager path.  RRAM_EINVAL for nets with
+ * per-iteration host state (Dropout, HDF5Data).  Bit-identical to eager. */
+int rram_solver_set_graph(rram_solver_t s, int enable);
+int rram_solver_graph_active(rram_solver_t s, int* active);
 int rram_solver_solve(rram_solver_t s);
 int rram_solver_iter(rram_solver_t s, int* iter);
 int rram_solver_smoothed_loss(rram_solver_t s, float* loss);

@@ -408,6 +408,19 @@ int rram_solver_create(const char* sp, const char* np, const char* options, rram
 int rram_solver_destroy(rram_solver_t s) {
   return guarded([&] { delete s; });
 }
+int rram_solver_set_graph(rram_solver_t s, int enable) {
+  return guarded([&] {
+    NEED(s);
+    s->solver->set_graph(enable != 0);
+  });
+}
+int rram_solver_graph_active(rram_solver_t s, int* active) {
+  return guarded([&] {
+    NEED(s);
+    NEED(active);
+    *active = s->solver->graph_active() ? 1 : 0;
+  });
+}
 int rram_solver_step(rram_solver_t s, int iters) {
   return guarded([&] {
     NEED(s);

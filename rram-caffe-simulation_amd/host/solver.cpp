@@ -190,6 +190,7 @@ Solver<Dtype>::Solver(const Msg& sp, const Msg* net_param, const Msg& options) :
 
 template <typename Dtype>
 Solver<Dtype>::~Solver() {
+  drop_graphs();
   if (flat_) {
     (void)hipStreamSynchronize(Caffe::hip_stream());
     (void)hipFree(flat_);
@@ -347,6 +348,77 @@ void Solver<Dtype>::FusedTail() {
   }
 }
 
+template <typename Dtype>
+void Solver<Dtype>::drop_graphs() {
+  for (int k = 0; k < 2; ++k) {
+    if (gx_[k]) (void)hipGraphExecDestroy(gx_[k]);
+    if (gg_[k]) (void)hipGraphDestroy(gg_[k]);
+    gx_[k] = nullptr;
+    gg_[k] = nullptr;
+  }
+  graph_warm_ = false;
+  graph_ptrs_.clear();
+}
+
+template <typename Dtype>
+void Solver<Dtype>::set_graph(bool on) {
+  if (on)
+    for (const auto& l : net_->layers()) {
+      const std::string t = l->type();
+      CAFFE_CHECK(t != "Dropout" && t != "HDF5Data",
+                  "Solver graph replay: " << l->name() << " (" << t << ") changes per iteration on the host");
+    }
+  else
+    drop_graphs();
+  graph_ = on;
+}
+
+// the device pointers a captured iteration depends on
+template <typename Dtype>
+std::vector<const void*> Solver<Dtype>::graph_key() const {
+  std::vector<const void*> k;
+  for (const auto& b : net_->blobs()) {
+    k.push_back(b->data()->gpu_data());
+    k.push_back(b->diff()->gpu_data());
+  }
+  for (auto* p : net_->learnable_params()) {
+    k.push_back(p->data()->gpu_data());
+    k.push_back(p->diff()->gpu_data());
+  }
+  for (const auto& h : history_) k.push_back(h->data()->gpu_data());
+  if (fmaker_) {
+    for (auto* b : fmaker_->fail_iterations()) {
+      k.push_back(b->data()->gpu_data());
+      k.push_back(b->diff()->gpu_data());
+    }
+    k.push_back(fmaker_->device_counts());
+  }
+  k.push_back(Caffe::hip_stream());
+  return k;
+}
+
+// graph k (0: clear + forward + backward, 1: the fused tail): captured from
+// body() on first use, then launched
+template <typename Dtype>
+template <typename F>
+void Solver<Dtype>::capture_launch(int k, F&& body) {
+  hipStream_t st = Caffe::hip_stream();
+  if (!gx_[k]) {
+    HIP_CALL(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+    try {
+      body();
+    } catch (...) {
+      hipGraph_t g = nullptr;
+      (void)hipStreamEndCapture(st, &g);
+      if (g) (void)hipGraphDestroy(g);
+      throw;
+    }
+    HIP_CALL(hipStreamEndCapture(st, &gg_[k]));
+    HIP_CALL(hipGraphInstantiate(&gx_[k], gg_[k], nullptr, nullptr, 0));
+  }
+  HIP_CALL(hipGraphLaunch(gx_[k], st));
+}
+
 // solver.cpp:237-325 (fork order: ComputeUpdate -> ApplyStrategy -> ApplyUpdate -> Fail)
 template <typename Dtype>
 void Solver<Dtype>::Step(int iters) {
@@ -365,10 +437,37 @@ void Solver<Dtype>::Step(int iters) {
   const bool can_fuse = fused_update_ && fusable_strategies && param_.num("clip_gradients", -1.0) < 0 &&
                         iter_size == 1 && param_.str("regularization_type", "L2") == "L2";
   while (iter_ < stop) {
-    net_->ClearParamDiffs();
-    if (test_interval && iter_ % test_interval == 0 && (iter_ > 0 || param_.boolean("test_initialization", true)))
-      TestAll();
+    const bool test_now =
+        test_interval && iter_ % test_interval == 0 && (iter_ > 0 || param_.boolean("test_initialization", true));
     const bool disp = display && iter_ % display == 0;
+    // (a learning rate that moves every iteration, e.g. lr_policy "inv",
+    // keeps the eager path: a graph is only worth its capture when replayed)
+    const Dtype rate_now = graph_ ? GetLearningRate() : Dtype(0);
+    const bool rate_stable = rate_now == graph_prev_rate_;
+    graph_prev_rate_ = rate_now;
+    if (graph_ && rate_stable && can_fuse && !test_now && !disp && average_loss <= 1 && !net_->on_backward_layer) {
+      const Dtype rate = rate_now;
+      if (gx_[0] && (rate != graph_rate_ || graph_key() != graph_ptrs_)) drop_graphs();
+      if (graph_warm_) {
+        net_->set_iter((uint64_t)iter_);
+        capture_launch(0, [&] {
+          net_->ClearParamDiffs();
+          net_->Forward(false);
+          net_->Backward();
+        });
+        if (on_gradients_ready) on_gradients_ready();
+        capture_launch(1, [&] { FusedTail(); });
+        graph_rate_ = rate;
+        graph_ptrs_ = graph_key();
+        ++iter_;
+        const long long snap = param_.integer("snapshot", 0);
+        if (snap && iter_ % snap == 0) Snapshot();
+        continue;
+      }
+      graph_warm_ = true;  // this iteration runs eager (workspaces allocated), the next one captures
+    }
+    net_->ClearParamDiffs();
+    if (test_now) TestAll();
     net_->set_iter((uint64_t)iter_);
     Dtype loss = 0;
     for (int i = 0; i < iter_size; ++i) {

@@ -199,8 +199,29 @@ class Solver {
   // hook (RCCL all-reduce of the flat gradient buffer).
   std::function<void()> on_gradients_ready;
   std::function<void(const std::string&)> log;
+  // hipGraph replay of the training iteration (opt-in; launch-bound small
+  // nets, no reference counterpart): [ClearParamDiffs + Forward + Backward]
+  // and the fused update tail are each captured once, after one eager
+  // iteration, and replayed; on_gradients_ready (the data-parallel RCCL
+  // all-reduce) runs between the two launches, outside any graph.
+  // Iterations that display, test, snapshot or average the loss run eager,
+  // as does everything when the fused tail is off or a per-layer backward
+  // hook is set; a changed learning rate or moved buffers recapture.  Nets
+  // with per-iteration host state (Dropout, HDF5Data) are refused.
+  // Bit-identical to the eager iterations.
+  void set_graph(bool on);
+  bool graph_active() const { return gx_[0] != nullptr; }
 
  protected:
+  bool graph_ = false, graph_warm_ = false;
+  hipGraph_t gg_[2] = {nullptr, nullptr};
+  hipGraphExec_t gx_[2] = {nullptr, nullptr};
+  Dtype graph_rate_ = 0, graph_prev_rate_ = -1;
+  std::vector<const void*> graph_ptrs_;
+  std::vector<const void*> graph_key() const;
+  void drop_graphs();
+  template <typename F>
+  void capture_launch(int k, F&& body);
   void InitFailurePattern(const Msg& failure_param);
   void ComputeUpdate();
   void ApplyStrategy();

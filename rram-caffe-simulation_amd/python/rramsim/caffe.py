@@ -57,6 +57,8 @@ SIGNATURES = {
     "rram_solver_create": (I, [C.c_char_p, C.c_char_p, C.c_char_p, PP]),
     "rram_solver_destroy": (I, [P]),
     "rram_solver_step": (I, [P, I]),
+    "rram_solver_set_graph": (I, [P, I]),
+    "rram_solver_graph_active": (I, [P, PI]),
     "rram_solver_solve": (I, [P]),
     "rram_solver_iter": (I, [P, PI]),
     "rram_solver_smoothed_loss": (I, [P, PF]),
@@ -495,6 +497,15 @@ class Solver:
         v = C.c_float()
         check(self._lib.rram_solver_smoothed_loss(self.h, C.byref(v)), "smoothed_loss")
         return v.value
+
+    def set_graph(self, on: bool):
+        """Opt-in hipGraph replay of the training iteration (include/rram_caffe.h rram_solver_set_graph)."""
+        check(self._lib.rram_solver_set_graph(self.h, int(on)), "solver_set_graph")
+
+    def graph_active(self) -> bool:
+        a = C.c_int()
+        check(self._lib.rram_solver_graph_active(self.h, C.byref(a)), "solver_graph_active")
+        return bool(a.value)
 
     def step(self, iters: int):
         check(self._lib.rram_solver_step(self.h, iters), "step")

@@ -268,6 +268,7 @@ def run_workload(args, world, rank, dev):
         opts = dict(opts, fused_update=True)
         # bucketed gradient all-reduce overlapped with backward (world > 1 only)
         dp = DataParallelSolver(sp, net_txt, opts, seed=args.seed, overlap=True)
+        dp.solver.set_graph(_graph_on())  # launch-bound: iteration replayed as two hipGraphs around the all-reduce
         el = _timed(world, dev, lambda i: dp.step(1), args.steps, args.warmup)
         res = _base(f"fault-aware training images/sec, {args.workload}", "images/s",
                     world * args.steps * batch / el, world, args, el, workload=args.workload,
@@ -275,6 +276,7 @@ def run_workload(args, world, rank, dev):
                     parallelism=f"dp{world} (RCCL all-reduce of {dp.num_params} fp32 grads"
                                 f"{', bucketed, overlapped with backward' if dp.overlap else ''})")
         res["broken_cells"] = sum(dp.solver.broken_counts())
+        res["hipgraph"] = dp.solver.graph_active()
         # training roofline over the whole iteration: forward + weight-gradient +
         # data-gradient contractions (the first layer computes no data gradient;
         # the backward GEMMs run on the fp32 MFMA engine), against the step time

@@ -77,3 +77,36 @@ def test_graph_quantised_lognormal_equals_eager(device):
     assert got[0]["per_map"] == ref[0]["per_map"] and got[0]["broken"] == ref[0]["broken"]
     for a, b in zip(got[1], ref[1]):
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def _train(graph, iters, lr_policy="fixed", **kw):
+    from rramsim import caffe, models
+    caffe.set_stream_from_torch()
+    caffe.set_random_seed(1701)
+    sp = models.solver(base_lr=0.001, momentum=0.9, weight_decay=0.004, lr_policy=lr_policy, max_iter=1000,
+                       failure_mean=5e4, failure_std=1.5e4, failure_prob=(5, 90, 5), threshold=0.001, **kw)
+    s = caffe.Solver(sp, models.cifar10_full(train_batch=20, test_batch=20),
+                     dict(models.net_options("cifar10_full"), fused_update=True))
+    s.set_graph(graph)
+    for n in iters:
+        s.step(n)
+    ps = [N(p["data"]) for p in s.net.params()]
+    hist = [N(h) for h in s.history()]
+    fs = s.fail_state()
+    st = (ps, hist, [N(e) for e, v in fs], s.broken_counts(), s.graph_active())
+    s.close()
+    return st
+
+
+@pytest.mark.parametrize("policy", [dict(), dict(lr_policy="step", gamma=0.5, stepsize=4)], ids=["fixed", "step"])
+def test_graph_training_equals_eager(device, policy):
+    """C4's fault-aware training (fused update + threshold + Fail): 10
+    iterations in three step() calls replayed as graphs equal the eager
+    iterations bit for bit — weights, momentum history, endurance, broken
+    counts; the step policy's rate change at iteration 4 / 8 recaptures."""
+    ref = _train(False, [3, 4, 3], **policy)
+    got = _train(True, [3, 4, 3], **policy)
+    assert got[4] and not ref[4]
+    for a, b in zip(got[0] + got[1] + got[2], ref[0] + ref[1] + ref[2]):
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert got[3] == ref[3]
