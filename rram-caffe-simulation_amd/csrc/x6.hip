@@ -965,6 +965,143 @@ __global__ void __launch_bounds__(256) k_pack_octets_x6(const float* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------
+// k_conv1x1_x6: the 1 x 1, stride-1, pad-free convolution (GoogLeNet's
+// inception 1x1 / 3x3_reduce / 5x5_reduce / pool_proj layers,
+// conv_layer.cu:9-30 with kernel 1) on the bf16x6 engine.  Per image
+// Y (Cout x HW) = W (Cout x C) . X (C x HW), X read straight from NCHW fp32:
+// no input pack pass and no octet companion, so the 4 bytes per input element
+// are the kernel's only HBM read of it (once per M-tile).
+//  - Weights: pre-split fragments (k_conv_cb_pack_x6 with T = 1, cached per
+//    fault map), straight from L2 into registers one K-tile ahead.
+//  - Activations: a K-tile is 16 channels x BNc positions; RING K-tiles are
+//    in flight in registers ahead of the one written to the 2-stage LDS tile
+//    [16 channels][BNc positions] fp32 (one barrier per K-tile).  A wave's B
+//    fragment (8 channels of one position) is 8 conflict-free ds_read_b32,
+//    split in registers once and shared by the wave's MI row blocks.
+// Tile 32 MI WR x 32 NB (4 / WR): wave (wr, wc) owns rows 32 MI wr .. + 32 MI - 1
+// and columns 32 NB wc .. + 32 NB - 1.  VEC = 4: 16-byte loads of 4
+// consecutive positions (HW % 4 == 0, 16-byte aligned input); VEC = 1:
+// 4-byte loads (any HW: the 7 x 7 layers).
+namespace c1x1 {
+constexpr int RING = 4;  // K-tiles loaded ahead (registers); a multiple of 2
+}  // namespace c1x1
+template <int MI, int NB, int WR, int VEC>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, MI * NB <= 4 ? 2 : 1)))
+k_conv1x1_x6(Params P, const x6::bf16x8* __restrict__ wpack, const float* __restrict__ x, uint32_t xrange) {
+  using namespace g2;
+  constexpr int WC = 4 / WR, BMc = 32 * MI * WR, BNc = 32 * NB * WC;
+  constexpr int STG = 16 * BNc;           // floats per LDS stage
+  constexpr int LPT = STG / VEC / 256;    // loads per thread per K-tile
+  constexpr int RING = c1x1::RING;
+  static_assert(LPT >= 1 && STG % (VEC * 256) == 0, "tile");
+  typedef int int4x __attribute__((ext_vector_type(4)));
+  using SV = typename std::conditional<VEC == 4, int4x, int>::type;
+  __shared__ __attribute__((aligned(16))) float smem[2 * STG];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lr = lane & 31, lh = lane >> 5;
+  const int wr = wave % WR, wc = wave / WR;
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, loc = bid >> 3;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int tid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const int tm = __builtin_amdgcn_readfirstlane(tid % P.tiles_m);
+  const int tn = __builtin_amdgcn_readfirstlane(tid / P.tiles_m);
+  const int m0 = tm * BMc, n0 = tn * BNc;
+  const int HW = static_cast<int>(P.cv.howo.d), C = P.cv.C, KT = C >> 4;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), 0, static_cast<int>(xrange),
+                                                                      0x00020000);
+  // byte offset of load i at K-tile 0 (past the range: zeros)
+  uint32_t loff[LPT];
+#pragma unroll
+  for (int i = 0; i < LPT; ++i) {
+    const int e = i * 256 + static_cast<int>(threadIdx.x);
+    const int c = e / (BNc / VEC), n = n0 + (e - c * (BNc / VEC)) * VEC;
+    uint32_t off = 0x80000000u;
+    if (n < P.N) {
+      const uint32_t img = fdiv(static_cast<uint32_t>(n), P.cv.howo);
+      const uint32_t sp = static_cast<uint32_t>(n) - img * static_cast<uint32_t>(HW);
+      off = ((img * static_cast<uint32_t>(C) + static_cast<uint32_t>(c)) * static_cast<uint32_t>(HW) + sp) * 4u;
+    }
+    loff[i] = off;
+  }
+  const uint32_t kstep = static_cast<uint32_t>(HW) * 64u;  // bytes per K-tile (16 channel planes)
+  SV stg[RING][LPT];
+  auto load_b = [&](SV (&r)[LPT], int kt) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int o = static_cast<int>(loff[i] + static_cast<uint32_t>(kt) * kstep);
+      if constexpr (VEC == 4)
+        r[i] = __builtin_bit_cast(int4x, __builtin_amdgcn_raw_buffer_load_b128(xr, o, 0, 0));
+      else
+        r[i] = __builtin_bit_cast(int, __builtin_amdgcn_raw_buffer_load_b32(xr, o, 0, 0));
+    }
+  };
+  auto store_b = [&](const SV (&r)[LPT], int stage) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i)
+      *reinterpret_cast<SV*>(smem + stage * STG + (i * 256 + static_cast<int>(threadIdx.x)) * VEC) = r[i];
+  };
+  // weight fragments of row block rb = tm (BMc / 32) + MI wr + i, K-tile kt
+  const x6::bf16x8* ap = wpack + (int64_t)(tm * (BMc / 32) + MI * wr) * KT * cbx6::FRAG + lane;
+  x6::Parts fa[2][MI];
+  auto load_a = [&](x6::Parts (&f)[MI], int kt) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const x6::bf16x8* q = ap + ((int64_t)i * KT + kt) * cbx6::FRAG;
+      f[i].h = q[0];
+      f[i].m = q[64];
+      f[i].l = q[128];
+    }
+  };
+  floatx16 acc[MI][NB];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+  // prologue: K-tiles 0 .. RING - 1 in flight, K-tile 0 in LDS stage 0
+#pragma unroll
+  for (int q = 0; q < RING; ++q)
+    if (q < KT) load_b(stg[q], q);
+  load_a(fa[0], 0);
+  store_b(stg[0], 0);
+  __syncthreads();
+
+  const int colw = 32 * NB * wc + lr;
+  // K-tile kt (kt % RING == PH): its B from LDS stage PH & 1
+  auto step = [&](int kt, auto ph_c) {
+    constexpr int PH = decltype(ph_c)::value;
+    if (kt + RING < KT) load_b(stg[PH], kt + RING);
+    if (kt + 1 < KT) load_a(fa[(PH + 1) & 1], kt + 1);
+    const float* bs = smem + (PH & 1) * STG + 8 * lh * BNc + colw;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = bs[e * BNc + 32 * j];
+      x6::Parts bp;
+      x6::split8_safe(v, bp);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) acc[i][j] = x6::mfma6(fa[PH & 1][i], bp, acc[i][j]);
+    }
+    if (kt + 1 < KT) store_b(stg[(PH + 1) % RING], (PH + 1) & 1);
+    __syncthreads();
+  };
+  for (int kt = 0; kt < KT; kt += RING) {
+    static_for<0, RING>([&](auto ph) {
+      if (kt + decltype(ph)::value < KT) step(kt + decltype(ph)::value, ph);
+    });
+  }
+  Epi ep = P.e;
+  conv_epilogue_nchw<MI, NB>(acc, P, ep, m0 + 32 * MI * wr, n0 + 32 * NB * wc, lr, lh);
+}
+
 // w [G*M][Cg][T] -> fragments [G][tiles_m][WR][Cg/16][T][term][64 lanes][8]:
 // lane (lr, h) of fragment (kt, s) holds row 32 (tm WR + wr) + lr, channels
 // 16 kt + 8 h .. + 7 at tap s.  One thread per (fragment, lane).
@@ -1006,24 +1143,27 @@ __global__ void __launch_bounds__(256) k_conv_cb_pack_x6(const float* __restrict
 // each element already split into its three bf16 terms, stored as plain rows
 // [term][row][ic] (ROWE elements per row, columns >= W zero).
 // K order ("quads"): a kernel row is padded to 12 columns = 3 quads of 4
-// consecutive columns; lane half h takes kernel rows 6h .. 6h + 5 (row 11 and
-// column 11 have zero weights), and quad qi = 2g + (j >> 2) of group g is
-// channel qi / 18, kernel row 6h + (qi / 3) % 6, columns 4 (qi % 3) .. + 3
-// (54 quads per half, 27 groups).  The im2col values of one quad at output
-// column ow are input columns 4 ow + 4 kq .. + 3 of one row: 4 consecutive
-// bf16 = one ds_read_b64 at a compile-time offset from a per-lane base, and
-// consecutive lanes (output columns) read consecutive 8-byte words, so a B
-// fragment term is two conflict-free ds_read_b64 with no VALU at all (the
-// per-element u16 gathers of the previous layout cost 1.3 ds_read + 0.7
-// v_perm per MFMA).  The padding costs 27 groups where 363 items need 23.
+// consecutive columns (column 11 has zero weights); the 99 quads (channel,
+// kernel row, quad) are taken four per MFMA group, lane half h reading quads
+// 4g + h and 4g + 2 + h of group g (25 groups; the 100th quad is padding).
+// The im2col values of one quad at output column ow are input columns
+// 4 ow + 4 kq .. + 3 of one row: 4 consecutive bf16 = one ds_read_b64 at a
+// compile-time offset from a per-lane base (half 1 adds its own compile-time
+// quad distance, one select per quad pair), and consecutive lanes (output
+// columns) read consecutive 8-byte words, so a B fragment term is two
+// ds_read_b64 with no gather VALU.  The padding costs 25 groups where 363
+// items need 23 (round 3 padded the kernel rows to 12 as well: 27 groups).
 // The slots are refilled for the next tile while this one computes: slot 0
-// once group 8 (the last reader of channel 0) is done, slot 1 after group 17,
-// slot 2 at the start of the tile it serves (read from group 18 on); three
+// once group 8 (the last reader of channel 0) is done, slot 1 after group 16,
+// slot 2 at the start of the tile it serves (read from group 16 on); three
 // barriers per tile.  The weight fragments come from L2 into registers two
 // groups ahead (fragment order, k_conv1_pack_x6).
 namespace c1x6 {
 constexpr int BM = 96, BN = 256;
-constexpr int HR = 6, KQ = 3, C = 3, QH = C * HR * KQ, G = QH / 2;  // 54 quads per half, 27 groups
+// K in quads: (channel, kernel row, quad of 4 kernel columns; column 11 is
+// the padding) = 3 x 11 x 3 = 99 quads, group g = quads 4g .. 4g + 3 (lane
+// half h takes 4g + h and 4g + 2 + h): 25 groups, the last with one padded quad
+constexpr int KR = 11, KQ = 3, C = 3, NQ = C * KR * KQ, G = (NQ + 3) / 4;
 constexpr int ROWS = 32;                 // slot rows
 // elements per slot row (>= 228: the last quad of output column 54 reads
 // input column 227, which is zero).  ROWE = 24 (mod 32) 8-byte words: a
@@ -1037,13 +1177,20 @@ constexpr int QP = ROWE / 8;             // 8-column chunks per row
 constexpr int CHUNKS = ROWS * QP;        // chunks per slot
 constexpr int CPT = (CHUNKS + 255) / 256;  // chunks per thread
 static_assert(3 * SLOTB + BM * 4 <= 160 * 1024, "LDS");
-// first / last group reading channel c
-constexpr int first_group(int c) { return c * (G / C); }
-constexpr int last_group(int c) { return (c + 1) * (G / C) - 1; }
-// LDS byte offset of quad qi (relative to the lane's base): channel, row, column
-constexpr int quad_off(int qi) {
-  return (qi / (HR * KQ)) * SLOTB + (((qi / KQ) % HR) * ROWE + 4 * (qi % KQ)) * 2;
+// first / last group reading channel c (quads 33 c .. 33 c + 32)
+constexpr int first_group(int c) { return (c * KR * KQ) / 4; }
+constexpr int last_group(int c) { return (c * KR * KQ + KR * KQ - 1) / 4; }
+// LDS byte offset of quad q (relative to the lane's base): channel, row, column
+constexpr int quad_off(int q) {
+  return (q / (KR * KQ)) * SLOTB + (((q / KQ) % KR) * ROWE + 4 * (q % KQ)) * 2;
 }
+// the lane half 1 reads quad q + 1 where half 0 reads quad q (q = 4g + 2e):
+// its extra byte offset (0 for the padded quad, which reads quad q again)
+constexpr int half_delta(int q) { return q + 1 < NQ ? quad_off(q + 1) - quad_off(q) : 0; }
+// mask of a quad's upper dword: column 11 (element 3 of a row's last quad)
+// is padding; the padded quad is zero altogether
+constexpr uint32_t hi_mask(int q) { return q >= NQ ? 0u : (q % KQ == KQ - 1 ? 0x0000FFFFu : 0xFFFFFFFFu); }
+constexpr uint32_t lo_mask(int q) { return q >= NQ ? 0u : 0xFFFFFFFFu; }
 }  // namespace c1x6
 
 template <int W>
@@ -1192,27 +1339,31 @@ k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img,
     for (int j = 0; j < 2; ++j) {
       const int sp = min(sp0 + wave * 64 + j * 32 + lr, HWo - 1);
       const int oh = sp / OW, ow = sp - oh * OW;
-      lb[j] = static_cast<uint32_t>(((4 * (oh - f) + HR * lh) * ROWE + 4 * ow) * 2);
+      lb[j] = static_cast<uint32_t>((4 * (oh - f) * ROWE + 4 * ow) * 2);
     }
     // B fragment term tt of column block j for group g: quads 2g, 2g + 1 =
     // two ds_read_b64 at compile-time offsets, issued one group ahead
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    // the padded K items (kernel column 11, and kernel row 11 in lane half 1)
-    // carry zero weights but read real input elements; their B values are
-    // zeroed too, so a non-finite input outside the 11 x 11 window never
-    // meets a zero weight (0 * Inf = NaN where fp32 has no such product)
-    const uint32_t row11_keep = lh ? 0u : 0xFFFFFFFFu;
-    auto mask_quad = [&](u32x2 v, int qi) __attribute__((always_inline)) {
-      if (qi % KQ == KQ - 1) v[1] &= 0x0000FFFFu;               // column 11: element 3 of the last quad
-      if ((qi / KQ) % HR == HR - 1) v = v & u32x2{row11_keep, row11_keep};  // row 11 (half 1)
+    // the padded K items (kernel column 11, the 100th quad) carry zero
+    // weights but read real input elements; their B values are zeroed too,
+    // so a non-finite input outside the 11 x 11 window never meets a zero
+    // weight (0 * Inf = NaN where fp32 has no such product).  Lane half h
+    // reads quads 4g + 2e + h: its offset and masks are the half's own
+    // compile-time constants, picked per lane once per quad pair.
+    auto pick = [&](uint32_t h0, uint32_t h1) __attribute__((always_inline)) { return lh ? h1 : h0; };
+    auto mask_q = [&](u32x2 v, int q0) __attribute__((always_inline)) {
+      if (lo_mask(q0) != 0xFFFFFFFFu || lo_mask(q0 + 1) != 0xFFFFFFFFu) v[0] &= pick(lo_mask(q0), lo_mask(q0 + 1));
+      if (hi_mask(q0) != 0xFFFFFFFFu || hi_mask(q0 + 1) != 0xFFFFFFFFu) v[1] &= pick(hi_mask(q0), hi_mask(q0 + 1));
       return v;
     };
     auto read_part = [&](x6::Parts (&F)[2], int g, int part) __attribute__((always_inline)) {
       const int j = part / 3, tt = part % 3;
-      const char* b = smem + lb[j] + tt * TERMB;
-      const u32x2 lo = mask_quad(*reinterpret_cast<const u32x2*>(b + quad_off(2 * g)), 2 * g);
-      const u32x2 hi = mask_quad(*reinterpret_cast<const u32x2*>(b + quad_off(2 * g + 1)), 2 * g + 1);
+      const int qa = 4 * g, qb = 4 * g + 2;
+      const char* ba = smem + lb[j] + (lh ? half_delta(qa) : 0) + tt * TERMB;
+      const char* bb = smem + lb[j] + (lh ? half_delta(qb) : 0) + tt * TERMB;
+      const u32x2 lo = mask_q(*reinterpret_cast<const u32x2*>(ba + quad_off(qa)), qa);
+      const u32x2 hi = mask_q(*reinterpret_cast<const u32x2*>(bb + quad_off(qb)), qb);
       const x6::bf16x8 v = __builtin_bit_cast(x6::bf16x8, u32x4{lo[0], lo[1], hi[0], hi[1]});
       if (tt == 0) F[j].h = v;
       else if (tt == 1) F[j].m = v;
@@ -1312,9 +1463,9 @@ __global__ void __launch_bounds__(256) k_conv1_pack_x6(const float* __restrict__
     float v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int qi = 2 * g + (j >> 2);
-      const int c = qi / (HR * KQ), kh = HR * h + (qi / KQ) % HR, kw = 4 * (qi % KQ) + (j & 3);
-      v[j] = (row < M && kh < 11 && kw < 11) ? w[((row * 3 + c) * 11 + kh) * 11 + kw] : 0.0f;
+      const int q = 4 * g + 2 * (j >> 2) + h;  // the quad lane half h reads for items j
+      const int c = q / (KR * KQ), kh = (q / KQ) % KR, kw = 4 * (q % KQ) + (j & 3);
+      v[j] = (row < M && q < NQ && kw < 11) ? w[((row * 3 + c) * 11 + kh) * 11 + kw] : 0.0f;
     }
     x6::Parts t;
     x6::split8_safe(v, t);
@@ -1953,6 +2104,98 @@ int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, c
   return rc ? rc : 1;
 }
 
+// ---- k_conv1x1_x6 plan ----
+struct C1Plan {
+  int MI, NB, WR, VEC, tiles_m, tiles_n;
+};
+// (MI, NB, WR) instantiated for VEC = 4 and VEC = 1
+#define RRAM_C1X1_LIST(X) X(1, 2, 1) X(2, 1, 1) X(2, 2, 1) X(2, 1, 2) X(4, 1, 1) X(4, 2, 1) X(4, 1, 2) X(4, 2, 2)
+bool conv_1x1_plan(const rram_conv_desc* d, const float* x, C1Plan& pl) {
+  static const int enabled = [] {
+    const char* e = getenv("RRAM_C1X1");  // 0: the fp32-MFMA table-gather GEMM instead (A/B runs)
+    return e ? atoi(e) : 1;
+  }();
+  if (!enabled) return false;
+  if (d->kernel_h != 1 || d->kernel_w != 1 || d->stride_h != 1 || d->stride_w != 1 || d->pad_h != 0 ||
+      d->pad_w != 0 || d->dilation_h != 1 || d->dilation_w != 1 || d->group != 1)
+    return false;
+  const int M = d->num_output, C = d->channels, HW = d->height * d->width;
+  if (C % 16 != 0 || M < 1 || d->num < 1) return false;
+  const int64_t N = (int64_t)d->num * HW;
+  if ((int64_t)d->num * C * HW * 4 >= (1ll << 31) || (int64_t)d->num * M * HW * 4 >= (1ll << 31)) return false;
+  if (x != nullptr && (reinterpret_cast<uintptr_t>(x) & 3u) != 0) return false;
+  const bool v4 = HW % 4 == 0 && (x == nullptr || (reinterpret_cast<uintptr_t>(x) & 15u) == 0);
+  // least estimated time: MFMA makespan (rounds of 256 workgroups x tile work
+  // at the bf16x6 rate of one CU) against the HBM stream (input once per M-tile)
+  static const int cfg[][3] = {{1, 2, 1}, {2, 1, 1}, {2, 2, 1}, {2, 1, 2}, {4, 1, 1}, {4, 2, 1}, {4, 1, 2}, {4, 2, 2}};
+  double best = -1.0;
+  for (const auto& c : cfg) {
+    const int MI = c[0], NB = c[1], WR = c[2];
+    const int BM = 32 * MI * WR, BN = 32 * NB * (4 / WR);
+    if (BM > 32 && (BM / 2) >= M) continue;                  // half the tile would pad
+    const int64_t tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+    if (tm * tn >= (1ll << 31)) continue;
+    const double t_mfma = (double)((tm * tn + 255) / 256) * BM * BN * C * 2.0 / (416.7e12 / 256);
+    const double t_mem = ((double)tm * N * C * 4 + (double)N * M * 4) / 5.0e12;
+    const double t = std::max(t_mfma, t_mem) * (1.0 + 0.02 * (MI * NB == 8 ? 0 : 1));
+    if (best < 0 || t < best) {
+      best = t;
+      pl = C1Plan{MI, NB, WR, v4 ? 4 : 1, static_cast<int>(tm), static_cast<int>(tn)};
+    }
+  }
+  return best >= 0;
+}
+
+int conv_1x1_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const float* bias, float* y, int relu,
+                    hipStream_t s, const WPack& wk) {
+  C1Plan pl;
+  if (!conv_1x1_plan(d, wk.query ? nullptr : x, pl)) return 0;
+  const int M = d->num_output, C = d->channels, HW = d->height * d->width;
+  const int BMc = 32 * pl.MI * pl.WR;
+  const int rblocks = pl.tiles_m * (BMc / 32);
+  const int64_t wfrags = (int64_t)rblocks * (C / 16);
+  if (wk.query) {
+    *wk.query = static_cast<size_t>(wfrags * 3072);
+    return 1;
+  }
+  Params P{};
+  P.M = M;
+  P.N = d->num * HW;
+  P.K = C;
+  P.split = 1;
+  P.cv.C = C;
+  P.cv.howo = make_fastdiv(HW);
+  P.e = make_epi(y, HW, 1.0f, 0.0f, bias, RRAM_BIAS_ROW, relu);
+  P.e.cimg = wk.y_img > 0 ? wk.y_img : (int64_t)M * HW;
+  P.e.hw = make_fastdiv(HW);
+  P.tiles_m = pl.tiles_m;
+  P.tiles_n = pl.tiles_n;
+  P.tiles_z = 1;
+  char* wbuf = wk.p ? static_cast<char*>(wk.p) : reinterpret_cast<char*>(pack_buffer(static_cast<size_t>(wfrags * 768), s));
+  RRAM_REQUIRE(wbuf != nullptr, "conv 1x1: packed-weight buffer allocation failed");
+  if (!wk.valid) {
+    const int wunits = static_cast<int>(wfrags * 64);
+    hipLaunchKernelGGL(k_conv_cb_pack_x6, dim3(stream_blocks(wunits)), dim3(256), 0, s, w, wbuf, M, C, 1, rblocks,
+                       wunits);
+    const int rc = launch_status("conv 1x1 weight pack x6");
+    if (rc) return rc;
+  }
+  const auto* wp = reinterpret_cast<const x6::bf16x8*>(wbuf);
+  const uint32_t xrange = static_cast<uint32_t>((int64_t)d->num * C * HW * 4);
+  const unsigned nwg = static_cast<unsigned>((int64_t)pl.tiles_m * pl.tiles_n);
+#define RRAM_X(mi, nb, wr)                                                                                 \
+  if (pl.MI == mi && pl.NB == nb && pl.WR == wr) {                                                         \
+    if (pl.VEC == 4)                                                                                       \
+      hipLaunchKernelGGL((k_conv1x1_x6<mi, nb, wr, 4>), dim3(nwg), dim3(256), 0, s, P, wp, x, xrange);     \
+    else                                                                                                   \
+      hipLaunchKernelGGL((k_conv1x1_x6<mi, nb, wr, 1>), dim3(nwg), dim3(256), 0, s, P, wp, x, xrange);     \
+  } else
+  RRAM_C1X1_LIST(RRAM_X) { return 0; }
+#undef RRAM_X
+  const int rc = launch_status("conv 1x1 x6");
+  return rc ? rc : 1;
+}
+
 int conv_patch_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const float* bias, float* y, int relu,
                       hipStream_t s, const WPack& wk);
 // The bf16x6 convolution forward.  x_oct: NULL or the octet companion of x
@@ -1968,7 +2211,8 @@ int conv_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, cons
     const int rc = conv_cb_x6_fwd(d, x, x_oct, w, bias, y, y_oct, relu, s, wk);
     if (rc != 0) return rc;
   }
-  int rc = conv_wide_x6_fwd(d, x, w, bias, y, relu, s, wk);
+  int rc = conv_1x1_x6_fwd(d, x, w, bias, y, relu, s, wk);
+  if (rc == 0) rc = conv_wide_x6_fwd(d, x, w, bias, y, relu, s, wk);
   if (rc == 0) rc = conv_patch_x6_fwd(d, x, w, bias, y, relu, s, wk);
   if (wk.query) return rc;
   if (rc > 0 && y_oct != nullptr) {
@@ -2140,9 +2384,10 @@ int rram_f32_engine_for_conv(const rram_conv_desc* d) {
   RRAM_REQUIRE(d != nullptr, "engine query: desc is NULL");
   rram::ConvPlan pl;
   rram::CbPlan cpl;
+  rram::C1Plan c1;
   return rram::f32_engine().load() == RRAM_ENGINE_BF16X6 &&
                  (rram::conv_x6_plan(d, pl) || rram::conv1_ring_ok(d) ||
-                  rram::conv_cb_plan(d, cpl))
+                  rram::conv_cb_plan(d, cpl) || rram::conv_1x1_plan(d, nullptr, c1))
              ? RRAM_ENGINE_BF16X6
              : RRAM_ENGINE_F32;
 }
