@@ -161,6 +161,8 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+    if os.environ.get("RRAM_BENCH_STREAM") == "1":   # A/B runs: a created stream instead of the NULL stream
+        torch.cuda.set_stream(torch.cuda.Stream())
     caffe.set_stream_from_torch()
     caffe.set_random_seed(args.seed)
     if args.workload not in ("alexnet_mc", "alexnet_mc_reuse_prefix"):

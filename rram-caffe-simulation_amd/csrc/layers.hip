@@ -116,53 +116,94 @@ __global__ void __launch_bounds__(256) k_pool_max_fixed(const float* __restrict_
   }
 }
 
-// The same max pool for small planes (H*W <= kPlaneTile): a block stages
-// whole (n, c) planes - contiguous in NCHW - in LDS with coalesced 16-byte
-// loads, then computes every output of those planes from LDS, so each input
-// is read from HBM once and the K*K window re-reads stay on-chip.  Outputs
-// are written contiguously.  Same window, order and tie rule as above.
-constexpr int kPlaneTile = 4096;  // floats of LDS per block
+// Pooling of small planes (H*W <= kPlaneMax): a block stages whole (n, c)
+// planes - contiguous in NCHW - in LDS, then computes every output of those
+// planes from LDS, so each input is read from HBM once and the window re-reads
+// stay on-chip.  The staging issues kStageU 16-byte raw buffer loads per
+// thread before the first LDS store (any 4-byte alignment; the per-dword range
+// check zeroes the tail), so a block keeps ~kStageU KB per wave in flight.
+// Outputs are written contiguously.  K = 2, 3: MAX with that square window
+// (k_pool_max_fixed's loop); K = 0: any window, MAX or AVE, with k_pool_fwd's
+// loops - the same window, summation order, divisor, tie rule and argmax.
+constexpr int kPlaneTile = 4096;   // floats: planes per block fill this much LDS
+constexpr int kPlaneMax = 16384;   // larger planes (64 KB) take one block each
+constexpr int kStageU = 8;
+// floor(a / b) for 0 <= a < 2^22, b >= 1 via the float reciprocal: (a + 0.5) / b
+// is >= 0.5 / b away from an integer, and the product's relative error
+// (<= 2^-23) is smaller than that while a + 0.5 < 4e6.
+__device__ __forceinline__ int div_small(int a, float inv_b) {
+  return static_cast<int>((static_cast<float>(a) + 0.5f) * inv_b);
+}
 template <int K>
-__global__ void __launch_bounds__(256) k_pool_max_planes(const float* __restrict__ x, float* __restrict__ y,
-                                                         int* __restrict__ mask, int planes, int H, int W, int PH,
-                                                         int PW, int sh, int sw, int ph, int pw, int ppb) {
-  __shared__ __attribute__((aligned(16))) float tile[kPlaneTile];
+__global__ void __launch_bounds__(256) k_pool_planes(const float* __restrict__ x, float* __restrict__ y,
+                                                     int* __restrict__ mask, int planes, int H, int W, int PH,
+                                                     int PW, int kh, int kw, int sh, int sw, int ph, int pw,
+                                                     int method, int ppb, float inv_phw, float inv_pw) {
+  extern __shared__ __attribute__((aligned(16))) float tile[];
   const int HW = H * W, PHW = PH * PW;
   const int p0 = blockIdx.x * ppb;
   const int np = min(ppb, planes - p0);
-  const float* src = x + (int64_t)p0 * HW;
   const int n_in = np * HW;
-  if ((reinterpret_cast<uintptr_t>(src) & 15u) == 0) {
-    const int n4 = n_in >> 2;
-    for (int i = threadIdx.x; i < n4; i += 256)
-      reinterpret_cast<float4*>(tile)[i] = reinterpret_cast<const float4*>(src)[i];
-    for (int i = (n4 << 2) + threadIdx.x; i < n_in; i += 256) tile[i] = src[i];
-  } else {
-    for (int i = threadIdx.x; i < n_in; i += 256) tile[i] = src[i];
+  const int n4 = (n_in + 3) >> 2;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(x + (int64_t)p0 * HW), 0, n_in * 4, 0x00020000);
+  for (int i0 = threadIdx.x; i0 < n4; i0 += 256 * kStageU) {
+    float4 r[kStageU];
+#pragma unroll
+    for (int u = 0; u < kStageU; ++u) {
+      const int i = min(i0 + 256 * u, n4);  // i == n4: past the range, loads zeros
+      r[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * i, 0, 0));
+    }
+#pragma unroll
+    for (int u = 0; u < kStageU; ++u)
+      if (i0 + 256 * u < n4) reinterpret_cast<float4*>(tile)[i0 + 256 * u] = r[u];
   }
   __syncthreads();
   const int n_out = np * PHW;
   float* dst = y + (int64_t)p0 * PHW;
   for (int o = threadIdx.x; o < n_out; o += 256) {
-    const int pl = o / PHW, r = o - pl * PHW;
-    const int phi = r / PW, pwi = r - phi * PW;
-    const int hs = phi * sh - ph, ws = pwi * sw - pw;
+    const int pl = div_small(o, inv_phw), r = o - pl * PHW;
+    const int phi = div_small(r, inv_pw), pwi = r - phi * PW;
+    int hs = phi * sh - ph, ws = pwi * sw - pw;
     const float* t = tile + pl * HW;
     float mv = -FLT_MAX;
     int mi = -1;
+    if constexpr (K > 0) {
 #pragma unroll
-    for (int a = 0; a < K; ++a)
+      for (int a = 0; a < K; ++a)
 #pragma unroll
-      for (int b = 0; b < K; ++b) {
-        const int h = hs + a, w = ws + b;
-        const bool ok = static_cast<unsigned>(h) < static_cast<unsigned>(H) &&
-                        static_cast<unsigned>(w) < static_cast<unsigned>(W);
-        const float v = t[ok ? h * W + w : 0];
-        if (ok && v > mv) {
-          mv = v;
-          mi = h * W + w;
+        for (int b = 0; b < K; ++b) {
+          const int h = hs + a, w = ws + b;
+          const bool ok = static_cast<unsigned>(h) < static_cast<unsigned>(H) &&
+                          static_cast<unsigned>(w) < static_cast<unsigned>(W);
+          const float v = t[ok ? h * W + w : 0];
+          if (ok && v > mv) {
+            mv = v;
+            mi = h * W + w;
+          }
         }
-      }
+    } else if (method == RRAM_POOL_MAX) {
+      const int he = min(hs + kh, H), we = min(ws + kw, W);
+      hs = max(hs, 0);
+      ws = max(ws, 0);
+      for (int h = hs; h < he; ++h)
+        for (int w = ws; w < we; ++w)
+          if (t[h * W + w] > mv) {
+            mi = h * W + w;
+            mv = t[mi];
+          }
+    } else {
+      int he = min(hs + kh, H + ph), we = min(ws + kw, W + pw);
+      const int psize = (he - hs) * (we - ws);
+      hs = max(hs, 0);
+      ws = max(ws, 0);
+      he = min(he, H);
+      we = min(we, W);
+      float s = 0.0f;
+      for (int h = hs; h < he; ++h)
+        for (int w = ws; w < we; ++w) s += t[h * W + w];
+      mv = s / psize;
+    }
     dst[o] = mv;
     if (mask) mask[(int64_t)p0 * PHW + o] = mi;
   }
@@ -732,17 +773,17 @@ int rram_pool_fwd(const float* x, float* y, int* mask, int num, int C, int H, in
   if (total == 0) return RRAM_OK;
   RRAM_REQUIRE(x && y, "pool_fwd: NULL");
   const int planes = num * C;
-  if (method == RRAM_POOL_MAX && kh == kw && (kh == 3 || kh == 2) && H * W <= kPlaneTile) {
+  if (H * W <= kPlaneMax) {
     // planes per block: fill the LDS tile, but keep >= 2048 blocks when possible
-    int ppb = kPlaneTile / (H * W);
+    int ppb = H * W <= kPlaneTile ? kPlaneTile / (H * W) : 1;
     while (ppb > 1 && (planes + ppb - 1) / ppb < 2048) --ppb;
     const dim3 grid(static_cast<unsigned>((planes + ppb - 1) / ppb));
-    if (kh == 3)
-      hipLaunchKernelGGL(k_pool_max_planes<3>, grid, dim3(kThreads), 0, as_stream(s), x, y, mask, planes, H, W, PH,
-                         PW, sh, sw, ph, pw, ppb);
-    else
-      hipLaunchKernelGGL(k_pool_max_planes<2>, grid, dim3(kThreads), 0, as_stream(s), x, y, mask, planes, H, W, PH,
-                         PW, sh, sw, ph, pw, ppb);
+    const size_t lds = (static_cast<size_t>(ppb) * H * W + 3) / 4 * 16;
+    const float inv_phw = 1.0f / static_cast<float>(PH * PW), inv_pw = 1.0f / static_cast<float>(PW);
+    const int k = method == RRAM_POOL_MAX && kh == kw && (kh == 3 || kh == 2) ? kh : 0;
+    auto kern = k == 3 ? k_pool_planes<3> : k == 2 ? k_pool_planes<2> : k_pool_planes<0>;
+    hipLaunchKernelGGL(kern, grid, dim3(kThreads), lds, as_stream(s), x, y, mask, planes, H, W, PH, PW, kh, kw, sh,
+                       sw, ph, pw, method, ppb, inv_phw, inv_pw);
   } else if (method == RRAM_POOL_MAX && kh == kw && kh == 3)
     hipLaunchKernelGGL(k_pool_max_fixed<3>, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), x, y,
                        mask, num, C, H, W, PH, PW, sh, sw, ph, pw);

@@ -1030,10 +1030,10 @@ k_conv1x1_x6(Params P, const x6::bf16x8* __restrict__ wpack, const float* __rest
   }
   const uint32_t kstep = static_cast<uint32_t>(HW) * 64u;  // bytes per K-tile (16 channel planes)
   SV stg[RING][LPT];
-  auto load_b = [&](SV (&r)[LPT], int kt) {
+  auto load_b = [&](SV (&r)[LPT], int kt, bool ok) {  // !ok: past the range (zeros, no traffic)
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
-      const int o = static_cast<int>(loff[i] + static_cast<uint32_t>(kt) * kstep);
+      const int o = static_cast<int>(ok ? loff[i] + static_cast<uint32_t>(kt) * kstep : 0x80000000u);
       if constexpr (VEC == 4)
         r[i] = __builtin_bit_cast(int4x, __builtin_amdgcn_raw_buffer_load_b128(xr, o, 0, 0));
       else
@@ -1065,39 +1065,48 @@ k_conv1x1_x6(Params P, const x6::bf16x8* __restrict__ wpack, const float* __rest
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
+  // Every load is issued unconditionally (K-tiles past the end read zeros
+  // past the buffer range, weight fragments re-read the last K-tile): vmcnt
+  // counts in issue order, and a load the compiler cannot prove issued (one
+  // under a branch) makes it drain the whole ring at the next wait.
   // prologue: K-tiles 0 .. RING - 1 in flight, K-tile 0 in LDS stage 0
 #pragma unroll
-  for (int q = 0; q < RING; ++q)
-    if (q < KT) load_b(stg[q], q);
+  for (int q = 0; q < RING; ++q) load_b(stg[q], q, q < KT);
   load_a(fa[0], 0);
+  __builtin_amdgcn_sched_barrier(0);
   store_b(stg[0], 0);
   __syncthreads();
 
   const int colw = 32 * NB * wc + lr;
-  // K-tile kt (kt % RING == PH): its B from LDS stage PH & 1
+  // K-tile kt (kt % RING == PH): its B from LDS stage PH & 1.  K-tiles
+  // KT .. KTP - 1 only keep the load stream uniform.
   auto step = [&](int kt, auto ph_c) {
     constexpr int PH = decltype(ph_c)::value;
-    if (kt + RING < KT) load_b(stg[PH], kt + RING);
-    if (kt + 1 < KT) load_a(fa[(PH + 1) & 1], kt + 1);
-    const float* bs = smem + (PH & 1) * STG + 8 * lh * BNc + colw;
+    // this step's loads go out before any MFMA (the scheduler would otherwise
+    // sink them next to their uses)
+    load_b(stg[PH], kt + RING, kt + RING < KT);
+    load_a(fa[(PH + 1) & 1], min(kt + 1, KT - 1));
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt < KT) {
+      const float* bs = smem + (PH & 1) * STG + 8 * lh * BNc + colw;
 #pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      float v[8];
+      for (int j = 0; j < NB; ++j) {
+        float v[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = bs[e * BNc + 32 * j];
-      x6::Parts bp;
-      x6::split8_safe(v, bp);
+        for (int e = 0; e < 8; ++e) v[e] = bs[e * BNc + 32 * j];
+        x6::Parts bp;
+        x6::split8_safe(v, bp);
 #pragma unroll
-      for (int i = 0; i < MI; ++i) acc[i][j] = x6::mfma6(fa[PH & 1][i], bp, acc[i][j]);
+        for (int i = 0; i < MI; ++i) acc[i][j] = x6::mfma6(fa[PH & 1][i], bp, acc[i][j]);
+      }
     }
+    __builtin_amdgcn_sched_barrier(0);
     if (kt + 1 < KT) store_b(stg[(PH + 1) % RING], (PH + 1) & 1);
     __syncthreads();
   };
-  for (int kt = 0; kt < KT; kt += RING) {
-    static_for<0, RING>([&](auto ph) {
-      if (kt + decltype(ph)::value < KT) step(kt + decltype(ph)::value, ph);
-    });
-  }
+  const int KTP = (KT + RING - 1) / RING * RING;
+  for (int kt = 0; kt < KTP; kt += RING)
+    static_for<0, RING>([&](auto ph) { step(kt + decltype(ph)::value, ph); });
   Epi ep = P.e;
   conv_epilogue_nchw<MI, NB>(acc, P, ep, m0 + 32 * MI * wr, n0 + 32 * NB * wc, lr, lh);
 }
@@ -1937,7 +1946,30 @@ bool conv_cb_plan(const rram_conv_desc* d, CbPlan& pl) {
     int PD = 0;
     for (int p : {8, 12, 14, 15})
       if (PD == 0 && p >= need && cb_instantiated(KH, WR, NB, p)) PD = p;
-    if (PD == 0) continue;
+    if (PD == 0) {
+      // the contiguous tiles' patch does not fit (tiles spanning two images
+      // carry two halos): per-image tiles of this shape, one halo each, the
+      // last tile of an image short (GoogLeNet conv2, 64 x 256 on 56 x 56:
+      // 13 tiles per image instead of 128 x 128 tiles with 1/4 padded rows)
+      const int tpi = (HW + BN - 1) / BN;
+      int rm = 0;
+      for (int t = 0; t < tpi; ++t) {
+        const int f = t * BN / OW, l = (std::min((t + 1) * BN, HW) - 1) / OW;
+        rm = std::max(rm, l - f + KH);
+      }
+      const int ob = rm * RPC * 16;
+      const int nd = (2 * ob / 16 + 255) / 256;
+      for (int p : {8, 12, 14, 15})
+        if (PD == 0 && p >= nd && cb_instantiated(KH, WR, NB, p)) PD = p;
+      const int64_t nwg = (int64_t)G * tiles_m * tpi * d->num;
+      if (PD == 0 || nwg >= (1ll << 31)) continue;
+      const int64_t cost = (nwg + 255) / 256 * BM * BN;
+      if (best < 0 || cost < best) {
+        best = cost;
+        pl = CbPlan{WR, NB, RPC, PD, ob, tiles_m, static_cast<int>(tpi * d->num), 1, tpi};
+      }
+      continue;
+    }
     const int64_t nwg = (int64_t)G * tiles_m * tiles_n;
     if (nwg >= (1ll << 31)) continue;
     const int64_t cost = (nwg + 255) / 256 * BM * BN;

@@ -12,6 +12,37 @@
 
 namespace caffe {
 
+GraphStream::~GraphStream() {
+  if (own_) {
+    (void)hipStreamSynchronize(own_);
+    (void)hipStreamDestroy(own_);
+  }
+  if (ev_in_) (void)hipEventDestroy(ev_in_);
+  if (ev_out_) (void)hipEventDestroy(ev_out_);
+}
+
+void GraphStream::enter() {
+  if (Caffe::hip_stream() != nullptr) return;
+  if (!own_) {
+    HIP_CALL(hipStreamCreateWithFlags(&own_, hipStreamNonBlocking));
+    HIP_CALL(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming));
+    HIP_CALL(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming));
+  }
+  HIP_CALL(hipEventRecord(ev_in_, nullptr));
+  HIP_CALL(hipStreamWaitEvent(own_, ev_in_, 0));
+  Caffe::set_stream(reinterpret_cast<rram_stream_t>(own_));
+  active_ = true;
+}
+
+void GraphStream::leave() {
+  if (!active_) return;
+  active_ = false;
+  Caffe::set_stream(nullptr);
+  // no throw from a destructor path: a failed record / wait surfaces at the
+  // caller's next synchronisation
+  if (hipEventRecord(ev_out_, own_) == hipSuccess) (void)hipStreamWaitEvent(nullptr, ev_out_, 0);
+}
+
 // ============================================================ FailureMaker
 template <typename Dtype>
 FailureMaker<Dtype>::~FailureMaker() {
@@ -446,25 +477,40 @@ void Solver<Dtype>::Step(int iters) {
     const bool rate_stable = rate_now == graph_prev_rate_;
     graph_prev_rate_ = rate_now;
     if (graph_ && rate_stable && can_fuse && !test_now && !disp && average_loss <= 1 && !net_->on_backward_layer) {
+      // the first such iteration runs eager (workspaces and scratch buffers
+      // get allocated on the section's stream), the next one captures
       const Dtype rate = rate_now;
-      if (gx_[0] && (rate != graph_rate_ || graph_key() != graph_ptrs_)) drop_graphs();
-      if (graph_warm_) {
-        net_->set_iter((uint64_t)iter_);
-        capture_launch(0, [&] {
+      const bool warm = graph_warm_;
+      net_->set_iter((uint64_t)iter_);
+      {
+        GraphStreamScope sc(gstream_);
+        if (warm && gx_[0] && (rate != graph_rate_ || graph_key() != graph_ptrs_)) drop_graphs();
+        auto fb = [&] {
           net_->ClearParamDiffs();
           net_->Forward(false);
           net_->Backward();
-        });
-        if (on_gradients_ready) on_gradients_ready();
-        capture_launch(1, [&] { FusedTail(); });
-        graph_rate_ = rate;
-        graph_ptrs_ = graph_key();
-        ++iter_;
-        const long long snap = param_.integer("snapshot", 0);
-        if (snap && iter_ % snap == 0) Snapshot();
-        continue;
+        };
+        if (warm)
+          capture_launch(0, fb);
+        else
+          fb();
       }
-      graph_warm_ = true;  // this iteration runs eager (workspaces allocated), the next one captures
+      if (on_gradients_ready) on_gradients_ready();  // on the caller's stream, after the section
+      {
+        GraphStreamScope sc(gstream_);
+        if (warm) {
+          capture_launch(1, [&] { FusedTail(); });
+          graph_rate_ = rate;
+          graph_ptrs_ = graph_key();
+        } else {
+          FusedTail();
+        }
+      }
+      graph_warm_ = true;
+      ++iter_;
+      const long long snap = param_.integer("snapshot", 0);
+      if (snap && iter_ % snap == 0) Snapshot();
+      continue;
     }
     net_->ClearParamDiffs();
     if (test_now) TestAll();
@@ -874,6 +920,7 @@ void MonteCarlo<Dtype>::map_body(bool dev_state, uint32_t m) {
 template <typename Dtype>
 void MonteCarlo<Dtype>::Run(uint32_t map_begin, uint32_t map_count) {
   if (graph_ && !overlap_ && !reuse_prefix_ && !timing_ && !net_->timing_on() && map_count > 0) {
+    GraphStreamScope sc(gstream_);
     hipStream_t st = Caffe::hip_stream();
     HIP_CALL(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_state_), static_cast<int>(map_begin), 1, st));
     if (gexec_ && graph_key() != graph_ptrs_) drop_graph();

@@ -20,6 +20,32 @@
 
 namespace caffe {
 
+// hipStreamBeginCapture refuses the legacy NULL stream (e.g. torch's default
+// stream).  On it, a graph section (eager warm-up, capture, launches) runs on
+// a private non-blocking stream instead, ordered after the caller's earlier
+// work and before its later work by two events, with Caffe's stream switched
+// for the section so every launch and stream-keyed scratch buffer of the
+// section sees one stream.  On any other stream it does nothing.
+class GraphStream {
+ public:
+  GraphStream() = default;
+  GraphStream(const GraphStream&) = delete;
+  GraphStream& operator=(const GraphStream&) = delete;
+  ~GraphStream();
+  void enter();
+  void leave();
+
+ private:
+  hipStream_t own_ = nullptr;
+  hipEvent_t ev_in_ = nullptr, ev_out_ = nullptr;
+  bool active_ = false;
+};
+struct GraphStreamScope {
+  explicit GraphStreamScope(GraphStream& g) : g_(g) { g_.enter(); }
+  ~GraphStreamScope() { g_.leave(); }
+  GraphStream& g_;
+};
+
 template <typename Dtype>
 class Solver;
 
@@ -216,6 +242,7 @@ class Solver {
   bool graph_ = false, graph_warm_ = false;
   hipGraph_t gg_[2] = {nullptr, nullptr};
   hipGraphExec_t gx_[2] = {nullptr, nullptr};
+  GraphStream gstream_;
   Dtype graph_rate_ = 0, graph_prev_rate_ = -1;
   std::vector<const void*> graph_ptrs_;
   std::vector<const void*> graph_key() const;
@@ -330,6 +357,7 @@ class MonteCarlo {
   uint32_t* d_state_ = nullptr;
   hipGraph_t graph_g_ = nullptr;
   hipGraphExec_t gexec_ = nullptr;
+  GraphStream gstream_;
   std::vector<const void*> graph_ptrs_;  // the device pointers the graph was captured with
   void map_body(bool dev_state, uint32_t m);  // one map's launches on the working stream
   std::vector<const void*> graph_key() const;

@@ -178,8 +178,12 @@ def lenet_cpu_baseline(batch, p_fault, seed, budget_s=10.0):
 
 
 def _graph_on():
-    """MonteCarlo hipGraph replay for the launch-bound MC workloads (RRAM_MC_GRAPH=0: eager, for A/Bs)."""
-    return os.environ.get("RRAM_MC_GRAPH", "1") != "0"
+    """MonteCarlo / Solver hipGraph replay for the launch-bound workloads: off
+    by default (RRAM_MC_GRAPH=1 turns it on).  Measured on MI355X / ROCm 7 it
+    is slower than eager launches on every one of them, on torch's NULL stream
+    (a private capture stream + 2 events per call) and on a created stream
+    alike (profiles/r04_ab_graph.txt)."""
+    return os.environ.get("RRAM_MC_GRAPH", "0") != "0"
 
 
 def run_workload(args, world, rank, dev):
@@ -199,7 +203,7 @@ def run_workload(args, world, rank, dev):
             cfgs.append(make_inject_cfg(0.01, 10, 20, 10, quant_levels=16, g_max=gmax, var_sigma=0.1,
                                         stuck_scale=gmax))
         mc = caffe.MonteCarlo(net, cfgs, seed=args.seed, max_maps=(args.steps + args.warmup) * 10 + 8)
-        mc.set_graph(_graph_on())         # launch-bound: replay each map as one hipGraph
+        mc.set_graph(_graph_on())         # replay each map as one hipGraph (opt-in, see _graph_on)
         maps_per_step = 10
         el = _timed(world, dev, lambda i: mc.run((rank + world * i) * maps_per_step, maps_per_step),
                     args.steps, args.warmup)
@@ -268,7 +272,7 @@ def run_workload(args, world, rank, dev):
         opts = dict(opts, fused_update=True)
         # bucketed gradient all-reduce overlapped with backward (world > 1 only)
         dp = DataParallelSolver(sp, net_txt, opts, seed=args.seed, overlap=True)
-        dp.solver.set_graph(_graph_on())  # launch-bound: iteration replayed as two hipGraphs around the all-reduce
+        dp.solver.set_graph(_graph_on())  # iteration as two hipGraphs around the all-reduce (opt-in)
         el = _timed(world, dev, lambda i: dp.step(1), args.steps, args.warmup)
         res = _base(f"fault-aware training images/sec, {args.workload}", "images/s",
                     world * args.steps * batch / el, world, args, el, workload=args.workload,

@@ -30,6 +30,8 @@ CASES = [
     dict(x=(2, 96, 27, 27), cout=256, k=5, s=1, p=2, g=2),    # conv2: channel-octet kernel
     dict(x=(2, 256, 13, 13), cout=384, k=3, s=1, p=1, g=1),   # conv3: channel-octet kernel
     dict(x=(2, 24, 20, 20), cout=96, k=3, s=1, p=1, g=1),     # Cin % 16 != 0: patch kernel
+    dict(x=(3, 480, 14, 14), cout=192, k=1, s=1, p=0, g=1),   # 1x1: k_conv1x1_x6 (16-byte loads)
+    dict(x=(3, 832, 7, 7), cout=48, k=1, s=1, p=0, g=1),      # 1x1: k_conv1x1_x6 (4-byte loads)
 ]
 
 
@@ -62,12 +64,14 @@ def test_cached_pack_bit_identical(device, cs):
 
 
 def test_no_pack_for_fp32_engine_shapes(device):
-    """Shapes the fp32 MFMA engine takes (1x1, 7x7 stride 2) have no pack;
-    the cached entry point refuses a pack for them instead of ignoring it."""
+    """Shapes the fp32 MFMA engine takes (1x1 with C % 16 != 0, 7x7 stride 2)
+    have no pack; the cached entry point refuses a pack for them instead of
+    ignoring it.  (A 1x1 with C % 16 == 0 runs k_conv1x1_x6 and has one.)"""
     import torch
     from rramsim import ops
     from rramsim import _kernels as K
-    for xs, co, k, s, p in (((2, 32, 14, 14), 64, 1, 1, 0), ((2, 3, 64, 64), 64, 7, 2, 3)):
+    assert ops.conv_weight_pack_bytes(ops.conv_desc((2, 32, 14, 14), 64, 1, 1, 0, 1, 1)) == 2 * 2 * 3072
+    for xs, co, k, s, p in (((2, 24, 14, 14), 64, 1, 1, 0), ((2, 3, 64, 64), 64, 7, 2, 3)):
         d = ops.conv_desc(xs, co, k, s, p, 1, 1)
         assert ops.conv_weight_pack_bytes(d) == 0
         x = torch.zeros(xs, device=device)
