@@ -69,7 +69,18 @@ __global__ void __launch_bounds__(256)
   static_assert(kBandPix == 2 * 256, "two pixels per thread: the packed LRN pair");
   constexpr int PRE = (SIZE - 1) / 2;
   constexpr int D = G;
-  __shared__ float ybuf[2][D][kBandPix];
+  // WT rows: input row i at rowbase(i) = (i / 2) R2 + (i % 2) WT, R2 >= 2 WT with
+  // R2 = PWT (mod 32), PWT the pooled width: a pooled row (two input rows
+  // down) then starts PWT banks after the previous one, so the 32 consecutive
+  // outputs of a ds_read_b32 lane group sit on 32 distinct banks even across a
+  // row wrap (a plain pitch put 2 addresses on some bank of almost every read:
+  // 40-46 % of the LDS-active cycles were conflicts in round 4)
+  constexpr int PWT = WT > 0 ? (WT - K + 1) / 2 + 1 : 1;
+  constexpr int R2 = WT > 0 ? 2 * WT + (((PWT - 2 * WT) % 32) + 32) % 32 : 0;
+  constexpr int YBS = WT > 0 ? ((kBandPix / WT - 1) / 2 * R2 + ((kBandPix / WT - 1) % 2) * WT + WT + 3) / 4 * 4
+                             : kBandPix;
+  auto rowbase = [](int i) { return (i >> 1) * R2 + (i & 1) * WT; };
+  __shared__ float ybuf[2][D][YBS];
   __shared__ float obuf[OCT ? 8 : 1][OCT ? 256 : 1];
   // XCD-aware tile order: consecutive workgroups go to the 8 XCDs in turn, so
   // workgroup L runs on XCD L % 8 as that XCD's (L / 8)-th; each XCD gets a
@@ -99,7 +110,7 @@ __global__ void __launch_bounds__(256)
   auto slot = [&](int pix) {
     if constexpr (WT > 0) {
       const int r = pix / WT, c = pix - r * WT;
-      return r * WT + (c & 1) * HWC + (c >> 1);
+      return rowbase(r) + (c & 1) * HWC + (c >> 1);
     } else {
       return pix;
     }
@@ -164,14 +175,15 @@ __global__ void __launch_bounds__(256)
                                     static_cast<unsigned>(wr + b) < static_cast<unsigned>(W))
               << (a * K + b);
     it_d[i] = it < D * NO ? d : D;  // D = no item
-    it_l[i] = (hr - h0) * W + (WT > 0 ? (wr >> 1) : wr);  // WT: wr is even (stride 2, no column pad)
+    // WT: wr is even (stride 2, no column pad) and hr - h0 too (stride 2, no row pad)
+    it_l[i] = WT > 0 ? rowbase(hr - h0) + (wr >> 1) : (hr - h0) * W + wr;
     it_out[i] = (pr0 + prl) * PW + pwi;
     it_vo[i] = (d * PHW + it_out[i]) * 4;
     it_ok[i] = ok;
   }
   // one channel group: c0 = its first channel, yb = its LDS plane buffer,
   // gi = its place in the staging rotation (g % NS)
-  auto group = [&](int c0, float (*yb)[kBandPix], auto gi) {
+  auto group = [&](int c0, float (*yb)[YBS], auto gi) {
     constexpr int GI = decltype(gi)::value;
     f32x2(&load_into)[D] = st[GI];
     const f32x2(&fill_from)[D] = st[(GI + 1) % NS];
@@ -200,7 +212,7 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
           for (int a = 0; a < K; ++a)
 #pragma unroll
-            for (int b = 0; b < K; ++b) t[a * K + b] = yl[a * WT + (b & 1) * HWC + (b >> 1)];
+            for (int b = 0; b < K; ++b) t[a * K + b] = yl[rowbase(a) + (b & 1) * HWC + (b >> 1)];
           // v_max3 over the taps: the strict-">" walk's value whenever the
           // maximum is not zero (a quiet NaN loses to any number in both; the
           // plane holds products, never a signalling NaN); for a zero maximum
@@ -219,7 +231,7 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
             for (int b = 0; b < K; ++b) {
               const bool ok = (it_ok[i] >> (a * K + b)) & 1u;
-              const int tap = WT > 0 ? a * WT + (b & 1) * HWC + (b >> 1) : a * W + b;
+              const int tap = WT > 0 ? rowbase(a) + (b & 1) * HWC + (b >> 1) : a * W + b;
               const float v = yl[ok ? tap : -it_l[i]];  // masked taps read element 0
               if (ok && v > mv) mv = v;
             }
@@ -327,7 +339,9 @@ int rram_lrn_maxpool_fwd_octets(const float* x, float* y, void* y_oct, int num, 
   else                                                                                                             \
     hipLaunchKernelGGL((k_lrn_maxpool_band<K_, S_, kLrnG, false, WT_>), grid, dim3(kThreads), 0, as_stream(s), x,  \
                        y, yo, C, H, W, PH, PW, sh, sw, ph, pw, rb, cc, bands, nchunks, aos, beta, k);
-  const bool wt_ok = sw == 2 && pw == 0;  // the WT plane rows are de-interleaved by a window stride of 2
+  // the WT plane rows are de-interleaved by a window stride of 2 and paired
+  // two rows per pitch (a pooled row = two input rows down, from an even row)
+  const bool wt_ok = sw == 2 && pw == 0 && sh == 2 && ph == 0;
 #define RRAM_LP(K_, S_)                                  \
   if (kernel == K_ && size == S_) {                      \
     if (K_ == 3 && S_ == 5 && W == 55 && wt_ok) {        \
