@@ -1111,6 +1111,144 @@ k_conv1x1_x6(Params P, const x6::bf16x8* __restrict__ wpack, const float* __rest
   conv_epilogue_nchw<MI, NB>(acc, P, ep, m0 + 32 * MI * wr, n0 + 32 * NB * wc, lr, lh);
 }
 
+// k_conv1x1_dma_x6: the same contraction with every operand LDS-DMA'd
+// (buffer_load ... lds) into an NS-stage ring, NS - 1 K-tiles ahead: per
+// K-tile the weight fragments of the tile's row blocks (3 KB each) and the
+// fp32 activation tile [16 channels][BNc positions].  The wait for K-tile
+// kt + 1 is a hand-counted vmcnt (every wave issues the same number of
+// pieces, OOB dummies included), so no weight load issued after the next
+// activation tile forces that tile to land early (the register-ring form's
+// in-order vmcnt did: about one K-tile of latency hiding).
+namespace c1x1 {
+constexpr int NS = 4;  // LDS stages
+}  // namespace c1x1
+template <int MI, int NB, int WR, int VEC>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+k_conv1x1_dma_x6(Params P, const x6::bf16x8* __restrict__ wpack, const float* __restrict__ x, uint32_t xrange,
+                 uint32_t wrange) {
+  using namespace g2;
+  constexpr int WC = 4 / WR, BMc = 32 * MI * WR, BNc = 32 * NB * WC, RBL = BMc / 32;
+  constexpr int NS = c1x1::NS;
+  constexpr int A_BYTES = RBL * 3072, B_BYTES = 64 * BNc, STB = A_BYTES + B_BYTES;
+  constexpr int NA = RBL * 3;                         // 1 KB weight pieces per K-tile
+  constexpr int PIECE_B = VEC == 4 ? 1024 : 256;      // bytes per activation piece
+  constexpr int NBP = B_BYTES / PIECE_B;
+  constexpr int PA = (NA + 3) / 4, PB = (NBP + 3) / 4, PPW = PA + PB;
+  static_assert(NS * STB + 1024 <= 160 * 1024, "LDS");
+  static_assert((NS - 2) * PPW <= 63, "vmcnt");
+  __shared__ __attribute__((aligned(16))) char smem[NS * STB + 1024];  // + the dummy pieces' landing pad
+  const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem));
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lr = lane & 31, lh = lane >> 5;
+  const int wr = wave % WR, wc = wave / WR;
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, loc = bid >> 3;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int tid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const int tm = __builtin_amdgcn_readfirstlane(tid % P.tiles_m);
+  const int tn = __builtin_amdgcn_readfirstlane(tid / P.tiles_m);
+  const int m0 = tm * BMc, n0 = tn * BNc;
+  const int HW = static_cast<int>(P.cv.howo.d), C = P.cv.C, KT = C >> 4;
+  const int4v xrs = make_rsrc(x, xrange);
+  const int4v wrs = make_rsrc(reinterpret_cast<const float*>(wpack), wrange);
+  // weight piece a = wave + 4 i: row block a / 3, term a % 3 of K-tile kt at
+  // (((tm RBL + a / 3) KT + kt) 3072 + (a % 3) 1024) + 16 lane
+  uint32_t aoff[PA], alds[PA];
+#pragma unroll
+  for (int i = 0; i < PA; ++i) {
+    const int a = wave + 4 * i;
+    const bool ok = a < NA;
+    aoff[i] = ok ? static_cast<uint32_t>(((tm * RBL + a / 3) * KT) * 3072 + (a % 3) * 1024 + lane * 16) : 0x80000000u;
+    alds[i] = ok ? static_cast<uint32_t>((a / 3 * 3 + a % 3) * 1024) : 0xFFFFFFFFu;
+  }
+  // activation piece q = wave + 4 i: floats q PIECE_B / 4 .. of the stage's
+  // [16][BNc] tile, this lane's VEC of them at element q PIECE_B / 4 + VEC lane
+  uint32_t boff[PB], blds[PB];
+#pragma unroll
+  for (int i = 0; i < PB; ++i) {
+    const int q = wave + 4 * i;
+    uint32_t off = 0x80000000u;
+    if (q < NBP) {
+      const int e = q * (PIECE_B / 4) + lane * VEC;
+      const int c = e / BNc, n = n0 + (e - c * BNc);
+      if (n < P.N) {
+        const uint32_t img = fdiv(static_cast<uint32_t>(n), P.cv.howo);
+        const uint32_t sp = static_cast<uint32_t>(n) - img * static_cast<uint32_t>(HW);
+        off = ((img * static_cast<uint32_t>(C) + static_cast<uint32_t>(c)) * static_cast<uint32_t>(HW) + sp) * 4u;
+      }
+    }
+    boff[i] = off;
+    blds[i] = q < NBP ? static_cast<uint32_t>(A_BYTES + q * PIECE_B) : 0xFFFFFFFFu;
+  }
+  const uint32_t kstep = static_cast<uint32_t>(HW) * 64u;  // activation bytes per K-tile
+  // every wave issues PPW pieces per K-tile (past the end: OOB, zeros into the pad)
+  auto issue = [&](int kt) {
+    const bool ok = kt < KT;
+    const uint32_t st = lds0 + static_cast<uint32_t>((kt % NS) * STB);
+#pragma unroll
+    for (int i = 0; i < PA; ++i) {
+      const bool real = ok && alds[i] != 0xFFFFFFFFu;
+      dma_b128(wrs, real ? aoff[i] + static_cast<uint32_t>(kt) * 3072u : 0x80000000u,
+               real ? st + alds[i] : lds0 + static_cast<uint32_t>(NS * STB));
+    }
+#pragma unroll
+    for (int i = 0; i < PB; ++i) {
+      const bool real = ok && blds[i] != 0xFFFFFFFFu;
+      const uint32_t vo = real && boff[i] != 0x80000000u ? boff[i] + static_cast<uint32_t>(kt) * kstep : 0x80000000u;
+      const uint32_t dst = real ? st + blds[i] : lds0 + static_cast<uint32_t>(NS * STB);
+      if constexpr (VEC == 4)
+        dma_b128(xrs, vo, dst);
+      else
+        dma_b32(xrs, vo, dst);
+    }
+  };
+  floatx16 acc[MI][NB];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t) issue(t);
+  wait_vm<(NS - 2) * PPW>();
+  __builtin_amdgcn_s_barrier();
+  const int colw = 32 * NB * wc + lr;
+  for (int kt = 0; kt < KT; ++kt) {
+    issue(kt + NS - 1);
+    const char* st = smem + (kt % NS) * STB;
+    x6::Parts fa[MI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const char* f = st + (MI * wr + i) * 3072 + lane * 16;
+      fa[i].h = *reinterpret_cast<const x6::bf16x8*>(f);
+      fa[i].m = *reinterpret_cast<const x6::bf16x8*>(f + 1024);
+      fa[i].l = *reinterpret_cast<const x6::bf16x8*>(f + 2048);
+    }
+    const float* bs = reinterpret_cast<const float*>(st + A_BYTES) + 8 * lh * BNc + colw;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = bs[e * BNc + 32 * j];
+      x6::Parts bp;
+      x6::split8_safe(v, bp);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) acc[i][j] = x6::mfma6(fa[i], bp, acc[i][j]);
+    }
+    wait_vm<(NS - 2) * PPW>();  // this wave's pieces of K-tile kt + 1 have landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // ... and every wave's; stage kt % NS is free
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  Epi ep = P.e;
+  conv_epilogue_nchw<MI, NB>(acc, P, ep, m0 + 32 * MI * wr, n0 + 32 * NB * wc, lr, lh);
+}
+
 // w [G*M][Cg][T] -> fragments [G][tiles_m][WR][Cg/16][T][term][64 lanes][8]:
 // lane (lr, h) of fragment (kt, s) holds row 32 (tm WR + wr) + lr, channels
 // 16 kt + 8 h .. + 7 at tap s.  One thread per (fragment, lane).
@@ -1941,7 +2079,10 @@ bool conv_cb_plan(const rram_conv_desc* d, CbPlan& pl) {
     if ((tiles_m * BM - M) * 4 > tiles_m * BM) continue;  // > 1/4 padded rows
     const int rmax = patch_rows(N, HW, OW, OH, KH, BN, 3);
     if (rmax < 0) continue;
-    const int octb = rmax * RPC * 16;
+    // octet plane size rounded to 256 bytes: the 16x16x32 form reads both
+    // planes in one ds_read_b128 lane group, conflict-free only when the
+    // plane offset is a multiple of the 64 banks
+    const int octb = (rmax * RPC * 16 + 255) / 256 * 256;
     const int need = (2 * octb / 16 + 255) / 256;  // 1 KB pieces per wave
     int PD = 0;
     for (int p : {8, 12, 14, 15})
@@ -1957,7 +2098,7 @@ bool conv_cb_plan(const rram_conv_desc* d, CbPlan& pl) {
         const int f = t * BN / OW, l = (std::min((t + 1) * BN, HW) - 1) / OW;
         rm = std::max(rm, l - f + KH);
       }
-      const int ob = rm * RPC * 16;
+      const int ob = (rm * RPC * 16 + 255) / 256 * 256;
       const int nd = (2 * ob / 16 + 255) / 256;
       for (int p : {8, 12, 14, 15})
         if (PD == 0 && p >= nd && cb_instantiated(KH, WR, NB, p)) PD = p;
@@ -1995,7 +2136,7 @@ bool conv_cb_plan(const rram_conv_desc* d, CbPlan& pl) {
       const int f = t * BN / OW, l = (std::min((t + 1) * BN, HW) - 1) / OW;
       rmax = std::max(rmax, l - f + KH);
     }
-    const int octb = rmax * RPC * 16;
+    const int octb = (rmax * RPC * 16 + 255) / 256 * 256;
     const int need = (2 * octb / 16 + 255) / 256;
     const int64_t nwg = (int64_t)G * tiles_m * tpi * d->num;
     const int64_t cost = (nwg + 511) / 512 * 2 * BM * BN;
@@ -2137,17 +2278,23 @@ int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, c
 }
 
 // ---- k_conv1x1_x6 plan ----
+// RRAM_C1X1 (A/B runs): 1 = per-shape choice (default), 2 = k_conv1x1_x6
+// (register ring) only, 3 = k_conv1x1_dma_x6 only, 0 = neither (the fp32-MFMA
+// table-gather GEMM)
+int c1x1_mode() {
+  static const int mode = [] {
+    const char* e = getenv("RRAM_C1X1");
+    return e ? atoi(e) : 1;
+  }();
+  return mode;
+}
 struct C1Plan {
   int MI, NB, WR, VEC, tiles_m, tiles_n;
 };
 // (MI, NB, WR) instantiated for VEC = 4 and VEC = 1
 #define RRAM_C1X1_LIST(X) X(1, 2, 1) X(2, 1, 1) X(2, 2, 1) X(2, 1, 2) X(4, 1, 1) X(4, 2, 1) X(4, 1, 2) X(4, 2, 2)
 bool conv_1x1_plan(const rram_conv_desc* d, const float* x, C1Plan& pl) {
-  static const int enabled = [] {
-    const char* e = getenv("RRAM_C1X1");  // 0: the fp32-MFMA table-gather GEMM instead (A/B runs)
-    return e ? atoi(e) : 1;
-  }();
-  if (!enabled) return false;
+  if (!c1x1_mode()) return false;
   if (d->kernel_h != 1 || d->kernel_w != 1 || d->stride_h != 1 || d->stride_w != 1 || d->pad_h != 0 ||
       d->pad_w != 0 || d->dilation_h != 1 || d->dilation_w != 1 || d->group != 1)
     return false;
@@ -2215,12 +2362,23 @@ int conv_1x1_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, con
   const auto* wp = reinterpret_cast<const x6::bf16x8*>(wbuf);
   const uint32_t xrange = static_cast<uint32_t>((int64_t)d->num * C * HW * 4);
   const unsigned nwg = static_cast<unsigned>((int64_t)pl.tiles_m * pl.tiles_n);
-#define RRAM_X(mi, nb, wr)                                                                                 \
-  if (pl.MI == mi && pl.NB == nb && pl.WR == wr) {                                                         \
-    if (pl.VEC == 4)                                                                                       \
-      hipLaunchKernelGGL((k_conv1x1_x6<mi, nb, wr, 4>), dim3(nwg), dim3(256), 0, s, P, wp, x, xrange);     \
-    else                                                                                                   \
-      hipLaunchKernelGGL((k_conv1x1_x6<mi, nb, wr, 1>), dim3(nwg), dim3(256), 0, s, P, wp, x, xrange);     \
+  const uint32_t wrange = static_cast<uint32_t>(wfrags * 3072);
+  // the DMA form measured faster where the weight panel is tall (M > 64: 4-18 %
+  // per layer), the register ring on 16-byte loads with M <= 64 and on the
+  // 4-byte loads of the 7 x 7 layers (profiles/r04_ab_conv1x1.txt)
+  const bool dma = c1x1_mode() == 3 || (c1x1_mode() == 1 && pl.VEC == 4 && M > 64);
+#define RRAM_X(mi, nb, wr)                                                                                  \
+  if (pl.MI == mi && pl.NB == nb && pl.WR == wr) {                                                          \
+    if (dma && pl.VEC == 4)                                                                                 \
+      hipLaunchKernelGGL((k_conv1x1_dma_x6<mi, nb, wr, 4>), dim3(nwg), dim3(256), 0, s, P, wp, x, xrange,   \
+                         wrange);                                                                           \
+    else if (dma)                                                                                           \
+      hipLaunchKernelGGL((k_conv1x1_dma_x6<mi, nb, wr, 1>), dim3(nwg), dim3(256), 0, s, P, wp, x, xrange,   \
+                         wrange);                                                                           \
+    else if (pl.VEC == 4)                                                                                   \
+      hipLaunchKernelGGL((k_conv1x1_x6<mi, nb, wr, 4>), dim3(nwg), dim3(256), 0, s, P, wp, x, xrange);      \
+    else                                                                                                    \
+      hipLaunchKernelGGL((k_conv1x1_x6<mi, nb, wr, 1>), dim3(nwg), dim3(256), 0, s, P, wp, x, xrange);      \
   } else
   RRAM_C1X1_LIST(RRAM_X) { return 0; }
 #undef RRAM_X
