@@ -965,6 +965,49 @@ __global__ void __launch_bounds__(256) k_pack_octets_x6(const float* __restrict_
   }
 }
 
+// The output's channel-octet companion from a 32x32-accumulator epilogue
+// (k_pack_octets_x6 layout, the next convolution's pre-split input): the split
+// of the stored values (bias and ReLU applied; conv_epilogue_nchw left the
+// pre-ReLU values in acc).  Row block i of the wave: lane (lr, h) holds
+// channels 8 k + 4 h .. + 3 of octets k = 0..3 of its 32 rows; the two lane
+// halves trade halves (lane ^ 32) so half 0 owns octets 0, 1 and half 1
+// octets 2, 3, whole (k_conv_cb_x6's epilogue, per row block).
+template <int MI, int NB>
+__device__ __forceinline__ void octet_epilogue(floatx16 (&acc)[MI][NB], const Params& P, const Epi& ep, int mwave,
+                                               int nwave, int lr, int lh, char* __restrict__ yoct, int cout8) {
+  const int HW = static_cast<int>(ep.hw.d);
+  const bool relu = ep.relu != 0;
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int mw = mwave + 32 * i;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int n = nwave + 32 * j + lr;
+      float o[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[r] = relu ? fmaxf(acc[i][j][r], 0.0f) : acc[i][j][r];
+      float rcv[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) rcv[r] = __shfl_xor(lh ? o[r] : o[8 + r], 32);
+      if (n >= P.N) continue;
+      const uint32_t im = fdiv(static_cast<uint32_t>(n), ep.hw);
+      const int sp = n - static_cast<int>(im) * HW;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int k = 2 * lh + u;
+        if (mw + 8 * k >= P.M) continue;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = lh ? rcv[4 * u + e] : o[4 * u + e];
+          v[4 + e] = lh ? o[8 + 4 * u + e] : rcv[4 * u + e];
+        }
+        x6::store_terms8(v, yoct + (((int64_t)im * cout8 + mw / 8 + k) * HW + sp) * 48);
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // k_conv1x1_x6: the 1 x 1, stride-1, pad-free convolution (GoogLeNet's
 // inception 1x1 / 3x3_reduce / 5x5_reduce / pool_proj layers,
@@ -988,7 +1031,8 @@ constexpr int RING = 4;  // K-tiles loaded ahead (registers); a multiple of 2
 }  // namespace c1x1
 template <int MI, int NB, int WR, int VEC>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, MI * NB <= 4 ? 2 : 1)))
-k_conv1x1_x6(Params P, const x6::bf16x8* __restrict__ wpack, const float* __restrict__ x, uint32_t xrange) {
+k_conv1x1_x6(Params P, const x6::bf16x8* __restrict__ wpack, const float* __restrict__ x, uint32_t xrange,
+             char* __restrict__ yoct, int cout8) {
   using namespace g2;
   constexpr int WC = 4 / WR, BMc = 32 * MI * WR, BNc = 32 * NB * WC;
   constexpr int STG = 16 * BNc;           // floats per LDS stage
@@ -1109,6 +1153,7 @@ k_conv1x1_x6(Params P, const x6::bf16x8* __restrict__ wpack, const float* __rest
     static_for<0, RING>([&](auto ph) { step(kt + decltype(ph)::value, ph); });
   Epi ep = P.e;
   conv_epilogue_nchw<MI, NB>(acc, P, ep, m0 + 32 * MI * wr, n0 + 32 * NB * wc, lr, lh);
+  if (yoct != nullptr) octet_epilogue<MI, NB>(acc, P, ep, m0 + 32 * MI * wr, n0 + 32 * NB * wc, lr, lh, yoct, cout8);
 }
 
 // k_conv1x1_dma_x6: the same contraction with every operand LDS-DMA'd
@@ -1125,7 +1170,7 @@ constexpr int NS = 4;  // LDS stages
 template <int MI, int NB, int WR, int VEC>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 k_conv1x1_dma_x6(Params P, const x6::bf16x8* __restrict__ wpack, const float* __restrict__ x, uint32_t xrange,
-                 uint32_t wrange) {
+                 uint32_t wrange, char* __restrict__ yoct, int cout8) {
   using namespace g2;
   constexpr int WC = 4 / WR, BMc = 32 * MI * WR, BNc = 32 * NB * WC, RBL = BMc / 32;
   constexpr int NS = c1x1::NS;
@@ -1247,6 +1292,7 @@ k_conv1x1_dma_x6(Params P, const x6::bf16x8* __restrict__ wpack, const float* __
   }
   Epi ep = P.e;
   conv_epilogue_nchw<MI, NB>(acc, P, ep, m0 + 32 * MI * wr, n0 + 32 * NB * wc, lr, lh);
+  if (yoct != nullptr) octet_epilogue<MI, NB>(acc, P, ep, m0 + 32 * MI * wr, n0 + 32 * NB * wc, lr, lh, yoct, cout8);
 }
 
 // w [G*M][Cg][T] -> fragments [G][tiles_m][WR][Cg/16][T][term][64 lanes][8]:
@@ -2325,8 +2371,8 @@ bool conv_1x1_plan(const rram_conv_desc* d, const float* x, C1Plan& pl) {
   return best >= 0;
 }
 
-int conv_1x1_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const float* bias, float* y, int relu,
-                    hipStream_t s, const WPack& wk) {
+int conv_1x1_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const float* bias, float* y, void* y_oct,
+                    int relu, hipStream_t s, const WPack& wk) {
   C1Plan pl;
   if (!conv_1x1_plan(d, wk.query ? nullptr : x, pl)) return 0;
   const int M = d->num_output, C = d->channels, HW = d->height * d->width;
@@ -2363,6 +2409,9 @@ int conv_1x1_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, con
   const uint32_t xrange = static_cast<uint32_t>((int64_t)d->num * C * HW * 4);
   const unsigned nwg = static_cast<unsigned>((int64_t)pl.tiles_m * pl.tiles_n);
   const uint32_t wrange = static_cast<uint32_t>(wfrags * 3072);
+  // the output's octet companion straight from the epilogue (whole octets: M % 8 == 0)
+  char* const yo = (y_oct != nullptr && M % 8 == 0) ? static_cast<char*>(y_oct) : nullptr;
+  const int cout8 = M / 8;
   // the DMA form measured faster where the weight panel is tall (M > 64: 4-18 %
   // per layer), the register ring on 16-byte loads with M <= 64 and on the
   // 4-byte loads of the 7 x 7 layers (profiles/r04_ab_conv1x1.txt)
@@ -2371,18 +2420,21 @@ int conv_1x1_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, con
   if (pl.MI == mi && pl.NB == nb && pl.WR == wr) {                                                          \
     if (dma && pl.VEC == 4)                                                                                 \
       hipLaunchKernelGGL((k_conv1x1_dma_x6<mi, nb, wr, 4>), dim3(nwg), dim3(256), 0, s, P, wp, x, xrange,   \
-                         wrange);                                                                           \
+                         wrange, yo, cout8);                                                                \
     else if (dma)                                                                                           \
       hipLaunchKernelGGL((k_conv1x1_dma_x6<mi, nb, wr, 1>), dim3(nwg), dim3(256), 0, s, P, wp, x, xrange,   \
-                         wrange);                                                                           \
+                         wrange, yo, cout8);                                                                \
     else if (pl.VEC == 4)                                                                                   \
-      hipLaunchKernelGGL((k_conv1x1_x6<mi, nb, wr, 4>), dim3(nwg), dim3(256), 0, s, P, wp, x, xrange);      \
+      hipLaunchKernelGGL((k_conv1x1_x6<mi, nb, wr, 4>), dim3(nwg), dim3(256), 0, s, P, wp, x, xrange, yo,   \
+                         cout8);                                                                            \
     else                                                                                                    \
-      hipLaunchKernelGGL((k_conv1x1_x6<mi, nb, wr, 1>), dim3(nwg), dim3(256), 0, s, P, wp, x, xrange);      \
+      hipLaunchKernelGGL((k_conv1x1_x6<mi, nb, wr, 1>), dim3(nwg), dim3(256), 0, s, P, wp, x, xrange, yo,   \
+                         cout8);                                                                            \
   } else
   RRAM_C1X1_LIST(RRAM_X) { return 0; }
 #undef RRAM_X
-  const int rc = launch_status("conv 1x1 x6");
+  int rc = launch_status("conv 1x1 x6");
+  if (rc == 0 && y_oct != nullptr && yo == nullptr) rc = pack_octets(y, y_oct, d->num, M, HW, s);
   return rc ? rc : 1;
 }
 
@@ -2401,8 +2453,11 @@ int conv_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, cons
     const int rc = conv_cb_x6_fwd(d, x, x_oct, w, bias, y, y_oct, relu, s, wk);
     if (rc != 0) return rc;
   }
-  int rc = conv_1x1_x6_fwd(d, x, w, bias, y, relu, s, wk);
-  if (rc == 0) rc = conv_wide_x6_fwd(d, x, w, bias, y, relu, s, wk);
+  {
+    const int rc1 = conv_1x1_x6_fwd(d, x, w, bias, y, y_oct, relu, s, wk);  // writes y_oct itself
+    if (rc1 != 0) return rc1;
+  }
+  int rc = conv_wide_x6_fwd(d, x, w, bias, y, relu, s, wk);
   if (rc == 0) rc = conv_patch_x6_fwd(d, x, w, bias, y, relu, s, wk);
   if (wk.query) return rc;
   if (rc > 0 && y_oct != nullptr) {

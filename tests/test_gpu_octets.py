@@ -83,7 +83,10 @@ OCT_CASES = [
     dict(x=(3, 256, 13, 13), cout=384, k=3, p=1, g=1),
     dict(x=(3, 384, 13, 13), cout=384, k=3, p=1, g=2),
     dict(x=(3, 384, 13, 13), cout=256, k=3, p=1, g=2),
-    dict(x=(2, 32, 14, 14), cout=64, k=1, p=0, g=1),     # 1x1: im2col GEMM path
+    dict(x=(2, 32, 14, 14), cout=64, k=1, p=0, g=1),     # 1x1: register-ring kernel, companion from its epilogue
+    dict(x=(3, 192, 28, 28), cout=96, k=1, p=0, g=1),    # 1x1: LDS-DMA kernel, companion from its epilogue
+    dict(x=(2, 64, 7, 7), cout=48, k=1, p=0, g=1),       # 1x1: 4-byte loads, partial last column tile
+    dict(x=(2, 16, 9, 9), cout=40, k=1, p=0, g=1),       # 1x1: a row block with one octet of rows
     dict(x=(2, 16, 20, 20), cout=32, k=3, p=1, g=1),     # M = 32: patch / fp32 path
 ]
 
