@@ -96,6 +96,8 @@ def classify(name):
         return "conv1 k_conv1_ring_x6"
     if "lrn_maxpool" in name:
         return None  # split below by grid
+    # (k_conv_cb16_x6: the 16x16x32 form of the same kernel, round 4)
+    name = name.replace("k_conv_cb16_x6", "k_conv_cb_x6")
     if "k_conv_cb_x6ILi5ELi5" in name or "k_conv_cb_x6<5, 5" in name:
         return "conv2 k_conv_cb_x6<5,5,...>"
     if "k_conv_cb_x6ILi3ELi3ELi4ELi8" in name:
