@@ -645,6 +645,10 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
   static_assert(2 * SFB <= 160 * 1024, "LDS");
   static_assert(PP >= 2, "pair groups");
   __shared__ __attribute__((aligned(16))) char smem[2 * SFB];
+  // the patch pieces' source offsets, one word per (piece, thread): read per
+  // refill instead of held in PD registers (at two workgroups per CU the
+  // 5x5 form otherwise spills)
+  __shared__ uint32_t poff_lds[PD * 256];
   const uint32_t lds0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)smem));
 
   const int lane = threadIdx.x & 63;
@@ -684,7 +688,6 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
   const int p2 = p1 + (nseg > 1 ? seg_last(1) + KH : 0);
   const int R = p2 + (nseg > 2 ? seg_last(2) + KH : 0);
   const int PW = cv.W + 2 * cv.pw;
-  uint32_t poff[PD];
 #pragma unroll
   for (int i = 0; i < PD; ++i) {
     const int c = (wave * PD + i) * 64 + lane;
@@ -700,8 +703,10 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
         off = static_cast<uint32_t>(img0 + sg) * static_cast<uint32_t>(ximg) + static_cast<uint32_t>(h) * PL +
               static_cast<uint32_t>((y * cv.W + x) * 48 + t * 16);
     }
-    poff[i] = off;
+    poff_lds[i * 256 + threadIdx.x] = off;
   }
+  auto poff = [&](int i) { return poff_lds[i * 256 + threadIdx.x]; };
+  __syncthreads();
   // B fragment bases (bytes into a stage) of this lane's column in block j,
   // at tap 0 of its octet (g & 1)
   int bb[NJ];
@@ -723,7 +728,7 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
       for (int r = 0; r < 4; ++r) acc[i][j][r] = 0.0f;
 
   auto issue = [&](int kt, int stg, int i) {
-    dma_b128(xrsrc, poff[i] + static_cast<uint32_t>(kt) * 2u * PL,
+    dma_b128(xrsrc, poff(i) + static_cast<uint32_t>(kt) * 2u * PL,
              lds0 + static_cast<uint32_t>(stg * SFB + (wave * PD + i) * 1024));
   };
   // K order (T odd: 3x3, 5x5): K-tiles alternate even / odd.  An even K-tile
@@ -810,7 +815,7 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
           for (int i = cbx6::piece_lo(gi, PD, NG); i < cbx6::piece_lo(gi + 1, PD, NG); ++i)
             stg[gi & 1][i - cbx6::piece_lo(gi, PD, NG)] = __builtin_bit_cast(
                 int4x, __builtin_amdgcn_raw_buffer_load_b128(
-                           xr, static_cast<int>(poff[i] + static_cast<uint32_t>(kt + 1) * 2u * PL), 0, 0));
+                           xr, static_cast<int>(poff(i) + static_cast<uint32_t>(kt + 1) * 2u * PL), 0, 0));
         }
         if (gi + 1 < NG || MORE) load_a(fa[pa ^ 1], q + 1);
 #pragma unroll
