@@ -45,9 +45,19 @@ __global__ void __launch_bounds__(256) k_bias_bwd(const float* __restrict__ dy, 
   __shared__ float part[4];
   const int c = blockIdx.x;
   float s = 0.0f;
-  for (int n = 0; n < num; ++n) {
-    const float* row = dy + ((int64_t)n * C + c) * inner;
-    for (int q = threadIdx.x; q < inner; q += blockDim.x) s += row[q];
+  if (inner >= 128) {
+    for (int n = 0; n < num; ++n) {
+      const float* row = dy + ((int64_t)n * C + c) * inner;
+      for (int q = threadIdx.x; q < inner; q += blockDim.x) s += row[q];
+    }
+  } else {
+    // short rows (InnerProduct: inner = 1): the threads walk (n, q) jointly so
+    // every thread has work instead of `inner` of them walking all n
+    const int total = num * inner;
+    for (int t = threadIdx.x; t < total; t += blockDim.x) {
+      const int n = t / inner, q = t - n * inner;
+      s += dy[((int64_t)n * C + c) * inner + q];
+    }
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
@@ -75,13 +85,43 @@ __global__ void __launch_bounds__(256) k_bias_bwd_part(const float* __restrict__
   __syncthreads();
   if (threadIdx.x == 0) part[(int64_t)c * gridDim.y + j] = red[0] + red[1] + red[2] + red[3];
 }
-__global__ void __launch_bounds__(256) k_bias_bwd_reduce(const float* __restrict__ part, float* __restrict__ db,
-                                                         int C, int S) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// one wave per channel: lane l sums partials l, l + 64, ...; fixed xor tree
+__global__ void __launch_bounds__(64) k_bias_bwd_reduce(const float* __restrict__ part, float* __restrict__ db,
+                                                        int C, int S) {
+  const int c = blockIdx.x;
   float s = 0.0f;
-  for (int j = 0; j < S; ++j) s += part[(int64_t)c * S + j];
-  db[c] += s;
+  for (int j = threadIdx.x; j < S; j += 64) s += part[(int64_t)c * S + j];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (threadIdx.x == 0) db[c] += s;
+}
+
+// wt[g*cin_g + c][co][tap] = w[g*cout_g + co][c][T-1-tap]: each group's kernel
+// transposed (in <-> out channels) and rotated 180 degrees (taps reversed), the
+// weights of the stride-1 data gradient as a forward convolution
+__global__ void __launch_bounds__(256) k_flip_kernel(const float* __restrict__ w, float* __restrict__ wt,
+                                                     int G, int cin_g, int cout_g, int T) {
+  const int total = G * cin_g * cout_g * T;  // < 2^31 (checked by the caller)
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    int t = i;
+    const int tap = t % T;
+    t /= T;
+    const int co = t % cout_g;
+    t /= cout_g;
+    const int c = t % cin_g;
+    const int g = t / cin_g;
+    wt[i] = w[((g * cout_g + co) * cin_g + c) * T + (T - 1 - tap)];
+  }
+}
+
+// RRAM_DX_FWD (A/B runs): 1 = stride-1 data gradients as a forward convolution
+// of dY with the flipped kernel (default), 0 = always data GEMM + col2im
+bool dx_fwd_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("RRAM_DX_FWD");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return on;
 }
 
 int check_desc(const rram_conv_desc* d) {
@@ -280,7 +320,7 @@ int rram_conv2d_bwd(const rram_conv_desc* d_in, const float* x, const float* w, 
       const int Sx = (d.num + per - 1) / per;
       hipLaunchKernelGGL(k_bias_bwd_part, dim3(d.num_output, Sx), dim3(256), 0, s, dy, part, d.num, d.num_output,
                          HoWo, per);
-      hipLaunchKernelGGL(k_bias_bwd_reduce, dim3((d.num_output + 255) / 256), dim3(256), 0, s, part, db,
+      hipLaunchKernelGGL(k_bias_bwd_reduce, dim3(d.num_output), dim3(64), 0, s, part, db,
                          d.num_output, Sx);
     } else {
       hipLaunchKernelGGL(k_bias_bwd, dim3(d.num_output), dim3(256), 0, s, dy, db, d.num, d.num_output, HoWo);
@@ -290,6 +330,39 @@ int rram_conv2d_bwd(const rram_conv_desc* d_in, const float* x, const float* w, 
   }
   if (!dw && !dx) return RRAM_OK;
   RRAM_REQUIRE(x && w, "conv2d_bwd: x/w NULL");
+  // Stride 1: dX = dY (*) rot180(W^T), a forward convolution with padding
+  // dil*(k-1) - pad (>= 0 needed), so no column matrix is written and
+  // gathered back (conv_layer.cu:47-52's data GEMM + col2im); the flipped
+  // kernel lives in the workspace head after the weight-gradient passes
+  const int G = d.group, cin_g = d.channels / G, cout_g = d.num_output / G;
+  const int T = d.kernel_h * d.kernel_w;
+  const int eph = d.dilation_h * (d.kernel_h - 1) - d.pad_h, epw = d.dilation_w * (d.kernel_w - 1) - d.pad_w;
+  const size_t wt_bytes = (size_t)d.channels * cout_g * T * sizeof(float);
+  // The forward's grid must fill the chip: below ~128 tiles of 32 channels x
+  // 128 positions (CIFAR conv3 100x32x8x8, LeNet conv2 64x20x12x12: 50 / 72)
+  // each workgroup walks a long K = cout*k*k alone and the GEMM + col2im pair
+  // is 1.4-1.6x faster (scripts/dx_ab.py, profiles/r04_ab_dx_fwd.txt)
+  const int64_t dx_tiles = (int64_t)G * ((cin_g + 31) / 32) * (((int64_t)d.num * d.height * d.width + 127) / 128);
+  const bool dx_fwd = dx && dx_fwd_enabled() && dx_tiles >= 128 && d.stride_h == 1 && d.stride_w == 1 &&
+                      eph >= 0 && epw >= 0 &&
+                      ws != nullptr && ws_bytes >= wt_bytes && wt_bytes < (1ull << 31) &&
+                      (int64_t)d.num * d.height * d.width < (1ll << 31) &&
+                      (int64_t)d.num * d.num_output * HoWo * 4 < (1ll << 31);
+  auto dx_as_fwd = [&]() -> int {
+    float* wt = static_cast<float*>(ws);
+    const int64_t n = (int64_t)d.channels * cout_g * T;
+    hipLaunchKernelGGL(k_flip_kernel, dim3(stream_blocks(n)), dim3(256), 0, s, w, wt, G, cin_g, cout_g, T);
+    int r = launch_status("conv bwd kernel flip");
+    if (r) return r;
+    rram_conv_desc t{d.num, d.num_output, d.out_h, d.out_w, d.channels, d.kernel_h, d.kernel_w,
+                     eph, epw, 1, 1, d.dilation_h, d.dilation_w, G, 0, 0};
+    r = rram_conv_out_shape(&t);
+    if (r) return r;
+    RRAM_REQUIRE(t.out_h == d.height && t.out_w == d.width, "conv2d_bwd: flipped-kernel output %dx%d != input %dx%d",
+                 t.out_h, t.out_w, d.height, d.width);
+    return conv_fwd_core(&t, dy, wt, nullptr, dx, 0, s);
+  };
+  if (dx_fwd && !dw) return dx_as_fwd();
   const size_t per_img = col_bytes(d, 1);
   RRAM_REQUIRE(ws != nullptr && ws_bytes >= per_img, "conv2d_bwd: workspace needs >= %zu bytes",
                per_img);
@@ -316,14 +389,14 @@ int rram_conv2d_bwd(const rram_conv_desc* d_in, const float* x, const float* w, 
       rc = conv_bwd_weight_core(&d, nimg, dy + n0 * ohw, col, ldcol, dw, part, part ? part_bytes : 0, s);
       if (rc) return rc;
     }
-    if (dx) {
+    if (dx && !dx_fwd) {
       rc = conv_bwd_data_col_core(&d, nimg, w, dy + n0 * ohw, col, ldcol, s);
       if (rc) return rc;
       rc = col2im_core(col, ldcol, nimg, &d, dx + n0 * chw, chw, 0, s);
       if (rc) return rc;
     }
   }
-  return RRAM_OK;
+  return dx_fwd ? dx_as_fwd() : RRAM_OK;
 }
 
 int rram_im2col(const float* im, int C, int H, int W, int kh, int kw, int ph, int pw, int sh,

@@ -1220,6 +1220,41 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// im2col, four consecutive output positions per thread and one 16-byte store
+// (HoWo % 4 == 0, ldcol % 4 == 0, col 16-byte aligned: a quad never spans two
+// images; it may wrap output rows when Wo % 4 != 0)
+__global__ void __launch_bounds__(256)
+    k_im2col4(const float* __restrict__ im, int64_t im_img, int nimg, int C, int H, int W, int KH,
+              int KW, int ph, int pw, int sh, int sw, int dh, int dw, int Ho, int Wo,
+              float* __restrict__ col, int64_t ldcol, FastDiv howo, FastDiv wo_div) {
+  const int krow = blockIdx.y;
+  const int kw = krow % KW, kh = (krow / KW) % KH, c = krow / (KW * KH);
+  const int P4 = nimg * Ho * Wo / 4;
+  float4* dst = reinterpret_cast<float4*>(col + (int64_t)krow * ldcol);
+  const float* src = im + (int64_t)c * H * W;
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < P4; q += gridDim.x * blockDim.x) {
+    const uint32_t p = 4u * static_cast<uint32_t>(q);
+    const uint32_t n = fdiv(p, howo);
+    const uint32_t r = p - n * howo.d;
+    int ho = static_cast<int>(fdiv(r, wo_div));
+    int wo = static_cast<int>(r) - ho * Wo;
+    const float* img = src + n * im_img;
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int iy = ho * sh - ph + kh * dh;
+      const int ix = wo * sw - pw + kw * dw;
+      const bool ok = static_cast<unsigned>(iy) < static_cast<unsigned>(H) && static_cast<unsigned>(ix) < static_cast<unsigned>(W);
+      v[j] = ok ? img[iy * W + ix] : 0.0f;
+      if (++wo == Wo) {
+        wo = 0;
+        ++ho;
+      }
+    }
+    dst[q] = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
 // col2im: one thread per image pixel, gathers all column entries that map to it
 __global__ void __launch_bounds__(256)
     k_col2im(const float* __restrict__ col, int64_t ldcol, int nimg, int C, int H, int W, int KH,
@@ -1805,6 +1840,14 @@ int im2col_core(const float* im, int64_t im_img, int nimg, const rram_conv_desc*
   const int64_t P = (int64_t)nimg * d->out_h * d->out_w;
   RRAM_REQUIRE(P < (1ll << 31) && (int64_t)nimg * im_img < (1ll << 31) && rows < 65536,
                "im2col: more than 2^31 positions / input elements or 65535 rows is not supported");
+  if ((d->out_h * d->out_w) % 4 == 0 && ldcol % 4 == 0 && (reinterpret_cast<uintptr_t>(col) & 15u) == 0) {
+    const int gx4 = static_cast<int>(std::min<int64_t>((P / 4 + 255) / 256, 64));
+    hipLaunchKernelGGL(k_im2col4, dim3(gx4, rows), dim3(256), 0, s, im, im_img, nimg,
+                       d->channels, d->height, d->width, d->kernel_h, d->kernel_w, d->pad_h,
+                       d->pad_w, d->stride_h, d->stride_w, d->dilation_h, d->dilation_w, d->out_h,
+                       d->out_w, col, ldcol, make_fastdiv(d->out_h * d->out_w), make_fastdiv(d->out_w));
+    return launch_status("im2col");
+  }
   const int gx = static_cast<int>(std::min<int64_t>((P + 255) / 256, 64));
   hipLaunchKernelGGL(k_im2col, dim3(gx, rows), dim3(256), 0, s, im, im_img, nimg,
                      d->channels, d->height, d->width, d->kernel_h, d->kernel_w, d->pad_h,

@@ -301,9 +301,10 @@ void ConvolutionLayer<Dtype>::Backward_gpu(const std::vector<Blob<Dtype>*>& top,
   const bool dx = pd.size() > 0 && pd[0];
   if (!dw && !db && !dx) return;
   const size_t need = rram_conv2d_bwd_workspace(&desc_, 1);
-  // chunk up to 64 images per col buffer (bounded at 1 GiB), plus the
-  // weight-gradient split-K partials
-  int imgs = std::max(1, std::min(desc_.num, (int)std::min<size_t>(64, (1ull << 30) / std::max<size_t>(need, 1))));
+  // chunk up to 256 images per col buffer (bounded at 1 GiB), plus the
+  // weight-gradient split-K partials (64 before round 4: CIFAR conv2 at b100
+  // then ran two im2col + weight-GEMM + split-K passes instead of one)
+  int imgs = std::max(1, std::min(desc_.num, (int)std::min<size_t>(256, (1ull << 30) / std::max<size_t>(need, 1))));
   void* ws = Caffe::workspace(rram_conv2d_bwd_workspace(&desc_, imgs) + 256);
   RRAM_CALL(rram_conv2d_bwd(&desc_, bottom[0]->gpu_data(), this->blobs_[0]->gpu_data(),
                             top[0]->gpu_diff(), dw ? this->blobs_[0]->mutable_gpu_diff() : nullptr,

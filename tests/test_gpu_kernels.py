@@ -598,6 +598,71 @@ def test_conv_bwd_vs_fp64(device, cs):
         R.assert_scaled(got.cpu().numpy(), ref, sc, nm)
 
 
+DX_FWD_CASES = [  # fwd: the flipped-kernel forward runs (>= 128 tiles of 32 channels x 128 positions)
+    dict(x=(64, 32, 16, 16), cout=32, k=5, s=1, p=2, d=1, g=1, fwd=True),     # CIFAR conv2
+    dict(x=(6, 96, 27, 27), cout=256, k=5, s=1, p=2, d=1, g=2, fwd=True),     # AlexNet conv2, groups
+    dict(x=(8, 384, 13, 13), cout=384, k=3, s=1, p=1, d=1, g=2, fwd=True),    # conv4
+    dict(x=(6, 480, 14, 14), cout=64, k=1, s=1, p=0, d=1, g=1, fwd=True),     # GoogLeNet 1x1
+    dict(x=(40, 5, 19, 23), cout=8, k=9, s=1, p=4, d=1, g=1, fwd=True),       # 81 taps
+    dict(x=(58, 4, 13, 11), cout=6, k=3, s=1, p=2, d=2, g=2, fwd=True),       # dilation + groups + padding
+    dict(x=(300, 3, 8, 7), cout=4, k=3, s=1, p=0, d=2, g=1, fwd=True),        # flipped padding 4 > kernel
+    dict(x=(230, 3, 9, 8), cout=5, k=(3, 1), s=1, p=(1, 0), d=1, g=1, fwd=True),  # non-square kernel
+    dict(x=(4, 32, 8, 8), cout=64, k=5, s=1, p=2, d=1, g=1, fwd=False),       # small grid: GEMM + col2im
+    dict(x=(2, 3, 6, 6), cout=4, k=3, s=1, p=3, d=1, g=1, fwd=False),         # pad > k-1: GEMM + col2im
+]
+
+
+@pytest.mark.parametrize("eng", ["f32", "bf16x6"])
+@pytest.mark.parametrize("cs", DX_FWD_CASES)
+def test_conv_bwd_dx_stride1_vs_fp64(device, cs, eng):
+    """Stride-1 data gradient as a forward convolution of dY with the flipped,
+    channel-transposed kernel (padding dil*(k-1) - pad) instead of the data GEMM
+    + col2im (conv_layer.cu:47-52), on both fp32 engines, with and without the
+    weight gradient in the same call.  Which path ran is observable: with dX
+    alone the forward needs only the flipped kernel's bytes of workspace, the
+    col2im path one image's column matrix."""
+    import torch
+    from rramsim import ops
+    from rramsim import _kernels as Kmod
+    kh, kw = cs["k"] if isinstance(cs["k"], tuple) else (cs["k"], cs["k"])
+    ph, pw = cs["p"] if isinstance(cs["p"], tuple) else (cs["p"], cs["p"])
+    torch.manual_seed(3)
+    x = torch.randn(cs["x"], dtype=torch.float32)
+    w = torch.randn(cs["cout"], cs["x"][1] // cs["g"], kh, kw) * 0.1
+    b = torch.randn(cs["cout"])
+    fwd = lambda xx, ww, bb: torch.nn.functional.conv2d(xx, ww, bb, 1, (ph, pw), cs["d"], cs["g"])  # noqa: E731
+    dy = torch.randn_like(fwd(x, w, b))
+    (gx, gw, gb), (sx, sw, sb) = _bwd_ref64(fwd, (x, w, b), dy)
+    d = ops.conv_desc(cs["x"], cs["cout"], (kh, kw), 1, (ph, pw), cs["d"], cs["g"])
+    import _ref64 as R
+    wt_floats = w.numel()
+    col_floats = cs["x"][1] * kh * kw * d.out_h * d.out_w
+    xd, wd, dyd = x.to(device), w.to(device), dy.to(device)
+    prev = ops.set_f32_engine(ops.ENGINE_F32 if eng == "f32" else ops.ENGINE_BF16X6)
+    try:
+        if wt_floats < col_floats:
+            small = torch.empty(wt_floats, device=device)
+            dx = torch.full_like(x, float("nan"), device=device)
+            if cs["fwd"]:
+                ops.conv2d_bwd(d, xd, wd, dyd, None, None, dx, small)
+                torch.cuda.synchronize()
+                R.assert_scaled(dx.cpu().numpy(), gx, sx, "dX (flipped-kernel forward)")
+            else:
+                with pytest.raises(Kmod.RramError):
+                    ops.conv2d_bwd(d, xd, wd, dyd, None, None, dx, small)
+        for with_dw in (False, True):
+            dw = torch.zeros_like(w, device=device) if with_dw else None
+            dx = torch.full_like(x, float("nan"), device=device)
+            ws = torch.empty(ops.conv2d_bwd_workspace(d, cs["x"][0]) // 4 + 1, device=device)
+            ops.conv2d_bwd(d, xd, wd, dyd, dw, None, dx, ws)
+            torch.cuda.synchronize()
+            R.assert_scaled(dx.cpu().numpy(), gx, sx, "dX")
+            if with_dw:
+                R.assert_scaled(dw.cpu().numpy(), gw, sw, "dW")
+    finally:
+        ops.set_f32_engine(prev)
+
+
 def test_ip_bwd_vs_fp64(device):
     """InnerProduct backward (inner_product_layer.cu:40-75) at LeNet ip1 and
     AlexNet fc6 shapes within 1e-4 of Σ|a·b| of a float64 reference."""
@@ -693,3 +758,34 @@ def test_pool_lrn_softmax_accuracy_vs_oracle(device, oracle_mod):
     for k in (1, 5):
         ops.accuracy(T(logits, device), T(label, device), cor, cnt, 256, 1000, 1, top_k=k)
         assert int(N(cor)[0]) == oracle_mod.accuracy(logits, label, k) and int(N(cnt)[0]) == 256
+
+
+IM2COL_CASES = [  # (C, H, W, kh, kw, ph, pw, sh, sw, dh, dw)
+    (3, 32, 32, 5, 5, 2, 2, 1, 1, 1, 1),     # CIFAR conv1: Ho*Wo % 4 == 0 (16-byte stores)
+    (32, 8, 8, 5, 5, 2, 2, 1, 1, 1, 1),      # CIFAR conv3
+    (3, 227, 227, 11, 11, 0, 0, 4, 4, 1, 1), # AlexNet conv1: 55 x 55 (scalar form)
+    (5, 9, 6, 3, 3, 1, 1, 1, 1, 1, 1),       # Wo = 6: quads wrap output rows
+    (4, 5, 2, 3, 1, 1, 0, 1, 1, 1, 1),       # Wo = 2: a quad spans two rows
+    (2, 11, 13, 3, 3, 2, 1, 2, 1, 2, 1),     # stride + dilation + padding
+    (1, 1, 1, 1, 1, 0, 0, 1, 1, 1, 1),       # 1 x 1
+]
+
+
+@pytest.mark.parametrize("cs", IM2COL_CASES)
+def test_im2col_col2im_bit_exact(device, oracle_mod, cs):
+    """im2col (im2col.cu:9-36; the 4-position 16-byte-store form when Ho*Wo %
+    4 == 0) bit-exact against the oracle; col2im (im2col.cu:65-116) against the
+    oracle's accumulation within fp32 summation-order tolerance."""
+    import torch
+    from rramsim import ops
+    C_, H, W, kh, kw, ph, pw, sh, sw, dh, dw = cs
+    rng = np.random.default_rng(sum(cs))
+    im = rng.standard_normal((C_, H, W)).astype(np.float32)
+    ref = oracle_mod.im2col(im, kh, kw, ph, pw, sh, sw, dh, dw)
+    col = torch.full(ref.shape, float("nan"), device=device)
+    ops.im2col(T(im, device), C_, H, W, kh, kw, ph, pw, sh, sw, dh, dw, col)
+    assert bits_equal(N(col), ref)
+    back = torch.empty((C_, H, W), device=device)
+    ops.col2im(T(ref, device), C_, H, W, kh, kw, ph, pw, sh, sw, dh, dw, back)
+    np.testing.assert_allclose(N(back), oracle_mod.col2im(ref, C_, H, W, kh, kw, ph, pw, sh, sw, dh, dw),
+                               rtol=1e-6, atol=1e-5)
