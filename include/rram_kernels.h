@@ -222,6 +222,26 @@ int rram_fused_update_fail(float* w, float* g, float* h, float* endurance,
                            unsigned long long* broken_count,
                            rram_stream_t stream);
 
+/* The same fused tail for every learnable blob of a net in ONE launch (the
+ * solver's per-iteration tail, sgd_solver.cpp:101-116 + solver.cpp:300-305,
+ * was one launch per blob).  Per segment: the arguments of
+ * rram_fused_update_fail; momentum, decrement and eps are solver-wide.
+ * Element-wise identical arithmetic, so bit-identical to nsegs calls of
+ * rram_fused_update_fail; broken_count may repeat across segments. */
+typedef struct rram_update_seg {
+  float* w;
+  float* g;
+  float* h;
+  float* endurance;     /* NULL for a non-faultable blob */
+  const float* values;  /* NULL iff endurance is NULL */
+  int64_t n;
+  float decay, local_rate, thr;
+  int apply_thr;
+  unsigned long long* broken_count; /* may be NULL */
+} rram_update_seg;
+int rram_fused_update_fail_batched(const rram_update_seg* segs, int nsegs, float momentum,
+                                   float decrement, float eps, rram_stream_t stream);
+
 /* Level-1 helpers used by Blob::Update, Regularize, P2PSync-equivalent
  * scaling (src/caffe/util/math_functions.cu:45-207). */
 int rram_axpy(int64_t n, float alpha, const float* x, float* y, rram_stream_t stream);

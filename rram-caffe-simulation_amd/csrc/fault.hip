@@ -488,6 +488,61 @@ __global__ void __launch_bounds__(256)
   wave_count_add_n(cnt, counter);
 }
 
+// k_fused_update_fail over all of a net's learnable blobs: block-chunks of
+// kUpdChunk elements dealt across the segments (as k_fail_apply_batched), the
+// per-element arithmetic k_fused_update_fail's
+struct UpdateSegs {
+  rram_update_seg s[RRAM_MAX_SEGS];
+  int64_t chunk_start[RRAM_MAX_SEGS + 1];
+  int nsegs;
+};
+constexpr int kUpdChunk = 256 * 8;
+
+__global__ void __launch_bounds__(256)
+    k_fused_update_fail_batched(UpdateSegs segs, float mom, float dec, float eps) {
+#pragma clang fp contract(off)
+  const int64_t total = segs.chunk_start[segs.nsegs];
+  int cur = -1;  // block-uniform: flush the count once per segment visited
+  unsigned cnt = 0;
+  for (int64_t c = blockIdx.x; c < total; c += gridDim.x) {
+    int s = 0;
+    while (c >= segs.chunk_start[s + 1]) ++s;
+    if (s != cur) {
+      if (cur >= 0) block_count_flush(cnt, segs.s[cur].broken_count);
+      cnt = 0;
+      cur = s;
+    }
+    const rram_update_seg& sg = segs.s[s];
+    const int64_t begin = (c - segs.chunk_start[s]) * kUpdChunk;
+    const int64_t end = min(begin + (int64_t)kUpdChunk, sg.n);
+    float* __restrict__ w = sg.w;
+    float* __restrict__ g = sg.g;
+    float* __restrict__ h = sg.h;
+    float* __restrict__ e = sg.endurance;
+    const float* __restrict__ v = sg.values;
+    for (int64_t i = begin + threadIdx.x; i < end; i += blockDim.x) {
+      float wi = w[i];
+      float gi = g[i];
+      if (sg.decay != 0.0f) gi = sg.decay * wi + gi;
+      gi = mom * h[i] + sg.local_rate * gi;
+      h[i] = gi;
+      if (sg.apply_thr && fabsf(gi) <= sg.thr) gi = 0.0f;
+      g[i] = gi;
+      wi = wi - gi;
+      if (e != nullptr) {
+        float ee = e[i];
+        bool wr;
+        float wv;
+        cnt += fail_one(gi, wv, ee, v[i], dec, eps, wr);
+        e[i] = ee;
+        if (wr) wi = wv;
+      }
+      w[i] = wi;
+    }
+  }
+  if (cur >= 0) block_count_flush(cnt, segs.s[cur].broken_count);
+}
+
 // ---------------------------------------------------------------------------
 // level-1 helpers
 // ---------------------------------------------------------------------------
@@ -875,6 +930,30 @@ int rram_fused_update_fail(float* w, float* g, float* h, float* e, const float* 
   hipLaunchKernelGGL(k_fused_update_fail, dim3(stream_blocks(n)), dim3(kThreads), 0, as_stream(s),
                      w, g, h, e, v, n, decay, mom, lr, apply_thr, thr, dec, eps, counter);
   return launch_status("fused_update_fail");
+}
+
+int rram_fused_update_fail_batched(const rram_update_seg* segs, int nsegs, float mom, float dec, float eps,
+                                   rram_stream_t s) {
+  using namespace rram;
+  RRAM_REQUIRE(nsegs >= 0 && nsegs <= RRAM_MAX_SEGS, "fused_update_fail_batched: nsegs out of range");
+  if (nsegs == 0) return RRAM_OK;
+  RRAM_REQUIRE(segs, "fused_update_fail_batched: segs is NULL");
+  UpdateSegs us{};
+  us.nsegs = nsegs;
+  for (int i = 0; i < nsegs; ++i) {
+    const rram_update_seg& sg = segs[i];
+    RRAM_REQUIRE(sg.n >= 0, "fused_update_fail_batched: segment %d n < 0", i);
+    if (sg.n > 0) RRAM_REQUIRE(sg.w && sg.g && sg.h, "fused_update_fail_batched: segment %d NULL pointer", i);
+    RRAM_REQUIRE((sg.endurance == nullptr) == (sg.values == nullptr),
+                 "fused_update_fail_batched: segment %d endurance/values mismatch", i);
+    us.s[i] = sg;
+    us.chunk_start[i + 1] = us.chunk_start[i] + (sg.n + kUpdChunk - 1) / kUpdChunk;
+  }
+  const int64_t total = us.chunk_start[nsegs];
+  if (total == 0) return RRAM_OK;
+  const int grid = static_cast<int>(total < 2048 ? total : 2048);
+  hipLaunchKernelGGL(k_fused_update_fail_batched, dim3(grid), dim3(kThreads), 0, as_stream(s), us, mom, dec, eps);
+  return launch_status("fused_update_fail_batched");
 }
 
 int rram_axpy(int64_t n, float a, const float* x, float* y, rram_stream_t s) {

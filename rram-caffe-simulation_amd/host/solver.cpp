@@ -365,18 +365,31 @@ void Solver<Dtype>::FusedTail() {
   unsigned long long* counts = fmaker_ ? fmaker_->device_counts() : nullptr;
   if (counts)
     HIP_CALL(hipMemsetAsync(counts, 0, fi.size() * sizeof(unsigned long long), Caffe::hip_stream()));
+  // one launch for all blobs (rram_fused_update_fail_batched; a net with more
+  // learnable blobs than one launch takes goes one launch per RRAM_MAX_SEGS)
+  std::vector<rram_update_seg> segs;
   for (int i = 0; i < (int)ps.size(); ++i) {
     int f = -1;
     for (int k = 0; k < (int)fids.size(); ++k)
       if (fids[k] == i) f = k;
     const bool faulty = gm && f >= 0;
-    RRAM_CALL(rram_fused_update_fail(
-        ps[i]->mutable_gpu_data(), ps[i]->mutable_gpu_diff(), history_[i]->mutable_gpu_data(),
-        faulty ? fi[f]->mutable_gpu_data() : nullptr, faulty ? fi[f]->gpu_diff() : nullptr, ps[i]->count(),
-        wd * net_->params_weight_decay()[i], mom, rate * net_->params_lr()[i], (faulty && thr) ? 1 : 0,
-        (faulty && thr) ? thr->threshold_for(f) : 0.0f, gm ? gm->decrement : 100.0f, gm ? gm->epsilon : 1e-20f,
-        (faulty && counts) ? counts + f : nullptr, Caffe::stream()));
+    rram_update_seg sg{};
+    sg.w = ps[i]->mutable_gpu_data();
+    sg.g = ps[i]->mutable_gpu_diff();
+    sg.h = history_[i]->mutable_gpu_data();
+    sg.endurance = faulty ? fi[f]->mutable_gpu_data() : nullptr;
+    sg.values = faulty ? fi[f]->gpu_diff() : nullptr;
+    sg.n = ps[i]->count();
+    sg.decay = wd * net_->params_weight_decay()[i];
+    sg.local_rate = rate * net_->params_lr()[i];
+    sg.apply_thr = (faulty && thr) ? 1 : 0;
+    sg.thr = (faulty && thr) ? thr->threshold_for(f) : 0.0f;
+    sg.broken_count = (faulty && counts) ? counts + f : nullptr;
+    segs.push_back(sg);
   }
+  for (size_t b = 0; b < segs.size(); b += RRAM_MAX_SEGS)
+    RRAM_CALL(rram_fused_update_fail_batched(segs.data() + b, (int)std::min<size_t>(RRAM_MAX_SEGS, segs.size() - b), mom,
+                                             gm ? gm->decrement : 100.0f, gm ? gm->epsilon : 1e-20f, Caffe::stream()));
 }
 
 template <typename Dtype>

@@ -51,6 +51,12 @@ class FailSeg(C.Structure):
                 ("values", C.c_void_p), ("n", C.c_int64)]
 
 
+class UpdateSeg(C.Structure):
+    _fields_ = [("w", C.c_void_p), ("g", C.c_void_p), ("h", C.c_void_p), ("endurance", C.c_void_p),
+                ("values", C.c_void_p), ("n", C.c_int64), ("decay", C.c_float), ("local_rate", C.c_float),
+                ("thr", C.c_float), ("apply_thr", C.c_int), ("broken_count", C.c_void_p)]
+
+
 class ConvDesc(C.Structure):
     _fields_ = [(k, C.c_int) for k in (
         "num", "channels", "height", "width", "num_output", "kernel_h", "kernel_w", "pad_h",
@@ -84,6 +90,7 @@ SIGNATURES = {
     "rram_permute_elems": (I, [P, P, P, P, I, P]),
     "rram_sgd_update": (I, [P, P, I64, F, F, P]),
     "rram_fused_update_fail": (I, [P, P, P, P, P, I64, F, F, F, I, F, F, F, P, P]),
+    "rram_fused_update_fail_batched": (I, [P, I, F, F, F, P]),
     "rram_axpy": (I, [I64, F, P, P, P]),
     "rram_axpby": (I, [I64, F, P, F, P, P]),
     "rram_scal": (I, [I64, F, P, P]),

@@ -132,6 +132,18 @@ def fused_update_fail(w, g, h, e, v, decay, momentum, lr, apply_thr, thr, decrem
                                           _p(counter), _stream()), "fused_update_fail")
 
 
+def fused_update_fail_batched(segs, momentum, decrement=100.0, eps=1e-20):
+    """segs: list of (w, g, h, e, v, decay, lr, apply_thr, thr, counter); one launch."""
+    arr = (K.UpdateSeg * len(segs))()
+    for i, (w, g, h, e, v, decay, lr, apply_thr, thr, counter) in enumerate(segs):
+        for t, nm in ((w, "w"), (g, "g"), (h, "h"), (e, "endurance"), (v, "values")):
+            _f32(t, nm)
+        arr[i] = K.UpdateSeg(_p(w), _p(g), _p(h), _p(e), _p(v), w.numel(), decay, lr, thr, int(apply_thr),
+                             _p(counter))
+    K.check(_lib().rram_fused_update_fail_batched(arr, len(segs), momentum, decrement, eps, _stream()),
+            "fused_update_fail_batched")
+
+
 def gemm(trans_a, trans_b, M, N, K_, alpha, A, B, beta, Cm):
     K.check(_lib().rram_gemm_f32(int(trans_a), int(trans_b), M, N, K_, alpha, _p(A), _p(B), beta,
                                  _p(Cm), _stream()), "gemm")

@@ -31,6 +31,9 @@ def test_kernel_structs_match_header():
     assert ctypes.sizeof(K.InjectCfg) == 56
     assert ctypes.sizeof(K.InjectSeg) == 8 + 8 + 8 + 4 + 4 + 56
     assert ctypes.sizeof(K.FailSeg) == 40
+    # 5 pointers, n, 3 floats + int, counter pointer
+    assert ctypes.sizeof(K.UpdateSeg) == 5 * 8 + 8 + 4 * 4 + 8
+    assert K.UpdateSeg.broken_count.offset == 64
     assert ctypes.sizeof(K.ConvDesc) == 16 * 4
 
 
@@ -52,6 +55,9 @@ def test_invalid_args_return_status_not_abort():
     assert lib.rram_conv_out_shape(ctypes.byref(d)) == K.RRAM_EINVAL
     d = K.ConvDesc(2, 3, 227, 227, 96, 11, 11, 0, 0, 4, 4, 1, 1, 1, 0, 0)
     assert lib.rram_conv_out_shape(ctypes.byref(d)) == K.RRAM_OK and d.out_h == 55 == d.out_w
+    seg = K.UpdateSeg(None, None, None, None, None, -1, 0.0, 0.0, 0.0, 0, None)
+    assert lib.rram_fused_update_fail_batched(ctypes.byref(seg), 1, 0.9, 100.0, 1e-20, None) == K.RRAM_EINVAL
+    assert lib.rram_fused_update_fail_batched(None, 33, 0.9, 100.0, 1e-20, None) == K.RRAM_EINVAL
     # zero-size work is a successful no-op that never touches the device
     assert lib.rram_fail_apply(None, None, None, None, 0, 100.0, 1e-20, None, None) == K.RRAM_OK
 

@@ -338,6 +338,47 @@ def test_sgd_update_and_fused_tail(device, oracle_mod):
         assert bits_equal(N(uw), w3) and bits_equal(N(ue), e3) and int(N(c2)[0]) == nb
 
 
+def test_fused_tail_batched_equals_per_blob(device, oracle_mod):
+    """rram_fused_update_fail_batched (the solver's one-launch tail) gives the
+    bits of one rram_fused_update_fail per blob and of the oracle: ragged
+    sizes (incl. 1 and a non-multiple of the block chunk), a blob with no
+    fault state, per-blob decay / lr / threshold, two segments sharing one
+    broken counter."""
+    from rramsim import ops
+    rng = np.random.default_rng(21)
+    sizes = [1, 4095, 2048, 300_001, 17, 96 * 363]
+    blobs = []
+    for k, n in enumerate(sizes):
+        w, g, h = (rng.standard_normal(n).astype(np.float32) for _ in range(3))
+        e = rng.normal(150, 100, n).astype(np.float32)
+        v = rng.integers(-1, 2, n).astype(np.float32)
+        faulty = k != 2
+        blobs.append((w, g, h, e if faulty else None, v if faulty else None,
+                      0.004 * (k % 2), np.float32(0.01 * (k + 1)), faulty, np.float32(1e-3 * (k + 1))))
+    cnt_b = ops.counters(len(sizes), device)
+    cnt_u = ops.counters(len(sizes), device)
+    segs, outs_b, outs_u = [], [], []
+    for k, (w, g, h, e, v, decay, lr, faulty, thr) in enumerate(blobs):
+        tb = [T(x, device) if x is not None else None for x in (w, g, h, e, v)]
+        tu = [T(x, device) if x is not None else None for x in (w, g, h, e, v)]
+        slot = 0 if k in (0, 5) else k          # blobs 0 and 5 share counter 0
+        segs.append((*tb, decay, lr, faulty, thr, cnt_b[slot:slot + 1] if faulty else None))
+        ops.fused_update_fail(*tu, decay, 0.9, lr, faulty, thr,
+                              counter=cnt_u[slot:slot + 1] if faulty else None)
+        outs_b.append(tb)
+        outs_u.append(tu)
+    ops.fused_update_fail_batched(segs, 0.9)
+    for k, (tb, tu) in enumerate(zip(outs_b, outs_u)):
+        for a, b in zip(tb, tu):
+            if a is not None:
+                assert bits_equal(N(a), N(b)), k
+        w, g, h, e, v, decay, lr, faulty, thr = blobs[k]
+        if faulty:
+            w3, g3, h3, e3, _ = oracle_mod.fused_update_fail(w, g, h, e, v, decay, 0.9, lr, True, thr)
+            assert bits_equal(N(tb[0]), w3) and bits_equal(N(tb[3]), e3)
+    assert (N(cnt_b) == N(cnt_u)).all()
+
+
 # ------------------------------------------------------------------ GEMM
 def test_gemm_kat_exact(device):
     import torch
