@@ -440,6 +440,15 @@ int rram_pool_bwd(const float* dy, const int* mask, float* dx, int num,
                   int channels, int height, int width, int pooled_h,
                   int pooled_w, int kernel_h, int kernel_w, int stride_h,
                   int stride_w, int pad_h, int pad_w, int method, rram_stream_t s);
+/* rram_pool_fwd followed by an in-place ReLU of y (relu_layer.cu:9-15, y =
+ * y > 0 ? y : y * relu_slope) in the same launch: a Pooling layer whose top
+ * an in-place ReLU rewrites (CIFAR-10 pool1 -> relu1).  y is bit-identical to
+ * rram_pool_fwd + rram_relu_fwd; the MAX mask is the pre-ReLU argmax, as
+ * there. */
+int rram_pool_relu_fwd(const float* x, float* y, int* mask, int num, int channels,
+                       int height, int width, int pooled_h, int pooled_w,
+                       int kernel_h, int kernel_w, int stride_h, int stride_w,
+                       int pad_h, int pad_w, int method, float relu_slope, rram_stream_t s);
 
 /* y[i] = (float)x[i]: a MAX pool's int32 argmax as the float top mask
  * (pooling_layer.cu:30-34, the optional second top). */

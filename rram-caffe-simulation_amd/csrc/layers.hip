@@ -37,9 +37,13 @@ __global__ void k_relu_bwd(const float* __restrict__ x, const float* __restrict_
 }
 
 // pooling_layer.cu MaxPoolForward / AvePoolForward
+// relu != 0: the in-place ReLU that follows (rram_pool_relu_fwd), k_relu_fwd's expression
+__device__ __forceinline__ float pool_out(float v, int relu, float slope) {
+  return relu ? (v > 0.0f ? v : v * slope) : v;
+}
 __global__ void k_pool_fwd(const float* __restrict__ x, float* __restrict__ y, int* __restrict__ mask,
                            int num, int C, int H, int W, int PH, int PW, int kh, int kw, int sh,
-                           int sw, int ph, int pw, int method) {
+                           int sw, int ph, int pw, int method, int relu, float slope) {
   const int64_t total = (int64_t)num * C * PH * PW;
   GRID_LOOP(idx, total) {
     const int pwi = idx % PW;
@@ -59,7 +63,7 @@ __global__ void k_pool_fwd(const float* __restrict__ x, float* __restrict__ y, i
             mi = h * W + w;
             mv = xs[mi];
           }
-      y[idx] = mv;
+      y[idx] = pool_out(mv, relu, slope);
       if (mask) mask[idx] = mi;
     } else {
       int he = min(hs + kh, H + ph), we = min(ws + kw, W + pw);
@@ -71,7 +75,7 @@ __global__ void k_pool_fwd(const float* __restrict__ x, float* __restrict__ y, i
       float s = 0.0f;
       for (int h = hs; h < he; ++h)
         for (int w = ws; w < we; ++w) s += xs[h * W + w];
-      y[idx] = s / psize;
+      y[idx] = pool_out(s / psize, relu, slope);
     }
   }
 }
@@ -82,7 +86,8 @@ __global__ void k_pool_fwd(const float* __restrict__ x, float* __restrict__ y, i
 template <int K>
 __global__ void __launch_bounds__(256) k_pool_max_fixed(const float* __restrict__ x, float* __restrict__ y,
                                                         int* __restrict__ mask, int num, int C, int H, int W,
-                                                        int PH, int PW, int sh, int sw, int ph, int pw) {
+                                                        int PH, int PW, int sh, int sw, int ph, int pw,
+                                                        int relu, float slope) {
   const int total = num * C * PH * PW;
   GRID_LOOP(idx, total) {
     const int pwi = idx % PW;
@@ -111,7 +116,7 @@ __global__ void __launch_bounds__(256) k_pool_max_fixed(const float* __restrict_
           mv = v[a * K + b];
           mi = (hs + a) * W + (ws + b);
         }
-    y[idx] = mv;
+    y[idx] = pool_out(mv, relu, slope);
     if (mask) mask[idx] = mi;
   }
 }
@@ -138,7 +143,8 @@ template <int K>
 __global__ void __launch_bounds__(256) k_pool_planes(const float* __restrict__ x, float* __restrict__ y,
                                                      int* __restrict__ mask, int planes, int H, int W, int PH,
                                                      int PW, int kh, int kw, int sh, int sw, int ph, int pw,
-                                                     int method, int ppb, float inv_phw, float inv_pw) {
+                                                     int method, int ppb, float inv_phw, float inv_pw, int relu,
+                                                     float slope) {
   extern __shared__ __attribute__((aligned(16))) float tile[];
   const int HW = H * W, PHW = PH * PW;
   const int p0 = blockIdx.x * ppb;
@@ -204,7 +210,7 @@ __global__ void __launch_bounds__(256) k_pool_planes(const float* __restrict__ x
         for (int w = ws; w < we; ++w) s += t[h * W + w];
       mv = s / psize;
     }
-    dst[o] = mv;
+    dst[o] = pool_out(mv, relu, slope);
     if (mask) mask[(int64_t)p0 * PHW + o] = mi;
   }
 }
@@ -762,8 +768,11 @@ int rram_relu_bwd(const float* x, const float* dy, float* dx, int64_t n, float s
   return launch_status("relu_bwd");
 }
 
-int rram_pool_fwd(const float* x, float* y, int* mask, int num, int C, int H, int W, int PH, int PW,
-                  int kh, int kw, int sh, int sw, int ph, int pw, int method, rram_stream_t s) {
+}  // extern "C"
+namespace rram {
+namespace {
+int pool_fwd_core(const float* x, float* y, int* mask, int num, int C, int H, int W, int PH, int PW, int kh, int kw,
+                  int sh, int sw, int ph, int pw, int method, int relu, float slope, hipStream_t s) {
   RRAM_REQUIRE(num >= 0 && C > 0 && H > 0 && W > 0 && PH > 0 && PW > 0 && kh > 0 && kw > 0 &&
                    sh > 0 && sw > 0 && ph >= 0 && pw >= 0,
                "pool_fwd: bad geometry");
@@ -782,18 +791,32 @@ int rram_pool_fwd(const float* x, float* y, int* mask, int num, int C, int H, in
     const float inv_phw = 1.0f / static_cast<float>(PH * PW), inv_pw = 1.0f / static_cast<float>(PW);
     const int k = method == RRAM_POOL_MAX && kh == kw && (kh == 3 || kh == 2) ? kh : 0;
     auto kern = k == 3 ? k_pool_planes<3> : k == 2 ? k_pool_planes<2> : k_pool_planes<0>;
-    hipLaunchKernelGGL(kern, grid, dim3(kThreads), lds, as_stream(s), x, y, mask, planes, H, W, PH, PW, kh, kw, sh,
-                       sw, ph, pw, method, ppb, inv_phw, inv_pw);
+    hipLaunchKernelGGL(kern, grid, dim3(kThreads), lds, s, x, y, mask, planes, H, W, PH, PW, kh, kw, sh, sw, ph, pw,
+                       method, ppb, inv_phw, inv_pw, relu, slope);
   } else if (method == RRAM_POOL_MAX && kh == kw && kh == 3)
-    hipLaunchKernelGGL(k_pool_max_fixed<3>, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), x, y,
-                       mask, num, C, H, W, PH, PW, sh, sw, ph, pw);
+    hipLaunchKernelGGL(k_pool_max_fixed<3>, dim3(stream_blocks(total)), dim3(kThreads), 0, s, x, y, mask, num, C, H,
+                       W, PH, PW, sh, sw, ph, pw, relu, slope);
   else if (method == RRAM_POOL_MAX && kh == kw && kh == 2)
-    hipLaunchKernelGGL(k_pool_max_fixed<2>, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), x, y,
-                       mask, num, C, H, W, PH, PW, sh, sw, ph, pw);
+    hipLaunchKernelGGL(k_pool_max_fixed<2>, dim3(stream_blocks(total)), dim3(kThreads), 0, s, x, y, mask, num, C, H,
+                       W, PH, PW, sh, sw, ph, pw, relu, slope);
   else
-    hipLaunchKernelGGL(k_pool_fwd, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), x, y,
-                       mask, num, C, H, W, PH, PW, kh, kw, sh, sw, ph, pw, method);
+    hipLaunchKernelGGL(k_pool_fwd, dim3(stream_blocks(total)), dim3(kThreads), 0, s, x, y, mask, num, C, H, W, PH,
+                       PW, kh, kw, sh, sw, ph, pw, method, relu, slope);
   return launch_status("pool_fwd");
+}
+}  // namespace
+}  // namespace rram
+
+extern "C" {
+
+int rram_pool_fwd(const float* x, float* y, int* mask, int num, int C, int H, int W, int PH, int PW,
+                  int kh, int kw, int sh, int sw, int ph, int pw, int method, rram_stream_t s) {
+  return pool_fwd_core(x, y, mask, num, C, H, W, PH, PW, kh, kw, sh, sw, ph, pw, method, 0, 0.0f, as_stream(s));
+}
+int rram_pool_relu_fwd(const float* x, float* y, int* mask, int num, int C, int H, int W, int PH, int PW, int kh,
+                       int kw, int sh, int sw, int ph, int pw, int method, float relu_slope, rram_stream_t s) {
+  return pool_fwd_core(x, y, mask, num, C, H, W, PH, PW, kh, kw, sh, sw, ph, pw, method, 1, relu_slope,
+                       as_stream(s));
 }
 int rram_pool_bwd(const float* dy, const int* mask, float* dx, int num, int C, int H, int W, int PH,
                   int PW, int kh, int kw, int sh, int sw, int ph, int pw, int method, rram_stream_t s) {

@@ -91,6 +91,10 @@ class Layer {
     return false;
   }
   bool folded_into_next = false;
+  // ReLU fold into a Pooling producer (Net::Net, any phase): an in-place ReLU
+  // right after a layer that accepts it is applied in that layer's output
+  // store (rram_pool_relu_fwd); the ReLU's Backward still runs.
+  virtual bool fuse_relu_after(float /*slope*/) { return false; }
   // TEST-phase Concat fold (Net::Net): a producer whose top only feeds a
   // channel Concat writes its output straight into the Concat top at a
   // channel offset (write_into_concat: true when it can), and the Concat then

@@ -374,7 +374,7 @@ void InnerProductLayer<Dtype>::Backward_gpu(const std::vector<Blob<Dtype>*>& top
 template <typename Dtype>
 void ReLULayer<Dtype>::Forward_gpu(const std::vector<Blob<Dtype>*>& bottom,
                                    const std::vector<Blob<Dtype>*>& top) {
-  if (folded) return;  // applied in the producer's GEMM epilogue
+  if (folded) return;  // applied in the producer's epilogue / output store
   RRAM_CALL(rram_relu_fwd(bottom[0]->gpu_data(), top[0]->mutable_gpu_data(), bottom[0]->count(),
                           negative_slope(), Caffe::stream()));
 }
@@ -466,6 +466,12 @@ class PoolingLayer : public Layer<Dtype> {
     lrn_k_ = k;
     return true;
   }
+  bool fuse_relu_after(float slope) override {
+    if (lrn_src_ != nullptr) return false;  // the LRN + pool kernel has no ReLU store
+    relu_ = true;
+    relu_slope_ = slope;
+    return true;
+  }
 
  protected:
   void Forward_gpu(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
@@ -481,8 +487,13 @@ class PoolingLayer : public Layer<Dtype> {
     const bool top_mask = top.size() > 1;
     int* mask = (method_ == RRAM_POOL_MAX && (this->phase_ == TRAIN || top_mask))
                     ? reinterpret_cast<int*>(mask_.mutable_gpu_data()) : nullptr;
-    RRAM_CALL(rram_pool_fwd(bottom[0]->gpu_data(), top[0]->mutable_gpu_data(), mask, bottom[0]->shape(0),
-                            C_, H_, W_, PH_, PW_, kh_, kw_, sh_, sw_, ph_, pw_, method_, Caffe::stream()));
+    if (relu_)  // the in-place ReLU that follows (Net::Net fold), in the same store
+      RRAM_CALL(rram_pool_relu_fwd(bottom[0]->gpu_data(), top[0]->mutable_gpu_data(), mask, bottom[0]->shape(0), C_,
+                                   H_, W_, PH_, PW_, kh_, kw_, sh_, sw_, ph_, pw_, method_, relu_slope_,
+                                   Caffe::stream()));
+    else
+      RRAM_CALL(rram_pool_fwd(bottom[0]->gpu_data(), top[0]->mutable_gpu_data(), mask, bottom[0]->shape(0), C_, H_,
+                              W_, PH_, PW_, kh_, kw_, sh_, sw_, ph_, pw_, method_, Caffe::stream()));
     // the top mask holds the argmax index as a float (pooling_layer.cu:30-34)
     if (top_mask) RRAM_CALL(rram_i32_to_f32(mask, top[1]->mutable_gpu_data(), top[1]->count(), Caffe::stream()));
   }
@@ -497,7 +508,8 @@ class PoolingLayer : public Layer<Dtype> {
   }
   int method_ = RRAM_POOL_MAX, kh_ = 0, kw_ = 0, sh_ = 1, sw_ = 1, ph_ = 0, pw_ = 0;
   int C_ = 0, H_ = 0, W_ = 0, PH_ = 0, PW_ = 0;
-  bool global_ = false, top_mask_ = false;
+  bool global_ = false, top_mask_ = false, relu_ = false;
+  float relu_slope_ = 0.0f;
   Blob<Dtype> mask_;
   Blob<Dtype>* lrn_src_ = nullptr;  // bottom of a folded LRN (nullptr: unfused)
   int lrn_size_ = 5;

@@ -266,6 +266,8 @@ Net<Dtype>::Net(const Msg& in_param, Phase phase, const Msg& options) : phase_(p
           relu->folded = true;
         }
       }
+      // a Pooling producer (not itself carrying a folded LRN) stores relu(y)
+      if (relu && !relu->folded && prev_makes_it && prev->fuse_relu_after(relu->negative_slope())) relu->folded = true;
     }
     // TEST phase: fold an ACROSS_CHANNELS LRN into the MAX pool that is the only
     // reader of its top (a second reader would sit behind a Split layer); the

@@ -286,6 +286,11 @@ def pool_fwd(x, y, mask, geom, method):
     K.check(_lib().rram_pool_fwd(_p(x), _p(y), _p(mask), *geom, method, _stream()), "pool_fwd")
 
 
+def pool_relu_fwd(x, y, mask, geom, method, slope):
+    """pool_fwd then an in-place ReLU of y, one launch (rram_pool_relu_fwd)."""
+    K.check(_lib().rram_pool_relu_fwd(_p(x), _p(y), _p(mask), *geom, method, slope, _stream()), "pool_relu_fwd")
+
+
 def pool_bwd(dy, mask, dx, geom, method):
     K.check(_lib().rram_pool_bwd(_p(dy), _p(mask), _p(dx), *geom, method, _stream()), "pool_bwd")
 

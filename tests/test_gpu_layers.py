@@ -266,6 +266,75 @@ def test_lrn_maxpool_fusion_in_alexnet_test_net(device):
         assert torch.equal(outs[0][b], outs[1][b]), b
 
 
+@pytest.mark.parametrize("shape,k,s,p,method", [
+    ((8, 32, 32, 32), 3, 2, 0, 0),      # CIFAR pool1: LDS-plane kernel, 3x3 MAX
+    ((4, 20, 24, 24), 2, 2, 0, 0),      # LeNet-shaped 2x2 MAX
+    ((3, 5, 13, 11), 3, 2, 1, 1),       # AVE (plane kernel, generic window)
+    ((2, 3, 130, 130), 3, 2, 0, 0),     # planes > 16384: k_pool_max_fixed<3>
+    ((2, 3, 130, 130), 5, 3, 1, 1),     # planes > 16384, AVE: k_pool_fwd
+])
+@pytest.mark.parametrize("slope", [0.0, 0.1])
+def test_pool_relu_fused_equals_unfused(device, shape, k, s, p, method, slope):
+    """rram_pool_relu_fwd == rram_pool_fwd then rram_relu_fwd in place, bit
+    for bit (values incl. -0, +-Inf, NaN; the MAX argmax mask unchanged)."""
+    import torch
+    from rramsim import ops
+    torch.manual_seed(11)
+    x = torch.randn(*shape, device=device)
+    x[0, 0, :4, :4] = -0.0
+    x[0, 1, :2, :2] = float("-inf")
+    x[-1, -1, 1, 1] = float("nan")
+    x[-1, 0, :3, :3] = float("inf")
+    N, C, H, W = shape
+    PH = -(-(H + 2 * p - k) // s) + 1
+    PW = -(-(W + 2 * p - k) // s) + 1
+    if p and (PH - 1) * s >= H + p:
+        PH -= 1
+    if p and (PW - 1) * s >= W + p:
+        PW -= 1
+    geom = (N, C, H, W, PH, PW, k, k, s, s, p, p)
+    yu = torch.empty((N, C, PH, PW), device=device)
+    yf = torch.full_like(yu, 7.0)
+    mu = torch.empty(yu.shape, dtype=torch.int32, device=device)
+    mf = torch.full_like(mu, -7)
+    ops.pool_fwd(x, yu, mu if method == 0 else None, geom, method)
+    ops.relu_fwd(yu, yu, slope)
+    ops.pool_relu_fwd(x, yf, mf if method == 0 else None, geom, method, slope)
+    assert torch.equal(yu.view(torch.int32), yf.view(torch.int32))
+    if method == 0:
+        assert torch.equal(mu, mf)
+
+
+@pytest.mark.parametrize("net_name,phase", [("cifar10_quick", "test"), ("cifar10_full", "train")])
+def test_pool_relu_fold_in_net(device, net_name, phase):
+    """Net folds the in-place ReLU after a Pooling layer (CIFAR-10 pool1 ->
+    relu1) into the pool's store: blobs, loss and (TRAIN) every parameter
+    gradient bit-identical to the net with the fold off."""
+    import torch
+    from rramsim import caffe, models
+    caffe.set_stream_from_torch()
+    outs = []
+    for fuse in (False, True):
+        caffe.set_random_seed(1701)
+        spec = getattr(models, net_name)(train_batch=16, test_batch=16)
+        net = caffe.Net(spec, phase, models.net_options(net_name, fuse_relu=fuse))
+        net.forward()
+        if phase == "train":
+            net.backward()
+        torch.cuda.synchronize()
+        d = {b: net.blob(b).detach().cpu().clone() for b in ("pool1", "conv2")}
+        if phase == "train":
+            d.update({f"p{i}": q["diff"].detach().cpu().clone() for i, q in enumerate(net.params())})
+        outs.append(d)
+        net.close()
+    # pool1 (this fold) bit for bit; the rest by value: the Conv / IP epilogue
+    # ReLU fold (on with fuse_relu, relu2 / relu3 here) stores +0 where the
+    # ReLU layer's v * 0 stores -0 for a negative v
+    assert torch.equal(outs[0]["pool1"].view(torch.int32), outs[1]["pool1"].view(torch.int32))
+    for b in outs[0]:
+        assert torch.equal(outs[0][b], outs[1][b]), b
+
+
 @pytest.mark.parametrize("size", [3, 5])
 def test_lrn_within_fwd_bwd_vs_autograd(device, size):
     """cifar10_full's norm1/norm2 (lrn_layer.cpp WithinChannelForward/Backward)."""
