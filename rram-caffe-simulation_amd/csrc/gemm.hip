@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <array>
 #include <map>
+#include <tuple>
 #include <mutex>
 #include <type_traits>
 #include <vector>
@@ -1565,16 +1566,17 @@ std::mutex& pack_mutex() {
   static std::mutex mu;
   return mu;
 }
-std::map<std::pair<int, hipStream_t>, std::pair<float*, size_t>>& pack_cache() {
-  static std::map<std::pair<int, hipStream_t>, std::pair<float*, size_t>> cache;
+// key: (device, stream, slot); slot 0 = pack buffers, 1 = conv split-K partials
+std::map<std::tuple<int, hipStream_t, int>, std::pair<float*, size_t>>& pack_cache() {
+  static std::map<std::tuple<int, hipStream_t, int>, std::pair<float*, size_t>> cache;
   return cache;
 }
 
-float* pack_buffer(size_t floats, hipStream_t s) {
+float* stream_buffer(int slot, size_t floats, hipStream_t s) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   std::lock_guard<std::mutex> g(pack_mutex());
-  auto& e = pack_cache()[{dev, s}];
+  auto& e = pack_cache()[{dev, s, slot}];
   if (e.second >= floats) return e.first;
   if (e.first) {
     if (hipStreamSynchronize(s) != hipSuccess) return nullptr;
@@ -1586,6 +1588,7 @@ float* pack_buffer(size_t floats, hipStream_t s) {
   e = {p, floats};
   return p;
 }
+float* pack_buffer(size_t floats, hipStream_t s) { return stream_buffer(0, floats, s); }
 
 template <int KH, int KW, int CPH, int MI, int PD>
 int launch_patch(Params P, const float* wpack, int PW, int CS, int gz, hipStream_t s) {
@@ -1675,6 +1678,24 @@ int conv_patch_fwd(const rram_conv_desc* d, const float* w, Params& P, hipStream
   return rc ? rc : 1;
 }
 
+// split-K factor of the fp32 implicit-GEMM convolution forward (1: none):
+// ungrouped, M <= 64, K >= 256 and fewer than 256 output tiles of 32 or 64
+// rows x 128 positions, split toward RRAM_CONV_SPLIT workgroups (default
+// 1024, profiles/r04_ab_conv_split.txt; 0 turns it off, for A/B runs) with
+// >= 128 K per split
+int conv_fwd_split(const rram_conv_desc* d, int M, int N, int K) {
+  static const int target = [] {
+    const char* e = getenv("RRAM_CONV_SPLIT");
+    return e ? atoi(e) : 1024;
+  }();
+  if (target <= 0 || d->group != 1 || M > 64 || K < 256) return 1;
+  const int64_t tiles = (int64_t)((M + 31) / 32) * ((N + 127) / 128);
+  if (tiles >= 256) return 1;
+  int split = static_cast<int>((target + tiles - 1) / tiles);
+  split = std::min(split, std::max(1, K / 128));
+  return std::min(split, 16);
+}
+
 int conv_fwd_core(const rram_conv_desc* d, const float* x, const float* w, const float* bias,
                   float* y, int relu, hipStream_t s, int64_t y_img) {
   {
@@ -1744,6 +1765,28 @@ int conv_fwd_core(const rram_conv_desc* d, const float* x, const float* w, const
   if (amode == KC && bmode == CONVT && (reinterpret_cast<uintptr_t>(w) & 3u) == 0 &&
       (int64_t)g * cout_g * K * 4 < (1ll << 31))
     amode = KCU;
+  // thin, short-grid convolutions (CIFAR-10 conv2 / conv3, LeNet conv2 at
+  // batch 100: M = 32..64, a few hundred K, 50-200 tiles of 32/64 x 128) leave
+  // most CUs idle for K / KB serial K-tiles: split K toward ~1024 workgroups,
+  // partials summed in order by k_splitk_reduce_nchw
+  {
+    const int split = conv_fwd_split(d, P.M, P.N, K);
+    if (split > 1) {
+      const int kb = conv_kb(K);
+      const int kc = ((K + split - 1) / split + kb - 1) / kb * kb;
+      const int sp = (K + kc - 1) / kc;
+      float* ws = stream_buffer(1, (size_t)sp * P.M * P.N, s);
+      RRAM_REQUIRE(ws != nullptr, "conv2d_fwd: split-K buffer allocation failed");
+      P.split = sp;
+      P.k_chunk = kc;
+      P.ws = ws;
+      int rc = dispatch(amode, bmode, OUT_NCHW, P, sp, s);
+      if (rc) return rc;
+      hipLaunchKernelGGL(k_splitk_reduce_nchw, dim3(stream_blocks((int64_t)P.M * P.N)), dim3(256), 0, s, ws, sp, P.M,
+                         P.N, P.e);
+      return launch_status("conv fwd split-K reduce");
+    }
+  }
   return dispatch(amode, bmode, OUT_NCHW, P, g, s);
 }
 

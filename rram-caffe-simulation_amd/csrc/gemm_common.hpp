@@ -323,6 +323,24 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(const float* __restrict__
   }
 }
 
+// k_splitk_reduce for an NCHW convolution output (column n = image * HW +
+// position): partials summed in split order, then bias (per row) and ReLU as
+// gemm_epilogue's beta = 0 path
+__global__ void __launch_bounds__(256) k_splitk_reduce_nchw(const float* __restrict__ ws, int split, int M, int N,
+                                                            Epi ep) {
+  const int64_t total = (int64_t)M * N;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.0f;
+    for (int z = 0; z < split; ++z) s += ws[(int64_t)z * total + idx];
+    const int m = static_cast<int>(idx / N);
+    const uint32_t n = static_cast<uint32_t>(idx - (int64_t)m * N);
+    const uint32_t im = fdiv(n, ep.hw), sp = n - im * ep.hw.d;
+    const float o = ep.alpha * s + (ep.bias_mode == RRAM_BIAS_ROW ? ep.bias[m] : 0.0f);
+    ep.C[(int64_t)im * ep.cimg + (int64_t)m * ep.ldc + sp] = ep.relu ? fmaxf(o, 0.0f) : o;
+  }
+}
+
 namespace g2 {
 typedef int int4v __attribute__((ext_vector_type(4)));
 

@@ -830,3 +830,28 @@ def test_im2col_col2im_bit_exact(device, oracle_mod, cs):
     ops.col2im(T(ref, device), C_, H, W, kh, kw, ph, pw, sh, sw, dh, dw, back)
     np.testing.assert_allclose(N(back), oracle_mod.col2im(ref, C_, H, W, kh, kw, ph, pw, sh, sw, dh, dw),
                                rtol=1e-6, atol=1e-5)
+
+
+@pytest.mark.parametrize("shape,cout,k,pad,relu", [
+    ((100, 32, 16, 16), 32, 5, 2, True),    # CIFAR-10 quick / full conv2 (split-K forward)
+    ((100, 32, 8, 8), 64, 5, 2, True),      # CIFAR-10 quick conv3
+    ((100, 20, 12, 12), 50, 5, 0, False),   # LeNet conv2
+    ((7, 33, 9, 9), 40, 3, 1, True),        # ragged: K % 32 != 0, N % 128 != 0
+])
+def test_conv_fwd_split_k_vs_fp64(device, shape, cout, k, pad, relu):
+    """The fp32 convolution forward with K split over workgroups
+    (conv_fwd_split: thin, short-grid layers) + k_splitk_reduce_nchw: within
+    fp32 accumulation error of float64 (<= 2e-6 of sum|a*b| + |bias|), bias and
+    ReLU applied once, NCHW layout."""
+    import torch
+    from rramsim import ops
+    from _ref64 import conv64, assert_scaled
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal(shape).astype(np.float32)
+    w = (rng.standard_normal((cout, shape[1], k, k)) * 0.1).astype(np.float32)
+    b = rng.standard_normal(cout).astype(np.float32)
+    d = ops.conv_desc(shape, cout, k, 1, pad)
+    y = torch.full((shape[0], cout, d.out_h, d.out_w), float("nan"), device=device)
+    ops.conv2d_fwd(d, T(x, device), T(w, device), T(b, device), y, relu=relu)
+    ref, scale = conv64(x, w, b, 1, pad)
+    assert_scaled(N(y), ref, scale, "conv fwd split-K", tol=2e-6, relu=relu)
