@@ -450,6 +450,17 @@ int rram_pool_relu_fwd(const float* x, float* y, int* mask, int num, int channel
                        int kernel_h, int kernel_w, int stride_h, int stride_w,
                        int pad_h, int pad_w, int method, float relu_slope, rram_stream_t s);
 
+/* rram_pool_bwd followed by the backward of the in-place ReLU that produced
+ * the pool's input (relu_layer.cu:35-44: dx *= (y > 0) + (y <= 0) * slope,
+ * y = relu_y, the ReLU's output = the pool's bottom data) in the same launch:
+ * a ReLU -> Pooling pair (CIFAR-10 full relu2 -> pool2).  Bit-identical to
+ * rram_pool_bwd + rram_relu_bwd. */
+int rram_pool_relu_bwd(const float* dy, const int* mask, float* dx, int num,
+                       int channels, int height, int width, int pooled_h,
+                       int pooled_w, int kernel_h, int kernel_w, int stride_h,
+                       int stride_w, int pad_h, int pad_w, int method,
+                       const float* relu_y, float relu_slope, rram_stream_t s);
+
 /* y[i] = (float)x[i]: a MAX pool's int32 argmax as the float top mask
  * (pooling_layer.cu:30-34, the optional second top). */
 int rram_i32_to_f32(const int* x, float* y, int64_t n, rram_stream_t s);

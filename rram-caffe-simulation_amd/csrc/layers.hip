@@ -216,9 +216,12 @@ __global__ void __launch_bounds__(256) k_pool_planes(const float* __restrict__ x
 }
 
 // pooling_layer.cu MaxPoolBackward / AvePoolBackward
+// ry != nullptr: times the backward factor of the in-place ReLU whose output
+// ry is (rram_pool_relu_bwd; k_relu_bwd's expression)
 __global__ void k_pool_bwd(const float* __restrict__ dy, const int* __restrict__ mask,
                            float* __restrict__ dx, int num, int C, int H, int W, int PH, int PW,
-                           int kh, int kw, int sh, int sw, int ph, int pw, int method) {
+                           int kh, int kw, int sh, int sw, int ph, int pw, int method,
+                           const float* __restrict__ ry, float slope) {
   const int64_t total = (int64_t)num * C * H * W;
   GRID_LOOP(idx, total) {
     const int w = idx % W;
@@ -248,6 +251,7 @@ __global__ void k_pool_bwd(const float* __restrict__ dy, const int* __restrict__
           g += d[a * PW + b] / ((he - hs) * (we - ws));
         }
     }
+    if (ry != nullptr) g = g * ((ry[idx] > 0.0f) + (ry[idx] <= 0.0f) * slope);
     dx[idx] = g;
   }
 }
@@ -820,6 +824,11 @@ int rram_pool_relu_fwd(const float* x, float* y, int* mask, int num, int C, int 
 }
 int rram_pool_bwd(const float* dy, const int* mask, float* dx, int num, int C, int H, int W, int PH,
                   int PW, int kh, int kw, int sh, int sw, int ph, int pw, int method, rram_stream_t s) {
+  return rram_pool_relu_bwd(dy, mask, dx, num, C, H, W, PH, PW, kh, kw, sh, sw, ph, pw, method, nullptr, 0.0f, s);
+}
+int rram_pool_relu_bwd(const float* dy, const int* mask, float* dx, int num, int C, int H, int W, int PH,
+                       int PW, int kh, int kw, int sh, int sw, int ph, int pw, int method, const float* relu_y,
+                       float relu_slope, rram_stream_t s) {
   RRAM_REQUIRE(num >= 0 && C > 0 && H > 0 && W > 0 && PH > 0 && PW > 0 && sh > 0 && sw > 0,
                "pool_bwd: bad geometry");
   RRAM_REQUIRE(method != RRAM_POOL_MAX || mask != nullptr, "pool_bwd: MAX needs mask");
@@ -828,7 +837,7 @@ int rram_pool_bwd(const float* dy, const int* mask, float* dx, int num, int C, i
   if (total == 0) return RRAM_OK;
   RRAM_REQUIRE(dy && dx, "pool_bwd: NULL");
   hipLaunchKernelGGL(k_pool_bwd, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), dy,
-                     mask, dx, num, C, H, W, PH, PW, kh, kw, sh, sw, ph, pw, method);
+                     mask, dx, num, C, H, W, PH, PW, kh, kw, sh, sw, ph, pw, method, relu_y, relu_slope);
   return launch_status("pool_bwd");
 }
 

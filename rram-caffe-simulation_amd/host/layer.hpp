@@ -95,6 +95,10 @@ class Layer {
   // right after a layer that accepts it is applied in that layer's output
   // store (rram_pool_relu_fwd); the ReLU's Backward still runs.
   virtual bool fuse_relu_after(float /*slope*/) { return false; }
+  // the mirror in backward (TRAIN): a layer right after an in-place ReLU that
+  // applies the ReLU's backward factor to the bottom diff it writes
+  // (rram_pool_relu_bwd); the ReLU's Backward then does nothing
+  virtual bool fuse_relu_before_bwd(float /*slope*/) { return false; }
   // TEST-phase Concat fold (Net::Net): a producer whose top only feeds a
   // channel Concat writes its output straight into the Concat top at a
   // channel offset (write_into_concat: true when it can), and the Concat then

@@ -381,7 +381,7 @@ void ReLULayer<Dtype>::Forward_gpu(const std::vector<Blob<Dtype>*>& bottom,
 template <typename Dtype>
 void ReLULayer<Dtype>::Backward_gpu(const std::vector<Blob<Dtype>*>& top, const std::vector<bool>& pd,
                                     const std::vector<Blob<Dtype>*>& bottom) {
-  if (!pd.size() || !pd[0]) return;
+  if (!pd.size() || !pd[0] || bwd_folded) return;  // bwd_folded: applied by the consumer's backward
   // in-place: bottom data is the ReLU output; x > 0 <=> y > 0 for slope 0 (relu_layer.cu:35-44)
   RRAM_CALL(rram_relu_bwd(bottom[0]->gpu_data(), top[0]->gpu_diff(), bottom[0]->mutable_gpu_diff(),
                           bottom[0]->count(), negative_slope(), Caffe::stream()));
@@ -466,6 +466,12 @@ class PoolingLayer : public Layer<Dtype> {
     lrn_k_ = k;
     return true;
   }
+  bool fuse_relu_before_bwd(float slope) override {
+    if (this->phase_ != TRAIN) return false;
+    relu_bwd_ = true;
+    relu_bwd_slope_ = slope;
+    return true;
+  }
   bool fuse_relu_after(float slope) override {
     if (lrn_src_ != nullptr) return false;  // the LRN + pool kernel has no ReLU store
     relu_ = true;
@@ -501,15 +507,17 @@ class PoolingLayer : public Layer<Dtype> {
                     const std::vector<Blob<Dtype>*>& bottom) override {
     if (!pd.size() || !pd[0]) return;
     CAFFE_CHECK(method_ != RRAM_POOL_MAX || this->phase_ == TRAIN, "MAX pool backward needs TRAIN phase");
-    RRAM_CALL(rram_pool_bwd(top[0]->gpu_diff(),
-                            method_ == RRAM_POOL_MAX ? reinterpret_cast<const int*>(mask_.gpu_data()) : nullptr,
-                            bottom[0]->mutable_gpu_diff(), bottom[0]->shape(0), C_, H_, W_, PH_, PW_, kh_,
-                            kw_, sh_, sw_, ph_, pw_, method_, Caffe::stream()));
+    // relu_bwd_: the in-place ReLU before this pool (Net::Net fold); its output is our bottom data
+    RRAM_CALL(rram_pool_relu_bwd(top[0]->gpu_diff(),
+                                 method_ == RRAM_POOL_MAX ? reinterpret_cast<const int*>(mask_.gpu_data()) : nullptr,
+                                 bottom[0]->mutable_gpu_diff(), bottom[0]->shape(0), C_, H_, W_, PH_, PW_, kh_, kw_,
+                                 sh_, sw_, ph_, pw_, method_, relu_bwd_ ? bottom[0]->gpu_data() : nullptr,
+                                 relu_bwd_slope_, Caffe::stream()));
   }
   int method_ = RRAM_POOL_MAX, kh_ = 0, kw_ = 0, sh_ = 1, sw_ = 1, ph_ = 0, pw_ = 0;
   int C_ = 0, H_ = 0, W_ = 0, PH_ = 0, PW_ = 0;
-  bool global_ = false, top_mask_ = false, relu_ = false;
-  float relu_slope_ = 0.0f;
+  bool global_ = false, top_mask_ = false, relu_ = false, relu_bwd_ = false;
+  float relu_slope_ = 0.0f, relu_bwd_slope_ = 0.0f;
   Blob<Dtype> mask_;
   Blob<Dtype>* lrn_src_ = nullptr;  // bottom of a folded LRN (nullptr: unfused)
   int lrn_size_ = 5;

@@ -81,6 +81,8 @@ class ReLULayer : public Layer<Dtype> {
   }
   // set by Net when the producing Conv/IP layer applies the ReLU in its epilogue
   bool folded = false;
+  // set by Net when the consuming layer applies the ReLU's backward factor
+  bool bwd_folded = false;
 
  protected:
   void Forward_gpu(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override;

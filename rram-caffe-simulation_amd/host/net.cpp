@@ -269,6 +269,15 @@ Net<Dtype>::Net(const Msg& in_param, Phase phase, const Msg& options) : phase_(p
       // a Pooling producer (not itself carrying a folded LRN) stores relu(y)
       if (relu && !relu->folded && prev_makes_it && prev->fuse_relu_after(relu->negative_slope())) relu->folded = true;
     }
+    // the backward mirror: a layer whose single bottom is the top of the
+    // in-place ReLU right before it applies that ReLU's backward factor
+    if (fuse_relu && type == "Pooling" && lid > 0 && bottoms.size() == 1) {
+      auto* relu = dynamic_cast<ReLULayer<Dtype>*>(layers_[lid - 1].get());
+      if (relu && bottom_vecs_[lid - 1].size() == 1 && top_id_vecs_[lid - 1].size() == 1 &&
+          bottom_id_vecs_[lid - 1][0] == top_id_vecs_[lid - 1][0] && top_id_vecs_[lid - 1][0] == bottom_id_vecs_[lid][0] &&
+          layer->fuse_relu_before_bwd(relu->negative_slope()))
+        relu->bwd_folded = true;
+    }
     // TEST phase: fold an ACROSS_CHANNELS LRN into the MAX pool that is the only
     // reader of its top (a second reader would sit behind a Split layer); the
     // LRN top is then never materialised (rram_lrn_maxpool_fwd)

@@ -124,6 +124,7 @@ SIGNATURES = {
     "rram_relu_bwd": (I, [P, P, P, I64, F, P]),
     "rram_pool_fwd": (I, [P, P, P] + [I] * 13 + [P]),
     "rram_pool_relu_fwd": (I, [P, P, P] + [I] * 13 + [F, P]),
+    "rram_pool_relu_bwd": (I, [P, P, P] + [I] * 13 + [P, F, P]),
     "rram_pool_bwd": (I, [P, P, P] + [I] * 13 + [P]),
     "rram_lrn_fwd": (I, [P, P, P, I, I, I, I, I, F, F, F, P]),
     "rram_lrn_bwd": (I, [P, P, P, P, P, I, I, I, I, I, F, F, P]),

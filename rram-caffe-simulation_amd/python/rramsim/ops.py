@@ -286,6 +286,12 @@ def pool_fwd(x, y, mask, geom, method):
     K.check(_lib().rram_pool_fwd(_p(x), _p(y), _p(mask), *geom, method, _stream()), "pool_fwd")
 
 
+def pool_relu_bwd(dy, mask, dx, geom, method, relu_y, slope):
+    """pool_bwd then the in-place ReLU's backward on dx (factor from relu_y), one launch."""
+    K.check(_lib().rram_pool_relu_bwd(_p(dy), _p(mask), _p(dx), *geom, method, _p(relu_y), slope, _stream()),
+            "pool_relu_bwd")
+
+
 def pool_relu_fwd(x, y, mask, geom, method, slope):
     """pool_fwd then an in-place ReLU of y, one launch (rram_pool_relu_fwd)."""
     K.check(_lib().rram_pool_relu_fwd(_p(x), _p(y), _p(mask), *geom, method, slope, _stream()), "pool_relu_fwd")

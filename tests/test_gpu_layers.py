@@ -305,11 +305,48 @@ def test_pool_relu_fused_equals_unfused(device, shape, k, s, p, method, slope):
         assert torch.equal(mu, mf)
 
 
+@pytest.mark.parametrize("shape,k,s,p,method", [
+    ((8, 32, 32, 32), 3, 2, 0, 0),      # MAX 3x3/2
+    ((4, 32, 16, 16), 3, 2, 0, 1),      # CIFAR-10 full pool2: AVE 3x3/2
+    ((3, 5, 13, 11), 3, 2, 1, 1),       # AVE, padded
+])
+@pytest.mark.parametrize("slope", [0.0, 0.1])
+def test_pool_relu_bwd_fused_equals_unfused(device, shape, k, s, p, method, slope):
+    """rram_pool_relu_bwd == rram_pool_bwd then rram_relu_bwd in place (the
+    ReLU's output y = the pool's bottom data), bit for bit, incl. y = +-0 / NaN."""
+    import torch
+    from rramsim import ops
+    torch.manual_seed(12)
+    x = torch.randn(*shape, device=device)
+    y = torch.where(x > 0, x, x * slope)            # the in-place ReLU's output
+    y[0, 0, :2, :2] = -0.0
+    y[-1, -1, 0, 0] = float("nan")
+    N, C, H, W = shape
+    PH = -(-(H + 2 * p - k) // s) + 1
+    PW = -(-(W + 2 * p - k) // s) + 1
+    if p and (PH - 1) * s >= H + p:
+        PH -= 1
+    if p and (PW - 1) * s >= W + p:
+        PW -= 1
+    geom = (N, C, H, W, PH, PW, k, k, s, s, p, p)
+    top = torch.empty((N, C, PH, PW), device=device)
+    mask = torch.empty(top.shape, dtype=torch.int32, device=device)
+    ops.pool_fwd(y, top, mask if method == 0 else None, geom, method)
+    dy = torch.randn_like(top)
+    du, df = torch.empty_like(x), torch.full_like(x, 7.0)
+    ops.pool_bwd(dy, mask if method == 0 else None, du, geom, method)
+    ops.relu_bwd(y, du, du, slope)
+    ops.pool_relu_bwd(dy, mask if method == 0 else None, df, geom, method, y, slope)
+    assert torch.equal(du.view(torch.int32), df.view(torch.int32))
+
+
 @pytest.mark.parametrize("net_name,phase", [("cifar10_quick", "test"), ("cifar10_full", "train")])
 def test_pool_relu_fold_in_net(device, net_name, phase):
     """Net folds the in-place ReLU after a Pooling layer (CIFAR-10 pool1 ->
-    relu1) into the pool's store: blobs, loss and (TRAIN) every parameter
-    gradient bit-identical to the net with the fold off."""
+    relu1) into the pool's store, and (TRAIN) the backward of an in-place ReLU
+    before a Pooling layer (relu2 -> pool2, relu3 -> pool3) into the pool's
+    backward: blobs, loss and every parameter gradient equal to the net with
+    the folds off."""
     import torch
     from rramsim import caffe, models
     caffe.set_stream_from_torch()
