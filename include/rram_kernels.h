@@ -482,6 +482,12 @@ int rram_lrn_within_fwd(const float* x, float* y, float* scale, int num, int cha
 int rram_lrn_within_bwd(const float* x, const float* scale, const float* dy, float* dx, int num,
                         int channels, int height, int width, int size, float alpha, float beta,
                         rram_stream_t s);
+/* rram_lrn_within_bwd followed by the backward of the in-place ReLU that
+ * produced x (dx *= (x > 0) + (x <= 0) * relu_slope, relu_layer.cu:35-44) in
+ * the same launch: a ReLU -> LRN pair (CIFAR-10 full relu1 -> norm1).
+ * Bit-identical to rram_lrn_within_bwd + rram_relu_bwd. */
+int rram_lrn_within_relu_bwd(const float* x, const float* scale, const float* dy, float* dx, int num, int C,
+                             int H, int W, int size, float alpha, float beta, float relu_slope, rram_stream_t s);
 
 /* Inference fusion (TEST phase) of LRN ACROSS_CHANNELS followed by MAX
  * pooling whose bottom is the LRN top and nothing else reads it:

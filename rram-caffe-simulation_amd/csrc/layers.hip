@@ -378,9 +378,11 @@ __global__ void k_lrn_within_fwd(const float* __restrict__ x, float* __restrict_
     y[idx] = x[idx] * pow_pos(sc, -beta);
   }
 }
+// relu != 0: times the backward factor of the in-place ReLU whose output x is
+// (rram_lrn_within_relu_bwd; k_relu_bwd's expression)
 __global__ void k_lrn_within_bwd(const float* __restrict__ x, const float* __restrict__ scale,
                                  const float* __restrict__ dy, float* __restrict__ dx, int64_t planes, int H,
-                                 int W, int size, float alpha, float beta) {
+                                 int W, int size, float alpha, float beta, int relu, float slope) {
   const int64_t total = planes * H * W;
   const int pre = (size - 1) / 2;
   GRID_LOOP(idx, total) {
@@ -397,7 +399,9 @@ __global__ void k_lrn_within_bwd(const float* __restrict__ x, const float* __res
         const float n = static_cast<float>(within_psize(a, pre, size, H) * within_psize(b, pre, size, W));
         acc += dy[o] * x[o] * pow_pos(scale[o], -beta - 1.0f) / n;
       }
-    dx[idx] = dy[idx] * pow_pos(scale[idx], -beta) - 2.0f * alpha * beta * x[idx] * acc;
+    float g = dy[idx] * pow_pos(scale[idx], -beta) - 2.0f * alpha * beta * x[idx] * acc;
+    if (relu) g = g * ((x[idx] > 0.0f) + (x[idx] <= 0.0f) * slope);
+    dx[idx] = g;
   }
 }
 
@@ -751,6 +755,14 @@ __global__ void k_scale_copy(const float* __restrict__ x, float* __restrict__ y,
 }  // namespace
 }  // namespace rram
 
+namespace rram {
+namespace {
+int rram_lrn_within_relu_bwd_core(const float* x, const float* scale, const float* dy, float* dx, int num, int C,
+                                  int H, int W, int size, float alpha, float beta, int relu, float slope,
+                                  rram_stream_t s);
+}  // namespace
+}  // namespace rram
+
 using namespace rram;
 
 extern "C" {
@@ -887,15 +899,30 @@ int rram_lrn_within_fwd(const float* x, float* y, float* scale, int num, int C, 
 }
 int rram_lrn_within_bwd(const float* x, const float* scale, const float* dy, float* dx, int num, int C, int H,
                         int W, int size, float alpha, float beta, rram_stream_t s) {
+  return rram_lrn_within_relu_bwd_core(x, scale, dy, dx, num, C, H, W, size, alpha, beta, 0, 0.0f, s);
+}
+int rram_lrn_within_relu_bwd(const float* x, const float* scale, const float* dy, float* dx, int num, int C, int H,
+                             int W, int size, float alpha, float beta, float relu_slope, rram_stream_t s) {
+  return rram_lrn_within_relu_bwd_core(x, scale, dy, dx, num, C, H, W, size, alpha, beta, 1, relu_slope, s);
+}
+}  // extern "C"
+namespace rram {
+namespace {
+int rram_lrn_within_relu_bwd_core(const float* x, const float* scale, const float* dy, float* dx, int num, int C,
+                                  int H, int W, int size, float alpha, float beta, int relu, float slope,
+                                  rram_stream_t s) {
   RRAM_REQUIRE(num >= 0 && C > 0 && H > 0 && W > 0 && size > 0 && (size & 1), "lrn_within_bwd: bad geometry");
   const int64_t total = (int64_t)num * C * H * W;
   RRAM_REQUIRE_I32(total, "layer kernel");
   if (total == 0) return RRAM_OK;
   RRAM_REQUIRE(x && scale && dy && dx, "lrn_within_bwd: NULL");
   hipLaunchKernelGGL(k_lrn_within_bwd, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), x, scale,
-                     dy, dx, (int64_t)num * C, H, W, size, alpha, beta);
+                     dy, dx, (int64_t)num * C, H, W, size, alpha, beta, relu, slope);
   return launch_status("lrn_within_bwd");
 }
+}  // namespace
+}  // namespace rram
+extern "C" {
 
 int rram_softmax_fwd(const float* x, float* y, int outer, int C, int inner, rram_stream_t s) {
   RRAM_REQUIRE(outer >= 0 && C > 0 && inner > 0, "softmax: bad shape");

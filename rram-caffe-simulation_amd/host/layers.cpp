@@ -557,6 +557,13 @@ class LRNLayer : public Layer<Dtype> {
     return true;
   }
 
+  bool fuse_relu_before_bwd(float slope) override {
+    if (this->phase_ != TRAIN || !within_) return false;
+    relu_bwd_ = true;
+    relu_bwd_slope_ = slope;
+    return true;
+  }
+
  protected:
   void Forward_gpu(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
     CAFFE_CHECK(bottom[0] != top[0], "LRN cannot run in place");
@@ -574,7 +581,11 @@ class LRNLayer : public Layer<Dtype> {
                     const std::vector<Blob<Dtype>*>& bottom) override {
     if (!pd.size() || !pd[0]) return;
     auto& b = *bottom[0];
-    if (within_)
+    if (within_ && relu_bwd_)  // the in-place ReLU before this LRN (Net::Net fold); its output is our bottom
+      RRAM_CALL(rram_lrn_within_relu_bwd(b.gpu_data(), scale_.gpu_data(), top[0]->gpu_diff(), b.mutable_gpu_diff(),
+                                         b.shape(0), b.shape(1), b.shape(2), b.shape(3), size_, alpha_, beta_,
+                                         relu_bwd_slope_, Caffe::stream()));
+    else if (within_)
       RRAM_CALL(rram_lrn_within_bwd(b.gpu_data(), scale_.gpu_data(), top[0]->gpu_diff(), b.mutable_gpu_diff(),
                                     b.shape(0), b.shape(1), b.shape(2), b.shape(3), size_, alpha_, beta_,
                                     Caffe::stream()));
@@ -585,7 +596,8 @@ class LRNLayer : public Layer<Dtype> {
   }
   int size_ = 5;
   float alpha_ = 1, beta_ = 0.75f, k_ = 1;
-  bool within_ = false;
+  bool within_ = false, relu_bwd_ = false;
+  float relu_bwd_slope_ = 0.0f;
   Blob<Dtype> scale_;
 };
 

@@ -271,7 +271,7 @@ Net<Dtype>::Net(const Msg& in_param, Phase phase, const Msg& options) : phase_(p
     }
     // the backward mirror: a layer whose single bottom is the top of the
     // in-place ReLU right before it applies that ReLU's backward factor
-    if (fuse_relu && type == "Pooling" && lid > 0 && bottoms.size() == 1) {
+    if (fuse_relu && lid > 0 && bottoms.size() == 1) {
       auto* relu = dynamic_cast<ReLULayer<Dtype>*>(layers_[lid - 1].get());
       if (relu && bottom_vecs_[lid - 1].size() == 1 && top_id_vecs_[lid - 1].size() == 1 &&
           bottom_id_vecs_[lid - 1][0] == top_id_vecs_[lid - 1][0] && top_id_vecs_[lid - 1][0] == bottom_id_vecs_[lid][0] &&

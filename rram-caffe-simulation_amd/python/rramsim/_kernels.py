@@ -130,6 +130,7 @@ SIGNATURES = {
     "rram_lrn_bwd": (I, [P, P, P, P, P, I, I, I, I, I, F, F, P]),
     "rram_lrn_within_fwd": (I, [P, P, P, I, I, I, I, I, F, F, P]),
     "rram_lrn_within_bwd": (I, [P, P, P, P, I, I, I, I, I, F, F, P]),
+    "rram_lrn_within_relu_bwd": (I, [P, P, P, P, I, I, I, I, I, F, F, F, P]),
     "rram_lrn_maxpool_fwd": (I, [P, P, I, I, I, I, I, I, I, I, I, I, I, I, F, F, F, P]),
     "rram_lrn_maxpool_fwd_octets": (I, [P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, F, F, F, P]),
     "rram_softmax_fwd": (I, [P, P, I, I, I, P]),

@@ -331,6 +331,12 @@ def lrn_within_bwd(x, scale, dy, dx, n, c, h, w, size, alpha, beta):
                                        beta, _stream()), "lrn_within_bwd")
 
 
+def lrn_within_relu_bwd(x, scale, dy, dx, n, c, h, w, size, alpha, beta, slope):
+    """lrn_within_bwd then the in-place ReLU's backward on dx (factor from x), one launch."""
+    K.check(_lib().rram_lrn_within_relu_bwd(_p(x), _p(scale), _p(dy), _p(dx), n, c, h, w, size, alpha, beta,
+                                            slope, _stream()), "lrn_within_relu_bwd")
+
+
 def relu_fwd(x, y, slope=0.0):
     K.check(_lib().rram_relu_fwd(_p(x), _p(y), x.numel(), slope, _stream()), "relu_fwd")
 

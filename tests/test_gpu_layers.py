@@ -340,13 +340,36 @@ def test_pool_relu_bwd_fused_equals_unfused(device, shape, k, s, p, method, slop
     assert torch.equal(du.view(torch.int32), df.view(torch.int32))
 
 
+@pytest.mark.parametrize("slope", [0.0, 0.1])
+def test_lrn_within_relu_bwd_fused_equals_unfused(device, slope):
+    """rram_lrn_within_relu_bwd == rram_lrn_within_bwd then rram_relu_bwd in
+    place (x = the ReLU's output = the LRN's bottom), bit for bit; CIFAR-10
+    full norm1's parameters (local_size 3, WITHIN_CHANNEL)."""
+    import torch
+    from rramsim import ops
+    torch.manual_seed(13)
+    N, C, H, W = 4, 32, 16, 16
+    x0 = 3 * torch.randn(N, C, H, W, device=device)
+    x = torch.where(x0 > 0, x0, x0 * slope)
+    x[0, 0, :2, :2] = -0.0
+    alpha, beta = 5e-5, 0.75
+    y, sc = torch.empty_like(x), torch.empty_like(x)
+    ops.lrn_within_fwd(x, y, sc, N, C, H, W, 3, alpha, beta)
+    dy = torch.randn_like(x)
+    du, df = torch.empty_like(x), torch.full_like(x, 7.0)
+    ops.lrn_within_bwd(x, sc, dy, du, N, C, H, W, 3, alpha, beta)
+    ops.relu_bwd(x, du, du, slope)
+    ops.lrn_within_relu_bwd(x, sc, dy, df, N, C, H, W, 3, alpha, beta, slope)
+    assert torch.equal(du.view(torch.int32), df.view(torch.int32))
+
+
 @pytest.mark.parametrize("net_name,phase", [("cifar10_quick", "test"), ("cifar10_full", "train")])
 def test_pool_relu_fold_in_net(device, net_name, phase):
     """Net folds the in-place ReLU after a Pooling layer (CIFAR-10 pool1 ->
     relu1) into the pool's store, and (TRAIN) the backward of an in-place ReLU
-    before a Pooling layer (relu2 -> pool2, relu3 -> pool3) into the pool's
-    backward: blobs, loss and every parameter gradient equal to the net with
-    the folds off."""
+    before a Pooling or LRN layer (relu2 -> pool2, relu3 -> pool3, relu1 ->
+    norm1) into that layer's backward: blobs, loss and every parameter
+    gradient equal to the net with the folds off."""
     import torch
     from rramsim import caffe, models
     caffe.set_stream_from_torch()
