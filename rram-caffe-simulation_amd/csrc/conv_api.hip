@@ -12,12 +12,13 @@ int gemm_core(int trans_a, int trans_b, int M, int N, int K, float alpha, const 
 int conv_fwd_core(const rram_conv_desc* d, const float* x, const float* w, const float* bias,
                   float* y, int relu, hipStream_t s, int64_t y_img = 0);
 int conv_bwd_weight_core(const rram_conv_desc* d, int nimg, const float* dy, const float* col,
-                         int64_t ldcol, float* dw, void* part, size_t part_bytes, hipStream_t s);
+                         int64_t ldcol, float* dw, void* part, size_t part_bytes, hipStream_t s,
+                         float* db = nullptr);
 int bwd_weight_split(int M, int N, int64_t K);
 int conv_bwd_data_col_core(const rram_conv_desc* d, int nimg, const float* w, const float* dy,
                            float* col, int64_t ldcol, hipStream_t s);
 int im2col_core(const float* im, int64_t im_img, int nimg, const rram_conv_desc* d, float* col,
-                int64_t ldcol, hipStream_t s);
+                int64_t ldcol, hipStream_t s, int ones_row = 0);
 int col2im_core(const float* col, int64_t ldcol, int nimg, const rram_conv_desc* d, float* im,
                 int64_t im_img, int accumulate, hipStream_t s);
 int gemv_core(int trans, int M, int N, float alpha, const float* A, const float* x, float beta,
@@ -284,14 +285,24 @@ int rram_conv2d_fwd_strided(const rram_conv_desc* d_in, const float* x, const vo
 namespace {
 // split-K partial buffer of the weight gradient (conv_bwd_weight_core) for
 // chunks of `imgs` images
+// (N = K + 1: room for the folded bias column, see rram_conv2d_bwd)
 size_t bwd_part_bytes(const rram_conv_desc& d, int imgs) {
   const int M = d.num_output / d.group;
-  const int N = d.channels / d.group * d.kernel_h * d.kernel_w;
+  const int N = d.channels / d.group * d.kernel_h * d.kernel_w + 1;
   const int sp = bwd_weight_split(M, N, (int64_t)imgs * d.out_h * d.out_w);
   return sp > 1 ? (size_t)sp * M * N * sizeof(float) : 0;
 }
+// the K column rows + the ones row of the folded bias gradient
 size_t col_bytes(const rram_conv_desc& d, int imgs) {
-  return (size_t)d.channels * d.kernel_h * d.kernel_w * (size_t)imgs * d.out_h * d.out_w * sizeof(float);
+  return ((size_t)d.channels * d.kernel_h * d.kernel_w + 1) * (size_t)imgs * d.out_h * d.out_w * sizeof(float);
+}
+// RRAM_BIAS_FOLD=0 (A/B runs): the bias gradient by its own partial + reduce kernels
+bool bias_fold_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("RRAM_BIAS_FOLD");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return on;
 }
 }  // namespace
 
@@ -310,7 +321,23 @@ int rram_conv2d_bwd(const rram_conv_desc* d_in, const float* x, const float* w, 
   RRAM_REQUIRE(dy != nullptr, "conv2d_bwd: dy is NULL");
   hipStream_t s = as_stream(st);
   const int HoWo = d.out_h * d.out_w;
-  if (db) {
+  // The bias gradient folded into the weight-gradient GEMM (one more output
+  // column against a ones row of the column matrix, summed by the split-K
+  // reduce): no bias kernels.  Ungrouped layers whose weight GEMM is split
+  // (partials in the workspace) and whose every image chunk has >= 2 K-tiles.
+  bool fold_db = false;
+  if (db && dw && x && w && ws && d.group == 1 && HoWo >= 2 * 32 && bias_fold_enabled()) {
+    const size_t per_img = col_bytes(d, 1);
+    int chunk = ws_bytes >= per_img ? static_cast<int>(ws_bytes / per_img) : 0;
+    if (chunk > d.num) chunk = d.num;
+    size_t pb = chunk > 0 ? bwd_part_bytes(d, chunk) : 0;
+    while (chunk > 1 && col_bytes(d, chunk) + pb > ws_bytes) {
+      --chunk;
+      pb = bwd_part_bytes(d, chunk);
+    }
+    fold_db = chunk >= 1 && pb > 0 && (col_bytes(d, chunk) + 255) / 256 * 256 + pb <= ws_bytes;
+  }
+  if (db && !fold_db) {
     const int S = d.num < 64 ? d.num : 64;
     if (ws && S > 1 && ws_bytes >= (size_t)d.num_output * S * sizeof(float)) {
       // the workspace head holds the partials; the passes below reuse it after
@@ -384,9 +411,10 @@ int rram_conv2d_bwd(const rram_conv_desc* d_in, const float* x, const float* w, 
     const int nimg = (d.num - n0) < chunk ? (d.num - n0) : chunk;
     const int64_t ldcol = (int64_t)nimg * HoWo;
     if (dw) {
-      rc = im2col_core(x + n0 * chw, chw, nimg, &d, col, ldcol, s);
+      rc = im2col_core(x + n0 * chw, chw, nimg, &d, col, ldcol, s, fold_db ? 1 : 0);
       if (rc) return rc;
-      rc = conv_bwd_weight_core(&d, nimg, dy + n0 * ohw, col, ldcol, dw, part, part ? part_bytes : 0, s);
+      rc = conv_bwd_weight_core(&d, nimg, dy + n0 * ohw, col, ldcol, dw, part, part ? part_bytes : 0, s,
+                                fold_db ? db : nullptr);
       if (rc) return rc;
     }
     if (dx && !dx_fwd) {

@@ -1206,6 +1206,10 @@ __global__ void __launch_bounds__(256)
   const int HoWo = Ho * Wo;
   const int P = nimg * HoWo;
   float* dst = col + (int64_t)krow * ldcol;
+  if (krow == C * KH * KW) {  // the ones row (im2col_core ones_row: bias gradient in the dW GEMM)
+    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) dst[p] = 1.0f;
+    return;
+  }
   const float* src = im + (int64_t)c * H * W;
   for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
     const uint32_t n = fdiv(static_cast<uint32_t>(p), howo);
@@ -1232,6 +1236,11 @@ __global__ void __launch_bounds__(256)
   const int kw = krow % KW, kh = (krow / KW) % KH, c = krow / (KW * KH);
   const int P4 = nimg * Ho * Wo / 4;
   float4* dst = reinterpret_cast<float4*>(col + (int64_t)krow * ldcol);
+  if (krow == C * KH * KW) {  // the ones row (see k_im2col)
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < P4; q += gridDim.x * blockDim.x)
+      dst[q] = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+    return;
+  }
   const float* src = im + (int64_t)c * H * W;
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < P4; q += gridDim.x * blockDim.x) {
     const uint32_t p = 4u * static_cast<uint32_t>(q);
@@ -1807,12 +1816,43 @@ int bwd_weight_split(int M, int N, int64_t K) {
 
 // dW_g[co][k] += sum_p dY_g[co][p] col_g[k][p]   (col: [Cin*kh*kw][ldcol]);
 // part (nullable): part_bytes of split-K partials (see bwd_weight_split)
+// db (nullable; ungrouped only, part required): the bias gradient as one more
+// GEMM column against the ones row im2col_core wrote after the K column rows,
+// always split (>= 2), the reduce routing column K to db
 int conv_bwd_weight_core(const rram_conv_desc* d, int nimg, const float* dy, const float* col,
-                         int64_t ldcol, float* dw, void* part, size_t part_bytes, hipStream_t s) {
+                         int64_t ldcol, float* dw, void* part, size_t part_bytes, hipStream_t s, float* db) {
   const int g = d->group;
   const int cin_g = d->channels / g, cout_g = d->num_output / g;
   const int K = cin_g * d->kernel_h * d->kernel_w;
   const int HoWo = d->out_h * d->out_w;
+  RRAM_REQUIRE(db == nullptr || (g == 1 && part != nullptr), "conv bwd weight: folded bias needs group 1 + partials");
+  if (db) {
+    Params P{};
+    P.M = cout_g;
+    P.N = K + 1;
+    P.K = nimg * HoWo;
+    P.a = make_view(dy, HoWo, cout_g, P.K);
+    P.a.img = (int64_t)d->num_output * HoWo;
+    P.a.hw = make_fastdiv(HoWo);
+    P.b = make_view(col, ldcol, K + 1, P.K);
+    P.e = make_epi(dw, K, 1.0f, 1.0f, nullptr, 0, 0);
+    const int bm = vec_ok(P.b.p, ldcol, P.K) ? KCV : KC;
+    int split = std::max(2, bwd_weight_split(P.M, P.N, P.K));
+    while (split > 2 && (size_t)split * P.M * P.N * sizeof(float) > part_bytes) --split;
+    int chunk = (P.K + split - 1) / split;
+    chunk = (chunk + BK - 1) / BK * BK;
+    split = (P.K + chunk - 1) / chunk;
+    RRAM_REQUIRE(split >= 2 && (size_t)split * P.M * P.N * sizeof(float) <= part_bytes,
+                 "conv bwd weight: folded bias needs >= 2 K splits");
+    P.split = split;
+    P.k_chunk = chunk;
+    P.ws = static_cast<float*>(part);
+    int rc = dispatch(NCHW, bm, OUT_ROWMAJOR, P, split, s, true);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_splitk_reduce_dwdb, dim3(stream_blocks((int64_t)P.M * P.N)), dim3(256), 0, s, P.ws, split,
+                       P.M, K, dw, db);
+    return launch_status("conv bwd weight + bias split-K reduce");
+  }
   for (int gi = 0; gi < g; ++gi) {
     Params P{};
     P.M = cout_g;
@@ -1876,10 +1916,11 @@ int conv_bwd_data_col_core(const rram_conv_desc* d, int nimg, const float* w, co
 }
 
 int im2col_core(const float* im, int64_t im_img, int nimg, const rram_conv_desc* d, float* col,
-                int64_t ldcol, hipStream_t s) {
+                int64_t ldcol, hipStream_t s, int ones_row) {
   const int64_t total = (int64_t)nimg * d->channels * d->kernel_h * d->kernel_w * d->out_h * d->out_w;
   if (total == 0) return RRAM_OK;
-  const int rows = d->channels * d->kernel_h * d->kernel_w;
+  // ones_row: one more row of 1.0 after the Cin*kh*kw column rows
+  const int rows = d->channels * d->kernel_h * d->kernel_w + (ones_row ? 1 : 0);
   const int64_t P = (int64_t)nimg * d->out_h * d->out_w;
   RRAM_REQUIRE(P < (1ll << 31) && (int64_t)nimg * im_img < (1ll << 31) && rows < 65536,
                "im2col: more than 2^31 positions / input elements or 65535 rows is not supported");

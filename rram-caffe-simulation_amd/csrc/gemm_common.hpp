@@ -341,6 +341,26 @@ __global__ void __launch_bounds__(256) k_splitk_reduce_nchw(const float* __restr
   }
 }
 
+// k_splitk_reduce of the weight gradient with the bias folded in (N = K + 1
+// columns): column K goes to db, the rest to dw [M][K]; dst += sum in split
+// order, as k_splitk_reduce's alpha = beta = 1 path
+__global__ void __launch_bounds__(256) k_splitk_reduce_dwdb(const float* __restrict__ ws, int split, int M, int K,
+                                                            float* __restrict__ dw, float* __restrict__ db) {
+  const int N = K + 1;
+  const int64_t total = (int64_t)M * N;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.0f;
+    for (int z = 0; z < split; ++z) s += ws[(int64_t)z * total + idx];
+    const int m = static_cast<int>(idx / N);
+    const int n = static_cast<int>(idx - (int64_t)m * N);
+    float* dst = n < K ? dw + (int64_t)m * K + n : db + m;
+    float o = 1.0f * s;
+    o += 1.0f * *dst;
+    *dst = o;
+  }
+}
+
 namespace g2 {
 typedef int int4v __attribute__((ext_vector_type(4)));
 

@@ -855,3 +855,36 @@ def test_conv_fwd_split_k_vs_fp64(device, shape, cout, k, pad, relu):
     ops.conv2d_fwd(d, T(x, device), T(w, device), T(b, device), y, relu=relu)
     ref, scale = conv64(x, w, b, 1, pad)
     assert_scaled(N(y), ref, scale, "conv fwd split-K", tol=2e-6, relu=relu)
+
+
+@pytest.mark.parametrize("shape,cout,k,pad,chunk", [
+    ((100, 3, 32, 32), 32, 5, 2, None),     # CIFAR-10 full conv1 (bias folded into the dW GEMM)
+    ((100, 32, 16, 16), 32, 5, 2, None),    # conv2
+    ((100, 32, 8, 8), 64, 5, 2, None),      # conv3
+    ((9, 16, 8, 8), 24, 3, 1, 2),           # workspace for 2 images: chunks of 2 and a last one of 1
+])
+def test_conv_bwd_bias_folded_vs_fp64(device, shape, cout, k, pad, chunk):
+    """The conv bias gradient as one more column of the split weight-gradient
+    GEMM (a ones row after the im2col rows; k_splitk_reduce_dwdb routes it to
+    db) accumulates into db like the separate reduction: db, dW and dX within
+    1e-5 of sum|a*b| of float64, over several image chunks too."""
+    import torch
+    from rramsim import ops
+    import _ref64 as R
+    torch.manual_seed(3)
+    x = torch.randn(shape)
+    w = torch.randn(cout, shape[1], k, k) * 0.1
+    b = torch.randn(cout)
+    fwd = lambda xx, ww, bb: torch.nn.functional.conv2d(xx, ww, bb, 1, pad)  # noqa: E731
+    dy = torch.randn_like(fwd(x, w, b))
+    (gx, gw, gb), (sx, sw, sb) = _bwd_ref64(fwd, (x, w, b), dy)
+    d = ops.conv_desc(shape, cout, k, 1, pad)
+    dw = torch.full_like(w, 0.25, device=device)          # accumulates: += on 0.25 / -0.5
+    db = torch.full_like(b, -0.5, device=device)
+    dx = torch.empty_like(x, device=device)
+    ws = torch.empty(ops.conv2d_bwd_workspace(d, chunk or shape[0]) // 4 + 64, device=device)
+    ops.conv2d_bwd(d, x.to(device), w.to(device), dy.to(device), dw, db, dx, ws)
+    torch.cuda.synchronize()
+    R.assert_scaled(dw.cpu().numpy() - 0.25, gw, sw, "dW", tol=1e-5)
+    R.assert_scaled(db.cpu().numpy() + 0.5, gb, sb, "db", tol=1e-5)
+    R.assert_scaled(dx.cpu().numpy(), gx, sx, "dX", tol=1e-5)
