@@ -515,15 +515,29 @@ int rram_softmax_fwd(const float* x, float* y, int outer, int channels, int inne
 int rram_softmax_loss_fwd(const float* prob, const float* label, float* loss_out,
                           int outer, int channels, int inner, int ignore_label,
                           rram_stream_t s);
+/* rram_softmax_loss_fwd that also folds the loss into a MonteCarlo statistic:
+ * *acc_sum += loss, *acc_row = loss when non-NULL (rram_mc_accumulate's
+ * arithmetic for that output, so the MC driver needs no accumulate launch). */
+int rram_softmax_loss_fwd_acc(const float* prob, const float* label, float* out, int outer, int C, int inner,
+                              int ignore, float* acc_sum, float* acc_row, rram_stream_t s);
 int rram_softmax_loss_bwd(const float* prob, const float* label, float* dx,
                           int outer, int channels, int inner, int ignore_label,
                           float loss_weight, rram_stream_t s);
+/* rram_softmax_loss_fwd and rram_softmax_loss_bwd in one launch (a TRAIN-phase
+ * SoftmaxWithLoss head of <= 65536 elements: CIFAR-10 / LeNet): out = the
+ * loss, dx = the bottom gradient, both bit-identical to the two calls. */
+int rram_softmax_loss_fwd_bwd(const float* prob, const float* label, float* out, float* dx, int outer, int C,
+                              int inner, int ignore, float loss_weight, rram_stream_t s);
 /* Top-k accuracy (accuracy_layer.cpp:48-90): correct_out[0] = #correct,
  * count_out[0] = #counted, ratio_out[0] (nullable) = #correct / #counted
  * (device floats; the layer's top). */
 int rram_accuracy(const float* x, const float* label, float* correct_out,
                   float* count_out, float* ratio_out, int outer, int channels,
                   int inner, int top_k, int ignore_label, rram_stream_t s);
+/* rram_accuracy with the same MonteCarlo fold of the ratio (see
+ * rram_softmax_loss_fwd_acc; acc_sum requires ratio). */
+int rram_accuracy_acc(const float* x, const float* label, float* correct, float* count, float* ratio, int outer,
+                      int C, int inner, int top_k, int ignore, float* acc_sum, float* acc_row, rram_stream_t s);
 /* EuclideanLoss (euclidean_loss_layer.cu:9-38): diff = a - b,
  * loss_out[0] = sum(diff^2) / num / 2 (device scalar, the layer's top);
  * backward dx = alpha * diff with alpha = +-loss_weight / num. */

@@ -472,10 +472,12 @@ __global__ void __launch_bounds__(256) k_softmax_reg(const float* __restrict__ x
 }
 
 // softmax_loss_layer.cpp:95-112 (single block, deterministic)
+// acc_sum / acc_row (nullable): the MonteCarlo statistics of this output
+// (k_mc_accumulate's sum += v, row = v) written by the thread that stores v
 __global__ void __launch_bounds__(1024) k_softmax_loss_fwd(const float* __restrict__ prob,
                                                            const float* __restrict__ label,
                                                            float* out, int outer, int C, int inner,
-                                                           int ignore) {
+                                                           int ignore, float* acc_sum, float* acc_row) {
   __shared__ float sl[16], sc[16];
   float loss = 0.0f, cnt = 0.0f;
   const int64_t cols = (int64_t)outer * inner;
@@ -502,7 +504,64 @@ __global__ void __launch_bounds__(1024) k_softmax_loss_fwd(const float* __restri
       L += sl[i];
       N += sc[i];
     }
+    const float v = L / fmaxf(N, 1.0f);
+    out[0] = v;
+    if (acc_sum) *acc_sum += v;
+    if (acc_row) *acc_row = v;
+  }
+}
+
+// k_softmax_loss_fwd + k_softmax_loss_bwd in one block (TRAIN phase, small
+// heads): the loss in k_softmax_loss_fwd's order, then dx with
+// k_softmax_loss_bwd's expression; scale = scale_all (host: loss_weight /
+// (outer * inner)) without an ignore label, else loss_weight / max(#valid, 1)
+// as rram_softmax_loss_bwd forms it from k_count_valid's exact count
+__global__ void __launch_bounds__(1024) k_softmax_loss_fwd_bwd(const float* __restrict__ prob,
+                                                               const float* __restrict__ label, float* out,
+                                                               float* __restrict__ dx, int outer, int C, int inner,
+                                                               int ignore, float loss_weight, float scale_all) {
+  __shared__ float sl[16], sc[16], sscale;
+  float loss = 0.0f, cnt = 0.0f;
+  const int64_t cols = (int64_t)outer * inner;
+  for (int64_t col = threadIdx.x; col < cols; col += blockDim.x) {
+    const int64_t o = col / inner, q = col - o * inner;
+    const int lv = static_cast<int>(label[col]);
+    if (ignore >= 0 && lv == ignore) continue;
+    loss -= logf(fmaxf(prob[(o * C + lv) * inner + q], FLT_MIN));
+    cnt += 1.0f;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    loss += __shfl_xor(loss, off, 64);
+    cnt += __shfl_xor(cnt, off, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    sl[threadIdx.x >> 6] = loss;
+    sc[threadIdx.x >> 6] = cnt;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float L = 0.0f, N = 0.0f;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
+      L += sl[i];
+      N += sc[i];
+    }
     out[0] = L / fmaxf(N, 1.0f);
+    sscale = ignore >= 0 ? loss_weight / fmaxf(N, 1.0f) : scale_all;
+  }
+  __syncthreads();
+  const float scale_valid = sscale;
+  const int64_t total = cols * C;
+  for (int64_t idx = threadIdx.x; idx < total; idx += blockDim.x) {
+    const int64_t q = idx % inner;
+    const int c = static_cast<int>((idx / inner) % C);
+    const int64_t o = idx / inner / C;
+    const int lv = static_cast<int>(label[o * inner + q]);
+    if (ignore >= 0 && lv == ignore) {
+      dx[idx] = 0.0f;
+    } else {
+      dx[idx] = (prob[idx] - (c == lv ? 1.0f : 0.0f)) * scale_valid;
+    }
   }
 }
 
@@ -523,6 +582,7 @@ __global__ void k_softmax_loss_bwd(const float* __restrict__ prob, const float* 
   }
 }
 
+constexpr int kLossFusedMax = 65536;  // rram_softmax_loss_fwd_bwd: one block writes every dx
 __global__ void k_count_valid(const float* __restrict__ label, int64_t n, int ignore, float* out) {
   __shared__ float part[16];
   float c = 0.0f;
@@ -591,7 +651,8 @@ __device__ int g_acc_part[2 * kAccFusedBlocks];
 __device__ unsigned g_acc_ticket;
 __global__ void __launch_bounds__(256) k_accuracy_fused(const float* __restrict__ x, const float* __restrict__ label,
                                                         float* correct, float* count, float* ratio, int outer, int C,
-                                                        int inner, int top_k, int ignore) {
+                                                        int inner, int top_k, int ignore, float* acc_sum,
+                                                        float* acc_row) {
   __shared__ int sa[4], sc[4];
   __shared__ bool last;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -653,7 +714,10 @@ __global__ void __launch_bounds__(256) k_accuracy_fused(const float* __restrict_
     N = sc[0] + sc[1] + sc[2] + sc[3];
     *correct = static_cast<float>(A);
     *count = static_cast<float>(N);
-    if (ratio) *ratio = static_cast<float>(A) / static_cast<float>(N > 0 ? N : 1);
+    const float v = static_cast<float>(A) / static_cast<float>(N > 0 ? N : 1);
+    if (ratio) *ratio = v;
+    if (acc_sum) *acc_sum += v;
+    if (acc_row) *acc_row = v;
     g_acc_ticket = 0u;
   }
 }
@@ -665,7 +729,7 @@ __global__ void __launch_bounds__(256) k_accuracy_fused(const float* __restrict_
 constexpr int kAccSmall = 1 << 16;
 __global__ void __launch_bounds__(1024) k_accuracy_small(const float* __restrict__ x, const float* __restrict__ label,
                                                          float* correct, float* count, float* ratio, int outer, int C,
-                                                         int inner, int top_k, int ignore) {
+                                                         int inner, int top_k, int ignore, float* acc_sum, float* acc_row) {
   __shared__ int sa[16], sc[16];
   const int cols = outer * inner;
   int hits = 0, cnt = 0;
@@ -701,12 +765,19 @@ __global__ void __launch_bounds__(1024) k_accuracy_small(const float* __restrict
     }
     correct[0] = static_cast<float>(A);
     count[0] = static_cast<float>(N);
-    if (ratio) ratio[0] = static_cast<float>(A) / fmaxf(static_cast<float>(N), 1.0f);
+    const float v = static_cast<float>(A) / fmaxf(static_cast<float>(N), 1.0f);
+    if (ratio) ratio[0] = v;
+    if (acc_sum) *acc_sum += v;
+    if (acc_row) *acc_row = v;
   }
 }
 
-__global__ void k_accuracy_ratio(const float* correct, const float* count, float* ratio) {
-  ratio[0] = correct[0] / fmaxf(count[0], 1.0f);
+__global__ void k_accuracy_ratio(const float* correct, const float* count, float* ratio, float* acc_sum,
+                                 float* acc_row) {
+  const float v = correct[0] / fmaxf(count[0], 1.0f);
+  ratio[0] = v;
+  if (acc_sum) *acc_sum += v;
+  if (acc_row) *acc_row = v;
 }
 
 // concat_layer.cu Concat kernel (axis 1)
@@ -940,11 +1011,28 @@ int rram_softmax_fwd(const float* x, float* y, int outer, int C, int inner, rram
 
 int rram_softmax_loss_fwd(const float* prob, const float* label, float* out, int outer, int C,
                           int inner, int ignore, rram_stream_t s) {
+  return rram_softmax_loss_fwd_acc(prob, label, out, outer, C, inner, ignore, nullptr, nullptr, s);
+}
+int rram_softmax_loss_fwd_acc(const float* prob, const float* label, float* out, int outer, int C, int inner,
+                              int ignore, float* acc_sum, float* acc_row, rram_stream_t s) {
   RRAM_REQUIRE(outer >= 0 && C > 0 && inner > 0 && out, "softmax_loss_fwd: bad args");
   RRAM_REQUIRE(outer == 0 || (prob && label), "softmax_loss_fwd: NULL");
+  RRAM_REQUIRE(acc_row == nullptr || acc_sum != nullptr, "softmax_loss_fwd: acc_row without acc_sum");
   hipLaunchKernelGGL(k_softmax_loss_fwd, dim3(1), dim3(1024), 0, as_stream(s), prob, label, out,
-                     outer, C, inner, ignore);
+                     outer, C, inner, ignore, acc_sum, acc_row);
   return launch_status("softmax_loss_fwd");
+}
+
+int rram_softmax_loss_fwd_bwd(const float* prob, const float* label, float* out, float* dx, int outer, int C,
+                              int inner, int ignore, float loss_weight, rram_stream_t s) {
+  RRAM_REQUIRE(outer >= 0 && C > 0 && inner > 0 && out, "softmax_loss_fwd_bwd: bad args");
+  const int64_t total = (int64_t)outer * C * inner;
+  RRAM_REQUIRE(total <= kLossFusedMax, "softmax_loss_fwd_bwd: more than %d elements", kLossFusedMax);
+  RRAM_REQUIRE(outer == 0 || (prob && label && dx), "softmax_loss_fwd_bwd: NULL");
+  const float scale_all = loss_weight / static_cast<float>((int64_t)outer * inner);
+  hipLaunchKernelGGL(k_softmax_loss_fwd_bwd, dim3(1), dim3(1024), 0, as_stream(s), prob, label, out, dx, outer, C,
+                     inner, ignore, loss_weight, scale_all);
+  return launch_status("softmax_loss_fwd_bwd");
 }
 
 int rram_softmax_loss_bwd(const float* prob, const float* label, float* dx, int outer, int C,
@@ -974,6 +1062,12 @@ int rram_softmax_loss_bwd(const float* prob, const float* label, float* dx, int 
 
 int rram_accuracy(const float* x, const float* label, float* correct, float* count, float* ratio,
                   int outer, int C, int inner, int top_k, int ignore, rram_stream_t s) {
+  return rram_accuracy_acc(x, label, correct, count, ratio, outer, C, inner, top_k, ignore, nullptr, nullptr, s);
+}
+int rram_accuracy_acc(const float* x, const float* label, float* correct, float* count, float* ratio, int outer,
+                      int C, int inner, int top_k, int ignore, float* acc_sum, float* acc_row, rram_stream_t s) {
+  RRAM_REQUIRE(acc_row == nullptr || acc_sum != nullptr, "accuracy: acc_row without acc_sum");
+  RRAM_REQUIRE(acc_sum == nullptr || ratio != nullptr, "accuracy: acc_sum needs the ratio output");
   RRAM_REQUIRE(outer >= 0 && C > 0 && inner > 0 && top_k >= 1 && correct && count,
                "accuracy: bad args");
   RRAM_REQUIRE(outer == 0 || (x && label), "accuracy: NULL");
@@ -981,12 +1075,12 @@ int rram_accuracy(const float* x, const float* label, float* correct, float* cou
   RRAM_REQUIRE(cols < (1ll << 24), "accuracy: more than 2^24 samples (float counts would round)");
   if (cols * C <= kAccSmall && C <= 64) {
     hipLaunchKernelGGL(k_accuracy_small, dim3(1), dim3(1024), 0, as_stream(s), x, label, correct, count, ratio,
-                       outer, C, inner, top_k, ignore);
+                       outer, C, inner, top_k, ignore, acc_sum, acc_row);
     return launch_status("accuracy");
   }
   if (cols > 0 && (cols + 3) / 4 <= kAccFusedBlocks) {
     hipLaunchKernelGGL(k_accuracy_fused, dim3(static_cast<unsigned>((cols + 3) / 4)), dim3(256), 0, as_stream(s), x,
-                       label, correct, count, ratio, outer, C, inner, top_k, ignore);
+                       label, correct, count, ratio, outer, C, inner, top_k, ignore, acc_sum, acc_row);
     return launch_status("accuracy");
   }
   RRAM_HIP_RET(hipMemsetAsync(correct, 0, sizeof(float), as_stream(s)));
@@ -994,7 +1088,8 @@ int rram_accuracy(const float* x, const float* label, float* correct, float* cou
   if (cols > 0)
     hipLaunchKernelGGL(k_accuracy, dim3(static_cast<unsigned>((cols + 3) / 4)), dim3(256), 0, as_stream(s), x,
                        label, correct, count, outer, C, inner, top_k, ignore);
-  if (ratio) hipLaunchKernelGGL(k_accuracy_ratio, dim3(1), dim3(1), 0, as_stream(s), correct, count, ratio);
+  if (ratio)
+    hipLaunchKernelGGL(k_accuracy_ratio, dim3(1), dim3(1), 0, as_stream(s), correct, count, ratio, acc_sum, acc_row);
   return launch_status("accuracy");
 }
 

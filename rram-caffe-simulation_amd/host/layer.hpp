@@ -99,6 +99,12 @@ class Layer {
   // applies the ReLU's backward factor to the bottom diff it writes
   // (rram_pool_relu_bwd); the ReLU's Backward then does nothing
   virtual bool fuse_relu_before_bwd(float /*slope*/) { return false; }
+  // MonteCarlo statistics folded into the producer of a scalar output
+  // (Accuracy, SoftmaxWithLoss in TEST): while set, Forward also does
+  // *sum += top, *row = top (row nullable) in the kernel that stores the top,
+  // so the MC driver launches no accumulate kernel.  sum == nullptr clears it;
+  // false: the layer cannot (the driver then accumulates itself).
+  virtual bool set_top_accumulator(float* /*sum*/, float* /*row*/) { return false; }
   // TEST-phase Concat fold (Net::Net): a producer whose top only feeds a
   // channel Concat writes its output straight into the Concat top at a
   // channel offset (write_into_concat: true when it can), and the Concat then

@@ -697,15 +697,30 @@ class SoftmaxWithLossLayer : public Layer<Dtype> {
     top[0]->Reshape({});
     if (top.size() > 1) top[1]->ReshapeLike(*bottom[0]);
   }
+  bool set_top_accumulator(float* sum, float* row) override {
+    if (this->phase_ == TRAIN && sum) return false;  // the TRAIN head (loss + dx in one launch) has no fold
+    acc_sum_ = sum;
+    acc_row_ = sum ? row : nullptr;
+    return true;
+  }
 
  protected:
   void Forward_gpu(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
     int o, c, i;
     softmax_dims(*bottom[0], axis_, o, c, i);
-    // (a one-block fused softmax+loss measured slower on the CIFAR-10 quick MC head: latency-bound)
+    // (a one-block fused softmax + loss measured slower on the CIFAR-10 quick MC head: latency-bound)
     RRAM_CALL(rram_softmax_fwd(bottom[0]->gpu_data(), prob_.mutable_gpu_data(), o, c, i, Caffe::stream()));
-    RRAM_CALL(rram_softmax_loss_fwd(prob_.gpu_data(), bottom[1]->gpu_data(), top[0]->mutable_gpu_data(), o,
-                                    c, i, ignore_, Caffe::stream()));
+    // TRAIN, small head: the bottom gradient in the same launch as the loss
+    // (Backward then has nothing left to do; writing it when no backward
+    // follows is harmless: nothing else writes this diff)
+    dx_in_fwd_ = this->phase_ == TRAIN && (int64_t)o * c * i <= 65536;
+    if (dx_in_fwd_)
+      RRAM_CALL(rram_softmax_loss_fwd_bwd(prob_.gpu_data(), bottom[1]->gpu_data(), top[0]->mutable_gpu_data(),
+                                          bottom[0]->mutable_gpu_diff(), o, c, i, ignore_, this->loss(0),
+                                          Caffe::stream()));
+    else
+      RRAM_CALL(rram_softmax_loss_fwd_acc(prob_.gpu_data(), bottom[1]->gpu_data(), top[0]->mutable_gpu_data(), o,
+                                          c, i, ignore_, acc_sum_, acc_row_, Caffe::stream()));
     if (top.size() > 1)
       HIP_CALL(hipMemcpyAsync(top[1]->mutable_gpu_data(), prob_.gpu_data(), prob_.count() * sizeof(Dtype),
                               hipMemcpyDeviceToDevice, Caffe::hip_stream()));
@@ -713,7 +728,7 @@ class SoftmaxWithLossLayer : public Layer<Dtype> {
   void Backward_gpu(const std::vector<Blob<Dtype>*>&, const std::vector<bool>& pd,
                     const std::vector<Blob<Dtype>*>& bottom) override {
     CAFFE_CHECK(pd.size() < 2 || !pd[1], this->name() << " cannot backpropagate to label inputs");
-    if (!pd.size() || !pd[0]) return;
+    if (!pd.size() || !pd[0] || dx_in_fwd_) return;
     int o, c, i;
     softmax_dims(*bottom[0], axis_, o, c, i);
     RRAM_CALL(rram_softmax_loss_bwd(prob_.gpu_data(), bottom[1]->gpu_data(), bottom[0]->mutable_gpu_diff(),
@@ -721,6 +736,8 @@ class SoftmaxWithLossLayer : public Layer<Dtype> {
   }
   Blob<Dtype> prob_;
   int ignore_ = -1, axis_ = 1;
+  bool dx_in_fwd_ = false;
+  float *acc_sum_ = nullptr, *acc_row_ = nullptr;  // set_top_accumulator (TEST)
 };
 
 // --------------------------------------------------------------- Accuracy
@@ -746,19 +763,26 @@ class AccuracyLayer : public Layer<Dtype> {
     counts_.Reshape({2});
   }
   bool AllowForceBackward(int) const override { return false; }
+  bool set_top_accumulator(float* sum, float* row) override {
+    acc_sum_ = sum;
+    acc_row_ = sum ? row : nullptr;
+    return true;
+  }
 
  protected:
   void Forward_gpu(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override {
     int o, c, i;
     softmax_dims(*bottom[0], axis_, o, c, i);
     float* cnt = counts_.mutable_gpu_data();
-    RRAM_CALL(rram_accuracy(bottom[0]->gpu_data(), bottom[1]->gpu_data(), cnt, cnt + 1,
-                            top[0]->mutable_gpu_data(), o, c, i, top_k_, ignore_, Caffe::stream()));
+    RRAM_CALL(rram_accuracy_acc(bottom[0]->gpu_data(), bottom[1]->gpu_data(), cnt, cnt + 1,
+                                top[0]->mutable_gpu_data(), o, c, i, top_k_, ignore_, acc_sum_, acc_row_,
+                                Caffe::stream()));
   }
   void Backward_gpu(const std::vector<Blob<Dtype>*>&, const std::vector<bool>&,
                     const std::vector<Blob<Dtype>*>&) override {}
   int top_k_ = 1, axis_ = 1, ignore_ = -1;
   Blob<Dtype> counts_;
+  float *acc_sum_ = nullptr, *acc_row_ = nullptr;  // set_top_accumulator
 };
 
 // ----------------------------------------------------------------- Concat

@@ -982,7 +982,35 @@ void MonteCarlo<Dtype>::Run(uint32_t map_begin, uint32_t map_count) {
   // while conv1 runs beside it (conv1 0.400 -> 0.386 ms, +0.9 % maps/s;
   // profiles/r02_ab_mc_overlap.txt); serial, the default 2048
   const int prev_grid = rram_set_inject_grid(overlap_ ? 512 : 0);
+  // the statistics folded into the layers that store each scalar output
+  // (Layer::set_top_accumulator): no rram_mc_accumulate launch per map when
+  // every output's producer takes it (all or none)
+  std::vector<Layer<Dtype>*> acc_layers;
+  struct ClearAcc {  // the layers never keep pointers into this driver past Run (exceptions included)
+    std::vector<Layer<Dtype>*>& v;
+    ~ClearAcc() {
+      for (auto* a : v) a->set_top_accumulator(nullptr, nullptr);
+    }
+  } clear_acc{acc_layers};
+  {
+    const auto& L = net_->layers();
+    const auto& tops = net_->top_vecs();
+    for (size_t k = 0; k < no; ++k) {
+      Layer<Dtype>* prod = nullptr;
+      for (size_t l = 0; l < L.size(); ++l)
+        if (!tops[l].empty() && tops[l][0] == outs_[k]) prod = L[l].get();
+      if (!prod || !prod->set_top_accumulator(d_sums_ + k, nullptr)) {
+        for (auto* a : acc_layers) a->set_top_accumulator(nullptr, nullptr);
+        acc_layers.clear();
+        break;
+      }
+      acc_layers.push_back(prod);
+    }
+  }
   for (uint32_t m = map_begin; m < map_begin + map_count; ++m) {
+    for (size_t k = 0; k < acc_layers.size(); ++k)
+      acc_layers[k]->set_top_accumulator(d_sums_ + k, maps_run_ < max_maps_ ? d_per_map_ + (size_t)maps_run_ * no + k
+                                                                            : nullptr);
     if (m != map_begin)
       for (auto* p : params_) (void)p->mutable_gpu_data();
     hipStream_t is = Caffe::hip_stream();
@@ -1010,7 +1038,7 @@ void MonteCarlo<Dtype>::Run(uint32_t map_begin, uint32_t map_count) {
       net_->Forward(false);
     }
     if (reuse_prefix_) prefix_done_ = true;
-    for (size_t k0 = 0; k0 < no; k0 += RRAM_MC_MAX_OUTPUTS) {
+    for (size_t k0 = 0; acc_layers.empty() && k0 < no; k0 += RRAM_MC_MAX_OUTPUTS) {
       rram_mc_outputs mo{};
       mo.n = static_cast<int>(std::min<size_t>(RRAM_MC_MAX_OUTPUTS, no - k0));
       for (int k = 0; k < mo.n; ++k) mo.p[k] = outs_[k0 + k]->gpu_data();

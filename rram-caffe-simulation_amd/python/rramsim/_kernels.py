@@ -135,8 +135,11 @@ SIGNATURES = {
     "rram_lrn_maxpool_fwd_octets": (I, [P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, F, F, F, P]),
     "rram_softmax_fwd": (I, [P, P, I, I, I, P]),
     "rram_softmax_loss_fwd": (I, [P, P, P, I, I, I, I, P]),
+    "rram_softmax_loss_fwd_acc": (I, [P, P, P, I, I, I, I, P, P, P]),
     "rram_softmax_loss_bwd": (I, [P, P, P, I, I, I, I, F, P]),
+    "rram_softmax_loss_fwd_bwd": (I, [P, P, P, P, I, I, I, I, F, P]),
     "rram_accuracy": (I, [P, P, P, P, P, I, I, I, I, I, P]),
+    "rram_accuracy_acc": (I, [P, P, P, P, P, I, I, I, I, I, P, P, P]),
     "rram_concat_copy": (I, [P, P, I, I, I, I, I, P]),
     "rram_euclidean_loss_fwd": (I, [P, P, P, P, I64, I, P]),
     "rram_euclidean_loss_bwd": (I, [P, P, I64, F, P]),

@@ -355,6 +355,12 @@ def softmax_loss_bwd(prob, label, dx, outer, channels, inner, ignore=-1, loss_we
                                          loss_weight, _stream()), "softmax_loss_bwd")
 
 
+def softmax_loss_fwd_bwd(prob, label, loss, dx, outer, channels, inner, ignore=-1, loss_weight=1.0):
+    """softmax_loss_fwd + softmax_loss_bwd in one launch (<= 65536 elements)."""
+    K.check(_lib().rram_softmax_loss_fwd_bwd(_p(prob), _p(label), _p(loss), _p(dx), outer, channels, inner, ignore,
+                                             loss_weight, _stream()), "softmax_loss_fwd_bwd")
+
+
 def concat_copy(src, dst, num, src_cxi, dst_cxi, off_xi, backward=False):
     K.check(_lib().rram_concat_copy(_p(src), _p(dst), num, src_cxi, dst_cxi, off_xi, int(backward),
                                     _stream()), "concat")

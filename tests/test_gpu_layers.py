@@ -425,6 +425,26 @@ def test_lrn_within_matches_numpy_oracle(device, oracle_mod):
     np.testing.assert_allclose(y.cpu().numpy(), ref, rtol=2e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("outer,C,inner,ignore,lw", [(100, 10, 1, -1, 1.0), (64, 10, 1, 3, 1.0),
+                                                     (7, 5, 9, -1, 0.5), (3, 1000, 1, 2, 2.0)])
+def test_softmax_loss_fused_fwd_bwd_equals_separate(device, outer, C, inner, ignore, lw):
+    """rram_softmax_loss_fwd_bwd (the TRAIN-phase head in one launch) gives
+    the loss and dx of rram_softmax_loss_fwd + rram_softmax_loss_bwd bit for
+    bit, with and without an ignore label and a loss weight."""
+    import torch
+    from rramsim import ops
+    torch.manual_seed(14)
+    prob = torch.softmax(torch.randn(outer, C, inner, device=device), dim=1).contiguous()
+    label = torch.randint(0, C, (outer, inner), device=device).float()
+    l1, l2 = torch.zeros(1, device=device), torch.full((1,), 7.0, device=device)
+    d1, d2 = torch.empty_like(prob), torch.full_like(prob, 7.0)
+    ops.softmax_loss_fwd(prob, label, l1, outer, C, inner, ignore)
+    ops.softmax_loss_bwd(prob, label, d1, outer, C, inner, ignore, lw)
+    ops.softmax_loss_fwd_bwd(prob, label, l2, d2, outer, C, inner, ignore, lw)
+    assert torch.equal(l1.view(torch.int32), l2.view(torch.int32))
+    assert torch.equal(d1.view(torch.int32), d2.view(torch.int32))
+
+
 @pytest.mark.parametrize("inner", [1, 6])
 def test_softmax_loss_fwd_bwd_vs_autograd(device, inner):
     import torch
