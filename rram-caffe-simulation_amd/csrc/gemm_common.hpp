@@ -304,13 +304,29 @@ View make_view(const float* p, int64_t ld, int rows, int kdim) {
 }
 
 // split-K reduction + epilogue (row-major C only)
+// sum of the split-K partials of element idx in split order (s += p_0, p_1,
+// ...): the loads of 8 partials are issued together, the adds stay
+// sequential, so the result is the plain loop's bit for bit
+__device__ __forceinline__ float splitk_sum(const float* __restrict__ ws, int split, int64_t total, int64_t idx) {
+  float s = 0.0f;
+  int z = 0;
+  for (; z + 8 <= split; z += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = ws[(int64_t)(z + u) * total + idx];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; z < split; ++z) s += ws[(int64_t)z * total + idx];
+  return s;
+}
+
 __global__ void __launch_bounds__(256) k_splitk_reduce(const float* __restrict__ ws, int split, int M,
                                                        int N, Epi ep) {
   const int64_t total = (int64_t)M * N;
   for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
-    float s = 0.0f;
-    for (int z = 0; z < split; ++z) s += ws[(int64_t)z * total + idx];
+    const float s = splitk_sum(ws, split, total, idx);
     const int m = static_cast<int>(idx / N);
     const int n = static_cast<int>(idx - (int64_t)m * N);
     float* dst = ep.C + (int64_t)m * ep.ldc + n;
@@ -331,8 +347,7 @@ __global__ void __launch_bounds__(256) k_splitk_reduce_nchw(const float* __restr
   const int64_t total = (int64_t)M * N;
   for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
-    float s = 0.0f;
-    for (int z = 0; z < split; ++z) s += ws[(int64_t)z * total + idx];
+    const float s = splitk_sum(ws, split, total, idx);
     const int m = static_cast<int>(idx / N);
     const uint32_t n = static_cast<uint32_t>(idx - (int64_t)m * N);
     const uint32_t im = fdiv(n, ep.hw), sp = n - im * ep.hw.d;
@@ -350,8 +365,7 @@ __global__ void __launch_bounds__(256) k_splitk_reduce_dwdb(const float* __restr
   const int64_t total = (int64_t)M * N;
   for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
-    float s = 0.0f;
-    for (int z = 0; z < split; ++z) s += ws[(int64_t)z * total + idx];
+    const float s = splitk_sum(ws, split, total, idx);
     const int m = static_cast<int>(idx / N);
     const int n = static_cast<int>(idx - (int64_t)m * N);
     float* dst = n < K ? dw + (int64_t)m * K + n : db + m;
