@@ -1806,12 +1806,23 @@ int conv_fwd_core(const rram_conv_desc* d, const float* x, const float* w, const
 // so without a split the grid is a couple of blocks.  Aim for ~1024 blocks of
 // 64 x 64 (or 128 x 128) tiles with >= 512 K per split, <= 64 splits and
 // <= 256 MB of partials.
+// RRAM_DW_SPLIT_CAP / RRAM_DW_SPLIT_MINK (A/B runs; round 3-4 used 64 / 512):
+// the partials' reduce is cheap since k_splitk_reduce_wave, so the split may
+// go to 256 with >= 256 K per split (CIFAR-10 conv1's dW: 128 -> 512 workgroups)
 int bwd_weight_split(int M, int N, int64_t K) {
+  static const int cap = [] {
+    const char* e = getenv("RRAM_DW_SPLIT_CAP");
+    return e ? std::max(1, atoi(e)) : 256;
+  }();
+  static const int mink = [] {
+    const char* e = getenv("RRAM_DW_SPLIT_MINK");
+    return e ? std::max(32, atoi(e)) : 256;
+  }();
   const int64_t t = (M <= 64 || N <= 64) ? (int64_t)((M + 63) / 64) * ((N + 63) / 64)
                                          : (int64_t)((M + 127) / 128) * ((N + 127) / 128);
   int64_t sp = 1024 / (t > 0 ? t : 1);
-  if (sp > 64) sp = 64;
-  while (sp > 1 && K / sp < 512) --sp;
+  if (sp > cap) sp = cap;
+  while (sp > 1 && K / sp < mink) --sp;
   while (sp > 1 && sp * M * N * 4 > (256ll << 20)) --sp;
   return static_cast<int>(sp < 1 ? 1 : sp);
 }
@@ -1851,8 +1862,12 @@ int conv_bwd_weight_core(const rram_conv_desc* d, int nimg, const float* dy, con
     P.ws = static_cast<float*>(part);
     int rc = dispatch(NCHW, bm, OUT_ROWMAJOR, P, split, s, true);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_splitk_reduce_dwdb, dim3(stream_blocks((int64_t)P.M * P.N)), dim3(256), 0, s, P.ws, split,
-                       P.M, K, dw, db);
+    if (split >= 32)
+      hipLaunchKernelGGL(k_splitk_reduce_wave, dim3(static_cast<unsigned>(((int64_t)P.M * P.N + 3) / 4)), dim3(256), 0,
+                         s, P.ws, split, P.M, K, P.N, dw, db);
+    else
+      hipLaunchKernelGGL(k_splitk_reduce_dwdb, dim3(stream_blocks((int64_t)P.M * P.N)), dim3(256), 0, s, P.ws, split,
+                         P.M, K, dw, db);
     return launch_status("conv bwd weight + bias split-K reduce");
   }
   for (int gi = 0; gi < g; ++gi) {
@@ -1880,8 +1895,12 @@ int conv_bwd_weight_core(const rram_conv_desc* d, int nimg, const float* dy, con
       int rc = dispatch(NCHW, bm, OUT_ROWMAJOR, P, split, s, true);
       if (rc) return rc;
       // dw += sum of the partials (beta = 1), fixed summation order
-      hipLaunchKernelGGL(k_splitk_reduce, dim3(stream_blocks((int64_t)P.M * P.N)), dim3(256), 0, s, P.ws, split,
-                         P.M, P.N, P.e);
+      if (split >= 32)  // (dw of group gi: P.e.C)
+        hipLaunchKernelGGL(k_splitk_reduce_wave, dim3(static_cast<unsigned>(((int64_t)P.M * P.N + 3) / 4)), dim3(256),
+                           0, s, P.ws, split, P.M, P.N, P.N, P.e.C, nullptr);
+      else
+        hipLaunchKernelGGL(k_splitk_reduce, dim3(stream_blocks((int64_t)P.M * P.N)), dim3(256), 0, s, P.ws, split,
+                           P.M, P.N, P.e);
       rc = launch_status("conv bwd weight split-K reduce");
       if (rc) return rc;
       continue;

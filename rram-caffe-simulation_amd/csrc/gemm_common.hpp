@@ -375,6 +375,32 @@ __global__ void __launch_bounds__(256) k_splitk_reduce_dwdb(const float* __restr
   }
 }
 
+// The weight-gradient split-K reduce for few outputs over many splits
+// (CIFAR-10 conv1: 32 x 76 outputs, 256 partials each): one wave per output
+// element, lane l summing partials l, l + 64, ... in order, then a fixed xor
+// tree (deterministic; a different order than the sequential reduce's).
+// dst += sum: dw [M][K] for n < K, db (nullable: K + 1 columns) for n == K.
+__global__ void __launch_bounds__(256) k_splitk_reduce_wave(const float* __restrict__ ws, int split, int M, int K,
+                                                            int ncols, float* __restrict__ dw,
+                                                            float* __restrict__ db) {
+  const int lane = threadIdx.x & 63;
+  const int64_t total = (int64_t)M * ncols;
+  const int64_t idx = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (idx >= total) return;
+  float s = 0.0f;
+  for (int z = lane; z < split; z += 64) s += ws[(int64_t)z * total + idx];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) {
+    const int m = static_cast<int>(idx / ncols);
+    const int n = static_cast<int>(idx - (int64_t)m * ncols);
+    float* dst = n < K ? dw + (int64_t)m * K + n : db + m;
+    float o = 1.0f * s;
+    o += 1.0f * *dst;
+    *dst = o;
+  }
+}
+
 namespace g2 {
 typedef int int4v __attribute__((ext_vector_type(4)));
 
