@@ -1546,11 +1546,18 @@ int gemm_core(int trans_a, int trans_b, int M, int N, int K, float alpha, const 
   int split = 1;
   constexpr int target = 256;  // split-K target grid (blocks)
   // (kept for tiny products too: CIFAR-10 ip1 without the split measured
-  // slower, 8.1k -> 7.3k maps/s, profiles/r04_ab_tail_batched.txt)
-  if (ws != nullptr && tiles < target && K >= 1024) {
+  // slower, 8.1k -> 7.3k maps/s, profiles/r04_ab_tail_batched.txt).
+  // RRAM_GEMM_SPLIT_MINK (A/B runs; rounds 1-4: 1024): the least K that
+  // splits, and half of it the least K per split (LeNet ip1 / ip2, K = 800 /
+  // 500: a lone workgroup walking K is all latency)
+  static const int mink = [] {
+    const char* e = getenv("RRAM_GEMM_SPLIT_MINK");
+    return e ? std::max(64, atoi(e)) : 256;
+  }();
+  if (ws != nullptr && tiles < target && K >= mink) {
     split = static_cast<int>(target / (tiles > 0 ? tiles : 1));
     if (split > 16) split = 16;
-    while (split > 1 && (K / split) < 256) --split;
+    while (split > 1 && (K / split) < std::min(256, mink / 2)) --split;
     while (split > 1 && (size_t)split * M * N * sizeof(float) > ws_bytes) --split;
   }
   if (split > 1) {
