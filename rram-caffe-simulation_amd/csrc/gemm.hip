@@ -1544,7 +1544,8 @@ int gemm_core(int trans_a, int trans_b, int M, int N, int K, float alpha, const 
   // split-K when the 128x128 grid is far below the CU count and K is long
   const int64_t tiles = (int64_t)((N + 127) / 128) * ((M + 127) / 128);
   int split = 1;
-  constexpr int target = 256;  // split-K target grid (blocks)
+  // split-K target grid (blocks; 512 measured neutral, profiles/r04_ab_tail_batched.txt)
+  constexpr int target = 256;
   // (kept for tiny products too: CIFAR-10 ip1 without the split measured
   // slower, 8.1k -> 7.3k maps/s, profiles/r04_ab_tail_batched.txt).
   // RRAM_GEMM_SPLIT_MINK (A/B runs; rounds 1-4: 1024): the least K that
@@ -1556,7 +1557,7 @@ int gemm_core(int trans_a, int trans_b, int M, int N, int K, float alpha, const 
   }();
   if (ws != nullptr && tiles < target && K >= mink) {
     split = static_cast<int>(target / (tiles > 0 ? tiles : 1));
-    if (split > 16) split = 16;
+    if (split > target / 16) split = target / 16;
     while (split > 1 && (K / split) < std::min(256, mink / 2)) --split;
     while (split > 1 && (size_t)split * M * N * sizeof(float) > ws_bytes) --split;
   }
