@@ -40,6 +40,12 @@ int rram_device_synchronize(void);
  * HIP device (lazily built on first use).  Synchronises every device that
  * holds one; call only when no kernel of this library is in flight. */
 int rram_release_caches(void);
+/* Generation of this library's internal device scratch (the per-stream packed
+ * operand and split-K partial buffers, the convolution gather tables): bumped
+ * whenever one of them is freed or reallocated.  A caller that captured
+ * launches into a hipGraph (which holds raw pointers into that scratch)
+ * re-captures when it changes. */
+uint64_t rram_scratch_generation(void);
 
 /* ------------------------------------------------------------------------
  * Fault model

@@ -24,6 +24,7 @@ int col2im_core(const float* col, int64_t ldcol, int nimg, const rram_conv_desc*
 int gemv_core(int trans, int M, int N, float alpha, const float* A, const float* x, float beta,
               float* y, hipStream_t s);
 int release_conv_tables();
+std::atomic<uint64_t>& scratch_gen();
 int pack_octets(const float* x, void* oct, int num, int C, int HWi, hipStream_t s);
 std::atomic<int>& f32_engine();
 
@@ -115,16 +116,6 @@ __global__ void __launch_bounds__(256) k_flip_kernel(const float* __restrict__ w
   }
 }
 
-// RRAM_DX_FWD (A/B runs): 1 = stride-1 data gradients as a forward convolution
-// of dY with the flipped kernel (default), 0 = always data GEMM + col2im
-bool dx_fwd_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("RRAM_DX_FWD");
-    return e ? atoi(e) != 0 : true;
-  }();
-  return on;
-}
-
 int check_desc(const rram_conv_desc* d) {
   RRAM_REQUIRE(d != nullptr, "conv: desc is NULL");
   RRAM_REQUIRE(d->num >= 0 && d->channels > 0 && d->height > 0 && d->width > 0 &&
@@ -146,6 +137,8 @@ using namespace rram;
 extern "C" {
 
 int rram_release_caches(void) { return rram::release_conv_tables(); }
+
+uint64_t rram_scratch_generation(void) { return rram::scratch_gen().load(); }
 
 int rram_set_f32_engine(int engine) {
   RRAM_REQUIRE(engine == RRAM_ENGINE_F32 || engine == RRAM_ENGINE_BF16X6, "conv engine: unknown engine");
@@ -296,14 +289,6 @@ size_t bwd_part_bytes(const rram_conv_desc& d, int imgs) {
 size_t col_bytes(const rram_conv_desc& d, int imgs) {
   return ((size_t)d.channels * d.kernel_h * d.kernel_w + 1) * (size_t)imgs * d.out_h * d.out_w * sizeof(float);
 }
-// RRAM_BIAS_FOLD=0 (A/B runs): the bias gradient by its own partial + reduce kernels
-bool bias_fold_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("RRAM_BIAS_FOLD");
-    return e ? atoi(e) != 0 : true;
-  }();
-  return on;
-}
 }  // namespace
 
 size_t rram_conv2d_bwd_workspace(const rram_conv_desc* d_in, int images_per_chunk) {
@@ -326,7 +311,7 @@ int rram_conv2d_bwd(const rram_conv_desc* d_in, const float* x, const float* w, 
   // reduce): no bias kernels.  Ungrouped layers whose weight GEMM is split
   // (partials in the workspace) and whose every image chunk has >= 2 K-tiles.
   bool fold_db = false;
-  if (db && dw && x && w && ws && d.group == 1 && HoWo >= 2 * 32 && bias_fold_enabled()) {
+  if (db && dw && x && w && ws && d.group == 1 && HoWo >= 2 * 32) {
     const size_t per_img = col_bytes(d, 1);
     int chunk = ws_bytes >= per_img ? static_cast<int>(ws_bytes / per_img) : 0;
     if (chunk > d.num) chunk = d.num;
@@ -368,9 +353,9 @@ int rram_conv2d_bwd(const rram_conv_desc* d_in, const float* x, const float* w, 
   // The forward's grid must fill the chip: below ~128 tiles of 32 channels x
   // 128 positions (CIFAR conv3 100x32x8x8, LeNet conv2 64x20x12x12: 50 / 72)
   // each workgroup walks a long K = cout*k*k alone and the GEMM + col2im pair
-  // is 1.4-1.6x faster (scripts/dx_ab.py, profiles/r04_ab_dx_fwd.txt)
+  // is 1.4-1.6x faster (profiles/r04_ab_dx_fwd.txt)
   const int64_t dx_tiles = (int64_t)G * ((cin_g + 31) / 32) * (((int64_t)d.num * d.height * d.width + 127) / 128);
-  const bool dx_fwd = dx && dx_fwd_enabled() && dx_tiles >= 128 && d.stride_h == 1 && d.stride_w == 1 &&
+  const bool dx_fwd = dx && dx_tiles >= 128 && d.stride_h == 1 && d.stride_w == 1 &&
                       eph >= 0 && epw >= 0 &&
                       ws != nullptr && ws_bytes >= wt_bytes && wt_bytes < (1ull << 31) &&
                       (int64_t)d.num * d.height * d.width < (1ll << 31) &&

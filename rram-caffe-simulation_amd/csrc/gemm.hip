@@ -19,6 +19,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <array>
 #include <map>
 #include <tuple>
@@ -1492,10 +1493,17 @@ const int2* conv_table(const ConvGeom& cv, int K, bool padded, bool wide, hipStr
 
 }  // namespace
 
+// bumped whenever internal scratch is freed (rram_scratch_generation)
+std::atomic<uint64_t>& scratch_gen() {
+  static std::atomic<uint64_t> g{0};
+  return g;
+}
+
 // Frees every cached gather table (all devices).  Called by
 // rram_release_caches(); the caller guarantees no launch still reads them.
 int release_conv_tables() {
   std::lock_guard<std::mutex> g(conv_table_mutex());
+  scratch_gen().fetch_add(1);
   int cur = 0;
   (void)hipGetDevice(&cur);
   for (auto& kv : conv_table_cache()) {
@@ -1548,13 +1556,10 @@ int gemm_core(int trans_a, int trans_b, int M, int N, int K, float alpha, const 
   constexpr int target = 256;
   // (kept for tiny products too: CIFAR-10 ip1 without the split measured
   // slower, 8.1k -> 7.3k maps/s, profiles/r04_ab_tail_batched.txt).
-  // RRAM_GEMM_SPLIT_MINK (A/B runs; rounds 1-4: 1024): the least K that
-  // splits, and half of it the least K per split (LeNet ip1 / ip2, K = 800 /
-  // 500: a lone workgroup walking K is all latency)
-  static const int mink = [] {
-    const char* e = getenv("RRAM_GEMM_SPLIT_MINK");
-    return e ? std::max(64, atoi(e)) : 256;
-  }();
+  // the least K that splits, and half of it the least K per split (rounds
+  // 1-4: 1024; 256 since LeNet ip1 / ip2, K = 800 / 500: a lone workgroup
+  // walking K is all latency, profiles/r04_ab_tail_batched.txt)
+  constexpr int mink = 256;
   if (ws != nullptr && tiles < target && K >= mink) {
     split = static_cast<int>(target / (tiles > 0 ? tiles : 1));
     if (split > target / 16) split = target / 16;
@@ -1601,6 +1606,7 @@ float* stream_buffer(int slot, size_t floats, hipStream_t s) {
     if (hipStreamSynchronize(s) != hipSuccess) return nullptr;
     (void)hipFree(e.first);
     e = {nullptr, 0};
+    scratch_gen().fetch_add(1);
   }
   float* p = nullptr;
   if (hipMalloc(&p, floats * sizeof(float)) != hipSuccess) return nullptr;
@@ -1699,15 +1705,12 @@ int conv_patch_fwd(const rram_conv_desc* d, const float* w, Params& P, hipStream
 
 // split-K factor of the fp32 implicit-GEMM convolution forward (1: none):
 // ungrouped, M <= 64, K >= 256 and fewer than 256 output tiles of 32 or 64
-// rows x 128 positions, split toward RRAM_CONV_SPLIT workgroups (default
-// 1024, profiles/r04_ab_conv_split.txt; 0 turns it off, for A/B runs) with
-// >= 128 K per split
+// rows x 128 positions, split toward 1024 workgroups (512 / 2048 measured
+// slower, profiles/r04_ab_conv_split.txt and the round-4 sweep of
+// scripts/r04/gpu_r04_aq.sh) with >= 128 K per split
 int conv_fwd_split(const rram_conv_desc* d, int M, int N, int K) {
-  static const int target = [] {
-    const char* e = getenv("RRAM_CONV_SPLIT");
-    return e ? atoi(e) : 1024;
-  }();
-  if (target <= 0 || d->group != 1 || M > 64 || K < 256) return 1;
+  constexpr int target = 1024;
+  if (d->group != 1 || M > 64 || K < 256) return 1;
   const int64_t tiles = (int64_t)((M + 31) / 32) * ((N + 127) / 128);
   if (tiles >= 256) return 1;
   int split = static_cast<int>((target + tiles - 1) / tiles);
@@ -1814,18 +1817,12 @@ int conv_fwd_core(const rram_conv_desc* d, const float* x, const float* w, const
 // so without a split the grid is a couple of blocks.  Aim for ~1024 blocks of
 // 64 x 64 (or 128 x 128) tiles with >= 512 K per split, <= 64 splits and
 // <= 256 MB of partials.
-// RRAM_DW_SPLIT_CAP / RRAM_DW_SPLIT_MINK (A/B runs; round 3-4 used 64 / 512):
-// the partials' reduce is cheap since k_splitk_reduce_wave, so the split may
-// go to 256 with >= 256 K per split (CIFAR-10 conv1's dW: 128 -> 512 workgroups)
+// Rounds 3-4 capped it at 64 splits of >= 512 K; the partials' reduce is
+// cheap since k_splitk_reduce_wave, so the split goes to 256 with >= 256 K
+// per split (CIFAR-10 conv1's dW: 128 -> 512 workgroups; cap / min-K sweep in
+// profiles/r04_ab_tail_batched.txt)
 int bwd_weight_split(int M, int N, int64_t K) {
-  static const int cap = [] {
-    const char* e = getenv("RRAM_DW_SPLIT_CAP");
-    return e ? std::max(1, atoi(e)) : 256;
-  }();
-  static const int mink = [] {
-    const char* e = getenv("RRAM_DW_SPLIT_MINK");
-    return e ? std::max(32, atoi(e)) : 256;
-  }();
+  constexpr int cap = 256, mink = 256;
   const int64_t t = (M <= 64 || N <= 64) ? (int64_t)((M + 63) / 64) * ((N + 63) / 64)
                                          : (int64_t)((M + 127) / 128) * ((N + 127) / 128);
   int64_t sp = 1024 / (t > 0 ? t : 1);

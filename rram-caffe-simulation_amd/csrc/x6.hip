@@ -306,6 +306,21 @@ k_conv_patch_x6(Params P, const uint16_t* __restrict__ wpack, int PW, int CS) {
 // global loads: the loop is MFMA-paced.
 namespace cbx6 {
 constexpr int FRAG = 3 * 64;  // bf16x8 units per pre-split weight fragment (3 terms x 64 lanes)
+// Patch segment shift (chunks).  Within one image's rows the B column n of a
+// lane group sits at chunk 3 n + const (mod 16) (RPC = 3 OW mod 16), so the 16
+// lanes of a ds_read_b128 group hit 16 bank quads.  The next image's segment
+// starts KH halo rows later, which breaks that sequence (AlexNet conv3 / conv4:
+// 14 % of the B reads' LDS cycles were 2-way conflicts); shifting segment s by
+// s * dlt chunks restores it: dlt = 3 OW (1 - KH) (mod 16).  The gap chunks
+// hold nothing (their DMA lanes load out of range: zero).  The host sizes the
+// octet plane for the two shifts (up to 30 chunks).
+__device__ __forceinline__ int seg_shift(int OW, int KH) { return (3 * OW * (1 - KH)) & 15; }
+// column n of a lane past the tile's last position: the same column mod 16
+// inside the tile (its value is never stored), so a lane group keeps 16
+// distinct bank quads (clamping to plast made them collide in short tiles)
+__device__ __forceinline__ int clamp_col(int n, int n0, int plast) {
+  return n <= plast ? n : max(n0, n - (((n - plast) + 15) & ~15));
+}
 // first patch piece of K-tile kt + 1 staged at tap s (pieces spread evenly
 // over taps 0 .. T - 2)
 constexpr int piece_lo(int s, int PD, int T) { return s >= T - 1 ? PD : (s * PD + T - 2) / (T - 1); }
@@ -371,6 +386,7 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
   const int p2 = p1 + (nseg > 1 ? seg_last(1) + KH : 0);
   const int R = p2 + (nseg > 2 ? seg_last(2) + KH : 0);
   const int PW = cv.W + 2 * cv.pw;
+  const int dlt = cbx6::seg_shift(OW, KH);
   // LDS stage = [octet h][patch row: rpc chunks = positions x 3 terms + pad];
   // chunk c (16 B) of piece i of this wave = DMA lane's slot
   uint32_t poff[PD];
@@ -378,11 +394,13 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
   for (int i = 0; i < PD; ++i) {
     const int c = (wave * PD + i) * 64 + lane;
     const int h = static_cast<int>(fdiv(static_cast<uint32_t>(c), oct_div)), rem = c - h * (octb >> 4);
-    const int prow = static_cast<int>(fdiv(static_cast<uint32_t>(rem), rpc_div)), pc = rem - prow * rpc;
+    // segment of this chunk (segment s starts s * dlt chunks late), then its row
+    const int sg = (nseg > 2 && rem >= p2 * rpc + 2 * dlt) ? 2 : (nseg > 1 && rem >= p1 * rpc + dlt) ? 1 : 0;
+    const int r2 = rem - sg * dlt;
+    const int prow = static_cast<int>(fdiv(static_cast<uint32_t>(r2), rpc_div)), pc = r2 - prow * rpc;
     const int pcol = pc / 3, t = pc - pcol * 3;
     uint32_t off = 0x80000000u;
-    if (h < 2 && prow < R && pcol < PW) {
-      const int sg = prow >= p2 ? 2 : prow >= p1 ? 1 : 0;
+    if (h < 2 && prow < (sg == 0 ? p1 : sg == 1 ? p2 : R) && prow < R && pcol < PW) {
       const int y = (sg == 0 ? f0 + prow : prow - (sg == 1 ? p1 : p2)) - cv.ph;
       const int x = pcol - cv.pw;
       if (y >= 0 && y < cv.H && x >= 0 && x < cv.W)
@@ -395,12 +413,12 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
   int bb[NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
-    const int n = min(n0 + wc * 32 * NB + 32 * j + lr, plast);
+    const int n = cbx6::clamp_col(n0 + wc * 32 * NB + 32 * j + lr, n0, plast);
     const int img = static_cast<int>(fdiv(static_cast<uint32_t>(n), cv.howo)), sp = n - img * HW;
     const int oh = static_cast<int>(fdiv(static_cast<uint32_t>(sp), cv.wo_div)), ow = sp - oh * OW;
     const int sg = img - img0;
     const int prow = sg == 0 ? oh - f0 : (sg == 1 ? p1 : p2) + oh;
-    bb[j] = lh * octb + prow * rpc * 16 + ow * 48;
+    bb[j] = lh * octb + (prow * rpc + sg * dlt) * 16 + ow * 48;
   }
   floatx16 acc[1][NB];
 #pragma unroll
@@ -412,7 +430,11 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
     dma_b128(xrsrc, poff[i] + static_cast<uint32_t>(kt) * 2u * PL,
              lds0 + static_cast<uint32_t>(stg * SFB + (wave * PD + i) * 1024));
   };
-  x6::bf16x8 fa[2][3], fb[2][3];
+  // weight fragments: a ring of WD groups, loaded WD - 1 groups ahead (WD = 3
+  // when the tap count is a multiple of 3, so the ring slot of group (kt, s)
+  // is s % 3 at compile time: 3x3; else 2, by parity)
+  constexpr int WD = T % 3 == 0 ? 3 : 2;
+  x6::bf16x8 fa[WD][3], fb[2][3];
   auto read_b = [&](x6::bf16x8 (&f)[3], const char* st, int s, int j) {
     const int kh = s / KW, kw = s - kh * KW;
     const char* p = st + bb[j] + kh * rpc * 16 + kw * 48;
@@ -434,6 +456,7 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
 #pragma unroll
     for (int i = 0; i < PD; ++i) issue(0, 0, i);
     load_a(fa[0], 0);
+    if (WD == 3 && (T > 1 || KT > 1)) load_a(fa[1 % WD], 1);
     wait_vm<0>();
     __builtin_amdgcn_s_barrier();
     read_b(fb[0], smem, 0, 0);
@@ -445,7 +468,7 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
       char* nst = smem + ((kt + 1) & 1) * SFB + wave * PD * 1024 + lane * 16;
 #pragma unroll
       for (int s = 0; s < T; ++s) {
-        const int pa = (s + PAR) & 1;
+        const int pa = WD == 3 ? s % 3 : (s + PAR) & 1;
         const int q = kt * T + s;
         if (MORE) {
           // block 0: the pieces loaded at tap s - 1 into the next stage, this
@@ -461,7 +484,11 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
                 int4x, __builtin_amdgcn_raw_buffer_load_b128(
                            xr, static_cast<int>(poff[i] + static_cast<uint32_t>(kt + 1) * 2u * PL), 0, 0));
         }
-        if (s + 1 < T || MORE) load_a(fa[pa ^ 1], q + 1);
+        if constexpr (WD == 3) {
+          if (s + 2 < T || MORE) load_a(fa[(s + 2) % WD], q + 2);
+        } else {
+          if (s + 1 < T || MORE) load_a(fa[(pa + 1) % WD], q + 1);
+        }
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
           const bool last = s == T - 1 && j == NB - 1;
@@ -634,7 +661,13 @@ __device__ __forceinline__ void conv_epilogue_nchw16(floatx4 (&acc)[MI][NJ], con
   }
 }
 
-template <int KH, int KW, int WR, int NB, int PD, int OCC>
+// KTO = KT & 1 (the K-tile count's parity, host-checked): one tail shape per
+// instantiation.  With both tails in one kernel (a runtime branch after the
+// K-tile pair loop) the register allocator could not keep the loop's values
+// in place and the two-workgroups-per-CU forms spilled 12-68 bytes per lane
+// (conv2's 5 x 5: ~176 MB of scratch traffic per b256 launch, round 4);
+// per parity they take 184-188 VGPRs and no scratch.
+template <int KH, int KW, int WR, int NB, int PD, int OCC, int KTO>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __restrict__ xpack, int octb, int rpc,
                uint32_t xrange, int ximg, char* __restrict__ yoct, int cout8, FastDiv oct_div, FastDiv rpc_div,
@@ -688,15 +721,18 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
   const int p2 = p1 + (nseg > 1 ? seg_last(1) + KH : 0);
   const int R = p2 + (nseg > 2 ? seg_last(2) + KH : 0);
   const int PW = cv.W + 2 * cv.pw;
+  const int dlt = cbx6::seg_shift(OW, KH);
 #pragma unroll
   for (int i = 0; i < PD; ++i) {
     const int c = (wave * PD + i) * 64 + lane;
     const int h = static_cast<int>(fdiv(static_cast<uint32_t>(c), oct_div)), rem = c - h * (octb >> 4);
-    const int prow = static_cast<int>(fdiv(static_cast<uint32_t>(rem), rpc_div)), pc = rem - prow * rpc;
+    // segment of this chunk (segment s starts s * dlt chunks late), then its row
+    const int sg = (nseg > 2 && rem >= p2 * rpc + 2 * dlt) ? 2 : (nseg > 1 && rem >= p1 * rpc + dlt) ? 1 : 0;
+    const int r2 = rem - sg * dlt;
+    const int prow = static_cast<int>(fdiv(static_cast<uint32_t>(r2), rpc_div)), pc = r2 - prow * rpc;
     const int pcol = pc / 3, t = pc - pcol * 3;
     uint32_t off = 0x80000000u;
-    if (h < 2 && prow < R && pcol < PW) {
-      const int sg = prow >= p2 ? 2 : prow >= p1 ? 1 : 0;
+    if (h < 2 && prow < (sg == 0 ? p1 : sg == 1 ? p2 : R) && prow < R && pcol < PW) {
       const int y = (sg == 0 ? f0 + prow : prow - (sg == 1 ? p1 : p2)) - cv.ph;
       const int x = pcol - cv.pw;
       if (y >= 0 && y < cv.H && x >= 0 && x < cv.W)
@@ -712,12 +748,12 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
   int bb[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    const int n = min(n0 + wc * 32 * NB + 16 * j + c16, plast);
+    const int n = cbx6::clamp_col(n0 + wc * 32 * NB + 16 * j + c16, n0, plast);
     const int img = static_cast<int>(fdiv(static_cast<uint32_t>(n), cv.howo)), sp = n - img * HW;
     const int oh = static_cast<int>(fdiv(static_cast<uint32_t>(sp), cv.wo_div)), ow = sp - oh * OW;
     const int sg = img - img0;
     const int prow = sg == 0 ? oh - f0 : (sg == 1 ? p1 : p2) + oh;
-    bb[j] = (g & 1) * octb + prow * rpc * 16 + ow * 48;
+    bb[j] = (g & 1) * octb + (prow * rpc + sg * dlt) * 16 + ow * 48;
   }
   floatx4 acc[MI][NJ];
 #pragma unroll
@@ -767,14 +803,22 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
 
   {
     const int NQ = (KT * T + 1) / 2;  // MFMA groups of the whole K
-    const x6::bf16x8* ap = wpack + ((int64_t)((z * P.tiles_m + tm) * WR + wr) * NQ) * MI * cb16::FRAG + lane;
+    // this wave's weight fragments through a buffer resource: the group's
+    // offset is uniform (SGPR soffset), the lane's 16 bytes the only VGPR
+    // (64-bit per-load addresses cost the registers this kernel spills)
+    const x6::bf16x8* ap = wpack + ((int64_t)((z * P.tiles_m + tm) * WR + wr) * NQ) * MI * cb16::FRAG;
+    const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<x6::bf16x8*>(ap), 0, NQ * MI * cb16::FRAG * 16, 0x00020000);
+    const int alane = lane * 16;
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint16_t*>(xg), 0, static_cast<int>(xrange - static_cast<uint32_t>(z * (cv.C >> 3)) * PL), 0x00020000);
     auto load_a = [&](x6::bf16x8 (&f)[MI][3], int q) {
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int t = 0; t < 3; ++t) f[i][t] = ap[(q * MI + i) * cb16::FRAG + t * 64];
+        for (int t = 0; t < 3; ++t)
+          f[i][t] = __builtin_bit_cast(
+              x6::bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ar, alane, (q * MI + i) * cb16::FRAG * 16 + t * 1024, 0));
     };
     constexpr int PMAX = (PD + H - 2) / (H - 1);  // patch pieces per group (the shortest K-tile spreads them over H - 1 groups)
     static_assert(H >= 2, "pair groups");
@@ -868,7 +912,7 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
         for (int t = 0; t < 3; ++t) fa[0][i][t] = fa[1][i][t];
     }
     const int q0 = (kt / 2) * (2 * H + 1);
-    if (kt + 1 < KT) {
+    if constexpr (KTO == 0) {
       ktile(kt, q0, F_{}, T_{}, F_{});
       ktile(kt + 1, q0 + H, T_{}, F_{}, F_{});
     } else {
@@ -2094,15 +2138,18 @@ int pack_octets(const float* x, void* oct, int num, int C, int HWi, hipStream_t 
 struct CbPlan {
   int WR, NB, RPC, PD, octb, tiles_m, tiles_n, OCC, tpi;
 };
-// instantiated (KH, WR, NB, PD, OCC) combinations; OCC = workgroups per CU
+// instantiated (KH, WR, NB, PD, OCC) combinations; OCC = workgroups per CU.
+// One workgroup per CU: k_conv_cb_x6 (32x32x16); two: k_conv_cb16_x6
+// (16x16x32, RRAM_CB16_LIST below)
 #define RRAM_CB_LIST(X)                                                                              \
   X(5, 4, 8, 15, 1) X(5, 4, 4, 12, 1) X(5, 4, 4, 14, 1) X(5, 2, 4, 14, 1) X(3, 4, 8, 12, 1)          \
-  X(3, 4, 8, 15, 1) X(3, 4, 4, 8, 1) X(3, 4, 4, 12, 1) X(3, 2, 4, 12, 1) X(3, 2, 4, 14, 1)          \
-  X(5, 4, 4, 8, 2) X(3, 4, 4, 8, 2)
+  X(3, 4, 8, 15, 1) X(3, 4, 4, 8, 1) X(3, 4, 4, 12, 1) X(3, 2, 4, 12, 1) X(3, 2, 4, 14, 1)
+#define RRAM_CB16_LIST(X) X(5, 4, 4, 8, 2) X(3, 4, 4, 8, 2)
 bool cb_instantiated(int KH, int WR, int NB, int PD, int OCC = 1) {
 #define RRAM_X(kh, wr, nb, pd, occ) \
   if (KH == kh && WR == wr && NB == nb && PD == pd && OCC == occ) return true;
   RRAM_CB_LIST(RRAM_X)
+  RRAM_CB16_LIST(RRAM_X)
 #undef RRAM_X
   return false;
 }
@@ -2133,7 +2180,8 @@ bool conv_cb_plan(const rram_conv_desc* d, CbPlan& pl) {
     // octet plane size rounded to 256 bytes: the 16x16x32 form reads both
     // planes in one ds_read_b128 lane group, conflict-free only when the
     // plane offset is a multiple of the 64 banks
-    const int octb = (rmax * RPC * 16 + 255) / 256 * 256;
+    // (+ the two segment shifts of cbx6::seg_shift)
+    const int octb = ((rmax * RPC + 2 * ((3 * OW * (1 - KH)) & 15)) * 16 + 255) / 256 * 256;
     const int need = (2 * octb / 16 + 255) / 256;  // 1 KB pieces per wave
     int PD = 0;
     for (int p : {8, 12, 14, 15})
@@ -2197,38 +2245,18 @@ bool conv_cb_plan(const rram_conv_desc* d, CbPlan& pl) {
   return best > 0;
 }
 
-// k_conv_cb16_x6 instantiations (KH, WR, NB, PD, OCC): the 16x16x32 form of
-// the octet kernel for a plan of the same tile
-#define RRAM_CB16_LIST(X) \
-  X(5, 4, 4, 8, 2) X(3, 4, 4, 8, 2) X(3, 4, 8, 12, 1) X(3, 4, 8, 15, 1) X(3, 2, 4, 12, 1) X(3, 2, 4, 14, 1)
-bool cb16_instantiated(int KH, int WR, int NB, int PD, int OCC) {
-#define RRAM_X(kh, wr, nb, pd, occ) \
-  if (KH == kh && WR == wr && NB == nb && PD == pd && OCC == occ) return true;
-  RRAM_CB16_LIST(RRAM_X)
-#undef RRAM_X
-  return false;
-}
-// Which octet-kernel plans run on 16x16x32: bit 0 the 5x5 plans, bit 1 the
-// 3x3 plans at one workgroup per CU, bit 2 the 3x3 plans at two.  Default 5
-// (RRAM_CB16 overrides it for A/Bs).  Measured on MI355X (AlexNet b256,
+// The plans at two workgroups per CU run on 16x16x32 (k_conv_cb16_x6), the
+// others on 32x32x16.  Measured on MI355X (AlexNet b256,
 // profiles/r04_ab_cb16.txt): the 16x16x32 loop holds a 6-13 % higher clock;
 // conv2 (5x5, two workgroups per CU) 0.482 -> 0.457-0.461 ms, conv5 (3x3, two
 // per CU) 0.170 -> 0.166; conv3 / conv4 (one per CU) lose MFMA-busy (0.64 ->
 // 0.59, 0.54 -> 0.51) faster than they gain clock (0.340 -> 0.350, 0.287 ->
 // 0.300), so they stay on 32x32x16.
-bool cb16_for(int KH, int OCC) {
-  static const int mode = [] {
-    const char* e = getenv("RRAM_CB16");
-    return e ? atoi(e) : 5;
-  }();
-  return (mode & (KH == 5 ? 1 : OCC == 1 ? 2 : 4)) != 0;
-}
-
 int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, const float* w, const float* bias,
                    float* y, void* y_oct, int relu, hipStream_t s, const WPack& wk) {
   CbPlan pl;
   if (!conv_cb_plan(d, pl)) return 0;
-  const bool use16 = cb16_for(d->kernel_h, pl.OCC) && cb16_instantiated(d->kernel_h, pl.WR, pl.NB, pl.PD, pl.OCC);
+  const bool use16 = pl.OCC == 2;
   if (y_oct != nullptr && d->num_output % 8 != 0) return 0;
   const int KH = d->kernel_h, KW = d->kernel_w, T = KH * KW;
   const int G = d->group, Cg = d->channels / G, M = d->num_output / G;
@@ -2300,15 +2328,18 @@ int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, c
   const unsigned nwg = static_cast<unsigned>((int64_t)G * pl.tiles_m * pl.tiles_n);
   const uint32_t xrange = static_cast<uint32_t>(xbytes);  // whole packed input (the kernel narrows it per group)
   if (use16) {
-#define RRAM_X(kh, wr, nb, pd, occ)                                                                             \
-  if (KH == kh && pl.WR == wr && pl.NB == nb && pl.PD == pd && pl.OCC == occ) {                                 \
-    hipLaunchKernelGGL((k_conv_cb16_x6<kh, kh, wr, nb, pd, occ>), dim3(nwg), dim3(256), 0, s, P, wp, xp, pl.octb, \
-                       pl.RPC, xrange, ximg, static_cast<char*>(y_oct_k), d->num_output / 8,                    \
+    const int kto = (Cg / 16) & 1;
+#define RRAM_X2(kh, wr, nb, pd, occ, kpar)                                                                          \
+  if (KH == kh && pl.WR == wr && pl.NB == nb && pl.PD == pd && pl.OCC == occ && kto == kpar) {                      \
+    hipLaunchKernelGGL((k_conv_cb16_x6<kh, kh, wr, nb, pd, occ, kpar>), dim3(nwg), dim3(256), 0, s, P, wp, xp,        \
+                       pl.octb, pl.RPC, xrange, ximg, static_cast<char*>(y_oct_k), d->num_output / 8,               \
                        make_fastdiv(static_cast<uint32_t>(pl.octb >> 4)), make_fastdiv(static_cast<uint32_t>(pl.RPC)), \
-                       pl.tpi);                                                                                  \
+                       pl.tpi);                                                                                     \
   } else
+#define RRAM_X(kh, wr, nb, pd, occ) RRAM_X2(kh, wr, nb, pd, occ, 0) RRAM_X2(kh, wr, nb, pd, occ, 1)
     RRAM_CB16_LIST(RRAM_X) { return 0; }
 #undef RRAM_X
+#undef RRAM_X2
     rc = launch_status("conv cb16 x6");
     if (rc == 0 && y_oct != nullptr && y_oct_k == nullptr) rc = pack_octets(y, y_oct, d->num, d->num_output, HW, s);
     return rc ? rc : 1;
@@ -2329,23 +2360,12 @@ int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, c
 }
 
 // ---- k_conv1x1_x6 plan ----
-// RRAM_C1X1 (A/B runs): 1 = per-shape choice (default), 2 = k_conv1x1_x6
-// (register ring) only, 3 = k_conv1x1_dma_x6 only, 0 = neither (the fp32-MFMA
-// table-gather GEMM)
-int c1x1_mode() {
-  static const int mode = [] {
-    const char* e = getenv("RRAM_C1X1");
-    return e ? atoi(e) : 1;
-  }();
-  return mode;
-}
 struct C1Plan {
   int MI, NB, WR, VEC, tiles_m, tiles_n;
 };
 // (MI, NB, WR) instantiated for VEC = 4 and VEC = 1
 #define RRAM_C1X1_LIST(X) X(1, 2, 1) X(2, 1, 1) X(2, 2, 1) X(2, 1, 2) X(4, 1, 1) X(4, 2, 1) X(4, 1, 2) X(4, 2, 2)
 bool conv_1x1_plan(const rram_conv_desc* d, const float* x, C1Plan& pl) {
-  if (!c1x1_mode()) return false;
   if (d->kernel_h != 1 || d->kernel_w != 1 || d->stride_h != 1 || d->stride_w != 1 || d->pad_h != 0 ||
       d->pad_w != 0 || d->dilation_h != 1 || d->dilation_w != 1 || d->group != 1)
     return false;
@@ -2420,7 +2440,7 @@ int conv_1x1_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, con
   // the DMA form measured faster where the weight panel is tall (M > 64: 4-18 %
   // per layer), the register ring on 16-byte loads with M <= 64 and on the
   // 4-byte loads of the 7 x 7 layers (profiles/r04_ab_conv1x1.txt)
-  const bool dma = c1x1_mode() == 3 || (c1x1_mode() == 1 && pl.VEC == 4 && M > 64);
+  const bool dma = pl.VEC == 4 && M > 64;
 #define RRAM_X(mi, nb, wr)                                                                                  \
   if (pl.MI == mi && pl.NB == nb && pl.WR == wr) {                                                          \
     if (dma && pl.VEC == 4)                                                                                 \

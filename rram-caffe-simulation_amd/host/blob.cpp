@@ -1,5 +1,6 @@
 #include "blob.hpp"
 
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 
@@ -10,12 +11,18 @@ Caffe& Caffe::Get() {
   return inst;
 }
 
+std::atomic<uint64_t>& Caffe::scratch_gen() {
+  static std::atomic<uint64_t> g{0};
+  return g;
+}
+
 void* Caffe::workspace(size_t bytes) {
   Caffe& c = Get();
   if (bytes > c.ws_bytes_) {
     if (c.ws_) {
       HIP_CALL(hipStreamSynchronize(hip_stream()));
       HIP_CALL(hipFree(c.ws_));
+      scratch_gen().fetch_add(1);
     }
     c.ws_ = nullptr;
     HIP_CALL(hipMalloc(&c.ws_, bytes));
@@ -38,6 +45,7 @@ void* SyncedMemory::wpack(size_t bytes) {
     if (wp_ptr_) {
       HIP_CALL(hipStreamSynchronize(Caffe::hip_stream()));
       HIP_CALL(hipFree(wp_ptr_));
+      Caffe::scratch_gen().fetch_add(1);
     }
     wp_ptr_ = nullptr;
     HIP_CALL(hipMalloc(&wp_ptr_, bytes));
@@ -52,6 +60,7 @@ void* SyncedMemory::octets(size_t bytes) {
     if (oct_ptr_) {
       HIP_CALL(hipStreamSynchronize(Caffe::hip_stream()));
       HIP_CALL(hipFree(oct_ptr_));
+      Caffe::scratch_gen().fetch_add(1);
     }
     oct_ptr_ = nullptr;
     HIP_CALL(hipMalloc(&oct_ptr_, bytes));

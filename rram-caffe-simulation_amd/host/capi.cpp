@@ -247,6 +247,7 @@ int rram_net_blob(rram_net_t n, const char* name, float** data, float** diff, in
     NEED(name);
     auto b = n->net->blob_by_name(name);
     if (!b) throw Error(std::string("Unknown blob name ") + name);
+    n->net->materialize_blob(b.get());  // a folded Concat bottom holds its output again
     if (data) {
       *data = b->mutable_gpu_data();
       b->data()->expose();  // the caller may write a new batch through it unseen

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <sstream>
 #include <stdexcept>
 #include <string>
@@ -60,6 +61,11 @@ class Caffe {
   // Grows monotonically; never shrinks while a net is alive.
   static void* workspace(size_t bytes);
   static size_t workspace_size() { return Get().ws_bytes_; }
+  // Bumped whenever a device scratch buffer of the host side (this
+  // workspace, a weight pack, an octet companion) is freed: captured graphs
+  // hold raw pointers into them and are re-captured when it moves (with the
+  // kernel library's rram_scratch_generation).
+  static std::atomic<uint64_t>& scratch_gen();
   static void synchronize();
 
  private:

@@ -109,9 +109,10 @@ class Layer {
   // channel Concat writes its output straight into the Concat top at a
   // channel offset (write_into_concat: true when it can), and the Concat then
   // skips that bottom's copy (skip_concat_bottom).  The producer's own top is
-  // then never materialised (like a folded LRN's).
+  // then never materialised (like a folded LRN's) until Net::materialize_blob
+  // undoes the fold (the C-ABI does for every blob it hands out).
   virtual bool write_into_concat(Blob<Dtype>* /*concat_top*/, int /*channel_offset*/) { return false; }
-  virtual void skip_concat_bottom(int /*bottom_index*/) {}
+  virtual void skip_concat_bottom(int /*bottom_index*/, bool /*skip*/) {}
 
  protected:
   virtual void Forward_gpu(const std::vector<Blob<Dtype>*>& bottom,

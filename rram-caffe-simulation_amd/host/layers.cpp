@@ -832,9 +832,9 @@ class ConcatLayer : public Layer<Dtype> {
     }
   }
  public:
-  void skip_concat_bottom(int i) override {
+  void skip_concat_bottom(int i, bool skip) override {
     if ((int)skip_.size() <= i) skip_.resize(i + 1, false);
-    skip_[i] = true;
+    skip_[i] = skip;
   }
   int axis() const { return axis_; }
 

@@ -289,8 +289,10 @@ Net<Dtype>::Net(const Msg& in_param, Phase phase, const Msg& options) : phase_(p
                                  top_id_vecs_[lid - 1][0] == bottom_id_vecs_[lid][0] &&
                                  bottom_id_vecs_[lid - 1][0] != top_id_vecs_[lid - 1][0];
       if (prev_makes_it && prev->lrn_params(sz, a, b, kk) &&
-          layer->fuse_lrn_before(bottom_vecs_[lid - 1][0], sz, a, b, kk))
+          layer->fuse_lrn_before(bottom_vecs_[lid - 1][0], sz, a, b, kk)) {
         prev->folded_into_next = true;
+        lrn_folds_.push_back({lid - 1, lid, sz, a, b, kk});
+      }
     }
     ++lid;
   }
@@ -338,8 +340,10 @@ Net<Dtype>::Net(const Msg& in_param, Phase phase, const Msg& options) : phase_(p
           ok = false;                                            // another reader or writer
         }
         if (ok && writer >= 0 && j < bottom_need_backward_[l].size() &&
-            layers_[writer]->write_into_concat(ct, off))
-          layers_[l]->skip_concat_bottom(static_cast<int>(j));
+            layers_[writer]->write_into_concat(ct, off)) {
+          layers_[l]->skip_concat_bottom(static_cast<int>(j), true);
+          concat_folds_.push_back({writer, l, static_cast<int>(j), off});
+        }
         off += chans;
       }
     }
@@ -350,6 +354,37 @@ Net<Dtype>::Net(const Msg& in_param, Phase phase, const Msg& options) : phase_(p
     net_output_blob_indices_.push_back(id);
   }
   blob_loss_weights_.resize(blobs_.size(), 0.f);
+}
+
+template <typename Dtype>
+void Net<Dtype>::materialize_blob(const Blob<Dtype>* b) {
+  for (size_t i = 0; i < concat_folds_.size();) {
+    const ConcatFold f = concat_folds_[i];
+    Blob<Dtype>* bot = bottom_vecs_[f.concat][f.bottom];
+    if (bot != b) {
+      ++i;
+      continue;
+    }
+    Blob<Dtype>* ct = top_vecs_[f.concat][0];
+    const int inner = static_cast<int>(ct->count(2)), num = ct->shape(0);
+    if (bot->count() == (int64_t)num * bot->shape(1) * inner && ct->count() > 0)
+      RRAM_CALL(rram_concat_copy(bot->mutable_gpu_data(), ct->mutable_gpu_data(), num, bot->shape(1) * inner,
+                                 ct->shape(1) * inner, f.offset * inner, 1, Caffe::stream()));
+    layers_[f.writer]->write_into_concat(nullptr, 0);
+    layers_[f.concat]->skip_concat_bottom(f.bottom, false);
+    concat_folds_.erase(concat_folds_.begin() + static_cast<long>(i));
+  }
+  for (size_t i = 0; i < lrn_folds_.size();) {
+    const LrnFold f = lrn_folds_[i];
+    if (top_vecs_[f.lrn][0] != b) {
+      ++i;
+      continue;
+    }
+    layers_[f.pool]->fuse_lrn_before(nullptr, f.size, f.alpha, f.beta, f.k);
+    layers_[f.lrn]->folded_into_next = false;
+    if (bottom_vecs_[f.lrn][0]->count() > 0) layers_[f.lrn]->Forward(bottom_vecs_[f.lrn], top_vecs_[f.lrn]);
+    lrn_folds_.erase(lrn_folds_.begin() + static_cast<long>(i));
+  }
 }
 
 template <typename Dtype>

@@ -99,9 +99,25 @@ class Net {
   // convolution layers keep their packed weights between forwards while the
   // weights are unchanged (ConvolutionLayer::cache_wpack); off drops every pack
   void set_weight_pack_cache(bool on);
+  // Undo a TEST-phase fold that leaves blob b unwritten (a caller asked for it
+  // through the C-ABI, so it must hold its layer's output as in the
+  // reference).  A folded Concat bottom gets its current values back from the
+  // Concat top's slice; a folded LRN's top is computed now from its bottom.
+  // Later forwards write b again (the producer stores it, the consumer reads it).
+  void materialize_blob(const Blob<Dtype>* b);
   EventTimer& timer() { return timer_; }
 
  private:
+  struct ConcatFold {
+    int writer, concat, bottom;  // producing Convolution, Concat layer, bottom index
+    int offset;                  // channel offset of the slice
+  };
+  std::vector<ConcatFold> concat_folds_;
+  struct LrnFold {
+    int lrn, pool, size;  // the folded LRN, the MAX pool computing it, its parameters
+    float alpha, beta, k;
+  };
+  std::vector<LrnFold> lrn_folds_;
   int timing_ = 0;
   int timed_layer_ = -1;
   EventTimer timer_;

@@ -438,6 +438,11 @@ std::vector<const void*> Solver<Dtype>::graph_key() const {
     k.push_back(fmaker_->device_counts());
   }
   k.push_back(Caffe::hip_stream());
+  // the scratch the captured launches read and write (workspace, packs,
+  // split-K partials, gather tables): eager work between replays may have
+  // reallocated it (a larger test batch, another net on this thread)
+  k.push_back(reinterpret_cast<const void*>(static_cast<uintptr_t>(Caffe::scratch_gen().load())));
+  k.push_back(reinterpret_cast<const void*>(static_cast<uintptr_t>(rram_scratch_generation())));
   return k;
 }
 
@@ -489,7 +494,8 @@ void Solver<Dtype>::Step(int iters) {
     const Dtype rate_now = graph_ ? GetLearningRate() : Dtype(0);
     const bool rate_stable = rate_now == graph_prev_rate_;
     graph_prev_rate_ = rate_now;
-    if (graph_ && rate_stable && can_fuse && !test_now && !disp && average_loss <= 1 && !net_->on_backward_layer) {
+    if (graph_ && rate_stable && can_fuse && !test_now && !disp && average_loss <= 1 && !net_->on_backward_layer &&
+        !net_->timing_on()) {
       // the first such iteration runs eager (workspaces and scratch buffers
       // get allocated on the section's stream), the next one captures
       const Dtype rate = rate_now;
@@ -890,6 +896,11 @@ std::vector<const void*> MonteCarlo<Dtype>::graph_key() const {
   k.push_back(d_per_map_);
   k.push_back(d_broken_);
   k.push_back(Caffe::hip_stream());
+  // the scratch the captured launches read and write (workspace, packs,
+  // split-K partials, gather tables): eager work between replays may have
+  // reallocated it (a larger test batch, another net on this thread)
+  k.push_back(reinterpret_cast<const void*>(static_cast<uintptr_t>(Caffe::scratch_gen().load())));
+  k.push_back(reinterpret_cast<const void*>(static_cast<uintptr_t>(rram_scratch_generation())));
   return k;
 }
 
@@ -997,9 +1008,16 @@ void MonteCarlo<Dtype>::Run(uint32_t map_begin, uint32_t map_count) {
     const auto& tops = net_->top_vecs();
     for (size_t k = 0; k < no; ++k) {
       Layer<Dtype>* prod = nullptr;
+      int prod_l = -1;
       for (size_t l = 0; l < L.size(); ++l)
-        if (!tops[l].empty() && tops[l][0] == outs_[k]) prod = L[l].get();
-      if (!prod || !prod->set_top_accumulator(d_sums_ + k, nullptr)) {
+        if (!tops[l].empty() && tops[l][0] == outs_[k]) {
+          prod = L[l].get();
+          prod_l = static_cast<int>(l);
+        }
+      // a producer inside the reused prefix runs on the first map only: its
+      // constant output is then accumulated by rram_mc_accumulate every map
+      const bool in_prefix = reuse_prefix_ && prod_l < first_fault_layer_;
+      if (!prod || in_prefix || !prod->set_top_accumulator(d_sums_ + k, nullptr)) {
         for (auto* a : acc_layers) a->set_top_accumulator(nullptr, nullptr);
         acc_layers.clear();
         break;

@@ -70,6 +70,7 @@ SIGNATURES = {
     "rram_last_error": (C.c_char_p, []),
     "rram_device_synchronize": (I, []),
     "rram_release_caches": (I, []),
+    "rram_scratch_generation": (U64, []),
     "rram_set_f32_engine": (I, [I]),
     "rram_get_f32_engine": (I, []),
     "rram_f32_engine_for_conv": (I, [P]),

@@ -323,14 +323,14 @@ def googlenet(train_batch=32, test_batch=256) -> str:
 def solver(base_lr=0.01, momentum=0.9, weight_decay=0.0005, lr_policy="fixed", max_iter=100, test_iter=1,
            test_interval=0, display=0, gamma=None, power=None, stepsize=None, random_seed=1701,
            failure_mean: Optional[float] = None, failure_std: Optional[float] = None, failure_prob=None,
-           threshold: Optional[float] = None, test_initialization=False) -> str:
+           threshold: Optional[float] = None, test_initialization=False, average_loss: Optional[int] = None) -> str:
     """SolverParameter text with the fork's failure_pattern / failure_strategy
     blocks (caffe.proto:244-290), as run_gaussian_exp.py:50-103 writes them."""
     lines = [f"base_lr: {base_lr}", f"momentum: {momentum}", f"weight_decay: {weight_decay}",
              f'lr_policy: "{lr_policy}"', f"max_iter: {max_iter}", f"test_iter: {test_iter}",
              f"test_interval: {test_interval}", f"display: {display}", f"random_seed: {random_seed}",
              f"test_initialization: {'true' if test_initialization else 'false'}"]
-    for k, v in (("gamma", gamma), ("power", power), ("stepsize", stepsize)):
+    for k, v in (("gamma", gamma), ("power", power), ("stepsize", stepsize), ("average_loss", average_loss)):
         if v is not None:
             lines.append(f"{k}: {v}")
     if failure_mean is not None:

@@ -202,13 +202,28 @@ def run_workload(args, world, rank, dev):
             gmax = float(f["data"].abs().max().item()) or 1.0
             cfgs.append(make_inject_cfg(0.01, 10, 20, 10, quant_levels=16, g_max=gmax, var_sigma=0.1,
                                         stuck_scale=gmax))
-        mc = caffe.MonteCarlo(net, cfgs, seed=args.seed, max_maps=(args.steps + args.warmup) * 10 + 8)
+        # 100 maps per step: the driver-style `--steps 10` runs BASELINE.json's
+        # "1000 fault maps on one MI355X" in one line
+        maps_per_step = 100
+        mc = caffe.MonteCarlo(net, cfgs, seed=args.seed, max_maps=(args.steps + args.warmup) * maps_per_step + 8)
         mc.set_graph(_graph_on())         # replay each map as one hipGraph (opt-in, see _graph_on)
-        maps_per_step = 10
         el = _timed(world, dev, lambda i: mc.run((rank + world * i) * maps_per_step, maps_per_step),
                     args.steps, args.warmup)
         st = mc.stats()
         graph = mc.graph_active()
+        # per-output mean / std / 95 % CI over the timed maps of every rank
+        names = [k for k, v in net.outputs().items() if v.numel() == 1][:len(st["sums"])]
+        rows = st["per_map"][args.warmup * maps_per_step:(args.warmup + args.steps) * maps_per_step]
+        acc = []
+        for k in range(len(names)):
+            acc += [sum(r[k] for r in rows), sum(r[k] * r[k] for r in rows)]
+        tot_m = allreduce_stats(acc + [len(rows)], dev)
+        per_output = {}
+        nm = max(tot_m[-1], 1)
+        for k, name in enumerate(names):
+            mean = tot_m[2 * k] / nm
+            var = max(tot_m[2 * k + 1] / nm - mean * mean, 0.0) * nm / max(nm - 1, 1)
+            per_output[name] = dict(mean=mean, std=var ** 0.5, ci95=1.96 * (var / nm) ** 0.5, maps=int(tot_m[-1]))
         # the contraction table: events around every conv / IP layer over K
         # further maps after the timed region (the maps run eager while timed)
         net.layer_times(reset=True)
@@ -225,6 +240,7 @@ def run_workload(args, world, rank, dev):
         res["images_per_s"] = round(n_maps * batch / el, 1)
         res["hipgraph"] = graph
         res["mc_mean_outputs"] = [x / max(tot[-1], 1) for x in tot[:-1]]
+        res["mc_timed_maps"] = per_output     # mean, sample std and 95 % CI half-width over the timed maps
         res["roofline"] = contraction_roofline(net, args.steps * maps_per_step, net.layer_times())
         mc.close()
         net.close()

@@ -2,7 +2,7 @@
 # Try a kernel variant on one box: the GPU tests named in $TESTS under the
 # environment $TENV (default: the octet / conv / guard files), then the
 # interleaved bench A/B of the variants given as arguments (scripts/ab.sh).
-#   TENV="RRAM_CB16=3" scripts/gpu_try.sh "RRAM_CB16=0" "RRAM_CB16=3"
+#   scripts/gpu_try.sh "RRAM_LIB_DIR=rram-caffe-simulation_amd/lib_base" -   (baseline build vs this tree)
 set -o pipefail
 O=gpurun_out/try; mkdir -p $O
 T=${TESTS:-tests/test_gpu_octets.py tests/test_gpu_wpack.py tests/test_gpu_fp32_guard.py tests/test_gpu_kernels.py}

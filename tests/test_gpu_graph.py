@@ -79,22 +79,27 @@ def test_graph_quantised_lognormal_equals_eager(device):
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
-def _train(graph, iters, lr_policy="fixed", **kw):
+def _train(graph, iters, lr_policy="fixed", test_batch=20, side_stream=False, **kw):
+    import contextlib
+    import torch
     from rramsim import caffe, models
+    ctx = torch.cuda.stream(torch.cuda.Stream()) if side_stream else contextlib.nullcontext()
+    with ctx:
+        caffe.set_stream_from_torch()
+        caffe.set_random_seed(1701)
+        sp = models.solver(base_lr=0.001, momentum=0.9, weight_decay=0.004, lr_policy=lr_policy, max_iter=1000,
+                           failure_mean=5e4, failure_std=1.5e4, failure_prob=(5, 90, 5), threshold=0.001, **kw)
+        s = caffe.Solver(sp, models.cifar10_full(train_batch=20, test_batch=test_batch),
+                         dict(models.net_options("cifar10_full"), fused_update=True))
+        s.set_graph(graph)
+        for n in iters:
+            s.step(n)
+        ps = [N(p["data"]) for p in s.net.params()]
+        hist = [N(h) for h in s.history()]
+        fs = s.fail_state()
+        st = (ps, hist, [N(e) for e, v in fs], s.broken_counts(), s.graph_active())
+        s.close()
     caffe.set_stream_from_torch()
-    caffe.set_random_seed(1701)
-    sp = models.solver(base_lr=0.001, momentum=0.9, weight_decay=0.004, lr_policy=lr_policy, max_iter=1000,
-                       failure_mean=5e4, failure_std=1.5e4, failure_prob=(5, 90, 5), threshold=0.001, **kw)
-    s = caffe.Solver(sp, models.cifar10_full(train_batch=20, test_batch=20),
-                     dict(models.net_options("cifar10_full"), fused_update=True))
-    s.set_graph(graph)
-    for n in iters:
-        s.step(n)
-    ps = [N(p["data"]) for p in s.net.params()]
-    hist = [N(h) for h in s.history()]
-    fs = s.fail_state()
-    st = (ps, hist, [N(e) for e, v in fs], s.broken_counts(), s.graph_active())
-    s.close()
     return st
 
 
@@ -107,6 +112,28 @@ def test_graph_training_equals_eager(device, policy):
     ref = _train(False, [3, 4, 3], **policy)
     got = _train(True, [3, 4, 3], **policy)
     assert got[4] and not ref[4]
+    for a, b in zip(got[0] + got[1] + got[2], ref[0] + ref[1] + ref[2]):
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert got[3] == ref[3]
+
+
+@pytest.mark.parametrize("mode", ["test_interval", "display", "average_loss", "side_stream"])
+def test_graph_training_interleaved_equals_eager(device, mode):
+    """Graph iterations interleaved with the eager work that breaks a replay
+    (ADVICE r04): TestAll every 3 iterations on a larger test batch (its
+    forward grows the shared workspace / pack buffers the captured launches
+    point into: the scratch generation in Solver::graph_key recaptures),
+    display iterations (eager), average_loss > 1 (no graph at all), and a
+    non-NULL caller stream (captured directly on it).  Every variant equals
+    the eager run bit for bit."""
+    kw = dict(test_interval=dict(test_interval=3, test_iter=1, test_batch=100),
+              display=dict(display=2),
+              average_loss=dict(display=2, average_loss=2),
+              side_stream=dict(side_stream=True))[mode]
+    ref = _train(False, [4, 5], **kw)
+    got = _train(True, [4, 5], **kw)
+    if mode != "average_loss":
+        assert got[4]                                   # the graph ran
     for a, b in zip(got[0] + got[1] + got[2], ref[0] + ref[1] + ref[2]):
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
     assert got[3] == ref[3]

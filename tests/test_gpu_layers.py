@@ -552,3 +552,35 @@ def test_concat_fold_in_googlenet_test_net(device):
     assert len(outs[0]) == 11
     for n in outs[0]:
         assert torch.equal(outs[0][n], outs[1][n]), n
+
+
+def test_folded_blobs_materialise_when_read(device):
+    """A blob a TEST-phase fold leaves unwritten (an inception branch output
+    written straight into its Concat top; an LRN top computed inside the
+    following MAX pool) holds its layer's output once the C-ABI hands it out
+    (Net::materialize_blob, ADVICE r04): equal to the unfolded net's blob
+    bit for bit, right away and after a further forward, and the net's
+    outputs stay bit-identical."""
+    import torch
+    from rramsim import caffe, models
+    caffe.set_stream_from_torch()
+    cases = [("googlenet", models.googlenet, ["inception_3a/1x1", "inception_4e/pool_proj"], "fuse_concat",
+              ["inception_3a/output", "loss3/classifier"]),
+             ("alexnet", models.alexnet, ["norm1", "norm2"], "fuse_lrn_pool", ["pool2", "fc8"])]
+    for name, build, folded, opt, outs in cases:
+        got = {}
+        for fuse in (False, True):
+            caffe.set_random_seed(1701)
+            net = caffe.Net(build(test_batch=4), "test", models.net_options(name, **{opt: fuse}))
+            net.forward()
+            torch.cuda.synchronize()
+            first = {n: net.blob(n).detach().cpu().clone() for n in folded}
+            net.forward()
+            torch.cuda.synchronize()
+            again = {n: net.blob(n).detach().cpu().clone() for n in folded + outs}
+            got[fuse] = (first, again)
+            net.close()
+        for n in folded:
+            assert torch.equal(got[True][0][n], got[False][0][n]), (name, n)
+        for n in folded + outs:
+            assert torch.equal(got[True][1][n], got[False][1][n]), (name, n)
