@@ -15,6 +15,9 @@ int conv_bwd_weight_core(const rram_conv_desc* d, int nimg, const float* dy, con
                          int64_t ldcol, float* dw, void* part, size_t part_bytes, hipStream_t s,
                          float* db = nullptr);
 int bwd_weight_split(int M, int N, int64_t K);
+bool conv_bwd_weight_im2t_ok(const rram_conv_desc* d, size_t part_bytes);
+int conv_bwd_weight_im2t(const rram_conv_desc* d, const float* x, const float* dy, float* dw, float* db, void* part,
+                         size_t part_bytes, hipStream_t s);
 int conv_bwd_data_col_core(const rram_conv_desc* d, int nimg, const float* w, const float* dy,
                            float* col, int64_t ldcol, hipStream_t s);
 int im2col_core(const float* im, int64_t im_img, int nimg, const rram_conv_desc* d, float* col,
@@ -310,8 +313,12 @@ int rram_conv2d_bwd(const rram_conv_desc* d_in, const float* x, const float* w, 
   // column against a ones row of the column matrix, summed by the split-K
   // reduce): no bias kernels.  Ungrouped layers whose weight GEMM is split
   // (partials in the workspace) and whose every image chunk has >= 2 K-tiles.
-  bool fold_db = false;
-  if (db && dw && x && w && ws && d.group == 1 && HoWo >= 2 * 32) {
+  // The weight gradient gathers its column matrix inside the GEMM
+  // (conv_bwd_weight_im2t: no im2col pass, all images in one split GEMM) when
+  // the workspace holds its split-K partials; else the column path below.
+  const bool im2t = dw && x && w && ws && conv_bwd_weight_im2t_ok(&d, ws_bytes);
+  bool fold_db = im2t && db && d.group == 1;
+  if (!im2t && db && dw && x && w && ws && d.group == 1 && HoWo >= 2 * 32) {
     const size_t per_img = col_bytes(d, 1);
     int chunk = ws_bytes >= per_img ? static_cast<int>(ws_bytes / per_img) : 0;
     if (chunk > d.num) chunk = d.num;
@@ -355,7 +362,12 @@ int rram_conv2d_bwd(const rram_conv_desc* d_in, const float* x, const float* w, 
   // each workgroup walks a long K = cout*k*k alone and the GEMM + col2im pair
   // is 1.4-1.6x faster (profiles/r04_ab_dx_fwd.txt)
   const int64_t dx_tiles = (int64_t)G * ((cin_g + 31) / 32) * (((int64_t)d.num * d.height * d.width + 127) / 128);
+#ifdef RRAM_DX_FWD_ALL
+  (void)dx_tiles;
+  const bool dx_fwd = dx && d.stride_h == 1 && d.stride_w == 1 &&
+#else
   const bool dx_fwd = dx && dx_tiles >= 128 && d.stride_h == 1 && d.stride_w == 1 &&
+#endif
                       eph >= 0 && epw >= 0 &&
                       ws != nullptr && ws_bytes >= wt_bytes && wt_bytes < (1ull << 31) &&
                       (int64_t)d.num * d.height * d.width < (1ll << 31) &&
@@ -374,6 +386,12 @@ int rram_conv2d_bwd(const rram_conv_desc* d_in, const float* x, const float* w, 
                  t.out_h, t.out_w, d.height, d.width);
     return conv_fwd_core(&t, dy, wt, nullptr, dx, 0, s);
   };
+  if (im2t) {
+    rc = conv_bwd_weight_im2t(&d, x, dy, dw, fold_db ? db : nullptr, ws, ws_bytes, s);
+    if (rc) return rc;
+    dw = nullptr;  // done
+  }
+  if (!dw && !dx) return RRAM_OK;
   if (dx_fwd && !dw) return dx_as_fwd();
   const size_t per_img = col_bytes(d, 1);
   RRAM_REQUIRE(ws != nullptr && ws_bytes >= per_img, "conv2d_bwd: workspace needs >= %zu bytes",

@@ -69,7 +69,7 @@ __device__ __forceinline__ float ld_nchwt(const View& vw, int row, int k, bool k
 // are k-fastest (memory is contiguous along k); the others are row-fastest.
 template <int MODE, int ROWS, int KB>
 __device__ __forceinline__ void tile_coord(int e, int& row, int& k) {
-  if (MODE == KC || MODE == NCHW) {
+  if (MODE == KC || MODE == NCHW || MODE == IM2T) {
     row = e / KB;
     k = e % KB;
   } else {
@@ -166,6 +166,40 @@ __device__ __forceinline__ void load_tile(Loader<ROWS, KB>& L, const View& vw, c
       const uint32_t bad = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(word), t.y & 31, 1));
       L.v[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, (pb4 + static_cast<uint32_t>(t.x)) | bad, 0, 0));
     }
+    return;
+  }
+  if constexpr (MODE == IM2T) {
+    // the column matrix of the weight gradient, transposed and gathered: the
+    // thread's position k0 + tid % KB is fixed for the tile (k-fastest tile
+    // order, 256 % KB == 0), its rows step by 256 / KB.  Per element: one
+    // table load (the row's input offset and kernel offsets), two bounds
+    // compares, one add; an invalid element's offset is pushed out of the
+    // buffer's range (the load returns 0).  The ones row (table y = -1) is
+    // set to 1.0 in store_tile (after the MFMAs, where the loads are waited
+    // for anyway), recorded in kn[0]'s bits.
+    static_assert(256 % KB == 0 && EPT <= 32, "IM2T tile");
+    const int p = k0 + static_cast<int>(threadIdx.x) % KB;
+    const bool pv = p < kend;
+    const uint32_t im = fdiv(static_cast<uint32_t>(p), cv.howo);
+    const uint32_t sp = static_cast<uint32_t>(p) - im * cv.howo.d;
+    const uint32_t ho = fdiv(sp, cv.wo_div);
+    const int hb = static_cast<int>(ho) * cv.sh - cv.ph;
+    const int wb = static_cast<int>(sp - ho * cv.wo_div.d) * cv.sw - cv.pw;
+    const uint32_t pb4 = static_cast<uint32_t>((static_cast<int64_t>(im) * cv.chw + hb * cv.W + wb) * 4);
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(vw.p), 0, cv.in_bytes, 0x00020000);
+    const int r0 = row0 + static_cast<int>(threadIdx.x) / KB;
+    uint32_t ones = 0;
+#pragma unroll
+    for (int i = 0; i < EPT; ++i) {
+      const int2 t = cv.tbl[r0 + i * (256 / KB)];
+      const bool ok = pv && static_cast<unsigned>(hb + (t.y & 0xFFFF)) < static_cast<unsigned>(cv.H) &&
+                      static_cast<unsigned>(wb + (t.y >> 16)) < static_cast<unsigned>(cv.W);
+      L.v[i] = __builtin_bit_cast(
+          float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, (pb4 + static_cast<uint32_t>(t.x)) | (ok ? 0u : 0xFFFFFFFFu), 0, 0));
+      ones |= (pv && t.y == -1) ? (1u << i) : 0u;
+    }
+    L.kn[0] = static_cast<int>(ones);
     return;
   }
   if (MODE == CONV) {
@@ -274,7 +308,7 @@ __device__ __forceinline__ void store_tile(const Loader<ROWS, KB>& L, float* lds
     const int e = threadIdx.x + i * 256;
     int r, kk;
     tile_coord<MODE, ROWS, KB>(e, r, kk);
-    lds[r * LDK + kk] = L.v[i];
+    lds[r * LDK + kk] = (MODE == IM2T && ((static_cast<uint32_t>(L.kn[0]) >> i) & 1u)) ? 1.0f : L.v[i];
   }
 }
 
@@ -1437,6 +1471,7 @@ int dispatch(int am, int bm, int om, const Params& P, int gz, hipStream_t s, boo
   RRAM_D(KCV, CONVT64, OUT_NCHW)
   RRAM_D(NCHW, KC, OUT_ROWMAJOR)
   RRAM_D(NCHW, KCV, OUT_ROWMAJOR)
+  RRAM_D(NCHW, IM2T, OUT_ROWMAJOR)
   RRAM_D(RC, NCHWT, OUT_ROWMAJOR)
 #undef RRAM_D
   set_error("gemm: unsupported operand combination %d/%d/%d", am, bm, om);
@@ -1480,6 +1515,38 @@ const int2* conv_table(const ConvGeom& cv, int K, bool padded, bool wide, hipStr
     h[k].x = 4 * (c * cv.H * cv.W + kh * cv.dh * cv.W + kw * cv.dw);
     h[k].y = padded ? r : 0;
   }
+  int2* d = nullptr;
+  if (hipMalloc(&d, len * sizeof(int2)) != hipSuccess) return nullptr;
+  if (hipMemcpyAsync(d, h.data(), len * sizeof(int2), hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess) {
+    (void)hipFree(d);
+    return nullptr;
+  }
+  cache[key] = d;
+  return d;
+}
+
+// Row table of the IM2T loader (cached with the CONVT tables): entry n < K
+// holds row n = (c, kh, kw) of the column matrix as {4 (c H W + kh dh W +
+// kw dw), kh dh | kw dw << 16}; entry K the ones row {0, -1} when `ones`;
+// the rest (tile padding) {0, 0x7FFF7FFF}, never inside the image.
+const int2* im2t_table(const ConvGeom& cv, int K, bool ones, int rows_pad, hipStream_t s) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  auto& cache = conv_table_cache();
+  const int len = (K + 1 + rows_pad - 1) / rows_pad * rows_pad + rows_pad;
+  const std::array<int, 11> key{dev, cv.C, cv.H, cv.W, cv.KH, cv.KW, cv.dh, cv.dw, len, K, ones ? 3 : 2};
+  std::lock_guard<std::mutex> g(conv_table_mutex());
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  std::vector<int2> h(len, int2{0, 0x7FFF7FFF});
+  for (int k = 0; k < K; ++k) {
+    const int c = k / (cv.KH * cv.KW), r = k % (cv.KH * cv.KW);
+    const int kh = r / cv.KW, kw = r % cv.KW;
+    h[k].x = 4 * (c * cv.H * cv.W + kh * cv.dh * cv.W + kw * cv.dw);
+    h[k].y = (kh * cv.dh) | ((kw * cv.dw) << 16);
+  }
+  if (ones) h[K] = int2{0, -1};
   int2* d = nullptr;
   if (hipMalloc(&d, len * sizeof(int2)) != hipSuccess) return nullptr;
   if (hipMemcpyAsync(d, h.data(), len * sizeof(int2), hipMemcpyHostToDevice, s) != hipSuccess ||
@@ -1837,6 +1904,91 @@ int bwd_weight_split(int M, int N, int64_t K) {
 // db (nullable; ungrouped only, part required): the bias gradient as one more
 // GEMM column against the ones row im2col_core wrote after the K column rows,
 // always split (>= 2), the reduce routing column K to db
+// The weight gradient with the column matrix gathered inside the GEMM (IM2T,
+// no im2col pass and no column buffer): dW_g[co][k] += sum_p dY_g[co][p]
+// x_g[k, p] over all d->num images; db (group 1 only) as the ones row's
+// column of the same split GEMM.  part: the split-K partials (required:
+// these are long-K GEMMs); 0 when not covered (the caller falls back to the
+// column path), < 0 on error.  The same K-tiles, split and element values as
+// the im2col + KC path, so the same bits.
+bool conv_bwd_weight_im2t_ok(const rram_conv_desc* d, size_t part_bytes) {
+  const int g = d->group;
+  const int cout_g = d->num_output / g, K = d->channels / g * d->kernel_h * d->kernel_w;
+  const int64_t P_all = (int64_t)d->num * d->out_h * d->out_w;
+  const int64_t in_elems = (int64_t)d->num * d->channels * d->height * d->width;
+  return P_all >= 2 * BK && P_all < (1ll << 31) && in_elems * 4 < (1ll << 31) && K + 1 < (1 << 24) &&
+         (d->kernel_h - 1) * d->dilation_h < 32768 && (d->kernel_w - 1) * d->dilation_w < 32768 &&
+         part_bytes >= 2 * (size_t)cout_g * (K + 1) * sizeof(float);
+}
+int conv_bwd_weight_im2t(const rram_conv_desc* d, const float* x, const float* dy, float* dw, float* db, void* part,
+                         size_t part_bytes, hipStream_t s) {
+  const int g = d->group;
+  const int cin_g = d->channels / g, cout_g = d->num_output / g;
+  const int K = cin_g * d->kernel_h * d->kernel_w;
+  const int HoWo = d->out_h * d->out_w;
+  const int64_t P_all = (int64_t)d->num * HoWo;
+  const int64_t in_elems = (int64_t)d->num * d->channels * d->height * d->width;
+  RRAM_REQUIRE(part != nullptr && conv_bwd_weight_im2t_ok(d, part_bytes) && (db == nullptr || g == 1),
+               "conv bwd weight (gathered): shape or workspace not covered");
+  ConvGeom cv{};
+  cv.C = cin_g;
+  cv.H = d->height;
+  cv.W = d->width;
+  cv.KH = d->kernel_h;
+  cv.KW = d->kernel_w;
+  cv.ph = d->pad_h;
+  cv.pw = d->pad_w;
+  cv.sh = d->stride_h;
+  cv.sw = d->stride_w;
+  cv.dh = d->dilation_h;
+  cv.dw = d->dilation_w;
+  cv.Ho = d->out_h;
+  cv.Wo = d->out_w;
+  cv.howo = make_fastdiv(HoWo);
+  cv.wo_div = make_fastdiv(d->out_w);
+  cv.chw = (int64_t)d->channels * d->height * d->width;
+  cv.tbl = im2t_table(cv, K, db != nullptr, 256, s);
+  RRAM_REQUIRE(cv.tbl != nullptr, "conv bwd weight: gather table allocation failed");
+  const int N = K + (db ? 1 : 0);
+  for (int gi = 0; gi < g; ++gi) {
+    Params P{};
+    P.M = cout_g;
+    P.N = N;
+    P.K = static_cast<int>(P_all);
+    P.a = make_view(dy + (int64_t)gi * cout_g * HoWo, HoWo, cout_g, P.K);
+    P.a.img = (int64_t)d->num_output * HoWo;
+    P.a.hw = make_fastdiv(HoWo);
+    P.b = make_view(x + (int64_t)gi * cin_g * d->height * d->width, 0, N, P.K);
+    P.cv = cv;
+    P.cv.in_bytes = static_cast<int>((in_elems - (int64_t)gi * cin_g * d->height * d->width) * 4);
+    P.e = make_epi(dw + (int64_t)gi * cout_g * K, K, 1.0f, 1.0f, nullptr, 0, 0);
+    int split = std::max(2, bwd_weight_split(P.M, P.N, P.K));
+    while (split > 2 && (size_t)split * P.M * P.N * sizeof(float) > part_bytes) --split;
+    int chunk = (P.K + split - 1) / split;
+    chunk = (chunk + BK - 1) / BK * BK;
+    split = (P.K + chunk - 1) / chunk;
+    RRAM_REQUIRE(split >= 2 && (size_t)split * P.M * P.N * sizeof(float) <= part_bytes,
+                 "conv bwd weight (gathered): split-K partials do not fit");
+    P.split = split;
+    P.k_chunk = chunk;
+    P.ws = static_cast<float*>(part);
+    int rc = dispatch(NCHW, IM2T, OUT_ROWMAJOR, P, split, s, true);
+    if (rc) return rc;
+    if (split >= 32)
+      hipLaunchKernelGGL(k_splitk_reduce_wave, dim3(static_cast<unsigned>(((int64_t)P.M * P.N + 3) / 4)), dim3(256), 0,
+                         s, P.ws, split, P.M, K, P.N, P.e.C, db);
+    else if (db)
+      hipLaunchKernelGGL(k_splitk_reduce_dwdb, dim3(stream_blocks((int64_t)P.M * P.N)), dim3(256), 0, s, P.ws, split,
+                         P.M, K, P.e.C, db);
+    else
+      hipLaunchKernelGGL(k_splitk_reduce, dim3(stream_blocks((int64_t)P.M * P.N)), dim3(256), 0, s, P.ws, split,
+                         P.M, P.N, P.e);
+    rc = launch_status("conv bwd weight (gathered) split-K reduce");
+    if (rc) return rc;
+  }
+  return RRAM_OK;
+}
+
 int conv_bwd_weight_core(const rram_conv_desc* d, int nimg, const float* dy, const float* col,
                          int64_t ldcol, float* dw, void* part, size_t part_bytes, hipStream_t s, float* db) {
   const int g = d->group;

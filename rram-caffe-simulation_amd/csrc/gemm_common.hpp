@@ -29,7 +29,12 @@ constexpr int ldk_of() { return KB + 4; }
 // not a multiple of 4, e.g. AlexNet conv1 K = 363): a float4 may run into the
 // next row (or past the buffer end, where the per-dword range check returns
 // 0); the elements at k >= K are zeroed when the tile is written to LDS.
-enum Mode : int { KC = 0, RC = 1, CONV = 2, NCHW = 3, NCHWT = 4, KCV = 5, CONVT = 6, CONVT64 = 7, KCU = 8 };
+// IM2T = the transposed column matrix of a convolution's weight gradient,
+// gathered from the input (no im2col pass): row = reduction index (c, kh,
+// kw) of the column matrix (row K = the folded bias gradient's ones row),
+// k = output position (image, ho, wo); per-row {offset, kh*dh | kw*dw << 16}
+// table (im2t_table), per-thread position decoded once per K-tile.
+enum Mode : int { KC = 0, RC = 1, CONV = 2, NCHW = 3, NCHWT = 4, KCV = 5, CONVT = 6, CONVT64 = 7, KCU = 8, IM2T = 9 };
 enum OutMode : int { OUT_ROWMAJOR = 0, OUT_NCHW = 1 };
 
 // Fast unsigned division by a runtime constant (x < 2^31).

@@ -324,6 +324,8 @@ __device__ __forceinline__ int clamp_col(int n, int n0, int plast) {
 // first patch piece of K-tile kt + 1 staged at tap s (pieces spread evenly
 // over taps 0 .. T - 2)
 constexpr int piece_lo(int s, int PD, int T) { return s >= T - 1 ? PD : (s * PD + T - 2) / (T - 1); }
+// the same over taps 0 .. T - 1 - SD (pieces loaded at tap s, stored at s + SD)
+constexpr int piece_lo_d(int s, int PD, int T, int SD) { return s >= T - SD ? PD : (s * PD + T - SD - 1) / (T - SD); }
 }  // namespace cbx6
 
 // The loop's global reads are compiler-visible register loads: weights
@@ -430,11 +432,7 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
     dma_b128(xrsrc, poff[i] + static_cast<uint32_t>(kt) * 2u * PL,
              lds0 + static_cast<uint32_t>(stg * SFB + (wave * PD + i) * 1024));
   };
-  // weight fragments: a ring of WD groups, loaded WD - 1 groups ahead (WD = 3
-  // when the tap count is a multiple of 3, so the ring slot of group (kt, s)
-  // is s % 3 at compile time: 3x3; else 2, by parity)
-  constexpr int WD = T % 3 == 0 ? 3 : 2;
-  x6::bf16x8 fa[WD][3], fb[2][3];
+  x6::bf16x8 fa[2][3], fb[2][3];
   auto read_b = [&](x6::bf16x8 (&f)[3], const char* st, int s, int j) {
     const int kh = s / KW, kw = s - kh * KW;
     const char* p = st + bb[j] + kh * rpc * 16 + kw * 48;
@@ -450,13 +448,16 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
 #pragma unroll
       for (int t = 0; t < 3; ++t) f[t] = ap[q * cbx6::FRAG + t * 64];
     };
-    constexpr int PMAX = (PD + T - 2) / (T - 1);  // patch pieces per tap
+    // the next K-tile's patch pieces: loaded into staging registers at tap s,
+    // stored to the next stage SD taps later (SD = 2: a load has two taps of
+    // MFMAs, >= 1.5k cycles, to land; the input companion is mostly L2 misses)
+    constexpr int SD = T >= 4 ? 2 : 1;
+    constexpr int PMAX = (PD + T - SD - 1) / (T - SD);  // patch pieces per tap
     typedef int int4x __attribute__((ext_vector_type(4)));
-    int4x stg[2][PMAX];
+    int4x stg[SD + 1][PMAX];
 #pragma unroll
     for (int i = 0; i < PD; ++i) issue(0, 0, i);
     load_a(fa[0], 0);
-    if (WD == 3 && (T > 1 || KT > 1)) load_a(fa[1 % WD], 1);
     wait_vm<0>();
     __builtin_amdgcn_s_barrier();
     read_b(fb[0], smem, 0, 0);
@@ -468,27 +469,24 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
       char* nst = smem + ((kt + 1) & 1) * SFB + wave * PD * 1024 + lane * 16;
 #pragma unroll
       for (int s = 0; s < T; ++s) {
-        const int pa = WD == 3 ? s % 3 : (s + PAR) & 1;
+        const int pa = (s + PAR) & 1;
         const int q = kt * T + s;
         if (MORE) {
-          // block 0: the pieces loaded at tap s - 1 into the next stage, this
+          // block 0: the pieces loaded at tap s - SD into the next stage, this
           // tap's pieces into staging registers
-          if (s > 0) {
+          if (s >= SD) {
+            const int s0 = s - SD;
 #pragma unroll
-            for (int i = cbx6::piece_lo(s - 1, PD, T); i < cbx6::piece_lo(s, PD, T); ++i)
-              *reinterpret_cast<int4x*>(nst + i * 1024) = stg[(s - 1) & 1][i - cbx6::piece_lo(s - 1, PD, T)];
+            for (int i = cbx6::piece_lo_d(s0, PD, T, SD); i < cbx6::piece_lo_d(s0 + 1, PD, T, SD); ++i)
+              *reinterpret_cast<int4x*>(nst + i * 1024) = stg[s0 % (SD + 1)][i - cbx6::piece_lo_d(s0, PD, T, SD)];
           }
 #pragma unroll
-          for (int i = cbx6::piece_lo(s, PD, T); i < cbx6::piece_lo(s + 1, PD, T); ++i)
-            stg[s & 1][i - cbx6::piece_lo(s, PD, T)] = __builtin_bit_cast(
+          for (int i = cbx6::piece_lo_d(s, PD, T, SD); i < cbx6::piece_lo_d(s + 1, PD, T, SD); ++i)
+            stg[s % (SD + 1)][i - cbx6::piece_lo_d(s, PD, T, SD)] = __builtin_bit_cast(
                 int4x, __builtin_amdgcn_raw_buffer_load_b128(
                            xr, static_cast<int>(poff[i] + static_cast<uint32_t>(kt + 1) * 2u * PL), 0, 0));
         }
-        if constexpr (WD == 3) {
-          if (s + 2 < T || MORE) load_a(fa[(s + 2) % WD], q + 2);
-        } else {
-          if (s + 1 < T || MORE) load_a(fa[(pa + 1) % WD], q + 1);
-        }
+        if (s + 1 < T || MORE) load_a(fa[pa ^ 1], q + 1);
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
           const bool last = s == T - 1 && j == NB - 1;
@@ -1435,10 +1433,37 @@ constexpr uint32_t hi_mask(int q) { return q >= NQ ? 0u : (q % KQ == KQ - 1 ? 0x
 constexpr uint32_t lo_mask(int q) { return q >= NQ ? 0u : 0xFFFFFFFFu; }
 }  // namespace c1x6
 
+// RRAM_C1_STAMP (diagnostic build only, never the product): per-group
+// s_memtime cycle sums of k_conv1_ring_x6 (slots 0 .. G - 1: group g's
+// compute, G .. G + 2: the three barriers, G + 3: per-tile setup, G + 4: tile
+// count), summed over waves into g_c1_stamp (read by rram_debug_c1_stamps)
+#ifdef RRAM_C1_STAMP
+__device__ unsigned long long g_c1_stamp[64];
+__device__ __forceinline__ unsigned long long c1_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#endif
 template <int W>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img, int tiles) {
   using namespace c1x6;
+#ifdef RRAM_C1_STAMP
+  __shared__ unsigned long long st_lds[4][32];
+  if ((threadIdx.x & 63) < 32) st_lds[threadIdx.x >> 6][threadIdx.x & 63] = 0;
+  unsigned long long tprev = 0;
+  auto stamp_to = [&](int slot) __attribute__((always_inline)) {
+    const unsigned long long tn = c1_stamp();
+    if ((threadIdx.x & 63) == 0) st_lds[threadIdx.x >> 6][slot] += tn - tprev;
+    tprev = tn;
+  };
+#define RRAM_C1_ST(slot) stamp_to(slot)
+#else
+#define RRAM_C1_ST(slot)
+#endif
   constexpr int OW = (W - 11) / 4 + 1, MI = 3;
   static_assert(4 * (OW - 1) + 4 * KQ <= ROWE, "slot rows too short");
   __shared__ __attribute__((aligned(16))) char smem[3 * SLOTB];
@@ -1573,6 +1598,10 @@ k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img,
   };
   auto tile_body = [&](auto cc, int t) __attribute__((always_inline)) {
     constexpr int CUR = decltype(cc)::value;
+#ifdef RRAM_C1_STAMP
+    tprev = c1_stamp();
+    if ((threadIdx.x & 63) == 0) st_lds[threadIdx.x >> 6][G + 4] += 1;
+#endif
     const TileRef cur = tile_ref(t), nxt = tile_ref(t + nwg);
     const int img = cur.img, sp0 = (t - img * tiles_per_img) * BN, f = cur.f;
     // per-lane slot byte offsets (term 0, quad 0) of this wave's two 32-column blocks
@@ -1626,6 +1655,7 @@ k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img,
     x6::Parts F[2][2];
 #pragma unroll
     for (int part = 0; part < 6; ++part) read_part(F[0], 0, part);
+    RRAM_C1_ST(G + 3);
     static_for<0, G>([&](auto gc) {
       constexpr int g = decltype(gc)::value;
       x6::Parts (&fc)[2] = F[g & 1];
@@ -1665,7 +1695,11 @@ k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img,
       }
       // barriers: after the last readers of channel 0 / 1 (their slots are then
       // refilled) and at the end of the tile
-      if (g == last_group(0) || g == last_group(1) || g == G - 1) lds_barrier();
+      RRAM_C1_ST(g);
+      if (g == last_group(0) || g == last_group(1) || g == G - 1) {
+        lds_barrier();
+        RRAM_C1_ST(G + (g == last_group(0) ? 0 : g == last_group(1) ? 1 : 2));
+      }
     });
     // this tile's output offsets, stored under the next tile (bias + ReLU:
     // conv_epilogue_nchw's arithmetic; the bias from LDS)
@@ -1681,6 +1715,10 @@ k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img,
     if (t + nwg >= tiles) {
 #pragma unroll
       for (int s8 = 0; s8 < 12; ++s8) store_part(acc[0], s8);
+#ifdef RRAM_C1_STAMP
+      if ((threadIdx.x & 63) == 0)
+        for (int k = 0; k < G + 5; ++k) atomicAdd(&g_c1_stamp[k], st_lds[threadIdx.x >> 6][k]);
+#endif
       return;
     }
     tile_body(std::integral_constant<int, 1>{}, t + nwg);
@@ -1689,7 +1727,12 @@ k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img,
 #pragma unroll
     for (int s8 = 0; s8 < 12; ++s8) store_part(acc[1], s8);
   }
+#ifdef RRAM_C1_STAMP
+  if ((threadIdx.x & 63) == 0)
+    for (int k = 0; k < G + 5; ++k) atomicAdd(&g_c1_stamp[k], st_lds[threadIdx.x >> 6][k]);
+#endif
 }
+#undef RRAM_C1_ST
 
 // Weight repack for k_conv1_ring_x6: w [M][3][11][11] -> fragments
 // [27 groups][3 row blocks][3 terms][64 lanes][8 bf16]; lane (lr, h) of
@@ -1777,15 +1820,17 @@ constexpr int RLB = 2 * 96 + 16;  // packed A row bytes per K-tile ([g][h][term]
 // pieces of t + 1 are issued first, then the B pieces of t + 2, and the end
 // of the tile waits with vmcnt(B pieces) (the B of t + 1, issued a tile
 // earlier, and the A of t + 1 have then landed).
-template <int MI, int NJ>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+// NW waves per workgroup (4, or 8 = two per SIMD at one workgroup per CU:
+// one wave's LDS / weight waits then run under the other's MFMAs).
+template <int MI, int NJ, int NW>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4, NW / 4)))
 k_gemm_x6(Params P, const uint16_t* __restrict__ apack, int ktiles_all, int ktc) {
   using namespace g2;
-  // tile 32 MI x 128 NJ: wave w owns all rows x columns 32 NJ w .. 32 NJ w + 32 NJ - 1
-  constexpr int BMc = 32 * MI, BNc = 128 * NJ, KT = gx6::KT;
+  // tile 32 MI x 32 NJ NW: wave w owns all rows x columns 32 NJ w .. 32 NJ w + 32 NJ - 1
+  constexpr int BMc = 32 * MI, BNc = 32 * NJ * NW, KT = gx6::KT;
   constexpr int A_B = BMc * gx6::RLB;
-  constexpr int A_DMA = ((A_B + 1023) / 1024 + 3) / 4;
-  constexpr int A_REGB = A_DMA * 4 * 1024;
+  constexpr int A_DMA = ((A_B + 1023) / 1024 + NW - 1) / NW;
+  constexpr int A_REGB = A_DMA * NW * 1024;
   constexpr int B_DMA = 4 * NJ;                          // 1 KB pieces (8 rows x 32 k) per wave
   constexpr int B_REGB = BNc * KT * 4, NBS = 3;
   constexpr int NVM = A_DMA + B_DMA;
@@ -2144,7 +2189,7 @@ struct CbPlan {
 #define RRAM_CB_LIST(X)                                                                              \
   X(5, 4, 8, 15, 1) X(5, 4, 4, 12, 1) X(5, 4, 4, 14, 1) X(5, 2, 4, 14, 1) X(3, 4, 8, 12, 1)          \
   X(3, 4, 8, 15, 1) X(3, 4, 4, 8, 1) X(3, 4, 4, 12, 1) X(3, 2, 4, 12, 1) X(3, 2, 4, 14, 1)
-#define RRAM_CB16_LIST(X) X(5, 4, 4, 8, 2) X(3, 4, 4, 8, 2)
+#define RRAM_CB16_LIST(X) X(5, 4, 4, 8, 2) X(3, 4, 4, 8, 2) X(3, 2, 2, 8, 2)
 bool cb_instantiated(int KH, int WR, int NB, int PD, int OCC = 1) {
 #define RRAM_X(kh, wr, nb, pd, occ) \
   if (KH == kh && WR == wr && NB == nb && PD == pd && OCC == occ) return true;
@@ -2218,29 +2263,52 @@ bool conv_cb_plan(const rram_conv_desc* d, CbPlan& pl) {
       pl = CbPlan{WR, NB, RPC, PD, octb, tiles_m, tiles_n, 1, 0};
     }
   }
-  // a 128 x 128 tile whose patch fits 8 pieces per wave runs two workgroups
-  // per CU (64 KB LDS, <= 256 registers each): one's prologue / epilogue then
-  // overlaps the other's MFMAs (AlexNet conv5 215 -> 204 us per layer; forced
-  // on conv4's 192-row groups it lost to the 64 x 256 tile, 279 -> 335)
-  if (best > 0 && pl.WR == 4 && pl.NB == 4 && pl.PD == 8 && cb_instantiated(KH, 4, 4, 8, 2)) pl.OCC = 2;
-  // a layer whose 128 x 128 contiguous tiles need more than 8 pieces (tiles
-  // spanning two images carry two halos: AlexNet conv2's 5 x 5) takes
-  // per-image tiles at two workgroups per CU when their patch fits 8 pieces
-  // and their makespan (rounds of 512 half-CU tiles) is no worse
-  if (best > 0 && pl.OCC == 1 && cb_instantiated(KH, 4, 4, 8, 2)) {
-    const int BM = 128, BN = 128;
-    const int tiles_m = (M + BM - 1) / BM, tpi = (HW + BN - 1) / BN;
-    int rmax = 0;
-    for (int t = 0; t < tpi; ++t) {
-      const int f = t * BN / OW, l = (std::min((t + 1) * BN, HW) - 1) / OW;
-      rmax = std::max(rmax, l - f + KH);
+  // Two workgroups per CU (k_conv_cb16_x6: <= 256 registers and 8 LDS
+  // pieces = 64 KB each): one workgroup's waits, prologue and epilogue then
+  // run under the other's MFMAs.  Tiles 128 x 128 or 64 x 128, contiguous
+  // positions or per-image (one halo: AlexNet conv2's 5 x 5); the least
+  // makespan in rounds of 512 half-CU tiles wins (ties: taller, contiguous)
+  // and replaces the one-per-CU plan unless that one's makespan is > 10 %
+  // shorter.
+  // Measured on MI355X (AlexNet b256): conv3 128 x 256 -> 128 x 128 here
+  // 0.342 -> 0.308 ms (profiles/r05_ab_occ2.txt); round 4: conv5 215 -> 204.
+  if (best > 0) {
+    int64_t best2 = -1;
+    CbPlan p2{};
+    static const int cfg2[2][2] = {{4, 4}, {2, 2}};
+    for (const auto& c : cfg2) {
+      const int WR = c[0], NB = c[1], BM = 32 * WR, BN = 32 * NB * (4 / WR);
+      if (!cb_instantiated(KH, WR, NB, 8, 2)) continue;
+      const int tiles_m = (M + BM - 1) / BM;
+      if ((tiles_m * BM - M) * 4 > tiles_m * BM) continue;
+      for (int per_image = 0; per_image < 2; ++per_image) {
+        int rmax = 0, tpi = 0, octb = 0;
+        if (!per_image) {
+          rmax = patch_rows(N, HW, OW, OH, KH, BN, 3);
+          if (rmax < 0) continue;
+          octb = ((rmax * RPC + 2 * ((3 * OW * (1 - KH)) & 15)) * 16 + 255) / 256 * 256;
+        } else {
+          tpi = (HW + BN - 1) / BN;
+          for (int t = 0; t < tpi; ++t) {
+            const int f = t * BN / OW, l = (std::min((t + 1) * BN, HW) - 1) / OW;
+            rmax = std::max(rmax, l - f + KH);
+          }
+          octb = (rmax * RPC * 16 + 255) / 256 * 256;
+        }
+        if ((2 * octb / 16 + 255) / 256 > 8) continue;
+        const int tiles_n = per_image ? tpi * d->num : (N + BN - 1) / BN;
+        const int64_t nwg = (int64_t)G * tiles_m * tiles_n;
+        if (nwg >= (1ll << 31)) continue;
+        const int64_t cost = (nwg + 511) / 512 * 2 * BM * BN;
+        if (best2 < 0 || cost < best2) {
+          best2 = cost;
+          p2 = CbPlan{WR, NB, RPC, 8, octb, tiles_m, tiles_n, 2, tpi};
+        }
+      }
     }
-    const int octb = (rmax * RPC * 16 + 255) / 256 * 256;
-    const int need = (2 * octb / 16 + 255) / 256;
-    const int64_t nwg = (int64_t)G * tiles_m * tpi * d->num;
-    const int64_t cost = (nwg + 511) / 512 * 2 * BM * BN;
-    if ((tiles_m * BM - M) * 4 <= tiles_m * BM && need <= 8 && nwg < (1ll << 31) && cost <= best)
-      pl = CbPlan{4, 4, RPC, 8, octb, tiles_m, static_cast<int>(tpi * d->num), 2, tpi};
+    // (rounds x area prices a round of two workgroups like one of twice the
+    // area; measured, the pair runs ~10 % faster: conv3 0.342 -> 0.308 ms)
+    if (best2 > 0 && best2 * 9 <= best * 10) pl = p2;
   }
   return best > 0;
 }
@@ -2249,9 +2317,8 @@ bool conv_cb_plan(const rram_conv_desc* d, CbPlan& pl) {
 // others on 32x32x16.  Measured on MI355X (AlexNet b256,
 // profiles/r04_ab_cb16.txt): the 16x16x32 loop holds a 6-13 % higher clock;
 // conv2 (5x5, two workgroups per CU) 0.482 -> 0.457-0.461 ms, conv5 (3x3, two
-// per CU) 0.170 -> 0.166; conv3 / conv4 (one per CU) lose MFMA-busy (0.64 ->
-// 0.59, 0.54 -> 0.51) faster than they gain clock (0.340 -> 0.350, 0.287 ->
-// 0.300), so they stay on 32x32x16.
+// per CU) 0.170 -> 0.166; at one workgroup per CU the 16x16x32 form lost
+// MFMA-busy (conv3 0.64 -> 0.59) faster than it gained clock.
 int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, const float* w, const float* bias,
                    float* y, void* y_oct, int relu, hipStream_t s, const WPack& wk) {
   CbPlan pl;
@@ -2560,7 +2627,7 @@ int conv_patch_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, c
 
 // shape plan of the x6 GEMM (false: not covered)
 struct GemmPlan {
-  int MI, NJ, tiles_m, tiles_n, ktiles, split, ktc;
+  int MI, NJ, NW, tiles_m, tiles_n, ktiles, split, ktc;
 };
 bool gemm_x6_plan(int M, int N, int K, size_t ws_bytes, GemmPlan& pl) {
   if (K < 256 || K % 4 != 0 || (int64_t)M * N * K < (1ll << 24)) return false;
@@ -2568,14 +2635,22 @@ bool gemm_x6_plan(int M, int N, int K, size_t ws_bytes, GemmPlan& pl) {
   // the rows pad, else 128 (or 96) x 256
   const int t256 = (M + 255) / 256 * 256, t128 = (M + 127) / 128 * 128, t96 = (M + 95) / 96 * 96;
   // (128 x 256 tiles for fc6 / fc7 measured 1-3 % slower, round 4)
+  pl.NW = 4;
   if ((t256 - M) * 4 <= t256) {
     pl.MI = 8;
     pl.NJ = 1;
+#ifdef RRAM_FC_NW8
+    // (A/B build) 128 x 256 tiles of 8 waves: two waves per SIMD
+    if ((t128 - M) * 4 <= t128) {
+      pl.MI = 4;
+      pl.NW = 8;
+    }
+#endif
   } else {
     pl.MI = (t96 - M) < (t128 - M) ? 3 : 4;
     pl.NJ = 2;
   }
-  const int BMc = 32 * pl.MI, BNc = 128 * pl.NJ;
+  const int BMc = 32 * pl.MI, BNc = 32 * pl.NJ * pl.NW;
   pl.tiles_m = (M + BMc - 1) / BMc;
   pl.tiles_n = (N + BNc - 1) / BNc;
   pl.ktiles = (K + gx6::KT - 1) / gx6::KT;
@@ -2630,12 +2705,14 @@ int gemm_x6_nt(int M, int N, int K, float alpha, const float* A, int lda, const 
   P.tiles_n = tiles_n;
   P.tiles_z = split;
   const unsigned nwg = static_cast<unsigned>(tiles * split);
-  if (MI == 8)
-    hipLaunchKernelGGL((k_gemm_x6<8, 1>), dim3(nwg), dim3(256), 0, s, P, ap, ktiles, ktc);
+  if (pl.NW == 8)
+    hipLaunchKernelGGL((k_gemm_x6<4, 1, 8>), dim3(nwg), dim3(512), 0, s, P, ap, ktiles, ktc);
+  else if (MI == 8)
+    hipLaunchKernelGGL((k_gemm_x6<8, 1, 4>), dim3(nwg), dim3(256), 0, s, P, ap, ktiles, ktc);
   else if (MI == 3)
-    hipLaunchKernelGGL((k_gemm_x6<3, 2>), dim3(nwg), dim3(256), 0, s, P, ap, ktiles, ktc);
+    hipLaunchKernelGGL((k_gemm_x6<3, 2, 4>), dim3(nwg), dim3(256), 0, s, P, ap, ktiles, ktc);
   else
-    hipLaunchKernelGGL((k_gemm_x6<4, 2>), dim3(nwg), dim3(256), 0, s, P, ap, ktiles, ktc);
+    hipLaunchKernelGGL((k_gemm_x6<4, 2, 4>), dim3(nwg), dim3(256), 0, s, P, ap, ktiles, ktc);
   rc = launch_status("gemm x6");
   if (rc) return rc;
   if (split > 1) {
@@ -2650,6 +2727,16 @@ int gemm_x6_nt(int M, int N, int K, float alpha, const float* A, int lda, const 
 }  // namespace rram
 
 extern "C" {
+
+#ifdef RRAM_C1_STAMP
+// diagnostic build only: the conv1 stamp sums (and reset)
+int rram_debug_c1_stamps(unsigned long long* out, int n) {
+  if (out != nullptr && hipMemcpyFromSymbol(out, HIP_SYMBOL(rram::g_c1_stamp), sizeof(unsigned long long) * n) != hipSuccess)
+    return -2;
+  unsigned long long z[64] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(rram::g_c1_stamp), z, sizeof(z)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 int rram_f32_engine_for_conv(const rram_conv_desc* d) {
   RRAM_REQUIRE(d != nullptr, "engine query: desc is NULL");
