@@ -357,17 +357,12 @@ int rram_conv2d_bwd(const rram_conv_desc* d_in, const float* x, const float* w, 
   const int T = d.kernel_h * d.kernel_w;
   const int eph = d.dilation_h * (d.kernel_h - 1) - d.pad_h, epw = d.dilation_w * (d.kernel_w - 1) - d.pad_w;
   const size_t wt_bytes = (size_t)d.channels * cout_g * T * sizeof(float);
-  // The forward's grid must fill the chip: below ~128 tiles of 32 channels x
-  // 128 positions (CIFAR conv3 100x32x8x8, LeNet conv2 64x20x12x12: 50 / 72)
-  // each workgroup walks a long K = cout*k*k alone and the GEMM + col2im pair
-  // is 1.4-1.6x faster (profiles/r04_ab_dx_fwd.txt)
-  const int64_t dx_tiles = (int64_t)G * ((cin_g + 31) / 32) * (((int64_t)d.num * d.height * d.width + 127) / 128);
-#ifdef RRAM_DX_FWD_ALL
-  (void)dx_tiles;
+  // (round 4 kept the data GEMM + col2im for grids below 128 tiles of 32
+  // channels x 128 positions, 1.4-1.6x faster then, profiles/r04_ab_dx_fwd.txt;
+  // since the thin convolution forwards split K, the flipped-kernel forward
+  // wins there too: CIFAR-10 full training 0.419-0.421 -> 0.408-0.411 ms per
+  // iteration, profiles/r05_ab_occ2_plans.txt)
   const bool dx_fwd = dx && d.stride_h == 1 && d.stride_w == 1 &&
-#else
-  const bool dx_fwd = dx && dx_tiles >= 128 && d.stride_h == 1 && d.stride_w == 1 &&
-#endif
                       eph >= 0 && epw >= 0 &&
                       ws != nullptr && ws_bytes >= wt_bytes && wt_bytes < (1ull << 31) &&
                       (int64_t)d.num * d.height * d.width < (1ll << 31) &&

@@ -1734,6 +1734,214 @@ k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img,
 }
 #undef RRAM_C1_ST
 
+// ---------------------------------------------------------------------------
+// k_conv1_pair_x6: AlexNet conv1 at two workgroups per CU, six waves each
+// (three per SIMD), so one wave's refill split, LDS waits and epilogue run
+// under the other waves' MFMAs (k_conv1_ring_x6 has one wave per SIMD and
+// its MFMA pipe sat idle half the time).  Same K order as the ring kernel
+// (25 groups of 4 quads, lane half h reading quads 4g + h and 4g + 2 + h,
+// the same packed weight fragments from k_conv1_pack_x6, the same padding
+// masks); what changes is the tiling:
+//  * a tile is 96 filters x 128 positions of one image (<= 4 output rows,
+//    so <= 23 input rows); wave (wm, wn) owns rows 32 wm .. + 31 (its row
+//    block of every weight fragment: the six waves together read the weights
+//    once per tile, as the ring kernel's four) and columns 64 wn .. + 63;
+//  * the input is split into bf16 terms once per element into two LDS
+//    channel slots (channel 0 -> slot 0, 1 -> slot 1, 2 -> slot 0 again):
+//    channel 2's loads are issued in the prologue and land under groups
+//    0 .. 8; its split + stores follow the barrier after group 8 (the last
+//    reader of channel 0), and a barrier after group 14 makes them visible
+//    before group 15 prefetches group 16's B (the first reader of channel 2);
+//  * weights from L2 two groups ahead; accumulators single-buffered (the
+//    other workgroup covers the epilogue).
+// LDS: 2 slots x 3 terms x 23 rows x 248 bf16 = 67 KB per workgroup.
+namespace c1p {
+constexpr int BN = 128, NT = 384;
+constexpr int ROWS = 23;                          // input rows of <= 4 output rows: 3 * 4 + 11
+constexpr int ROWE = c1x6::ROWE;                  // 248 elements per row (bank spacing of c1x6)
+constexpr int TERMB = ROWS * ROWE * 2;
+constexpr int SLOTB = 3 * TERMB;
+constexpr int QP = ROWE / 8;                      // 8-element chunks per row
+constexpr int CHUNKS = ROWS * QP;
+constexpr int CPT = (CHUNKS + NT - 1) / NT;       // chunks per thread per channel
+constexpr int slot_of(int c) { return c == 1 ? 1 : 0; }
+// LDS byte offset of quad q (channel slot, kernel row, column quad) relative to a lane's base
+constexpr int quad_off(int q) {
+  return slot_of(q / (c1x6::KR * c1x6::KQ)) * SLOTB + (((q / c1x6::KQ) % c1x6::KR) * ROWE + 4 * (q % c1x6::KQ)) * 2;
+}
+constexpr int half_delta(int q) { return q + 1 < c1x6::NQ ? quad_off(q + 1) - quad_off(q) : 0; }
+static_assert(2 * SLOTB <= 80 * 1024, "two workgroups per CU");
+}  // namespace c1p
+
+template <int W>
+__global__ void __launch_bounds__(c1p::NT) __attribute__((amdgpu_waves_per_eu(3, 3)))
+k_conv1_pair_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img) {
+  using namespace c1x6;
+  using c1p::BN;
+  using c1p::NT;
+  constexpr int OW = (W - 11) / 4 + 1;
+  static_assert(4 * (OW - 1) + 4 * KQ <= c1p::ROWE, "slot rows too short");
+  __shared__ __attribute__((aligned(16))) char smem[2 * c1p::SLOTB];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave % 3, wn = wave / 3;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int HWo = P.cv.howo.d, H = P.cv.H;
+  const float* const xin = P.b.p;
+  const int in_bytes = static_cast<int>(P.cv.in_bytes);
+
+  // XCD-aware tile order: each XCD walks a contiguous range of tiles, so the
+  // input rows two consecutive tiles of an image share are L2 hits
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, loc = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+  const int t = __builtin_amdgcn_readfirstlane((xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc);
+  const int img = __builtin_amdgcn_readfirstlane(t / tiles_per_img);
+  const int sp0 = __builtin_amdgcn_readfirstlane((t - img * tiles_per_img) * BN);
+  const int f = __builtin_amdgcn_readfirstlane(sp0 / OW);
+
+  // ---- staging: chunk k of this thread = (slot row, 8 input columns); the
+  // last threads' extra chunks redo chunk CHUNKS - 1 (a benign duplicate) ----
+  float sv[c1p::CPT][8];
+  auto chunk_of = [&](int k) __attribute__((always_inline)) { return min((int)threadIdx.x + k * NT, c1p::CHUNKS - 1); };
+  auto stage_load = [&](int c, int k) __attribute__((always_inline)) {
+    const int q = chunk_of(k);
+    const int ri = q / c1p::QP, qp = q - ri * c1p::QP;
+    const bool ok = 4 * f + ri < H;
+    const int rowoff = (((img * 3 + c) * H + 4 * f + ri) * W + 8 * qp) * 4;
+    const uint32_t voff = ok ? static_cast<uint32_t>(rowoff) : 0x80000000u;
+    const __amdgpu_buffer_rsrc_t xrs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xin), 0, in_bytes, 0x00020000);
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      sv[k][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xrs, static_cast<int>(voff + 4 * e), 0, 0));
+  };
+  auto stage_store = [&](int c, int k) __attribute__((always_inline)) {
+    const int q = chunk_of(k);
+    const int ri = q / c1p::QP, qp = q - ri * c1p::QP;
+    // columns past the image row loaded the next row's (or, past the buffer,
+    // zero) values: zero them (kernel column 11's weights are zero, and an
+    // Inf there would make 0 * Inf = NaN)
+    const int nv = W - 8 * qp;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = e < nv ? sv[k][e] : 0.0f;
+    char* base = smem + c1p::slot_of(c) * c1p::SLOTB + (ri * c1p::ROWE + 8 * qp) * 2;
+    x6::Parts tp;
+    x6::split8_safe(v, tp);
+    *reinterpret_cast<x6::bf16x8*>(base) = tp.h;
+    *reinterpret_cast<x6::bf16x8*>(base + c1p::TERMB) = tp.m;
+    *reinterpret_cast<x6::bf16x8*>(base + 2 * c1p::TERMB) = tp.l;
+  };
+  auto lds_barrier = [&]() __attribute__((always_inline)) {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done
+    __builtin_amdgcn_s_barrier();
+  };
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+#pragma unroll
+    for (int k = 0; k < c1p::CPT; ++k) stage_load(c, k);
+#pragma unroll
+    for (int k = 0; k < c1p::CPT; ++k) stage_store(c, k);
+  }
+#pragma unroll
+  for (int k = 0; k < c1p::CPT; ++k) stage_load(2, k);  // channel 2: stored after group last_group(0)
+
+  // weights: this wave's row block of fragment (g, wm), two groups ahead
+  const x6::bf16x8* ap = reinterpret_cast<const x6::bf16x8*>(wpack) + wm * 3 * 64 + lane;
+  auto load_a = [&](x6::bf16x8 (&fr)[3], int g) __attribute__((always_inline)) {
+#pragma unroll
+    for (int tt = 0; tt < 3; ++tt) fr[tt] = ap[(g * 9 + tt) * 64];
+  };
+  x6::bf16x8 fg[3][3];
+  load_a(fg[0], 0);
+  load_a(fg[1], 1);
+
+  // per-lane slot byte offsets (term 0, quad 0) of this wave's two 32-column blocks
+  uint32_t lb[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int sp = min(sp0 + wn * 64 + j * 32 + lr, HWo - 1);
+    const int oh = sp / OW, ow = sp - oh * OW;
+    lb[j] = static_cast<uint32_t>((4 * (oh - f) * c1p::ROWE + 4 * ow) * 2);
+  }
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  auto pick = [&](uint32_t h0, uint32_t h1) __attribute__((always_inline)) { return lh ? h1 : h0; };
+  auto mask_q = [&](u32x2 v, int q0) __attribute__((always_inline)) {
+    if (lo_mask(q0) != 0xFFFFFFFFu || lo_mask(q0 + 1) != 0xFFFFFFFFu) v[0] &= pick(lo_mask(q0), lo_mask(q0 + 1));
+    if (hi_mask(q0) != 0xFFFFFFFFu || hi_mask(q0 + 1) != 0xFFFFFFFFu) v[1] &= pick(hi_mask(q0), hi_mask(q0 + 1));
+    return v;
+  };
+  // B fragment term tt of column block j for group g: quads 4g + h and 4g + 2 + h
+  auto read_part = [&](x6::Parts (&F)[2], int g, int part) __attribute__((always_inline)) {
+    const int j = part / 3, tt = part % 3;
+    const int qa = 4 * g, qb = 4 * g + 2;
+    const char* ba = smem + lb[j] + (lh ? c1p::half_delta(qa) : 0) + tt * c1p::TERMB;
+    const char* bb = smem + lb[j] + (lh ? c1p::half_delta(qb) : 0) + tt * c1p::TERMB;
+    const u32x2 lo = mask_q(*reinterpret_cast<const u32x2*>(ba + c1p::quad_off(qa)), qa);
+    const u32x2 hi = mask_q(*reinterpret_cast<const u32x2*>(bb + c1p::quad_off(qb)), qb);
+    const x6::bf16x8 v = __builtin_bit_cast(x6::bf16x8, u32x4{lo[0], lo[1], hi[0], hi[1]});
+    if (tt == 0) F[j].h = v;
+    else if (tt == 1) F[j].m = v;
+    else F[j].l = v;
+  };
+  floatx16 acc[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
+  lds_barrier();  // channels 0 and 1 in their slots
+  x6::Parts F[2][2];
+#pragma unroll
+  for (int part = 0; part < 6; ++part) read_part(F[0], 0, part);
+  static_for<0, G>([&](auto gc) {
+    constexpr int g = decltype(gc)::value;
+    x6::Parts (&fc)[2] = F[g & 1];
+    x6::Parts (&fn)[2] = F[(g + 1) & 1];
+    if (g + 2 < G) load_a(fg[(g + 2) % 3], g + 2);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const auto& fa = fg[g % 3];
+      acc[j] = x6::mfma6(x6::Parts{fa[0], fa[1], fa[2]}, fc[j], acc[j]);
+      // the next group's B fragments under this block's MFMAs
+      if (g + 1 < G) {
+#pragma unroll
+        for (int part = 3 * j; part < 3 * j + 3; ++part) read_part(fn, g + 1, part);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (g == last_group(0)) {
+      // every wave is past channel 0 (its last B fragments were read during
+      // group g - 1 and consumed here): slot 0 takes channel 2
+      lds_barrier();
+#pragma unroll
+      for (int k = 0; k < c1p::CPT; ++k) stage_store(2, k);
+    }
+    // channel 2's stores visible before group first_group(2)'s B is read
+    // (during group first_group(2) - 1)
+    if (g == first_group(2) - 2) lds_barrier();
+  });
+  // epilogue: bias + ReLU (conv_epilogue_nchw's arithmetic), lanes past the
+  // image's last position store nothing
+  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(P.e.C, 0, 0x7FFFFFFF, 0x00020000);
+  const bool relu = P.e.relu != 0;
+  const int mw = 32 * wm + 4 * lh;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int sp = sp0 + wn * 64 + j * 32 + lr;
+    const uint32_t ob = sp < HWo ? static_cast<uint32_t>(((int64_t)img * P.e.cimg + sp + (int64_t)mw * HWo) * 4)
+                                 : 0x80000000u;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int dr = (r & 3) + 8 * (r >> 2);
+      const float b = P.e.bias != nullptr ? P.e.bias[mw + dr] : 0.0f;
+      const float o = acc[j][r] + b;
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, relu ? fmaxf(o, 0.0f) : o), ors,
+                                            static_cast<int>(ob), dr * HWo * 4, 0);
+    }
+  }
+}
+
 // Weight repack for k_conv1_ring_x6: w [M][3][11][11] -> fragments
 // [27 groups][3 row blocks][3 terms][64 lanes][8 bf16]; lane (lr, h) of
 // fragment (g, i): row 32 i + lr, items j of half h = quads 2 g, 2 g + 1 in
@@ -1820,17 +2028,15 @@ constexpr int RLB = 2 * 96 + 16;  // packed A row bytes per K-tile ([g][h][term]
 // pieces of t + 1 are issued first, then the B pieces of t + 2, and the end
 // of the tile waits with vmcnt(B pieces) (the B of t + 1, issued a tile
 // earlier, and the A of t + 1 have then landed).
-// NW waves per workgroup (4, or 8 = two per SIMD at one workgroup per CU:
-// one wave's LDS / weight waits then run under the other's MFMAs).
-template <int MI, int NJ, int NW>
-__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4, NW / 4)))
+template <int MI, int NJ>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 k_gemm_x6(Params P, const uint16_t* __restrict__ apack, int ktiles_all, int ktc) {
   using namespace g2;
-  // tile 32 MI x 32 NJ NW: wave w owns all rows x columns 32 NJ w .. 32 NJ w + 32 NJ - 1
-  constexpr int BMc = 32 * MI, BNc = 32 * NJ * NW, KT = gx6::KT;
+  // tile 32 MI x 128 NJ: wave w owns all rows x columns 32 NJ w .. 32 NJ w + 32 NJ - 1
+  constexpr int BMc = 32 * MI, BNc = 128 * NJ, KT = gx6::KT;
   constexpr int A_B = BMc * gx6::RLB;
-  constexpr int A_DMA = ((A_B + 1023) / 1024 + NW - 1) / NW;
-  constexpr int A_REGB = A_DMA * NW * 1024;
+  constexpr int A_DMA = ((A_B + 1023) / 1024 + 3) / 4;
+  constexpr int A_REGB = A_DMA * 4 * 1024;
   constexpr int B_DMA = 4 * NJ;                          // 1 KB pieces (8 rows x 32 k) per wave
   constexpr int B_REGB = BNc * KT * 4, NBS = 3;
   constexpr int NVM = A_DMA + B_DMA;
@@ -2108,6 +2314,8 @@ int conv_wide_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, co
     const int rc = launch_status("conv1 weight pack x6");
     if (rc) return rc;
   }
+#ifdef RRAM_C1_RING
+  // (A/B build) the persistent one-workgroup-per-CU ring kernel
   const int tpi = (HW + c1x6::BN - 1) / c1x6::BN;
   const int tiles = d->num * tpi;
   int cus = 256;
@@ -2115,7 +2323,14 @@ int conv_wide_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, co
   const unsigned nwg = static_cast<unsigned>(std::min(tiles, cus));
   hipLaunchKernelGGL((k_conv1_ring_x6<227>), dim3(nwg), dim3(256), 0, s, P, reinterpret_cast<const uint16_t*>(wp),
                      tpi, tiles);
-  const int rc = launch_status("conv1 ring x6");
+#else
+  const int tpi = (HW + c1p::BN - 1) / c1p::BN;
+  const int64_t tiles = (int64_t)d->num * tpi;
+  RRAM_REQUIRE(tiles < (1ll << 31), "conv1: grid too large");
+  hipLaunchKernelGGL((k_conv1_pair_x6<227>), dim3(static_cast<unsigned>(tiles)), dim3(c1p::NT), 0, s, P,
+                     reinterpret_cast<const uint16_t*>(wp), tpi);
+#endif
+  const int rc = launch_status("conv1 x6");
   return rc ? rc : 1;
 }
 
@@ -2268,8 +2483,7 @@ bool conv_cb_plan(const rram_conv_desc* d, CbPlan& pl) {
   // run under the other's MFMAs.  Tiles 128 x 128 or 64 x 128, contiguous
   // positions or per-image (one halo: AlexNet conv2's 5 x 5); the least
   // makespan in rounds of 512 half-CU tiles wins (ties: taller, contiguous)
-  // and replaces the one-per-CU plan unless that one's makespan is > 10 %
-  // shorter.
+  // and replaces the one-per-CU plan (see the rule below).
   // Measured on MI355X (AlexNet b256): conv3 128 x 256 -> 128 x 128 here
   // 0.342 -> 0.308 ms (profiles/r05_ab_occ2.txt); round 4: conv5 215 -> 204.
   if (best > 0) {
@@ -2299,16 +2513,26 @@ bool conv_cb_plan(const rram_conv_desc* d, CbPlan& pl) {
         const int tiles_n = per_image ? tpi * d->num : (N + BN - 1) / BN;
         const int64_t nwg = (int64_t)G * tiles_m * tiles_n;
         if (nwg >= (1ll << 31)) continue;
-        const int64_t cost = (nwg + 511) / 512 * 2 * BM * BN;
+        // a 64-row tile pays about a third more per MFMA (two waves read each
+        // weight fragment for half the columns): AlexNet conv5 (128 rows per
+        // group) 0.172 ms on 128 x 128 vs 0.184 on 64 x 128, while conv4
+        // (192 rows per group: 128-row tiles pad a quarter) 0.297 on its
+        // one-per-CU 64 x 256 plan vs 0.267 on 64 x 128
+        const int64_t cost = (nwg + 511) / 512 * 2 * BM * BN * (BM == 64 ? 4 : 3) / 3;
         if (best2 < 0 || cost < best2) {
           best2 = cost;
           p2 = CbPlan{WR, NB, RPC, 8, octb, tiles_m, tiles_n, 2, tpi};
         }
       }
     }
-    // (rounds x area prices a round of two workgroups like one of twice the
-    // area; measured, the pair runs ~10 % faster: conv3 0.342 -> 0.308 ms)
-    if (best2 > 0 && best2 * 9 <= best * 10) pl = p2;
+    // Rounds x area prices a round of two workgroups like one of twice the
+    // area, but measured the pair hides its waits: every AlexNet layer runs
+    // faster there although its estimate is up to a third longer (conv3
+    // 0.342 -> 0.308 ms at an equal estimate; conv4 0.297 -> 0.267 and conv5
+    // (round 4) 0.215 -> 0.204 at 4/3 of it).  Taken within 1.4x; round 4's
+    // loser, conv4 on 128 x 128 (a quarter of the rows padded, 0.279 ->
+    // 0.335 ms), estimates 1.5x.
+    if (best2 > 0 && best2 * 5 <= best * 7) pl = p2;
   }
   return best > 0;
 }
@@ -2627,7 +2851,7 @@ int conv_patch_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, c
 
 // shape plan of the x6 GEMM (false: not covered)
 struct GemmPlan {
-  int MI, NJ, NW, tiles_m, tiles_n, ktiles, split, ktc;
+  int MI, NJ, tiles_m, tiles_n, ktiles, split, ktc;
 };
 bool gemm_x6_plan(int M, int N, int K, size_t ws_bytes, GemmPlan& pl) {
   if (K < 256 || K % 4 != 0 || (int64_t)M * N * K < (1ll << 24)) return false;
@@ -2635,22 +2859,16 @@ bool gemm_x6_plan(int M, int N, int K, size_t ws_bytes, GemmPlan& pl) {
   // the rows pad, else 128 (or 96) x 256
   const int t256 = (M + 255) / 256 * 256, t128 = (M + 127) / 128 * 128, t96 = (M + 95) / 96 * 96;
   // (128 x 256 tiles for fc6 / fc7 measured 1-3 % slower, round 4)
-  pl.NW = 4;
+  // (an 8-wave 128 x 256 form, two waves per SIMD, measured no faster on
+  // fc6 / fc7: 0.122-0.124 vs 0.122-0.124 ms, profiles/r05_ab_occ2_plans.txt)
   if ((t256 - M) * 4 <= t256) {
     pl.MI = 8;
     pl.NJ = 1;
-#ifdef RRAM_FC_NW8
-    // (A/B build) 128 x 256 tiles of 8 waves: two waves per SIMD
-    if ((t128 - M) * 4 <= t128) {
-      pl.MI = 4;
-      pl.NW = 8;
-    }
-#endif
   } else {
     pl.MI = (t96 - M) < (t128 - M) ? 3 : 4;
     pl.NJ = 2;
   }
-  const int BMc = 32 * pl.MI, BNc = 32 * pl.NJ * pl.NW;
+  const int BMc = 32 * pl.MI, BNc = 128 * pl.NJ;
   pl.tiles_m = (M + BMc - 1) / BMc;
   pl.tiles_n = (N + BNc - 1) / BNc;
   pl.ktiles = (K + gx6::KT - 1) / gx6::KT;
@@ -2705,14 +2923,12 @@ int gemm_x6_nt(int M, int N, int K, float alpha, const float* A, int lda, const 
   P.tiles_n = tiles_n;
   P.tiles_z = split;
   const unsigned nwg = static_cast<unsigned>(tiles * split);
-  if (pl.NW == 8)
-    hipLaunchKernelGGL((k_gemm_x6<4, 1, 8>), dim3(nwg), dim3(512), 0, s, P, ap, ktiles, ktc);
-  else if (MI == 8)
-    hipLaunchKernelGGL((k_gemm_x6<8, 1, 4>), dim3(nwg), dim3(256), 0, s, P, ap, ktiles, ktc);
+  if (MI == 8)
+    hipLaunchKernelGGL((k_gemm_x6<8, 1>), dim3(nwg), dim3(256), 0, s, P, ap, ktiles, ktc);
   else if (MI == 3)
-    hipLaunchKernelGGL((k_gemm_x6<3, 2, 4>), dim3(nwg), dim3(256), 0, s, P, ap, ktiles, ktc);
+    hipLaunchKernelGGL((k_gemm_x6<3, 2>), dim3(nwg), dim3(256), 0, s, P, ap, ktiles, ktc);
   else
-    hipLaunchKernelGGL((k_gemm_x6<4, 2, 4>), dim3(nwg), dim3(256), 0, s, P, ap, ktiles, ktc);
+    hipLaunchKernelGGL((k_gemm_x6<4, 2>), dim3(nwg), dim3(256), 0, s, P, ap, ktiles, ktc);
   rc = launch_status("gemm x6");
   if (rc) return rc;
   if (split > 1) {

@@ -31,7 +31,7 @@ def sim(kind,OW,Ho,W,pad,KH,BN,NB,WC,N,tpi=0,shift=False):
         p1=sl(0)-f0+KH; p2=p1+(sl(1)+KH if nseg>1 else 0); R=p2+(sl(2)+KH if nseg>2 else 0)
         octb=((R*RPC+2*d)*16+255)//256*256
         def addr(n,plane):
-            n=min(n,plast); img=n//HW; sp=n-img*HW; oh=sp//OW; ow=sp-oh*OW; sg=img-img0
+            n=n if n<=plast else (max(n0,n-((n-plast+15)&~15)) if shift else plast); img=n//HW; sp=n-img*HW; oh=sp//OW; ow=sp-oh*OW; sg=img-img0
             prow= oh-f0 if sg==0 else (p1 if sg==1 else p2)+oh
             return plane*octb+(prow*RPC+sg*d)*16+ow*48
         toff=lambda s:(s//KH)*RPC*16+(s%KH)*48
@@ -52,4 +52,4 @@ cfgs=[("conv2 cb16",("cb16",27,27,27,2,5,128,4,1,256*729,6)),
       ("conv4 cb",("cb",13,13,13,1,3,256,4,2,256*169)),
       ("conv5 cb16",("cb16",13,13,13,1,3,128,4,1,256*169))]
 for name,a in cfgs:
-    print(name,"conflict frac %.3f -> shifted %.3f"%(sim(*a),sim(*a,shift=True)))
+    print(name,"conflict frac %.3f -> shifted + clamped %.3f"%(sim(*a),sim(*a,shift=True)))

@@ -106,14 +106,14 @@ def test_octet_kernel_tile_plans_host_side():
     """The channel-octet kernel's tile plans for AlexNet b256 (host logic, no
     GPU): every layer at two workgroups per CU (16x16x32 form):
     conv2's 5x5 on 128 x 128 per-image tiles (its contiguous 128 x 128 tiles
-    spanning two images would need more than 8 LDS pieces), conv3 on
-    contiguous 128 x 128 tiles, conv4 (192 rows per group) and conv5 (128 per
-    group) on contiguous 64 x 128 tiles (no padded rows, > 2 rounds of 512)."""
+    spanning two images would need more than 8 LDS pieces), conv3 and conv5
+    on contiguous 128 x 128 tiles, conv4 (192 rows per group) on contiguous
+    64 x 128 tiles (128-row tiles would pad a quarter of its rows)."""
     from rramsim import ops
     want = {"conv2": (((256, 96, 27, 27), 256, 5, 2, 2), dict(rows=128, cols=128, per_cu=2, tiles_per_image=6)),
             "conv3": (((256, 256, 13, 13), 384, 3, 1, 1), dict(rows=128, cols=128, per_cu=2, tiles_per_image=0)),
             "conv4": (((256, 384, 13, 13), 384, 3, 1, 2), dict(rows=64, cols=128, per_cu=2, tiles_per_image=0)),
-            "conv5": (((256, 384, 13, 13), 256, 3, 1, 2), dict(rows=64, cols=128, per_cu=2, tiles_per_image=0))}
+            "conv5": (((256, 384, 13, 13), 256, 3, 1, 2), dict(rows=128, cols=128, per_cu=2, tiles_per_image=0))}
     for name, ((x, cout, k, p, g), exp) in want.items():
         pl = ops.conv_octet_plan(ops.conv_desc(x, cout, k, 1, p, 1, g))
         assert pl is not None, name
