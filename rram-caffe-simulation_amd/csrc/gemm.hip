@@ -188,11 +188,10 @@ __device__ __forceinline__ void load_tile(Loader<ROWS, KB>& L, const View& vw, c
     const uint32_t pb4 = static_cast<uint32_t>((static_cast<int64_t>(im) * cv.chw + hb * cv.W + wb) * 4);
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(vw.p), 0, cv.in_bytes, 0x00020000);
-    const int r0 = row0 + static_cast<int>(threadIdx.x) / KB;
     uint32_t ones = 0;
 #pragma unroll
     for (int i = 0; i < EPT; ++i) {
-      const int2 t = cv.tbl[r0 + i * (256 / KB)];
+      const int2 t = L.rt[i];  // (loaded once per block: the thread's rows do not move)
       const bool ok = pv && static_cast<unsigned>(hb + (t.y & 0xFFFF)) < static_cast<unsigned>(cv.H) &&
                       static_cast<unsigned>(wb + (t.y >> 16)) < static_cast<unsigned>(cv.W);
       L.v[i] = __builtin_bit_cast(
@@ -448,6 +447,11 @@ __global__ void __launch_bounds__(256) RRAM_GEMM_OCC k_gemm(Params P) {
 
   Loader<BMr, KB> la;
   Loader<BNr, KB> lb;
+  if constexpr (BMODE == IM2T) {
+#pragma unroll
+    for (int i = 0; i < Loader<BNr, KB>::EPT; ++i)
+      lb.rt[i] = P.cv.tbl[n0 + static_cast<int>(threadIdx.x) / KB + i * (256 / KB)];
+  }
   const int ntiles = (kend - kbeg + KB - 1) / KB;
   if (ntiles > 0) {
     load_tile<AM, BMr, KB>(la, va, P.cv, col, m0, kbeg, kend);

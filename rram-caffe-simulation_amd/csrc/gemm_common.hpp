@@ -118,6 +118,7 @@ struct Loader {
   static constexpr int EPT = ROWS * KB / 256;
   float v[EPT];
   int kn[EPT / 4 > 0 ? EPT / 4 : 1];  // KCU: valid elements of float4 i (K - k, may be <= 0 or >= 4)
+  int2 rt[EPT];                       // IM2T: the table entries of this thread's rows (fixed per block)
 };
 
 // 16-byte zero block that guarded loads and bias selects read for out-of-range elements

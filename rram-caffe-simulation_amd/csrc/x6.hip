@@ -1734,214 +1734,6 @@ k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img,
 }
 #undef RRAM_C1_ST
 
-// ---------------------------------------------------------------------------
-// k_conv1_pair_x6: AlexNet conv1 at two workgroups per CU, six waves each
-// (three per SIMD), so one wave's refill split, LDS waits and epilogue run
-// under the other waves' MFMAs (k_conv1_ring_x6 has one wave per SIMD and
-// its MFMA pipe sat idle half the time).  Same K order as the ring kernel
-// (25 groups of 4 quads, lane half h reading quads 4g + h and 4g + 2 + h,
-// the same packed weight fragments from k_conv1_pack_x6, the same padding
-// masks); what changes is the tiling:
-//  * a tile is 96 filters x 128 positions of one image (<= 4 output rows,
-//    so <= 23 input rows); wave (wm, wn) owns rows 32 wm .. + 31 (its row
-//    block of every weight fragment: the six waves together read the weights
-//    once per tile, as the ring kernel's four) and columns 64 wn .. + 63;
-//  * the input is split into bf16 terms once per element into two LDS
-//    channel slots (channel 0 -> slot 0, 1 -> slot 1, 2 -> slot 0 again):
-//    channel 2's loads are issued in the prologue and land under groups
-//    0 .. 8; its split + stores follow the barrier after group 8 (the last
-//    reader of channel 0), and a barrier after group 14 makes them visible
-//    before group 15 prefetches group 16's B (the first reader of channel 2);
-//  * weights from L2 two groups ahead; accumulators single-buffered (the
-//    other workgroup covers the epilogue).
-// LDS: 2 slots x 3 terms x 23 rows x 248 bf16 = 67 KB per workgroup.
-namespace c1p {
-constexpr int BN = 128, NT = 384;
-constexpr int ROWS = 23;                          // input rows of <= 4 output rows: 3 * 4 + 11
-constexpr int ROWE = c1x6::ROWE;                  // 248 elements per row (bank spacing of c1x6)
-constexpr int TERMB = ROWS * ROWE * 2;
-constexpr int SLOTB = 3 * TERMB;
-constexpr int QP = ROWE / 8;                      // 8-element chunks per row
-constexpr int CHUNKS = ROWS * QP;
-constexpr int CPT = (CHUNKS + NT - 1) / NT;       // chunks per thread per channel
-constexpr int slot_of(int c) { return c == 1 ? 1 : 0; }
-// LDS byte offset of quad q (channel slot, kernel row, column quad) relative to a lane's base
-constexpr int quad_off(int q) {
-  return slot_of(q / (c1x6::KR * c1x6::KQ)) * SLOTB + (((q / c1x6::KQ) % c1x6::KR) * ROWE + 4 * (q % c1x6::KQ)) * 2;
-}
-constexpr int half_delta(int q) { return q + 1 < c1x6::NQ ? quad_off(q + 1) - quad_off(q) : 0; }
-static_assert(2 * SLOTB <= 80 * 1024, "two workgroups per CU");
-}  // namespace c1p
-
-template <int W>
-__global__ void __launch_bounds__(c1p::NT) __attribute__((amdgpu_waves_per_eu(3, 3)))
-k_conv1_pair_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img) {
-  using namespace c1x6;
-  using c1p::BN;
-  using c1p::NT;
-  constexpr int OW = (W - 11) / 4 + 1;
-  static_assert(4 * (OW - 1) + 4 * KQ <= c1p::ROWE, "slot rows too short");
-  __shared__ __attribute__((aligned(16))) char smem[2 * c1p::SLOTB];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave % 3, wn = wave / 3;
-  const int lr = lane & 31, lh = lane >> 5;
-  const int HWo = P.cv.howo.d, H = P.cv.H;
-  const float* const xin = P.b.p;
-  const int in_bytes = static_cast<int>(P.cv.in_bytes);
-
-  // XCD-aware tile order: each XCD walks a contiguous range of tiles, so the
-  // input rows two consecutive tiles of an image share are L2 hits
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, loc = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
-  const int t = __builtin_amdgcn_readfirstlane((xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc);
-  const int img = __builtin_amdgcn_readfirstlane(t / tiles_per_img);
-  const int sp0 = __builtin_amdgcn_readfirstlane((t - img * tiles_per_img) * BN);
-  const int f = __builtin_amdgcn_readfirstlane(sp0 / OW);
-
-  // ---- staging: chunk k of this thread = (slot row, 8 input columns); the
-  // last threads' extra chunks redo chunk CHUNKS - 1 (a benign duplicate) ----
-  float sv[c1p::CPT][8];
-  auto chunk_of = [&](int k) __attribute__((always_inline)) { return min((int)threadIdx.x + k * NT, c1p::CHUNKS - 1); };
-  auto stage_load = [&](int c, int k) __attribute__((always_inline)) {
-    const int q = chunk_of(k);
-    const int ri = q / c1p::QP, qp = q - ri * c1p::QP;
-    const bool ok = 4 * f + ri < H;
-    const int rowoff = (((img * 3 + c) * H + 4 * f + ri) * W + 8 * qp) * 4;
-    const uint32_t voff = ok ? static_cast<uint32_t>(rowoff) : 0x80000000u;
-    const __amdgpu_buffer_rsrc_t xrs =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xin), 0, in_bytes, 0x00020000);
-#pragma unroll
-    for (int e = 0; e < 8; ++e)
-      sv[k][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xrs, static_cast<int>(voff + 4 * e), 0, 0));
-  };
-  auto stage_store = [&](int c, int k) __attribute__((always_inline)) {
-    const int q = chunk_of(k);
-    const int ri = q / c1p::QP, qp = q - ri * c1p::QP;
-    // columns past the image row loaded the next row's (or, past the buffer,
-    // zero) values: zero them (kernel column 11's weights are zero, and an
-    // Inf there would make 0 * Inf = NaN)
-    const int nv = W - 8 * qp;
-    float v[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = e < nv ? sv[k][e] : 0.0f;
-    char* base = smem + c1p::slot_of(c) * c1p::SLOTB + (ri * c1p::ROWE + 8 * qp) * 2;
-    x6::Parts tp;
-    x6::split8_safe(v, tp);
-    *reinterpret_cast<x6::bf16x8*>(base) = tp.h;
-    *reinterpret_cast<x6::bf16x8*>(base + c1p::TERMB) = tp.m;
-    *reinterpret_cast<x6::bf16x8*>(base + 2 * c1p::TERMB) = tp.l;
-  };
-  auto lds_barrier = [&]() __attribute__((always_inline)) {
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done
-    __builtin_amdgcn_s_barrier();
-  };
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-#pragma unroll
-    for (int k = 0; k < c1p::CPT; ++k) stage_load(c, k);
-#pragma unroll
-    for (int k = 0; k < c1p::CPT; ++k) stage_store(c, k);
-  }
-#pragma unroll
-  for (int k = 0; k < c1p::CPT; ++k) stage_load(2, k);  // channel 2: stored after group last_group(0)
-
-  // weights: this wave's row block of fragment (g, wm), two groups ahead
-  const x6::bf16x8* ap = reinterpret_cast<const x6::bf16x8*>(wpack) + wm * 3 * 64 + lane;
-  auto load_a = [&](x6::bf16x8 (&fr)[3], int g) __attribute__((always_inline)) {
-#pragma unroll
-    for (int tt = 0; tt < 3; ++tt) fr[tt] = ap[(g * 9 + tt) * 64];
-  };
-  x6::bf16x8 fg[3][3];
-  load_a(fg[0], 0);
-  load_a(fg[1], 1);
-
-  // per-lane slot byte offsets (term 0, quad 0) of this wave's two 32-column blocks
-  uint32_t lb[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int sp = min(sp0 + wn * 64 + j * 32 + lr, HWo - 1);
-    const int oh = sp / OW, ow = sp - oh * OW;
-    lb[j] = static_cast<uint32_t>((4 * (oh - f) * c1p::ROWE + 4 * ow) * 2);
-  }
-  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  auto pick = [&](uint32_t h0, uint32_t h1) __attribute__((always_inline)) { return lh ? h1 : h0; };
-  auto mask_q = [&](u32x2 v, int q0) __attribute__((always_inline)) {
-    if (lo_mask(q0) != 0xFFFFFFFFu || lo_mask(q0 + 1) != 0xFFFFFFFFu) v[0] &= pick(lo_mask(q0), lo_mask(q0 + 1));
-    if (hi_mask(q0) != 0xFFFFFFFFu || hi_mask(q0 + 1) != 0xFFFFFFFFu) v[1] &= pick(hi_mask(q0), hi_mask(q0 + 1));
-    return v;
-  };
-  // B fragment term tt of column block j for group g: quads 4g + h and 4g + 2 + h
-  auto read_part = [&](x6::Parts (&F)[2], int g, int part) __attribute__((always_inline)) {
-    const int j = part / 3, tt = part % 3;
-    const int qa = 4 * g, qb = 4 * g + 2;
-    const char* ba = smem + lb[j] + (lh ? c1p::half_delta(qa) : 0) + tt * c1p::TERMB;
-    const char* bb = smem + lb[j] + (lh ? c1p::half_delta(qb) : 0) + tt * c1p::TERMB;
-    const u32x2 lo = mask_q(*reinterpret_cast<const u32x2*>(ba + c1p::quad_off(qa)), qa);
-    const u32x2 hi = mask_q(*reinterpret_cast<const u32x2*>(bb + c1p::quad_off(qb)), qb);
-    const x6::bf16x8 v = __builtin_bit_cast(x6::bf16x8, u32x4{lo[0], lo[1], hi[0], hi[1]});
-    if (tt == 0) F[j].h = v;
-    else if (tt == 1) F[j].m = v;
-    else F[j].l = v;
-  };
-  floatx16 acc[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
-  lds_barrier();  // channels 0 and 1 in their slots
-  x6::Parts F[2][2];
-#pragma unroll
-  for (int part = 0; part < 6; ++part) read_part(F[0], 0, part);
-  static_for<0, G>([&](auto gc) {
-    constexpr int g = decltype(gc)::value;
-    x6::Parts (&fc)[2] = F[g & 1];
-    x6::Parts (&fn)[2] = F[(g + 1) & 1];
-    if (g + 2 < G) load_a(fg[(g + 2) % 3], g + 2);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const auto& fa = fg[g % 3];
-      acc[j] = x6::mfma6(x6::Parts{fa[0], fa[1], fa[2]}, fc[j], acc[j]);
-      // the next group's B fragments under this block's MFMAs
-      if (g + 1 < G) {
-#pragma unroll
-        for (int part = 3 * j; part < 3 * j + 3; ++part) read_part(fn, g + 1, part);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (g == last_group(0)) {
-      // every wave is past channel 0 (its last B fragments were read during
-      // group g - 1 and consumed here): slot 0 takes channel 2
-      lds_barrier();
-#pragma unroll
-      for (int k = 0; k < c1p::CPT; ++k) stage_store(2, k);
-    }
-    // channel 2's stores visible before group first_group(2)'s B is read
-    // (during group first_group(2) - 1)
-    if (g == first_group(2) - 2) lds_barrier();
-  });
-  // epilogue: bias + ReLU (conv_epilogue_nchw's arithmetic), lanes past the
-  // image's last position store nothing
-  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(P.e.C, 0, 0x7FFFFFFF, 0x00020000);
-  const bool relu = P.e.relu != 0;
-  const int mw = 32 * wm + 4 * lh;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int sp = sp0 + wn * 64 + j * 32 + lr;
-    const uint32_t ob = sp < HWo ? static_cast<uint32_t>(((int64_t)img * P.e.cimg + sp + (int64_t)mw * HWo) * 4)
-                                 : 0x80000000u;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int dr = (r & 3) + 8 * (r >> 2);
-      const float b = P.e.bias != nullptr ? P.e.bias[mw + dr] : 0.0f;
-      const float o = acc[j][r] + b;
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, relu ? fmaxf(o, 0.0f) : o), ors,
-                                            static_cast<int>(ob), dr * HWo * 4, 0);
-    }
-  }
-}
-
 // Weight repack for k_conv1_ring_x6: w [M][3][11][11] -> fragments
 // [27 groups][3 row blocks][3 terms][64 lanes][8 bf16]; lane (lr, h) of
 // fragment (g, i): row 32 i + lr, items j of half h = quads 2 g, 2 g + 1 in
@@ -2017,6 +1809,9 @@ __global__ void __launch_bounds__(256) k_conv_patch_pack_x6(const float* __restr
 // partial slabs reduced by k_splitk_reduce.
 // K order inside a K-tile: group g, lane half h holds k = 16 h + 8 g + j
 // (the B rows' 16-byte quads 4h + 2g + u, u = 0, 1, swizzled as k_gemm2).
+#ifndef RRAM_FC_ABLATE
+#define RRAM_FC_ABLATE 0
+#endif
 namespace gx6 {
 constexpr int KT = 32;
 constexpr int RLB = 2 * 96 + 16;  // packed A row bytes per K-tile ([g][h][term][8 bf16] + pad, RLB/16 odd)
@@ -2186,10 +1981,13 @@ k_gemm_x6(Params P, const uint16_t* __restrict__ apack, int ktiles_all, int ktc)
 #pragma unroll
           for (int e = 0; e < NVM; ++e)
             if ((e * NB) / NVM == q) {
-              if (e < A_DMA)
-                issue_a(t + 1, e);
-              else if (more2)
-                issue_b(t + 2, e - A_DMA);
+              // RRAM_FC_ABLATE (diagnostic builds only, wrong results): 1 drops
+              // the A pieces, 2 the B pieces of the K-tile loop
+              if (e < A_DMA) {
+                if (RRAM_FC_ABLATE != 1) issue_a(t + 1, e);
+              } else if (more2) {
+                if (RRAM_FC_ABLATE != 2) issue_b(t + 2, e - A_DMA);
+              }
             }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -2314,8 +2112,8 @@ int conv_wide_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, co
     const int rc = launch_status("conv1 weight pack x6");
     if (rc) return rc;
   }
-#ifdef RRAM_C1_RING
-  // (A/B build) the persistent one-workgroup-per-CU ring kernel
+  // (a non-persistent form at two workgroups of six waves per CU, 96 x 128
+  // tiles, two channel slots: 0.462 vs 0.326 ms, profiles/r05_ab_c1_pair.txt)
   const int tpi = (HW + c1x6::BN - 1) / c1x6::BN;
   const int tiles = d->num * tpi;
   int cus = 256;
@@ -2323,14 +2121,7 @@ int conv_wide_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, co
   const unsigned nwg = static_cast<unsigned>(std::min(tiles, cus));
   hipLaunchKernelGGL((k_conv1_ring_x6<227>), dim3(nwg), dim3(256), 0, s, P, reinterpret_cast<const uint16_t*>(wp),
                      tpi, tiles);
-#else
-  const int tpi = (HW + c1p::BN - 1) / c1p::BN;
-  const int64_t tiles = (int64_t)d->num * tpi;
-  RRAM_REQUIRE(tiles < (1ll << 31), "conv1: grid too large");
-  hipLaunchKernelGGL((k_conv1_pair_x6<227>), dim3(static_cast<unsigned>(tiles)), dim3(c1p::NT), 0, s, P,
-                     reinterpret_cast<const uint16_t*>(wp), tpi);
-#endif
-  const int rc = launch_status("conv1 x6");
+  const int rc = launch_status("conv1 ring x6");
   return rc ? rc : 1;
 }
 
