@@ -4,7 +4,7 @@
 # bench command (+ the per-kernel traffic table), the other configs' lines.
 # Every GPU step has its own time limit; the chain stops at the first failure.
 set -o pipefail
-O=gpurun_out; mkdir -p $O
+O=${O:-gpurun_out}; mkdir -p $O
 R=$GRAFT_REPO_ROOT
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
 tail -3 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
@@ -13,8 +13,8 @@ tail -1 $O/smoke.log
 timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || exit $?
 cut -c1-300 $O/bench.json
 ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/$O/prof -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $R/$O/prof_bench.json 2> $R/$O/prof.err ) || exit $?
-timeout -k 10 900 ./scripts/pmc.sh gpurun_out/pmc > $O/pmc.log 2>&1 || { tail $O/pmc.log; exit 1; }
-python3 scripts/pmc_traffic.py gpurun_out/pmc > $O/pmc_traffic.json && python3 scripts/pmc_summary.py gpurun_out/pmc > $O/pmc_summary.txt
+timeout -k 10 900 ./scripts/pmc.sh $O/pmc > $O/pmc.log 2>&1 || { tail $O/pmc.log; exit 1; }
+python3 scripts/pmc_traffic.py $O/pmc > $O/pmc_traffic.json && python3 scripts/pmc_summary.py $O/pmc > $O/pmc_summary.txt
 for w in cifar10_quick_mc cifar10_full_train googlenet_sweep lenet_mc lenet_train; do
   timeout -k 10 400 python bench.py --workload $w --steps 10 --warmup 2 > $O/wl_$w.json 2> $O/wl_$w.err || { tail -5 $O/wl_$w.err; exit 1; }
 done

@@ -89,7 +89,7 @@ ALG = {  # class: (algorithmic bytes per step, description)
 }
 
 
-def classify(name):
+def classify(name, grid=0):
     if "k_inject_batched" in name:
         return "injection k_inject_batched"
     if "k_conv1_ring_x6" in name:
@@ -102,10 +102,12 @@ def classify(name):
         return "conv2 k_conv_cb_x6<5,5,...>"
     if "k_conv_cb_x6ILi3ELi3ELi4ELi8" in name:
         return "conv3 k_conv_cb_x6<3,3,4,8,...>"
-    if "k_conv_cb_x6ILi3ELi3ELi2ELi4" in name:
+    if "k_conv_cb_x6ILi3ELi3ELi2ELi" in name:
         return "conv4 k_conv_cb_x6<3,3,2,4,...>"
     if "k_conv_cb_x6ILi3ELi3ELi4ELi4" in name:
-        return "conv5 k_conv_cb_x6<3,3,4,4,...>"
+        # round 5: conv3 and conv5 both run the 128 x 128 16x16x32 form; conv3's
+        # grid is the larger (3 x 338 vs 2 x 338 workgroups)
+        return "conv3 k_conv_cb_x6<3,3,4,8,...>" if grid > 200000 else "conv5 k_conv_cb_x6<3,3,4,4,...>"
     if "k_pack_octets_x6" in name:
         return "conv4/conv5 input packs k_pack_octets_x6"
     if "k_gemm_x6" in name or "k_pack_rows_x6" in name:
@@ -129,7 +131,7 @@ for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
         name, c = r["Kernel_Name"], r["Counter_Name"]
         if c not in ("FETCH_SIZE", "WRITE_SIZE"):
             continue
-        k = classify(name)
+        k = classify(name, int(r.get("Grid_Size", 0) or 0))
         if k is None:
             lrn_grids.setdefault(int(r["Grid_Size"]), []).append((c, float(r["Counter_Value"])))
             continue
