@@ -15,6 +15,20 @@ namespace {
 // a^b for a > 0 via the native v_log_f32 / v_exp_f32 (powf's special-case
 // handling is not needed for LRN scales, which are >= k > 0)
 __device__ __forceinline__ float pow_pos(float a, float b) { return exp2f(b * log2f(a)); }
+// unsigned division by a runtime constant for in-plane indices (x < 2^31)
+struct FastDivI {
+  uint32_t d, m, s;
+};
+static FastDivI make_fastdivi(uint32_t d) {
+  FastDivI f{d, 0, 0};
+  if (d <= 1) return f;
+  uint32_t sh = 0;
+  while ((1ull << sh) < d) ++sh;
+  f.s = sh;
+  f.m = static_cast<uint32_t>(((1ull << 32) * ((1ull << sh) - d)) / d + 1);
+  return f;
+}
+__device__ __forceinline__ uint32_t fdivi(uint32_t x, const FastDivI& f) { return (__umulhi(x, f.m) + x) >> f.s; }
 
 // 32-bit index arithmetic (64-bit division is a long software sequence on
 // the VALU); every host wrapper checks that its element count is < 2^31.
@@ -402,6 +416,72 @@ __global__ void k_lrn_within_bwd(const float* __restrict__ x, const float* __res
     float g = dy[idx] * pow_pos(scale[idx], -beta) - 2.0f * alpha * beta * x[idx] * acc;
     if (relu) g = g * ((x[idx] > 0.0f) + (x[idx] <= 0.0f) * slope);
     dx[idx] = g;
+  }
+}
+
+// k_lrn_within_bwd with one plane per block (H * W <= kBwdPlaneMax): every
+// element's window term dy x scale^(-beta-1) / n is formed once into LDS (the
+// per-element kernel formed it once per window holding the element: 9x the
+// pow for local_size 3) and summed from there in the same (a, b) order, so
+// each dx is the same bits.
+constexpr int kBwdPlaneMax = 4096;
+__global__ void __launch_bounds__(256) k_lrn_within_bwd_plane(const float* __restrict__ x,
+                                                              const float* __restrict__ scale,
+                                                              const float* __restrict__ dy, float* __restrict__ dx,
+                                                              int H, int W, FastDivI wdiv, int size, float alpha,
+                                                              float beta, int relu, float slope) {
+  __shared__ float tl[kBwdPlaneMax];
+  const int HW = H * W, pre = (size - 1) / 2;
+  const int64_t base = (int64_t)blockIdx.x * HW;
+  for (int e = threadIdx.x; e < HW; e += blockDim.x) {
+    const int a = static_cast<int>(fdivi(static_cast<uint32_t>(e), wdiv)), b = e - a * W;
+    const float n = static_cast<float>(within_psize(a, pre, size, H) * within_psize(b, pre, size, W));
+    tl[e] = dy[base + e] * x[base + e] * pow_pos(scale[base + e], -beta - 1.0f) / n;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < HW; e += blockDim.x) {
+    const int h = static_cast<int>(fdivi(static_cast<uint32_t>(e), wdiv)), w = e - h * W;
+    const int ps = max(h + pre - size + 1, 0), pe = min(h + pre, H - 1);
+    const int qs = max(w + pre - size + 1, 0), qe = min(w + pre, W - 1);
+    float acc = 0.0f;
+    for (int a = ps; a <= pe; ++a)
+      for (int b = qs; b <= qe; ++b) acc += tl[a * W + b];
+    const int64_t idx = base + e;
+    float g = dy[idx] * pow_pos(scale[idx], -beta) - 2.0f * alpha * beta * x[idx] * acc;
+    if (relu) g = g * ((x[idx] > 0.0f) + (x[idx] <= 0.0f) * slope);
+    dx[idx] = g;
+  }
+}
+
+// k_pool_bwd (MAX, mask) with one plane per block (H * W <= kBwdPlaneMax,
+// PH * PW <= 1024): the pooled gradients and argmax indices of the plane in
+// LDS, each input element gathering from them in k_pool_bwd's (a, b) order
+// (same bits), with no 64-bit index arithmetic
+__global__ void __launch_bounds__(256) k_pool_bwd_plane(const float* __restrict__ dy, const int* __restrict__ mask,
+                                                        float* __restrict__ dx, int H, int W, int PH, int PW,
+                                                        FastDivI wdiv, int kh, int kw, int sh, int sw, int ph,
+                                                        int pw, const float* __restrict__ ry, float slope) {
+  __shared__ float dl[1024];
+  __shared__ int ml[1024];
+  const int HW = H * W, PHW = PH * PW;
+  const int64_t pb = (int64_t)blockIdx.x * PHW, xb = (int64_t)blockIdx.x * HW;
+  for (int e = threadIdx.x; e < PHW; e += blockDim.x) {
+    dl[e] = dy[pb + e];
+    ml[e] = mask[pb + e];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < HW; e += blockDim.x) {
+    const int h = static_cast<int>(fdivi(static_cast<uint32_t>(e), wdiv)), w = e - h * W;
+    const int phs = (h + ph < kh) ? 0 : (h + ph - kh) / sh + 1;
+    const int phe = min((h + ph) / sh + 1, PH);
+    const int pws = (w + pw < kw) ? 0 : (w + pw - kw) / sw + 1;
+    const int pwe = min((w + pw) / sw + 1, PW);
+    float g = 0.0f;
+    for (int a = phs; a < phe; ++a)
+      for (int b = pws; b < pwe; ++b)
+        if (ml[a * PW + b] == e) g += dl[a * PW + b];
+    if (ry != nullptr) g = g * ((ry[xb + e] > 0.0f) + (ry[xb + e] <= 0.0f) * slope);
+    dx[xb + e] = g;
   }
 }
 
@@ -919,6 +999,11 @@ int rram_pool_relu_bwd(const float* dy, const int* mask, float* dx, int num, int
   RRAM_REQUIRE_I32(total, "layer kernel");
   if (total == 0) return RRAM_OK;
   RRAM_REQUIRE(dy && dx, "pool_bwd: NULL");
+  if (method == RRAM_POOL_MAX && H * W <= kBwdPlaneMax && PH * PW <= 1024 && (int64_t)num * C < (1ll << 31)) {
+    hipLaunchKernelGGL(k_pool_bwd_plane, dim3(static_cast<unsigned>(num * C)), dim3(256), 0, as_stream(s), dy, mask,
+                       dx, H, W, PH, PW, make_fastdivi(W), kh, kw, sh, sw, ph, pw, relu_y, relu_slope);
+    return launch_status("pool_bwd");
+  }
   hipLaunchKernelGGL(k_pool_bwd, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), dy,
                      mask, dx, num, C, H, W, PH, PW, kh, kw, sh, sw, ph, pw, method, relu_y, relu_slope);
   return launch_status("pool_bwd");
@@ -987,6 +1072,11 @@ int rram_lrn_within_relu_bwd_core(const float* x, const float* scale, const floa
   RRAM_REQUIRE_I32(total, "layer kernel");
   if (total == 0) return RRAM_OK;
   RRAM_REQUIRE(x && scale && dy && dx, "lrn_within_bwd: NULL");
+  if (H * W <= kBwdPlaneMax && (int64_t)num * C < (1ll << 31)) {
+    hipLaunchKernelGGL(k_lrn_within_bwd_plane, dim3(static_cast<unsigned>(num * C)), dim3(256), 0, as_stream(s), x,
+                       scale, dy, dx, H, W, make_fastdivi(W), size, alpha, beta, relu, slope);
+    return launch_status("lrn_within_bwd");
+  }
   hipLaunchKernelGGL(k_lrn_within_bwd, dim3(stream_blocks(total)), dim3(kThreads), 0, as_stream(s), x, scale,
                      dy, dx, (int64_t)num * C, H, W, size, alpha, beta, relu, slope);
   return launch_status("lrn_within_bwd");

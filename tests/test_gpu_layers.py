@@ -584,3 +584,46 @@ def test_folded_blobs_materialise_when_read(device):
             assert torch.equal(got[True][0][n], got[False][0][n]), (name, n)
         for n in folded + outs:
             assert torch.equal(got[True][1][n], got[False][1][n]), (name, n)
+
+
+@pytest.mark.parametrize("shape,k,s,p", [((2, 5, 13, 11), 3, 2, 0), ((3, 4, 32, 32), 3, 2, 0), ((2, 3, 16, 16), 3, 2, 1),
+                                         ((1, 2, 64, 64), 2, 2, 0), ((1, 1, 70, 70), 3, 2, 0)])
+def test_max_pool_bwd_bit_exact(device, shape, k, s, p):
+    """MAX pooling backward (pooling_layer.cu:145-167: each input element
+    sums, in (a, b) row-major order, the gradients of the pooled outputs whose
+    argmax it is) bit for bit against a float32 numpy restatement, on the
+    plane-per-block kernel (H * W <= 4096) and the per-element one (70 x 70)."""
+    import torch
+    from rramsim import ops
+    torch.manual_seed(21)
+    N, C, H, W = shape
+    PH = -(-(H + 2 * p - k) // s) + 1
+    PW = -(-(W + 2 * p - k) // s) + 1
+    if p > 0:
+        PH -= (PH - 1) * s >= H + p
+        PW -= (PW - 1) * s >= W + p
+    x = torch.randn(shape, device=device)
+    geom = (N, C, H, W, PH, PW, k, k, s, s, p, p)
+    y = torch.empty((N, C, PH, PW), device=device)
+    mask = torch.empty((N, C, PH, PW), dtype=torch.int32, device=device)
+    ops.pool_fwd(x, y, mask, geom, 0)
+    dy = torch.randn_like(y)
+    dx = torch.empty_like(x)
+    ops.pool_bwd(dy, mask, dx, geom, 0)
+    m, g = mask.cpu().numpy(), dy.cpu().numpy()
+    ref = np.zeros(shape, np.float32)
+    for n in range(N):
+        for c in range(C):
+            for h in range(H):
+                for w in range(W):
+                    phs = 0 if h + p < k else (h + p - k) // s + 1
+                    phe = min((h + p) // s + 1, PH)
+                    pws = 0 if w + p < k else (w + p - k) // s + 1
+                    pwe = min((w + p) // s + 1, PW)
+                    acc = np.float32(0)
+                    for a in range(phs, phe):
+                        for b in range(pws, pwe):
+                            if m[n, c, a, b] == h * W + w:
+                                acc = np.float32(acc + g[n, c, a, b])
+                    ref[n, c, h, w] = acc
+    assert np.array_equal(dx.cpu().numpy().view(np.uint32), ref.view(np.uint32))
