@@ -42,11 +42,11 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: bf16 dense MFMA (no spars
 # fp32 product: its roofline is the bf16 dense peak / 6 in fp32 FLOPs
 MFMA_X6_PEAK_TFLOPS = MFMA_BF16_PEAK_TFLOPS / 6.0
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
-# the dominant kernel of the step: conv2's k_conv_cb_x6<5,5,...> (22 % of GPU
+# the dominant kernel of the step: conv2's k_conv_cb16_x6<5,5,...> (22 % of GPU
 # time, profiles/r03_*_kernel_stats.csv); the only layer timed inside the
 # timed region, so the stream carries two markers per map for it
 DOMINANT_LAYER = "conv2"
-DOMINANT_PMC_CLASS = "conv2 k_conv_cb_x6<5,5,...>"
+DOMINANT_PMC_CLASS = "conv2 k_conv_cb16_x6<5,5,...>"
 
 
 def alexnet_gemm_table(batch):

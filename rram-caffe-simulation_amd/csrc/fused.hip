@@ -21,8 +21,8 @@ namespace {
 // band per block, walking all channels, left AlexNet's norm2 at 512 blocks,
 // latency-bound).  Per channel, every thread produces the LRN value of up to
 // PPT input pixels of the band (the band's input rows are contiguous in
-// memory, so the loads are coalesced), from a register ring of the SIZE
-// channels around it: scale = k + alpha/size * sum of the SIZE squares in
+// memory, so the loads are coalesced), from a register ring of 16 channels
+// (the SIZE around it and the loads of the next NS groups in flight): scale = k + alpha/size * sum of the SIZE squares in
 // channel order (lrn_sq_add, the unfused k_lrn_fwd_slide's sum, so each LRN
 // value x * scale^-beta (lrn_layer.cu:72-78) is the unfused kernel's bit for
 // bit, whatever chunk it falls in).  A chunk reads its PRE / POST halo
@@ -35,7 +35,19 @@ namespace {
 // and the chunk halos), y written once; the LRN output never leaves the CU.
 constexpr int kBandPix = 512;  // input pixels per band (PPT = 2 per thread)
 // target grid of the LRN + pool band kernel: several block waves of 256 CUs
-constexpr int kLrnBlocks = 4096;
+#ifndef RRAM_LRN_BLOCKS
+#define RRAM_LRN_BLOCKS 4096
+#endif
+#ifndef RRAM_LRN_ALT
+#define RRAM_LRN_ALT 0
+#endif
+#ifndef RRAM_LRN_DIAG
+#define RRAM_LRN_DIAG 0
+#endif
+#ifndef RRAM_LRN_XCD
+#define RRAM_LRN_XCD 1
+#endif
+constexpr int kLrnBlocks = RRAM_LRN_BLOCKS;
 constexpr int kLrnG = 2;
 
 // G channels per barrier (kLrnG = 2: measured on MI355X for both AlexNet
@@ -54,18 +66,23 @@ constexpr int kLrnG = 2;
 // plain row had consecutive lanes two words apart (2-way LDS bank conflicts
 // on every tap: 46-48 % of the LDS-active cycles in round 3).  WT = 0: any W,
 // plain rows.
+// CCT > 0: every chunk is exactly CCT channels (host check; AlexNet b256:
+// 32-channel chunks of both planes): the channel walk is straight-line code
+// (round 5: 84.7 / 112 us per launch with the looped walk, whose back edge
+// made the compiler drain every load in flight at each trip top).
 __device__ __forceinline__ float max3f(float a, float b, float c) {
   float r;
   asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
 
-template <int K, int SIZE, int G, bool OCT, int WT = 0>
+template <int K, int SIZE, int G, bool OCT, int WT = 0, int CCT = 0>
 __global__ void __launch_bounds__(256)
     k_lrn_maxpool_band(const float* __restrict__ x, float* __restrict__ y, char* __restrict__ yo, int C, int H, int W,
                        int PH, int PW, int sh, int sw, int ph, int pw, int RB, int CC, int bands, int chunks,
                        float alpha_over_size, float beta, float k) {
   static_assert(!OCT || (8 % (2 * G) == 0), "the octet walk needs G in {2, 4}");
+  static_assert(CCT % 16 == 0, "straight-line walks cover whole ring trips");
   static_assert(kBandPix == 2 * 256, "two pixels per thread: the packed LRN pair");
   constexpr int PRE = (SIZE - 1) / 2;
   constexpr int D = G;
@@ -91,7 +108,7 @@ __global__ void __launch_bounds__(256)
   const int total = bands * chunks * static_cast<int>(gridDim.y);  // gridDim.y = images
   const int L = blockIdx.x + static_cast<int>(gridDim.x) * blockIdx.y;
   const int xq = total / 8, xr = total % 8, xcd = L % 8, xk = L / 8;
-  const int tile = xcd < xr ? xcd * (xq + 1) + xk : xr * (xq + 1) + (xcd - xr) * xq + xk;
+  const int tile = !RRAM_LRN_XCD ? L : xcd < xr ? xcd * (xq + 1) + xk : xr * (xq + 1) + (xcd - xr) * xq + xk;
   const int band = tile % bands, rest = tile / bands;
   const int n = rest / chunks;
   const int cb = (rest - n * chunks) * CC;
@@ -131,22 +148,23 @@ __global__ void __launch_bounds__(256)
     return f32x2{__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xrs, static_cast<int>(vo0 + co), 0, 0)),
                  __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xrs, static_cast<int>(vo1 + co), 0, 0))};
   };
-  // win[j] = both pixels at channel (c0 - PRE + j), zero outside [0, C).
-  // NS staging arrays rotate by group (st[g % NS], so the registers are named
-  // statically): the entering channels of group g + NS are loaded at the top
-  // of group g and moved into the ring at the bottom of group g + NS - 1, so
-  // NS groups of loads (NS * D channels) stay in flight across the LDS / pool
-  // work.  With octets NS = 8 / D (the octet's groups, 8 channels ahead),
-  // else 2.
-  constexpr int NS = OCT ? 8 / D : 2;
-  f32x2 win[SIZE + D];
-  f32x2 st[NS][D];
-#pragma unroll
-  for (int j = 0; j < SIZE + D; ++j) win[j] = ld(cb + j - PRE);
-#pragma unroll
-  for (int j = 1; j < NS; ++j)  // the entering channels of groups 1 .. NS - 1
-#pragma unroll
-    for (int d = 0; d < D; ++d) st[j][d] = ld(cb - PRE + SIZE + j * D + d);
+  // The channel walk keeps both pixels of a ring of RL = 16 consecutive
+  // channels in registers: ring[r & 15] holds the channel at walk position r
+  // (UP: channel base + r, base = cb - PRE; DN: channel base - r, base = the
+  // top group's window end), so the walk, unrolled over 16 channels (8 groups
+  // of D = 2) per loop trip, names every register statically with no copy at
+  // the loop latch.  (Round 4's window + staging arrays rotated by copies:
+  // the compiler moved the freshly loaded staging registers at the latch,
+  // behind a vmcnt(0), which drained every load in flight once per octet.)
+  // Group g's window is positions 2 g .. 2 g + SIZE + D - 1; it loads the
+  // positions its NS-th successor enters with, 2 g + SIZE + NS D + {0 .. D-1},
+  // so NS groups of loads stay in flight across the LDS / pool work.
+  constexpr int RL = 16;
+  constexpr int NS = (RL - SIZE - D) / D;  // 4 (SIZE 5) / 5 (SIZE 3) groups ahead
+  // the live positions at a group (its window up to the entering channels of
+  // its NS-th successor, loaded before the window is read) span SIZE + NS D + D
+  static_assert(SIZE + NS * D + D <= RL && D == 2, "ring span");
+  f32x2 ring[RL];
   const int NO = (pr1 - pr0) * PW;  // pooled outputs of the band per channel
   const int PHW = PH * PW;
   // y of image n through a buffer resource too (one image < 2 GiB: host check)
@@ -181,26 +199,41 @@ __global__ void __launch_bounds__(256)
     it_vo[i] = (d * PHW + it_out[i]) * 4;
     it_ok[i] = ok;
   }
-  // one channel group: c0 = its first channel, yb = its LDS plane buffer,
-  // gi = its place in the staging rotation (g % NS)
-  auto group = [&](int c0, float (*yb)[YBS], auto gi) {
-    constexpr int GI = decltype(gi)::value;
-    f32x2(&load_into)[D] = st[GI];
-    const f32x2(&fill_from)[D] = st[(GI + 1) % NS];
+  // one channel group: c0 = its first channel, g = its place in the loop trip
+  // (static: ring slots and LDS plane buffer g & 1), DN = the walk's direction
+  auto group = [&](int c0, auto gi, auto dn) {
+    constexpr int GG = decltype(gi)::value;
+    constexpr bool DN = decltype(dn)::value;
+    // entering channels of group g + NS: positions 2 g + SIZE + NS D + d
 #pragma unroll
-    for (int d = 0; d < D; ++d) load_into[d] = ld(c0 - PRE + SIZE + NS * D + d);
+    for (int d = 0; d < D; ++d) {
+      constexpr int P0 = 2 * GG + SIZE + NS * D;
+      ring[(P0 + d) & (RL - 1)] = ld(DN ? c0 - PRE + D - 1 - NS * D - d : c0 - PRE + SIZE + NS * D + d);
+    }
+    // the window in channel order: w[j] = channel c0 - PRE + j (UP: position
+    // 2 g + j; DN: position 2 g + SIZE + D - 1 - j)
+    f32x2 w[SIZE + D];
+#pragma unroll
+    for (int j = 0; j < SIZE + D; ++j) w[j] = ring[(DN ? 2 * GG + SIZE + D - 1 - j : 2 * GG + j) & (RL - 1)];
+    float(*yb)[YBS] = ybuf[GG & 1];
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       // lrn_sq_add / lrn_scale / lrn_out (the unfused kernels' arithmetic) on
       // both pixels at once
-      const f32x2 v = lrn_value2<SIZE>(win + d, alpha_over_size, beta, k);
+#if RRAM_LRN_DIAG == 1  // diagnostic builds only: no LRN arithmetic
+      const f32x2 v = w[d + PRE];
+#else
+      const f32x2 v = lrn_value2<SIZE>(w + d, alpha_over_size, beta, k);
+#endif
       if (own0) yb[d][sl0] = v.x;
       if (own1) yb[d][sl1] = v.y;
     }
+#if RRAM_LRN_DIAG != 3  // diagnostic builds only: no barrier (garbage values)
     __syncthreads();
+#endif
     // pool the group's D channels (MaxPoolForward: -FLT_MAX start, strict ">"
     // in row-major window order over the taps inside the image)
-    const int nd = min(D, ce - c0);
+    const int nd = RRAM_LRN_DIAG == 2 ? 0 : min(D, ce - c0);  // DIAG 2: no pooling
 #pragma unroll
     for (int i = 0; i < MAXI; ++i) {
       const int d = it_d[i];
@@ -240,29 +273,10 @@ __global__ void __launch_bounds__(256)
         if (OCT) obuf[(c0 + d) & 7][it_out[i] - pr0 * PW] = mv;
       }
     }
-#pragma unroll
-    for (int j = 0; j < SIZE; ++j) win[j] = win[j + D];
-#pragma unroll
-    for (int d = 0; d < D; ++d) win[SIZE + d] = fill_from[d];
   };
-  using G0 = std::integral_constant<int, 0>;
-  using G1 = std::integral_constant<int, 1>;
-  if (!OCT) {
-    for (int c0 = cb; c0 < ce; c0 += 2 * D) {
-      group(c0, ybuf[0], G0{});
-      if (c0 + D < ce) group(c0 + D, ybuf[1], G1{});
-    }
-    return;
-  }
-  // OCT: 8 channels per step (an even number of groups), then the octet
-  char* yon = yo + (int64_t)n * (C / 8) * PHW * 48;
-  for (int c0 = cb; c0 < ce; c0 += 8) {
-    group(c0, ybuf[0], G0{});
-    group(c0 + D, ybuf[1], G1{});
-    if constexpr (NS == 4) {  // D == 2 with octets
-      group(c0 + 4, ybuf[0], std::integral_constant<int, 2>{});
-      group(c0 + 6, ybuf[1], std::integral_constant<int, 3>{});
-    }
+  // OCT: after each 8 channels (4 groups) the octet's companion
+  char* yon = OCT ? yo + (int64_t)n * (C / 8) * PHW * 48 : nullptr;
+  auto octet_out = [&](int c8) {
     __syncthreads();  // obuf complete (the next group's barrier orders its rewrite)
     const int o = threadIdx.x;
     if (o < NO) {
@@ -271,9 +285,68 @@ __global__ void __launch_bounds__(256)
       for (int e = 0; e < 8; ++e) v[e] = obuf[e][o];
       const int prl = o / PW;
       const int64_t out = (int64_t)(pr0 + prl) * PW + (o - prl * PW);
-      x6::store_terms8(v, yon + ((int64_t)(c0 / 8) * PHW + out) * 48);
+      x6::store_terms8(v, yon + ((int64_t)(c8 / 8) * PHW + out) * 48);
     }
-  }
+  };
+  // the walk: prime the window of group 0 and the entering channels of groups
+  // 1 .. NS - 1 (positions 0 .. SIZE + NS D - 1), then 16 channels per trip
+  auto walk = [&](auto dn) {
+    constexpr bool DN = decltype(dn)::value;
+    // UP: groups at cb, cb + 2, ...; DN: at top, top - 2, ... (top = the
+    // highest group start; octets: ce - 2)
+    const int top = OCT ? ce - D : cb + (ce - cb - 1) / D * D;
+    const int first = DN ? top : cb;
+    const int base = DN ? top - PRE + SIZE + D - 1 : cb - PRE;
+#pragma unroll
+    for (int r = 0; r < SIZE + NS * D; ++r) ring[r] = ld(DN ? base - r : base + r);
+    if constexpr (CCT > 0) {
+      // a chunk of exactly CCT channels (host check): the whole walk straight
+      // line, no loop and no per-group branch, so the compiler's wait counts
+      // stay exact (each group waits only for its own window's loads, NS
+      // groups old; the loop form's back edge made it drain every load in
+      // flight at the trip top and behind each group's loads)
+      auto step = [&](auto gi) {
+        constexpr int GG = decltype(gi)::value;
+        const int cg = DN ? first - GG * D : first + GG * D;
+        group(cg, gi, dn);
+        if constexpr (OCT && (GG & 3) == 3) octet_out(DN ? cg : cg - 6);
+      };
+      [&]<int... I>(std::integer_sequence<int, I...>) {
+        (step(std::integral_constant<int, I>{}), ...);
+      }(std::make_integer_sequence<int, CCT / D>{});
+      return;
+    }
+    for (int t0 = 0;; t0 += RL) {
+      const int c0 = DN ? first - t0 : first + t0;  // group 0 of the trip
+      auto live = [&](int c) { return DN ? c >= cb : c < ce; };
+      if (!live(c0)) break;
+      auto step = [&](auto gi) {
+        constexpr int GG = decltype(gi)::value;
+        const int cg = DN ? c0 - GG * D : c0 + GG * D;
+        if (live(cg)) {
+          group(cg, gi, dn);
+          // the octet ends with the group at its top (UP) / bottom (DN)
+          if constexpr (OCT && (GG & 3) == 3) octet_out(DN ? cg : cg - 6);
+        }
+      };
+      step(std::integral_constant<int, 0>{});
+      step(std::integral_constant<int, 1>{});
+      step(std::integral_constant<int, 2>{});
+      step(std::integral_constant<int, 3>{});
+      step(std::integral_constant<int, 4>{});
+      step(std::integral_constant<int, 5>{});
+      step(std::integral_constant<int, 6>{});
+      step(std::integral_constant<int, 7>{});
+    }
+  };
+  // Odd channel chunks walk down (RRAM_LRN_ALT): chunk i's last halo channels
+  // and chunk i + 1's first ones are then the same channels read at the same
+  // time (both at the chunks' shared boundary, start or end of the walk), so
+  // the second read can merge in the XCD's L2 instead of going to memory
+  if (RRAM_LRN_ALT && (((rest - n * chunks) & 1) != 0))
+    walk(std::true_type{});
+  else
+    walk(std::false_type{});
 }
 
 }  // namespace
@@ -332,13 +405,23 @@ int rram_lrn_maxpool_fwd_octets(const float* x, float* y, void* y_oct, int num, 
   const dim3 grid(static_cast<unsigned>(bands * nchunks), static_cast<unsigned>(num));
   const float aos = alpha / size;
   char* yo = static_cast<char*>(y_oct);
-#define RRAM_LP3(K_, S_, WT_)                                                                                      \
-  if (yo)                                                                                                          \
-    hipLaunchKernelGGL((k_lrn_maxpool_band<K_, S_, kLrnG, true, WT_>), grid, dim3(kThreads), 0, as_stream(s), x, y, \
-                       yo, C, H, W, PH, PW, sh, sw, ph, pw, rb, cc, bands, nchunks, aos, beta, k);                 \
-  else                                                                                                             \
-    hipLaunchKernelGGL((k_lrn_maxpool_band<K_, S_, kLrnG, false, WT_>), grid, dim3(kThreads), 0, as_stream(s), x,  \
-                       y, yo, C, H, W, PH, PW, sh, sw, ph, pw, rb, cc, bands, nchunks, aos, beta, k);
+#define RRAM_LP4(K_, S_, WT_, CCT_)                                                                             \
+  if (yo)                                                                                                       \
+    hipLaunchKernelGGL((k_lrn_maxpool_band<K_, S_, kLrnG, true, WT_, CCT_>), grid, dim3(kThreads), 0,          \
+                       as_stream(s), x, y, yo, C, H, W, PH, PW, sh, sw, ph, pw, rb, cc, bands, nchunks, aos, beta, \
+                       k);                                                                                      \
+  else                                                                                                          \
+    hipLaunchKernelGGL((k_lrn_maxpool_band<K_, S_, kLrnG, false, WT_, CCT_>), grid, dim3(kThreads), 0,         \
+                       as_stream(s), x, y, yo, C, H, W, PH, PW, sh, sw, ph, pw, rb, cc, bands, nchunks, aos, beta, \
+                       k);
+  // AlexNet's planes (WT > 0) in whole 32-channel chunks take the
+  // straight-line walk
+#define RRAM_LP3(K_, S_, WT_)                          \
+  if (WT_ > 0 && cc == 32 && C % 32 == 0) {            \
+    RRAM_LP4(K_, S_, WT_, (WT_ > 0 ? 32 : 0))          \
+  } else {                                             \
+    RRAM_LP4(K_, S_, WT_, 0)                           \
+  }
   // the WT plane rows are de-interleaved by a window stride of 2 and paired
   // two rows per pitch (a pooled row = two input rows down, from an even row)
   const bool wt_ok = sw == 2 && pw == 0 && sh == 2 && ph == 0;
@@ -356,6 +439,7 @@ int rram_lrn_maxpool_fwd_octets(const float* x, float* y, void* y_oct, int num, 
   else RRAM_LP(3, 3) else RRAM_LP(2, 5) else RRAM_LP(2, 3)
 #undef RRAM_LP
 #undef RRAM_LP3
+#undef RRAM_LP4
   return launch_status("lrn_maxpool_fwd");
 }
 

@@ -692,9 +692,30 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
   const int xcd = bid & 7, loc = bid >> 3;
   const int q8 = nwg >> 3, r8 = nwg & 7;
   const int tid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
-  const int tm = __builtin_amdgcn_readfirstlane(tid % P.tiles_m);
-  const int tn = __builtin_amdgcn_readfirstlane((tid / P.tiles_m) % P.tiles_n);
+#ifndef RRAM_CB16_BAND
+#define RRAM_CB16_BAND 0
+#endif
+  // RRAM_CB16_BAND = B > 0 (A/B builds): the row tiles walked in bands of B
+  // column tiles, row-tile major inside a band (one row block's weights live
+  // in L2 at a time); 0: row tiles fastest (the row tiles of a column share
+  // its patch)
+  int tm_, tn_;
   const int z = __builtin_amdgcn_readfirstlane(tid / (P.tiles_m * P.tiles_n));
+  {
+    const int r = tid - z * P.tiles_m * P.tiles_n;
+    if (RRAM_CB16_BAND > 0 && P.tiles_m > 1) {
+      const int band = r / (P.tiles_m * RRAM_CB16_BAND);
+      const int rb = r - band * P.tiles_m * RRAM_CB16_BAND;
+      const int w = min(RRAM_CB16_BAND, P.tiles_n - band * RRAM_CB16_BAND);
+      tm_ = rb / w;
+      tn_ = band * RRAM_CB16_BAND + (rb - tm_ * w);
+    } else {
+      tm_ = r % P.tiles_m;
+      tn_ = r / P.tiles_m;
+    }
+  }
+  const int tm = __builtin_amdgcn_readfirstlane(tm_);
+  const int tn = __builtin_amdgcn_readfirstlane(tn_);
   const int m0 = tm * BMc;
 
   const ConvGeom& cv = P.cv;
@@ -818,10 +839,16 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
           f[i][t] = __builtin_bit_cast(
               x6::bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ar, alane, (q * MI + i) * cb16::FRAG * 16 + t * 1024, 0));
     };
-    constexpr int PMAX = (PD + H - 2) / (H - 1);  // patch pieces per group (the shortest K-tile spreads them over H - 1 groups)
+#ifndef RRAM_CB16_SD
+#define RRAM_CB16_SD 1
+#endif
+    // staging distance (groups): the next K-tile's patch pieces are loaded at
+    // group g and stored to the next stage at g + SD
+    constexpr int SD = H >= 2 + RRAM_CB16_SD ? RRAM_CB16_SD : 1;
+    constexpr int PMAX = (PD + H - SD - 1) / (H - SD);  // patch pieces per group (the shortest K-tile spreads them over H - SD groups)
     static_assert(H >= 2, "pair groups");
     typedef int int4x __attribute__((ext_vector_type(4)));
-    int4x stg[2][PMAX];
+    int4x stg[SD + 1][PMAX];
 #pragma unroll
     for (int i = 0; i < PD; ++i) issue(0, 0, i);
     load_a(fa[0], 0);
@@ -848,14 +875,15 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
         constexpr int NS0 = ODD ? 2 * gi : 2 * (gi + 1);
         const int q = q0 + gi;
         if (MORE) {
-          if (gi > 0) {
+          if (gi >= SD) {
+            constexpr int g0 = gi - SD;
 #pragma unroll
-            for (int i = cbx6::piece_lo(gi - 1, PD, NG); i < cbx6::piece_lo(gi, PD, NG); ++i)
-              *reinterpret_cast<int4x*>(nst + i * 1024) = stg[(gi - 1) & 1][i - cbx6::piece_lo(gi - 1, PD, NG)];
+            for (int i = cbx6::piece_lo_d(g0, PD, NG, SD); i < cbx6::piece_lo_d(g0 + 1, PD, NG, SD); ++i)
+              *reinterpret_cast<int4x*>(nst + i * 1024) = stg[g0 % (SD + 1)][i - cbx6::piece_lo_d(g0, PD, NG, SD)];
           }
 #pragma unroll
-          for (int i = cbx6::piece_lo(gi, PD, NG); i < cbx6::piece_lo(gi + 1, PD, NG); ++i)
-            stg[gi & 1][i - cbx6::piece_lo(gi, PD, NG)] = __builtin_bit_cast(
+          for (int i = cbx6::piece_lo_d(gi, PD, NG, SD); i < cbx6::piece_lo_d(gi + 1, PD, NG, SD); ++i)
+            stg[gi % (SD + 1)][i - cbx6::piece_lo_d(gi, PD, NG, SD)] = __builtin_bit_cast(
                 int4x, __builtin_amdgcn_raw_buffer_load_b128(
                            xr, static_cast<int>(poff(i) + static_cast<uint32_t>(kt + 1) * 2u * PL), 0, 0));
         }

@@ -75,12 +75,12 @@ Y5 = 256*13*13*B*4
 ALG = {  # class: (algorithmic bytes per step, description)
     "conv1 k_conv1_ring_x6": (A1 + 96*363*4 + Y1, "x fp32 + w + y"),
     "norm1+pool1 (LRN + max pool, octets)": (Y1 + P1Y + P1O, "x + y + y octets"),
-    "conv2 k_conv_cb_x6<5,5,...>": (P1O + 256*48*25*4 + Y2, "x octets + w + y"),
+    "conv2 k_conv_cb16_x6<5,5,...>": (P1O + 256*48*25*4 + Y2, "x octets + w + y"),
     "norm2+pool2 (LRN + max pool, octets)": (Y2 + P2Y + P2O, "x + y + y octets"),
-    "conv3 k_conv_cb_x6<3,3,4,8,...>": (P2O + 384*256*9*4 + Y3, "x octets + w + y"),
+    "conv3 k_conv_cb16_x6<3,3,4,4,...>": (P2O + 384*256*9*4 + Y3, "x octets + w + y"),
     "conv4/conv5 input packs k_pack_octets_x6": (2 * (Y3 + O4), "2 x (read fp32, write octets)"),
-    "conv4 k_conv_cb_x6<3,3,2,4,...>": (O4 + 384*192*9*4 + Y4, "x octets + w + y"),
-    "conv5 k_conv_cb_x6<3,3,4,4,...>": (O4 + 256*192*9*4 + Y5, "x octets + w + y"),
+    "conv4 k_conv_cb16_x6<3,3,2,2,...>": (O4 + 384*192*9*4 + Y4, "x octets + w + y"),
+    "conv5 k_conv_cb16_x6<3,3,4,4,...>": (O4 + 256*192*9*4 + Y5, "x octets + w + y"),
     "fc6/fc7 k_gemm_x6 + k_pack_rows_x6": ((9216 + 4096)*B*(4 + 6 + 6) + (4096*9216 + 4096*4096)*4 + 2*4096*B*4,
                                             "x read + slabs written/read, w, y"),
     "fc8 k_gemm2": (4096*B*4 + 1000*4096*4 + 1000*B*4, "x + w + y"),
@@ -99,15 +99,15 @@ def classify(name, grid=0):
     # (k_conv_cb16_x6: the 16x16x32 form of the same kernel, round 4)
     name = name.replace("k_conv_cb16_x6", "k_conv_cb_x6")
     if "k_conv_cb_x6ILi5ELi5" in name or "k_conv_cb_x6<5, 5" in name:
-        return "conv2 k_conv_cb_x6<5,5,...>"
+        return "conv2 k_conv_cb16_x6<5,5,...>"
     if "k_conv_cb_x6ILi3ELi3ELi4ELi8" in name:
-        return "conv3 k_conv_cb_x6<3,3,4,8,...>"
+        return "conv3 k_conv_cb16_x6<3,3,4,4,...>"
     if "k_conv_cb_x6ILi3ELi3ELi2ELi" in name:
-        return "conv4 k_conv_cb_x6<3,3,2,4,...>"
+        return "conv4 k_conv_cb16_x6<3,3,2,2,...>"
     if "k_conv_cb_x6ILi3ELi3ELi4ELi4" in name:
         # round 5: conv3 and conv5 both run the 128 x 128 16x16x32 form; conv3's
         # grid is the larger (3 x 338 vs 2 x 338 workgroups)
-        return "conv3 k_conv_cb_x6<3,3,4,8,...>" if grid > 200000 else "conv5 k_conv_cb_x6<3,3,4,4,...>"
+        return "conv3 k_conv_cb16_x6<3,3,4,4,...>" if grid > 200000 else "conv5 k_conv_cb16_x6<3,3,4,4,...>"
     if "k_pack_octets_x6" in name:
         return "conv4/conv5 input packs k_pack_octets_x6"
     if "k_gemm_x6" in name or "k_pack_rows_x6" in name:
@@ -144,8 +144,8 @@ for i, (gsz, vals) in enumerate(sorted(lrn_grids.items(), reverse=True)):
 # since round 3): conv3 / conv4 write their outputs' companions and no input
 # pack runs, so those bytes move from the pack row to the producers' rows
 if per.get("conv4/conv5 input packs k_pack_octets_x6", 0.0) == 0.0:
-    ALG["conv3 k_conv_cb_x6<3,3,4,8,...>"] = (P2O + 384*256*9*4 + Y3 + O4, "x octets + w + y + y octets")
-    ALG["conv4 k_conv_cb_x6<3,3,2,4,...>"] = (O4 + 384*192*9*4 + Y4 + O4, "x octets + w + y + y octets")
+    ALG["conv3 k_conv_cb16_x6<3,3,4,4,...>"] = (P2O + 384*256*9*4 + Y3 + O4, "x octets + w + y + y octets")
+    ALG["conv4 k_conv_cb16_x6<3,3,2,2,...>"] = (O4 + 384*192*9*4 + Y4 + O4, "x octets + w + y + y octets")
     ALG["conv4/conv5 input packs k_pack_octets_x6"] = (0.0, "none run (companions from the conv3 / conv4 epilogues)")
 table = {}
 for k, (alg, what) in ALG.items():

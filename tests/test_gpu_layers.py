@@ -181,15 +181,17 @@ def test_lrn_maxpool_fused_equals_unfused(device, size, k, s, p, C, H):
                                rtol=2e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("C,H", [(96, 55), (256, 27)])
-def test_lrn_maxpool_fused_equals_unfused_alexnet_planes(device, C, H):
+@pytest.mark.parametrize("C,H,N", [(96, 55, 3), (256, 27, 3), (96, 55, 256), (256, 27, 256)])
+def test_lrn_maxpool_fused_equals_unfused_alexnet_planes(device, C, H, N):
     """AlexNet's square 55 x 55 / 27 x 27 planes take the band kernel's
     compile-time-width path (immediate-offset pooling taps): bit for bit the
-    unfused LRN + max pool, with and without the octet companion."""
+    unfused LRN + max pool, with and without the octet companion.  At b256
+    the host cuts both planes' channels into 32-channel chunks, which take the
+    straight-line channel walk (N = 3: 8-channel chunks, the loop walk)."""
     import torch
     from rramsim import ops
     torch.manual_seed(11)
-    N, W = 3, H
+    W = H
     x = 4 * torch.randn(N, C, H, W, device=device)
     alpha, beta, kk = 1e-2, 0.75, 1.5
     lrn = torch.empty_like(x)
