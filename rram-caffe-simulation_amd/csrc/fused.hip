@@ -41,6 +41,9 @@ constexpr int kBandPix = 512;  // input pixels per band (PPT = 2 per thread)
 #ifndef RRAM_LRN_ALT
 #define RRAM_LRN_ALT 0
 #endif
+#ifndef RRAM_LRN_YNT  // cache policy of the pooled y stores (A/B builds: 2 = nontemporal)
+#define RRAM_LRN_YNT 0
+#endif
 #ifndef RRAM_LRN_DIAG
 #define RRAM_LRN_DIAG 0
 #endif
@@ -245,7 +248,8 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
           for (int a = 0; a < K; ++a)
 #pragma unroll
-            for (int b = 0; b < K; ++b) t[a * K + b] = yl[rowbase(a) + (b & 1) * HWC + (b >> 1)];
+            for (int b = 0; b < K; ++b)  // DIAG 5: no tap reads
+              t[a * K + b] = RRAM_LRN_DIAG == 5 ? __builtin_bit_cast(float, it_l[i] + a + b) : yl[rowbase(a) + (b & 1) * HWC + (b >> 1)];
           // v_max3 over the taps: the strict-">" walk's value whenever the
           // maximum is not zero (a quiet NaN loses to any number in both; the
           // plane holds products, never a signalling NaN); for a zero maximum
@@ -253,7 +257,7 @@ __global__ void __launch_bounds__(256)
           // -0, so such a window is walked again in order
 #pragma unroll
           for (int j = 0; j < K * K; j += 2) mv = max3f(mv, t[j], t[j + 1 < K * K ? j + 1 : j]);
-          if (mv == 0.0f) {
+          if (RRAM_LRN_DIAG != 6 && mv == 0.0f) {  // DIAG 6: no in-order re-walk
             mv = -FLT_MAX;
 #pragma unroll
             for (int j = 0; j < K * K; ++j) mv = t[j] > mv ? t[j] : mv;
@@ -269,7 +273,9 @@ __global__ void __launch_bounds__(256)
               if (ok && v > mv) mv = v;
             }
         }
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, mv), yrs, it_vo[i], c0 * PHW * 4, 0);
+        if (RRAM_LRN_DIAG != 4)  // DIAG 4: no y store
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, mv), yrs, it_vo[i], c0 * PHW * 4,
+                                                RRAM_LRN_YNT);
         if (OCT) obuf[(c0 + d) & 7][it_out[i] - pr0 * PW] = mv;
       }
     }
@@ -278,14 +284,20 @@ __global__ void __launch_bounds__(256)
   char* yon = OCT ? yo + (int64_t)n * (C / 8) * PHW * 48 : nullptr;
   auto octet_out = [&](int c8) {
     __syncthreads();  // obuf complete (the next group's barrier orders its rewrite)
-    const int o = threadIdx.x;
-    if (o < NO) {
+    // the band's outputs are consecutive (pr0 PW + o), so the octet's
+    // companion run is NO x 48 contiguous bytes: thread p stores 16-byte piece
+    // p (output p / 3, term p % 3), consecutive lanes on consecutive pieces
+    // (one thread per output storing its three terms left each store
+    // instruction 16 bytes per lane at a 48-byte stride)
+    char* run = yon + ((int64_t)(c8 / 8) * PHW + (int64_t)pr0 * PW) * 48;
+    for (int p = threadIdx.x; p < 3 * NO; p += kThreads) {
+      const int o = p / 3, tt = p - 3 * o;
       float v[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = obuf[e][o];
-      const int prl = o / PW;
-      const int64_t out = (int64_t)(pr0 + prl) * PW + (o - prl * PW);
-      x6::store_terms8(v, yon + ((int64_t)(c8 / 8) * PHW + out) * 48);
+      x6::Parts t;
+      x6::split8_safe(v, t);
+      *reinterpret_cast<x6::bf16x8*>(run + p * 16) = tt == 0 ? t.h : tt == 1 ? t.m : t.l;
     }
   };
   // the walk: prime the window of group 0 and the entering channels of groups

@@ -692,28 +692,13 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
   const int xcd = bid & 7, loc = bid >> 3;
   const int q8 = nwg >> 3, r8 = nwg & 7;
   const int tid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
-#ifndef RRAM_CB16_BAND
-#define RRAM_CB16_BAND 0
-#endif
-  // RRAM_CB16_BAND = B > 0 (A/B builds): the row tiles walked in bands of B
-  // column tiles, row-tile major inside a band (one row block's weights live
-  // in L2 at a time); 0: row tiles fastest (the row tiles of a column share
-  // its patch)
-  int tm_, tn_;
+  // row tiles fastest: the row tiles of a column tile share its patch (a
+  // band order, 48 column tiles per band so one row block's weights stay in
+  // L2, raised conv3 / conv4 traffic 403 -> 461 / 389 -> 528 MB:
+  // profiles/r05_ab_cb16_sd_band.txt)
   const int z = __builtin_amdgcn_readfirstlane(tid / (P.tiles_m * P.tiles_n));
-  {
-    const int r = tid - z * P.tiles_m * P.tiles_n;
-    if (RRAM_CB16_BAND > 0 && P.tiles_m > 1) {
-      const int band = r / (P.tiles_m * RRAM_CB16_BAND);
-      const int rb = r - band * P.tiles_m * RRAM_CB16_BAND;
-      const int w = min(RRAM_CB16_BAND, P.tiles_n - band * RRAM_CB16_BAND);
-      tm_ = rb / w;
-      tn_ = band * RRAM_CB16_BAND + (rb - tm_ * w);
-    } else {
-      tm_ = r % P.tiles_m;
-      tn_ = r / P.tiles_m;
-    }
-  }
+  const int r_ = tid - z * P.tiles_m * P.tiles_n;
+  const int tm_ = r_ % P.tiles_m, tn_ = r_ / P.tiles_m;
   const int tm = __builtin_amdgcn_readfirstlane(tm_);
   const int tn = __builtin_amdgcn_readfirstlane(tn_);
   const int m0 = tm * BMc;
@@ -839,12 +824,11 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
           f[i][t] = __builtin_bit_cast(
               x6::bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ar, alane, (q * MI + i) * cb16::FRAG * 16 + t * 1024, 0));
     };
-#ifndef RRAM_CB16_SD
-#define RRAM_CB16_SD 1
-#endif
     // staging distance (groups): the next K-tile's patch pieces are loaded at
-    // group g and stored to the next stage at g + SD
-    constexpr int SD = H >= 2 + RRAM_CB16_SD ? RRAM_CB16_SD : 1;
+    // group g and stored to the next stage at g + SD; SD = 2 where the K-tile
+    // has >= 4 groups (the 3x3 forms: +0.5 % maps/s, conv3 / conv4 -1 %,
+    // profiles/r05_ab_cb16_sd_band.txt; the 5x5 form keeps 1)
+    constexpr int SD = H >= 4 ? 2 : 1;
     constexpr int PMAX = (PD + H - SD - 1) / (H - SD);  // patch pieces per group (the shortest K-tile spreads them over H - SD groups)
     static_assert(H >= 2, "pair groups");
     typedef int int4x __attribute__((ext_vector_type(4)));
@@ -1528,7 +1512,17 @@ k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img,
   // chunk index: the last thread group's extra chunks (q >= CHUNKS) redo chunk
   // CHUNKS - 1 (same loads, same values, same LDS bytes: a benign duplicate
   // write), so the refill has no branch for the scheduler to stop at
-  auto chunk_of = [&](int k) __attribute__((always_inline)) { return min((int)threadIdx.x + k * 256, CHUNKS - 1); };
+  // (the thread index is re-derived per use from mbcnt behind an opaque asm,
+  // so the chunk addresses are recomputed where they are used instead of
+  // being hoisted out of the tile loop as live per-lane values: at 256 VGPRs
+  // those went to scratch, and every scratch reload is a vmcnt(0) that drained
+  // the weight loads in flight and the epilogue stores)
+  auto tid_now = [&]() __attribute__((always_inline)) {
+    int l = static_cast<int>(__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)));
+    asm volatile("" : "+v"(l));
+    return wave * 64 + l;
+  };
+  auto chunk_of = [&](int k) __attribute__((always_inline)) { return min(tid_now() + k * 256, CHUNKS - 1); };
   auto stage_load = [&](const TileRef& tr, int c, int k, float (&v)[8]) {
     const int q = chunk_of(k);
     const int ri = q / QP, qp = q - ri * QP;
@@ -1575,20 +1569,26 @@ k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img,
     if (step < 2 && 2 * step + u < CPT) stage_load(tr, c, 2 * step + u, sv[u]);
   };
 
-  // the weight fragments are the same for every tile: the base address is
+  // the weight fragments are the same for every tile: the resource is
   // laundered once per tile so the tile loop does not hoist all groups'
-  // loads out of itself
-  const x6::bf16x8* ap = reinterpret_cast<const x6::bf16x8*>(wpack) + lane;
+  // loads out of itself.  Buffer loads: one per-lane offset register and the
+  // fragment's constant offset in soffset (global loads needed a 64-bit
+  // address pair per 4 KB of fragments)
+  const uint32_t alane = static_cast<uint32_t>(lane) * 16u;
+  __amdgpu_buffer_rsrc_t ars =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(wpack), 0, G * MI * 3 * 1024, 0x00020000);
   auto launder_a = [&]() __attribute__((always_inline)) {
     int z = 0;
     asm volatile("" : "+s"(z));
-    ap = reinterpret_cast<const x6::bf16x8*>(wpack) + lane + z;
+    ars = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(wpack) + z, 0, G * MI * 3 * 1024, 0x00020000);
   };
   auto load_a = [&](x6::bf16x8 (&f)[MI][3], int g) {
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int tt = 0; tt < 3; ++tt) f[i][tt] = ap[((g * MI + i) * 3 + tt) * 64];
+      for (int tt = 0; tt < 3; ++tt)
+        f[i][tt] = __builtin_bit_cast(
+            x6::bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ars, static_cast<int>(alane), ((g * MI + i) * 3 + tt) * 1024, 0));
   };
   auto lds_barrier = [&]() __attribute__((always_inline)) {
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done
@@ -1688,6 +1688,8 @@ k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img,
       constexpr int g = decltype(gc)::value;
       x6::Parts (&fc)[2] = F[g & 1];
       x6::Parts (&fn)[2] = F[(g + 1) & 1];
+      // (a two-group ring that prefetched across the tile boundary measured
+      // flat: profiles/r05_ab_c1_scratch.txt)
       if (g + 2 < G) load_a(fg[(g + 2) % 3], g + 2);
       // slot refills (see the header): channel 2 of this tile at groups 1, 3, 5;
       // channel 0 / 1 of the next tile two, four and six groups after their last reader
