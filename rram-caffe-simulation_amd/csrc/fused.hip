@@ -71,8 +71,10 @@ constexpr int kLrnG = 2;
 // plain rows.
 // CCT > 0: every chunk is exactly CCT channels (host check; AlexNet b256:
 // 32-channel chunks of both planes): the channel walk is straight-line code
-// (round 5: 84.7 / 112 us per launch with the looped walk, whose back edge
-// made the compiler drain every load in flight at each trip top).
+// (the looped walk's back edge made the compiler drain every load in flight
+// at each trip top).  Round 5, norm2 / norm1 per launch: 84.6 / 112.1 us ->
+// 80.5 / 109.0 (ring, straight line) -> 73.8 / 102.1 (coalesced companion
+// stores), profiles/r05_ab_lrn_walk.txt.
 __device__ __forceinline__ float max3f(float a, float b, float c) {
   float r;
   asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));

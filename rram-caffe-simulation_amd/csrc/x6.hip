@@ -1512,17 +1512,7 @@ k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img,
   // chunk index: the last thread group's extra chunks (q >= CHUNKS) redo chunk
   // CHUNKS - 1 (same loads, same values, same LDS bytes: a benign duplicate
   // write), so the refill has no branch for the scheduler to stop at
-  // (the thread index is re-derived per use from mbcnt behind an opaque asm,
-  // so the chunk addresses are recomputed where they are used instead of
-  // being hoisted out of the tile loop as live per-lane values: at 256 VGPRs
-  // those went to scratch, and every scratch reload is a vmcnt(0) that drained
-  // the weight loads in flight and the epilogue stores)
-  auto tid_now = [&]() __attribute__((always_inline)) {
-    int l = static_cast<int>(__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)));
-    asm volatile("" : "+v"(l));
-    return wave * 64 + l;
-  };
-  auto chunk_of = [&](int k) __attribute__((always_inline)) { return min(tid_now() + k * 256, CHUNKS - 1); };
+  auto chunk_of = [&](int k) __attribute__((always_inline)) { return min((int)threadIdx.x + k * 256, CHUNKS - 1); };
   auto stage_load = [&](const TileRef& tr, int c, int k, float (&v)[8]) {
     const int q = chunk_of(k);
     const int ri = q / QP, qp = q - ri * QP;
@@ -1569,26 +1559,22 @@ k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img,
     if (step < 2 && 2 * step + u < CPT) stage_load(tr, c, 2 * step + u, sv[u]);
   };
 
-  // the weight fragments are the same for every tile: the resource is
+  // the weight fragments are the same for every tile: the base address is
   // laundered once per tile so the tile loop does not hoist all groups'
-  // loads out of itself.  Buffer loads: one per-lane offset register and the
-  // fragment's constant offset in soffset (global loads needed a 64-bit
-  // address pair per 4 KB of fragments)
-  const uint32_t alane = static_cast<uint32_t>(lane) * 16u;
-  __amdgpu_buffer_rsrc_t ars =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(wpack), 0, G * MI * 3 * 1024, 0x00020000);
+  // loads out of itself.  (At 512 registers the allocator keeps 20 bytes of
+  // scratch; a spill-free form -- thread index re-derived per use, buffer-
+  // loaded fragments -- measured ~1 % slower: profiles/r05_ab_c1_scratch.txt)
+  const x6::bf16x8* ap = reinterpret_cast<const x6::bf16x8*>(wpack) + lane;
   auto launder_a = [&]() __attribute__((always_inline)) {
     int z = 0;
     asm volatile("" : "+s"(z));
-    ars = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(wpack) + z, 0, G * MI * 3 * 1024, 0x00020000);
+    ap = reinterpret_cast<const x6::bf16x8*>(wpack) + lane + z;
   };
   auto load_a = [&](x6::bf16x8 (&f)[MI][3], int g) {
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int tt = 0; tt < 3; ++tt)
-        f[i][tt] = __builtin_bit_cast(
-            x6::bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ars, static_cast<int>(alane), ((g * MI + i) * 3 + tt) * 1024, 0));
+      for (int tt = 0; tt < 3; ++tt) f[i][tt] = ap[((g * MI + i) * 3 + tt) * 64];
   };
   auto lds_barrier = [&]() __attribute__((always_inline)) {
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes done
@@ -1688,8 +1674,6 @@ k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img,
       constexpr int g = decltype(gc)::value;
       x6::Parts (&fc)[2] = F[g & 1];
       x6::Parts (&fn)[2] = F[(g + 1) & 1];
-      // (a two-group ring that prefetched across the tile boundary measured
-      // flat: profiles/r05_ab_c1_scratch.txt)
       if (g + 2 < G) load_a(fg[(g + 2) % 3], g + 2);
       // slot refills (see the header): channel 2 of this tile at groups 1, 3, 5;
       // channel 0 / 1 of the next tile two, four and six groups after their last reader
