@@ -41,6 +41,9 @@ constexpr int kBandPix = 512;  // input pixels per band (PPT = 2 per thread)
 #ifndef RRAM_LRN_ALT
 #define RRAM_LRN_ALT 0
 #endif
+#ifndef RRAM_LRN_BAL  // even band heights (A/B builds: 0 = the tallest bands first)
+#define RRAM_LRN_BAL 1
+#endif
 #ifndef RRAM_LRN_YNT  // cache policy of the pooled y stores (A/B builds: 2 = nontemporal)
 #define RRAM_LRN_YNT 0
 #endif
@@ -402,6 +405,10 @@ int rram_lrn_maxpool_fwd_octets(const float* x, float* y, void* y_oct, int num, 
   RRAM_REQUIRE(fits(1), "lrn_maxpool_fwd: a pooled row needs more than %d input pixels", kBandPix);
   int rb = 1;
   while (rb < PH && fits(rb + 1)) ++rb;
+  // the fewest bands at that height, then their rows evened out (AlexNet
+  // norm2: 7 + 6 pooled rows, not 8 + 5, so no block carries 1.5x another's
+  // pixels)
+  if (RRAM_LRN_BAL) rb = (PH + (PH + rb - 1) / rb - 1) / ((PH + rb - 1) / rb);
   // channel chunks: as few as give >= kLrnBlocks blocks (each chunk re-reads
   // SIZE - 1 halo channels), equal sizes in multiples of 8 (2 * G without octets)
   const int step = y_oct ? 8 : 2 * kLrnG;
