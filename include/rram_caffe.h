@@ -82,8 +82,14 @@ int rram_net_layer_info(rram_net_t net, int i, char* name, char* type, int cap, 
 int rram_net_layer_contraction(rram_net_t net, int i, double* flops, int* engine);
 int rram_net_num_blobs(rram_net_t net, int* n);
 int rram_net_blob_name(rram_net_t net, int i, char* name, int cap);
-/* device pointers and shape (up to 8 axes) of a named blob */
+/* device pointers and shape (up to 8 axes) of a named blob (a blob a
+ * TEST-phase fold left unwritten is materialised first, and stays so) */
 int rram_net_blob(rram_net_t net, const char* name, float** data, float** diff, int* shape, int* num_axes);
+/* *stale = 1 when the named blob's fp32 contents were not written by the last
+ * forward (its producer wrote only the octet companion its one reader takes:
+ * the pooled-output fold), 0 otherwise; does not materialise.  No reference
+ * counterpart (a fusion of this build). */
+int rram_net_blob_stale(rram_net_t net, const char* name, int* stale);
 int rram_net_num_params(rram_net_t net, int* n);
 int rram_net_param(rram_net_t net, int i, float** data, float** diff, int64_t* count, float* lr_mult,
                    float* decay_mult);

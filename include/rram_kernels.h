@@ -508,7 +508,10 @@ int rram_lrn_maxpool_fwd(const float* x, float* y, int num, int channels, int he
                          rram_stream_t s);
 
 /* rram_lrn_maxpool_fwd that also writes y's channel-octet companion
- * (y_oct nullable; channels % 8 == 0), see rram_conv2d_fwd_octets. */
+ * (y_oct nullable; channels % 8 == 0), see rram_conv2d_fwd_octets.  y may be
+ * NULL when y_oct is not: only the companion is written (the caller's only
+ * reader of y takes the companion; it must re-run with y before anything
+ * reads y itself). */
 int rram_lrn_maxpool_fwd_octets(const float* x, float* y, void* y_oct, int num, int channels, int height,
                                 int width, int pooled_h, int pooled_w, int kernel, int stride_h, int stride_w,
                                 int pad_h, int pad_w, int size, float alpha, float beta, float k,

@@ -33,6 +33,8 @@ namespace {
 // the image, -FLT_MAX start, strict ">" in row-major order.
 // HBM traffic: x read once (plus the shared input row between adjacent bands
 // and the chunk halos), y written once; the LRN output never leaves the CU.
+// y == nullptr (with a companion): only the companion is written (the host's
+// pooled-output fold, Net::Net: its one reader takes the companion).
 constexpr int kBandPix = 512;  // input pixels per band (PPT = 2 per thread)
 // target grid of the LRN + pool band kernel: several block waves of 256 CUs
 #ifndef RRAM_LRN_BLOCKS
@@ -176,8 +178,12 @@ __global__ void __launch_bounds__(256)
   const int NO = (pr1 - pr0) * PW;  // pooled outputs of the band per channel
   const int PHW = PH * PW;
   // y of image n through a buffer resource too (one image < 2 GiB: host check)
+  // (y == nullptr: the pooled fp32 output is not materialised, only its
+  // octet companion -- the host's pooled-output fold; the range-0 resource
+  // then drops the stores)
+  const bool ys = y != nullptr;
   const __amdgpu_buffer_rsrc_t yrs =
-      __builtin_amdgcn_make_buffer_rsrc(y + (int64_t)n * C * PHW, 0, C * PHW * 4, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc(ys ? y + (int64_t)n * C * PHW : y, 0, ys ? C * PHW * 4 : 0, 0x00020000);
   // pooling items of a group: (channel d, output o), consecutive outputs of
   // one channel on consecutive lanes (coalesced stores); each thread's items
   // and their windows are fixed for the whole channel walk, so they are
@@ -278,7 +284,7 @@ __global__ void __launch_bounds__(256)
               if (ok && v > mv) mv = v;
             }
         }
-        if (RRAM_LRN_DIAG != 4)  // DIAG 4: no y store
+        if (RRAM_LRN_DIAG != 4 && ys)  // DIAG 4: no y store
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, mv), yrs, it_vo[i], c0 * PHW * 4,
                                                 RRAM_LRN_YNT);
         if (OCT) obuf[(c0 + d) & 7][it_out[i] - pr0 * PW] = mv;
@@ -395,7 +401,7 @@ int rram_lrn_maxpool_fwd_octets(const float* x, float* y, void* y_oct, int num, 
   RRAM_REQUIRE((int64_t)C * H * W * 4 < 2147483647ll && (int64_t)C * PH * PW * 4 < 2147483647ll,
                "lrn_maxpool_fwd: one image must be < 2 GiB");
   if (num == 0) return RRAM_OK;
-  RRAM_REQUIRE(x && y, "lrn_maxpool_fwd: NULL");
+  RRAM_REQUIRE(x && (y || y_oct), "lrn_maxpool_fwd: NULL (y may be NULL only with a companion)");
   // band height: input rows of RB pooled rows must fit the block's pixel
   // budget and RB * PW outputs its threads
   auto fits = [&](int rb) {

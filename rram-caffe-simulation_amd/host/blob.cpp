@@ -126,6 +126,8 @@ void SyncedMemory::to_gpu() {
 }
 
 const void* SyncedMemory::cpu_data() {
+  CAFFE_CHECK(!fp32_stale, "host read of a blob whose producer wrote only its octet companion "
+                           "(Net::materialize_blob first)");
   to_cpu();
   return cpu_ptr_;
 }
@@ -136,6 +138,7 @@ const void* SyncedMemory::gpu_data() {
 void* SyncedMemory::mutable_cpu_data() {
   oct_valid_ = false;
   wp_valid_ = false;
+  fp32_stale = false;
   to_cpu();
   head_ = HEAD_AT_CPU;
   return cpu_ptr_;
@@ -143,6 +146,7 @@ void* SyncedMemory::mutable_cpu_data() {
 void* SyncedMemory::mutable_gpu_data() {
   oct_valid_ = false;
   wp_valid_ = false;
+  fp32_stale = false;
   to_gpu();
   head_ = HEAD_AT_GPU;
   return gpu_ptr_;
@@ -151,6 +155,7 @@ void SyncedMemory::set_cpu_data(void* data) {
   CAFFE_CHECK(data, "set_cpu_data(NULL)");
   oct_valid_ = false;
   wp_valid_ = false;
+  fp32_stale = false;
   if (own_cpu_ && cpu_ptr_) std::free(cpu_ptr_);
   cpu_ptr_ = data;
   own_cpu_ = false;
@@ -160,6 +165,7 @@ void SyncedMemory::set_gpu_data(void* data) {
   CAFFE_CHECK(data, "set_gpu_data(NULL)");
   oct_valid_ = false;
   wp_valid_ = false;
+  fp32_stale = false;
   if (own_gpu_ && gpu_ptr_) (void)hipFree(gpu_ptr_);
   gpu_ptr_ = data;
   own_gpu_ = false;

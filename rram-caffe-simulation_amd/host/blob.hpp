@@ -43,6 +43,9 @@ class SyncedMemory {
   const void* valid_octets(const int (&shape)[4]) const;
   void set_octets_valid(const int (&shape)[4]);
   bool wants_octets = false;  // a consumer would read the companion
+  // the producer wrote only the companion (TEST-phase pooled-output fold,
+  // Net::Net): the fp32 contents are stale until Net::materialize_blob
+  bool fp32_stale = false;
 
   // Packed-weight companion (rram_conv2d_fwd_cached): the bf16x6 engine's
   // pre-split form of these weights, valid for one key (the layer's shape and

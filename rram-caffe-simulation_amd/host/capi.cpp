@@ -258,6 +258,16 @@ int rram_net_blob(rram_net_t n, const char* name, float** data, float** diff, in
       for (int a = 0; a < b->num_axes() && a < 8; ++a) shape[a] = b->shape(a);
   });
 }
+int rram_net_blob_stale(rram_net_t n, const char* name, int* stale) {
+  return guarded([&] {
+    NEED(n);
+    NEED(name);
+    NEED(stale);
+    auto b = n->net->blob_by_name(name);
+    if (!b) throw Error(std::string("Unknown blob name ") + name);
+    *stale = b->data()->fp32_stale ? 1 : 0;
+  });
+}
 int rram_net_num_params(rram_net_t n, int* k) {
   return guarded([&] {
     NEED(n);

@@ -91,6 +91,14 @@ class Layer {
     return false;
   }
   bool folded_into_next = false;
+  // TEST-phase pooled-output fold (Net::Net): a folded LRN + MAX pool whose
+  // top's only reader is a Convolution that reads the top's octet companion
+  // writes only the companion; set_octet_reader() names that reader (nullptr
+  // undoes it), input_octets_now() is the reader's check, per forward, that it
+  // will read the companion of an input shaped like `bottom` (engine and plan
+  // as they stand then)
+  virtual bool set_octet_reader(Layer* /*reader*/) { return false; }
+  virtual bool input_octets_now(const Blob<Dtype>* /*bottom*/) const { return false; }
   // ReLU fold into a Pooling producer (Net::Net, any phase): an in-place ReLU
   // right after a layer that accepts it is applied in that layer's output
   // store (rram_pool_relu_fwd); the ReLU's Backward still runs.

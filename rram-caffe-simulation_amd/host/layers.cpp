@@ -230,6 +230,8 @@ void ConvolutionLayer<Dtype>::Forward_gpu(const std::vector<Blob<Dtype>*>& botto
     // inception branches) reuse it instead of each packing a scratch copy
     SyncedMemory* xm = bottom[0]->data().get();
     xo = xm->valid_octets(shp);
+    CAFFE_CHECK(xo != nullptr || !xm->fp32_stale,
+                this->name() << ": input companion invalid while its producer skipped the fp32 output");
     if (xo == nullptr) {
       void* buf = xm->octets(static_cast<size_t>(bottom[0]->count()) * 6);
       RRAM_CALL(rram_pack_octets(bottom[0]->gpu_data(), buf, shp[0], shp[1], shp[2], shp[3], Caffe::stream()));
@@ -460,10 +462,16 @@ class PoolingLayer : public Layer<Dtype> {
         ph_ >= kh_ || pw_ >= kw_ || (size != 3 && size != 5))
       return false;
     lrn_src_ = lrn_bottom;
+    if (lrn_bottom == nullptr) octet_reader_ = nullptr;  // a plain pool writes its top
     lrn_size_ = size;
     lrn_alpha_ = alpha;
     lrn_beta_ = beta;
     lrn_k_ = k;
+    return true;
+  }
+  bool set_octet_reader(Layer<Dtype>* reader) override {
+    if (reader != nullptr && lrn_src_ == nullptr) return false;
+    octet_reader_ = reader;
     return true;
   }
   bool fuse_relu_before_bwd(float slope) override {
@@ -484,10 +492,14 @@ class PoolingLayer : public Layer<Dtype> {
     if (lrn_src_ != nullptr) {  // LRN folded into this pool (Net::Net, TEST phase)
       float* y = top[0]->mutable_gpu_data();
       void* yo = octets_for(top[0], kOctPool);
-      RRAM_CALL(rram_lrn_maxpool_fwd_octets(lrn_src_->gpu_data(), y, yo, bottom[0]->shape(0), C_, H_, W_, PH_, PW_,
-                                            kh_, sh_, sw_, ph_, pw_, lrn_size_, lrn_alpha_, lrn_beta_, lrn_k_,
-                                            Caffe::stream()));
+      // pooled-output fold: the only reader takes the companion, so the fp32
+      // top is not written (materialised on demand by Net::materialize_blob)
+      const bool skip_y = yo != nullptr && octet_reader_ != nullptr && octet_reader_->input_octets_now(top[0]);
+      RRAM_CALL(rram_lrn_maxpool_fwd_octets(lrn_src_->gpu_data(), skip_y ? nullptr : y, yo, bottom[0]->shape(0), C_,
+                                            H_, W_, PH_, PW_, kh_, sh_, sw_, ph_, pw_, lrn_size_, lrn_alpha_,
+                                            lrn_beta_, lrn_k_, Caffe::stream()));
       if (yo) mark_octets(top[0]);
+      top[0]->data()->fp32_stale = skip_y;
       return;
     }
     const bool top_mask = top.size() > 1;
@@ -520,6 +532,7 @@ class PoolingLayer : public Layer<Dtype> {
   float relu_slope_ = 0.0f, relu_bwd_slope_ = 0.0f;
   Blob<Dtype> mask_;
   Blob<Dtype>* lrn_src_ = nullptr;  // bottom of a folded LRN (nullptr: unfused)
+  Layer<Dtype>* octet_reader_ = nullptr;  // pooled-output fold: the top's only reader
   int lrn_size_ = 5;
   float lrn_alpha_ = 1, lrn_beta_ = 0.75f, lrn_k_ = 1;
 };

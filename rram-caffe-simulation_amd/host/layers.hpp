@@ -26,6 +26,14 @@ class ConvolutionLayer : public Layer<Dtype> {
   // unchanged; set by Net::set_weight_pack_cache for the Monte-Carlo driver
   bool cache_wpack = false;
   const rram_conv_desc& desc() const { return desc_; }
+  bool input_octets_now(const Blob<Dtype>* bottom) const override {
+    if (bottom->num_axes() != 4) return false;
+    rram_conv_desc d = desc_;
+    d.num = bottom->shape(0);
+    d.height = bottom->shape(2);
+    d.width = bottom->shape(3);
+    return bottom->shape(1) == d.channels && rram_conv_input_octets(&d) == 1;
+  }
   bool write_into_concat(Blob<Dtype>* concat_top, int channel_offset) override {
     concat_top_ = concat_top;
     concat_off_ = channel_offset;

@@ -348,6 +348,35 @@ Net<Dtype>::Net(const Msg& in_param, Phase phase, const Msg& options) : phase_(p
       }
     }
   }
+  // TEST phase: a folded LRN + MAX pool whose top is read by exactly one
+  // layer, a Convolution with no other writer of that top in between, writes
+  // only the top's octet companion whenever that Convolution reads it (each
+  // forward checks: engine and plan as they stand); the fp32 top is then
+  // materialised only on demand (materialize_blob; the C-ABI does for every
+  // blob it hands out), like a folded LRN's top
+#ifndef RRAM_POOL_Y_FOLD  // A/B builds: 0 = the pool always writes its fp32 top
+#define RRAM_POOL_Y_FOLD 1
+#endif
+  if (RRAM_POOL_Y_FOLD && fuse_lrn_pool && phase == TEST) {
+    const int L = static_cast<int>(layers_.size());
+    for (const LrnFold& f : lrn_folds_) {
+      if (top_id_vecs_[f.pool].size() != 1) continue;
+      const int t = top_id_vecs_[f.pool][0];
+      int reader = -1;
+      bool ok = true;
+      for (int k = 0; k < L && ok; ++k) {
+        if (k == f.pool) continue;
+        const bool reads = std::count(bottom_id_vecs_[k].begin(), bottom_id_vecs_[k].end(), t) > 0;
+        const bool writes = std::count(top_id_vecs_[k].begin(), top_id_vecs_[k].end(), t) > 0;
+        if (writes || (reads && reader >= 0)) ok = false;
+        else if (reads) reader = k;
+      }
+      if (ok && reader > f.pool && bottom_vecs_[reader].size() == 1 &&
+          dynamic_cast<ConvolutionLayer<Dtype>*>(layers_[reader].get()) != nullptr &&
+          layers_[f.pool]->set_octet_reader(layers_[reader].get()))
+        pool_y_folds_.push_back(f.pool);
+    }
+  }
   for (auto& n : available) {
     const int id = blob_names_index_[n];
     net_output_blobs_.push_back(blobs_[id].get());
@@ -373,6 +402,18 @@ void Net<Dtype>::materialize_blob(const Blob<Dtype>* b) {
     layers_[f.writer]->write_into_concat(nullptr, 0);
     layers_[f.concat]->skip_concat_bottom(f.bottom, false);
     concat_folds_.erase(concat_folds_.begin() + static_cast<long>(i));
+  }
+  for (size_t i = 0; i < pool_y_folds_.size();) {
+    const int l = pool_y_folds_[i];
+    Blob<Dtype>* t = top_vecs_[l][0];
+    if (t != b) {
+      ++i;
+      continue;
+    }
+    layers_[l]->set_octet_reader(nullptr);
+    if (t->data()->fp32_stale && bottom_vecs_[l][0]->count() > 0) layers_[l]->Forward(bottom_vecs_[l], top_vecs_[l]);
+    t->data()->fp32_stale = false;
+    pool_y_folds_.erase(pool_y_folds_.begin() + static_cast<long>(i));
   }
   for (size_t i = 0; i < lrn_folds_.size();) {
     const LrnFold f = lrn_folds_[i];

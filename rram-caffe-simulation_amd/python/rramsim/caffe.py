@@ -36,6 +36,7 @@ SIGNATURES = {
     "rram_net_num_blobs": (I, [P, PI]),
     "rram_net_blob_name": (I, [P, I, C.c_char_p, I]),
     "rram_net_blob": (I, [P, C.c_char_p, PP, PP, PI, PI]),
+    "rram_net_blob_stale": (I, [P, C.c_char_p, PI]),
     "rram_net_num_params": (I, [P, PI]),
     "rram_net_param": (I, [P, I, PP, PP, PI64, PF, PF]),
     "rram_net_num_failure_params": (I, [P, PI]),
@@ -361,6 +362,13 @@ class Net:
         check(self._lib.rram_net_blob(self.h, name.encode(), C.byref(d), C.byref(g), shape, C.byref(na)),
               f"blob {name}")
         return _wrap_device((g if diff else d).value, [shape[i] for i in range(na.value)])
+
+    def blob_stale(self, name: str) -> bool:
+        """True when the last forward left the blob's fp32 contents unwritten
+        (the pooled-output fold); blob() materialises it."""
+        st = C.c_int()
+        check(self._lib.rram_net_blob_stale(self.h, name.encode(), C.byref(st)), f"blob_stale {name}")
+        return bool(st.value)
 
     def params(self):
         n = C.c_int()

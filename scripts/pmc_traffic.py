@@ -74,9 +74,11 @@ O4 = 384*13*13*B*6
 Y5 = 256*13*13*B*4
 ALG = {  # class: (algorithmic bytes per step, description)
     "conv1 k_conv1_ring_x6": (A1 + 96*363*4 + Y1, "x fp32 + w + y"),
-    "norm1+pool1 (LRN + max pool, octets)": (Y1 + P1Y + P1O, "x + y + y octets"),
+    # (round 5: the pooled fp32 y is materialised only on read -- the
+    # pooled-output fold, conv2 / conv3 take the companion -- so not written)
+    "norm1+pool1 (LRN + max pool, octets)": (Y1 + P1O, "x + y octets"),
     "conv2 k_conv_cb16_x6<5,5,...>": (P1O + 256*48*25*4 + Y2, "x octets + w + y"),
-    "norm2+pool2 (LRN + max pool, octets)": (Y2 + P2Y + P2O, "x + y + y octets"),
+    "norm2+pool2 (LRN + max pool, octets)": (Y2 + P2O, "x + y octets"),
     "conv3 k_conv_cb16_x6<3,3,4,4,...>": (P2O + 384*256*9*4 + Y3, "x octets + w + y"),
     "conv4/conv5 input packs k_pack_octets_x6": (2 * (Y3 + O4), "2 x (read fp32, write octets)"),
     "conv4 k_conv_cb16_x6<3,3,2,2,...>": (O4 + 384*192*9*4 + Y4, "x octets + w + y"),

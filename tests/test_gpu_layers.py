@@ -588,6 +588,39 @@ def test_folded_blobs_materialise_when_read(device):
             assert torch.equal(got[True][1][n], got[False][1][n]), (name, n)
 
 
+def test_pooled_output_fold_materialises(device):
+    """AlexNet TEST net, LRN + max pool folds on: from the second forward on,
+    pool1 / pool2 (each read only by a convolution that takes their octet
+    companion) are left unwritten in fp32 -- the kernel writes only the
+    companion -- and are materialised when the C-ABI hands them out: bit for
+    bit the unfused net's blobs; the net outputs stay bit-identical, and
+    after the read the pool writes its fp32 output again."""
+    import torch
+    from rramsim import caffe, models
+    caffe.set_stream_from_torch()
+    got = {}
+    for fuse in (False, True):
+        caffe.set_random_seed(1701)
+        net = caffe.Net(models.alexnet(test_batch=8), "test", models.net_options("alexnet", fuse_lrn_pool=fuse))
+        for _ in range(3):
+            net.forward()
+        torch.cuda.synchronize()
+        stale = {n: net.blob_stale(n) for n in ("pool1", "pool2", "norm1", "fc8")}
+        got[fuse] = {n: net.blob(n).detach().cpu().clone() for n in ("pool1", "pool2", "fc8")}
+        after = {n: net.blob_stale(n) for n in ("pool1", "pool2")}
+        net.forward()
+        torch.cuda.synchronize()
+        again = {n: net.blob_stale(n) for n in ("pool1", "pool2")}
+        net.close()
+        if fuse:
+            assert stale["pool1"] and stale["pool2"] and not stale["fc8"], stale
+            assert not any(after.values()) and not any(again.values()), (after, again)
+        else:
+            assert not any(stale.values()), stale
+    for n in got[False]:
+        assert torch.equal(got[True][n], got[False][n]), n
+
+
 @pytest.mark.parametrize("shape,k,s,p", [((2, 5, 13, 11), 3, 2, 0), ((3, 4, 32, 32), 3, 2, 0), ((2, 3, 16, 16), 3, 2, 1),
                                          ((1, 2, 64, 64), 2, 2, 0), ((1, 1, 70, 70), 3, 2, 0)])
 def test_max_pool_bwd_bit_exact(device, shape, k, s, p):

@@ -139,6 +139,10 @@ def test_lrn_maxpool_octets_bit_identical(device):
         ref = N(y0)
         np.testing.assert_array_equal(N(y1), ref)
         np.testing.assert_array_equal(_as_u16(yo, (n, c, ph, pw)), octets_ref(ref))
+        # y = NULL (the pooled-output fold): the same companion, no fp32 store
+        yo2 = _oct_buf((n, c, ph, pw), device)
+        ops.lrn_maxpool_fwd_octets(xd, None, yo2, n, c, h, w, ph, pw, 3, 2, 0, 5, 1e-4, 0.75)
+        np.testing.assert_array_equal(_as_u16(yo2, (n, c, ph, pw)), octets_ref(ref))
 
 
 def test_alexnet_forward_pool_companions_only_bit_identical(device):
