@@ -1357,6 +1357,17 @@ int launch_cfg(Params P, int gz, hipStream_t s) {
 template <int AM, int BMODE, int OM, int KB>
 int launch(const Params& P, int gz, hipStream_t s, bool force_big) {
   if (force_big) {
+#ifndef RRAM_SPLIT_THIN32
+#define RRAM_SPLIT_THIN32 1
+#endif
+    // split-K grids with M <= 32 and N > 64 (the CIFAR-10 weight gradients:
+    // Cout = 32, N = 76 / 801): 32 x 128 tiles, which waste no MFMA rows (64 x
+    // 64 padded half): C4 0.362 -> 0.348 ms per iteration.  Not for N <= 64
+    // (LeNet conv1, N = 26: 0.199 -> 0.204 ms, the 128-wide B tile gathers
+    // mostly padding), profiles/r05_ab_split_thin32.txt
+    if constexpr (KB == 32) {
+      if (RRAM_SPLIT_THIN32 && P.M <= 32 && P.N > 64) return launch_cfg<1, 4, 1, 1, AM, BMODE, OM, KB>(P, gz, s);
+    }
     // split-K grids: 64 x 64 tiles when an operand is that thin (conv weight gradients)
     if (P.M <= 64 || P.N <= 64) return launch_cfg<2, 2, 1, 1, AM, BMODE, OM, KB>(P, gz, s);
     return launch_cfg<2, 2, 2, 2, AM, BMODE, OM, KB>(P, gz, s);

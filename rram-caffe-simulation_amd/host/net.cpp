@@ -387,6 +387,17 @@ Net<Dtype>::Net(const Msg& in_param, Phase phase, const Msg& options) : phase_(p
 
 template <typename Dtype>
 void Net<Dtype>::materialize_blob(const Blob<Dtype>* b) {
+  const size_t folds = concat_folds_.size() + pool_y_folds_.size() + lrn_folds_.size();
+  // a captured MC / Solver graph replays the folded launches: undoing a fold
+  // must make it recapture (the graph keys include this generation)
+  struct Bump {
+    const Net* n;
+    size_t before;
+    ~Bump() {
+      if (n->concat_folds_.size() + n->pool_y_folds_.size() + n->lrn_folds_.size() != before)
+        Caffe::scratch_gen().fetch_add(1);
+    }
+  } bump{this, folds};
   for (size_t i = 0; i < concat_folds_.size();) {
     const ConcatFold f = concat_folds_[i];
     Blob<Dtype>* bot = bottom_vecs_[f.concat][f.bottom];
