@@ -137,3 +137,41 @@ def test_graph_training_interleaved_equals_eager(device, mode):
     for a, b in zip(got[0] + got[1] + got[2], ref[0] + ref[1] + ref[2]):
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
     assert got[3] == ref[3]
+
+
+def test_graph_maps_with_pooled_output_fold_read_between_runs(device):
+    """AlexNet (LRN + max pool folds, the pooled-output fold on): maps
+    replayed from a graph, pool1 read through the C-ABI between two runs
+    (materialised; the fold is undone, which must force a recapture: the
+    captured map skips the fp32 pooled top), then more maps: per-map
+    statistics, broken counts, pool1 and the outputs bit-identical to the
+    eager sequence."""
+    import torch
+    from rramsim import caffe, make_inject_cfg, models
+
+    def run(graph):
+        caffe.set_stream_from_torch()
+        caffe.set_random_seed(1701)
+        net = caffe.Net(models.alexnet(test_batch=4), "test", models.net_options("alexnet"))
+        mc = caffe.MonteCarlo(net, make_inject_cfg(0.05), seed=77, max_maps=16)
+        mc.set_graph(graph)
+        mc.run(0, 3)
+        torch.cuda.synchronize()
+        p1 = N(net.blob("pool1"))
+        mc.run(3, 3)
+        torch.cuda.synchronize()
+        p2 = N(net.blob("pool1"))
+        st = mc.stats()
+        outs = {k: N(v) for k, v in net.outputs().items()}
+        active = mc.graph_active()
+        mc.close()
+        net.close()
+        return st, p1, p2, outs, active
+
+    ref = run(False)
+    got = run(True)
+    assert got[4] and not ref[4]
+    assert got[0]["per_map"] == ref[0]["per_map"] and got[0]["broken"] == ref[0]["broken"]
+    assert np.array_equal(got[1], ref[1]) and np.array_equal(got[2], ref[2])
+    for k in ref[3]:
+        assert np.array_equal(got[3][k], ref[3][k]), k
