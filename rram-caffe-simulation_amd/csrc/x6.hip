@@ -2209,6 +2209,8 @@ struct CbPlan {
 #define RRAM_CB_LIST(X)                                                                              \
   X(5, 4, 8, 15, 1) X(5, 4, 4, 12, 1) X(5, 4, 4, 14, 1) X(5, 2, 4, 14, 1) X(3, 4, 8, 12, 1)          \
   X(3, 4, 8, 15, 1) X(3, 4, 4, 8, 1) X(3, 4, 4, 12, 1) X(3, 2, 4, 12, 1) X(3, 2, 4, 14, 1)
+// (a 64 x 256 form for conv4 does not fit two per CU: its contiguous patch
+// spans up to 27 rows = 9 LDS pieces, the per-image one wastes a third)
 #define RRAM_CB16_LIST(X) X(5, 4, 4, 8, 2) X(3, 4, 4, 8, 2) X(3, 2, 2, 8, 2)
 bool cb_instantiated(int KH, int WR, int NB, int PD, int OCC = 1) {
 #define RRAM_X(kh, wr, nb, pd, occ) \
