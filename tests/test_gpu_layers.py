@@ -621,6 +621,31 @@ def test_pooled_output_fold_materialises(device):
         assert torch.equal(got[True][n], got[False][n]), n
 
 
+def test_pooled_output_fold_needs_a_sole_convolution_reader(device):
+    """A second reader of pool1 (here a ReLU writing its own top) keeps the
+    pool writing its fp32 top: pool1 is never stale, the extra reader sees
+    the unfused values, and pool2 (still read by conv3 alone) stays folded."""
+    import torch
+    from rramsim import caffe, models
+    caffe.set_stream_from_torch()
+    proto = models.alexnet(test_batch=4) + (
+        '\nlayer { name: "pool1_relu" type: "ReLU" bottom: "pool1" top: "pool1_relu" }\n')
+    got = {}
+    for fuse in (False, True):
+        caffe.set_random_seed(1701)
+        net = caffe.Net(proto, "test", models.net_options("alexnet", fuse_lrn_pool=fuse))
+        for _ in range(3):
+            net.forward()
+        torch.cuda.synchronize()
+        stale = (net.blob_stale("pool1"), net.blob_stale("pool2"))
+        got[fuse] = {n: net.blob(n).detach().cpu().clone() for n in ("pool1", "pool1_relu", "pool2", "fc8")}
+        net.close()
+        if fuse:
+            assert stale == (False, True), stale
+    for n in got[False]:
+        assert torch.equal(got[True][n], got[False][n]), n
+
+
 @pytest.mark.parametrize("shape,k,s,p", [((2, 5, 13, 11), 3, 2, 0), ((3, 4, 32, 32), 3, 2, 0), ((2, 3, 16, 16), 3, 2, 1),
                                          ((1, 2, 64, 64), 2, 2, 0), ((1, 1, 70, 70), 3, 2, 0)])
 def test_max_pool_bwd_bit_exact(device, shape, k, s, p):
