@@ -27,6 +27,16 @@ MFMA_X6_PEAK_TFLOPS = 2500.0 / 6  # bf16 dense peak / the bf16x6 engine's 6 prod
 PEAK_OF_ENGINE = {0: MFMA_F32_PEAK_TFLOPS, 1: MFMA_X6_PEAK_TFLOPS}
 
 
+def map_statistics(s, s2, n):
+    """Mean, sample standard deviation and 95 % CI half-width (normal
+    approximation, 1.96 sigma / sqrt(n)) of n per-map values from their sum s
+    and sum of squares s2 (all-reduced over ranks by the caller)."""
+    nm = max(int(n), 1)
+    mean = s / nm
+    var = max(s2 / nm - mean * mean, 0.0) * nm / max(nm - 1, 1)
+    return dict(mean=mean, std=var ** 0.5, ci95=1.96 * (var / nm) ** 0.5, maps=int(n))
+
+
 def contraction_roofline(net, passes, lt=None, note=""):
     """Roofline of a net's Convolution / InnerProduct forward contractions
     (the dominant kernels): algorithmic FLOPs per forward pass from
@@ -218,12 +228,7 @@ def run_workload(args, world, rank, dev):
         for k in range(len(names)):
             acc += [sum(r[k] for r in rows), sum(r[k] * r[k] for r in rows)]
         tot_m = allreduce_stats(acc + [len(rows)], dev)
-        per_output = {}
-        nm = max(tot_m[-1], 1)
-        for k, name in enumerate(names):
-            mean = tot_m[2 * k] / nm
-            var = max(tot_m[2 * k + 1] / nm - mean * mean, 0.0) * nm / max(nm - 1, 1)
-            per_output[name] = dict(mean=mean, std=var ** 0.5, ci95=1.96 * (var / nm) ** 0.5, maps=int(tot_m[-1]))
+        per_output = {name: map_statistics(tot_m[2 * k], tot_m[2 * k + 1], tot_m[-1]) for k, name in enumerate(names)}
         # the contraction table: events around every conv / IP layer over K
         # further maps after the timed region (the maps run eager while timed)
         net.layer_times(reset=True)
