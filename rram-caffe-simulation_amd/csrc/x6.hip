@@ -2211,6 +2211,9 @@ struct CbPlan {
   X(3, 4, 8, 15, 1) X(3, 4, 4, 8, 1) X(3, 4, 4, 12, 1) X(3, 2, 4, 12, 1) X(3, 2, 4, 14, 1)
 // (a 64 x 256 form for conv4 does not fit two per CU: its contiguous patch
 // spans up to 27 rows = 9 LDS pieces, the per-image one wastes a third)
+// (128 x 64 tiles for conv5, whose 676 128 x 128 workgroups leave the second
+// of two rounds a third full, measured slower: 0.180-0.183 vs 0.166-0.168 ms,
+// profiles/r05_ab_conv5_n64.txt)
 #define RRAM_CB16_LIST(X) X(5, 4, 4, 8, 2) X(3, 4, 4, 8, 2) X(3, 2, 2, 8, 2)
 bool cb_instantiated(int KH, int WR, int NB, int PD, int OCC = 1) {
 #define RRAM_X(kh, wr, nb, pd, occ) \
