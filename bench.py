@@ -317,8 +317,9 @@ def main():
                             "frac": round(inj_gbps / HBM_PEAK_GBPS, 4),
                             "traffic": traffic.get("inject", {}).get("bytes_per_launch"),
                             "algorithmic_bytes_per_launch": 8 * inj_w, "avg_us_per_launch": round(inj_ms_per * 1e3, 2),
-                            "note": ("launched on a side stream, overlapped with conv1-5 of the same map "
-                                     "(RRAM_MC_OVERLAP=1; they share the CUs, so the launch stretches)"
+                            "note": ("launched on a side stream after conv2, overlapped with norm2 / pool2 / "
+                                     "conv3-5 of the same map (RRAM_MC_OVERLAP=1; they share the CUs, so the "
+                                     "launch stretches)"
                                      if os.environ.get("RRAM_MC_OVERLAP", "0") == "1" else
                                      "serial: each map's injection runs alone before its forward")},
         "traffic_source": traffic.get("source"),

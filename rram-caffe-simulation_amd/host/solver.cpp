@@ -766,16 +766,27 @@ MonteCarlo<Dtype>::MonteCarlo(std::shared_ptr<Net<Dtype>> net, const std::vector
   const auto& fl = net_->failure_learnable_layer_ids();
   first_fault_layer_ = *std::min_element(fl.begin(), fl.end());
   // RRAM_MC_OVERLAP=1 runs each map's injection on a side stream under the
-  // layers before the first faultable one.  Off by default since the
-  // persistent conv1 kernel holds every CU for its whole run (one 160 KB-LDS
-  // workgroup per CU): the injection then only finds room under pool1 / conv2
-  // and stretches to ~480 us, and the serial order measured the same maps/s
-  // (106.3-106.5k vs 104.5-105.5k overlapped, profiles/r03_ab_mc_overlap.txt;
-  // round 2's +0.1..2.4 % came from the non-persistent conv1 kernel)
+  // layers before the first faultable one, released after the second
+  // convolution (the persistent conv1 kernel holds every CU; conv2, the
+  // dominant kernel, keeps the chip to itself) on a 256-block grid.  Off by
+  // default: the injection shares the CUs with norm2 / pool2 / conv3 and
+  // stretches from 89 to ~310 us, conv3 from 0.303 to 0.375 ms, and the live
+  // bench measured serial 0.2-1.1 % ahead (profiles/r05_ab_mc_overlap.txt;
+  // with per-layer events the overlap had led by 1.2 %).  The graph replay
+  // (set_graph) is serial either way.
   {
     const char* e = getenv("RRAM_MC_OVERLAP");
     overlap_ = e && atoi(e) == 1 && first_fault_layer_ > 0;
   }
+#ifndef RRAM_MC_RELEASE_AFTER_CONV
+#define RRAM_MC_RELEASE_AFTER_CONV 2
+#endif
+  release_after_ = -1;  // no such convolution: the injection starts with the prefix
+  for (int i = 0, n = 0; RRAM_MC_RELEASE_AFTER_CONV && i < first_fault_layer_ - 1; ++i)
+    if (std::string(net_->layers()[i]->type()) == "Convolution" && ++n == RRAM_MC_RELEASE_AFTER_CONV) {
+      release_after_ = i;
+      break;
+    }
   // between maps only the injection rewrites weights: the convolutions keep
   // their packed weights (Net::set_weight_pack_cache) unless a faultable blob
   // is theirs (the conv-fault extension), which every map's mutable access
@@ -943,7 +954,7 @@ void MonteCarlo<Dtype>::map_body(bool dev_state, uint32_t m) {
 
 template <typename Dtype>
 void MonteCarlo<Dtype>::Run(uint32_t map_begin, uint32_t map_count) {
-  if (graph_ && !overlap_ && !reuse_prefix_ && !timing_ && !net_->timing_on() && map_count > 0) {
+  if (graph_ && !reuse_prefix_ && !timing_ && !net_->timing_on() && map_count > 0) {
     GraphStreamScope sc(gstream_);
     hipStream_t st = Caffe::hip_stream();
     HIP_CALL(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_state_), static_cast<int>(map_begin), 1, st));
@@ -989,10 +1000,12 @@ void MonteCarlo<Dtype>::Run(uint32_t map_begin, uint32_t map_count) {
     segs[i] = rram_inject_seg{clean_[i], params_[i]->mutable_gpu_data(), params_[i]->count(), (uint32_t)i, 0, cfgs_[i]};
   const size_t no = outs_.size();
   const int L = static_cast<int>(net_->layers().size());
-  // overlapped, the injection gets a 512-block grid: it then holds fewer CUs
-  // while conv1 runs beside it (conv1 0.400 -> 0.386 ms, +0.9 % maps/s;
-  // profiles/r02_ab_mc_overlap.txt); serial, the default 2048
-  const int prev_grid = rram_set_inject_grid(overlap_ ? 512 : 0);
+  // overlapped, the injection gets a 256-block grid (it shares the CUs);
+  // serial, the default 2048
+#ifndef RRAM_MC_OVERLAP_GRID
+#define RRAM_MC_OVERLAP_GRID 256
+#endif
+  const int prev_grid = rram_set_inject_grid(overlap_ && !reuse_prefix_ ? RRAM_MC_OVERLAP_GRID : 0);
   // the statistics folded into the layers that store each scalar output
   // (Layer::set_top_accumulator): no rram_mc_accumulate launch per map when
   // every output's producer takes it (all or none)
@@ -1035,6 +1048,8 @@ void MonteCarlo<Dtype>::Run(uint32_t map_begin, uint32_t map_count) {
     const bool skip_prefix = reuse_prefix_ && prefix_done_ && first_fault_layer_ > 0;
     const bool overlap = overlap_ && !skip_prefix;
     if (overlap) {
+      // released after the second convolution (see the constructor)
+      if (release_after_ >= 0) net_->ForwardFromTo(0, release_after_, false);
       HIP_CALL(hipEventRecord(ev_free_, Caffe::hip_stream()));  // previous map's forward is done with the weights
       HIP_CALL(hipStreamWaitEvent(side_, ev_free_, 0));
       is = side_;
@@ -1047,7 +1062,7 @@ void MonteCarlo<Dtype>::Run(uint32_t map_begin, uint32_t map_count) {
     if (timing_) timer_.stop(0, is);
     if (overlap) {
       HIP_CALL(hipEventRecord(ev_injected_, side_));
-      net_->ForwardFromTo(0, first_fault_layer_ - 1, false);  // the layers before the first faultable one run under the injection
+      net_->ForwardFromTo(release_after_ + 1, first_fault_layer_ - 1, false);  // the rest of the prefix runs under the injection
       HIP_CALL(hipStreamWaitEvent(Caffe::hip_stream(), ev_injected_, 0));
       net_->ForwardFromTo(first_fault_layer_, L - 1, false);
     } else if (skip_prefix) {

@@ -347,6 +347,7 @@ class MonteCarlo {
   // previous map's forward (ev_free_)
   bool overlap_ = true;
   int first_fault_layer_ = 0;
+  int release_after_ = -1;  // overlapped maps: the prefix layer after which the injection starts
   hipStream_t side_ = nullptr;
   hipEvent_t ev_free_ = nullptr, ev_injected_ = nullptr;
   Dtype* d_sums_ = nullptr;       // [n_outputs]
