@@ -679,6 +679,53 @@ __global__ void k_count_valid(const float* __restrict__ label, int64_t n, int ig
   }
 }
 
+// accuracy_layer.cpp:48-90 for one (outer, inner) column xs (stride inner),
+// lanes over classes: hit = the label's (value, index) pair is within the
+// top_k of the descending pair order, cnt = the label is not ignored.  For
+// C <= 1024 the class values are loaded 16 per lane before the label (a
+// strided loop waited one memory latency per 64 classes, and the label's own
+// value one more behind the label: 10 us for a 256 x 1000 head) and the
+// label's value is taken from the lane holding it; integer counts, so the
+// result is the loop's whatever the order.
+__device__ __forceinline__ void label_hit(const float* __restrict__ xs, int64_t inner, int C,
+                                          const float* __restrict__ lab, int ignore, int top_k, int lane, int& hit,
+                                          int& cnt) {
+  constexpr int R = 16;
+  int rank = 0;
+  if (C <= 64 * R) {
+    float u[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int c = lane + 64 * i;
+      u[i] = c < C ? xs[(int64_t)c * inner] : 0.0f;
+    }
+    const int lv = static_cast<int>(*lab);
+    if (ignore >= 0 && lv == ignore) return;
+    float mine = 0.0f;  // lv is wave-uniform
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+      if (i == (lv >> 6)) mine = u[i];
+    const float v = (lv >= 0 && lv < C) ? __shfl(mine, lv & 63, 64) : xs[(int64_t)lv * inner];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int c = lane + 64 * i;
+      rank += c < C && ((u[i] > v) || (u[i] == v && c > lv));
+    }
+  } else {
+    const int lv = static_cast<int>(*lab);
+    if (ignore >= 0 && lv == ignore) return;
+    const float v = xs[(int64_t)lv * inner];
+    for (int c = lane; c < C; c += 64) {
+      const float u = xs[(int64_t)c * inner];
+      rank += (u > v) || (u == v && c > lv);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) rank += __shfl_xor(rank, off, 64);
+  hit = rank < top_k;
+  cnt = 1;
+}
+
 // accuracy_layer.cpp:48-90: label counted correct when its (value, index)
 // pair is within the top_k of the descending pair order.  One wave per
 // (outer, inner) column (lanes over classes), many blocks; the per-block
@@ -693,20 +740,7 @@ __global__ void __launch_bounds__(256) k_accuracy(const float* __restrict__ x, c
   int hit = 0, cnt = 0;
   if (col < cols) {
     const int64_t o = col / inner, q = col - o * inner;
-    const int lv = static_cast<int>(label[col]);
-    if (!(ignore >= 0 && lv == ignore)) {
-      const float* xs = x + o * C * inner + q;
-      const float v = xs[(int64_t)lv * inner];
-      int rank = 0;  // #classes ahead of the label in Caffe's (value, index) descending order
-      for (int c = lane; c < C; c += 64) {
-        const float u = xs[(int64_t)c * inner];
-        rank += (u > v) || (u == v && c > lv);
-      }
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) rank += __shfl_xor(rank, off, 64);
-      hit = rank < top_k;
-      cnt = 1;
-    }
+    label_hit(x + o * C * inner + q, inner, C, label + col, ignore, top_k, lane, hit, cnt);
   }
   if (lane == 0) {
     sa[wave] = hit;
@@ -741,20 +775,7 @@ __global__ void __launch_bounds__(256) k_accuracy_fused(const float* __restrict_
   int hit = 0, cnt = 0;
   if (col < cols) {
     const int64_t o = col / inner, q = col - o * inner;
-    const int lv = static_cast<int>(label[col]);
-    if (!(ignore >= 0 && lv == ignore)) {
-      const float* xs = x + o * C * inner + q;
-      const float v = xs[(int64_t)lv * inner];
-      int rank = 0;  // #classes ahead of the label in Caffe's (value, index) descending order
-      for (int c = lane; c < C; c += 64) {
-        const float u = xs[(int64_t)c * inner];
-        rank += (u > v) || (u == v && c > lv);
-      }
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) rank += __shfl_xor(rank, off, 64);
-      hit = rank < top_k;
-      cnt = 1;
-    }
+    label_hit(x + o * C * inner + q, inner, C, label + col, ignore, top_k, lane, hit, cnt);
   }
   if (lane == 0) {
     sa[wave] = hit;
