@@ -2684,10 +2684,18 @@ bool gemm_x6_plan(int M, int N, int K, size_t ws_bytes, GemmPlan& pl) {
   pl.ktiles = (K + gx6::KT - 1) / gx6::KT;
   // split-K toward 256 workgroups, >= 8 K-tiles (256 k) per split
   const int64_t tiles = (int64_t)pl.tiles_m * pl.tiles_n;
+// (32 splits of >= 4 K-tiles, which moves fc8 onto this kernel, measured
+// 0.034 vs 0.032 ms on the fp32 engine: profiles/r05_ab_fc8_split32.txt)
+#ifndef RRAM_X6_SPLIT_MAX
+#define RRAM_X6_SPLIT_MAX 16
+#endif
+#ifndef RRAM_X6_MIN_KT
+#define RRAM_X6_MIN_KT 8
+#endif
   int split = 1;
   if (ws_bytes > 0 && tiles < 256) {
-    split = static_cast<int>(std::min<int64_t>(16, 256 / tiles));
-    while (split > 1 && pl.ktiles / split < 8) --split;
+    split = static_cast<int>(std::min<int64_t>(RRAM_X6_SPLIT_MAX, 256 / tiles));
+    while (split > 1 && pl.ktiles / split < RRAM_X6_MIN_KT) --split;
     while (split > 1 && (size_t)split * M * N * sizeof(float) > ws_bytes) --split;
   }
   pl.ktc = (pl.ktiles + split - 1) / split;
