@@ -742,13 +742,14 @@ def test_im2col_col2im_vs_oracle(device, oracle_mod):
 # ---------------------------------------------------------- support layers
 @pytest.mark.parametrize("outer,C,inner,ignore", [(100, 10, 1, -1), (7, 10, 5, 3), (64, 64, 1, -1), (1, 2, 1, -1),
                                                   (256, 1000, 1, -1), (50, 1000, 1, 7), (3, 100, 50, -1),
-                                                  (20000, 100, 1, -1)])
+                                                  (20000, 100, 1, -1), (6, 1500, 2, 4)])
 def test_accuracy_small_head_single_launch(device, oracle_mod, outer, C, inner, ignore):
     """Accuracy == the restated AccuracyLayer, with ties, an ignore label,
     spatial positions, and the ratio output (top-1 and top-3), twice per case:
     the one-block kernel (classes <= 64), the single-launch multi-block kernel
     (per-block slots + last-block sum; its ticket re-arms itself, so the
-    second call must agree), and past 4096 blocks the atomics + ratio form."""
+    second call must agree), and past 4096 blocks the atomics + ratio form;
+    C = 1500 takes the strided-loop branch (class values batched up to 1024)."""
     import torch
     from rramsim import ops
     rng = np.random.default_rng(outer + C)
