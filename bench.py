@@ -156,11 +156,19 @@ def main():
     # under torch.distributed.run the process group exists at every world
     # size (N = 1 included), so the collectives below are the ones N > 1 runs
     distributed = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ
+    comm = None
     if distributed:
+        # torch.distributed is the rendezvous only (gloo over TCP on the host):
+        # with RCCL (the default) every collective of the job -- the timing
+        # barriers, the max-over-ranks time, the statistics and the training
+        # gradients -- runs on the C++ host's own RCCL communicator
+        # (caffe.Comm / P2PSync, host/parallel.cpp); RRAM_BENCH_DIST_BACKEND=gloo
+        # (test hook, ranks sharing one GPU) keeps them on torch's gloo
+        dist.init_process_group("gloo")
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
+            from rramsim import parallel
+            comm = caffe.Comm(rank, world)
+            parallel.set_comm(comm)
     if os.environ.get("RRAM_BENCH_STREAM") == "1":   # A/B runs: a created stream instead of the NULL stream
         torch.cuda.set_stream(torch.cuda.Stream())
     caffe.set_stream_from_torch()
@@ -171,8 +179,7 @@ def main():
         res = run_workload(args, world, rank, dev)
         if rank == 0:
             print(json.dumps(res), flush=True)
-        if distributed:
-            dist.destroy_process_group()
+        _finish(comm, distributed)
         return
 
     net = caffe.Net(models.alexnet(test_batch=args.batch), "test", models.net_options("alexnet"))
@@ -200,8 +207,10 @@ def main():
         net.set_timing(0)
     mc.set_timing(True)
 
-    stats = torch.zeros(8, dtype=torch.float64, device=dev)
-    if distributed:
+    stats = torch.zeros(8, dtype=torch.float64)
+    if comm is not None:
+        comm.barrier()
+    elif distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -212,15 +221,21 @@ def main():
     net.set_timing(False)
     mc.set_timing(False)
     st = mc.stats()
-    vals = st["sums"] + [float(sum(st["broken"])), float(st["maps"])]
+    if comm is not None:
+        # one RCCL all-reduce of [output sums, broken cells, maps] from the C++ host
+        vals = comm.mc_stats(mc)
+        elapsed = comm.allreduce_host([elapsed], "max")[0]
+        comm.barrier()
+    else:
+        vals = st["sums"] + [float(sum(st["broken"])), float(st["maps"])]
+        if distributed:
+            t = torch.tensor(vals + [elapsed], dtype=torch.float64)
+            dist.all_reduce(t[:len(vals)])             # gloo rehearsal: accuracy / loss / broken-cell sums
+            dist.all_reduce(t[len(vals):], op=dist.ReduceOp.MAX)
+            dist.barrier()
+            vals, elapsed = t[:len(vals)].tolist(), float(t[-1].item())
     stats[:len(vals)] = torch.tensor(vals, dtype=torch.float64)
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if distributed:
-        dist.all_reduce(stats)                     # RCCL: accuracy / loss / broken-cell sums
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.barrier()
     torch.cuda.synchronize()
-    elapsed = float(t.item())
 
     # ---- roofline of the dominant kernel: live hipEvents of the timed region
     lt_timed = net.layer_times(reset=True)
@@ -286,7 +301,9 @@ def main():
                    "model": "AlexNet (bvlc_alexnet train_val, TEST)",
                    "global_batch": args.batch * world, "batch_per_map": args.batch, "maps_per_step": world,
                    "p_fault": args.p_fault, "stuck_split_neg_zero_pos": [10, 20, 10],
-                   "fault_layers": "InnerProduct (58,631,144 weights)", "parallelism": (f"mc-maps x{world} ({'RCCL' if backend == 'nccl' else backend} stats all-reduce)"
+                   "fault_layers": "InnerProduct (58,631,144 weights)",
+                   "parallelism": (f"mc-maps x{world} (RCCL stats all-reduce from the C++ host, rram_mc_allreduce_stats)"
+                                   if comm is not None else f"mc-maps x{world} (torch {backend} stats all-reduce)"
                                    if distributed else "mc-maps x1 (single process, no collective)"),
                    "f32_engine": "bf16x6 (exact 3-term bf16 split, 6 products, fp32 accumulation)"
                    if "bf16x6" in engines.values() else "f32 MFMA"},
@@ -334,6 +351,15 @@ def main():
         print(json.dumps(res), flush=True)
     mc.close()
     net.close()
+    _finish(comm, distributed)
+
+
+def _finish(comm, distributed):
+    import torch.distributed as dist
+    if comm is not None:
+        from rramsim import parallel
+        parallel.set_comm(None)
+        comm.close()
     if distributed:
         dist.destroy_process_group()
 

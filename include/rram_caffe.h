@@ -257,6 +257,64 @@ int rram_mc_set_graph(rram_mc_t mc, int enable);
 int rram_mc_graph_active(rram_mc_t mc, int* active);
 int rram_mc_inject_times(rram_mc_t mc, double* ms, long* launches, int64_t* weights, int reset);
 
+/* ------------------------------------------------------ multi-GPU (RCCL)
+ * The reference's P2PSync (include/caffe/parallel.hpp; src/caffe/parallel.cpp:
+ * 201-437; tools/caffe.cpp:247-249 `P2PSync<float> sync(solver, NULL, param);
+ * sync.Run(gpus)`), rebuilt for one process per GPU over RCCL (xGMI).  Each
+ * rank creates a communicator from one 128-byte id (rram_comm_unique_id on one
+ * rank, handed to the others by the caller: a file, MPI, a TCP store) after
+ * selecting its device, then attaches it to its solver with rram_dp_create.
+ * librram_caffe.so links librccl.so.1 (the RCCL of the ROCm install, or the one
+ * already loaded in the process). */
+typedef struct rram_comm_s* rram_comm_t;
+typedef struct rram_dp_s* rram_dp_t;
+#define RRAM_COMM_ID_BYTES 128
+/* ncclGetUniqueId: id[RRAM_COMM_ID_BYTES] */
+int rram_comm_unique_id(unsigned char* id);
+/* ncclCommInitRank on the calling thread's current device (collective: every
+ * rank of the world calls it with the same id) */
+int rram_comm_create(const unsigned char* id, int rank, int world, rram_comm_t* out);
+int rram_comm_destroy(rram_comm_t c);
+int rram_comm_info(rram_comm_t c, int* rank, int* world);
+/* in-place sum all-reduce of n device floats, asynchronous on the calling
+ * thread's rram_caffe_set_stream stream */
+int rram_comm_allreduce_f32(rram_comm_t c, float* buf, int64_t n);
+/* in-place all-reduce of n host doubles (op 0 = sum, 1 = max); synchronous */
+int rram_comm_allreduce_host_f64(rram_comm_t c, double* vals, int n, int op);
+int rram_comm_barrier(rram_comm_t c);
+/* P2PSync: broadcasts the solver's parameters from rank 0 now (on_start,
+ * parallel.cpp:286-322) and installs the on_gradients_ready hook: the flat
+ * gradient buffer (every learnable param aliased into one allocation, the
+ * GPUParams layout of parallel.cpp:25-115) is sum-all-reduced and scaled by
+ * 1/world (parallel.cpp:324-380) every iteration of rram_solver_step /
+ * rram_solver_solve.  overlap != 0 (world > 1, iter_size 1): gradients are
+ * reduced in buckets of >= bucket_mb MB started from the per-layer backward
+ * hook on a collective stream while earlier layers still run backward; the
+ * update waits for them.  Replaces rram_solver_set_gradient_callback /
+ * _backward_callback while attached; destroy before the solver. */
+int rram_dp_create(rram_solver_t s, rram_comm_t c, double bucket_mb, int overlap, rram_dp_t* out);
+/* the solver's flat learnable data / diff buffers (device pointers, *n
+ * floats each; NULL / 0 when the `flat_params: false` option disabled them) */
+int rram_solver_flat_params(rram_solver_t s, float** data, float** diff, int64_t* n);
+int rram_dp_destroy(rram_dp_t dp);
+/* counters: all-reduce rounds (iterations), bucket all-reduces, planned
+ * buckets, flat parameter count (nullable outputs) */
+int rram_dp_info(rram_dp_t dp, long long* allreduce_calls, long long* bucket_calls, int* buckets, int64_t* params);
+/* Host-only (no device): the bucket plan rram_dp_create uses for overlap.
+ * nranges[i] [begin, end) flat ranges of layer i's learnable params, packed
+ * in `ranges` (2 int64 each, layers in forward order); outputs the buckets in
+ * backward order: after layer layer_out[k]'s Backward, all-reduce
+ * [lo_out[k], hi_out[k]); the prefix left over goes in on_gradients_ready.
+ * *n = 0 when the ranges do not tile the buffer in layer order (shared
+ * params).  Needs cap >= the bucket count. */
+int rram_dp_plan_buckets(int nlayers, const int* nranges, const int64_t* ranges, int64_t bucket_elems,
+                         int* layer_out, int64_t* lo_out, int64_t* hi_out, int cap, int* n);
+/* Monte-Carlo job statistics over every rank (map m on rank m mod world):
+ * out[0 .. n_outputs) = the output sums, out[n_outputs] = broken cells summed
+ * over blobs, out[n_outputs + 1] = maps run, each summed over ranks with one
+ * RCCL all-reduce (fp64).  *n = n_outputs + 2 (needs cap >= *n). */
+int rram_mc_allreduce_stats(rram_mc_t mc, rram_comm_t c, double* out, int cap, int* n);
+
 #ifdef __cplusplus
 }
 #endif

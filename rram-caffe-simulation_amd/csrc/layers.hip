@@ -1020,7 +1020,9 @@ int rram_pool_relu_bwd(const float* dy, const int* mask, float* dx, int num, int
   RRAM_REQUIRE_I32(total, "layer kernel");
   if (total == 0) return RRAM_OK;
   RRAM_REQUIRE(dy && dx, "pool_bwd: NULL");
-  if (method == RRAM_POOL_MAX && H * W <= kBwdPlaneMax && PH * PW <= 1024 && (int64_t)num * C < (1ll << 31)) {
+  // plane path: one 256-thread block per (n, c) plane; the grid's work-item
+  // count (num * C * 256) must stay a 32-bit value, else the grid-stride form
+  if (method == RRAM_POOL_MAX && H * W <= kBwdPlaneMax && PH * PW <= 1024 && (int64_t)num * C <= (1ll << 24)) {
     hipLaunchKernelGGL(k_pool_bwd_plane, dim3(static_cast<unsigned>(num * C)), dim3(256), 0, as_stream(s), dy, mask,
                        dx, H, W, PH, PW, make_fastdivi(W), kh, kw, sh, sw, ph, pw, relu_y, relu_slope);
     return launch_status("pool_bwd");
@@ -1093,7 +1095,7 @@ int rram_lrn_within_relu_bwd_core(const float* x, const float* scale, const floa
   RRAM_REQUIRE_I32(total, "layer kernel");
   if (total == 0) return RRAM_OK;
   RRAM_REQUIRE(x && scale && dy && dx, "lrn_within_bwd: NULL");
-  if (H * W <= kBwdPlaneMax && (int64_t)num * C < (1ll << 31)) {
+  if (H * W <= kBwdPlaneMax && (int64_t)num * C <= (1ll << 24)) {  // num * C * 256 work-items fit 32 bits
     hipLaunchKernelGGL(k_lrn_within_bwd_plane, dim3(static_cast<unsigned>(num * C)), dim3(256), 0, as_stream(s), x,
                        scale, dy, dx, H, W, make_fastdivi(W), size, alpha, beta, relu, slope);
     return launch_status("lrn_within_bwd");

@@ -7,6 +7,7 @@
 
 #include "rram_caffe.h"
 #include "hdf5.hpp"
+#include "parallel.hpp"
 #include "solver.hpp"
 
 using namespace caffe;
@@ -30,6 +31,12 @@ struct rram_mc_s {
 };
 struct rram_syncedmem_s {
   std::unique_ptr<SyncedMemory> mem;
+};
+struct rram_comm_s {
+  std::shared_ptr<Comm> comm;
+};
+struct rram_dp_s {
+  std::unique_ptr<P2PSync<float>> sync;
 };
 
 static thread_local std::string g_caffe_err;
@@ -247,8 +254,11 @@ int rram_net_blob(rram_net_t n, const char* name, float** data, float** diff, in
     NEED(name);
     auto b = n->net->blob_by_name(name);
     if (!b) throw Error(std::string("Unknown blob name ") + name);
-    n->net->materialize_blob(b.get());  // a folded Concat bottom holds its output again
     if (data) {
+      // only a data read undoes the blob's folds (a folded Concat bottom /
+      // pooled output holds its fp32 values again); diff- or shape-only
+      // queries leave the TEST-phase folds in place
+      n->net->materialize_blob(b.get());
       *data = b->mutable_gpu_data();
       b->data()->expose();  // the caller may write a new batch through it unseen
     }
@@ -785,6 +795,140 @@ int rram_mc_stats(rram_mc_t m, double* sums, int sums_cap, int* n_out, unsigned 
     for (int i = 0; sums && i < (int)o.size() && i < sums_cap; ++i) sums[i] = o[i];
     for (int i = 0; broken && i < (int)b.size() && i < bcap; ++i) broken[i] = b[i];
     for (int i = 0; per_map && i < (int)pm.size() && i < pcap; ++i) per_map[i] = pm[i];
+  });
+}
+
+
+// ------------------------------------------------------------ multi-GPU
+int rram_comm_unique_id(unsigned char* id) {
+  return guarded([&] {
+    NEED(id);
+    Comm::unique_id(id);
+  });
+}
+int rram_comm_create(const unsigned char* id, int rank, int world, rram_comm_t* out) {
+  return guarded([&] {
+    NEED(id);
+    NEED(out);
+    auto* c = new rram_comm_s;
+    try {
+      c->comm = std::make_shared<Comm>(id, rank, world);
+    } catch (...) {
+      delete c;
+      throw;
+    }
+    *out = c;
+  });
+}
+int rram_comm_destroy(rram_comm_t c) {
+  return guarded([&] { delete c; });
+}
+int rram_comm_info(rram_comm_t c, int* rank, int* world) {
+  return guarded([&] {
+    NEED(c);
+    if (rank) *rank = c->comm->rank();
+    if (world) *world = c->comm->world();
+  });
+}
+int rram_comm_allreduce_f32(rram_comm_t c, float* buf, int64_t n) {
+  return guarded([&] {
+    NEED(c);
+    if (n > 0) NEED(buf);
+    c->comm->allreduce_f32(buf, n, Caffe::hip_stream());
+  });
+}
+int rram_comm_allreduce_host_f64(rram_comm_t c, double* vals, int n, int op) {
+  return guarded([&] {
+    NEED(c);
+    if (n > 0) NEED(vals);
+    c->comm->allreduce_host_f64(vals, n, op);
+  });
+}
+int rram_comm_barrier(rram_comm_t c) {
+  return guarded([&] {
+    NEED(c);
+    c->comm->barrier();
+  });
+}
+int rram_dp_create(rram_solver_t s, rram_comm_t c, double bucket_mb, int overlap, rram_dp_t* out) {
+  return guarded([&] {
+    NEED(s);
+    NEED(c);
+    NEED(out);
+    CAFFE_CHECK(bucket_mb > 0, "rram_dp_create: bucket_mb must be > 0");
+    // the sync owns both hooks while attached
+    s->grad_cb = nullptr;
+    s->bwd_cb = nullptr;
+    s->solver->on_gradients_ready = nullptr;
+    s->solver->net()->on_backward_layer = nullptr;
+    auto* d = new rram_dp_s;
+    try {
+      d->sync = std::make_unique<P2PSync<float>>(s->solver.get(), c->comm, bucket_mb, overlap != 0);
+    } catch (...) {
+      delete d;
+      throw;
+    }
+    *out = d;
+  });
+}
+int rram_solver_flat_params(rram_solver_t s, float** data, float** diff, int64_t* n) {
+  return guarded([&] {
+    NEED(s);
+    float* d = s->solver->flat_data();
+    if (data) *data = d;
+    if (diff) *diff = s->solver->flat_diff();
+    if (n) *n = d ? s->solver->net()->flat_param_count() : 0;
+  });
+}
+int rram_dp_destroy(rram_dp_t dp) {
+  return guarded([&] { delete dp; });
+}
+int rram_dp_info(rram_dp_t dp, long long* allreduce_calls, long long* bucket_calls, int* buckets, int64_t* params) {
+  return guarded([&] {
+    NEED(dp);
+    if (allreduce_calls) *allreduce_calls = dp->sync->allreduce_calls();
+    if (bucket_calls) *bucket_calls = dp->sync->bucket_calls();
+    if (buckets) *buckets = dp->sync->buckets();
+    if (params) *params = dp->sync->params();
+  });
+}
+int rram_dp_plan_buckets(int nlayers, const int* nranges, const int64_t* ranges, int64_t bucket_elems,
+                         int* layer_out, int64_t* lo_out, int64_t* hi_out, int cap, int* n) {
+  return guarded([&] {
+    NEED(n);
+    CAFFE_CHECK(nlayers >= 0 && bucket_elems > 0, "rram_dp_plan_buckets: bad arguments");
+    if (nlayers > 0) NEED(nranges);
+    std::vector<std::vector<std::pair<int64_t, int64_t>>> rs(nlayers);
+    int k = 0;
+    for (int i = 0; i < nlayers; ++i)
+      for (int j = 0; j < nranges[i]; ++j, ++k) rs[i].push_back({ranges[2 * k], ranges[2 * k + 1]});
+    const auto plan = plan_buckets(rs, bucket_elems);
+    *n = static_cast<int>(plan.size());
+    CAFFE_CHECK(cap >= *n || plan.empty(), "rram_dp_plan_buckets: cap " << cap << " < " << *n);
+    for (size_t b = 0; b < plan.size(); ++b) {
+      if (layer_out) layer_out[b] = plan[b].first;
+      if (lo_out) lo_out[b] = plan[b].second.first;
+      if (hi_out) hi_out[b] = plan[b].second.second;
+    }
+  });
+}
+int rram_mc_allreduce_stats(rram_mc_t m, rram_comm_t c, double* out, int cap, int* n) {
+  return guarded([&] {
+    NEED(m);
+    NEED(c);
+    NEED(out);
+    std::vector<double> o;
+    std::vector<unsigned long long> b;
+    std::vector<float> pm;
+    m->mc->Stats(o, b, pm);
+    unsigned long long broken = 0;
+    for (auto x : b) broken += x;
+    o.push_back(static_cast<double>(broken));
+    o.push_back(static_cast<double>(m->mc->maps_run()));
+    if (n) *n = static_cast<int>(o.size());
+    CAFFE_CHECK(cap >= static_cast<int>(o.size()), "rram_mc_allreduce_stats: cap " << cap << " < " << o.size());
+    c->comm->allreduce_host_f64(o.data(), static_cast<int>(o.size()), 0);
+    std::copy(o.begin(), o.end(), out);
   });
 }
 

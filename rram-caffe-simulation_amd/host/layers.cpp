@@ -239,6 +239,11 @@ void ConvolutionLayer<Dtype>::Forward_gpu(const std::vector<Blob<Dtype>*>& botto
       xo = buf;
     }
   }
+  // without a companion the kernel reads the fp32 bottom: it must have been
+  // written (a pooled-output fold decided at the producer's forward against
+  // an engine / plan that no longer holds would leave it stale)
+  CAFFE_CHECK(xo != nullptr || !bottom[0]->data()->fp32_stale,
+              this->name() << ": fp32 input unwritten (its producer wrote only the octet companion)");
   const float* bias = bias_term_ ? this->blobs_[1]->gpu_data() : nullptr;
   const size_t wpb = cache_wpack ? rram_conv_weight_pack_bytes(&desc_) : 0;
   if (concat_top_ != nullptr) {

@@ -499,11 +499,17 @@ void Solver<Dtype>::Step(int iters) {
       // the first such iteration runs eager (workspaces and scratch buffers
       // get allocated on the section's stream), the next one captures
       const Dtype rate = rate_now;
-      const bool warm = graph_warm_;
+      bool warm = graph_warm_;
       net_->set_iter((uint64_t)iter_);
       {
         GraphStreamScope sc(gstream_);
-        if (warm && gx_[0] && (rate != graph_rate_ || graph_key() != graph_ptrs_)) drop_graphs();
+        // a changed key means freed / reallocated scratch: this iteration
+        // runs eager again (rebuilding tables, growing buffers outside any
+        // capture) and the next one captures
+        if (warm && gx_[0] && (rate != graph_rate_ || graph_key() != graph_ptrs_)) {
+          drop_graphs();
+          warm = false;
+        }
         auto fb = [&] {
           net_->ClearParamDiffs();
           net_->Forward(false);

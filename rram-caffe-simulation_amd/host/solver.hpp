@@ -237,6 +237,10 @@ class Solver {
   // Bit-identical to the eager iterations.
   void set_graph(bool on);
   bool graph_active() const { return gx_[0] != nullptr; }
+  // the flat learnable data / diff buffers every param is aliased into
+  // (nullptr when the `flat_params: false` option turned them off)
+  Dtype* flat_data() const { return static_cast<Dtype*>(flat_); }
+  Dtype* flat_diff() const { return flat_ ? static_cast<Dtype*>(flat_) + net_->flat_param_count() : nullptr; }
 
  protected:
   bool graph_ = false, graph_warm_ = false;

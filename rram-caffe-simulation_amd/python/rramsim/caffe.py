@@ -103,6 +103,19 @@ SIGNATURES = {
     "rram_mc_reset": (I, [P]),
     "rram_mc_restore_clean": (I, [P]),
     "rram_mc_stats": (I, [P, C.POINTER(C.c_double), I, PI, C.POINTER(C.c_ulonglong), I, PI, PF, I, PI]),
+    "rram_comm_unique_id": (I, [C.c_char_p]),
+    "rram_comm_create": (I, [C.c_char_p, I, I, PP]),
+    "rram_comm_destroy": (I, [P]),
+    "rram_comm_info": (I, [P, PI, PI]),
+    "rram_comm_allreduce_f32": (I, [P, P, I64]),
+    "rram_comm_allreduce_host_f64": (I, [P, C.POINTER(C.c_double), I, I]),
+    "rram_comm_barrier": (I, [P]),
+    "rram_dp_create": (I, [P, P, C.c_double, I, PP]),
+    "rram_dp_destroy": (I, [P]),
+    "rram_dp_info": (I, [P, C.POINTER(C.c_longlong), C.POINTER(C.c_longlong), PI, PI64]),
+    "rram_solver_flat_params": (I, [P, PP, PP, PI64]),
+    "rram_mc_allreduce_stats": (I, [P, P, C.POINTER(C.c_double), I, PI]),
+    "rram_dp_plan_buckets": (I, [I, PI, PI64, I64, PI, PI64, PI64, I, PI]),
 }
 
 _lib = None
@@ -359,7 +372,10 @@ class Net:
         d, g = C.c_void_p(), C.c_void_p()
         shape = (C.c_int * 8)()
         na = C.c_int()
-        check(self._lib.rram_net_blob(self.h, name.encode(), C.byref(d), C.byref(g), shape, C.byref(na)),
+        # ask only for the pointer wanted: a data read materialises folded
+        # blobs (rram_net_blob), a diff read must not undo the folds
+        check(self._lib.rram_net_blob(self.h, name.encode(), None if diff else C.byref(d),
+                                      C.byref(g) if diff else None, shape, C.byref(na)),
               f"blob {name}")
         return _wrap_device((g if diff else d).value, [shape[i] for i in range(na.value)])
 
@@ -548,6 +564,15 @@ class Solver:
         check(self._lib.rram_solver_test(self.h, i, buf, 1024, C.byref(n)), "test")
         return [buf[k] for k in range(n.value)]
 
+    def flat_params(self):
+        """(data, diff) device views of the solver's flat learnable buffers
+        (every param aliased into them, the GPUParams layout), or None."""
+        d, g, n = C.c_void_p(), C.c_void_p(), C.c_int64()
+        check(self._lib.rram_solver_flat_params(self.h, C.byref(d), C.byref(g), C.byref(n)), "solver_flat_params")
+        if not d.value:
+            return None
+        return _wrap_device(d.value, (n.value,)), _wrap_device(g.value, (n.value,))
+
     def set_gradient_callback(self, fn):
         self._cb = CB(lambda _u: fn())
         check(self._lib.rram_solver_set_gradient_callback(self.h, self._cb, None), "set_gradient_callback")
@@ -676,6 +701,106 @@ class MonteCarlo:
     def close(self):
         if self.h:
             self._lib.rram_mc_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Comm:
+    """RCCL communicator of the C++ host (include/rram_caffe.h rram_comm_*):
+    the collective the native P2PSync (rram_dp_*) and the Monte-Carlo stats
+    reduction run on.  Rank 0 draws the 128-byte id; with world > 1 it reaches
+    the other ranks through torch.distributed's rendezvous (plumbing only:
+    broadcast_object_list on the process group, any backend), after which
+    every collective is RCCL called from librram_caffe.so."""
+
+    def __init__(self, rank: int = 0, world: int = 1, group=None):
+        self._lib = load()
+        uid = C.create_string_buffer(128)
+        if rank == 0:
+            check(self._lib.rram_comm_unique_id(uid), "comm_unique_id")
+        if world > 1:
+            import torch.distributed as dist
+            box = [uid.raw if rank == 0 else None]
+            dist.broadcast_object_list(box, src=0, group=group)
+            uid = C.create_string_buffer(box[0], 128)
+        h = C.c_void_p()
+        check(self._lib.rram_comm_create(uid, rank, world, C.byref(h)), "comm_create")
+        self.h, self.rank, self.world = h, rank, world
+
+    def allreduce_host(self, vals, op: str = "sum") -> List[float]:
+        """All-reduce of host doubles (sum | max), synchronous."""
+        buf = (C.c_double * max(len(vals), 1))(*vals)
+        check(self._lib.rram_comm_allreduce_host_f64(self.h, buf, len(vals), {"sum": 0, "max": 1}[op]),
+              "comm_allreduce_host_f64")
+        return [buf[i] for i in range(len(vals))]
+
+    def allreduce_(self, t):
+        """In-place sum all-reduce of a contiguous float32 device tensor on the
+        host runtime's stream (asynchronous)."""
+        assert t.dtype.is_floating_point and t.element_size() == 4 and t.is_contiguous()
+        check(self._lib.rram_comm_allreduce_f32(self.h, C.c_void_p(t.data_ptr()), t.numel()), "comm_allreduce_f32")
+
+    def barrier(self):
+        check(self._lib.rram_comm_barrier(self.h), "comm_barrier")
+
+    def mc_stats(self, mc: "MonteCarlo") -> List[float]:
+        """MonteCarlo statistics summed over every rank: output sums, broken
+        cells, maps (rram_mc_allreduce_stats, one RCCL all-reduce)."""
+        buf = (C.c_double * 64)()
+        n = C.c_int()
+        check(self._lib.rram_mc_allreduce_stats(mc.h, self.h, buf, 64, C.byref(n)), "mc_allreduce_stats")
+        return [buf[i] for i in range(n.value)]
+
+    def close(self):
+        if self.h:
+            self._lib.rram_comm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def dp_plan_buckets(layer_ranges, bucket_elems: int) -> Dict[int, tuple]:
+    """Host-only: the C++ P2PSync's bucket plan (rram_dp_plan_buckets) in the
+    form of rramsim.parallel.plan_buckets: {layer: (begin, end)}."""
+    nr = (C.c_int * max(len(layer_ranges), 1))(*[len(r) for r in layer_ranges])
+    flat = [x for r in layer_ranges for pair in r for x in pair]
+    rr = (C.c_int64 * max(len(flat), 1))(*flat)
+    cap = max(len(layer_ranges), 1)
+    lay, lo, hi, n = (C.c_int * cap)(), (C.c_int64 * cap)(), (C.c_int64 * cap)(), C.c_int()
+    check(load().rram_dp_plan_buckets(len(layer_ranges), nr, rr, bucket_elems, lay, lo, hi, cap, C.byref(n)),
+          "dp_plan_buckets")
+    return {lay[k]: (lo[k], hi[k]) for k in range(n.value)}
+
+
+class P2PSync:
+    """The native data-parallel hooks (rram_dp_*): parameter broadcast from
+    rank 0 now, then per iteration the RCCL all-reduce of the flat gradient
+    buffer + 1/N inside the solver's step (bucketed on a collective stream
+    when overlap is on)."""
+
+    def __init__(self, solver: Solver, comm: Comm, bucket_mb: float = 4.0, overlap: bool = False):
+        self._lib = load()
+        h = C.c_void_p()
+        check(self._lib.rram_dp_create(solver.h, comm.h, float(bucket_mb), int(overlap), C.byref(h)), "dp_create")
+        self.h, self.solver, self.comm = h, solver, comm
+
+    def info(self):
+        a, b, nb, n = C.c_longlong(), C.c_longlong(), C.c_int(), C.c_int64()
+        check(self._lib.rram_dp_info(self.h, C.byref(a), C.byref(b), C.byref(nb), C.byref(n)), "dp_info")
+        return dict(allreduce_calls=a.value, bucket_calls=b.value, buckets=nb.value, params=n.value)
+
+    def close(self):
+        if self.h:
+            self._lib.rram_dp_destroy(self.h)
             self.h = None
 
     def __del__(self):

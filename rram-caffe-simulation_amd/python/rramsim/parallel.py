@@ -1,4 +1,9 @@
-"""Multi-GPU: one process per GPU, torch.distributed over RCCL (xGMI).
+"""Multi-GPU: one process per GPU over RCCL (xGMI).
+
+Two carriers for the same arithmetic: the C++ host's own RCCL communicator
+(`caffe.Comm` + `caffe.P2PSync`, host/parallel.cpp: the product path a C or
+C++ caller of librram_caffe.so gets, and what bench.py uses on GPUs), and
+torch.distributed (gloo: the CPU / shared-GPU rehearsal backend of the tests).
 
 Replaces the reference's P2PSync (src/caffe/parallel.cpp:201-437): instead of
 a thread per GPU with a peer-to-peer tree broadcast of parameters and tree
@@ -18,6 +23,47 @@ from __future__ import annotations
 import os
 import re
 from typing import Dict, List, Optional
+
+
+# The job's RCCL communicator of the C++ host (caffe.Comm), when the caller
+# set one: the statistics / timing collectives below and DataParallelSolver's
+# default then run on it; unset, they run on torch.distributed (gloo rehearsal).
+_COMM = None
+
+
+def set_comm(comm) -> None:
+    global _COMM
+    _COMM = comm
+
+
+def get_comm():
+    return _COMM
+
+
+def _dist_on() -> bool:
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
+
+
+def barrier() -> None:
+    if _COMM is not None:
+        _COMM.barrier()
+    elif _dist_on():
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def allreduce_max(x: float, device) -> float:
+    """max over ranks of one host value (the bench's max-over-ranks time)."""
+    if _COMM is not None:
+        return _COMM.allreduce_host([float(x)], "max")[0]
+    if not _dist_on():
+        return float(x)
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
 
 def world_info():
@@ -73,6 +119,8 @@ def plan_buckets(layer_ranges: List[List[tuple]], n_layers: int, bucket_elems: i
 
 def allreduce_stats(values: List[float], device, group=None) -> List[float]:
     """One all-reduce (sum, fp64) of a small statistics vector."""
+    if _COMM is not None:
+        return _COMM.allreduce_host([float(v) for v in values], "sum")
     import torch
     import torch.distributed as dist
     t = torch.tensor(values, dtype=torch.float64, device=device)
@@ -85,15 +133,25 @@ class DataParallelSolver:
     """Fault-aware data-parallel SGD (C4) on top of caffe.Solver."""
 
     def __init__(self, solver_prototxt: str, net_prototxt: str, options: Optional[Dict] = None, seed: int = 1701,
-                 group=None, log=None, overlap: bool = False, bucket_mb: float = 4.0, shard_hdf5: bool = False):
+                 group=None, log=None, overlap: bool = False, bucket_mb: float = 4.0, shard_hdf5: bool = False,
+                 comm="auto"):
+        """comm: a caffe.Comm -> the native P2PSync (host/parallel.cpp, RCCL
+        from the C++ host); None -> torch.distributed on `group` (gloo
+        rehearsal); "auto" -> the communicator set_comm() installed, else None."""
+        if isinstance(comm, str):
+            comm = _COMM
         import torch
         import torch.distributed as dist
 
         from . import caffe
         self.rank, self.world, local = world_info()
-        if dist.is_available() and dist.is_initialized():
+        if comm is not None:
+            self.rank, self.world = comm.rank, comm.world
+        elif dist.is_available() and dist.is_initialized():
             self.rank, self.world = dist.get_rank(), dist.get_world_size()
         self.group = group
+        self.comm = comm
+        self.sync = None
         caffe.set_stream_from_torch()
         caffe.set_random_seed(seed)            # identical weights and fault maps on every rank
         opts = dict(options or {})
@@ -107,6 +165,16 @@ class DataParallelSolver:
             opts["solver_rank"] = self.rank
             opts["solver_count"] = self.world
         self.solver = caffe.Solver(solver_prototxt, net_prototxt, opts, log=log if self.rank == 0 else None)
+        m = re.search(r"^\s*iter_size\s*:\s*(\d+)", solver_prototxt, re.M)
+        if comm is not None:
+            # the C++ P2PSync: broadcast from rank 0 now, all-reduce + 1/N inside step()
+            self.sync = caffe.P2PSync(self.solver, comm, bucket_mb=bucket_mb, overlap=overlap)
+            flat = self.solver.flat_params()
+            assert flat is not None, "the native P2PSync needs the solver's flat parameter buffers"
+            self.flat_data, self.flat_diff = flat
+            self.overlap = self.sync.info()["buckets"] > 0
+            self.allreduce_calls = self.bucket_calls = 0
+            return
         net = self.solver.net
         n = net.flat_param_count()
         dev = torch.device("cuda", torch.cuda.current_device())
@@ -123,7 +191,6 @@ class DataParallelSolver:
         self._reduced_lo = n
         # iter_size > 1 runs several backward passes per update: only the last
         # one holds the final gradients, so the per-layer buckets stay off
-        m = re.search(r"^\s*iter_size\s*:\s*(\d+)", solver_prototxt, re.M)
         self.overlap = bool(overlap) and self.world > 1 and not (m and int(m.group(1)) > 1)
         if self.overlap:
             self._plan = self._make_plan(net, int(bucket_mb * (1 << 20)) // 4)
@@ -177,10 +244,15 @@ class DataParallelSolver:
 
     def step(self, iters: int):
         self.solver.step(iters)
+        if self.sync is not None:
+            i = self.sync.info()
+            self.allreduce_calls, self.bucket_calls = i["allreduce_calls"], i["bucket_calls"]
 
     @property
     def num_params(self) -> int:
         return self.flat_data.numel()
 
     def close(self):
+        if self.sync is not None:
+            self.sync.close()
         self.solver.close()

@@ -113,8 +113,8 @@ def _timed(world, dev, fn, steps, warmup, net=None):
     if net is not None:
         net.layer_times(reset=True)
         net.set_timing(2)
-    if _dist_on():
-        dist.barrier()
+    from rramsim import parallel
+    parallel.barrier()        # the C++ host's RCCL communicator when bench.py set one, else torch.distributed
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(steps):
@@ -123,10 +123,7 @@ def _timed(world, dev, fn, steps, warmup, net=None):
     el = time.perf_counter() - t0
     if net is not None:
         net.set_timing(0)
-    t = torch.tensor([el], dtype=torch.float64, device=dev)
-    if _dist_on():
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    return parallel.allreduce_max(el, dev)
 
 
 def _base(metric, unit, value, world, args, el, dtype="f32", **cfg):
@@ -299,7 +296,8 @@ def run_workload(args, world, rank, dev):
                     world * args.steps * batch / el, world, args, el, workload=args.workload,
                     model=args.workload.split("_")[0], global_batch=batch * world,
                     parallelism=f"dp{world} (RCCL all-reduce of {dp.num_params} fp32 grads"
-                                f"{', bucketed, overlapped with backward' if dp.overlap else ''})")
+                                f"{', bucketed, overlapped with backward' if dp.overlap else ''}; "
+                                f"{'C++ host P2PSync (librram_caffe RCCL)' if dp.sync is not None else 'torch.distributed ' + dist.get_backend() if _dist_on() else 'no collective'})")
         res["broken_cells"] = sum(dp.solver.broken_counts())
         res["hipgraph"] = dp.solver.graph_active()
         # training roofline over the whole iteration: forward + weight-gradient +

@@ -79,10 +79,10 @@ def test_graph_quantised_lognormal_equals_eager(device):
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
-def _train(graph, iters, lr_policy="fixed", test_batch=20, side_stream=False, **kw):
+def _train(graph, iters, lr_policy="fixed", test_batch=20, side_stream=False, release=False, **kw):
     import contextlib
     import torch
-    from rramsim import caffe, models
+    from rramsim import caffe, models, kernels
     ctx = torch.cuda.stream(torch.cuda.Stream()) if side_stream else contextlib.nullcontext()
     with ctx:
         caffe.set_stream_from_torch()
@@ -94,6 +94,9 @@ def _train(graph, iters, lr_policy="fixed", test_batch=20, side_stream=False, **
         s.set_graph(graph)
         for n in iters:
             s.step(n)
+            if release:                                 # gather tables freed between replays
+                torch.cuda.synchronize()
+                kernels.check(kernels.load().rram_release_caches(), "release_caches")
         ps = [N(p["data"]) for p in s.net.params()]
         hist = [N(h) for h in s.history()]
         fs = s.fail_state()
@@ -117,21 +120,26 @@ def test_graph_training_equals_eager(device, policy):
     assert got[3] == ref[3]
 
 
-@pytest.mark.parametrize("mode", ["test_interval", "display", "average_loss", "side_stream"])
+@pytest.mark.parametrize("mode", ["test_interval", "display", "average_loss", "side_stream", "release_caches"])
 def test_graph_training_interleaved_equals_eager(device, mode):
     """Graph iterations interleaved with the eager work that breaks a replay
     (ADVICE r04): TestAll every 3 iterations on a larger test batch (its
     forward grows the shared workspace / pack buffers the captured launches
     point into: the scratch generation in Solver::graph_key recaptures),
     display iterations (eager), average_loss > 1 (no graph at all), and a
-    non-NULL caller stream (captured directly on it).  Every variant equals
+    non-NULL caller stream (captured directly on it), and the gather tables
+    freed between step() calls (rram_release_caches, ADVICE r05: the changed
+    key drops the graphs and that iteration runs eager, rebuilding the tables
+    outside any capture; the next one recaptures).  Every variant equals
     the eager run bit for bit."""
     kw = dict(test_interval=dict(test_interval=3, test_iter=1, test_batch=100),
               display=dict(display=2),
               average_loss=dict(display=2, average_loss=2),
-              side_stream=dict(side_stream=True))[mode]
-    ref = _train(False, [4, 5], **kw)
-    got = _train(True, [4, 5], **kw)
+              side_stream=dict(side_stream=True),
+              release_caches=dict(release=True))[mode]
+    iters = [4, 5] if mode != "release_caches" else [3, 1, 3, 2]
+    ref = _train(False, iters, **kw)
+    got = _train(True, iters, **kw)
     if mode != "average_loss":
         assert got[4]                                   # the graph ran
     for a, b in zip(got[0] + got[1] + got[2], ref[0] + ref[1] + ref[2]):

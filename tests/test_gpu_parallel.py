@@ -187,9 +187,10 @@ def test_bench_two_ranks_rehearsal(device, workload):
 @pytest.mark.parametrize("workload", ["alexnet_mc", "cifar10_full_train"])
 def test_bench_rccl_world1(device, workload):
     """bench.py under torch.distributed.run with the default backend (RCCL):
-    world size 1 on this box's GPU runs init_process_group("nccl",
-    device_id=...), the barriers, the stats / max-time all-reduces and (for
-    training) the gradient all-reduce — the collectives an 8-GPU job issues
+    world size 1 on this box's GPU runs the C++ host's own RCCL communicator
+    (torch.distributed is only the gloo rendezvous that hands out its id):
+    the barriers, the stats / max-time all-reduces and (for training) the
+    native P2PSync gradient all-reduce — the collectives an 8-GPU job issues
     (replaces parallel.cpp:324-380)."""
     import json
     import subprocess
@@ -209,7 +210,9 @@ def test_bench_rccl_world1(device, workload):
     res = json.loads(lines[0])
     assert res["n_gpus"] == 1 and res["value"] > 0
     if workload == "alexnet_mc":
-        assert res["config"]["parallelism"] == "mc-maps x1 (RCCL stats all-reduce)"
+        assert res["config"]["parallelism"] == \
+            "mc-maps x1 (RCCL stats all-reduce from the C++ host, rram_mc_allreduce_stats)"
         assert res["mc_stats"]["maps"] == 3
     else:
-        assert res["config"]["parallelism"].startswith("dp1 (RCCL all-reduce")
+        p = res["config"]["parallelism"]
+        assert p.startswith("dp1 (RCCL all-reduce") and "C++ host P2PSync" in p, p

@@ -268,15 +268,20 @@ def _dp_worker(rank, world, port, backend, list_file, cases, q, shard=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
+    comm = None
     if backend == "nccl":
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    elif backend == "native":      # the C++ host's RCCL communicator; gloo only hands out its id
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from rramsim import caffe
+        comm = caffe.Comm(rank, world)
     else:
         dist.init_process_group(backend, rank=rank, world_size=world)
     from rramsim.parallel import DataParallelSolver
     out = []
     for lr, wd, mom, iters in cases:
         dp = DataParallelSolver(solver_proto(lr, wd, mom, iters), net_proto(list_file, NUM), seed=1701,
-                                shard_hdf5=shard)
+                                shard_hdf5=shard, comm=comm)
         dp.step(iters)
         torch.cuda.synchronize()
         ps = dp.solver.net.params()
@@ -286,6 +291,8 @@ def _dp_worker(rank, world, port, backend, list_file, cases, q, shard=False):
         dp.close()
     q.put((rank, out))
     dist.barrier()
+    if comm is not None:
+        comm.close()
     dist.destroy_process_group()
 
 
@@ -353,13 +360,15 @@ def test_least_squares_update_two_ranks_row_split(device, tmp_path):
         assert n0 == n1 > 0
 
 
-def test_least_squares_update_rccl_world1(device, tmp_path):
-    """The RCCL code path (init_process_group("nccl", device_id=...), the
-    gradient all-reduce of DataParallelSolver) in a real run: world size 1 on
-    this box's GPU, the devices = 1 case of the everything test."""
+@pytest.mark.parametrize("backend", ["nccl", "native"])
+def test_least_squares_update_rccl_world1(device, tmp_path, backend):
+    """The RCCL code paths in a real run, world size 1 on this box's GPU, the
+    devices = 1 case of the everything test: torch's (init_process_group
+    ("nccl", device_id=...), DataParallelSolver's torch all-reduce) and the
+    C++ host's own (caffe.Comm + the native P2PSync, host/parallel.cpp)."""
     cases = [(0.01, 0.5, 0.5, k + 1) for k in range(2)]
     exp = _multi_device_expected(tmp_path, cases, 1)
-    res = _run_dp(1, "nccl", _list_file(tmp_path), cases)
+    res = _run_dp(1, backend, _list_file(tmp_path), cases)
     for (ep, eu), (p0, h0, n0) in zip(exp, res[0][1]):
         _near(ep, p0.astype(np.float64))
         _near(eu, h0.astype(np.float64))

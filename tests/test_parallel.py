@@ -125,3 +125,54 @@ def test_gloo_world2_bucketed_allreduce_equals_flat():
         assert p.exitcode == 0
     assert res[0][1] and res[1][1]
     assert res[0][2] == [(1, (0, 3000)), (3, (3000, 10_000))]
+
+
+def test_native_plan_buckets_matches_python_plan():
+    """The C++ P2PSync's bucket plan (host/parallel.cpp plan_buckets, exposed
+    host-only as rram_dp_plan_buckets) is the Python rehearsal's plan on the
+    LeNet-shaped layout above, on random layouts with paramless layers, and
+    refuses layouts whose ranges do not tile the buffer in layer order (shared
+    params: the suffix property fails)."""
+    import random
+    from rramsim import caffe
+    from rramsim.parallel import plan_buckets
+    sizes = {1: (500, 20), 3: (25000, 50), 4: (400000, 500), 6: (5000, 10)}
+    rng = random.Random(5)
+    layouts = []
+    ranges, off = [], 0
+    for i in range(8):
+        rs = []
+        for n in sizes.get(i, ()):
+            rs.append((off, off + n))
+            off += n
+        ranges.append(rs)
+    layouts.append(ranges)
+    for _ in range(40):
+        ranges, off = [], 0
+        for i in range(rng.randint(1, 30)):
+            rs = []
+            for _ in range(rng.choice((0, 0, 1, 2, 3))):
+                n = rng.randint(1, 100_000)
+                rs.append((off, off + n))
+                off += n
+            ranges.append(rs)
+        layouts.append(ranges)
+    for ranges in layouts:
+        for be in (1, 1000, 30000, 200_000, 10 ** 9):
+            assert caffe.dp_plan_buckets(ranges, be) == plan_buckets(ranges, len(ranges), be), (ranges, be)
+    # a param shared by two layers (its range appears twice): no plan
+    shared = [[(0, 10)], [(10, 20)], [(0, 10)]]
+    assert caffe.dp_plan_buckets(shared, 1) == {}
+
+
+def test_caffe_signatures_cover_the_header():
+    """Every rram_caffe.h entry point, the multi-GPU ones included, has a
+    ctypes signature in rramsim.caffe (the Python view is complete)."""
+    import re
+    from pathlib import Path
+    from rramsim import caffe
+    text = (Path(__file__).resolve().parents[1] / "include" / "rram_caffe.h").read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = set(re.findall(r"\b(rram_[a-z0-9_]+)\s*\(", text))
+    assert {"rram_comm_create", "rram_dp_create", "rram_mc_allreduce_stats"} <= names
+    assert sorted(names - set(caffe.SIGNATURES)) == []
