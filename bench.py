@@ -12,7 +12,7 @@ data-path collective); one RCCL all-reduce of the statistics closes the job.
 
 Prints ONE JSON line (rank 0):
   value = images classified under faults per second, summed over ranks
-  roofline = the dominant kernel (conv2, k_conv_cb_x6 5x5) vs the peak of
+  roofline = the dominant kernel (conv2, k_conv_cb16_x6 5x5) vs the peak of
              its engine (bf16x6 split: bf16 dense peak / 6), hipEvents around
              its layer in the timed region; `contractions` = all conv / IP
              layers vs their engines' peaks, timed over K further maps after
@@ -42,9 +42,9 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: bf16 dense MFMA (no spars
 # fp32 product: its roofline is the bf16 dense peak / 6 in fp32 FLOPs
 MFMA_X6_PEAK_TFLOPS = MFMA_BF16_PEAK_TFLOPS / 6.0
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
-# the dominant kernel of the step: conv2's k_conv_cb16_x6<5,5,...> (22 % of GPU
-# time, profiles/r03_*_kernel_stats.csv); the only layer timed inside the
-# timed region, so the stream carries two markers per map for it
+# the dominant kernel of the step: conv2's k_conv_cb16_x6<5,5,4,4,8,2,1> (22 %
+# of GPU time, profiles/r05u_bench_kernel_stats.csv); the only layer timed
+# inside the timed region, so the stream carries two markers per map for it
 DOMINANT_LAYER = "conv2"
 DOMINANT_PMC_CLASS = "conv2 k_conv_cb16_x6<5,5,...>"
 
@@ -312,7 +312,8 @@ def main():
                      "traffic": (dom_pmc["measured_MB_per_step"] * 1e6 if dom_pmc.get("measured_MB_per_step")
                                  else None),
                      "kernel": ("k_gemm_x6 (fc6, the largest per-map contraction with the prefix reused) "
-                                if reuse else "k_conv_cb_x6 5x5 (128 x 128 per-image tiles, two workgroups per CU)")
+                                if reuse else "k_conv_cb16_x6<5,5,4,4,8,2,1> (5x5 channel-octet kernel on "
+                                "v_mfma_f32_16x16x32_bf16, 128 x 128 per-image tiles, two workgroups per CU)")
                                + f" = AlexNet {dom_layer} ({engines[dom_layer]} engine, "
                                "one launch per map), hipEvents around its layer over the timed region; peak = "
                                "bf16 dense 2500 / 6 products = 416.7 (f32 engine: v_mfma_f32_32x32x2_f32 157.3)",

@@ -201,13 +201,14 @@ int rram_conv2d_fwd_octets(const rram_conv_desc* d_in, const float* x, const voi
   int rc = rram_conv_out_shape(&d);
   if (rc) return rc;
   if (d.num == 0) return RRAM_OK;
-  RRAM_REQUIRE(x && w && y, "conv2d_fwd_octets: NULL pointer");
+  RRAM_REQUIRE(x && w && (y || y_oct), "conv2d_fwd_octets: NULL pointer");
   RRAM_REQUIRE((int64_t)d.num * d.out_h * d.out_w < (1ll << 31), "conv2d_fwd_octets: too many output positions");
   RRAM_REQUIRE(x_oct == nullptr || d.channels % 8 == 0, "conv2d_fwd_octets: input octets need channels %% 8 == 0");
   RRAM_REQUIRE(y_oct == nullptr || d.num_output % 8 == 0, "conv2d_fwd_octets: output octets need num_output %% 8 == 0");
   rc = conv_x6_fwd(&d, x, x_oct, w, bias, y, y_oct, relu, as_stream(s));
   if (rc < 0) return rc;
   if (rc > 0) return RRAM_OK;
+  RRAM_REQUIRE(y != nullptr, "conv2d_fwd_octets: y = NULL needs rram_conv_output_octets_only(d) == 1");
   rc = conv_fwd_core(&d, x, w, bias, y, relu, as_stream(s));
   if (rc == 0 && y_oct != nullptr) rc = pack_octets(y, y_oct, d.num, d.num_output, d.out_h * d.out_w, as_stream(s));
   return rc;
@@ -232,7 +233,7 @@ int rram_conv2d_fwd_cached(const rram_conv_desc* d_in, const float* x, const voi
   int rc = rram_conv_out_shape(&d);
   if (rc) return rc;
   if (d.num == 0) return RRAM_OK;
-  RRAM_REQUIRE(x && w && y, "conv2d_fwd_cached: NULL pointer");
+  RRAM_REQUIRE(x && w && (y || y_oct), "conv2d_fwd_cached: NULL pointer");
   RRAM_REQUIRE((int64_t)d.num * d.out_h * d.out_w < (1ll << 31), "conv2d_fwd_cached: too many output positions");
   RRAM_REQUIRE(x_oct == nullptr || d.channels % 8 == 0, "conv2d_fwd_cached: input octets need channels %% 8 == 0");
   RRAM_REQUIRE(y_oct == nullptr || d.num_output % 8 == 0, "conv2d_fwd_cached: output octets need num_output %% 8 == 0");

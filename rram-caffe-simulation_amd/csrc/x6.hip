@@ -604,7 +604,9 @@ __device__ __forceinline__ floatx4 mfma6_16(const Parts& a, const Parts& b, floa
 // Epilogue of MI x NJ 16x16 accumulator blocks (v_mfma_f32_16x16x32 layout:
 // col = lane & 15, row = 4 (lane >> 4) + r): conv_epilogue_nchw's arithmetic
 // and raw buffer stores, the lane's row group folded into its base address.
-// acc is left holding the stored values before the ReLU.
+// acc is left holding the stored values before the ReLU.  ep.C == nullptr
+// (the convolution-output fold: the only reader takes the octet companion)
+// computes the values and stores nothing.
 template <int MI, int NJ>
 __device__ __forceinline__ void conv_epilogue_nchw16(floatx4 (&acc)[MI][NJ], const Params& P, const Epi& ep, int mwave,
                                                      int nwave, int c16, int g, int nlim) {
@@ -614,6 +616,7 @@ __device__ __forceinline__ void conv_epilogue_nchw16(floatx4 (&acc)[MI][NJ], con
   const bool rows_full = mwave + MI * 16 <= P.M;
   const bool row_bias = ep.bias_mode == RRAM_BIAS_ROW, col_bias = ep.bias_mode == RRAM_BIAS_COL;
   const bool relu = ep.relu != 0;
+  const bool store = ep.C != nullptr;  // uniform
   const float alpha = ep.alpha;
   float bz[MI][4];
 #pragma unroll
@@ -640,6 +643,7 @@ __device__ __forceinline__ void conv_epilogue_nchw16(floatx4 (&acc)[MI][NJ], con
         acc[i][j][r] = o;
         ov[i][r] = relu ? fmaxf(o, 0.0f) : o;
       }
+    if (!store) continue;
     if (rows_full) {  // uniform: no per-store exec masking
 #pragma unroll
       for (int i = 0; i < MI; ++i)
@@ -659,6 +663,23 @@ __device__ __forceinline__ void conv_epilogue_nchw16(floatx4 (&acc)[MI][NJ], con
   }
 }
 
+// RRAM_CB_STAMP (diagnostic build only, never the product): per-group
+// s_memtime cycle sums of k_conv_cb16_x6 for the 3x3 forms (slots 0 .. 2H:
+// the groups of an (even, odd) K-tile pair, 2H + 1: the end-of-K-tile
+// barriers, 2H + 2: the barrier after an odd K-tile's cross group, 2H + 3:
+// the prologue, 2H + 4: the epilogue, 2H + 5: wave-tiles), summed over waves
+// into g_cb_stamp (read by rram_debug_cb_stamps)
+#ifdef RRAM_CB_STAMP
+__device__ unsigned long long g_cb_stamp[32];
+__device__ __forceinline__ unsigned long long cb_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#endif
+
 // KTO = KT & 1 (the K-tile count's parity, host-checked): one tail shape per
 // instantiation.  With both tails in one kernel (a runtime branch after the
 // K-tile pair loop) the register allocator could not keep the loop's values
@@ -675,6 +696,22 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
   constexpr int MI = 2, NJ = 2 * NB;
   static_assert(2 * SFB <= 160 * 1024, "LDS");
   static_assert(PP >= 2, "pair groups");
+#ifdef RRAM_CB_STAMP
+  constexpr bool STAMP = KH == 3;
+  __shared__ unsigned long long cst_lds[4][16];
+  if ((threadIdx.x & 63) < 16) cst_lds[threadIdx.x >> 6][threadIdx.x & 63] = 0;
+  unsigned long long ctprev = cb_stamp();
+  auto cstamp = [&](int slot) __attribute__((always_inline)) {
+    if constexpr (STAMP) {
+      const unsigned long long tn = cb_stamp();
+      if ((threadIdx.x & 63) == 0) cst_lds[threadIdx.x >> 6][slot] += tn - ctprev;
+      ctprev = tn;
+    }
+  };
+#define RRAM_CB_ST(slot) cstamp(slot)
+#else
+#define RRAM_CB_ST(slot)
+#endif
   __shared__ __attribute__((aligned(16))) char smem[2 * SFB];
   // the patch pieces' source offsets, one word per (piece, thread): read per
   // refill instead of held in PD registers (at two workgroups per CU the
@@ -711,7 +748,7 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
   const uint32_t PL = static_cast<uint32_t>(cv.H * cv.W * 48);
   Epi ep = P.e;
   if (z > 0) {
-    ep.C += z * P.grp_c;
+    if (ep.C) ep.C += z * P.grp_c;  // (NULL: the convolution-output fold stores no y, for any group)
     if (ep.bias) ep.bias += z * P.grp_bias;
   }
   const uint16_t* xg = xpack + (int64_t)z * (cv.C >> 3) * (PL >> 1);
@@ -826,9 +863,15 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
     };
     // staging distance (groups): the next K-tile's patch pieces are loaded at
     // group g and stored to the next stage at g + SD; SD = 2 where the K-tile
-    // has >= 4 groups (the 3x3 forms: +0.5 % maps/s, conv3 / conv4 -1 %,
-    // profiles/r05_ab_cb16_sd_band.txt; the 5x5 form keeps 1)
-    constexpr int SD = H >= 4 ? 2 : 1;
+    // has >= 4 groups: the 3x3 forms (H = 4: +0.5 % maps/s, conv3 / conv4
+    // -1 %, profiles/r05_ab_cb16_sd_band.txt) and, since H = 12 there, the
+    // 5x5 form too (the r05 A/B's "5x5 keeps 1" described a build
+    // that never shipped; RRAM_CB16_SD5 = 1 is that variant, round 6 A/B in
+    // profiles/r06_ab_*)
+#ifndef RRAM_CB16_SD5
+#define RRAM_CB16_SD5 2
+#endif
+    constexpr int SD = KH == 5 ? RRAM_CB16_SD5 : (H >= 4 ? 2 : 1);
     constexpr int PMAX = (PD + H - SD - 1) / (H - SD);  // patch pieces per group (the shortest K-tile spreads them over H - SD groups)
     static_assert(H >= 2, "pair groups");
     typedef int int4x __attribute__((ext_vector_type(4)));
@@ -876,9 +919,11 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
         for (int j = 0; j < NJ; ++j) {
           const bool last = gi == NG - 1 && j == NJ - 1;
           if (last && MORE) {  // the next stage is complete
+            RRAM_CB_ST(ODD ? H + gi : gi);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
+            RRAM_CB_ST(2 * H + 1);
           }
           if (!last) {
             if (j + 1 < NJ)  // (the cross group: lower half from the stage before)
@@ -901,15 +946,18 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
                                      x6::Parts{fb[j & 1][0], fb[j & 1][1], fb[j & 1][2]}, acc[i][j]);
           __builtin_amdgcn_sched_barrier(0);
         }
+        RRAM_CB_ST(ODD ? H + gi : gi);
         if (ODD && gi == 0 && MORE) {  // every wave is past the cross group: the refill may overwrite `oth`
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_s_barrier();
           __builtin_amdgcn_sched_barrier(0);
+          RRAM_CB_ST(2 * H + 2);
         }
       });
     };
     using T_ = std::true_type;
     using F_ = std::false_type;
+    RRAM_CB_ST(2 * H + 3);
     int kt = 0;
     for (; kt + 2 < KT; kt += 2) {
       const int q0 = (kt / 2) * (2 * H + 1);
@@ -962,7 +1010,17 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
       x6::store_terms8(v, yoct + (((int64_t)im * cout8 + oct) * HW + sp) * 48);
     }
   }
+#ifdef RRAM_CB_STAMP
+  if constexpr (STAMP) {
+    RRAM_CB_ST(2 * H + 4);
+    if ((threadIdx.x & 63) == 0) {
+      cst_lds[threadIdx.x >> 6][2 * H + 5] += 1;
+      for (int k = 0; k < 2 * H + 6; ++k) atomicAdd(&g_cb_stamp[k], cst_lds[threadIdx.x >> 6][k]);
+    }
+  }
+#endif
 }
+#undef RRAM_CB_ST
 
 // w [G*M][Cg][T] -> k_conv_cb16_x6 fragments [G][rblocks][NQ][2][term][64 lanes][8],
 // NQ = ceil(KT T / 2) groups in the kernel's K order: per (even, odd) pair
@@ -2365,6 +2423,9 @@ int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, c
   // count is not a multiple of 8 would share octets with its neighbour, so its
   // companion is packed from y after the kernel instead
   void* const y_oct_k = (y_oct != nullptr && M % 8 == 0) ? y_oct : nullptr;
+  // y == nullptr (the convolution-output fold) needs the companion from the
+  // 16x16x32 epilogue itself
+  if (y == nullptr && !wk.query && (!use16 || y_oct_k == nullptr)) return 0;
   const int HW = d->out_h * d->out_w, HWi = d->height * d->width;
   Params P{};
   P.M = M;
@@ -2579,6 +2640,9 @@ int conv_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, cons
     const int rc = conv_cb_x6_fwd(d, x, x_oct, w, bias, y, y_oct, relu, s, wk);
     if (rc != 0) return rc;
   }
+  // only the channel-octet kernel's epilogue writes a companion without y
+  RRAM_REQUIRE(y != nullptr || wk.query != nullptr,
+               "conv: y = NULL needs the channel-octet kernel's companion epilogue (rram_conv_output_octets_only)");
   {
     const int rc1 = conv_1x1_x6_fwd(d, x, w, bias, y, y_oct, relu, s, wk);  // writes y_oct itself
     if (rc1 != 0) return rc1;
@@ -2762,6 +2826,15 @@ int gemm_x6_nt(int M, int N, int K, float alpha, const float* A, int lda, const 
 
 extern "C" {
 
+#ifdef RRAM_CB_STAMP
+// diagnostic build only: the 3x3 octet-kernel stamp sums (and reset)
+int rram_debug_cb_stamps(unsigned long long* out, int n) {
+  if (out != nullptr && hipMemcpyFromSymbol(out, HIP_SYMBOL(rram::g_cb_stamp), sizeof(unsigned long long) * n) != hipSuccess)
+    return -2;
+  unsigned long long z[32] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(rram::g_cb_stamp), z, sizeof(z)) == hipSuccess ? 0 : -2;
+}
+#endif
 #ifdef RRAM_C1_STAMP
 // diagnostic build only: the conv1 stamp sums (and reset)
 int rram_debug_c1_stamps(unsigned long long* out, int n) {
@@ -2794,6 +2867,16 @@ int rram_conv_octet_plan(const rram_conv_desc* d, int* plan) {
   plan[3] = cpl.tpi;
   plan[4] = cpl.PD;
   return 1;
+}
+
+int rram_conv_output_octets_only(const rram_conv_desc* d_in) {
+  RRAM_REQUIRE(d_in != nullptr, "output octets query: desc is NULL");
+  if (rram::f32_engine().load(std::memory_order_relaxed) != RRAM_ENGINE_BF16X6) return 0;
+  rram_conv_desc d = *d_in;
+  if (rram_conv_out_shape(&d) != RRAM_OK || d.num == 0 || d.num_output % 8 != 0) return 0;
+  rram::CbPlan pl;
+  if (!rram::conv_cb_plan(&d, pl)) return 0;
+  return pl.OCC == 2 && (d.num_output / d.group) % 8 == 0 ? 1 : 0;
 }
 
 int rram_conv_input_octets(const rram_conv_desc* d) {

@@ -275,6 +275,11 @@ void ConvolutionLayer<Dtype>::Forward_gpu(const std::vector<Blob<Dtype>*>& botto
   }
   float* y = top[0]->mutable_gpu_data();  // invalidates top's companion
   void* yo = octets_for(top[0], kOctConv);
+  // convolution-output fold: the only reader takes the companion, so the
+  // fp32 top is not written (materialised on demand by Net::materialize_blob)
+  const bool skip_y = yo != nullptr && octet_reader_ != nullptr && octet_reader_->input_octets_now(top[0]) &&
+                      rram_conv_output_octets_only(&desc_) == 1;
+  if (skip_y) y = nullptr;
   if (wpb > 0) {
     // the pack is valid for this layer's shape and engine until the weights'
     // next mutable access (the MC driver's injection, a solver update, ...)
@@ -297,6 +302,7 @@ void ConvolutionLayer<Dtype>::Forward_gpu(const std::vector<Blob<Dtype>*>& botto
                                      fused_relu ? 1 : 0, Caffe::stream()));
   }
   if (yo) mark_octets(top[0]);
+  top[0]->data()->fp32_stale = skip_y;
 }
 
 template <typename Dtype>

@@ -39,6 +39,15 @@ class ConvolutionLayer : public Layer<Dtype> {
     concat_off_ = channel_offset;
     return true;
   }
+  // TEST-phase convolution-output fold (Net::Net): the top's only reader is
+  // a convolution taking its octet companion; each forward that both sides
+  // confirm (rram_conv_output_octets_only, the reader's input_octets_now)
+  // writes only the companion (the pooled-output fold's convolution form)
+  bool set_octet_reader(Layer<Dtype>* reader) override {
+    if (reader != nullptr && (this->phase_ != TEST || concat_top_ != nullptr)) return false;
+    octet_reader_ = reader;
+    return true;
+  }
 
  protected:
   void Forward_gpu(const std::vector<Blob<Dtype>*>& bottom, const std::vector<Blob<Dtype>*>& top) override;
@@ -51,6 +60,7 @@ class ConvolutionLayer : public Layer<Dtype> {
   int oct_key_[4] = {-1, -1, -1, -1};
   Blob<Dtype>* concat_top_ = nullptr;  // write_into_concat: the output goes to this top at channel concat_off_
   int concat_off_ = 0;
+  Layer<Dtype>* octet_reader_ = nullptr;  // convolution-output fold: the top's only reader
 };
 
 // ★ InnerProduct (inner_product_layer.cpp:9-141, .cu:9-75).

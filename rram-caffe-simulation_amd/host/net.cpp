@@ -156,6 +156,7 @@ Net<Dtype>::Net(const Msg& in_param, Phase phase, const Msg& options) : phase_(p
   const bool fuse_relu = options.boolean("fuse_relu", true);
   const bool fuse_lrn_pool = options.boolean("fuse_lrn_pool", true);
   const bool fuse_concat = options.boolean("fuse_concat", true);
+  const bool fuse_conv_y = options.boolean("fuse_conv_y", true);
   std::vector<int> data_shape;
   {
     std::string ds = options.str("data_shape", "");
@@ -374,7 +375,39 @@ Net<Dtype>::Net(const Msg& in_param, Phase phase, const Msg& options) : phase_(p
       if (ok && reader > f.pool && bottom_vecs_[reader].size() == 1 &&
           dynamic_cast<ConvolutionLayer<Dtype>*>(layers_[reader].get()) != nullptr &&
           layers_[f.pool]->set_octet_reader(layers_[reader].get()))
-        pool_y_folds_.push_back(f.pool);
+        oct_y_folds_.push_back(f.pool);
+    }
+  }
+  // TEST phase, the same for a Convolution producer (the convolution-output
+  // fold): its top read only by one Convolution (the producer's folded
+  // in-place ReLU aside) is written as the companion alone whenever the
+  // producer's epilogue writes it and the reader takes it (each forward
+  // checks); AlexNet conv3 -> conv4 and conv4 -> conv5
+#ifndef RRAM_CONV_Y_FOLD  // A/B builds: 0 = every convolution writes its fp32 top
+#define RRAM_CONV_Y_FOLD 1
+#endif
+  if (RRAM_CONV_Y_FOLD && fuse_conv_y && phase == TEST) {
+    const int L = static_cast<int>(layers_.size());
+    for (int l = 0; l < L; ++l) {
+      if (dynamic_cast<ConvolutionLayer<Dtype>*>(layers_[l].get()) == nullptr || top_id_vecs_[l].size() != 1)
+        continue;
+      const int t = top_id_vecs_[l][0];
+      int reader = -1;
+      bool ok = true;
+      for (int k = 0; k < L && ok; ++k) {
+        if (k == l) continue;
+        const bool reads = std::count(bottom_id_vecs_[k].begin(), bottom_id_vecs_[k].end(), t) > 0;
+        const bool writes = std::count(top_id_vecs_[k].begin(), top_id_vecs_[k].end(), t) > 0;
+        if (!reads && !writes) continue;
+        auto* relu = dynamic_cast<ReLULayer<Dtype>*>(layers_[k].get());
+        if (relu && relu->folded && k > l) continue;             // applied in the producer's epilogue
+        if (writes || reader >= 0) ok = false;
+        else reader = k;
+      }
+      if (ok && reader > l && bottom_vecs_[reader].size() == 1 &&
+          dynamic_cast<ConvolutionLayer<Dtype>*>(layers_[reader].get()) != nullptr &&
+          layers_[l]->set_octet_reader(layers_[reader].get()))
+        oct_y_folds_.push_back(l);
     }
   }
   for (auto& n : available) {
@@ -387,14 +420,14 @@ Net<Dtype>::Net(const Msg& in_param, Phase phase, const Msg& options) : phase_(p
 
 template <typename Dtype>
 void Net<Dtype>::materialize_blob(const Blob<Dtype>* b) {
-  const size_t folds = concat_folds_.size() + pool_y_folds_.size() + lrn_folds_.size();
+  const size_t folds = concat_folds_.size() + oct_y_folds_.size() + lrn_folds_.size();
   // a captured MC / Solver graph replays the folded launches: undoing a fold
   // must make it recapture (the graph keys include this generation)
   struct Bump {
     const Net* n;
     size_t before;
     ~Bump() {
-      if (n->concat_folds_.size() + n->pool_y_folds_.size() + n->lrn_folds_.size() != before)
+      if (n->concat_folds_.size() + n->oct_y_folds_.size() + n->lrn_folds_.size() != before)
         Caffe::scratch_gen().fetch_add(1);
     }
   } bump{this, folds};
@@ -414,8 +447,8 @@ void Net<Dtype>::materialize_blob(const Blob<Dtype>* b) {
     layers_[f.concat]->skip_concat_bottom(f.bottom, false);
     concat_folds_.erase(concat_folds_.begin() + static_cast<long>(i));
   }
-  for (size_t i = 0; i < pool_y_folds_.size();) {
-    const int l = pool_y_folds_[i];
+  for (size_t i = 0; i < oct_y_folds_.size();) {
+    const int l = oct_y_folds_[i];
     Blob<Dtype>* t = top_vecs_[l][0];
     if (t != b) {
       ++i;
@@ -424,7 +457,7 @@ void Net<Dtype>::materialize_blob(const Blob<Dtype>* b) {
     layers_[l]->set_octet_reader(nullptr);
     if (t->data()->fp32_stale && bottom_vecs_[l][0]->count() > 0) layers_[l]->Forward(bottom_vecs_[l], top_vecs_[l]);
     t->data()->fp32_stale = false;
-    pool_y_folds_.erase(pool_y_folds_.begin() + static_cast<long>(i));
+    oct_y_folds_.erase(oct_y_folds_.begin() + static_cast<long>(i));
   }
   for (size_t i = 0; i < lrn_folds_.size();) {
     const LrnFold f = lrn_folds_[i];

@@ -118,7 +118,7 @@ class Net {
     float alpha, beta, k;
   };
   std::vector<LrnFold> lrn_folds_;
-  std::vector<int> pool_y_folds_;  // pooled-output folds: the pool layers
+  std::vector<int> oct_y_folds_;  // pooled- / convolution-output folds: the producing layers
   int timing_ = 0;
   int timed_layer_ = -1;
   EventTimer timer_;

@@ -503,13 +503,13 @@ void Solver<Dtype>::Step(int iters) {
       net_->set_iter((uint64_t)iter_);
       {
         GraphStreamScope sc(gstream_);
-        // a changed key means freed / reallocated scratch: this iteration
-        // runs eager again (rebuilding tables, growing buffers outside any
-        // capture) and the next one captures
-        if (warm && gx_[0] && (rate != graph_rate_ || graph_key() != graph_ptrs_)) {
-          drop_graphs();
-          warm = false;
-        }
+        // a new rate recaptures now; a key changed since the capture -- or
+        // since the eager warm-up iteration -- means freed / reallocated
+        // scratch: this iteration then runs eager again (rebuilding tables,
+        // growing buffers outside any capture) and the next one captures
+        const bool moved = warm && graph_key() != graph_ptrs_;
+        if (gx_[0] && (rate != graph_rate_ || moved)) drop_graphs();
+        if (moved) warm = false;
         auto fb = [&] {
           net_->ClearParamDiffs();
           net_->Forward(false);
@@ -526,10 +526,10 @@ void Solver<Dtype>::Step(int iters) {
         if (warm) {
           capture_launch(1, [&] { FusedTail(); });
           graph_rate_ = rate;
-          graph_ptrs_ = graph_key();
         } else {
           FusedTail();
         }
+        graph_ptrs_ = graph_key();  // the scratch this iteration ran (or was captured) with
       }
       graph_warm_ = true;
       ++iter_;
@@ -964,7 +964,9 @@ void MonteCarlo<Dtype>::Run(uint32_t map_begin, uint32_t map_count) {
     GraphStreamScope sc(gstream_);
     hipStream_t st = Caffe::hip_stream();
     HIP_CALL(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_state_), static_cast<int>(map_begin), 1, st));
-    if (gexec_ && graph_key() != graph_ptrs_) drop_graph();
+    // the scratch moved since the capture -- or since the eager warm-up map
+    // (a capture now would rebuild freed tables inside it): eager again
+    if ((gexec_ || graph_warm_) && graph_key() != graph_ptrs_) drop_graph();
     for (uint32_t m = map_begin; m < map_begin + map_count; ++m) {
       if (!gexec_) {
         if (!graph_warm_) {
@@ -972,6 +974,7 @@ void MonteCarlo<Dtype>::Run(uint32_t map_begin, uint32_t map_count) {
           // the device-state path the graph will replay
           map_body(true, m);
           graph_warm_ = true;
+          graph_ptrs_ = graph_key();
           ++maps_run_;
           continue;
         }

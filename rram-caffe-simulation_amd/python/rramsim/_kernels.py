@@ -75,6 +75,7 @@ SIGNATURES = {
     "rram_get_f32_engine": (I, []),
     "rram_f32_engine_for_conv": (I, [P]),
     "rram_f32_engine_for_ip": (I, [I, I, I, SZ]),
+    "rram_conv_output_octets_only": (I, [P]),
     "rram_fault_threshold": (I, [P, I64, F, F, P]),
     "rram_fault_init": (I, [P, P, I64, F, F, U64, U64, U64, U32, U32, P]),
     "rram_fail_apply": (I, [P, P, P, P, I64, F, F, P, P]),

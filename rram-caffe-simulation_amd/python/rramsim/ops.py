@@ -233,6 +233,12 @@ def conv2d_fwd_strided(d, x, w, bias, y, y_image_stride, relu=False, x_oct=None,
                                            _stream()), "conv2d_fwd_strided")
 
 
+def conv_output_octets_only(d):
+    """1 when rram_conv2d_fwd_octets accepts y = None with y_oct for d now
+    (the channel-octet epilogue writes only the companion)."""
+    return _lib().rram_conv_output_octets_only(C.byref(d))
+
+
 def conv_input_octets(d):
     """1 when rram_conv2d_fwd_octets would read an input companion for d now."""
     return _lib().rram_conv_input_octets(C.byref(d))

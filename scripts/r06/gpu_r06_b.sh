@@ -6,9 +6,8 @@
 set -o pipefail
 O=gpurun_out/r06b; mkdir -p $O
 R=$GRAFT_REPO_ROOT
-timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_native_dp.py \
-  tests/test_gpu_parallel.py::test_bench_rccl_world1 "tests/test_gpu_solver_kat.py::test_least_squares_update_rccl_world1" \
-  tests/test_gpu_graph.py > $O/pytest.log 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_native_dp.py tests/test_gpu_parallel.py \
+  "tests/test_gpu_solver_kat.py::test_least_squares_update_rccl_world1" tests/test_gpu_graph.py > $O/pytest.log 2>&1; rc=$?
 tail -5 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --profile-layers > $O/bench.json 2> $O/bench.err || { tail -5 $O/bench.err; exit 1; }
 cut -c1-300 $O/bench.json

@@ -19,8 +19,9 @@ def N(t):
     return t.detach().cpu().numpy().copy()
 
 
-def _run(model, graph, calls, opts_extra=None, cfg_kw=None):
-    from rramsim import caffe, make_inject_cfg, models
+def _run(model, graph, calls, opts_extra=None, cfg_kw=None, release=False):
+    import torch
+    from rramsim import caffe, kernels, make_inject_cfg, models
     caffe.set_stream_from_torch()
     caffe.set_random_seed(1701)
     name = "cifar10_quick" if model == "cifar" else "lenet"
@@ -31,6 +32,9 @@ def _run(model, graph, calls, opts_extra=None, cfg_kw=None):
     mc.set_graph(graph)
     for begin, count in calls:
         mc.run(begin, count)
+        if release:                        # gather tables freed between runs
+            torch.cuda.synchronize()
+            kernels.check(kernels.load().rram_release_caches(), "release_caches")
     st = mc.stats()
     fps = [N(f["data"]) for f in net.failure_params()]
     outs = {k: N(v) for k, v in net.outputs().items()}
@@ -54,6 +58,21 @@ def test_graph_maps_equal_eager(device, model, calls):
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
     for k in ref[2]:
         assert np.array_equal(got[2][k], ref[2][k]), k
+
+
+def test_graph_maps_release_caches_between_runs(device):
+    """rram_release_caches between MonteCarlo::Run calls (ADVICE r05): after
+    the eager warm-up map (a one-map run) and after a captured graph, the
+    moved scratch generation sends the next map down the eager path (the
+    freed gather tables are rebuilt outside any capture) and the one after
+    recaptures; per-map statistics and weights equal the eager maps."""
+    calls = [(0, 1), (1, 1), (2, 3), (5, 2)]
+    ref = _run("cifar", False, calls, release=True)
+    got = _run("cifar", True, calls, release=True)
+    assert got[3]
+    assert got[0]["per_map"] == ref[0]["per_map"] and got[0]["broken"] == ref[0]["broken"]
+    for a, b in zip(got[1], ref[1]):
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
 
 
 def test_graph_conv_fault_extension_equals_eager(device):
@@ -137,7 +156,7 @@ def test_graph_training_interleaved_equals_eager(device, mode):
               average_loss=dict(display=2, average_loss=2),
               side_stream=dict(side_stream=True),
               release_caches=dict(release=True))[mode]
-    iters = [4, 5] if mode != "release_caches" else [3, 1, 3, 2]
+    iters = [4, 5] if mode != "release_caches" else [3, 1, 1, 3, 2]
     ref = _train(False, iters, **kw)
     got = _train(True, iters, **kw)
     if mode != "average_loss":

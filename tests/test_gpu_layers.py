@@ -621,6 +621,72 @@ def test_pooled_output_fold_materialises(device):
         assert torch.equal(got[True][n], got[False][n]), n
 
 
+def test_conv_output_fold_materialises(device):
+    """AlexNet TEST net (round 6): conv3 and conv4, each read only by the next
+    convolution through its octet companion, are left unwritten in fp32 --
+    the channel-octet epilogue writes only the companion -- and materialised
+    when the C-ABI hands them out: bit for bit the blobs of the same net with
+    the fold off (fuse_conv_y: false); conv5 (read by pool5) is always
+    written, the outputs are bit-identical, and after the read the producers
+    write their fp32 outputs again."""
+    import torch
+    from rramsim import caffe, models
+    caffe.set_stream_from_torch()
+    got = {}
+    names = ("conv3", "conv4", "conv5", "fc8")
+    for fold in (False, True):
+        caffe.set_random_seed(1701)
+        net = caffe.Net(models.alexnet(test_batch=8), "test", models.net_options("alexnet", fuse_conv_y=fold))
+        for _ in range(3):
+            net.forward()
+        torch.cuda.synchronize()
+        stale = {n: net.blob_stale(n) for n in names}
+        got[fold] = {n: net.blob(n).detach().cpu().clone() for n in names}
+        after = {n: net.blob_stale(n) for n in names}
+        net.forward()
+        torch.cuda.synchronize()
+        again = {n: net.blob_stale(n) for n in names}
+        got[fold]["fc8_again"] = net.blob("fc8").detach().cpu().clone()
+        net.close()
+        if fold:
+            assert stale["conv3"] and stale["conv4"] and not stale["conv5"] and not stale["fc8"], stale
+            assert not any(after.values()) and not any(again.values()), (after, again)
+        else:
+            assert not any(stale.values()), stale
+    for n in got[False]:
+        assert torch.equal(got[True][n], got[False][n]), n
+
+
+def test_conv_octets_only_epilogue_bit_identical(device):
+    """rram_conv2d_fwd_octets with y = NULL (the convolution-output fold)
+    writes the same companion as with y, on the AlexNet conv3 / conv4
+    shapes the fold takes; a shape the channel-octet epilogue does not take
+    refuses y = NULL instead of computing without an output."""
+    import torch
+    from rramsim import ops, RramError
+    rng = np.random.default_rng(5)
+    for (n, cin, cout, g) in [(4, 256, 384, 1), (4, 384, 384, 2)]:
+        d = ops.conv_desc((n, cin, 13, 13), cout, 3, 1, 1, 1, g)
+        assert ops.conv_output_octets_only(d) == 1
+        x = torch.from_numpy(rng.standard_normal((n, cin, 13, 13)).astype(np.float32)).to(device)
+        w = torch.from_numpy((rng.standard_normal((cout, cin // g, 3, 3)) * 0.05).astype(np.float32)).to(device)
+        b = torch.from_numpy(rng.standard_normal(cout).astype(np.float32)).to(device)
+        y = torch.empty((n, cout, 13, 13), device=device)
+        yo1 = torch.zeros(n * cout * 169 * 6, dtype=torch.uint8, device=device)
+        yo2 = torch.full_like(yo1, 7)
+        ops.conv2d_fwd_octets(d, x, None, w, b, y, yo1, relu=True)
+        ops.conv2d_fwd_octets(d, x, None, w, b, None, yo2, relu=True)
+        torch.cuda.synchronize()
+        assert torch.equal(yo1, yo2)
+    d = ops.conv_desc((2, 3, 32, 32), 32, 5, 1, 2, 1, 1)          # fp32-engine shape: no companion epilogue
+    assert ops.conv_output_octets_only(d) == 0
+    x = torch.randn(2, 3, 32, 32, device=device)
+    w = torch.randn(32, 3, 5, 5, device=device)
+    yo = torch.zeros(2 * 32 * 32 * 32 * 6, dtype=torch.uint8, device=device)
+    with pytest.raises(RramError):
+        ops.conv2d_fwd_octets(d, x, None, w, None, None, yo)
+
+
 def test_pooled_output_fold_needs_a_sole_convolution_reader(device):
     """A second reader of pool1 (here a ReLU writing its own top) keeps the
     pool writing its fp32 top: pool1 is never stale, the extra reader sees
