@@ -724,90 +724,107 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
   const int c16 = lane & 15, g = lane >> 4, up = g >> 1;
   const int wr = wave % WR, wc = wave / WR;
 
+  // Persistent (round 6): the grid holds at most two workgroups per CU.  XCD
+  // x owns the contiguous tile range [xs, xe) (row tiles of a column tile
+  // consecutive: they share its patch; a band order, 48 column tiles per band
+  // so one row block's weights stay in L2, raised conv3 / conv4 traffic
+  // 403 -> 461 / 389 -> 528 MB: profiles/r05_ab_cb16_sd_band.txt) and its
+  // workgroups take every wx-th tile of it.  After a tile's last MFMA group
+  // the next tile's patch pieces (K-tile 0) are DMA'd into the stage that
+  // K-tile leaves free and its first weight group is loaded, so that
+  // prologue's latency runs under this tile's epilogue stores instead of in
+  // front of the next tile's MFMAs (K-tile kt's stage is (kt ^ sp) & 1, sp
+  // flipping per tile when KT is odd).
   const int nwg = gridDim.x;
   const int bid = blockIdx.x;
   const int xcd = bid & 7, loc = bid >> 3;
   const int q8 = nwg >> 3, r8 = nwg & 7;
-  const int tid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
-  // row tiles fastest: the row tiles of a column tile share its patch (a
-  // band order, 48 column tiles per band so one row block's weights stay in
-  // L2, raised conv3 / conv4 traffic 403 -> 461 / 389 -> 528 MB:
-  // profiles/r05_ab_cb16_sd_band.txt)
-  const int z = __builtin_amdgcn_readfirstlane(tid / (P.tiles_m * P.tiles_n));
-  const int r_ = tid - z * P.tiles_m * P.tiles_n;
-  const int tm_ = r_ % P.tiles_m, tn_ = r_ / P.tiles_m;
-  const int tm = __builtin_amdgcn_readfirstlane(tm_);
-  const int tn = __builtin_amdgcn_readfirstlane(tn_);
-  const int m0 = tm * BMc;
+  const int wx = q8 + (xcd < r8 ? 1 : 0);  // workgroups on this XCD
+  const int ntiles = P.tiles_z * P.tiles_m * P.tiles_n;
+  const int qt = ntiles >> 3, rt = ntiles & 7;
+  const int xs = xcd * qt + min(xcd, rt), xe = xs + qt + (xcd < rt ? 1 : 0);
 
   const ConvGeom& cv = P.cv;
   const int HW = cv.howo.d, OW = cv.wo_div.d;
-  const int timg = tpi > 0 ? tn / tpi : 0;
-  const int n0 = tpi > 0 ? timg * HW + (tn - timg * tpi) * BNc : tn * BNc;
   const int KT = cv.C >> 4;
   const uint32_t PL = static_cast<uint32_t>(cv.H * cv.W * 48);
-  Epi ep = P.e;
-  if (z > 0) {
-    if (ep.C) ep.C += z * P.grp_c;  // (NULL: the convolution-output fold stores no y, for any group)
-    if (ep.bias) ep.bias += z * P.grp_bias;
-  }
-  const uint16_t* xg = xpack + (int64_t)z * (cv.C >> 3) * (PL >> 1);
-  const int4v xrsrc = make_rsrc(reinterpret_cast<const float*>(xg), xrange - static_cast<uint32_t>(z * (cv.C >> 3)) * PL);
-
-  const int plast = min(n0 + BNc, tpi > 0 ? (timg + 1) * HW : P.N) - 1;
-  const int img0 = n0 / HW, nseg = plast / HW - img0 + 1;
-  const int f0 = (n0 - img0 * HW) / OW;
-  auto seg_last = [&](int s) { return s == nseg - 1 ? (plast - (img0 + s) * HW) / OW : cv.Ho - 1; };
-  const int p1 = seg_last(0) - f0 + KH;
-  const int p2 = p1 + (nseg > 1 ? seg_last(1) + KH : 0);
-  const int R = p2 + (nseg > 2 ? seg_last(2) + KH : 0);
   const int PW = cv.W + 2 * cv.pw;
   const int dlt = cbx6::seg_shift(OW, KH);
+  const int NQ = (KT * T + 1) / 2;  // MFMA groups of the whole K
+  // one tile's geometry (uniform)
+  struct TileGeo {
+    int z, tm, m0, n0, plast, img0, nseg, f0, p1, p2, R;
+  };
+  auto geo = [&](int tid) __attribute__((always_inline)) {
+    TileGeo tg;
+    tg.z = __builtin_amdgcn_readfirstlane(tid / (P.tiles_m * P.tiles_n));
+    const int r_ = tid - tg.z * P.tiles_m * P.tiles_n;
+    tg.tm = __builtin_amdgcn_readfirstlane(r_ % P.tiles_m);
+    const int tn = __builtin_amdgcn_readfirstlane(r_ / P.tiles_m);
+    tg.m0 = tg.tm * BMc;
+    const int timg = tpi > 0 ? tn / tpi : 0;
+    tg.n0 = tpi > 0 ? timg * HW + (tn - timg * tpi) * BNc : tn * BNc;
+    tg.plast = min(tg.n0 + BNc, tpi > 0 ? (timg + 1) * HW : P.N) - 1;
+    tg.img0 = tg.n0 / HW;
+    tg.nseg = tg.plast / HW - tg.img0 + 1;
+    tg.f0 = (tg.n0 - tg.img0 * HW) / OW;
+    auto seg_last = [&](int s) { return s == tg.nseg - 1 ? (tg.plast - (tg.img0 + s) * HW) / OW : cv.Ho - 1; };
+    tg.p1 = seg_last(0) - tg.f0 + KH;
+    tg.p2 = tg.p1 + (tg.nseg > 1 ? seg_last(1) + KH : 0);
+    tg.R = tg.p2 + (tg.nseg > 2 ? seg_last(2) + KH : 0);
+    return tg;
+  };
+  // the patch pieces' source offsets, one word per (piece, thread), each
+  // thread reading only its own (no barrier between a write and its reads)
+  // (scalar arguments: with the geometry struct behind a reference the
+  // compiler kept it in scratch and indexed it per segment)
+  auto set_poff = [&](int nseg, int p1, int p2, int R, int f0, int img0) __attribute__((always_inline)) {
 #pragma unroll
-  for (int i = 0; i < PD; ++i) {
-    const int c = (wave * PD + i) * 64 + lane;
-    const int h = static_cast<int>(fdiv(static_cast<uint32_t>(c), oct_div)), rem = c - h * (octb >> 4);
-    // segment of this chunk (segment s starts s * dlt chunks late), then its row
-    const int sg = (nseg > 2 && rem >= p2 * rpc + 2 * dlt) ? 2 : (nseg > 1 && rem >= p1 * rpc + dlt) ? 1 : 0;
-    const int r2 = rem - sg * dlt;
-    const int prow = static_cast<int>(fdiv(static_cast<uint32_t>(r2), rpc_div)), pc = r2 - prow * rpc;
-    const int pcol = pc / 3, t = pc - pcol * 3;
-    uint32_t off = 0x80000000u;
-    if (h < 2 && prow < (sg == 0 ? p1 : sg == 1 ? p2 : R) && prow < R && pcol < PW) {
-      const int y = (sg == 0 ? f0 + prow : prow - (sg == 1 ? p1 : p2)) - cv.ph;
+    for (int i = 0; i < PD; ++i) {
+      const int c = (wave * PD + i) * 64 + lane;
+      const int h = static_cast<int>(fdiv(static_cast<uint32_t>(c), oct_div)), rem = c - h * (octb >> 4);
+      // segment of this chunk (segment s starts s * dlt chunks late), then its row
+      const bool s2 = nseg > 2 && rem >= p2 * rpc + 2 * dlt, s1 = !s2 && nseg > 1 && rem >= p1 * rpc + dlt;
+      const int sg = s2 ? 2 : s1 ? 1 : 0;
+      const int r2 = rem - sg * dlt;
+      const int prow = static_cast<int>(fdiv(static_cast<uint32_t>(r2), rpc_div)), pc = r2 - prow * rpc;
+      const int pcol = pc / 3, t = pc - pcol * 3;
+      const int plim = s2 ? R : s1 ? p2 : p1;
+      const int y = (s2 ? prow - p2 : s1 ? prow - p1 : f0 + prow) - cv.ph;
       const int x = pcol - cv.pw;
-      if (y >= 0 && y < cv.H && x >= 0 && x < cv.W)
+      uint32_t off = 0x80000000u;
+      if (h < 2 && prow < plim && prow < R && pcol < PW && y >= 0 && y < cv.H && x >= 0 && x < cv.W)
         off = static_cast<uint32_t>(img0 + sg) * static_cast<uint32_t>(ximg) + static_cast<uint32_t>(h) * PL +
               static_cast<uint32_t>((y * cv.W + x) * 48 + t * 16);
+      poff_lds[i * 256 + threadIdx.x] = off;
     }
-    poff_lds[i * 256 + threadIdx.x] = off;
-  }
+  };
   auto poff = [&](int i) { return poff_lds[i * 256 + threadIdx.x]; };
-  __syncthreads();
-  // B fragment bases (bytes into a stage) of this lane's column in block j,
-  // at tap 0 of its octet (g & 1)
-  int bb[NJ];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int n = cbx6::clamp_col(n0 + wc * 32 * NB + 16 * j + c16, n0, plast);
-    const int img = static_cast<int>(fdiv(static_cast<uint32_t>(n), cv.howo)), sp = n - img * HW;
-    const int oh = static_cast<int>(fdiv(static_cast<uint32_t>(sp), cv.wo_div)), ow = sp - oh * OW;
-    const int sg = img - img0;
-    const int prow = sg == 0 ? oh - f0 : (sg == 1 ? p1 : p2) + oh;
-    bb[j] = (g & 1) * octb + (prow * rpc + sg * dlt) * 16 + ow * 48;
-  }
-  floatx4 acc[MI][NJ];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[i][j][r] = 0.0f;
-
-  auto issue = [&](int kt, int stg, int i) {
-    dma_b128(xrsrc, poff(i) + static_cast<uint32_t>(kt) * 2u * PL,
+  // this group's octets start at octet z C/8 of every image
+  auto xg_of = [&](int z) { return xpack + (int64_t)z * (cv.C >> 3) * (PL >> 1); };
+  auto xbytes_of = [&](int z) { return xrange - static_cast<uint32_t>(z * (cv.C >> 3)) * PL; };
+  // K-tile kt's patch piece i of tile geometry tg into stage stg (LDS-DMA)
+  auto issue = [&](const int4v& rs, int kt, int stg, int i) {
+    dma_b128(rs, poff(i) + static_cast<uint32_t>(kt) * 2u * PL,
              lds0 + static_cast<uint32_t>(stg * SFB + (wave * PD + i) * 1024));
   };
+  // this wave's weight fragments through a buffer resource: the group's
+  // offset is uniform (SGPR soffset), the lane's 16 bytes the only VGPR
+  // (64-bit per-load addresses cost the registers this kernel spills)
+  auto a_rsrc = [&](const TileGeo& tg) {
+    const x6::bf16x8* ap = wpack + ((int64_t)((tg.z * P.tiles_m + tg.tm) * WR + wr) * NQ) * MI * cb16::FRAG;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<x6::bf16x8*>(ap), 0, NQ * MI * cb16::FRAG * 16, 0x00020000);
+  };
+  const int alane = lane * 16;
+  auto load_a_from = [&](const __amdgpu_buffer_rsrc_t& rs, x6::bf16x8 (&f)[MI][3], int q) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int t = 0; t < 3; ++t)
+        f[i][t] = __builtin_bit_cast(
+            x6::bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, alane, (q * MI + i) * cb16::FRAG * 16 + t * 1024, 0));
+  };
+
   // K order (T odd: 3x3, 5x5): K-tiles alternate even / odd.  An even K-tile
   // runs H = T / 2 pair groups (taps 2p, 2p + 1: lower / upper half) and
   // leaves tap T - 1; the odd K-tile after it starts with the cross group
@@ -819,6 +836,8 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
   // next: a barrier after it (odd K-tiles only) orders the refill behind it.
   constexpr int H = T / 2;
   static_assert(T % 2 == 1, "odd tap counts (3x3, 5x5)");
+  // a tile's last group runs on fa[0] (the next tile's first weights go to fa[1])
+  static_assert((H & 1) == 0 || KTO == 0, "last group's A parity");
   const int rowb = rpc * 16;
   auto toff = [&](int s) { return (s / KW) * rowb + (s % KW) * 48; };  // uniform
   // (opaque to the compiler: hoisted out of the K-tile loop, the NJ x H sums
@@ -829,6 +848,7 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
     return o;
   };
   x6::bf16x8 fa[2][MI][3], fb[2][3];
+  int bb[NJ];
   // group kinds: 0 pair (s0, s0 + 1), 1 cross (tap T - 1 of two K-tiles), 2 padded (tap T - 1, upper zero)
   auto read_b = [&](x6::bf16x8 (&f)[3], const char* lo, const char* hi, int kind, int s0, int j) {
     const char* st = kind == 1 ? (up ? hi : lo) : lo;
@@ -841,57 +861,78 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
       for (int t = 0; t < 3; ++t) f[t] = up ? x6::bf16x8{} : f[t];
     }
   };
-
-  {
-    const int NQ = (KT * T + 1) / 2;  // MFMA groups of the whole K
-    // this wave's weight fragments through a buffer resource: the group's
-    // offset is uniform (SGPR soffset), the lane's 16 bytes the only VGPR
-    // (64-bit per-load addresses cost the registers this kernel spills)
-    const x6::bf16x8* ap = wpack + ((int64_t)((z * P.tiles_m + tm) * WR + wr) * NQ) * MI * cb16::FRAG;
-    const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<x6::bf16x8*>(ap), 0, NQ * MI * cb16::FRAG * 16, 0x00020000);
-    const int alane = lane * 16;
-    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint16_t*>(xg), 0, static_cast<int>(xrange - static_cast<uint32_t>(z * (cv.C >> 3)) * PL), 0x00020000);
-    auto load_a = [&](x6::bf16x8 (&f)[MI][3], int q) {
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int t = 0; t < 3; ++t)
-          f[i][t] = __builtin_bit_cast(
-              x6::bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ar, alane, (q * MI + i) * cb16::FRAG * 16 + t * 1024, 0));
-    };
-    // staging distance (groups): the next K-tile's patch pieces are loaded at
-    // group g and stored to the next stage at g + SD; SD = 2 where the K-tile
-    // has >= 4 groups: the 3x3 forms (H = 4: +0.5 % maps/s, conv3 / conv4
-    // -1 %, profiles/r05_ab_cb16_sd_band.txt) and, since H = 12 there, the
-    // 5x5 form too (the r05 A/B's "5x5 keeps 1" described a build
-    // that never shipped; RRAM_CB16_SD5 = 1 is that variant, round 6 A/B in
-    // profiles/r06_ab_*)
+  // staging distance (groups): the next K-tile's patch pieces are loaded at
+  // group g and stored to the next stage at g + SD; SD = 2 where the K-tile
+  // has >= 4 groups: the 3x3 forms (H = 4: +0.5 % maps/s, conv3 / conv4
+  // -1 %, profiles/r05_ab_cb16_sd_band.txt) and, since H = 12 there, the
+  // 5x5 form too (the r05 A/B's "5x5 keeps 1" described a build
+  // that never shipped; RRAM_CB16_SD5 = 1 is that variant: no difference,
+  // profiles/r06_ab_conv_y_fold_sd5.txt)
 #ifndef RRAM_CB16_SD5
 #define RRAM_CB16_SD5 2
 #endif
-    constexpr int SD = KH == 5 ? RRAM_CB16_SD5 : (H >= 4 ? 2 : 1);
-    constexpr int PMAX = (PD + H - SD - 1) / (H - SD);  // patch pieces per group (the shortest K-tile spreads them over H - SD groups)
-    static_assert(H >= 2, "pair groups");
-    typedef int int4x __attribute__((ext_vector_type(4)));
-    int4x stg[SD + 1][PMAX];
+  constexpr int SD = KH == 5 ? RRAM_CB16_SD5 : (H >= 4 ? 2 : 1);
+  constexpr int PMAX = (PD + H - SD - 1) / (H - SD);  // patch pieces per group (the shortest K-tile spreads them over H - SD groups)
+  static_assert(H >= 2, "pair groups");
+  typedef int int4x __attribute__((ext_vector_type(4)));
+  int4x stg[SD + 1][PMAX];
+  floatx4 acc[MI][NJ];
+
+  int t = xs + loc;
+  if (t >= xe) return;  // (uniform; the host launches no such workgroup)
+  TileGeo cur = geo(t);
+  int sp = 0;
+  set_poff(cur.nseg, cur.p1, cur.p2, cur.R, cur.f0, cur.img0);
+  {
+    const int4v rs0 = make_rsrc(reinterpret_cast<const float*>(xg_of(cur.z)), xbytes_of(cur.z));
 #pragma unroll
-    for (int i = 0; i < PD; ++i) issue(0, 0, i);
-    load_a(fa[0], 0);
+    for (int i = 0; i < PD; ++i) issue(rs0, 0, 0, i);
+    load_a_from(a_rsrc(cur), fa[0], 0);
+  }
+  for (;;) {
+    const int tnext = t + wx;
+    const bool more_tiles = tnext < xe;  // uniform
+    Epi ep = P.e;
+    if (cur.z > 0) {
+      if (ep.C) ep.C += cur.z * P.grp_c;  // (NULL: the convolution-output fold stores no y, for any group)
+      if (ep.bias) ep.bias += cur.z * P.grp_bias;
+    }
+    const __amdgpu_buffer_rsrc_t ar = a_rsrc(cur);
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint16_t*>(xg_of(cur.z)), 0, static_cast<int>(xbytes_of(cur.z)), 0x00020000);
+    // B fragment bases (bytes into a stage) of this lane's column in block j,
+    // at tap 0 of its octet (g & 1)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int n = cbx6::clamp_col(cur.n0 + wc * 32 * NB + 16 * j + c16, cur.n0, cur.plast);
+      const int img = static_cast<int>(fdiv(static_cast<uint32_t>(n), cv.howo)), sp_ = n - img * HW;
+      const int oh = static_cast<int>(fdiv(static_cast<uint32_t>(sp_), cv.wo_div)), ow = sp_ - oh * OW;
+      const int sg = img - cur.img0;
+      const int prow = sg == 0 ? oh - cur.f0 : (sg == 1 ? cur.p1 : cur.p2) + oh;
+      bb[j] = (g & 1) * octb + (prow * rpc + sg * dlt) * 16 + ow * 48;
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = 0.0f;
+    auto load_a = [&](x6::bf16x8 (&f)[MI][3], int q) { load_a_from(ar, f, q); };
+    const char* smem0 = smem + sp * SFB;
     wait_vm<0>();
     __builtin_amdgcn_s_barrier();
     // the first K-tile is even: pair (0, 1), or the padded group when T == 1 ... (T >= 9 here)
-    read_b(fb[0], smem, smem, 0, 0, 0);
+    read_b(fb[0], smem0, smem0, 0, 0, 0);
     // K-tile kt of kind ODD (0 even, 1 odd); q0 = its first global group;
     // MORE: a next K-tile exists; PADT: the padded group ends it (last even K-tile)
     auto ktile = [&](int kt, int q0, auto odd_c, auto more_c, auto padt_c) {
       constexpr bool ODD = decltype(odd_c)::value, MORE = decltype(more_c)::value, PADT = decltype(padt_c)::value;
       constexpr int NG = ODD ? H + 1 : H + (PADT ? 1 : 0);
       constexpr int PAR = ODD ? (H & 1) : 0;  // A parity: an (even, odd) pair of K-tiles runs 2 H + 1 groups
-      const char* cur = smem + (kt & 1) * SFB;
-      const char* oth = smem + ((kt + 1) & 1) * SFB;  // the stage before = the stage refilled next
-      char* nst = smem + ((kt + 1) & 1) * SFB + wave * PD * 1024 + lane * 16;
+      const int ks = (kt ^ sp) & 1;
+      const char* cur_st = smem + ks * SFB;
+      const char* oth = smem + (ks ^ 1) * SFB;  // the stage before = the stage refilled next
+      char* nst = smem + (ks ^ 1) * SFB + wave * PD * 1024 + lane * 16;
       static_for<0, NG>([&](auto gc) {
         constexpr int gi = decltype(gc)::value;
         constexpr int KIND = ODD ? (gi == 0 ? 1 : 0) : (gi < H ? 0 : 2);
@@ -927,9 +968,9 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
           }
           if (!last) {
             if (j + 1 < NJ)  // (the cross group: lower half from the stage before)
-              read_b(fb[(j + 1) & 1], KIND == 1 ? oth : cur, cur, KIND, S0, j + 1);
+              read_b(fb[(j + 1) & 1], KIND == 1 ? oth : cur_st, cur_st, KIND, S0, j + 1);
             else
-              read_b(fb[(j + 1) & 1], cur, cur, NKIND, NS0, 0);
+              read_b(fb[(j + 1) & 1], cur_st, cur_st, NKIND, NS0, 0);
           } else if (MORE) {
             // the next K-tile's first group: after an even K-tile the cross
             // group (lower half here, upper half in the new stage), after an
@@ -937,7 +978,7 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
             if (ODD)
               read_b(fb[0], oth, oth, 0, 0, 0);
             else
-              read_b(fb[0], cur, oth, 1, 0, 0);
+              read_b(fb[0], cur_st, oth, 1, 0, 0);
           }
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -947,7 +988,9 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
           __builtin_amdgcn_sched_barrier(0);
         }
         RRAM_CB_ST(ODD ? H + gi : gi);
-        if (ODD && gi == 0 && MORE) {  // every wave is past the cross group: the refill may overwrite `oth`
+        // every wave is past the cross group: the refill -- or, after the
+        // tile's last K-tile, the next tile's patch -- may overwrite `oth`
+        if (ODD && gi == 0 && (MORE || more_tiles)) {
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_s_barrier();
           __builtin_amdgcn_sched_barrier(0);
@@ -967,57 +1010,84 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int t = 0; t < 3; ++t) fa[0][i][t] = fa[1][i][t];
+        for (int t2 = 0; t2 < 3; ++t2) fa[0][i][t2] = fa[1][i][t2];
     }
-    const int q0 = (kt / 2) * (2 * H + 1);
-    if constexpr (KTO == 0) {
-      ktile(kt, q0, F_{}, T_{}, F_{});
-      ktile(kt + 1, q0 + H, T_{}, F_{}, F_{});
-    } else {
-      ktile(kt, q0, F_{}, F_{}, T_{});
-    }
-  }
-  const int mwave = m0 + 32 * wr, nwave = n0 + wc * 32 * NB;
-  conv_epilogue_nchw16<MI, NJ>(acc, P, ep, mwave, nwave, c16, g, plast + 1);
-  if (yoct != nullptr) {
-    // the output's octet companion: lane group g holds rows 4 g .. 4 g + 3 of
-    // both 16-row blocks; lanes g, g ^ 1 (lane ^ 16) trade one block so that
-    // an even g stores octet g / 2 of block 0 and an odd g octet (g - 1) / 2
-    // of block 1, each whole (8 consecutive rows).
-    const bool relu = ep.relu != 0;
-    const bool ev = (g & 1) == 0;
-    const int orow = mwave + 16 * (g & 1) + 8 * (g >> 1);  // first row of the lane's octet
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int n = nwave + 16 * j + c16;
-      float o0[4], o1[4], rcv[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        o0[r] = relu ? fmaxf(acc[0][j][r], 0.0f) : acc[0][j][r];
-        o1[r] = relu ? fmaxf(acc[1][j][r], 0.0f) : acc[1][j][r];
-        rcv[r] = __shfl_xor(ev ? o1[r] : o0[r], 16);
+    {
+      const int q0 = (kt / 2) * (2 * H + 1);
+      if constexpr (KTO == 0) {
+        ktile(kt, q0, F_{}, T_{}, F_{});
+        ktile(kt + 1, q0 + H, T_{}, F_{}, F_{});
+      } else {
+        ktile(kt, q0, F_{}, F_{}, T_{});
       }
-      if (n > plast || orow >= P.M) continue;
-      float v[8];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        v[r] = ev ? o0[r] : rcv[r];
-        v[4 + r] = ev ? rcv[r] : o1[r];
-      }
-      const uint32_t im = fdiv(static_cast<uint32_t>(n), ep.hw);
-      const int sp = n - static_cast<int>(im) * HW;
-      const int oct = (z * P.M + orow) / 8;
-      x6::store_terms8(v, yoct + (((int64_t)im * cout8 + oct) * HW + sp) * 48);
     }
+    // the next tile's prologue, in flight under this tile's epilogue: its
+    // patch pieces of K-tile 0 into the stage the last K-tile left free (the
+    // last K-tile reads only its own stage, bar an odd one's cross group,
+    // which the barrier after it covers), its first weight group into fa[1]
+    // (the last group ran on fa[0])
+    TileGeo nxt = cur;
+    if (more_tiles) {
+      nxt = geo(tnext);
+      set_poff(nxt.nseg, nxt.p1, nxt.p2, nxt.R, nxt.f0, nxt.img0);
+      const int4v rsn = make_rsrc(reinterpret_cast<const float*>(xg_of(nxt.z)), xbytes_of(nxt.z));
+      const int sfree = (KT ^ sp) & 1;
+#pragma unroll
+      for (int i = 0; i < PD; ++i) issue(rsn, 0, sfree, i);
+      load_a_from(a_rsrc(nxt), fa[1], 0);
+    }
+    const int mwave = cur.m0 + 32 * wr, nwave = cur.n0 + wc * 32 * NB;
+    conv_epilogue_nchw16<MI, NJ>(acc, P, ep, mwave, nwave, c16, g, cur.plast + 1);
+    if (yoct != nullptr) {
+      // the output's octet companion: lane group g holds rows 4 g .. 4 g + 3 of
+      // both 16-row blocks; lanes g, g ^ 1 (lane ^ 16) trade one block so that
+      // an even g stores octet g / 2 of block 0 and an odd g octet (g - 1) / 2
+      // of block 1, each whole (8 consecutive rows).
+      const bool relu = ep.relu != 0;
+      const bool ev = (g & 1) == 0;
+      const int orow = mwave + 16 * (g & 1) + 8 * (g >> 1);  // first row of the lane's octet
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int n = nwave + 16 * j + c16;
+        float o0[4], o1[4], rcv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          o0[r] = relu ? fmaxf(acc[0][j][r], 0.0f) : acc[0][j][r];
+          o1[r] = relu ? fmaxf(acc[1][j][r], 0.0f) : acc[1][j][r];
+          rcv[r] = __shfl_xor(ev ? o1[r] : o0[r], 16);
+        }
+        if (n > cur.plast || orow >= P.M) continue;
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = ev ? o0[r] : rcv[r];
+          v[4 + r] = ev ? rcv[r] : o1[r];
+        }
+        const uint32_t im = fdiv(static_cast<uint32_t>(n), ep.hw);
+        const int sp_ = n - static_cast<int>(im) * HW;
+        const int oct = (cur.z * P.M + orow) / 8;
+        x6::store_terms8(v, yoct + (((int64_t)im * cout8 + oct) * HW + sp_) * 48);
+      }
+    }
+    RRAM_CB_ST(2 * H + 4);
+#ifdef RRAM_CB_STAMP
+    if constexpr (STAMP)
+      if ((threadIdx.x & 63) == 0) cst_lds[threadIdx.x >> 6][2 * H + 5] += 1;
+#endif
+    if (!more_tiles) break;
+    // the next tile's first weight group moves to fa[0]
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int t2 = 0; t2 < 3; ++t2) fa[0][i][t2] = fa[1][i][t2];
+    cur = nxt;
+    t = tnext;
+    sp ^= KTO;
   }
 #ifdef RRAM_CB_STAMP
-  if constexpr (STAMP) {
-    RRAM_CB_ST(2 * H + 4);
-    if ((threadIdx.x & 63) == 0) {
-      cst_lds[threadIdx.x >> 6][2 * H + 5] += 1;
+  if constexpr (STAMP)
+    if ((threadIdx.x & 63) == 0)
       for (int k = 0; k < 2 * H + 6; ++k) atomicAdd(&g_cb_stamp[k], cst_lds[threadIdx.x >> 6][k]);
-    }
-  }
 #endif
 }
 #undef RRAM_CB_ST
@@ -2491,9 +2561,20 @@ int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, c
   const uint32_t xrange = static_cast<uint32_t>(xbytes);  // whole packed input (the kernel narrows it per group)
   if (use16) {
     const int kto = (Cg / 16) & 1;
+    // persistent: at most two workgroups per CU (k_conv_cb16_x6 walks its
+    // XCD's tiles); a multiple of 8 whenever it is not one per tile
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+#ifndef RRAM_CB16_PERSIST_X2  // persistent while tiles <= slots * X2 / 2 (A/B builds)
+#define RRAM_CB16_PERSIST_X2 3
+#endif
+    const int64_t slots = (2 * cus) / 8 * 8;
+    const unsigned nwg16 =
+        static_cast<unsigned>(nwg * 2 <= slots * RRAM_CB16_PERSIST_X2 ? std::min<int64_t>(nwg, slots) : nwg);
 #define RRAM_X2(kh, wr, nb, pd, occ, kpar)                                                                          \
   if (KH == kh && pl.WR == wr && pl.NB == nb && pl.PD == pd && pl.OCC == occ && kto == kpar) {                      \
-    hipLaunchKernelGGL((k_conv_cb16_x6<kh, kh, wr, nb, pd, occ, kpar>), dim3(nwg), dim3(256), 0, s, P, wp, xp,        \
+    hipLaunchKernelGGL((k_conv_cb16_x6<kh, kh, wr, nb, pd, occ, kpar>), dim3(nwg16), dim3(256), 0, s, P, wp, xp,      \
                        pl.octb, pl.RPC, xrange, ximg, static_cast<char*>(y_oct_k), d->num_output / 8,               \
                        make_fastdiv(static_cast<uint32_t>(pl.octb >> 4)), make_fastdiv(static_cast<uint32_t>(pl.RPC)), \
                        pl.tpi);                                                                                     \
