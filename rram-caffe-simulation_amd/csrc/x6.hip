@@ -664,13 +664,13 @@ __device__ __forceinline__ void conv_epilogue_nchw16(floatx4 (&acc)[MI][NJ], con
 }
 
 // RRAM_CB_STAMP (diagnostic build only, never the product): per-group
-// s_memtime cycle sums of k_conv_cb16_x6 for the 3x3 forms (slots 0 .. 2H:
+// s_memtime cycle sums of k_conv_cb16_x6 (slots 0 .. 2H:
 // the groups of an (even, odd) K-tile pair, 2H + 1: the end-of-K-tile
 // barriers, 2H + 2: the barrier after an odd K-tile's cross group, 2H + 3:
 // the prologue, 2H + 4: the epilogue, 2H + 5: wave-tiles), summed over waves
 // into g_cb_stamp (read by rram_debug_cb_stamps)
 #ifdef RRAM_CB_STAMP
-__device__ unsigned long long g_cb_stamp[32];
+__device__ unsigned long long g_cb_stamp[64];
 __device__ __forceinline__ unsigned long long cb_stamp() {
   unsigned long long t;
   __builtin_amdgcn_sched_barrier(0);
@@ -697,9 +697,9 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
   static_assert(2 * SFB <= 160 * 1024, "LDS");
   static_assert(PP >= 2, "pair groups");
 #ifdef RRAM_CB_STAMP
-  constexpr bool STAMP = KH == 3;
-  __shared__ unsigned long long cst_lds[4][16];
-  if ((threadIdx.x & 63) < 16) cst_lds[threadIdx.x >> 6][threadIdx.x & 63] = 0;
+  constexpr bool STAMP = true;
+  __shared__ unsigned long long cst_lds[4][32];
+  if ((threadIdx.x & 63) < 32) cst_lds[threadIdx.x >> 6][threadIdx.x & 63] = 0;
   unsigned long long ctprev = cb_stamp();
   auto cstamp = [&](int slot) __attribute__((always_inline)) {
     if constexpr (STAMP) {
@@ -1651,9 +1651,21 @@ k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img,
     // lands in private memory and every load becomes a waterfall loop)
     const __amdgpu_buffer_rsrc_t xrs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xin), 0, in_bytes, 0x00020000);
+#ifdef RRAM_C1_LOAD128
+    // (A/B: two 16-byte loads at 4-byte alignment per chunk instead of eight 4-byte loads)
+    typedef float float4x __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float4x q = __builtin_bit_cast(
+          float4x, __builtin_amdgcn_raw_buffer_load_b128(xrs, static_cast<int>(voff + 16 * h), 0, 0));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[4 * h + e] = q[e];
+    }
+#else
 #pragma unroll
     for (int e = 0; e < 8; ++e)
       v[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xrs, static_cast<int>(voff + 4 * e), 0, 0));
+#endif
   };
   auto stage_store = [&](int c, int k, float (&v)[8]) {
     const int q = chunk_of(k);
@@ -2912,7 +2924,7 @@ extern "C" {
 int rram_debug_cb_stamps(unsigned long long* out, int n) {
   if (out != nullptr && hipMemcpyFromSymbol(out, HIP_SYMBOL(rram::g_cb_stamp), sizeof(unsigned long long) * n) != hipSuccess)
     return -2;
-  unsigned long long z[32] = {};
+  unsigned long long z[64] = {};
   return hipMemcpyToSymbol(HIP_SYMBOL(rram::g_cb_stamp), z, sizeof(z)) == hipSuccess ? 0 : -2;
 }
 #endif
