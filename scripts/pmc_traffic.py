@@ -145,9 +145,11 @@ for i, (gsz, vals) in enumerate(sorted(lrn_grids.items(), reverse=True)):
 # octet companions from the convolution epilogues (RRAM_OCTETS=1, the default
 # since round 3): conv3 / conv4 write their outputs' companions and no input
 # pack runs, so those bytes move from the pack row to the producers' rows
+# (round 6: the TEST-phase convolution-output fold -- conv3 / conv4 are read
+# only by conv4 / conv5 through the companion -- writes no fp32 y for them)
 if per.get("conv4/conv5 input packs k_pack_octets_x6", 0.0) == 0.0:
-    ALG["conv3 k_conv_cb16_x6<3,3,4,4,...>"] = (P2O + 384*256*9*4 + Y3 + O4, "x octets + w + y + y octets")
-    ALG["conv4 k_conv_cb16_x6<3,3,2,2,...>"] = (O4 + 384*192*9*4 + Y4 + O4, "x octets + w + y + y octets")
+    ALG["conv3 k_conv_cb16_x6<3,3,4,4,...>"] = (P2O + 384*256*9*4 + O4, "x octets + w + y octets (y fp32 folded)")
+    ALG["conv4 k_conv_cb16_x6<3,3,2,2,...>"] = (O4 + 384*192*9*4 + O4, "x octets + w + y octets (y fp32 folded)")
     ALG["conv4/conv5 input packs k_pack_octets_x6"] = (0.0, "none run (companions from the conv3 / conv4 epilogues)")
 table = {}
 for k, (alg, what) in ALG.items():

@@ -4,4 +4,7 @@
 set -o pipefail
 O=gpurun_out/r06h; mkdir -p $O
 RRAM_LIB_DIR=$PWD/rram-caffe-simulation_amd/lib_cbstamp timeout -k 10 300 python scripts/cb_stamp.py > $O/cb_stamp.txt 2>&1; rc=$?
-cat $O/cb_stamp.txt; exit $rc
+cat $O/cb_stamp.txt; [ $rc -eq 0 ] || exit $rc
+R=$GRAFT_REPO_ROOT
+( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$O/prof -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $R/$O/prof_bench.json 2> $R/$O/prof.err ) || exit $?
+echo done
