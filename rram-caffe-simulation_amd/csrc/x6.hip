@@ -1701,9 +1701,9 @@ k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img,
 
   // the weight fragments are the same for every tile: the base address is
   // laundered once per tile so the tile loop does not hoist all groups'
-  // loads out of itself.  (At 512 registers the allocator keeps 20 bytes of
-  // scratch; a spill-free form -- thread index re-derived per use, buffer-
-  // loaded fragments -- measured ~1 % slower: profiles/r05_ab_c1_scratch.txt)
+  // loads out of itself.  (With the round-5 refill schedule the allocator
+  // kept 20 bytes of scratch at 512 registers; the round-6 one-chunk-per-
+  // group refill needs 483 and none)
   const x6::bf16x8* ap = reinterpret_cast<const x6::bf16x8*>(wpack) + lane;
   auto launder_a = [&]() __attribute__((always_inline)) {
     int z = 0;
@@ -1817,6 +1817,10 @@ k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img,
       if (g + 2 < G) load_a(fg[(g + 2) % 3], g + 2);
       // slot refills (see the header): channel 2 of this tile at groups 1, 3, 5;
       // channel 0 / 1 of the next tile two, four and six groups after their last reader
+#ifndef RRAM_C1_SPREAD
+#define RRAM_C1_SPREAD 1
+#endif
+#if !RRAM_C1_SPREAD
       auto refill = [&](int u) __attribute__((always_inline)) {
         // (unconditional: the first tile re-fills slot 2 with what the prologue
         // put there; past the last tile the loads return zeros into dead slots)
@@ -1825,6 +1829,25 @@ k_conv1_ring_x6(Params P, const uint16_t* __restrict__ wpack, int tiles_per_img,
         if (d0 >= 0 && d0 <= 4 && (d0 & 1) == 0) refill_part(nxt, 0, d0 / 2, u);
         if (d1 >= 0 && d1 <= 4 && (d1 & 1) == 0) refill_part(nxt, 1, d1 / 2, u);
       };
+#else
+      // round 6: one chunk per group over CPT + 1 consecutive groups per slot
+      // -- load chunk s at step s, store it at step s + 1 -- instead of two
+      // per step on every other group (RRAM_C1_SPREAD=0); the same windows:
+      // slot 2 before the barrier after group last_group(0), slots 0 / 1
+      // before the next barriers.  483 VGPRs and no scratch (was 512 + 20 B),
+      // conv1 -0.6 % (profiles/r06_ab_conv1.txt)
+      auto refill1 = [&](const TileRef& tr, int c, int st) __attribute__((always_inline)) {
+        if (st > 0 && st - 1 < CPT) stage_store(c, st - 1, sv[(st - 1) & 1]);
+        if (st < CPT) stage_load(tr, c, st, sv[st & 1]);
+      };
+      auto refill = [&](int u) __attribute__((always_inline)) {
+        if (u != 0) return;
+        if (g >= 1 && g <= 1 + CPT) refill1(cur, 2, g - 1);
+        constexpr int d0 = g - last_group(0) - 1, d1 = g - last_group(1) - 1;
+        if (d0 >= 0 && d0 <= CPT) refill1(nxt, 0, d0);
+        if (d1 >= 0 && d1 <= CPT) refill1(nxt, 1, d1);
+      };
+#endif
 #pragma unroll
       for (int q = 0; q < 2 * MI; ++q) {
         const int i = q >> 1, j = q & 1;
