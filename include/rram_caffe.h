@@ -291,7 +291,8 @@ int rram_comm_barrier(rram_comm_t c);
  * reduced in buckets of >= bucket_mb MB started from the per-layer backward
  * hook on a collective stream while earlier layers still run backward; the
  * update waits for them.  Replaces rram_solver_set_gradient_callback /
- * _backward_callback while attached; destroy before the solver. */
+ * _backward_callback while attached; one per solver.  Destroying the solver
+ * first detaches it (rram_dp_destroy then only frees the handle). */
 int rram_dp_create(rram_solver_t s, rram_comm_t c, double bucket_mb, int overlap, rram_dp_t* out);
 /* the solver's flat learnable data / diff buffers (device pointers, *n
  * floats each; NULL / 0 when the `flat_params: false` option disabled them) */

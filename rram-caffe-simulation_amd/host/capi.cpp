@@ -15,8 +15,10 @@ using namespace caffe;
 struct rram_net_s {
   std::shared_ptr<Net<float>> net;
 };
+struct rram_dp_s;
 struct rram_solver_s {
   std::unique_ptr<Solver<float>> solver;
+  rram_dp_s* dp = nullptr;  // the attached P2PSync (rram_dp_create), detached on destroy
   rram_net_s train;
   std::vector<rram_net_s> tests;
   rram_callback_t grad_cb = nullptr;
@@ -36,7 +38,8 @@ struct rram_comm_s {
   std::shared_ptr<Comm> comm;
 };
 struct rram_dp_s {
-  std::unique_ptr<P2PSync<float>> sync;
+  std::unique_ptr<P2PSync<float>> sync;  // reset when its solver goes first
+  rram_solver_s* solver = nullptr;
 };
 
 static thread_local std::string g_caffe_err;
@@ -427,7 +430,13 @@ int rram_solver_create(const char* sp, const char* np, const char* options, rram
   });
 }
 int rram_solver_destroy(rram_solver_t s) {
-  return guarded([&] { delete s; });
+  return guarded([&] {
+    if (s && s->dp) {  // a P2PSync still attached: detach it (its hooks point into this solver)
+      s->dp->sync.reset();
+      s->dp->solver = nullptr;
+    }
+    delete s;
+  });
 }
 int rram_solver_set_graph(rram_solver_t s, int enable) {
   return guarded([&] {
@@ -861,6 +870,7 @@ int rram_dp_create(rram_solver_t s, rram_comm_t c, double bucket_mb, int overlap
     s->bwd_cb = nullptr;
     s->solver->on_gradients_ready = nullptr;
     s->solver->net()->on_backward_layer = nullptr;
+    CAFFE_CHECK(s->dp == nullptr, "rram_dp_create: the solver already has a P2PSync attached");
     auto* d = new rram_dp_s;
     try {
       d->sync = std::make_unique<P2PSync<float>>(s->solver.get(), c->comm, bucket_mb, overlap != 0);
@@ -868,6 +878,8 @@ int rram_dp_create(rram_solver_t s, rram_comm_t c, double bucket_mb, int overlap
       delete d;
       throw;
     }
+    d->solver = s;
+    s->dp = d;
     *out = d;
   });
 }
@@ -881,11 +893,15 @@ int rram_solver_flat_params(rram_solver_t s, float** data, float** diff, int64_t
   });
 }
 int rram_dp_destroy(rram_dp_t dp) {
-  return guarded([&] { delete dp; });
+  return guarded([&] {
+    if (dp && dp->solver) dp->solver->dp = nullptr;
+    delete dp;
+  });
 }
 int rram_dp_info(rram_dp_t dp, long long* allreduce_calls, long long* bucket_calls, int* buckets, int64_t* params) {
   return guarded([&] {
     NEED(dp);
+    CAFFE_CHECK(dp->sync != nullptr, "rram_dp_info: the P2PSync's solver was destroyed");
     if (allreduce_calls) *allreduce_calls = dp->sync->allreduce_calls();
     if (bucket_calls) *bucket_calls = dp->sync->bucket_calls();
     if (buckets) *buckets = dp->sync->buckets();

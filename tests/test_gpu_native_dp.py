@@ -119,3 +119,30 @@ def test_native_mc_stats_allreduce_world1(device):
         comm.close()
         mc.close()
         net.close()
+
+
+def test_native_p2psync_solver_destroyed_first(device):
+    """Destroying the solver before its P2PSync detaches the sync (its hooks
+    point into the solver): the later rram_dp_destroy only frees the handle,
+    rram_dp_info reports the detached state, and a second P2PSync on one
+    solver is refused."""
+    import ctypes as C
+    from rramsim import caffe
+    sp, net, opts = _c4()
+    caffe.set_stream_from_torch()
+    caffe.set_random_seed(1701)
+    comm = caffe.Comm(0, 1)
+    try:
+        s = caffe.Solver(sp, net, opts)
+        dp = caffe.P2PSync(s, comm)
+        with pytest.raises(Exception):
+            caffe.P2PSync(s, comm)                 # one per solver
+        s.step(1)
+        assert dp.info()["allreduce_calls"] == 1
+        s.close()                                  # the solver goes first
+        lib = caffe.load()
+        a = C.c_longlong()
+        assert lib.rram_dp_info(dp.h, C.byref(a), None, None, None) != 0
+        dp.close()
+    finally:
+        comm.close()
