@@ -614,23 +614,54 @@ __device__ __forceinline__ void conv_epilogue_nchw16(floatx4 (&acc)[MI][NJ], con
   const int HWo = static_cast<int>(ep.hw.d);
   const int mw = mwave + 4 * g;
   const bool rows_full = mwave + MI * 16 <= P.M;
-  const bool row_bias = ep.bias_mode == RRAM_BIAS_ROW, col_bias = ep.bias_mode == RRAM_BIAS_COL;
+  // (every octet-kernel launch passes a row bias or none: no column bias)
+  const bool row_bias = ep.bias_mode == RRAM_BIAS_ROW;
   const bool relu = ep.relu != 0;
   const bool store = ep.C != nullptr;  // uniform
   const float alpha = ep.alpha;
+  // The wave's 16 MI row biases by scalar loads (the constant address space;
+  // whole blocks when every row is in range), each lane taking its row
+  // group's, before the first store (round 5 loaded a value per column block
+  // between the stores, each load waiting in the in-order vmcnt for every
+  // store before it; time unchanged, profiles/r06_ab_cb16_epilogue.txt)
   float bz[MI][4];
+  if (row_bias) {
+    const int mb = __builtin_amdgcn_readfirstlane(mwave);
+    typedef const __attribute__((address_space(4))) float cfloat;
+    typedef float float8v __attribute__((ext_vector_type(8)));
+    typedef const __attribute__((address_space(4))) float8v cfloat8;
+    float sv[16 * MI];
+    if (rows_full) {
 #pragma unroll
-  for (int i = 0; i < MI; ++i)
+      for (int b = 0; b < 2 * MI; ++b) {
+        const float8v v = *(cfloat8*)((cfloat*)ep.bias + mb + 8 * b);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = mw + 16 * i + r;
-      bz[i][r] = *((row_bias && m < P.M) ? ep.bias + m : g_zero4);
+        for (int e = 0; e < 8; ++e) sv[8 * b + e] = v[e];
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 16 * MI; ++e) {
+        const float v = ((cfloat*)ep.bias)[min(mb + e, P.M - 1)];
+        sv[e] = mb + e < P.M ? v : 0.0f;
+      }
     }
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float* s = sv + 16 * i + r;
+        bz[i][r] = g == 0 ? s[0] : g == 1 ? s[4] : g == 2 ? s[8] : s[12];
+      }
+  } else {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bz[i][r] = 0.0f;
+  }
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int n = nwave + 16 * j + c16;
     if (n >= P.N || n >= nlim) continue;
-    const float cb = *(col_bias ? ep.bias + n : g_zero4);
     const uint32_t im = fdiv(static_cast<uint32_t>(n), ep.hw);
     const uint32_t sp = static_cast<uint32_t>(n) - im * ep.hw.d;
     const uint32_t base = static_cast<uint32_t>((im * ep.cimg + sp + static_cast<int64_t>(mw) * HWo) * 4);
@@ -639,7 +670,7 @@ __device__ __forceinline__ void conv_epilogue_nchw16(floatx4 (&acc)[MI][NJ], con
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float o = (alpha * acc[i][j][r] + bz[i][r]) + cb;
+        const float o = (alpha * acc[i][j][r] + bz[i][r]) + 0.0f;  // (+ the absent column bias: -0 -> +0 as before)
         acc[i][j][r] = o;
         ov[i][r] = relu ? fmaxf(o, 0.0f) : o;
       }
@@ -680,6 +711,16 @@ __device__ __forceinline__ unsigned long long cb_stamp() {
 }
 #endif
 
+// RRAM_CB16_ABLATE (diagnostic builds only, wrong results), a bit mask of
+// the parts left out: 1 the K loop's B fragment reads (the MFMAs reuse the
+// prologue's), 2 its weight loads, 4 the next K-tile's patch staging (loads
+// and LDS stores), 8 its barriers, 16 the epilogue's stores.  Read with care:
+// stale operands (1, 2) and unwritten outputs (16: the layers after it then
+// multiply zeros) lower the chip's power and raise its clock, so part of
+// those savings is DVFS, not the removed work (profiles/r06_ab_cb16_ablate.txt)
+#ifndef RRAM_CB16_ABLATE
+#define RRAM_CB16_ABLATE 0
+#endif
 // KTO = KT & 1 (the K-tile count's parity, host-checked): one tail shape per
 // instantiation.  With both tails in one kernel (a runtime branch after the
 // K-tile pair loop) the register allocator could not keep the loop's values
@@ -804,9 +845,15 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
   auto xg_of = [&](int z) { return xpack + (int64_t)z * (cv.C >> 3) * (PL >> 1); };
   auto xbytes_of = [&](int z) { return xrange - static_cast<uint32_t>(z * (cv.C >> 3)) * PL; };
   // K-tile kt's patch piece i of tile geometry tg into stage stg (LDS-DMA)
-  auto issue = [&](const int4v& rs, int kt, int stg, int i) {
-    dma_b128(rs, poff(i) + static_cast<uint32_t>(kt) * 2u * PL,
-             lds0 + static_cast<uint32_t>(stg * SFB + (wave * PD + i) * 1024));
+  // (K-tile 0 of a tile: every offset read before the first DMA -- a DMA
+  // writes LDS, so the compiler kept each offset read behind the DMA before
+  // it, one LDS round trip per piece)
+  auto issue_kt0 = [&](const int4v& rs, int stg) {
+    uint32_t po[PD];
+#pragma unroll
+    for (int i = 0; i < PD; ++i) po[i] = poff(i);
+#pragma unroll
+    for (int i = 0; i < PD; ++i) dma_b128(rs, po[i], lds0 + static_cast<uint32_t>(stg * SFB + (wave * PD + i) * 1024));
   };
   // this wave's weight fragments through a buffer resource: the group's
   // offset is uniform (SGPR soffset), the lane's 16 bytes the only VGPR
@@ -885,8 +932,7 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
   set_poff(cur.nseg, cur.p1, cur.p2, cur.R, cur.f0, cur.img0);
   {
     const int4v rs0 = make_rsrc(reinterpret_cast<const float*>(xg_of(cur.z)), xbytes_of(cur.z));
-#pragma unroll
-    for (int i = 0; i < PD; ++i) issue(rs0, 0, 0, i);
+    issue_kt0(rs0, 0);
     load_a_from(a_rsrc(cur), fa[0], 0);
   }
   for (;;) {
@@ -942,7 +988,7 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
         constexpr int NKIND = ODD ? 0 : (gi + 1 < H ? 0 : 2);
         constexpr int NS0 = ODD ? 2 * gi : 2 * (gi + 1);
         const int q = q0 + gi;
-        if (MORE) {
+        if (MORE && !(RRAM_CB16_ABLATE & 4)) {
           if (gi >= SD) {
             constexpr int g0 = gi - SD;
 #pragma unroll
@@ -955,18 +1001,19 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
                 int4x, __builtin_amdgcn_raw_buffer_load_b128(
                            xr, static_cast<int>(poff(i) + static_cast<uint32_t>(kt + 1) * 2u * PL), 0, 0));
         }
-        if (gi + 1 < NG || MORE) load_a(fa[pa ^ 1], q + 1);
+        if ((gi + 1 < NG || MORE) && !(RRAM_CB16_ABLATE & 2)) load_a(fa[pa ^ 1], q + 1);
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
           const bool last = gi == NG - 1 && j == NJ - 1;
-          if (last && MORE) {  // the next stage is complete
+          if (last && MORE && !(RRAM_CB16_ABLATE & 8)) {  // the next stage is complete
             RRAM_CB_ST(ODD ? H + gi : gi);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
             RRAM_CB_ST(2 * H + 1);
           }
-          if (!last) {
+          if (RRAM_CB16_ABLATE & 1) {
+          } else if (!last) {
             if (j + 1 < NJ)  // (the cross group: lower half from the stage before)
               read_b(fb[(j + 1) & 1], KIND == 1 ? oth : cur_st, cur_st, KIND, S0, j + 1);
             else
@@ -990,7 +1037,7 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
         RRAM_CB_ST(ODD ? H + gi : gi);
         // every wave is past the cross group: the refill -- or, after the
         // tile's last K-tile, the next tile's patch -- may overwrite `oth`
-        if (ODD && gi == 0 && (MORE || more_tiles)) {
+        if (ODD && gi == 0 && (MORE || more_tiles) && !(RRAM_CB16_ABLATE & 8)) {
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           __builtin_amdgcn_s_barrier();
           __builtin_amdgcn_sched_barrier(0);
@@ -1032,13 +1079,23 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
       set_poff(nxt.nseg, nxt.p1, nxt.p2, nxt.R, nxt.f0, nxt.img0);
       const int4v rsn = make_rsrc(reinterpret_cast<const float*>(xg_of(nxt.z)), xbytes_of(nxt.z));
       const int sfree = (KT ^ sp) & 1;
-#pragma unroll
-      for (int i = 0; i < PD; ++i) issue(rsn, 0, sfree, i);
+      issue_kt0(rsn, sfree);
       load_a_from(a_rsrc(nxt), fa[1], 0);
     }
     const int mwave = cur.m0 + 32 * wr, nwave = cur.n0 + wc * 32 * NB;
+    if (RRAM_CB16_ABLATE & 16) {  // keep the sums alive: one store under a condition never true at run time
+      float sum = 0.0f;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sum += acc[i][j][r];
+      if (ep.relu == 12345 && ep.C != nullptr) ep.C[lane] = sum;
+      ep.C = nullptr;
+    }
     conv_epilogue_nchw16<MI, NJ>(acc, P, ep, mwave, nwave, c16, g, cur.plast + 1);
-    if (yoct != nullptr) {
+    if (yoct != nullptr && !(RRAM_CB16_ABLATE & 16)) {
       // the output's octet companion: lane group g holds rows 4 g .. 4 g + 3 of
       // both 16-row blocks; lanes g, g ^ 1 (lane ^ 16) trade one block so that
       // an even g stores octet g / 2 of block 0 and an odd g octet (g - 1) / 2
