@@ -129,6 +129,9 @@ def main():
     ap.add_argument("--seed", type=int, default=1701)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-layers", action="store_true", help="print the per-layer table to stderr")
+    ap.add_argument("--no-conv-flip-cache", action="store_true",
+                    help="training workloads: flip each convolution kernel per backward instead of taking the copy "
+                         "the fused update wrote (net option conv_flip_cache; A/B runs)")
     ap.add_argument("--layer-events", choices=["dominant", "none"], default="dominant",
                     help="hipEvents in the timed region: around the dominant kernel's layer (roofline) or none")
     ap.add_argument("--workload", default="alexnet_mc",

@@ -244,6 +244,13 @@ typedef struct rram_update_seg {
   float decay, local_rate, thr;
   int apply_thr;
   unsigned long long* broken_count; /* may be NULL */
+  /* Optional (NULL: off).  A convolution kernel w [G*cout][cin][taps] also
+   * written, once updated, transposed per group and rotated 180 degrees into
+   * w_flip [G*cin][cout][taps] (G*cin*cout*taps == n): the weights of the
+   * stride-1 data gradient as a forward convolution, which
+   * rram_conv2d_bwd_ex then takes instead of flipping them itself. */
+  float* w_flip;
+  int flip_groups, flip_cin, flip_cout, flip_taps;
 } rram_update_seg;
 int rram_fused_update_fail_batched(const rram_update_seg* segs, int nsegs, float momentum,
                                    float decrement, float eps, rram_stream_t stream);
@@ -410,6 +417,15 @@ int rram_conv2d_bwd(const rram_conv_desc* d, const float* x, const float* w,
                     const float* dy, float* dw, float* db, float* dx,
                     void* workspace, size_t workspace_bytes,
                     rram_stream_t stream);
+/* rram_conv2d_bwd with the flipped kernel supplied: w_flipped (nullable) holds
+ * w in rram_update_seg's w_flip layout, read by the stride-1 data gradient in
+ * place of the flip pass (conv_layer.cu:47-52's data GEMM as a forward
+ * convolution).  rram_conv2d_flip_applies(d) = 1 when that path serves d. */
+int rram_conv2d_bwd_ex(const rram_conv_desc* d, const float* x, const float* w,
+                       const float* w_flipped, const float* dy, float* dw, float* db,
+                       float* dx, void* workspace, size_t workspace_bytes,
+                       rram_stream_t stream);
+int rram_conv2d_flip_applies(const rram_conv_desc* d);
 
 /* Replaces im2col_gpu / col2im_gpu (src/caffe/util/im2col.cu:41-62,
  * :300-320).  One image; col is [C*kh*kw][Ho*Wo]. col2im writes (not adds) im. */

@@ -119,6 +119,17 @@ __global__ void __launch_bounds__(256) k_flip_kernel(const float* __restrict__ w
   }
 }
 
+// the stride-1 data gradient as a forward convolution with the flipped
+// kernel: padding dil (k - 1) - pad >= 0 per axis, 32-bit sizes (d: shape
+// filled by rram_conv_out_shape)
+bool flip_geometry_ok(const rram_conv_desc& d) {
+  const int eph = d.dilation_h * (d.kernel_h - 1) - d.pad_h, epw = d.dilation_w * (d.kernel_w - 1) - d.pad_w;
+  const size_t wt_bytes = (size_t)d.channels * (d.num_output / d.group) * d.kernel_h * d.kernel_w * sizeof(float);
+  return d.stride_h == 1 && d.stride_w == 1 && eph >= 0 && epw >= 0 && wt_bytes < (1ull << 31) &&
+         (int64_t)d.num * d.height * d.width < (1ll << 31) &&
+         (int64_t)d.num * d.num_output * d.out_h * d.out_w * 4 < (1ll << 31);
+}
+
 int check_desc(const rram_conv_desc* d) {
   RRAM_REQUIRE(d != nullptr, "conv: desc is NULL");
   RRAM_REQUIRE(d->num >= 0 && d->channels > 0 && d->height > 0 && d->width > 0 &&
@@ -303,6 +314,19 @@ size_t rram_conv2d_bwd_workspace(const rram_conv_desc* d_in, int images_per_chun
 
 int rram_conv2d_bwd(const rram_conv_desc* d_in, const float* x, const float* w, const float* dy,
                     float* dw, float* db, float* dx, void* ws, size_t ws_bytes, rram_stream_t st) {
+  return rram_conv2d_bwd_ex(d_in, x, w, nullptr, dy, dw, db, dx, ws, ws_bytes, st);
+}
+
+int rram_conv2d_flip_applies(const rram_conv_desc* d_in) {
+  if (d_in == nullptr) return 0;
+  rram_conv_desc d = *d_in;
+  if (rram_conv_out_shape(&d) != RRAM_OK) return 0;
+  return flip_geometry_ok(d) ? 1 : 0;
+}
+
+int rram_conv2d_bwd_ex(const rram_conv_desc* d_in, const float* x, const float* w, const float* w_flipped,
+                       const float* dy, float* dw, float* db, float* dx, void* ws, size_t ws_bytes,
+                       rram_stream_t st) {
   rram_conv_desc d = *d_in;
   int rc = rram_conv_out_shape(&d);
   if (rc) return rc;
@@ -363,17 +387,19 @@ int rram_conv2d_bwd(const rram_conv_desc* d_in, const float* x, const float* w, 
   // since the thin convolution forwards split K, the flipped-kernel forward
   // wins there too: CIFAR-10 full training 0.419-0.421 -> 0.408-0.411 ms per
   // iteration, profiles/r05_ab_occ2_plans.txt)
-  const bool dx_fwd = dx && d.stride_h == 1 && d.stride_w == 1 &&
-                      eph >= 0 && epw >= 0 &&
-                      ws != nullptr && ws_bytes >= wt_bytes && wt_bytes < (1ull << 31) &&
-                      (int64_t)d.num * d.height * d.width < (1ll << 31) &&
-                      (int64_t)d.num * d.num_output * HoWo * 4 < (1ll << 31);
+  // (w_flipped: the caller's copy, rram_update_seg.w_flip, no flip pass)
+  const bool dx_fwd = dx && flip_geometry_ok(d) && (w_flipped != nullptr || (ws != nullptr && ws_bytes >= wt_bytes));
   auto dx_as_fwd = [&]() -> int {
-    float* wt = static_cast<float*>(ws);
-    const int64_t n = (int64_t)d.channels * cout_g * T;
-    hipLaunchKernelGGL(k_flip_kernel, dim3(stream_blocks(n)), dim3(256), 0, s, w, wt, G, cin_g, cout_g, T);
-    int r = launch_status("conv bwd kernel flip");
-    if (r) return r;
+    const float* wt = w_flipped;
+    int r = 0;
+    if (wt == nullptr) {
+      float* wf = static_cast<float*>(ws);
+      const int64_t n = (int64_t)d.channels * cout_g * T;
+      hipLaunchKernelGGL(k_flip_kernel, dim3(stream_blocks(n)), dim3(256), 0, s, w, wf, G, cin_g, cout_g, T);
+      r = launch_status("conv bwd kernel flip");
+      if (r) return r;
+      wt = wf;
+    }
     rram_conv_desc t{d.num, d.num_output, d.out_h, d.out_w, d.channels, d.kernel_h, d.kernel_w,
                      eph, epw, 1, 1, d.dilation_h, d.dilation_w, G, 0, 0};
     r = rram_conv_out_shape(&t);

@@ -538,6 +538,17 @@ __global__ void __launch_bounds__(256)
         if (wr) wi = wv;
       }
       w[i] = wi;
+      if (sg.w_flip != nullptr) {  // (the host checked G cin cout taps == n < 2^31)
+        const int T = sg.flip_taps, ci = sg.flip_cin, co = sg.flip_cout;
+        int t = static_cast<int>(i);
+        const int tap = t % T;
+        t /= T;
+        const int c = t % ci;
+        t /= ci;
+        const int o = t % co;
+        const int gr = t / co;
+        sg.w_flip[((gr * ci + c) * co + o) * T + (T - 1 - tap)] = wi;
+      }
     }
   }
   if (cur >= 0) block_count_flush(cnt, segs.s[cur].broken_count);
@@ -946,6 +957,11 @@ int rram_fused_update_fail_batched(const rram_update_seg* segs, int nsegs, float
     if (sg.n > 0) RRAM_REQUIRE(sg.w && sg.g && sg.h, "fused_update_fail_batched: segment %d NULL pointer", i);
     RRAM_REQUIRE((sg.endurance == nullptr) == (sg.values == nullptr),
                  "fused_update_fail_batched: segment %d endurance/values mismatch", i);
+    if (sg.w_flip != nullptr)
+      RRAM_REQUIRE(sg.flip_groups > 0 && sg.flip_cin > 0 && sg.flip_cout > 0 && sg.flip_taps > 0 &&
+                       (int64_t)sg.flip_groups * sg.flip_cin * sg.flip_cout * sg.flip_taps == sg.n && sg.n < (1ll << 31),
+                   "fused_update_fail_batched: segment %d flip geometry %d x %d x %d x %d != n %lld", i, sg.flip_groups,
+                   sg.flip_cin, sg.flip_cout, sg.flip_taps, (long long)sg.n);
     us.s[i] = sg;
     us.chunk_start[i + 1] = us.chunk_start[i] + (sg.n + kUpdChunk - 1) / kUpdChunk;
   }

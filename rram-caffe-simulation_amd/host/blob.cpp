@@ -38,6 +38,22 @@ SyncedMemory::~SyncedMemory() {
   if (own_gpu_ && gpu_ptr_) (void)hipFree(gpu_ptr_);
   if (oct_ptr_) (void)hipFree(oct_ptr_);
   if (wp_ptr_) (void)hipFree(wp_ptr_);
+  if (wf_ptr_) (void)hipFree(wf_ptr_);
+}
+
+void* SyncedMemory::wflip(size_t bytes) {
+  if (bytes > wf_bytes_) {
+    if (wf_ptr_) {
+      HIP_CALL(hipStreamSynchronize(Caffe::hip_stream()));
+      HIP_CALL(hipFree(wf_ptr_));
+      Caffe::scratch_gen().fetch_add(1);
+    }
+    wf_ptr_ = nullptr;
+    HIP_CALL(hipMalloc(&wf_ptr_, bytes));
+    wf_bytes_ = bytes;
+    wf_valid_ = false;
+  }
+  return wf_ptr_;
 }
 
 void* SyncedMemory::wpack(size_t bytes) {
@@ -138,6 +154,7 @@ const void* SyncedMemory::gpu_data() {
 void* SyncedMemory::mutable_cpu_data() {
   oct_valid_ = false;
   wp_valid_ = false;
+  wf_valid_ = false;
   fp32_stale = false;
   to_cpu();
   head_ = HEAD_AT_CPU;
@@ -146,6 +163,7 @@ void* SyncedMemory::mutable_cpu_data() {
 void* SyncedMemory::mutable_gpu_data() {
   oct_valid_ = false;
   wp_valid_ = false;
+  wf_valid_ = false;
   fp32_stale = false;
   to_gpu();
   head_ = HEAD_AT_GPU;
@@ -155,6 +173,7 @@ void SyncedMemory::set_cpu_data(void* data) {
   CAFFE_CHECK(data, "set_cpu_data(NULL)");
   oct_valid_ = false;
   wp_valid_ = false;
+  wf_valid_ = false;
   fp32_stale = false;
   if (own_cpu_ && cpu_ptr_) std::free(cpu_ptr_);
   cpu_ptr_ = data;
@@ -165,6 +184,7 @@ void SyncedMemory::set_gpu_data(void* data) {
   CAFFE_CHECK(data, "set_gpu_data(NULL)");
   oct_valid_ = false;
   wp_valid_ = false;
+  wf_valid_ = false;
   fp32_stale = false;
   if (own_gpu_ && gpu_ptr_) (void)hipFree(gpu_ptr_);
   gpu_ptr_ = data;

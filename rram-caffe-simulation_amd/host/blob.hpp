@@ -63,6 +63,19 @@ class SyncedMemory {
   }
   void drop_wpack() { wp_valid_ = false; }
 
+  // Flipped-kernel companion (rram_update_seg.w_flip): these convolution
+  // weights transposed per group and rotated 180 degrees, written by the
+  // solver's fused update next to the weights, read by the stride-1 data
+  // gradient (rram_conv2d_bwd_ex).  Valid for the Solver::Step call that
+  // wrote it (Caffe::step_epoch) until the next mutable_* / set_* access.
+  void* wflip(size_t bytes);  // the buffer, grown to `bytes`
+  bool wflip_valid(uint64_t epoch) const { return wf_valid_ && epoch != 0 && wf_epoch_ == epoch; }
+  void set_wflip_valid(uint64_t epoch) {
+    wf_epoch_ = epoch;
+    wf_valid_ = wf_ptr_ != nullptr && epoch != 0;
+  }
+  void drop_wflip() { wf_valid_ = false; }
+
  private:
   void to_cpu();
   void to_gpu();
@@ -79,6 +92,10 @@ class SyncedMemory {
   size_t wp_bytes_ = 0;
   bool wp_valid_ = false;
   uint64_t wp_key_ = 0;
+  void* wf_ptr_ = nullptr;
+  size_t wf_bytes_ = 0;
+  bool wf_valid_ = false;
+  uint64_t wf_epoch_ = 0;
   bool exposed_ = false;
 };
 

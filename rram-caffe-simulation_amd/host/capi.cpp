@@ -865,12 +865,13 @@ int rram_dp_create(rram_solver_t s, rram_comm_t c, double bucket_mb, int overlap
     NEED(c);
     NEED(out);
     CAFFE_CHECK(bucket_mb > 0, "rram_dp_create: bucket_mb must be > 0");
+    // (refused before any hook is touched: the attached sync keeps its own)
+    CAFFE_CHECK(s->dp == nullptr, "rram_dp_create: the solver already has a P2PSync attached");
     // the sync owns both hooks while attached
     s->grad_cb = nullptr;
     s->bwd_cb = nullptr;
     s->solver->on_gradients_ready = nullptr;
     s->solver->net()->on_backward_layer = nullptr;
-    CAFFE_CHECK(s->dp == nullptr, "rram_dp_create: the solver already has a P2PSync attached");
     auto* d = new rram_dp_s;
     try {
       d->sync = std::make_unique<P2PSync<float>>(s->solver.get(), c->comm, bucket_mb, overlap != 0);

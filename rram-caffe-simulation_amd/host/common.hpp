@@ -67,13 +67,28 @@ class Caffe {
   // kernel library's rram_scratch_generation).
   static std::atomic<uint64_t>& scratch_gen();
   static void synchronize();
+  // Nonzero while a Solver::Step call runs, a fresh value per call: the
+  // flipped convolution kernels one iteration's fused update writes
+  // (SyncedMemory::wflip) are read by the next iteration's backward only
+  // within the call that wrote them -- no caller code runs between the two
+  // but the gradient-sync hooks, which write diffs only.
+  static uint64_t step_epoch() { return Get().epoch_; }
+  static void set_step_epoch(uint64_t e) { Get().epoch_ = e; }
 
  private:
   Caffe() = default;
   rram_stream_t stream_ = nullptr;
   uint64_t seed_ = 1701;
+  uint64_t epoch_ = 0;
   void* ws_ = nullptr;
   size_t ws_bytes_ = 0;
 };
+
+// the working stream is inside a hipGraph capture (relaxed mode: the query is allowed)
+inline bool stream_capturing() {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  HIP_CALL(hipStreamIsCapturing(Caffe::hip_stream(), &st));
+  return st == hipStreamCaptureStatusActive;
+}
 
 }  // namespace caffe

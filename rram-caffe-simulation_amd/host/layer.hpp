@@ -98,6 +98,9 @@ class Layer {
   // will read the companion of an input shaped like `bottom` (engine and plan
   // as they stand then)
   virtual bool set_octet_reader(Layer* /*reader*/) { return false; }
+  // a convolution whose data gradient reads its kernel flipped: the geometry
+  // of blobs()[0] for rram_update_seg.w_flip (ConvolutionLayer)
+  virtual bool flip_geometry(int* /*g*/, int* /*cin_g*/, int* /*cout_g*/, int* /*taps*/) const { return false; }
   virtual bool input_octets_now(const Blob<Dtype>* /*bottom*/) const { return false; }
   // ReLU fold into a Pooling producer (Net::Net, any phase): an in-place ReLU
   // right after a layer that accepts it is applied in that layer's output

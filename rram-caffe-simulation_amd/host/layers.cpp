@@ -186,6 +186,17 @@ void ConvolutionLayer<Dtype>::Reshape(const std::vector<Blob<Dtype>*>& bottom,
   }
   // ask the producer of the input for its octet companion
   if (want_in_oct_) bottom[0]->data()->wants_octets = true;
+  flip_ok_ = this->phase_ == TRAIN && rram_conv2d_flip_applies(&desc_) == 1;
+}
+
+template <typename Dtype>
+bool ConvolutionLayer<Dtype>::flip_geometry(int* g, int* cin_g, int* cout_g, int* taps) const {
+  if (!flip_ok_) return false;
+  *g = desc_.group;
+  *cin_g = desc_.channels / desc_.group;
+  *cout_g = desc_.num_output / desc_.group;
+  *taps = desc_.kernel_h * desc_.kernel_w;
+  return true;
 }
 
 // the octet companion a producer writes next to top (nullptr: not wanted).
@@ -319,11 +330,18 @@ void ConvolutionLayer<Dtype>::Backward_gpu(const std::vector<Blob<Dtype>*>& top,
   // then ran two im2col + weight-GEMM + split-K passes instead of one)
   int imgs = std::max(1, std::min(desc_.num, (int)std::min<size_t>(256, (1ull << 30) / std::max<size_t>(need, 1))));
   void* ws = Caffe::workspace(rram_conv2d_bwd_workspace(&desc_, imgs) + 256);
-  RRAM_CALL(rram_conv2d_bwd(&desc_, bottom[0]->gpu_data(), this->blobs_[0]->gpu_data(),
-                            top[0]->gpu_diff(), dw ? this->blobs_[0]->mutable_gpu_diff() : nullptr,
-                            db ? this->blobs_[1]->mutable_gpu_diff() : nullptr,
-                            dx ? bottom[0]->mutable_gpu_diff() : nullptr, ws, Caffe::workspace_size(),
-                            Caffe::stream()));
+  // the flipped kernel the last fused update of this Solver::Step call wrote
+  // next to the weights (Solver::FusedTail), unless a graph is being captured
+  // (a replay must not depend on the host-side companion state)
+  const float* wf = nullptr;
+  SyncedMemory& wm = *this->blobs_[0]->data();
+  if (dx && flip_ok_ && wm.wflip_valid(Caffe::step_epoch()) && !stream_capturing())
+    wf = static_cast<const float*>(wm.wflip(0));
+  RRAM_CALL(rram_conv2d_bwd_ex(&desc_, bottom[0]->gpu_data(), this->blobs_[0]->gpu_data(), wf,
+                               top[0]->gpu_diff(), dw ? this->blobs_[0]->mutable_gpu_diff() : nullptr,
+                               db ? this->blobs_[1]->mutable_gpu_diff() : nullptr,
+                               dx ? bottom[0]->mutable_gpu_diff() : nullptr, ws, Caffe::workspace_size(),
+                               Caffe::stream()));
 }
 
 // ★ ------------------------------------------------------ InnerProduct

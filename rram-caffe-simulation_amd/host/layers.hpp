@@ -43,6 +43,10 @@ class ConvolutionLayer : public Layer<Dtype> {
   // a convolution taking its octet companion; each forward that both sides
   // confirm (rram_conv_output_octets_only, the reader's input_octets_now)
   // writes only the companion (the pooled-output fold's convolution form)
+  // (TRAIN phase) the stride-1 data gradient runs as a forward convolution
+  // with the flipped kernel (rram_conv2d_flip_applies): its geometry, for
+  // the solver's fused update to write that kernel (rram_update_seg.w_flip)
+  bool flip_geometry(int* g, int* cin_g, int* cout_g, int* taps) const override;
   bool set_octet_reader(Layer<Dtype>* reader) override {
     if (reader != nullptr && (this->phase_ != TEST || concat_top_ != nullptr)) return false;
     octet_reader_ = reader;
@@ -61,6 +65,7 @@ class ConvolutionLayer : public Layer<Dtype> {
   Blob<Dtype>* concat_top_ = nullptr;  // write_into_concat: the output goes to this top at channel concat_off_
   int concat_off_ = 0;
   Layer<Dtype>* octet_reader_ = nullptr;  // convolution-output fold: the top's only reader
+  bool flip_ok_ = false;
 };
 
 // ★ InnerProduct (inner_product_layer.cpp:9-141, .cu:9-75).

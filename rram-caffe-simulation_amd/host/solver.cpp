@@ -188,6 +188,7 @@ Solver<Dtype>::Solver(const Msg& sp, const Msg* net_param, const Msg& options) :
   if (sp.has("random_seed") && sp.integer("random_seed") >= 0)
     Caffe::set_random_seed(static_cast<uint64_t>(sp.integer("random_seed")));
   fused_update_ = options.boolean("fused_update", false);
+  flip_cache_ = options.boolean("conv_flip_cache", true);
   const Msg np = load_net_param(sp, net_param);
   net_ = std::make_shared<Net<Dtype>>(np, TRAIN, options);
   // solver.cpp:132-148: fault maker and strategies on the root solver
@@ -367,6 +368,25 @@ void Solver<Dtype>::FusedTail() {
     HIP_CALL(hipMemsetAsync(counts, 0, fi.size() * sizeof(unsigned long long), Caffe::hip_stream()));
   // one launch for all blobs (rram_fused_update_fail_batched; a net with more
   // learnable blobs than one launch takes goes one launch per RRAM_MAX_SEGS)
+  // The flipped kernels of the convolutions whose stride-1 data gradient
+  // reads them (Layer::flip_geometry) come out of the same pass, for the next
+  // iteration's backward within this Step call (Caffe::step_epoch); not while
+  // a graph is captured.  They replace a flip launch per layer per iteration.
+  const uint64_t epoch = Caffe::step_epoch();
+  struct Flip {
+    SyncedMemory* m;
+    int g, ci, co, t;
+  };
+  std::vector<Flip> flips;
+  if (flip_cache_ && epoch != 0 && !stream_capturing())
+    for (const auto& l : net_->layers()) {
+      Flip f{};
+      if (!l->blobs().empty() && l->flip_geometry(&f.g, &f.ci, &f.co, &f.t)) {
+        f.m = l->blobs()[0]->data().get();
+        flips.push_back(f);
+      }
+    }
+  std::vector<SyncedMemory*> flipped;
   std::vector<rram_update_seg> segs;
   for (int i = 0; i < (int)ps.size(); ++i) {
     int f = -1;
@@ -385,11 +405,22 @@ void Solver<Dtype>::FusedTail() {
     sg.apply_thr = (faulty && thr) ? 1 : 0;
     sg.thr = (faulty && thr) ? thr->threshold_for(f) : 0.0f;
     sg.broken_count = (faulty && counts) ? counts + f : nullptr;
+    for (const Flip& fl : flips)
+      if (fl.m == ps[i]->data().get() && (int64_t)fl.g * fl.ci * fl.co * fl.t == sg.n) {
+        sg.w_flip = static_cast<float*>(fl.m->wflip(static_cast<size_t>(sg.n) * sizeof(Dtype)));
+        sg.flip_groups = fl.g;
+        sg.flip_cin = fl.ci;
+        sg.flip_cout = fl.co;
+        sg.flip_taps = fl.t;
+        flipped.push_back(fl.m);
+        break;
+      }
     segs.push_back(sg);
   }
   for (size_t b = 0; b < segs.size(); b += RRAM_MAX_SEGS)
     RRAM_CALL(rram_fused_update_fail_batched(segs.data() + b, (int)std::min<size_t>(RRAM_MAX_SEGS, segs.size() - b), mom,
                                              gm ? gm->decrement : 100.0f, gm ? gm->epsilon : 1e-20f, Caffe::stream()));
+  for (SyncedMemory* m : flipped) m->set_wflip_valid(epoch);
 }
 
 template <typename Dtype>
@@ -471,6 +502,15 @@ void Solver<Dtype>::capture_launch(int k, F&& body) {
 // solver.cpp:237-325 (fork order: ComputeUpdate -> ApplyStrategy -> ApplyUpdate -> Fail)
 template <typename Dtype>
 void Solver<Dtype>::Step(int iters) {
+  // a fresh Caffe::step_epoch for this call (the flipped-kernel companions
+  // written by its updates are read only within it), 0 again on the way out
+  struct EpochScope {
+    EpochScope() {
+      static std::atomic<uint64_t> next{0};
+      Caffe::set_step_epoch(++next);
+    }
+    ~EpochScope() { Caffe::set_step_epoch(0); }
+  } epoch_scope;
   const int stop = iter_ + iters;
   const int display = (int)param_.integer("display", 0);
   const int test_interval = (int)param_.integer("test_interval", 0);
@@ -526,6 +566,9 @@ void Solver<Dtype>::Step(int iters) {
         if (warm) {
           capture_launch(1, [&] { FusedTail(); });
           graph_rate_ = rate;
+          // a replayed update rewrote the weights without FusedTail's host
+          // side: no flipped kernel written before it is current
+          for (auto* p : net_->learnable_params()) p->data()->drop_wflip();
         } else {
           FusedTail();
         }

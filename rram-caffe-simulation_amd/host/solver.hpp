@@ -286,6 +286,7 @@ class Solver {
   Dtype smoothed_loss_ = 0;
   std::vector<Dtype> losses_;
   bool fused_update_ = false;
+  bool flip_cache_ = true;  // option conv_flip_cache: FusedTail writes the flipped kernels (rram_update_seg.w_flip)
 };
 
 // Monte-Carlo fault-map inference (north_star).

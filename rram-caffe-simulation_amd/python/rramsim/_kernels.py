@@ -54,7 +54,9 @@ class FailSeg(C.Structure):
 class UpdateSeg(C.Structure):
     _fields_ = [("w", C.c_void_p), ("g", C.c_void_p), ("h", C.c_void_p), ("endurance", C.c_void_p),
                 ("values", C.c_void_p), ("n", C.c_int64), ("decay", C.c_float), ("local_rate", C.c_float),
-                ("thr", C.c_float), ("apply_thr", C.c_int), ("broken_count", C.c_void_p)]
+                ("thr", C.c_float), ("apply_thr", C.c_int), ("broken_count", C.c_void_p),
+                ("w_flip", C.c_void_p), ("flip_groups", C.c_int), ("flip_cin", C.c_int), ("flip_cout", C.c_int),
+                ("flip_taps", C.c_int)]
 
 
 class ConvDesc(C.Structure):
@@ -118,6 +120,8 @@ SIGNATURES = {
     "rram_pack_octets": (I, [P, P, I, I, I, I, P]),
     "rram_conv2d_bwd_workspace": (SZ, [P, I]),
     "rram_conv2d_bwd": (I, [P, P, P, P, P, P, P, P, SZ, P]),
+    "rram_conv2d_bwd_ex": (I, [P, P, P, P, P, P, P, P, P, SZ, P]),
+    "rram_conv2d_flip_applies": (I, [P]),
     "rram_im2col": (I, [P, I, I, I, I, I, I, I, I, I, I, I, P, P]),
     "rram_col2im": (I, [P, I, I, I, I, I, I, I, I, I, I, I, P, P]),
     "rram_ip_fwd": (I, [P, P, P, P, I, I, I, I, I, P, SZ, P]),

@@ -101,13 +101,19 @@ def _dist_on():
     return dist.is_available() and dist.is_initialized()
 
 
-def _timed(world, dev, fn, steps, warmup, net=None):
+def _timed(world, dev, fn, steps, warmup, net=None, block=None):
     """Warmup, then `steps` timed calls bracketed by barrier + synchronize;
     max over ranks.  With `net`, its hipEvent timers run around the
-    Convolution / InnerProduct layers during the timed calls only."""
+    Convolution / InnerProduct layers during the timed calls only.  With
+    `block`, the warmup and the timed steps are one call each, block(n), as
+    `caffe train` runs Solver::Step over all its iterations."""
     import torch
     import torch.distributed as dist
-    for i in range(warmup):
+    if block is not None:
+        fn = None
+        if warmup:
+            block(warmup)
+    for i in range(warmup if fn is not None else 0):
         fn(i)
     torch.cuda.synchronize()
     if net is not None:
@@ -117,8 +123,11 @@ def _timed(world, dev, fn, steps, warmup, net=None):
     parallel.barrier()        # the C++ host's RCCL communicator when bench.py set one, else torch.distributed
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(steps):
-        fn(warmup + i)
+    if block is not None:
+        block(steps)
+    else:
+        for i in range(steps):
+            fn(warmup + i)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     if net is not None:
@@ -287,11 +296,13 @@ def run_workload(args, world, rank, dev):
             sp = models.solver(base_lr=0.01, momentum=0.9, weight_decay=0.0005, lr_policy="inv", gamma=0.0001,
                                power=0.75, max_iter=100000, failure_mean=5e3, failure_std=1e3,
                                failure_prob=(10, 20, 10))
-        opts = dict(opts, fused_update=True)
+        opts = dict(opts, fused_update=True, conv_flip_cache=not getattr(args, "no_conv_flip_cache", False))
         # bucketed gradient all-reduce overlapped with backward (world > 1 only)
         dp = DataParallelSolver(sp, net_txt, opts, seed=args.seed, overlap=True)
         dp.solver.set_graph(_graph_on())  # iteration as two hipGraphs around the all-reduce (opt-in)
-        el = _timed(world, dev, lambda i: dp.step(1), args.steps, args.warmup)
+        # one Step call per region (the flipped kernels an update writes serve
+        # the next backward within a call, Caffe::step_epoch)
+        el = _timed(world, dev, None, args.steps, args.warmup, block=dp.step)
         res = _base(f"fault-aware training images/sec, {args.workload}", "images/s",
                     world * args.steps * batch / el, world, args, el, workload=args.workload,
                     model=args.workload.split("_")[0], global_batch=batch * world,

@@ -31,9 +31,10 @@ def test_kernel_structs_match_header():
     assert ctypes.sizeof(K.InjectCfg) == 56
     assert ctypes.sizeof(K.InjectSeg) == 8 + 8 + 8 + 4 + 4 + 56
     assert ctypes.sizeof(K.FailSeg) == 40
-    # 5 pointers, n, 3 floats + int, counter pointer
-    assert ctypes.sizeof(K.UpdateSeg) == 5 * 8 + 8 + 4 * 4 + 8
+    # 5 pointers, n, 3 floats + int, counter pointer, flipped-kernel pointer + 4 ints
+    assert ctypes.sizeof(K.UpdateSeg) == 5 * 8 + 8 + 4 * 4 + 8 + 8 + 4 * 4
     assert K.UpdateSeg.broken_count.offset == 64
+    assert K.UpdateSeg.w_flip.offset == 72 and K.UpdateSeg.flip_taps.offset == 92
     assert ctypes.sizeof(K.ConvDesc) == 16 * 4
 
 
@@ -58,6 +59,19 @@ def test_invalid_args_return_status_not_abort():
     seg = K.UpdateSeg(None, None, None, None, None, -1, 0.0, 0.0, 0.0, 0, None)
     assert lib.rram_fused_update_fail_batched(ctypes.byref(seg), 1, 0.9, 100.0, 1e-20, None) == K.RRAM_EINVAL
     assert lib.rram_fused_update_fail_batched(None, 33, 0.9, 100.0, 1e-20, None) == K.RRAM_EINVAL
+    # a flipped-kernel destination whose geometry does not cover the segment
+    seg = K.UpdateSeg(ctypes.c_void_p(16), ctypes.c_void_p(16), ctypes.c_void_p(16), None, None, 100, 0.0, 0.0, 0.0, 0,
+                      None, ctypes.c_void_p(16), 2, 3, 4, 9)
+    assert lib.rram_fused_update_fail_batched(ctypes.byref(seg), 1, 0.9, 100.0, 1e-20, None) == K.RRAM_EINVAL
+    assert b"flip geometry" in lib.rram_last_error()
+    # the flipped-kernel data gradient serves stride 1 with padding <= dil (k - 1) only
+    d = K.ConvDesc(8, 32, 16, 16, 32, 5, 5, 2, 2, 1, 1, 1, 1, 1, 0, 0)
+    assert lib.rram_conv2d_flip_applies(ctypes.byref(d)) == 1
+    d = K.ConvDesc(8, 3, 227, 227, 96, 11, 11, 0, 0, 4, 4, 1, 1, 1, 0, 0)
+    assert lib.rram_conv2d_flip_applies(ctypes.byref(d)) == 0
+    d = K.ConvDesc(8, 32, 16, 16, 32, 3, 3, 3, 3, 1, 1, 1, 1, 1, 0, 0)   # pad 3 > k - 1
+    assert lib.rram_conv2d_flip_applies(ctypes.byref(d)) == 0
+    assert lib.rram_conv2d_flip_applies(None) == 0
     # zero-size work is a successful no-op that never touches the device
     assert lib.rram_fail_apply(None, None, None, None, 0, 100.0, 1e-20, None, None) == K.RRAM_OK
 

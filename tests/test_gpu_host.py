@@ -179,6 +179,33 @@ def test_fused_tail_matches_reference_order(rs):
     assert sum(ref[2]) > 0                              # some cells broke along the way
 
 
+def test_flip_cache_same_bits(rs):
+    """The fused update writes each stride-1 convolution's flipped kernel next
+    to its weights (rram_update_seg.w_flip) and the next backward of the same
+    Step call reads it instead of flipping (conv_layer.cu:47-52's data
+    gradient as a forward convolution): CIFAR-10 full (conv2 / conv3 take it),
+    two Step calls (the second starts on the flip pass again), bit-identical
+    weights, endurance and counts with the cache off."""
+    caffe, models = rs
+
+    def run(cache):
+        caffe.set_random_seed(31)
+        sp = models.solver(base_lr=0.001, momentum=0.9, weight_decay=0.004, max_iter=100,
+                           failure_mean=2e3, failure_std=1e3, failure_prob=(5, 90, 5), threshold=0.001)
+        f, _, _ = models.CONFIGS["cifar10_full"]
+        s = caffe.Solver(sp, f(train_batch=32, test_batch=32),
+                         models.net_options("cifar10_full", fused_update=True, conv_flip_cache=cache))
+        s.step(3)
+        s.step(2)
+        out = ([N(p["data"]) for p in s.net.params()], [N(e) for e, _ in s.fail_state()], s.broken_counts())
+        s.close()
+        return out
+
+    on, off = run(True), run(False)
+    _assert_states_bit_equal(on, off)
+    assert sum(on[2]) > 0
+
+
 def test_fused_flag_with_remapping_runs_reference_order(rs, tmp_path):
     """[threshold, remapping] cannot be fused: fused_update=true must fall back
     to the reference order and give exactly the unfused result."""
