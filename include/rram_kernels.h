@@ -261,6 +261,10 @@ int rram_axpy(int64_t n, float alpha, const float* x, float* y, rram_stream_t st
 int rram_axpby(int64_t n, float alpha, const float* x, float beta, float* y, rram_stream_t stream);
 int rram_scal(int64_t n, float alpha, float* x, rram_stream_t stream);
 int rram_set(int64_t n, float alpha, float* x, rram_stream_t stream);
+/* a[0..na) = 0 and b[0..nb) = 0 in one launch: the solver's per-iteration
+ * clears (Net::ClearParamDiffs over the flat diff, net.cpp:566-576 in the
+ * reference, and the Fail counters) where two fills ran. */
+int rram_zero_pair(float* a, int64_t na, unsigned long long* b, int64_t nb, rram_stream_t stream);
 int rram_add(int64_t n, const float* a, const float* b, float* y, rram_stream_t stream);
 int rram_sign(int64_t n, const float* x, float* y, rram_stream_t stream);
 /* out[0] = sum(|x|) (device scalar). */

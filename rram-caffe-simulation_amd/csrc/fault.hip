@@ -571,6 +571,15 @@ __global__ void k_scal(int64_t n, float a, float* __restrict__ x) {
        i += (int64_t)gridDim.x * blockDim.x)
     x[i] = a * x[i];
 }
+// the solver's per-iteration clears in one launch: a[0..na) (the flat
+// parameter diff) and b[0..nb) (the Fail counters)
+__global__ void __launch_bounds__(256) k_zero_pair(float* __restrict__ a, int64_t na, unsigned long long* __restrict__ b,
+                                                   int64_t nb) {
+  const int64_t t0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x, st = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = t0; i < na; i += st) a[i] = 0.0f;
+  for (int64_t i = t0; i < nb; i += st) b[i] = 0ull;
+}
+
 __global__ void k_set(int64_t n, float a, float* __restrict__ x) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -1001,6 +1010,14 @@ int rram_set(int64_t n, float a, float* x, rram_stream_t s) {
   RRAM_REQUIRE(x, "set: NULL");
   hipLaunchKernelGGL(k_set, dim3(stream_blocks(n)), dim3(kThreads), 0, as_stream(s), n, a, x);
   return launch_status("set");
+}
+int rram_zero_pair(float* a, int64_t na, unsigned long long* b, int64_t nb, rram_stream_t s) {
+  RRAM_REQUIRE(na >= 0 && nb >= 0, "zero_pair: negative count");
+  RRAM_REQUIRE((na == 0 || a) && (nb == 0 || b), "zero_pair: NULL");
+  const int64_t n = na > nb ? na : nb;
+  if (n == 0) return RRAM_OK;
+  hipLaunchKernelGGL(k_zero_pair, dim3(stream_blocks(n)), dim3(kThreads), 0, as_stream(s), a, na, b, nb);
+  return launch_status("zero_pair");
 }
 int rram_add(int64_t n, const float* a, const float* b, float* y, rram_stream_t s) {
   RRAM_REQUIRE(n >= 0, "add: n < 0");

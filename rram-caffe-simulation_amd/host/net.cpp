@@ -566,13 +566,22 @@ void Net<Dtype>::Update() {
 }
 
 template <typename Dtype>
-void Net<Dtype>::ClearParamDiffs() {
-  if (flat_diff_) {  // every learnable diff lives in one buffer: one memset
-    HIP_CALL(hipMemsetAsync(flat_diff_, 0, flat_param_count() * sizeof(Dtype), Caffe::hip_stream()));
+void Net<Dtype>::ClearParamDiffs(unsigned long long* also, int64_t n_also) {
+#ifndef RRAM_ZERO_PAIR  // A/B builds: 0 = the round-5 clears (a memset here, the counters' in FusedTail)
+#define RRAM_ZERO_PAIR 1
+#endif
+  if (flat_diff_ && RRAM_ZERO_PAIR) {  // every learnable diff lives in one buffer: one launch, with the caller's counters
+    RRAM_CALL(rram_zero_pair(flat_diff_, flat_param_count(), also, also ? n_also : 0, Caffe::stream()));
     return;
   }
-  for (auto* p : learnable_params_)
-    HIP_CALL(hipMemsetAsync(p->mutable_gpu_diff(), 0, p->count() * sizeof(Dtype), Caffe::hip_stream()));
+  if (flat_diff_) {
+    HIP_CALL(hipMemsetAsync(flat_diff_, 0, flat_param_count() * sizeof(Dtype), Caffe::hip_stream()));
+  } else {
+    for (auto* p : learnable_params_)
+      HIP_CALL(hipMemsetAsync(p->mutable_gpu_diff(), 0, p->count() * sizeof(Dtype), Caffe::hip_stream()));
+  }
+  if (also && n_also > 0)
+    HIP_CALL(hipMemsetAsync(also, 0, n_also * sizeof(unsigned long long), Caffe::hip_stream()));
 }
 
 template <typename Dtype>

@@ -38,7 +38,8 @@ class Net {
     return l;
   }
   void Update();
-  void ClearParamDiffs();
+  // also (nullable): n_also counters cleared in the same launch (the solver's Fail counters)
+  void ClearParamDiffs(unsigned long long* also = nullptr, int64_t n_also = 0);
   void ShareTrainedLayersWith(const Net* other);
   // .caffemodel weights (net.cpp:765-880, binary proto only; io.hpp)
   void CopyTrainedLayersFrom(const NetProtoData& param);

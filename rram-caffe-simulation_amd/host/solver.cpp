@@ -363,9 +363,8 @@ void Solver<Dtype>::FusedTail() {
       strategys_.empty() ? nullptr : dynamic_cast<ThresholdFailureStrategy<Dtype>*>(strategys_[0].get());
   auto* gm = dynamic_cast<GaussianFailureMaker<Dtype>*>(fmaker_.get());
   std::vector<Blob<Dtype>*> fi = fmaker_ ? fmaker_->fail_iterations() : std::vector<Blob<Dtype>*>();
+  // (cleared with the parameter diffs at the iteration's start, Step)
   unsigned long long* counts = fmaker_ ? fmaker_->device_counts() : nullptr;
-  if (counts)
-    HIP_CALL(hipMemsetAsync(counts, 0, fi.size() * sizeof(unsigned long long), Caffe::hip_stream()));
   // one launch for all blobs (rram_fused_update_fail_batched; a net with more
   // learnable blobs than one launch takes goes one launch per RRAM_MAX_SEGS)
   // The flipped kernels of the convolutions whose stride-1 data gradient
@@ -525,6 +524,9 @@ void Solver<Dtype>::Step(int iters) {
     fusable_strategies = fusable_strategies && dynamic_cast<ThresholdFailureStrategy<Dtype>*>(st.get()) != nullptr;
   const bool can_fuse = fused_update_ && fusable_strategies && param_.num("clip_gradients", -1.0) < 0 &&
                         iter_size == 1 && param_.str("regularization_type", "L2") == "L2";
+  // the fused tail's Fail counters are cleared with the parameter diffs (one launch)
+  unsigned long long* fail_counts = can_fuse && fmaker_ ? fmaker_->device_counts() : nullptr;
+  const int64_t n_fail_counts = fail_counts ? static_cast<int64_t>(fmaker_->fail_iterations().size()) : 0;
   while (iter_ < stop) {
     const bool test_now =
         test_interval && iter_ % test_interval == 0 && (iter_ > 0 || param_.boolean("test_initialization", true));
@@ -551,7 +553,7 @@ void Solver<Dtype>::Step(int iters) {
         if (gx_[0] && (rate != graph_rate_ || moved)) drop_graphs();
         if (moved) warm = false;
         auto fb = [&] {
-          net_->ClearParamDiffs();
+          net_->ClearParamDiffs(fail_counts, n_fail_counts);
           net_->Forward(false);
           net_->Backward();
         };
@@ -580,7 +582,7 @@ void Solver<Dtype>::Step(int iters) {
       if (snap && iter_ % snap == 0) Snapshot();
       continue;
     }
-    net_->ClearParamDiffs();
+    net_->ClearParamDiffs(fail_counts, n_fail_counts);
     if (test_now) TestAll();
     net_->set_iter((uint64_t)iter_);
     Dtype loss = 0;

@@ -99,6 +99,7 @@ SIGNATURES = {
     "rram_axpby": (I, [I64, F, P, F, P, P]),
     "rram_scal": (I, [I64, F, P, P]),
     "rram_set": (I, [I64, F, P, P]),
+    "rram_zero_pair": (I, [P, I64, P, I64, P]),
     "rram_add": (I, [I64, P, P, P, P]),
     "rram_sign": (I, [I64, P, P, P]),
     "rram_asum": (I, [I64, P, P, P]),
