@@ -451,6 +451,18 @@ int rram_col2im(const float* col, int channels, int height, int width,
 int rram_ip_fwd(const float* x, const float* w, const float* bias, float* y,
                 int M, int N, int K, int transpose, int relu, void* workspace,
                 size_t workspace_bytes, rram_stream_t stream);
+/* The bf16x6 engine's packed-row form of an InnerProduct input, for
+ * inference chains (fc6 -> fc7): its bytes and tile rows for an M x K input of
+ * an N-output layer (rows_per_tile nullable; 0: the engine does not serve the
+ * shape).  rram_ip_fwd_rows = rram_ip_fwd (W [N][K], no transpose) where x_rows
+ * (nullable) already holds x in that form (no pack pass) and y_rows (nullable)
+ * receives y in the form of the next layer (its rows_per_tile; K = N there),
+ * written by the split-K reduce (inner_product_layer.cu:9-30 forwards, the same
+ * bits; *y_rows_written = 0 when the engine did not serve this shape). */
+size_t rram_ip_rows_pack_bytes(int M, int N, int K, size_t ws_bytes, int* rows_per_tile);
+int rram_ip_fwd_rows(const float* x, const void* x_rows, const float* w, const float* bias, float* y, void* y_rows,
+                     int y_rows_per_tile, int M, int N, int K, int relu, void* ws, size_t ws_bytes,
+                     int* y_rows_written, rram_stream_t stream);
 /* dw += ..., db += ... (nullable), dx = ... (nullable). */
 int rram_ip_bwd(const float* x, const float* w, const float* dy, float* dw,
                 float* db, float* dx, int M, int N, int K, int transpose,

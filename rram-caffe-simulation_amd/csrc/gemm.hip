@@ -1601,7 +1601,7 @@ int release_conv_tables() {
 // Shared by the C-ABI entry points in conv_api.hip.
 int gemm_x6_nt(int M, int N, int K, float alpha, const float* A, int lda, const float* B, int ldb, float beta,
                float* C, int ldc, const float* bias, int bias_mode, int relu, void* ws, size_t ws_bytes,
-               hipStream_t s);
+               hipStream_t s, const void* a_rows = nullptr, char* y_rows = nullptr, int y_bmc = 0);
 
 int gemm_core(int trans_a, int trans_b, int M, int N, int K, float alpha, const float* A, int lda,
               const float* B, int ldb, float beta, float* C, int ldc, const float* bias,

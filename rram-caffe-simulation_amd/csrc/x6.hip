@@ -2262,6 +2262,67 @@ __global__ void __launch_bounds__(256) k_pack_rows_x6(const float* __restrict__ 
   }
 }
 
+
+// k_splitk_reduce for a row-major InnerProduct output that also writes it in
+// the packed-row form the next k_gemm_x6 reads (rram_ip_fwd_rows: fc6 ->
+// fc7): one thread per (row, 8 columns), each element k_splitk_reduce's
+// (partials in split order, alpha, bias, ReLU; beta = 0), then those 8 values
+// as k_pack_rows_x6 stores them (the consumer's K-tile record, its pad zeroed
+// by the unit holding the tile's last 8 columns).  Host: N % 32 == 0, M a
+// multiple of the consumer's tile rows, C rows 16-byte aligned.
+__global__ void __launch_bounds__(256) k_splitk_reduce_rows_x6(const float* __restrict__ ws, int split, int M, int N,
+                                                               Epi ep, char* __restrict__ pack, int BMc, int ktiles,
+                                                               int units) {
+  const int64_t total = (int64_t)M * N;
+  const int n8 = N >> 3;
+  for (int u = blockIdx.x * blockDim.x + threadIdx.x; u < units; u += gridDim.x * blockDim.x) {
+    const int m = u / n8, n0 = 8 * (u - m * n8);
+    // splitk_sum of 8 consecutive elements: the partials as 16-byte loads, 8
+    // splits in flight, each element's adds in split order (same bits)
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = 0.0f;
+    const float* p0 = ws + (int64_t)m * N + n0;
+    int z = 0;
+    for (; z + 8 <= split; z += 8) {
+      float4 q[8][2];
+#pragma unroll
+      for (int zz = 0; zz < 8; ++zz) {
+        q[zz][0] = *reinterpret_cast<const float4*>(p0 + (int64_t)(z + zz) * total);
+        q[zz][1] = *reinterpret_cast<const float4*>(p0 + (int64_t)(z + zz) * total + 4);
+      }
+#pragma unroll
+      for (int zz = 0; zz < 8; ++zz) {
+        v[0] += q[zz][0].x; v[1] += q[zz][0].y; v[2] += q[zz][0].z; v[3] += q[zz][0].w;
+        v[4] += q[zz][1].x; v[5] += q[zz][1].y; v[6] += q[zz][1].z; v[7] += q[zz][1].w;
+      }
+    }
+    for (; z < split; ++z) {
+      const float4 a = *reinterpret_cast<const float4*>(p0 + (int64_t)z * total);
+      const float4 b = *reinterpret_cast<const float4*>(p0 + (int64_t)z * total + 4);
+      v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+      v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int n = n0 + j;
+      float o = ep.alpha * v[j];
+      if (ep.bias_mode == RRAM_BIAS_ROW) o += ep.bias[m];
+      else if (ep.bias_mode == RRAM_BIAS_COL) o += ep.bias[n];
+      if (ep.relu) o = fmaxf(o, 0.0f);
+      v[j] = o;
+    }
+    float* dst = ep.C + (int64_t)m * ep.ldc + n0;
+    *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(dst + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    const int kt = n0 >> 5, kk = n0 & 31, h = kk >> 4, g = (kk >> 3) & 1;
+    const int tm = m / BMc, row = m - tm * BMc;
+    char* rowp = pack + (((int64_t)tm * ktiles + kt) * BMc + row) * gx6::RLB;
+    x6::store_terms8(v, rowp + (g * 2 + h) * 48);
+    if (g == 1 && h == 1) *reinterpret_cast<uint4*>(rowp + 192) = make_uint4(0, 0, 0, 0);
+  }
+}
+
 }  // namespace
 
 float* pack_buffer(size_t floats, hipStream_t s);  // gemm.hip
@@ -2946,9 +3007,13 @@ bool gemm_x6_plan(int M, int N, int K, size_t ws_bytes, GemmPlan& pl) {
 // k_gemm_x6 for C = act(alpha * A . B^T + bias) with A [M][lda], B [N][ldb]
 // row-major fp32 (16-byte aligned rows), beta = 0.  Returns 1 when it ran, 0
 // when not covered (the caller runs the fp32-MFMA GEMM), < 0 on error.
+// a_rows (nullable): A already in the packed-row form of this plan (no pack
+// pass); y_rows (nullable): C also written in the packed-row form of a
+// consumer with y_bmc rows per tile and K = N (by the split-K reduce when it
+// can, else by a pack pass of C)
 int gemm_x6_nt(int M, int N, int K, float alpha, const float* A, int lda, const float* B, int ldb, float beta,
                float* C, int ldc, const float* bias, int bias_mode, int relu, void* ws, size_t ws_bytes,
-               hipStream_t s) {
+               hipStream_t s, const void* a_rows, char* y_rows, int y_bmc) {
   if (f32_engine().load(std::memory_order_relaxed) != RRAM_ENGINE_BF16X6 || beta != 0.0f) return 0;
   auto al16 = [](const void* p, int ld) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0 && ld % 4 == 0; };
   if (!al16(A, lda) || !al16(B, ldb)) return 0;
@@ -2959,13 +3024,18 @@ int gemm_x6_nt(int M, int N, int K, float alpha, const float* A, int lda, const 
   const int split = pl.split, ktc = pl.ktc;
   const int64_t tiles = (int64_t)tiles_m * tiles_n;
   const int64_t total = (int64_t)tiles_m * ktiles * BMc * (gx6::RLB / 2);
-  uint16_t* ap = reinterpret_cast<uint16_t*>(pack_buffer(static_cast<size_t>((total + 1) / 2), s));
-  RRAM_REQUIRE(ap != nullptr, "gemm x6: packed-operand buffer allocation failed");
-  const int units = tiles_m * BMc * ktiles * 4;
-  hipLaunchKernelGGL(k_pack_rows_x6, dim3(stream_blocks(units)), dim3(256), 0, s, A, (int64_t)lda, M, K,
-                     reinterpret_cast<char*>(ap), BMc, ktiles, units);
-  int rc = launch_status("gemm x6 pack");
-  if (rc) return rc;
+  const uint16_t* ap = static_cast<const uint16_t*>(a_rows);
+  int rc = 0;
+  if (ap == nullptr) {
+    uint16_t* pb = reinterpret_cast<uint16_t*>(pack_buffer(static_cast<size_t>((total + 1) / 2), s));
+    RRAM_REQUIRE(pb != nullptr, "gemm x6: packed-operand buffer allocation failed");
+    const int units = tiles_m * BMc * ktiles * 4;
+    hipLaunchKernelGGL(k_pack_rows_x6, dim3(stream_blocks(units)), dim3(256), 0, s, A, (int64_t)lda, M, K,
+                       reinterpret_cast<char*>(pb), BMc, ktiles, units);
+    rc = launch_status("gemm x6 pack");
+    if (rc) return rc;
+    ap = pb;
+  }
   Params P{};
   P.M = M;
   P.N = N;
@@ -2986,10 +3056,26 @@ int gemm_x6_nt(int M, int N, int K, float alpha, const float* A, int lda, const 
     hipLaunchKernelGGL((k_gemm_x6<4, 2>), dim3(nwg), dim3(256), 0, s, P, ap, ktiles, ktc);
   rc = launch_status("gemm x6");
   if (rc) return rc;
-  if (split > 1) {
+  const bool rows_in_reduce = y_rows != nullptr && split > 1 && N % 32 == 0 && y_bmc > 0 && M % y_bmc == 0 &&
+                              ldc % 4 == 0 && (reinterpret_cast<uintptr_t>(C) & 15u) == 0;
+  if (split > 1 && rows_in_reduce) {
+    const int units = M * (N / 8);
+    hipLaunchKernelGGL(k_splitk_reduce_rows_x6, dim3(stream_blocks(units)), dim3(256), 0, s, P.ws, split, M, N, P.e,
+                       y_rows, y_bmc, N / gx6::KT, units);
+    rc = launch_status("gemm x6 splitk reduce + rows");
+    if (rc) return rc;
+  } else if (split > 1) {
     hipLaunchKernelGGL(k_splitk_reduce, dim3(stream_blocks((int64_t)M * N)), dim3(256), 0, s, P.ws, split, M, N,
                        P.e);
     rc = launch_status("gemm x6 splitk reduce");
+    if (rc) return rc;
+  }
+  if (y_rows != nullptr && !rows_in_reduce) {  // the consumer's pack of C, as its own call would run it
+    const int ytm = (M + y_bmc - 1) / y_bmc, ykt = (N + gx6::KT - 1) / gx6::KT;
+    const int units = ytm * y_bmc * ykt * 4;
+    hipLaunchKernelGGL(k_pack_rows_x6, dim3(stream_blocks(units)), dim3(256), 0, s, C, (int64_t)ldc, M, N, y_rows,
+                       y_bmc, ykt, units);
+    rc = launch_status("gemm x6 rows of C");
     if (rc) return rc;
   }
   return 1;
@@ -3063,6 +3149,32 @@ int rram_pack_octets(const float* x, void* oct, int num, int channels, int heigh
   if (num == 0) return RRAM_OK;
   RRAM_REQUIRE(x != nullptr && oct != nullptr, "pack_octets: NULL");
   return rram::pack_octets(x, oct, num, channels, height * width, rram::as_stream(s));
+}
+
+size_t rram_ip_rows_pack_bytes(int M, int N, int K, size_t ws_bytes, int* rows_per_tile) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  rram::GemmPlan pl;
+  if (rram::f32_engine().load() != RRAM_ENGINE_BF16X6 || !rram::gemm_x6_plan(M, N, K, ws_bytes, pl)) return 0;
+  if (rows_per_tile) *rows_per_tile = 32 * pl.MI;
+  return (size_t)pl.tiles_m * pl.ktiles * 32 * pl.MI * rram::gx6::RLB;
+}
+
+int rram_ip_fwd_rows(const float* x, const void* x_rows, const float* w, const float* bias, float* y, void* y_rows,
+                     int y_rows_per_tile, int M, int N, int K, int relu, void* ws, size_t ws_bytes,
+                     int* y_rows_written, rram_stream_t st) {
+  RRAM_REQUIRE(M > 0 && N > 0 && K > 0 && x && w && y, "ip_fwd_rows: bad arguments");
+  RRAM_REQUIRE(y_rows == nullptr || y_rows_per_tile > 0, "ip_fwd_rows: y_rows without its tile rows");
+  if (y_rows_written) *y_rows_written = 0;
+  hipStream_t s = rram::as_stream(st);
+  const int rc = rram::gemm_x6_nt(M, N, K, 1.0f, x, K, w, K, 0.0f, y, N, bias, RRAM_BIAS_COL, relu, ws, ws_bytes, s,
+                                  x_rows, static_cast<char*>(y_rows), y_rows_per_tile);
+  if (rc < 0) return rc;
+  if (rc == 0) {  // not served: the plain forward, no rows written
+    RRAM_REQUIRE(x_rows == nullptr, "ip_fwd_rows: x_rows given for a shape the engine does not serve");
+    return rram_ip_fwd(x, w, bias, y, M, N, K, 0, relu, ws, ws_bytes, st);
+  }
+  if (y_rows_written) *y_rows_written = y_rows != nullptr ? 1 : 0;
+  return RRAM_OK;
 }
 
 int rram_f32_engine_for_ip(int M, int N, int K, size_t ws_bytes) {

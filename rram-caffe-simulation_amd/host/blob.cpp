@@ -39,6 +39,22 @@ SyncedMemory::~SyncedMemory() {
   if (oct_ptr_) (void)hipFree(oct_ptr_);
   if (wp_ptr_) (void)hipFree(wp_ptr_);
   if (wf_ptr_) (void)hipFree(wf_ptr_);
+  if (rw_ptr_) (void)hipFree(rw_ptr_);
+}
+
+void* SyncedMemory::rows(size_t bytes) {
+  if (bytes > rw_bytes_) {
+    if (rw_ptr_) {
+      HIP_CALL(hipStreamSynchronize(Caffe::hip_stream()));
+      HIP_CALL(hipFree(rw_ptr_));
+      Caffe::scratch_gen().fetch_add(1);
+    }
+    rw_ptr_ = nullptr;
+    HIP_CALL(hipMalloc(&rw_ptr_, bytes));
+    rw_bytes_ = bytes;
+    rw_valid_ = false;
+  }
+  return rw_ptr_;
 }
 
 void* SyncedMemory::wflip(size_t bytes) {
@@ -155,6 +171,7 @@ void* SyncedMemory::mutable_cpu_data() {
   oct_valid_ = false;
   wp_valid_ = false;
   wf_valid_ = false;
+  rw_valid_ = false;
   fp32_stale = false;
   to_cpu();
   head_ = HEAD_AT_CPU;
@@ -164,6 +181,7 @@ void* SyncedMemory::mutable_gpu_data() {
   oct_valid_ = false;
   wp_valid_ = false;
   wf_valid_ = false;
+  rw_valid_ = false;
   fp32_stale = false;
   to_gpu();
   head_ = HEAD_AT_GPU;
@@ -174,6 +192,7 @@ void SyncedMemory::set_cpu_data(void* data) {
   oct_valid_ = false;
   wp_valid_ = false;
   wf_valid_ = false;
+  rw_valid_ = false;
   fp32_stale = false;
   if (own_cpu_ && cpu_ptr_) std::free(cpu_ptr_);
   cpu_ptr_ = data;
@@ -185,6 +204,7 @@ void SyncedMemory::set_gpu_data(void* data) {
   oct_valid_ = false;
   wp_valid_ = false;
   wf_valid_ = false;
+  rw_valid_ = false;
   fp32_stale = false;
   if (own_gpu_ && gpu_ptr_) (void)hipFree(gpu_ptr_);
   gpu_ptr_ = data;

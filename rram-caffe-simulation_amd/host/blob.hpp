@@ -76,6 +76,20 @@ class SyncedMemory {
   }
   void drop_wflip() { wf_valid_ = false; }
 
+  // Packed-rows companion (rram_ip_fwd_rows): an InnerProduct input in the
+  // bf16x6 engine's packed-row form, written by the producing InnerProduct's
+  // split-K reduce for one key (the consumer's rows per tile and shape), valid
+  // until the next mutable_* / set_* access, like the octet companion.
+  // wants_rows: the key a consumer asked for at Reshape (0: none).
+  void* rows(size_t bytes);  // the buffer, grown to `bytes`
+  const void* valid_rows(uint64_t key) const { return rw_valid_ && !exposed_ && rw_key_ == key ? rw_ptr_ : nullptr; }
+  void set_rows_valid(uint64_t key) {
+    rw_key_ = key;
+    rw_valid_ = rw_ptr_ != nullptr;
+  }
+  uint64_t wants_rows = 0;
+  size_t wants_rows_bytes = 0;
+
  private:
   void to_cpu();
   void to_gpu();
@@ -92,6 +106,10 @@ class SyncedMemory {
   size_t wp_bytes_ = 0;
   bool wp_valid_ = false;
   uint64_t wp_key_ = 0;
+  void* rw_ptr_ = nullptr;
+  size_t rw_bytes_ = 0;
+  bool rw_valid_ = false;
+  uint64_t rw_key_ = 0;
   void* wf_ptr_ = nullptr;
   size_t wf_bytes_ = 0;
   bool wf_valid_ = false;

@@ -376,14 +376,44 @@ void InnerProductLayer<Dtype>::Reshape(const std::vector<Blob<Dtype>*>& bottom,
   std::vector<int> s(bottom[0]->shape().begin(), bottom[0]->shape().begin() + axis_);
   s.push_back(N_);
   top[0]->Reshape(s);
+  // TEST phase on the bf16x6 engine: ask the producer of the input for its
+  // packed-row form (an InnerProduct producer writes it from its split-K
+  // reduce: fc6 -> fc7), key = (M, K, rows per tile)
+  in_rows_key_ = 0;
+  int bmc = 0;
+  const size_t rb = (this->phase_ == TEST && !transpose_)
+                        ? rram_ip_rows_pack_bytes(M_, N_, K_, ws_request(), &bmc)
+                        : 0;
+#ifndef RRAM_IP_ROWS  // A/B builds: 0 = every InnerProduct packs its own input
+#define RRAM_IP_ROWS 1
+#endif
+  if (RRAM_IP_ROWS && rb > 0 && bmc > 0 && bmc < 4096) {
+    in_rows_key_ = (static_cast<uint64_t>(M_) << 40) | (static_cast<uint64_t>(K_) << 12) | static_cast<uint64_t>(bmc);
+    bottom[0]->data()->wants_rows = in_rows_key_;
+    bottom[0]->data()->wants_rows_bytes = rb;
+  }
 }
 
 template <typename Dtype>
 void InnerProductLayer<Dtype>::Forward_gpu(const std::vector<Blob<Dtype>*>& bottom,
                                            const std::vector<Blob<Dtype>*>& top) {
-  // split-K partials need up to 16 x M x N floats
-  const size_t ws_need = (size_t)16 * M_ * N_ * sizeof(float);
-  void* ws = Caffe::workspace(std::min<size_t>(ws_need, 256ull << 20));
+  void* ws = Caffe::workspace(ws_request());
+  // the packed-row companions (TEST, Reshape): read the input's when its
+  // producer wrote it, write the output's when the consumer asked
+  const void* xr = in_rows_key_ ? bottom[0]->data()->valid_rows(in_rows_key_) : nullptr;
+  SyncedMemory& ym = *top[0]->data();
+  const uint64_t ykey = (this->phase_ == TEST && !transpose_) ? ym.wants_rows : 0;
+  if (xr != nullptr || ykey != 0) {
+    float* y = top[0]->mutable_gpu_data();  // (drops the old companion; written again below)
+    void* yr = ykey ? ym.rows(ym.wants_rows_bytes) : nullptr;
+    int written = 0;
+    RRAM_CALL(rram_ip_fwd_rows(bottom[0]->gpu_data(), xr, this->blobs_[0]->gpu_data(),
+                               bias_term_ ? this->blobs_[1]->gpu_data() : nullptr, y, yr,
+                               static_cast<int>(ykey & 0xFFF), M_, N_, K_, fused_relu ? 1 : 0, ws,
+                               Caffe::workspace_size(), &written, Caffe::stream()));
+    if (written) ym.set_rows_valid(ykey);
+    return;
+  }
   RRAM_CALL(rram_ip_fwd(bottom[0]->gpu_data(), this->blobs_[0]->gpu_data(),
                         bias_term_ ? this->blobs_[1]->gpu_data() : nullptr,
                         top[0]->mutable_gpu_data(), M_, N_, K_, transpose_ ? 1 : 0,

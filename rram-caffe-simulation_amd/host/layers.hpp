@@ -89,6 +89,9 @@ class InnerProductLayer : public Layer<Dtype> {
                     const std::vector<Blob<Dtype>*>& bottom) override;
   int M_ = 0, N_ = 0, K_ = 0, axis_ = 1;
   bool bias_term_ = true, transpose_ = false;
+  // split-K partials need up to 16 x M x N floats (<= 256 MB)
+  size_t ws_request() const { return std::min<size_t>((size_t)16 * M_ * N_ * sizeof(float), 256ull << 20); }
+  uint64_t in_rows_key_ = 0;  // the packed-row companion this layer reads (Reshape; 0: none)
 };
 
 template <typename Dtype>

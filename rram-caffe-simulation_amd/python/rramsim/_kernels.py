@@ -127,6 +127,8 @@ SIGNATURES = {
     "rram_col2im": (I, [P, I, I, I, I, I, I, I, I, I, I, I, P, P]),
     "rram_ip_fwd": (I, [P, P, P, P, I, I, I, I, I, P, SZ, P]),
     "rram_ip_bwd": (I, [P, P, P, P, P, P, I, I, I, I, P]),
+    "rram_ip_rows_pack_bytes": (SZ, [I, I, I, SZ, P]),
+    "rram_ip_fwd_rows": (I, [P, P, P, P, P, P, I, I, I, I, I, P, SZ, P, P]),
     "rram_relu_fwd": (I, [P, P, I64, F, P]),
     "rram_relu_bwd": (I, [P, P, P, I64, F, P]),
     "rram_pool_fwd": (I, [P, P, P] + [I] * 13 + [P]),

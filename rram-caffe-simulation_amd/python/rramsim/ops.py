@@ -283,6 +283,22 @@ def ip_fwd(x, w, bias, y, M, N, K_, transpose=False, relu=False, workspace=None)
                                _p(workspace), wsb, _stream()), "ip_fwd")
 
 
+def ip_rows_pack_bytes(M, N, K_, ws_bytes):
+    """(bytes, rows per tile) of the bf16x6 engine's packed-row input form (0, 0: not served)."""
+    bmc = C.c_int(0)
+    b = _lib().rram_ip_rows_pack_bytes(M, N, K_, ws_bytes, C.byref(bmc))
+    return b, bmc.value
+
+
+def ip_fwd_rows(x, x_rows, w, bias, y, y_rows, y_rows_per_tile, M, N, K_, relu=False, workspace=None):
+    """rram_ip_fwd_rows: returns whether y_rows was written."""
+    wsb = workspace.numel() * workspace.element_size() if workspace is not None else 0
+    written = C.c_int(0)
+    K.check(_lib().rram_ip_fwd_rows(_p(x), _p(x_rows), _p(w), _p(bias), _p(y), _p(y_rows), y_rows_per_tile, M, N,
+                                    K_, int(relu), _p(workspace), wsb, C.byref(written), _stream()), "ip_fwd_rows")
+    return bool(written.value)
+
+
 def ip_bwd(x, w, dy, dw, db, dx, M, N, K_, transpose=False):
     K.check(_lib().rram_ip_bwd(_p(x), _p(w), _p(dy), _p(dw), _p(db), _p(dx), M, N, K_,
                                int(transpose), _stream()), "ip_bwd")

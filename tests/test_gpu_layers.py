@@ -753,3 +753,52 @@ def test_max_pool_bwd_bit_exact(device, shape, k, s, p):
                                 acc = np.float32(acc + g[n, c, a, b])
                     ref[n, c, h, w] = acc
     assert np.array_equal(dx.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+
+
+def test_ip_rows_chain_bit_identical(device):
+    """The packed-row chain of two InnerProducts on the bf16x6 engine
+    (rram_ip_fwd_rows, fc6 -> fc7 at b256): the first layer's split-K reduce
+    writes its output and the second layer's packed input; the second reads
+    that instead of packing -- both outputs bit-identical to rram_ip_fwd
+    (bias, ReLU, the split-K order); an AlexNet TEST forward's fc7 equals
+    rram_ip_fwd over its fc6 blob."""
+    import torch
+    from rramsim import caffe, models, ops
+    torch.manual_seed(3)
+    M, K1, N1, N2 = 256, 9216, 4096, 4096
+    x = torch.randn(M, K1, device=device)
+    w1 = torch.randn(N1, K1, device=device) * 0.01
+    b1 = torch.randn(N1, device=device)
+    w2 = torch.randn(N2, N1, device=device) * 0.01
+    b2 = torch.randn(N2, device=device)
+    ws = torch.empty(64 << 20, dtype=torch.uint8, device=device)
+    wsb = ws.numel()
+    nb, bmc = ops.ip_rows_pack_bytes(M, N2, N1, wsb)
+    assert nb > 0 and bmc > 0
+    rows = torch.empty(nb, dtype=torch.uint8, device=device)
+    y1 = torch.empty(M, N1, device=device)
+    assert ops.ip_fwd_rows(x, None, w1, b1, y1, rows, bmc, M, N1, K1, relu=True, workspace=ws)
+    y2 = torch.empty(M, N2, device=device)
+    assert not ops.ip_fwd_rows(y1, rows, w2, b2, y2, None, 0, M, N2, N1, relu=True, workspace=ws)
+    r1 = torch.empty_like(y1)
+    ops.ip_fwd(x, w1, b1, r1, M, N1, K1, relu=True, workspace=ws)
+    r2 = torch.empty_like(y2)
+    ops.ip_fwd(r1, w2, b2, r2, M, N2, N1, relu=True, workspace=ws)
+    torch.cuda.synchronize()
+    assert torch.equal(y1.view(torch.int32), r1.view(torch.int32))
+    assert torch.equal(y2.view(torch.int32), r2.view(torch.int32))
+    # the net: fc7 (read through fc6's packed rows) == rram_ip_fwd over the fc6 blob
+    caffe.set_stream_from_torch()
+    caffe.set_random_seed(1701)
+    net = caffe.Net(models.alexnet(test_batch=256), "test", models.net_options("alexnet"))
+    net.forward()
+    fc6 = net.blob("fc6").detach().clone()
+    fc7 = net.blob("fc7").detach().clone()
+    ps = net.params()
+    w7, b7 = ps[12]["data"], ps[13]["data"]
+    assert w7.numel() == 4096 * 4096 and b7.numel() == 4096
+    ref = torch.empty_like(fc7)
+    ops.ip_fwd(fc6, w7, b7, ref, 256, 4096, 4096, relu=True, workspace=ws)
+    torch.cuda.synchronize()
+    assert torch.equal(fc7.view(torch.int32), ref.view(torch.int32))
+    net.close()
