@@ -801,4 +801,17 @@ def test_ip_rows_chain_bit_identical(device):
     ops.ip_fwd(fc6, w7, b7, ref, 256, 4096, 4096, relu=True, workspace=ws)
     torch.cuda.synchronize()
     assert torch.equal(fc7.view(torch.int32), ref.view(torch.int32))
+    # pool5 == rram_pool_fwd
+    # over conv5, and fc6 == rram_ip_fwd over pool5
+    conv5 = net.blob("conv5").detach().clone()
+    pool5 = net.blob("pool5").detach().clone()
+    rp = torch.empty_like(pool5)
+    from rramsim import _kernels as KK
+    ops.pool_fwd(conv5, rp, None, (256, 256, 13, 13, 6, 6, 3, 3, 2, 2, 0, 0), KK.RRAM_POOL_MAX)
+    w6, b6 = ps[10]["data"], ps[11]["data"]
+    r6 = torch.empty_like(fc6)
+    ops.ip_fwd(pool5, w6, b6, r6, 256, 4096, 9216, relu=True, workspace=ws)
+    torch.cuda.synchronize()
+    assert torch.equal(pool5.view(torch.int32), rp.view(torch.int32))
+    assert torch.equal(fc6.view(torch.int32), r6.view(torch.int32))
     net.close()
