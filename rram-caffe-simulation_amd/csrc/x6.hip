@@ -1995,6 +1995,238 @@ __global__ void __launch_bounds__(256) k_conv1_pack_x6(const float* __restrict__
   }
 }
 
+// ---------------------------------------------------------------------------
+// k_conv_s2_x6: GoogLeNet conv1 (3 channels, 7 x 7, stride 2, 64 filters) on
+// the bf16x6 engine; the fp32 table-gather GEMM ran it before (round 6).
+//
+// A workgroup computes one tile of 64 filters x 256 output positions of one
+// image, two workgroups per CU (one stages while the other computes).  The
+// tile's input rows (4 output rows at most: 6 + 7 = 13 input rows per
+// channel) are staged once, split into their three bf16 terms, as plain rows
+// [channel][term][row][element], element e = input column e - pw (padding and
+// columns past the row zero).  K order: a K row is (channel, kernel row), 21
+// of them, each padded to 8 kernel columns (column 7 has zero weights and
+// masked B values); MFMA group g takes rows 2g (lane half 0) and 2g + 1 (half
+// 1), 11 groups, row 21 padding.  The im2col values of one K row at output
+// column ow are the 8 consecutive elements 2 ow .. 2 ow + 7 of one slot row:
+// a B fragment term is 16 bytes at a 4-byte aligned per-lane offset (two
+// ds_read2_b32), consecutive lanes 4 bytes apart.  The weight fragments come
+// from L2 into registers two groups ahead (fragment order, k_conv_s2_pack_x6).
+namespace c7x6 {
+constexpr int C = 3, KS = 7, S = 2, KC = 8;
+constexpr int R = C * KS;            // K rows (channel, kernel row)
+constexpr int G = (R + 1) / 2;       // MFMA groups (row 21 is padding)
+constexpr int BM = 64, MI = 2, BN = 256;
+constexpr int OR = 4;                // output rows a tile may touch (OW >= 85)
+constexpr int SR = S * (OR - 1) + KS;  // slot rows per channel: 13
+constexpr int ROWE = 232;            // elements per slot row: S (OW - 1) + KC <= ROWE
+constexpr int TERMB = SR * ROWE * 2; // bytes per (channel, term) plane
+constexpr int CHB = 3 * TERMB;       // bytes per channel
+constexpr int QR = ROWE / 4;         // 4-element staging chunks per row
+constexpr int NCH = C * SR * QR;     // chunks per tile
+constexpr int CPT = (NCH + 255) / 256;
+static_assert((ROWE * 2) % 8 == 0, "8-byte staging stores");
+static_assert(2 * (C * CHB + BM * 4) <= 160 * 1024, "two workgroups per CU");
+// LDS byte offset of K row rr (0 for the padding row, whose B values are masked)
+constexpr int row_off(int rr) { return rr < R ? (rr / KS) * CHB + (rr % KS) * ROWE * 2 : 0; }
+}  // namespace c7x6
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+k_conv_s2_x6(Params P, const x6::bf16x8* __restrict__ wpack, int tiles_per_img, int tiles) {
+  using namespace c7x6;
+  __shared__ __attribute__((aligned(16))) char smem[C * CHB];
+  __shared__ float bias_lds[BM];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lr = lane & 31, lh = lane >> 5;
+  // XCD-aware order: consecutive tiles (which share input rows) on one XCD
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, loc = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+  const int t = __builtin_amdgcn_readfirstlane((xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc);
+  if (t >= tiles) return;  // (uniform per workgroup; nwg == tiles)
+  const int img = t / tiles_per_img, sp0 = (t - img * tiles_per_img) * BN;
+  const int HWo = P.cv.howo.d, OW = P.cv.Wo, H = P.cv.H, W = P.cv.W;
+  const int f = sp0 / OW;
+  if (threadIdx.x < BM)
+    bias_lds[threadIdx.x] = (P.e.bias != nullptr && (int)threadIdx.x < P.M) ? P.e.bias[threadIdx.x] : 0.0f;
+
+  // ---- staging: chunk q = (channel, slot row, 4 elements), one 4-byte load
+  // per element (an element outside the image, in a row outside it or in the
+  // left / right padding loads from past the buffer's range, i.e. zero)
+  {
+    const __amdgpu_buffer_rsrc_t xrs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(P.b.p), 0, static_cast<int>(P.cv.in_bytes), 0x00020000);
+    const int row0 = S * f - P.cv.ph;
+    float v[CPT][4];
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      const int q = min((int)threadIdx.x + 256 * k, NCH - 1);  // (extra chunks redo the last: same bytes)
+      const int c = q / (SR * QR), rem = q - c * (SR * QR), ri = rem / QR, e4 = rem - ri * QR;
+      const int row = row0 + ri, col0 = 4 * e4 - P.cv.pw;
+      const bool rok = static_cast<unsigned>(row) < static_cast<unsigned>(H);
+      const int base = ((img * C + c) * H + row) * W + col0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool ok = rok && static_cast<unsigned>(col0 + e) < static_cast<unsigned>(W);
+        v[k][e] = __builtin_bit_cast(
+            float, __builtin_amdgcn_raw_buffer_load_b32(xrs, ok ? 4 * (base + e) : static_cast<int>(0x80000000u), 0, 0));
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      const int q = min((int)threadIdx.x + 256 * k, NCH - 1);
+      const int c = q / (SR * QR), rem = q - c * (SR * QR), ri = rem / QR, e4 = rem - ri * QR;
+      typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+      u32x2 hw, mw, lw;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const x6::float2v xv = {v[k][2 * p], v[k][2 * p + 1]};
+        x6::bf16x2 h;
+        const x6::float2v r1 = x6::bf16_high_safe(xv, h);
+        const x6::bf16x2 m = __builtin_convertvector(x6::clamp_bf16(r1), x6::bf16x2);
+        const x6::float2v r2 = r1 - __builtin_convertvector(m, x6::float2v);
+        const x6::bf16x2 l = __builtin_convertvector(r2, x6::bf16x2);
+        hw[p] = __builtin_bit_cast(uint32_t, h);
+        mw[p] = __builtin_bit_cast(uint32_t, m);
+        lw[p] = __builtin_bit_cast(uint32_t, l);
+      }
+      char* dst = smem + c * CHB + (ri * ROWE + 4 * e4) * 2;
+      *reinterpret_cast<u32x2*>(dst) = hw;
+      *reinterpret_cast<u32x2*>(dst + TERMB) = mw;
+      *reinterpret_cast<u32x2*>(dst + 2 * TERMB) = lw;
+    }
+  }
+  __syncthreads();
+
+  // ---- K loop: 11 groups x (2 row blocks x 2 column blocks) x 6 MFMAs ----
+  uint32_t lb[2];  // per-lane slot byte offset of column block j (K row 0)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int sp = min(sp0 + wave * 64 + j * 32 + lr, HWo - 1);
+    const int oh = sp / OW, ow = sp - oh * OW;
+    lb[j] = static_cast<uint32_t>((S * (oh - f) * ROWE + S * ow) * 2);
+  }
+  const x6::bf16x8* ap = wpack + lane;
+  auto load_a = [&](x6::bf16x8 (&fr)[MI][3], int g) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int tt = 0; tt < 3; ++tt) fr[i][tt] = ap[((g * MI + i) * 3 + tt) * 64];
+  };
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  // B term tt of column block j for group g: K row 2 g + lh; kernel column 7
+  // (the upper half of dword 3) and the padding row are zeroed, so a
+  // non-finite input never meets a padded zero weight.  The raw reads are
+  // issued a group ahead and masked at use, so no wait for them sits in
+  // front of the current group's MFMAs
+  auto read_b = [&](u32x4 (&Bq)[2][3], int g) __attribute__((always_inline)) {
+    const uint32_t ho = lh ? static_cast<uint32_t>(row_off(2 * g + 1)) : static_cast<uint32_t>(row_off(2 * g));
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int tt = 0; tt < 3; ++tt) {
+        const uint32_t* p = reinterpret_cast<const uint32_t*>(smem + lb[j] + ho + tt * TERMB);
+        Bq[j][tt] = u32x4{p[0], p[1], p[2], p[3]};
+      }
+  };
+  auto parts_b = [&](const u32x4 (&Bq)[2][3], int j, int g) __attribute__((always_inline)) {
+    const uint32_t m3 = (2 * g + 1 < R || lh == 0) ? 0x0000FFFFu : 0u;
+    const uint32_t m02 = (2 * g + 1 < R || lh == 0) ? 0xFFFFFFFFu : 0u;
+    x6::bf16x8 t[3];
+#pragma unroll
+    for (int tt = 0; tt < 3; ++tt) {
+      u32x4 d = Bq[j][tt];
+      asm volatile("" : "+v"(d));  // (keeps the masks here: hoisted to the reads they wait for them)
+      if (2 * g + 1 >= R) {
+        d[0] &= m02;
+        d[1] &= m02;
+        d[2] &= m02;
+      }
+      d[3] &= m3;
+      t[tt] = __builtin_bit_cast(x6::bf16x8, d);
+    }
+    return x6::Parts{t[0], t[1], t[2]};
+  };
+  floatx16 acc[MI][2];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+  x6::bf16x8 fa[3][MI][3];
+  load_a(fa[0], 0);
+  load_a(fa[1], 1);
+  u32x4 Bq[2][2][3];
+  read_b(Bq[0], 0);
+  // (scheduling barriers keep the prefetches where they are issued: left to
+  // itself the scheduler sinks each weight load next to its first MFMA and
+  // waits the full L2 latency there)
+  __builtin_amdgcn_sched_barrier(0);
+  static_for<0, G>([&](auto gc) {
+    constexpr int g = decltype(gc)::value;
+    if (g + 2 < G) load_a(fa[(g + 2) % 3], g + 2);
+    if (g + 1 < G) read_b(Bq[(g + 1) & 1], g + 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const x6::Parts b = parts_b(Bq[g & 1], j, g);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+        acc[i][j] = x6::mfma6(x6::Parts{fa[g % 3][i][0], fa[g % 3][i][1], fa[g % 3][i][2]}, b, acc[i][j]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  });
+
+  // ---- epilogue: bias + ReLU (conv_epilogue_nchw's arithmetic), NCHW ----
+  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(P.e.C, 0, 0x7FFFFFFF, 0x00020000);
+  const bool relu = P.e.relu != 0;
+  float bv[MI][16];  // (all bias reads before the first store: a store between them orders each read)
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) bv[i][r] = bias_lds[i * 32 + 4 * lh + (r & 3) + 8 * (r >> 2)];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int sp = sp0 + wave * 64 + j * 32 + lr;
+    const uint32_t ob = sp < HWo ? static_cast<uint32_t>(((int64_t)img * P.e.cimg + sp) * 4) : 0x80000000u;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = i * 32 + 4 * lh + (r & 3) + 8 * (r >> 2);
+        const float o = acc[i][j][r] + bv[i][r];
+        if (m < P.M)
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, relu ? fmaxf(o, 0.0f) : o), ors,
+                                                static_cast<int>(ob), m * HWo * 4, 0);
+      }
+  }
+}
+
+// Weight repack for k_conv_s2_x6: w [M][3][7][7] -> fragments
+// [11 groups][2 row blocks][3 terms][64 lanes][8 bf16]; lane (lr, h) of
+// fragment (g, i): filter 32 i + lr, K row 2 g + h = (channel, kernel row),
+// items = kernel columns 0 .. 7 (column 7, row 21 and filters >= M zero).
+__global__ void __launch_bounds__(256) k_conv_s2_pack_x6(const float* __restrict__ w, char* __restrict__ out, int M,
+                                                         int units) {
+  using namespace c7x6;
+  for (int u = blockIdx.x * blockDim.x + threadIdx.x; u < units; u += gridDim.x * blockDim.x) {
+    const int lane = u & 63, i = (u >> 6) % MI, g = (u >> 6) / MI;
+    const int m = 32 * i + (lane & 31), rr = 2 * g + (lane >> 5);
+    const int c = rr / KS, kr = rr % KS;
+    float v[8];
+#pragma unroll
+    for (int kc = 0; kc < 8; ++kc)
+      v[kc] = (m < M && rr < R && kc < KS) ? w[((m * C + c) * KS + kr) * KS + kc] : 0.0f;
+    x6::Parts tp;
+    x6::split8_safe(v, tp);
+    char* o = out + (int64_t)(u >> 6) * 3072 + lane * 16;
+    *reinterpret_cast<x6::bf16x8*>(o) = tp.h;
+    *reinterpret_cast<x6::bf16x8*>(o + 1024) = tp.m;
+    *reinterpret_cast<x6::bf16x8*>(o + 2048) = tp.l;
+  }
+}
+
 // Weight repack for k_conv_patch_x6: w [G*M][C*T] -> bf16 terms
 // [G][tiles_m][ktiles][64 MI][RLB]: row = [group g][half h][term][8 steps] + pad.
 // One thread per (row, group, half): 8 weights in, 48 bytes out.
@@ -2417,6 +2649,68 @@ int conv_wide_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, co
   hipLaunchKernelGGL((k_conv1_ring_x6<227>), dim3(nwg), dim3(256), 0, s, P, reinterpret_cast<const uint16_t*>(wp),
                      tpi, tiles);
   const int rc = launch_status("conv1 ring x6");
+  return rc ? rc : 1;
+}
+
+// ---- k_conv_s2_x6 (GoogLeNet conv1: 3 channels, 64 x 7 x 7, stride 2) ----
+bool conv_s2_ok(const rram_conv_desc* d) {
+  namespace k = c7x6;
+  return d->group == 1 && d->channels == k::C && d->kernel_h == k::KS && d->kernel_w == k::KS &&
+         d->stride_h == k::S && d->stride_w == k::S && d->dilation_h == 1 && d->dilation_w == 1 && d->pad_h >= 0 &&
+         d->pad_h <= 3 && d->pad_w >= 0 && d->pad_w <= 3 && d->num_output >= 1 && d->num_output <= k::BM &&
+         d->num > 0 && d->out_w >= 85 && d->out_h >= 1 && k::S * (d->out_w - 1) + k::KC <= k::ROWE &&
+         (d->out_w + 254) / d->out_w <= k::OR - 1 && (int64_t)d->num * k::C * d->height * d->width * 4 < (1ll << 31) &&
+         (int64_t)d->num * d->num_output * d->out_h * d->out_w * 4 < (1ll << 31);
+}
+
+int conv_s2_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const float* bias, float* y, int relu,
+                   hipStream_t s, const WPack& wk) {
+  if (!conv_s2_ok(d)) return 0;
+  if ((reinterpret_cast<uintptr_t>(w) & 3u) != 0) return 0;
+  const int HW = d->out_h * d->out_w;
+  Params P{};
+  P.M = d->num_output;
+  P.N = d->num * HW;
+  P.K = c7x6::R * c7x6::KS;
+  P.split = 1;
+  P.b = make_view(x, 0, P.N, P.K);
+  ConvGeom& cv = P.cv;
+  cv.C = c7x6::C;
+  cv.H = d->height;
+  cv.W = d->width;
+  cv.KH = cv.KW = c7x6::KS;
+  cv.ph = d->pad_h;
+  cv.pw = d->pad_w;
+  cv.sh = cv.sw = c7x6::S;
+  cv.dh = cv.dw = 1;
+  cv.Ho = d->out_h;
+  cv.Wo = d->out_w;
+  cv.howo = make_fastdiv(HW);
+  cv.wo_div = make_fastdiv(d->out_w);
+  cv.chw = (int64_t)c7x6::C * d->height * d->width;
+  cv.in_bytes = static_cast<int>((int64_t)d->num * cv.chw * 4);
+  P.e = make_epi(y, HW, 1.0f, 0.0f, bias, RRAM_BIAS_ROW, relu);
+  P.e.cimg = wk.y_img > 0 ? wk.y_img : (int64_t)d->num_output * HW;
+  P.e.hw = make_fastdiv(HW);
+  const int units = c7x6::G * c7x6::MI * 64;  // 3 KB fragments
+  const size_t wbytes = static_cast<size_t>(units) * 48;
+  if (wk.query) {
+    *wk.query = wbytes;
+    return 1;
+  }
+  char* wp = static_cast<char*>(wk.p ? wk.p : pack_buffer((wbytes + 3) / 4, s));
+  RRAM_REQUIRE(wp != nullptr, "conv: packed-weight buffer allocation failed");
+  if (!wk.valid) {
+    hipLaunchKernelGGL(k_conv_s2_pack_x6, dim3(stream_blocks(units)), dim3(256), 0, s, w, wp, d->num_output, units);
+    const int rc = launch_status("conv s2 weight pack x6");
+    if (rc) return rc;
+  }
+  const int tpi = (HW + c7x6::BN - 1) / c7x6::BN;
+  const int64_t tiles = (int64_t)d->num * tpi;
+  RRAM_REQUIRE(tiles < (1ll << 31), "conv: grid too large");
+  hipLaunchKernelGGL(k_conv_s2_x6, dim3(static_cast<unsigned>(tiles)), dim3(256), 0, s, P,
+                     reinterpret_cast<const x6::bf16x8*>(wp), tpi, static_cast<int>(tiles));
+  const int rc = launch_status("conv s2 x6");
   return rc ? rc : 1;
 }
 
@@ -2882,6 +3176,7 @@ int conv_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, cons
     if (rc1 != 0) return rc1;
   }
   int rc = conv_wide_x6_fwd(d, x, w, bias, y, relu, s, wk);
+  if (rc == 0) rc = conv_s2_x6_fwd(d, x, w, bias, y, relu, s, wk);
   if (rc == 0) rc = conv_patch_x6_fwd(d, x, w, bias, y, relu, s, wk);
   if (wk.query) return rc;
   if (rc > 0 && y_oct != nullptr) {
@@ -3110,7 +3405,7 @@ int rram_f32_engine_for_conv(const rram_conv_desc* d) {
   rram::CbPlan cpl;
   rram::C1Plan c1;
   return rram::f32_engine().load() == RRAM_ENGINE_BF16X6 &&
-                 (rram::conv_x6_plan(d, pl) || rram::conv1_ring_ok(d) ||
+                 (rram::conv_x6_plan(d, pl) || rram::conv1_ring_ok(d) || rram::conv_s2_ok(d) ||
                   rram::conv_cb_plan(d, cpl) || rram::conv_1x1_plan(d, nullptr, c1))
              ? RRAM_ENGINE_BF16X6
              : RRAM_ENGINE_F32;

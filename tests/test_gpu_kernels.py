@@ -540,6 +540,7 @@ ENGINE_CASES = [
     dict(x=(4, 384, 13, 13), cout=256, k=3, p=1, g=2),
     dict(x=(3, 64, 56, 56), cout=192, k=3, p=1, g=1),      # GoogLeNet conv2: 64 x 256 per-image tiles (13 per image)
     dict(x=(3, 128, 28, 28), cout=192, k=3, p=1, g=1),     # inception_3b/3x3: 64 x 256 contiguous tiles
+    dict(x=(2, 3, 224, 224), cout=64, k=7, p=3, g=1, s=2),  # GoogLeNet conv1 (k_conv_s2_x6)
 ]
 
 
@@ -575,6 +576,37 @@ def test_conv_engine_bf16x6_accuracy_vs_f32(device, cs):
     print(f"{cs}: max/mean err / Σ|a·b|: f32 {f32[0]:.2e}/{f32[1]:.2e}  bf16x6 {x6[0]:.2e}/{x6[1]:.2e}")
     assert x6[0] < 1e-6 and f32[0] < 1e-6          # fp32 level (the test bound is 1e-4)
     assert x6[0] <= 2.0 * f32[0] and x6[1] <= 2.0 * f32[1]
+
+
+# Shapes of k_conv_s2_x6 (3 channels, 7 x 7, stride 2, <= 64 filters, >= 85
+# output columns): GoogLeNet conv1, 40 of 64 filter rows with 4-row tiles,
+# no padding with a partial last tile, 17 filters at padding 2
+S2_CASES = [
+    dict(x=(2, 3, 224, 224), cout=64, p=3),
+    dict(x=(3, 3, 175, 173), cout=40, p=1),
+    dict(x=(2, 3, 181, 180), cout=64, p=0),
+    dict(x=(2, 3, 190, 191), cout=17, p=2),
+]
+
+
+@pytest.mark.parametrize("cs", S2_CASES)
+def test_conv_s2_x6_vs_fp64(device, cs):
+    """k_conv_s2_x6 within 1e-4 of Σ|a·b| of a float64 convolution, plain and
+    with the fused ReLU; the output starts as NaN so every element is written."""
+    import torch
+    from rramsim import ops
+    from _ref64 import check_conv
+    rng = np.random.default_rng(23)
+    x = rng.standard_normal(cs["x"]).astype(np.float32)
+    w = (rng.standard_normal((cs["cout"], 3, 7, 7)) * 0.1).astype(np.float32)
+    b = rng.standard_normal(cs["cout"]).astype(np.float32)
+    d = ops.conv_desc(cs["x"], cs["cout"], 7, 2, cs["p"], 1, 1)
+    assert ops.f32_engine_for_conv(d) == ops.ENGINE_BF16X6
+    for relu in (False, True):
+        y = torch.full((cs["x"][0], cs["cout"], d.out_h, d.out_w), float("nan"), device=device)
+        ops.conv2d_fwd(d, T(x, device), T(w, device), T(b, device), y, relu=relu)
+        torch.cuda.synchronize()
+        check_conv(N(y), x, w, b, 2, cs["p"], 1, relu=relu, what=f"conv s2 {cs} relu={relu}")
 
 
 @pytest.mark.parametrize("cs", [CONV_CASES[0], CONV_CASES[1], CONV_CASES[4], CONV_CASES[12]])

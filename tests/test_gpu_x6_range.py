@@ -6,7 +6,7 @@ Inf * 0 = NaN; the conv1 kernel's padded K items read zeroed B values, so no
 split exactly (below it the low terms fall under the normal range: the
 engine's documented limit, measured by scripts/x6_range_probe.py).  Checked on every
 kernel of the engine — the channel-octet convolution, the persistent conv1
-kernel, the patch kernel and the InnerProduct GEMM —
+kernel, the patch kernel, the GoogLeNet conv1 kernel and the InnerProduct GEMM —
 against a CPU float32 evaluation (NaN / +Inf / -Inf positions) and a float64
 one (finite outputs within 1e-4 of sum |a*b|)."""
 import numpy as np
@@ -18,6 +18,7 @@ CONVS = {
     "octet": ((2, 256, 13, 13), 384, 3, 1, 1),
     "conv1": ((2, 3, 227, 227), 96, 11, 4, 0),
     "patch": ((2, 24, 20, 20), 96, 3, 1, 1),
+    "conv7s2": ((2, 3, 224, 224), 64, 7, 2, 3),
 }
 
 
