@@ -229,6 +229,85 @@ __global__ void __launch_bounds__(256) k_pool_planes(const float* __restrict__ x
   }
 }
 
+// MAX pooling of small planes with a 3 x 3 window, stride 1 or 2, no argmax
+// (the TEST-phase pools of GoogLeNet: the inception branches' 3 x 3 / 1 and
+// pool1 / pool3 / pool4's 3 x 3 / 2).  Planes staged in LDS as in
+// k_pool_planes; the window is separable: a work item (plane, output column,
+// segment of kSepRows output rows) walks the input rows of its segment once,
+// each row's 3-column maximum formed once and kept in a 3-row ring, so an
+// output costs S new row maxima (3 S LDS reads) instead of 9 guarded taps.
+// The same strict-">" scan from -FLT_MAX as MaxPoolForward (pooling_layer.cu),
+// row by row: the first maximum in row-major order wins, so the value (its
+// sign of zero included) is the one k_pool_planes picks; taps outside the
+// image are skipped (here: -FLT_MAX, which no ">" replaces).
+constexpr int kSepRows = 8;
+__global__ void __launch_bounds__(256) k_pool_planes_sep3(const float* __restrict__ x, float* __restrict__ y, int planes,
+                                                          int H, int W, int PH, int PW, int S, int ph, int pw, int ppb,
+                                                          int nseg, float inv_pw, float inv_nseg, int relu,
+                                                          float slope) {
+  extern __shared__ __attribute__((aligned(16))) float tile[];
+  const int HW = H * W, PHW = PH * PW;
+  const int p0 = blockIdx.x * ppb;
+  const int np = min(ppb, planes - p0);
+  const int n_in = np * HW;
+  const int n4 = (n_in + 3) >> 2;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(x + (int64_t)p0 * HW), 0, n_in * 4, 0x00020000);
+  for (int i0 = threadIdx.x; i0 < n4; i0 += 256 * kStageU) {
+    float4 r[kStageU];
+#pragma unroll
+    for (int u = 0; u < kStageU; ++u) {
+      const int i = min(i0 + 256 * u, n4);  // i == n4: past the range, loads zeros
+      r[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * i, 0, 0));
+    }
+#pragma unroll
+    for (int u = 0; u < kStageU; ++u)
+      if (i0 + 256 * u < n4) reinterpret_cast<float4*>(tile)[i0 + 256 * u] = r[u];
+  }
+  __syncthreads();
+  const int items = np * nseg * PW;
+  float* dst = y + (int64_t)p0 * PHW;
+  for (int it = threadIdx.x; it < items; it += 256) {
+    const int rest = div_small(it, inv_pw), ow = it - rest * PW;
+    const int pl = div_small(rest, inv_nseg), sg = rest - pl * nseg;
+    const float* t = tile + pl * HW;
+    const int c0 = ow * S - pw;
+    const bool ok0 = static_cast<unsigned>(c0) < static_cast<unsigned>(W);
+    const bool ok1 = static_cast<unsigned>(c0 + 1) < static_cast<unsigned>(W);
+    const bool ok2 = static_cast<unsigned>(c0 + 2) < static_cast<unsigned>(W);
+    const int ca = ok0 ? c0 : 0, cb = ok1 ? c0 + 1 : 0, cc = ok2 ? c0 + 2 : 0;
+    const int oh0 = sg * kSepRows, nout = min(kSepRows, PH - oh0);
+    const int r0 = oh0 * S - ph;
+    auto rowmax = [&](int r) __attribute__((always_inline)) {
+      float m = -FLT_MAX;
+      if (static_cast<unsigned>(r) < static_cast<unsigned>(H)) {
+        const float* tr = t + r * W;
+        const float va = tr[ca], vb = tr[cb], vc = tr[cc];
+        if (ok0 && va > m) m = va;
+        if (ok1 && vb > m) m = vb;
+        if (ok2 && vc > m) m = vc;
+      }
+      return m;
+    };
+    float q0 = rowmax(r0), q1 = rowmax(r0 + 1);
+    float* out = dst + (int64_t)pl * PHW + oh0 * PW + ow;
+    for (int o = 0; o < nout; ++o) {
+      const float q2 = rowmax(r0 + S * o + 2);
+      float m = q0;  // rows top to bottom: the first row holding the maximum wins
+      if (q1 > m) m = q1;
+      if (q2 > m) m = q2;
+      out[o * PW] = pool_out(m, relu, slope);
+      if (S == 1) {  // next window: rows r0 + o + 1 .. r0 + o + 3
+        q0 = q1;
+        q1 = q2;
+      } else {  // next window: rows r0 + 2 o + 2 .. r0 + 2 o + 4
+        q0 = q2;
+        if (o + 1 < nout) q1 = rowmax(r0 + 2 * o + 3);
+      }
+    }
+  }
+}
+
 // pooling_layer.cu MaxPoolBackward / AvePoolBackward
 // ry != nullptr: times the backward factor of the in-place ReLU whose output
 // ry is (rram_pool_relu_bwd; k_relu_bwd's expression)
@@ -977,6 +1056,18 @@ int pool_fwd_core(const float* x, float* y, int* mask, int num, int C, int H, in
     const dim3 grid(static_cast<unsigned>((planes + ppb - 1) / ppb));
     const size_t lds = (static_cast<size_t>(ppb) * H * W + 3) / 4 * 16;
     const float inv_phw = 1.0f / static_cast<float>(PH * PW), inv_pw = 1.0f / static_cast<float>(PW);
+    if (mask == nullptr && method == RRAM_POOL_MAX && kh == 3 && kw == 3 && sh == sw && (sh == 1 || sh == 2) &&
+        H * W <= kPlaneTile) {
+      // separable 3 x 3 window (no argmax to record): k_pool_planes_sep3.
+      // GoogLeNet b256 (profiles/r06_ab_pool_sep3.txt): the inception pools,
+      // pool2 / pool3 / pool4 and 5a / 5b 947 -> 821 us per map; a 112 x 112
+      // plane (pool1: one plane per block, 392 items for 256 threads) ran
+      // slower there (211 -> 229 us) and stays on k_pool_planes
+      const int nseg = (PH + kSepRows - 1) / kSepRows;
+      hipLaunchKernelGGL(k_pool_planes_sep3, grid, dim3(kThreads), lds, s, x, y, planes, H, W, PH, PW, sh, ph, pw, ppb,
+                         nseg, 1.0f / static_cast<float>(PW), 1.0f / static_cast<float>(nseg), relu, slope);
+      return launch_status("pool_fwd");
+    }
     const int k = method == RRAM_POOL_MAX && kh == kw && (kh == 3 || kh == 2) ? kh : 0;
     auto kern = k == 3 ? k_pool_planes<3> : k == 2 ? k_pool_planes<2> : k_pool_planes<0>;
     hipLaunchKernelGGL(kern, grid, dim3(kThreads), lds, s, x, y, mask, planes, H, W, PH, PW, kh, kw, sh, sw, ph, pw,

@@ -120,6 +120,69 @@ def test_max_pool_plane_kernel_equals_direct(device, shape, k, s, p):
     np.testing.assert_array_equal(m.cpu().numpy(), rm)
 
 
+def _max_pool_scan(xs, k, s, p, PH, PW):
+    """MaxPoolForward's value (pooling_layer.cu:11-47) restated as a scan:
+    window clipped to the image, -FLT_MAX start, strict ">" in row-major order
+    (a NaN never wins, the first of equal values (+0 / -0) stays)."""
+    N, C, H, W = xs.shape
+    out = np.empty((N, C, PH, PW), np.float32)
+    for a in range(PH):
+        for b in range(PW):
+            hs, ws = a * s - p, b * s - p
+            he, we = min(hs + k, H), min(ws + k, W)
+            hs, ws = max(hs, 0), max(ws, 0)
+            m = np.full((N, C), np.finfo(np.float32).min, np.float32)
+            for h in range(hs, he):
+                for w in range(ws, we):
+                    v = xs[:, :, h, w]
+                    m = np.where(v > m, v, m)
+            out[:, :, a, b] = m
+    return out
+
+
+@pytest.mark.parametrize("shape,s,p", [((3, 64, 28, 28), 1, 1), ((2, 20, 14, 14), 1, 1), ((2, 100, 7, 7), 1, 1),
+                                       ((2, 5, 56, 56), 2, 0), ((2, 7, 28, 28), 2, 0), ((3, 6, 13, 11), 2, 1),
+                                       ((2, 9, 9, 10), 1, 0), ((1, 3, 129, 127), 2, 1)])
+def test_max_pool_sep3_equals_scan(device, shape, s, p):
+    """The TEST-phase 3 x 3 max pool without argmax (k_pool_planes_sep3: the
+    separable window, several planes per block) against
+    MaxPoolForward's scan, bit for bit, with ties of +0 / -0, NaN, +-Inf and
+    -FLT_MAX in the input; and the fused-ReLU form against relu() of it."""
+    import torch
+    from rramsim import ops
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(*shape, generator=g)
+    flat = x.view(-1)
+    n = flat.numel()
+    flat[torch.randint(0, n, (n // 50,), generator=g)] = 0.0
+    flat[torch.randint(0, n, (n // 50,), generator=g)] = -0.0
+    flat[torch.randint(0, n, (n // 200,), generator=g)] = float("nan")
+    flat[torch.randint(0, n, (n // 300,), generator=g)] = float("inf")
+    flat[torch.randint(0, n, (n // 300,), generator=g)] = -float("inf")
+    flat[torch.randint(0, n, (n // 300,), generator=g)] = float(np.finfo(np.float32).min)
+    x[0, 0] = -0.0                                   # a plane of signed zeros only
+    x[0, 0, 1::3, ::2] = 0.0
+    x[-1, -1] = float("nan")                         # all NaN: -FLT_MAX out
+    N, C, H, W = shape
+    k = 3
+    PH = -(-(H + 2 * p - k) // s) + 1
+    PW = -(-(W + 2 * p - k) // s) + 1
+    if (PH - 1) * s >= H + p:
+        PH -= 1
+    if (PW - 1) * s >= W + p:
+        PW -= 1
+    geom = (N, C, H, W, PH, PW, k, k, s, s, p, p)
+    ref = _max_pool_scan(x.numpy(), k, s, p, PH, PW)
+    xd = x.to(device)
+    y = torch.full((N, C, PH, PW), 7.0, device=device)
+    ops.pool_fwd(xd, y, None, geom, 0)
+    torch.cuda.synchronize()
+    assert y.cpu().numpy().tobytes() == ref.tobytes()
+    ops.pool_relu_fwd(xd, y, None, geom, 0, 0.0)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(y.cpu(), torch.relu(torch.from_numpy(ref)), rtol=0, atol=0)
+
+
 def _lrn_across_ref(x, size, alpha, beta, k):
     import torch.nn.functional as F
     pre = (size - 1) // 2
