@@ -2708,6 +2708,8 @@ int conv_s2_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, cons
   const int tpi = (HW + c7x6::BN - 1) / c7x6::BN;
   const int64_t tiles = (int64_t)d->num * tpi;
   RRAM_REQUIRE(tiles < (1ll << 31), "conv: grid too large");
+  // (a persistent form, one workgroup per CU with the weights in registers:
+  // 0.61 vs 0.43 ms in the GoogLeNet map, profiles/r06_ab_conv_s2_persistent.txt)
   hipLaunchKernelGGL(k_conv_s2_x6, dim3(static_cast<unsigned>(tiles)), dim3(256), 0, s, P,
                      reinterpret_cast<const x6::bf16x8*>(wp), tpi, static_cast<int>(tiles));
   const int rc = launch_status("conv s2 x6");
