@@ -229,20 +229,20 @@ __global__ void __launch_bounds__(256) k_pool_planes(const float* __restrict__ x
   }
 }
 
-// MAX pooling of small planes with a 3 x 3 window, stride 1 or 2, no argmax
-// (the TEST-phase pools of GoogLeNet: the inception branches' 3 x 3 / 1 and
-// pool1 / pool3 / pool4's 3 x 3 / 2).  Planes staged in LDS as in
-// k_pool_planes; the window is separable: a work item (plane, output column,
-// segment of kSepRows output rows) walks the input rows of its segment once,
-// each row's 3-column maximum formed once and kept in a 3-row ring, so an
-// output costs S new row maxima (3 S LDS reads) instead of 9 guarded taps.
+// MAX pooling of small planes with a 3 x 3 window, stride 1, no argmax (the
+// TEST-phase pools of GoogLeNet's inception branches).  Planes staged in LDS
+// as in k_pool_planes; the window is separable: a work item (plane, output
+// column, segment of kSepRows output rows) walks the input rows of its
+// segment once, each row's 3-column maximum formed once and kept in a 3-row
+// ring, so an output costs one new row maximum (3 LDS reads) instead of 9
+// guarded taps.
 // The same strict-">" scan from -FLT_MAX as MaxPoolForward (pooling_layer.cu),
 // row by row: the first maximum in row-major order wins, so the value (its
 // sign of zero included) is the one k_pool_planes picks; taps outside the
 // image are skipped (here: -FLT_MAX, which no ">" replaces).
 constexpr int kSepRows = 8;
 __global__ void __launch_bounds__(256) k_pool_planes_sep3(const float* __restrict__ x, float* __restrict__ y, int planes,
-                                                          int H, int W, int PH, int PW, int S, int ph, int pw, int ppb,
+                                                          int H, int W, int PH, int PW, int ph, int pw, int ppb,
                                                           int nseg, float inv_pw, float inv_nseg, int relu,
                                                           float slope) {
   extern __shared__ __attribute__((aligned(16))) float tile[];
@@ -271,13 +271,13 @@ __global__ void __launch_bounds__(256) k_pool_planes_sep3(const float* __restric
     const int rest = div_small(it, inv_pw), ow = it - rest * PW;
     const int pl = div_small(rest, inv_nseg), sg = rest - pl * nseg;
     const float* t = tile + pl * HW;
-    const int c0 = ow * S - pw;
+    const int c0 = ow - pw;
     const bool ok0 = static_cast<unsigned>(c0) < static_cast<unsigned>(W);
     const bool ok1 = static_cast<unsigned>(c0 + 1) < static_cast<unsigned>(W);
     const bool ok2 = static_cast<unsigned>(c0 + 2) < static_cast<unsigned>(W);
     const int ca = ok0 ? c0 : 0, cb = ok1 ? c0 + 1 : 0, cc = ok2 ? c0 + 2 : 0;
     const int oh0 = sg * kSepRows, nout = min(kSepRows, PH - oh0);
-    const int r0 = oh0 * S - ph;
+    const int r0 = oh0 - ph;
     auto rowmax = [&](int r) __attribute__((always_inline)) {
       float m = -FLT_MAX;
       if (static_cast<unsigned>(r) < static_cast<unsigned>(H)) {
@@ -292,18 +292,13 @@ __global__ void __launch_bounds__(256) k_pool_planes_sep3(const float* __restric
     float q0 = rowmax(r0), q1 = rowmax(r0 + 1);
     float* out = dst + (int64_t)pl * PHW + oh0 * PW + ow;
     for (int o = 0; o < nout; ++o) {
-      const float q2 = rowmax(r0 + S * o + 2);
+      const float q2 = rowmax(r0 + o + 2);
       float m = q0;  // rows top to bottom: the first row holding the maximum wins
       if (q1 > m) m = q1;
       if (q2 > m) m = q2;
       out[o * PW] = pool_out(m, relu, slope);
-      if (S == 1) {  // next window: rows r0 + o + 1 .. r0 + o + 3
-        q0 = q1;
-        q1 = q2;
-      } else {  // next window: rows r0 + 2 o + 2 .. r0 + 2 o + 4
-        q0 = q2;
-        if (o + 1 < nout) q1 = rowmax(r0 + 2 * o + 3);
-      }
+      q0 = q1;  // next window: rows r0 + o + 1 .. r0 + o + 3
+      q1 = q2;
     }
   }
 }
@@ -1056,15 +1051,14 @@ int pool_fwd_core(const float* x, float* y, int* mask, int num, int C, int H, in
     const dim3 grid(static_cast<unsigned>((planes + ppb - 1) / ppb));
     const size_t lds = (static_cast<size_t>(ppb) * H * W + 3) / 4 * 16;
     const float inv_phw = 1.0f / static_cast<float>(PH * PW), inv_pw = 1.0f / static_cast<float>(PW);
-    if (mask == nullptr && method == RRAM_POOL_MAX && kh == 3 && kw == 3 && sh == sw && (sh == 1 || sh == 2) &&
+    if (mask == nullptr && method == RRAM_POOL_MAX && kh == 3 && kw == 3 && sh == 1 && sw == 1 &&
         H * W <= kPlaneTile) {
-      // separable 3 x 3 window (no argmax to record): k_pool_planes_sep3.
-      // GoogLeNet b256 (profiles/r06_ab_pool_sep3.txt): the inception pools,
-      // pool2 / pool3 / pool4 and 5a / 5b 947 -> 821 us per map; a 112 x 112
-      // plane (pool1: one plane per block, 392 items for 256 threads) ran
-      // slower there (211 -> 229 us) and stays on k_pool_planes
+      // separable 3 x 3 / 1 window (no argmax to record): k_pool_planes_sep3.
+      // GoogLeNet b256 (profiles/r06_ab_pool_sep3.txt): the nine inception
+      // pools 554 -> 391 us per map; its stride-2 form (two new row maxima
+      // per output) ran slower than k_pool_planes on pool1 / pool3 / pool4
       const int nseg = (PH + kSepRows - 1) / kSepRows;
-      hipLaunchKernelGGL(k_pool_planes_sep3, grid, dim3(kThreads), lds, s, x, y, planes, H, W, PH, PW, sh, ph, pw, ppb,
+      hipLaunchKernelGGL(k_pool_planes_sep3, grid, dim3(kThreads), lds, s, x, y, planes, H, W, PH, PW, ph, pw, ppb,
                          nseg, 1.0f / static_cast<float>(PW), 1.0f / static_cast<float>(nseg), relu, slope);
       return launch_status("pool_fwd");
     }
