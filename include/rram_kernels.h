@@ -374,11 +374,12 @@ int rram_conv2d_fwd_strided(const rram_conv_desc* d, const float* x, const void*
 /* 1 when rram_conv2d_fwd_octets would read an x_oct for this shape now. */
 int rram_conv_input_octets(const rram_conv_desc* d);
 /* 1 when rram_conv2d_fwd_octets / _cached accept y = NULL with y_oct for this
- * shape now: the channel-octet kernel's 16x16x32 epilogue then writes only
- * the companion (bit-identical to the one it writes next to y), no fp32 y.
- * The TEST-phase convolution-output fold: a convolution whose top is read
- * only by another convolution that takes the companion (AlexNet conv3 ->
- * conv4, conv4 -> conv5).  No reference counterpart (a fusion of this build);
+ * shape now: the channel-octet kernel's 16x16x32 epilogue, or the 1x1
+ * kernels' (round 6), then writes only the companion (bit-identical to the
+ * one it writes next to y), no fp32 y.  The TEST-phase convolution-output
+ * fold: a convolution whose top is read only by another convolution that
+ * takes the companion (AlexNet conv3 -> conv4, conv4 -> conv5; GoogLeNet's
+ * 3x3_reduce -> 3x3).  No reference counterpart (a fusion of this build);
  * with y = NULL on a shape this returns 0 for, the calls return RRAM_EINVAL. */
 int rram_conv_output_octets_only(const rram_conv_desc* d);
 /* Host-side plan of the channel-octet kernel for d (no device work):

@@ -226,7 +226,9 @@ __device__ __forceinline__ void gemm_epilogue(floatx16 (&acc)[MI][NI], const Par
 // lane's rows are mwave + 4 h + (r & 3) + 8 (r >> 2) + 32 i), so a store
 // costs no per-element address arithmetic (the generic epilogue spent
 // ~3000 VALU per wave on 64-bit addresses, exposed at one wave per SIMD).
-// acc is left holding the stored values before the ReLU.
+// acc is left holding the stored values before the ReLU.  ep.C == nullptr:
+// nothing stored (the 1x1 kernels' convolution-output fold: only the octet
+// companion, from acc, is written).
 template <int MI, int NI>
 __device__ __forceinline__ void conv_epilogue_nchw(floatx16 (&acc)[MI][NI], const Params& P, const Epi& ep,
                                                    int mwave, int nwave, int lr, int lh, int nlim = 0x7FFFFFFF) {
@@ -262,6 +264,7 @@ __device__ __forceinline__ void conv_epilogue_nchw(floatx16 (&acc)[MI][NI], cons
         acc[i][j][r] = o;  // the stored value before the ReLU (k_conv_cb_x6's octet companion splits it)
         ov[i][r] = relu ? fmaxf(o, 0.0f) : o;
       }
+    if (ep.C == nullptr) continue;
     if (rows_full) {  // uniform: no per-store exec masking
 #pragma unroll
       for (int i = 0; i < MI; ++i)

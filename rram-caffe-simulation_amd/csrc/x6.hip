@@ -3093,6 +3093,9 @@ int conv_1x1_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, con
   C1Plan pl;
   if (!conv_1x1_plan(d, wk.query ? nullptr : x, pl)) return 0;
   const int M = d->num_output, C = d->channels, HW = d->height * d->width;
+  // y = NULL (the convolution-output fold): the epilogue writes the companion alone
+  RRAM_REQUIRE(y != nullptr || wk.query != nullptr || (y_oct != nullptr && M % 8 == 0),
+               "conv 1x1: y = NULL needs the octet companion (num_output % 8 == 0)");
   const int BMc = 32 * pl.MI * pl.WR;
   const int rblocks = pl.tiles_m * (BMc / 32);
   const int64_t wfrags = (int64_t)rblocks * (C / 16);
@@ -3170,13 +3173,13 @@ int conv_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, cons
     const int rc = conv_cb_x6_fwd(d, x, x_oct, w, bias, y, y_oct, relu, s, wk);
     if (rc != 0) return rc;
   }
-  // only the channel-octet kernel's epilogue writes a companion without y
-  RRAM_REQUIRE(y != nullptr || wk.query != nullptr,
-               "conv: y = NULL needs the channel-octet kernel's companion epilogue (rram_conv_output_octets_only)");
   {
     const int rc1 = conv_1x1_x6_fwd(d, x, w, bias, y, y_oct, relu, s, wk);  // writes y_oct itself
     if (rc1 != 0) return rc1;
   }
+  // only the channel-octet and 1x1 kernels' epilogues write a companion without y
+  RRAM_REQUIRE(y != nullptr || wk.query != nullptr,
+               "conv: y = NULL needs a companion-writing epilogue (rram_conv_output_octets_only)");
   int rc = conv_wide_x6_fwd(d, x, w, bias, y, relu, s, wk);
   if (rc == 0) rc = conv_s2_x6_fwd(d, x, w, bias, y, relu, s, wk);
   if (rc == 0) rc = conv_patch_x6_fwd(d, x, w, bias, y, relu, s, wk);
@@ -3430,6 +3433,9 @@ int rram_conv_output_octets_only(const rram_conv_desc* d_in) {
   if (rram::f32_engine().load(std::memory_order_relaxed) != RRAM_ENGINE_BF16X6) return 0;
   rram_conv_desc d = *d_in;
   if (rram_conv_out_shape(&d) != RRAM_OK || d.num == 0 || d.num_output % 8 != 0) return 0;
+  // the 1x1 kernels write the companion from their epilogue (whole octets)
+  rram::C1Plan c1;
+  if (rram::conv_1x1_plan(&d, nullptr, c1)) return 1;
   rram::CbPlan pl;
   if (!rram::conv_cb_plan(&d, pl)) return 0;
   return pl.OCC == 2 && (d.num_output / d.group) % 8 == 0 ? 1 : 0;

@@ -750,6 +750,55 @@ def test_conv_octets_only_epilogue_bit_identical(device):
         ops.conv2d_fwd_octets(d, x, None, w, None, None, yo)
 
 
+@pytest.mark.parametrize("n,cin,cout,hw", [(3, 64, 64, 56), (3, 192, 96, 28), (2, 480, 192, 14), (2, 832, 160, 7)])
+def test_conv1x1_octets_only_epilogue_bit_identical(device, n, cin, cout, hw):
+    """Round 6: the 1x1 kernels (register ring for M <= 64, LDS-DMA above)
+    with y = NULL write the same companion as with y (GoogLeNet conv2 /
+    3x3_reduce and inception reduce shapes)."""
+    import torch
+    from rramsim import ops
+    rng = np.random.default_rng(9)
+    d = ops.conv_desc((n, cin, hw, hw), cout, 1, 1, 0, 1, 1)
+    assert ops.conv_output_octets_only(d) == 1
+    x = torch.from_numpy(np.maximum(rng.standard_normal((n, cin, hw, hw)), 0).astype(np.float32)).to(device)
+    w = torch.from_numpy((rng.standard_normal((cout, cin, 1, 1)) * 0.05).astype(np.float32)).to(device)
+    b = torch.from_numpy(rng.standard_normal(cout).astype(np.float32)).to(device)
+    y = torch.empty((n, cout, hw, hw), device=device)
+    yo1 = torch.zeros(n * cout * hw * hw * 6, dtype=torch.uint8, device=device)
+    yo2 = torch.full_like(yo1, 7)
+    ops.conv2d_fwd_octets(d, x, None, w, b, y, yo1, relu=True)
+    ops.conv2d_fwd_octets(d, x, None, w, b, None, yo2, relu=True)
+    torch.cuda.synchronize()
+    assert torch.equal(yo1, yo2)
+
+
+def test_conv1x1_output_fold_in_googlenet(device):
+    """GoogLeNet TEST net (round 6): the 1x1 reductions read only by a 3x3 /
+    5x5 convolution that takes their octet companion are left unwritten in
+    fp32 after the first forwards and materialised when handed out -- bit
+    for bit the blobs with the fold off; the loss outputs are bit-identical."""
+    import torch
+    from rramsim import caffe, models
+    caffe.set_stream_from_torch()
+    names = ["conv2/3x3_reduce"] + [f"inception_{b}/{k}_reduce" for b in ("3a", "3b", "4a", "4e", "5b")
+                                     for k in ("3x3", "5x5")]
+    outs = ["loss1/loss1", "loss2/loss1", "loss3/loss3", "loss3/classifier"]
+    got, stale = {}, {}
+    for fold in (False, True):
+        caffe.set_random_seed(1701)
+        net = caffe.Net(models.googlenet(test_batch=4), "test", models.net_options("googlenet", fuse_conv_y=fold))
+        for _ in range(3):
+            net.forward()
+        torch.cuda.synchronize()
+        stale[fold] = {n: net.blob_stale(n) for n in names}
+        got[fold] = {n: net.blob(n).detach().cpu().clone() for n in names + outs}
+        net.close()
+    assert not any(stale[False].values()), stale[False]
+    assert stale[True]["conv2/3x3_reduce"] and stale[True]["inception_3a/3x3_reduce"], stale[True]
+    for n in names + outs:
+        assert torch.equal(got[True][n], got[False][n]), n
+
+
 def test_pooled_output_fold_needs_a_sole_convolution_reader(device):
     """A second reader of pool1 (here a ReLU writing its own top) keeps the
     pool writing its fp32 top: pool1 is never stale, the extra reader sees
