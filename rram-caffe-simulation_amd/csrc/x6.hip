@@ -366,7 +366,8 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
   // then fits the LDS of two workgroups per CU); tpi = 0: tiles of BNc
   // consecutive positions across images
   const int timg = tpi > 0 ? tn / tpi : 0;
-  const int n0 = tpi > 0 ? timg * HW + (tn - timg * tpi) * BNc : tn * BNc;
+  const int tpc = cv.tpitch > 0 ? cv.tpitch : BNc;  // positions per per-image tile
+  const int n0 = tpi > 0 ? timg * HW + (tn - timg * tpi) * tpc : tn * BNc;
   const int KT = cv.C >> 4;                      // K-tiles of 16 channels (>= 1, host)
   const uint32_t PL = static_cast<uint32_t>(cv.H * cv.W * 48);  // bytes per octet plane of the packed input
   Epi ep = P.e;
@@ -380,7 +381,7 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
 
   // patch: positions n0 .. plast cover images img0 .. img0 + nseg - 1 (<= 3);
   // segment s holds output rows f_s .. l_s of its image plus the KH - 1 halo
-  const int plast = min(n0 + BNc, tpi > 0 ? (timg + 1) * HW : P.N) - 1;
+  const int plast = tpi > 0 ? min(n0 + tpc, (timg + 1) * HW) - 1 : min(n0 + BNc, P.N) - 1;
   const int img0 = n0 / HW, nseg = plast / HW - img0 + 1;
   const int f0 = (n0 - img0 * HW) / OW;
   auto seg_last = [&](int s) { return s == nseg - 1 ? (plast - (img0 + s) * HW) / OW : cv.Ho - 1; };
@@ -804,8 +805,9 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
     const int tn = __builtin_amdgcn_readfirstlane(r_ / P.tiles_m);
     tg.m0 = tg.tm * BMc;
     const int timg = tpi > 0 ? tn / tpi : 0;
-    tg.n0 = tpi > 0 ? timg * HW + (tn - timg * tpi) * BNc : tn * BNc;
-    tg.plast = min(tg.n0 + BNc, tpi > 0 ? (timg + 1) * HW : P.N) - 1;
+    const int tpc = cv.tpitch > 0 ? cv.tpitch : BNc;  // positions per per-image tile
+    tg.n0 = tpi > 0 ? timg * HW + (tn - timg * tpi) * tpc : tn * BNc;
+    tg.plast = tpi > 0 ? min(tg.n0 + tpc, (timg + 1) * HW) - 1 : min(tg.n0 + BNc, P.N) - 1;
     tg.img0 = tg.n0 / HW;
     tg.nseg = tg.plast / HW - tg.img0 + 1;
     tg.f0 = (tg.n0 - tg.img0 * HW) / OW;
@@ -2779,6 +2781,7 @@ int pack_octets(const float* x, void* oct, int num, int C, int HWi, hipStream_t 
 // ---- k_conv_cb_x6 (channel-octet pre-split activations) ----
 struct CbPlan {
   int WR, NB, RPC, PD, octb, tiles_m, tiles_n, OCC, tpi;
+  int tp = 0;  // per-image tiles of tp positions (whole output rows; 0: the tile width)
 };
 // instantiated (KH, WR, NB, PD, OCC) combinations; OCC = workgroups per CU.
 // One workgroup per CU: k_conv_cb_x6 (32x32x16); two: k_conv_cb16_x6
@@ -2800,6 +2803,9 @@ bool cb_instantiated(int KH, int WR, int NB, int PD, int OCC = 1) {
 #undef RRAM_X
   return false;
 }
+#ifndef RRAM_CB_ROWALIGN  // 0: no row-aligned per-image tiles; 1: by the cost rule; 2: wherever they fit (A/B)
+#define RRAM_CB_ROWALIGN 1
+#endif
 bool conv_cb_plan(const rram_conv_desc* d, CbPlan& pl) {
   const int KH = d->kernel_h, KW = d->kernel_w;
   if (d->stride_h != 1 || d->stride_w != 1 || d->dilation_h != 1 || d->dilation_w != 1) return false;
@@ -2874,26 +2880,36 @@ bool conv_cb_plan(const rram_conv_desc* d, CbPlan& pl) {
   // Measured on MI355X (AlexNet b256): conv3 128 x 256 -> 128 x 128 here
   // 0.342 -> 0.308 ms (profiles/r05_ab_occ2.txt); round 4: conv5 215 -> 204.
   if (best > 0) {
-    int64_t best2 = -1;
-    CbPlan p2{};
+    int64_t best2 = -1, best3 = -1;  // best3: the row-aligned per-image plans
+    CbPlan p2{}, p3{};
     static const int cfg2[2][2] = {{4, 4}, {2, 2}};
     for (const auto& c : cfg2) {
       const int WR = c[0], NB = c[1], BM = 32 * WR, BN = 32 * NB * (4 / WR);
       if (!cb_instantiated(KH, WR, NB, 8, 2)) continue;
       const int tiles_m = (M + BM - 1) / BM;
       if ((tiles_m * BM - M) * 4 > tiles_m * BM) continue;
-      for (int per_image = 0; per_image < 2; ++per_image) {
-        int rmax = 0, tpi = 0, octb = 0;
-        if (!per_image) {
+      // per_image 2: per-image tiles of whole output rows (tp = the rows of
+      // OW that fit BN; the columns past tp computed and dropped), whose
+      // patch has no partial rows: GoogLeNet conv2 (56 x 56) fits 8 pieces
+      // at 112-position tiles where 128-position ones need 9
+      for (int per_image = 0; per_image < 3; ++per_image) {
+        int rmax = 0, tpi = 0, octb = 0, tp = 0;
+        if (per_image == 0) {
           rmax = patch_rows(N, HW, OW, OH, KH, BN, 3);
           if (rmax < 0) continue;
           octb = ((rmax * RPC + 2 * ((3 * OW * (1 - KH)) & 15)) * 16 + 255) / 256 * 256;
-        } else {
+        } else if (per_image == 1) {
           tpi = (HW + BN - 1) / BN;
           for (int t = 0; t < tpi; ++t) {
             const int f = t * BN / OW, l = (std::min((t + 1) * BN, HW) - 1) / OW;
             rmax = std::max(rmax, l - f + KH);
           }
+          octb = (rmax * RPC * 16 + 255) / 256 * 256;
+        } else {
+          if (!RRAM_CB_ROWALIGN || OW > BN || BN % OW == 0 || HW <= BN) continue;
+          tp = BN / OW * OW;
+          tpi = (HW + tp - 1) / tp;
+          rmax = tp / OW + KH - 1;
           octb = (rmax * RPC * 16 + 255) / 256 * 256;
         }
         if ((2 * octb / 16 + 255) / 256 > 8) continue;
@@ -2906,9 +2922,12 @@ bool conv_cb_plan(const rram_conv_desc* d, CbPlan& pl) {
         // (192 rows per group: 128-row tiles pad a quarter) 0.297 on its
         // one-per-CU 64 x 256 plan vs 0.267 on 64 x 128
         const int64_t cost = (nwg + 511) / 512 * 2 * BM * BN * (BM == 64 ? 4 : 3) / 3;
-        if (best2 < 0 || cost < best2) {
-          best2 = cost;
-          p2 = CbPlan{WR, NB, RPC, 8, octb, tiles_m, tiles_n, 2, tpi};
+        int64_t& bc = per_image == 2 ? best3 : best2;
+        CbPlan& pc = per_image == 2 ? p3 : p2;
+        if (bc < 0 || cost < bc) {
+          bc = cost;
+          pc = CbPlan{WR, NB, RPC, 8, octb, tiles_m, tiles_n, 2, tpi};
+          pc.tp = tp;
         }
       }
     }
@@ -2920,6 +2939,13 @@ bool conv_cb_plan(const rram_conv_desc* d, CbPlan& pl) {
     // loser, conv4 on 128 x 128 (a quarter of the rows padded, 0.279 ->
     // 0.335 ms), estimates 1.5x.
     if (best2 > 0 && best2 * 5 <= best * 7) pl = p2;
+    // row-aligned per-image tiles where no other two-per-CU plan fits, within
+    // 1.5x: GoogLeNet conv2 (56 x 56, one-per-CU 64 x 256 before) 0.935-0.940
+    // -> 0.856-0.860 ms at an estimate of 1.44x; where another two-per-CU plan
+    // fits they measured slower (profiles/r06_ab_cb_rowalign.txt).
+    // RRAM_CB_ROWALIGN == 2 (A/B builds): the row-aligned plan wherever it fits
+    else if (best3 > 0 && ((best2 < 0 && best3 * 2 <= best * 3) || RRAM_CB_ROWALIGN == 2)) pl = p3;
+    if (RRAM_CB_ROWALIGN == 2 && best3 > 0) pl = p3;
   }
   return best > 0;
 }
@@ -2962,6 +2988,7 @@ int conv_cb_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, c
   cv.sh = cv.sw = cv.dh = cv.dw = 1;
   cv.Ho = d->out_h;
   cv.Wo = d->out_w;
+  cv.tpitch = pl.tp;
   cv.howo = make_fastdiv(HW);
   cv.wo_div = make_fastdiv(d->out_w);
   P.e = make_epi(y, HW, 1.0f, 0.0f, bias, RRAM_BIAS_ROW, relu);
