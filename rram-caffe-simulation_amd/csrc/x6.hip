@@ -2907,6 +2907,13 @@ bool conv_cb_plan(const rram_conv_desc* d, CbPlan& pl) {
           octb = (rmax * RPC * 16 + 255) / 256 * 256;
         } else {
           if (!RRAM_CB_ROWALIGN || OW > BN || BN % OW == 0 || HW <= BN) continue;
+          // 64 x 128 tiles only: GoogLeNet conv2 0.875-0.886 ms there vs
+          // 0.943-0.963 on 128 x 128 (a quarter of the rows padded; equal
+          // estimates), profiles/r06_ab_cb_rowalign.txt
+#ifndef RRAM_CB_RA_WR
+#define RRAM_CB_RA_WR 2
+#endif
+          if (WR != RRAM_CB_RA_WR) continue;
           tp = BN / OW * OW;
           tpi = (HW + tp - 1) / tp;
           rmax = tp / OW + KH - 1;
@@ -2940,8 +2947,8 @@ bool conv_cb_plan(const rram_conv_desc* d, CbPlan& pl) {
     // 0.335 ms), estimates 1.5x.
     if (best2 > 0 && best2 * 5 <= best * 7) pl = p2;
     // row-aligned per-image tiles where no other two-per-CU plan fits, within
-    // 1.5x: GoogLeNet conv2 (56 x 56, one-per-CU 64 x 256 before) 0.935-0.940
-    // -> 0.856-0.860 ms at an estimate of 1.44x; where another two-per-CU plan
+    // 1.5x: GoogLeNet conv2 (56 x 56, one-per-CU 64 x 256 before) 0.935-0.963
+    // -> 0.856-0.886 ms at an estimate of 1.44x; where another two-per-CU plan
     // fits they measured slower (profiles/r06_ab_cb_rowalign.txt).
     // RRAM_CB_ROWALIGN == 2 (A/B builds): the row-aligned plan wherever it fits
     else if (best3 > 0 && ((best2 < 0 && best3 * 2 <= best * 3) || RRAM_CB_ROWALIGN == 2)) pl = p3;

@@ -538,7 +538,7 @@ ENGINE_CASES = [
     dict(x=(4, 256, 13, 13), cout=384, k=3, p=1, g=1),
     dict(x=(4, 384, 13, 13), cout=384, k=3, p=1, g=2),
     dict(x=(4, 384, 13, 13), cout=256, k=3, p=1, g=2),
-    dict(x=(3, 64, 56, 56), cout=192, k=3, p=1, g=1),      # GoogLeNet conv2: row-aligned 112-position tiles (28 per image)
+    dict(x=(3, 64, 56, 56), cout=192, k=3, p=1, g=1),      # GoogLeNet conv2: row-aligned 64 x 128 tiles, 112 positions (28 per image)
     dict(x=(3, 128, 28, 28), cout=192, k=3, p=1, g=1),     # inception_3b/3x3: 64 x 256 contiguous tiles
     dict(x=(2, 3, 224, 224), cout=64, k=7, p=3, g=1, s=2),  # GoogLeNet conv1 (k_conv_s2_x6)
 ]
