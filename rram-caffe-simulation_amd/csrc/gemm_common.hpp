@@ -76,8 +76,8 @@ struct ConvGeom {
   int in_bytes; // bytes addressable from the group's input base (buffer range)
   const int2* tbl;  // CONVT: per k {4*(c*H*W + kh*dh*W + kw*dw), tap}; tap 31 = never valid
   int taps;         // CONVT: kh*kw taps tracked in the per-column validity mask (0: pad-free)
-  int tpitch;       // octet kernels, per-image tiles: positions per tile (0: the tile width; else a
-                    // whole number of output rows, the columns past it computed and dropped)
+  int tpitch;       // octet kernels: positions per tile (0: the tile width; else whole output rows of
+                    // an image, or whole images; the columns past it computed and dropped)
 };
 
 struct Epi {

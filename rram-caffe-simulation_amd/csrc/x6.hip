@@ -366,8 +366,8 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
   // then fits the LDS of two workgroups per CU); tpi = 0: tiles of BNc
   // consecutive positions across images
   const int timg = tpi > 0 ? tn / tpi : 0;
-  const int tpc = cv.tpitch > 0 ? cv.tpitch : BNc;  // positions per per-image tile
-  const int n0 = tpi > 0 ? timg * HW + (tn - timg * tpi) * tpc : tn * BNc;
+  const int tpc = cv.tpitch > 0 ? cv.tpitch : BNc;  // positions per tile
+  const int n0 = tpi > 0 ? timg * HW + (tn - timg * tpi) * tpc : tn * tpc;
   const int KT = cv.C >> 4;                      // K-tiles of 16 channels (>= 1, host)
   const uint32_t PL = static_cast<uint32_t>(cv.H * cv.W * 48);  // bytes per octet plane of the packed input
   Epi ep = P.e;
@@ -381,7 +381,7 @@ k_conv_cb_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* __r
 
   // patch: positions n0 .. plast cover images img0 .. img0 + nseg - 1 (<= 3);
   // segment s holds output rows f_s .. l_s of its image plus the KH - 1 halo
-  const int plast = tpi > 0 ? min(n0 + tpc, (timg + 1) * HW) - 1 : min(n0 + BNc, P.N) - 1;
+  const int plast = min(n0 + tpc, tpi > 0 ? (timg + 1) * HW : P.N) - 1;
   const int img0 = n0 / HW, nseg = plast / HW - img0 + 1;
   const int f0 = (n0 - img0 * HW) / OW;
   auto seg_last = [&](int s) { return s == nseg - 1 ? (plast - (img0 + s) * HW) / OW : cv.Ho - 1; };
@@ -805,9 +805,9 @@ k_conv_cb16_x6(Params P, const x6::bf16x8* __restrict__ wpack, const uint16_t* _
     const int tn = __builtin_amdgcn_readfirstlane(r_ / P.tiles_m);
     tg.m0 = tg.tm * BMc;
     const int timg = tpi > 0 ? tn / tpi : 0;
-    const int tpc = cv.tpitch > 0 ? cv.tpitch : BNc;  // positions per per-image tile
-    tg.n0 = tpi > 0 ? timg * HW + (tn - timg * tpi) * tpc : tn * BNc;
-    tg.plast = tpi > 0 ? min(tg.n0 + tpc, (timg + 1) * HW) - 1 : min(tg.n0 + BNc, P.N) - 1;
+    const int tpc = cv.tpitch > 0 ? cv.tpitch : BNc;  // positions per tile
+    tg.n0 = tpi > 0 ? timg * HW + (tn - timg * tpi) * tpc : tn * tpc;
+    tg.plast = min(tg.n0 + tpc, tpi > 0 ? (timg + 1) * HW : P.N) - 1;
     tg.img0 = tg.n0 / HW;
     tg.nseg = tg.plast / HW - tg.img0 + 1;
     tg.f0 = (tg.n0 - tg.img0 * HW) / OW;
@@ -2806,13 +2806,49 @@ bool cb_instantiated(int KH, int WR, int NB, int PD, int OCC = 1) {
 #ifndef RRAM_CB_ROWALIGN  // 0: no row-aligned per-image tiles; 1: by the cost rule; 2: wherever they fit (A/B)
 #define RRAM_CB_ROWALIGN 1
 #endif
+#ifndef RRAM_CB_IMGALIGN  // 0: no octet plan for planes of < 64 positions
+#define RRAM_CB_IMGALIGN 1
+#endif
+// Planes of < 64 positions (GoogLeNet's 7 x 7 stage): 128 consecutive
+// positions would span 4 images (the patch holds 3 segments), so the tiles are
+// whole images -- tp = floor(128 / HW) images' positions per 128-column tile
+// at two workgroups per CU, the columns past tp computed and dropped -- when
+// the patch of those images fits the 8 LDS pieces.
+bool conv_cb_plan_whole_images(const rram_conv_desc* d, CbPlan& pl) {
+  const int KH = d->kernel_h, G = d->group, M = d->num_output / G;
+  const int HW = d->out_h * d->out_w, OW = d->out_w, OH = d->out_h, N = d->num * HW;
+  if ((int64_t)d->num * d->channels * d->height * d->width * 6 >= (1ll << 31)) return false;  // 32-bit offsets
+  const int PW = d->width + 2 * d->pad_w;
+  int RPC = 3 * PW;
+  while ((RPC - 3 * OW) % 16 != 0) ++RPC;
+  // 128 x 128 tiles where no row pads, else 64 x 128 (the instantiated ones)
+  static const int cfg[2][2] = {{4, 4}, {2, 2}};
+  for (const auto& c : cfg) {
+    const int WR = c[0], NB = c[1], BM = 32 * WR, BN = 32 * NB * (4 / WR);
+    if (HW > BN / 2 || !cb_instantiated(KH, WR, NB, 8, 2)) continue;
+    const int tiles_m = (M + BM - 1) / BM;
+    if (WR == 4 && tiles_m * BM != M && cb_instantiated(KH, 2, 2, 8, 2)) continue;
+    if ((tiles_m * BM - M) * 4 > tiles_m * BM) continue;
+    const int per = BN / HW, tp = per * HW;
+    const int rmax = per * (OH + KH - 1);
+    const int octb = ((rmax * RPC + 2 * ((3 * OW * (1 - KH)) & 15)) * 16 + 255) / 256 * 256;
+    if ((2 * octb / 16 + 255) / 256 > 8) continue;
+    const int64_t tiles_n = (N + tp - 1) / tp;
+    if ((int64_t)G * tiles_m * tiles_n >= (1ll << 31)) continue;
+    pl = CbPlan{WR, NB, RPC, 8, octb, tiles_m, static_cast<int>(tiles_n), 2, 0};
+    pl.tp = tp;
+    return true;
+  }
+  return false;
+}
 bool conv_cb_plan(const rram_conv_desc* d, CbPlan& pl) {
   const int KH = d->kernel_h, KW = d->kernel_w;
   if (d->stride_h != 1 || d->stride_w != 1 || d->dilation_h != 1 || d->dilation_w != 1) return false;
   if (!((KH == 3 && KW == 3) || (KH == 5 && KW == 5))) return false;
   const int G = d->group, Cg = d->channels / G, M = d->num_output / G;
   const int HW = d->out_h * d->out_w, OW = d->out_w, OH = d->out_h, N = d->num * HW;
-  if (Cg % 16 != 0 || M == 0 || HW < 64) return false;
+  if (Cg % 16 != 0 || M == 0) return false;
+  if (HW < 64) return RRAM_CB_IMGALIGN && conv_cb_plan_whole_images(d, pl);
   const int PW = d->width + 2 * d->pad_w;
   // row pitch in 16-byte chunks: >= 3 PW, = 3 OW (mod 16) (bank-conflict-free reads)
   int RPC = 3 * PW;

@@ -495,6 +495,10 @@ PATCH_CASES = [
     dict(x=(2, 32, 13, 13), cout=96, k=3, p=1, g=1),    # octet kernel: 96 of 128 rows (row masking), tiles over 2-3 images
     dict(x=(5, 16, 10, 13), cout=64, k=5, p=2, g=1),    # octet kernel: 5x5, 17-wide padded rows, 130 positions per image
     dict(x=(3, 64, 13, 13), cout=192, k=3, p=1, g=2),   # octet kernel: 64-row tiles (M = 96 per group), 4 K-tiles
+    dict(x=(5, 32, 7, 7), cout=64, k=3, p=1, g=1),      # 49-position planes: whole-image tiles (2 per tile, last one short)
+    dict(x=(3, 32, 7, 7), cout=128, k=5, p=2, g=1),     # 5x5 whole-image tiles, 128 x 128
+    dict(x=(4, 48, 6, 7), cout=96, k=3, p=1, g=1),      # 42 positions: 3 images per tile
+    dict(x=(3, 64, 7, 7), cout=192, k=3, p=1, g=2),     # whole-image tiles with groups
     dict(x=(2, 6, 13, 13), cout=128, k=3, p=1, g=1),    # C % 4 != 0: im2col path
     dict(x=(2, 8, 12, 12), cout=128, k=3, p=0, g=1),    # 100 positions per image: im2col path
 ]
@@ -541,6 +545,7 @@ ENGINE_CASES = [
     dict(x=(3, 64, 56, 56), cout=192, k=3, p=1, g=1),      # GoogLeNet conv2: row-aligned 64 x 128 tiles, 112 positions (28 per image)
     dict(x=(3, 128, 28, 28), cout=192, k=3, p=1, g=1),     # inception_3b/3x3: 64 x 256 contiguous tiles
     dict(x=(2, 3, 224, 224), cout=64, k=7, p=3, g=1, s=2),  # GoogLeNet conv1 (k_conv_s2_x6)
+    dict(x=(6, 192, 7, 7), cout=384, k=3, p=1, g=1),       # inception_5b/3x3: whole-image tiles
 ]
 
 
