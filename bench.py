@@ -43,7 +43,7 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: bf16 dense MFMA (no spars
 MFMA_X6_PEAK_TFLOPS = MFMA_BF16_PEAK_TFLOPS / 6.0
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 # the dominant kernel of the step: conv2's k_conv_cb16_x6<5,5,4,4,8,2,1> (23 %
-# of GPU time, profiles/r06v_bench_kernel_stats.csv); the only layer timed
+# of GPU time, profiles/r06f_bench_kernel_stats.csv); the only layer timed
 # inside the timed region, so the stream carries two markers per map for it
 DOMINANT_LAYER = "conv2"
 DOMINANT_PMC_CLASS = "conv2 k_conv_cb16_x6<5,5,...>"
