@@ -2018,24 +2018,33 @@ namespace c7x6 {
 constexpr int C = 3, KS = 7, S = 2, KC = 8;
 constexpr int R = C * KS;            // K rows (channel, kernel row)
 constexpr int G = (R + 1) / 2;       // MFMA groups (row 21 is padding)
-constexpr int BM = 64, MI = 2, BN = 256;
-constexpr int OR = 4;                // output rows a tile may touch (OW >= 85)
-constexpr int SR = S * (OR - 1) + KS;  // slot rows per channel: 13
+constexpr int BM = 64, MI = 2;
 constexpr int ROWE = 232;            // elements per slot row: S (OW - 1) + KC <= ROWE
-constexpr int TERMB = SR * ROWE * 2; // bytes per (channel, term) plane
-constexpr int CHB = 3 * TERMB;       // bytes per channel
 constexpr int QR = ROWE / 4;         // 4-element staging chunks per row
-constexpr int NCH = C * SR * QR;     // chunks per tile
-constexpr int CPT = (NCH + 255) / 256;
 static_assert((ROWE * 2) % 8 == 0, "8-byte staging stores");
-static_assert(2 * (C * CHB + BM * 4) <= 160 * 1024, "two workgroups per CU");
-// LDS byte offset of K row rr (0 for the padding row, whose B values are masked)
-constexpr int row_off(int rr) { return rr < R ? (rr / KS) * CHB + (rr % KS) * ROWE * 2 : 0; }
+// tile of 64 filters x 128 NBW positions (each wave NBW 32-column blocks)
+template <int NBW>
+struct Tile {
+  static constexpr int BN = 128 * NBW;
+  static constexpr int OR = NBW == 2 ? 4 : 3;     // output rows a tile may touch (host: OW large enough)
+  static constexpr int SR = S * (OR - 1) + KS;    // slot rows per channel: 13 / 11
+  static constexpr int TERMB = SR * ROWE * 2;     // bytes per (channel, term) plane
+  static constexpr int CHB = 3 * TERMB;           // bytes per channel
+  static constexpr int NCH = C * SR * QR;         // staging chunks per tile
+  static constexpr int CPT = (NCH + 255) / 256;
+  static constexpr int WGS = NBW == 2 ? 2 : 3;    // workgroups per CU
+  static_assert(WGS * (C * CHB + BM * 4) <= 160 * 1024, "LDS");
+  // LDS byte offset of K row rr (0 for the padding row, whose B values are masked)
+  static constexpr int row_off(int rr) { return rr < R ? (rr / KS) * CHB + (rr % KS) * ROWE * 2 : 0; }
+};
 }  // namespace c7x6
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+template <int NBW>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NBW == 2 ? 2 : 3, NBW == 2 ? 2 : 3)))
 k_conv_s2_x6(Params P, const x6::bf16x8* __restrict__ wpack, int tiles_per_img, int tiles) {
   using namespace c7x6;
+  using T = Tile<NBW>;
+  constexpr int BN = T::BN, SR = T::SR, TERMB = T::TERMB, CHB = T::CHB, NCH = T::NCH, CPT = T::CPT;
   __shared__ __attribute__((aligned(16))) char smem[C * CHB];
   __shared__ float bias_lds[BM];
   const int lane = threadIdx.x & 63;
@@ -2101,10 +2110,10 @@ k_conv_s2_x6(Params P, const x6::bf16x8* __restrict__ wpack, int tiles_per_img, 
   __syncthreads();
 
   // ---- K loop: 11 groups x (2 row blocks x 2 column blocks) x 6 MFMAs ----
-  uint32_t lb[2];  // per-lane slot byte offset of column block j (K row 0)
+  uint32_t lb[NBW];  // per-lane slot byte offset of column block j (K row 0)
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int sp = min(sp0 + wave * 64 + j * 32 + lr, HWo - 1);
+  for (int j = 0; j < NBW; ++j) {
+    const int sp = min(sp0 + wave * 32 * NBW + j * 32 + lr, HWo - 1);
     const int oh = sp / OW, ow = sp - oh * OW;
     lb[j] = static_cast<uint32_t>((S * (oh - f) * ROWE + S * ow) * 2);
   }
@@ -2121,17 +2130,17 @@ k_conv_s2_x6(Params P, const x6::bf16x8* __restrict__ wpack, int tiles_per_img, 
   // non-finite input never meets a padded zero weight.  The raw reads are
   // issued a group ahead and masked at use, so no wait for them sits in
   // front of the current group's MFMAs
-  auto read_b = [&](u32x4 (&Bq)[2][3], int g) __attribute__((always_inline)) {
-    const uint32_t ho = lh ? static_cast<uint32_t>(row_off(2 * g + 1)) : static_cast<uint32_t>(row_off(2 * g));
+  auto read_b = [&](u32x4 (&Bq)[NBW][3], int g) __attribute__((always_inline)) {
+    const uint32_t ho = lh ? static_cast<uint32_t>(T::row_off(2 * g + 1)) : static_cast<uint32_t>(T::row_off(2 * g));
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NBW; ++j)
 #pragma unroll
       for (int tt = 0; tt < 3; ++tt) {
         const uint32_t* p = reinterpret_cast<const uint32_t*>(smem + lb[j] + ho + tt * TERMB);
         Bq[j][tt] = u32x4{p[0], p[1], p[2], p[3]};
       }
   };
-  auto parts_b = [&](const u32x4 (&Bq)[2][3], int j, int g) __attribute__((always_inline)) {
+  auto parts_b = [&](const u32x4 (&Bq)[NBW][3], int j, int g) __attribute__((always_inline)) {
     const uint32_t m3 = (2 * g + 1 < R || lh == 0) ? 0x0000FFFFu : 0u;
     const uint32_t m02 = (2 * g + 1 < R || lh == 0) ? 0xFFFFFFFFu : 0u;
     x6::bf16x8 t[3];
@@ -2149,17 +2158,17 @@ k_conv_s2_x6(Params P, const x6::bf16x8* __restrict__ wpack, int tiles_per_img, 
     }
     return x6::Parts{t[0], t[1], t[2]};
   };
-  floatx16 acc[MI][2];
+  floatx16 acc[MI][NBW];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NBW; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
   x6::bf16x8 fa[3][MI][3];
   load_a(fa[0], 0);
   load_a(fa[1], 1);
-  u32x4 Bq[2][2][3];
+  u32x4 Bq[2][NBW][3];
   read_b(Bq[0], 0);
   // (scheduling barriers keep the prefetches where they are issued: left to
   // itself the scheduler sinks each weight load next to its first MFMA and
@@ -2171,7 +2180,7 @@ k_conv_s2_x6(Params P, const x6::bf16x8* __restrict__ wpack, int tiles_per_img, 
     if (g + 1 < G) read_b(Bq[(g + 1) & 1], g + 1);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < NBW; ++j) {
       const x6::Parts b = parts_b(Bq[g & 1], j, g);
 #pragma unroll
       for (int i = 0; i < MI; ++i)
@@ -2189,8 +2198,8 @@ k_conv_s2_x6(Params P, const x6::bf16x8* __restrict__ wpack, int tiles_per_img, 
 #pragma unroll
     for (int r = 0; r < 16; ++r) bv[i][r] = bias_lds[i * 32 + 4 * lh + (r & 3) + 8 * (r >> 2)];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int sp = sp0 + wave * 64 + j * 32 + lr;
+  for (int j = 0; j < NBW; ++j) {
+    const int sp = sp0 + wave * 32 * NBW + j * 32 + lr;
     const uint32_t ob = sp < HWo ? static_cast<uint32_t>(((int64_t)img * P.e.cimg + sp) * 4) : 0x80000000u;
 #pragma unroll
     for (int i = 0; i < MI; ++i)
@@ -2655,13 +2664,18 @@ int conv_wide_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, co
 }
 
 // ---- k_conv_s2_x6 (GoogLeNet conv1: 3 channels, 64 x 7 x 7, stride 2) ----
+#ifndef RRAM_S2_NBW  // 32-column blocks per wave of k_conv_s2_x6 (2: 64 x 256 tiles, two per CU; 1: 64 x 128, three)
+#define RRAM_S2_NBW 2
+#endif
 bool conv_s2_ok(const rram_conv_desc* d) {
   namespace k = c7x6;
+  using T = k::Tile<RRAM_S2_NBW>;
   return d->group == 1 && d->channels == k::C && d->kernel_h == k::KS && d->kernel_w == k::KS &&
          d->stride_h == k::S && d->stride_w == k::S && d->dilation_h == 1 && d->dilation_w == 1 && d->pad_h >= 0 &&
          d->pad_h <= 3 && d->pad_w >= 0 && d->pad_w <= 3 && d->num_output >= 1 && d->num_output <= k::BM &&
          d->num > 0 && d->out_w >= 85 && d->out_h >= 1 && k::S * (d->out_w - 1) + k::KC <= k::ROWE &&
-         (d->out_w + 254) / d->out_w <= k::OR - 1 && (int64_t)d->num * k::C * d->height * d->width * 4 < (1ll << 31) &&
+         (d->out_w + T::BN - 2) / d->out_w <= T::OR - 1 &&
+         (int64_t)d->num * k::C * d->height * d->width * 4 < (1ll << 31) &&
          (int64_t)d->num * d->num_output * d->out_h * d->out_w * 4 < (1ll << 31);
 }
 
@@ -2707,12 +2721,12 @@ int conv_s2_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, cons
     const int rc = launch_status("conv s2 weight pack x6");
     if (rc) return rc;
   }
-  const int tpi = (HW + c7x6::BN - 1) / c7x6::BN;
+  const int tpi = (HW + c7x6::Tile<RRAM_S2_NBW>::BN - 1) / c7x6::Tile<RRAM_S2_NBW>::BN;
   const int64_t tiles = (int64_t)d->num * tpi;
   RRAM_REQUIRE(tiles < (1ll << 31), "conv: grid too large");
   // (a persistent form, one workgroup per CU with the weights in registers:
   // 0.61 vs 0.43 ms in the GoogLeNet map, profiles/r06_ab_conv_s2_persistent.txt)
-  hipLaunchKernelGGL(k_conv_s2_x6, dim3(static_cast<unsigned>(tiles)), dim3(256), 0, s, P,
+  hipLaunchKernelGGL(k_conv_s2_x6<RRAM_S2_NBW>, dim3(static_cast<unsigned>(tiles)), dim3(256), 0, s, P,
                      reinterpret_cast<const x6::bf16x8*>(wp), tpi, static_cast<int>(tiles));
   const int rc = launch_status("conv s2 x6");
   return rc ? rc : 1;
