@@ -2843,7 +2843,7 @@ bool conv_cb_plan_whole_images(const rram_conv_desc* d, CbPlan& pl) {
     const int tiles_m = (M + BM - 1) / BM;
     if (WR == 4 && tiles_m * BM != M && cb_instantiated(KH, 2, 2, 8, 2)) continue;
     if ((tiles_m * BM - M) * 4 > tiles_m * BM) continue;
-    const int per = BN / HW, tp = per * HW;
+    const int per = std::min(BN / HW, 3), tp = per * HW;  // (the patch holds 3 segments)
     const int rmax = per * (OH + KH - 1);
     const int octb = ((rmax * RPC + 2 * ((3 * OW * (1 - KH)) & 15)) * 16 + 255) / 256 * 256;
     if ((2 * octb / 16 + 255) / 256 > 8) continue;

@@ -499,6 +499,8 @@ PATCH_CASES = [
     dict(x=(3, 32, 7, 7), cout=128, k=5, p=2, g=1),     # 5x5 whole-image tiles, 128 x 128
     dict(x=(4, 48, 6, 7), cout=96, k=3, p=1, g=1),      # 42 positions: 3 images per tile
     dict(x=(3, 64, 7, 7), cout=192, k=3, p=1, g=2),     # whole-image tiles with groups
+    dict(x=(7, 32, 5, 5), cout=64, k=3, p=1, g=1),      # 25 positions: capped at 3 images per tile
+    dict(x=(4, 32, 4, 8), cout=64, k=3, p=0, g=1),      # 12 positions per image (2 x 6), no padding
     dict(x=(2, 6, 13, 13), cout=128, k=3, p=1, g=1),    # C % 4 != 0: im2col path
     dict(x=(2, 8, 12, 12), cout=128, k=3, p=0, g=1),    # 100 positions per image: im2col path
 ]
