@@ -2607,7 +2607,8 @@ bool conv1_ring_ok(const rram_conv_desc* d) {
   return d->group == 1 && d->channels == 3 && d->kernel_h == 11 && d->kernel_w == 11 && d->stride_h == 4 &&
          d->stride_w == 4 && d->pad_h == 0 && d->pad_w == 0 && d->dilation_h == 1 && d->dilation_w == 1 &&
          d->width == 227 && d->height >= 11 && d->num_output == c1x6::BM && d->num > 0 &&
-         (int64_t)d->num * 3 * d->height * d->width * 4 < (1ll << 31);
+         (int64_t)d->num * 3 * d->height * d->width * 4 < (1ll << 31) &&
+         (int64_t)d->num * d->num_output * d->out_h * d->out_w * 4 < (1ll << 31);
 }
 
 int conv_wide_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, const float* bias, float* y, int relu,
@@ -2637,6 +2638,8 @@ int conv_wide_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, co
   P.e = make_epi(y, HW, 1.0f, 0.0f, bias, RRAM_BIAS_ROW, relu);
   P.e.cimg = wk.y_img > 0 ? wk.y_img : (int64_t)d->num_output * HW;
   P.e.hw = make_fastdiv(HW);
+  // the epilogue's 32-bit output offsets (image stride included)
+  if ((int64_t)d->num * P.e.cimg * 4 >= (1ll << 31)) return 0;
   const int units = c1x6::G * 3 * 64;  // 3 KB fragments
   const size_t wbytes = static_cast<size_t>(units) * 48;
   if (wk.query) {
@@ -2708,6 +2711,8 @@ int conv_s2_x6_fwd(const rram_conv_desc* d, const float* x, const float* w, cons
   P.e = make_epi(y, HW, 1.0f, 0.0f, bias, RRAM_BIAS_ROW, relu);
   P.e.cimg = wk.y_img > 0 ? wk.y_img : (int64_t)d->num_output * HW;
   P.e.hw = make_fastdiv(HW);
+  // the epilogue's 32-bit output offsets (image stride included)
+  if ((int64_t)d->num * P.e.cimg * 4 >= (1ll << 31)) return 0;
   const int units = c7x6::G * c7x6::MI * 64;  // 3 KB fragments
   const size_t wbytes = static_cast<size_t>(units) * 48;
   if (wk.query) {
@@ -3253,6 +3258,8 @@ int conv_x6_fwd(const rram_conv_desc* d, const float* x, const void* x_oct, cons
                 float* y, void* y_oct, int relu, hipStream_t s, const WPack& wk) {
   if (f32_engine().load(std::memory_order_relaxed) != RRAM_ENGINE_BF16X6) return 0;
   if (wk.query == nullptr && (reinterpret_cast<uintptr_t>(w) & 3u) != 0) return 0;
+  // the epilogues' 32-bit output offsets also hold a strided (Concat-slice) image stride
+  if (wk.y_img > 0 && (int64_t)d->num * wk.y_img * 4 >= (1ll << 31)) return 0;
   {
     const int rc = conv_cb_x6_fwd(d, x, x_oct, w, bias, y, y_oct, relu, s, wk);
     if (rc != 0) return rc;
