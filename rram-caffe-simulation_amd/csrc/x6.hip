@@ -2763,6 +2763,7 @@ bool conv_x6_plan(const rram_conv_desc* d, ConvPlan& pl) {
   pl.CPH = KH == 5 ? 1 : (Cg % 8 == 0 ? 4 : 2);
   if (HW < 128 || Cg == 0 || Cg % (2 * pl.CPH) != 0) return false;
   if ((int64_t)d->num * d->channels * d->height * d->width * 4 >= (1ll << 31)) return false;  // 32-bit offsets
+  if ((int64_t)d->num * d->num_output * HW * 4 >= (1ll << 31)) return false;                   // (output too)
   // M tile 128 or 96 rows, whichever pads less (<= 1/8 padded rows)
   const int t128 = (M + 127) / 128 * 128, t96 = (M + 95) / 96 * 96;
   pl.MI = (t96 - M) < (t128 - M) ? 3 : 4;
@@ -2837,6 +2838,7 @@ bool conv_cb_plan_whole_images(const rram_conv_desc* d, CbPlan& pl) {
   const int KH = d->kernel_h, G = d->group, M = d->num_output / G;
   const int HW = d->out_h * d->out_w, OW = d->out_w, OH = d->out_h, N = d->num * HW;
   if ((int64_t)d->num * d->channels * d->height * d->width * 6 >= (1ll << 31)) return false;  // 32-bit offsets
+  if ((int64_t)d->num * d->num_output * HW * 4 >= (1ll << 31)) return false;
   const int PW = d->width + 2 * d->pad_w;
   int RPC = 3 * PW;
   while ((RPC - 3 * OW) % 16 != 0) ++RPC;
@@ -2872,8 +2874,10 @@ bool conv_cb_plan(const rram_conv_desc* d, CbPlan& pl) {
   // row pitch in 16-byte chunks: >= 3 PW, = 3 OW (mod 16) (bank-conflict-free reads)
   int RPC = 3 * PW;
   while ((RPC - 3 * OW) % 16 != 0) ++RPC;
-  // packed input < 2 GB (32-bit buffer offsets)
+  // packed input < 2 GB (32-bit buffer offsets), and the fp32 output (the
+  // epilogues' 32-bit byte offsets)
   if ((int64_t)d->num * d->channels * d->height * d->width * 6 >= (1ll << 31)) return false;
+  if ((int64_t)d->num * d->num_output * HW * 4 >= (1ll << 31)) return false;
   // tile (WR, NB) with the least makespan (rounds of 256 workgroups x tile
   // area); ties: taller tiles (weights fetched by one wave)
   static const int cfg[3][2] = {{4, 8}, {4, 4}, {2, 4}};

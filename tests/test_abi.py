@@ -116,6 +116,29 @@ def test_engine_plans_host_side():
         ops.set_f32_engine(prev)
 
 
+def test_engine_plans_round6_host_side():
+    """Round-6 plans (host logic, no GPU): GoogLeNet conv2 on row-aligned
+    64 x 128 per-image tiles (28 per 56 x 56 image), the 7 x 7 stage's 3x3 /
+    5x5 on whole-image tiles, GoogLeNet conv1 (7x7 / 2, 3 channels) on the
+    bf16x6 engine without an octet input, the 1x1 reductions' companion-only
+    epilogue; and shapes whose outputs the 32-bit epilogue offsets cannot
+    address fall back to the fp32 engine."""
+    from rramsim import ops
+    pl = ops.conv_octet_plan(ops.conv_desc((256, 64, 56, 56), 192, 3, 1, 1, 1, 1))
+    assert {k: pl[k] for k in ("rows", "cols", "per_cu", "tiles_per_image")} == \
+        dict(rows=64, cols=128, per_cu=2, tiles_per_image=28), pl
+    for x, cout, k, p in [((256, 192, 7, 7), 384, 3, 1), ((256, 160, 7, 7), 320, 3, 1), ((256, 48, 7, 7), 128, 5, 2)]:
+        pl = ops.conv_octet_plan(ops.conv_desc(x, cout, k, 1, p, 1, 1))
+        assert pl is not None and pl["per_cu"] == 2 and pl["tiles_per_image"] == 0, (x, pl)
+    c1 = ops.conv_desc((256, 3, 224, 224), 64, 7, 2, 3, 1, 1)
+    assert ops.f32_engine_for_conv(c1) == ops.ENGINE_BF16X6 and ops.conv_input_octets(c1) == 0
+    assert ops.conv_output_octets_only(ops.conv_desc((256, 192, 28, 28), 96, 1, 1, 0, 1, 1)) == 1
+    assert ops.conv_output_octets_only(ops.conv_desc((256, 192, 28, 28), 20, 1, 1, 0, 1, 1)) == 0  # partial octet
+    for x, cout, k, s, p, g in [((4096, 96, 27, 27), 256, 5, 1, 2, 2), ((2048, 3, 227, 227), 96, 11, 4, 0, 1)]:
+        d = ops.conv_desc(x, cout, k, s, p, 1, g)
+        assert ops.f32_engine_for_conv(d) == ops.ENGINE_F32, x
+
+
 def test_octet_kernel_tile_plans_host_side():
     """The channel-octet kernel's tile plans for AlexNet b256 (host logic, no
     GPU): every layer at two workgroups per CU (16x16x32 form):
